@@ -1,0 +1,354 @@
+/*
+ * pgmg_oracle.c — CPU restatement of the reference's `mg_cpu_exec` multigrid.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity checker for the MI355X
+ * HIP path.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+ * leg may load it.  The product library (libpgmg.so) never links or calls it.
+ *
+ * Pinned: tests/golden/ holds vectors produced by the reference's own C++
+ * (/root/reference/2_part_MG/MultiGrid.hpp driven by oracle/ref_harness.cpp,
+ * built by oracle/Makefile into oracle/_ref/).  tests/test_oracle_golden.py
+ * checks this restatement against them bit for bit.
+ *
+ * Semantics restated (reference file:line):
+ *   - grid: N x N vertex-centred, row-major idx = y*W + x, h = a/(N-1)
+ *     (2_part_MG/MultiGridTestRunner.hpp:130-131, DynamicGridUtils.hpp:52)
+ *   - Jacobi smoother: num_iter+1 sweeps, out-of-place, copy back, then the
+ *     residual norm over the whole array (boundary 0) and `norm < eps` early
+ *     exit after EVERY sweep (Smoother.hpp:38-116)
+ *   - residual (DynamicGridUtils.hpp:59-69), norm (:21-27), rhs (:111-124),
+ *     exact solution (:97-108)
+ *   - v_cycle / w_cycle / f_cycle / compute_coarsest_grid
+ *     (2_part_MG/MultiGrid.hpp:28-183), restriction (:187-205),
+ *     prolongation incl. the skipped fine row/col 1 (:208-226)
+ * Floating point: compiled with -ffp-contract=off so every expression rounds
+ * exactly as the reference's plain C++ does (no FMA contraction).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#ifndef M_PI
+#define M_PI 3.14159265358979323846
+#endif
+
+typedef struct orc_ctx {
+    double eps;        /* smoother tolerance (MultiGridTestRunner.hpp:144 -> 1e-7) */
+    int n_coarse;      /* recursion floor N_coarse (MultiGrid.hpp:19 -> 5)        */
+    int v1, v2;        /* pre/post smoothing num_iter (MultiGrid.hpp:15-16)       */
+    int coarse_iter;   /* num_iter on the coarsest grid (MultiGrid.hpp:61 -> 10)  */
+    int alpha;         /* W-cycle recursions (main.cpp:15 -> 3)                   */
+    double a, p, q;    /* problem constants (globals.cpp:2-4)                     */
+    /* statistics */
+    long long sweeps;
+    long long early_exits;
+    long long smooth_calls;
+} orc_ctx;
+
+void orc_ctx_init(orc_ctx *c)
+{
+    c->eps = 1e-7;
+    c->n_coarse = 5;
+    c->v1 = 1;
+    c->v2 = 1;
+    c->coarse_iter = 10;
+    c->alpha = 3;
+    c->a = 1.0;
+    c->p = 1.0;
+    c->q = 1.0;
+    c->sweeps = 0;
+    c->early_exits = 0;
+    c->smooth_calls = 0;
+}
+
+int orc_ctx_size(void) { return (int)sizeof(orc_ctx); }
+
+/* ---- grid utilities (DynamicGridUtils.hpp) ---------------------------- */
+
+void orc_zero(double *x, long long n)
+{
+    for (long long i = 0; i < n; ++i)
+        x[i] = 0.0;
+}
+
+/* DynamicGridUtils.hpp:21-27 — sequential sum of squares over l entries */
+double orc_norm(const double *v, long long l)
+{
+    double s = 0.0;
+    for (long long i = 0; i < l; ++i)
+        s += v[i] * v[i];
+    return sqrt(s);
+}
+
+/* DynamicGridUtils.hpp:59-69 — interior only; boundary of r untouched */
+void orc_residual(double *r, const double *x, const double *f, int W, int H, double h)
+{
+    for (int y = 1; y < H - 1; ++y) {
+        for (int xi = 1; xi < W - 1; ++xi) {
+            long long k = (long long)y * W + xi;
+            r[k] = f[k] - (1.0 / (h * h)) *
+                              (4 * x[k] - x[k - 1] - x[k + 1] - x[k - W] - x[k + W]);
+        }
+    }
+}
+
+/* DynamicGridUtils.hpp:111-124 */
+void orc_rhs(const orc_ctx *c, double *f, int W, int H, double h)
+{
+    double factor = (M_PI * M_PI / (c->a * c->a)) * (c->p * c->p + c->q * c->q);
+    for (int j = 0; j < H; ++j) {
+        for (int i = 0; i < W; ++i) {
+            double xx = i * h;
+            double yy = j * h;
+            f[(long long)j * W + i] = factor * sin(c->p * M_PI * xx / c->a) *
+                                      sin(c->q * M_PI * yy / c->a);
+        }
+    }
+}
+
+/* DynamicGridUtils.hpp:97-108 */
+void orc_exact(const orc_ctx *c, double *u, double h, int W, int H)
+{
+    for (int j = 0; j < H; ++j) {
+        for (int i = 0; i < W; ++i) {
+            double xx = i * h;
+            double yy = j * h;
+            u[(long long)j * W + i] = sin(c->p * M_PI * xx / c->a) * sin(c->q * M_PI * yy / c->a);
+        }
+    }
+}
+
+/* ---- Jacobi smoother (Smoother.hpp:38-116) ------------------------------
+ * Returns the number of sweeps performed.  `work` must hold 2*W*H doubles.
+ */
+int orc_jacobi_smooth(orc_ctx *c, double *x, const double *f, int W, int H, double h,
+                      int num_iter, double *work)
+{
+    long long L = (long long)W * H;
+    double *out = work;     /* Smoother.hpp:46-47: seeded with x */
+    double *r = work + L;   /* Smoother.hpp:75: residual buffer, boundary 0 */
+    memcpy(out, x, sizeof(double) * L);
+    orc_zero(r, L);
+    int done = 0;
+    c->smooth_calls++;
+    for (int it = 0; it <= num_iter; ++it) {
+        for (int y = 1; y < H - 1; ++y) {
+            for (int xi = 1; xi < W - 1; ++xi) {
+                long long k = (long long)y * W + xi;
+                out[k] = 0.25 * ((h * h * f[k]) + x[k - 1] + x[k + 1] + x[k - W] + x[k + W]);
+            }
+        }
+        memcpy(x, out, sizeof(double) * L);
+        ++done;
+        c->sweeps++;
+        orc_residual(r, x, f, W, H, h);
+        double nr = orc_norm(r, L);
+        if (nr < c->eps) {
+            c->early_exits++;
+            break;
+        }
+    }
+    return done;
+}
+
+/* ---- transfer operators (MultiGrid.hpp:187-226) ------------------------ */
+
+void orc_restrict(const double *F, double *C, int Nf, int Nc)
+{
+    for (int jc = 1; jc < Nc - 1; ++jc) {
+        for (int ic = 1; ic < Nc - 1; ++ic) {
+            long long c = (long long)jc * Nc + ic;
+            long long k = (long long)(2 * jc) * Nf + 2 * ic;
+            C[c] = 0.25 * F[k] +
+                   0.125 * (F[k + 1] + F[k - 1] + F[k + Nf] + F[k - Nf]) +
+                   0.0625 * (F[k - Nf - 1] + F[k - Nf + 1] + F[k + Nf - 1] + F[k + Nf + 1]);
+        }
+    }
+}
+
+/* fine += P * coarse; the loop bounds never touch fine row/col 1 (MultiGrid.hpp:210-225) */
+void orc_prolong(double *F, const double *C, int Nf, int Nc)
+{
+    for (int jc = 1; jc < Nc - 1; ++jc) {
+        for (int ic = 1; ic < Nc - 1; ++ic) {
+            long long c = (long long)jc * Nc + ic;
+            long long J = 2 * jc, I = 2 * ic;
+            F[J * Nf + I] += C[c];
+            F[(J + 1) * Nf + I] += 0.5 * (C[c] + C[c + Nc]);
+            F[J * Nf + I + 1] += 0.5 * (C[c] + C[c + 1]);
+            F[(J + 1) * Nf + I + 1] += 0.25 * (C[c] + C[c + 1] + C[c + Nc] + C[c + Nc + 1]);
+        }
+    }
+}
+
+/* ---- cycles ------------------------------------------------------------- */
+
+static double *orc_alloc(long long n) { return (double *)calloc((size_t)n, sizeof(double)); }
+
+/* MultiGrid.hpp:57-94 */
+void orc_v_cycle(orc_ctx *c, double *phi, const double *f, int N, double h)
+{
+    long long L = (long long)N * N;
+    double *work = orc_alloc(2 * L);
+    if (N <= c->n_coarse) {
+        orc_jacobi_smooth(c, phi, f, N, N, h, c->coarse_iter, work);
+        free(work);
+        return;
+    }
+    orc_jacobi_smooth(c, phi, f, N, N, h, c->v1, work);
+    double *res = orc_alloc(L);
+    orc_residual(res, phi, f, N, N, h);
+    int Nc = (N - 1) / 2 + 1;
+    long long Lc = (long long)Nc * Nc;
+    double *rc = orc_alloc(Lc);
+    orc_restrict(res, rc, N, Nc);
+    double *ec = orc_alloc(Lc);
+    orc_v_cycle(c, ec, rc, Nc, 2 * h);
+    orc_prolong(phi, ec, N, Nc);
+    orc_jacobi_smooth(c, phi, f, N, N, h, c->v2, work);
+    free(res);
+    free(rc);
+    free(ec);
+    free(work);
+}
+
+/* MultiGrid.hpp:96-136 */
+void orc_w_cycle(orc_ctx *c, double *phi, const double *f, int N, double h)
+{
+    long long L = (long long)N * N;
+    double *work = orc_alloc(2 * L);
+    if (N <= c->n_coarse) {
+        orc_jacobi_smooth(c, phi, f, N, N, h, c->coarse_iter, work);
+        free(work);
+        return;
+    }
+    orc_jacobi_smooth(c, phi, f, N, N, h, c->v1, work);
+    double *res = orc_alloc(L);
+    orc_residual(res, phi, f, N, N, h);
+    int Nc = (N - 1) / 2 + 1;
+    long long Lc = (long long)Nc * Nc;
+    double *rc = orc_alloc(Lc);
+    orc_restrict(res, rc, N, Nc);
+    double *ec = orc_alloc(Lc);
+    for (int i = 0; i < c->alpha; ++i)
+        orc_w_cycle(c, ec, rc, Nc, 2.0 * h);
+    orc_prolong(phi, ec, N, Nc);
+    orc_jacobi_smooth(c, phi, f, N, N, h, c->v2, work);
+    free(res);
+    free(rc);
+    free(ec);
+    free(work);
+}
+
+/* MultiGrid.hpp:28-55 — restrict `fine` repeatedly down to N_coarsest.
+ * Writes the coarsest grid into `out` (N_coarsest^2 doubles). */
+void orc_coarsest_grid(const double *fine, double *out, int N_fine, int N_coarsest)
+{
+    int Nc = N_fine;
+    double *cur = orc_alloc((long long)Nc * Nc);
+    memcpy(cur, fine, sizeof(double) * (size_t)((long long)Nc * Nc));
+    while (Nc > N_coarsest) {
+        int Nn = (Nc - 1) / 2 + 1;
+        double *nx = orc_alloc((long long)Nn * Nn);
+        orc_restrict(cur, nx, Nc, Nn);
+        free(cur);
+        cur = nx;
+        Nc = Nn;
+    }
+    memcpy(out, cur, sizeof(double) * (size_t)((long long)Nc * Nc));
+    free(cur);
+}
+
+/* MultiGrid.hpp:138-183 — full multigrid from N_init up to N_final; the
+ * result (N_final^2) goes to `final_solution`.  The finer RHS is regenerated
+ * analytically on every level (MultiGrid.hpp:162). */
+void orc_f_cycle(orc_ctx *c, const double *phi, const double *f, int N_init, double h_init,
+                 int N_final, double *final_solution)
+{
+    int N = N_init;
+    double h = h_init;
+    long long L = (long long)N * N;
+    double *phic = orc_alloc(L);
+    double *fc = orc_alloc(L);
+    memcpy(phic, phi, sizeof(double) * (size_t)L);
+    memcpy(fc, f, sizeof(double) * (size_t)L);
+    while (N < N_final) {
+        double *work = orc_alloc(2 * (long long)N * N);
+        orc_jacobi_smooth(c, phic, fc, N, N, h, 3, work);
+        free(work);
+        int Nf = 2 * N - 1;
+        long long Lf = (long long)Nf * Nf;
+        double *phif = orc_alloc(Lf);
+        double *ff = orc_alloc(Lf);
+        orc_rhs(c, ff, Nf, Nf, h / 2);
+        orc_prolong(phif, phic, Nf, N);
+        orc_v_cycle(c, phif, ff, Nf, h / 2);
+        free(phic);
+        free(fc);
+        phic = phif;
+        fc = ff;
+        N = Nf;
+        h /= 2;
+    }
+    memcpy(final_solution, phic, sizeof(double) * (size_t)((long long)N * N));
+    free(phic);
+    free(fc);
+}
+
+/* One outer iteration of MultiGridTestRunner::run_cycle("F-cycle")
+ * (MultiGridTestRunner.hpp:192-205): restrict phi to N_coarse, run f_cycle
+ * from there with the analytic coarse RHS, copy the result into phi. */
+void orc_f_cycle_outer(orc_ctx *c, double *phi, int N)
+{
+    int n0 = c->n_coarse;
+    double h0 = 1.0 / (n0 - 1);
+    double *f0 = orc_alloc((long long)n0 * n0);
+    double *p0 = orc_alloc((long long)n0 * n0);
+    orc_rhs(c, f0, n0, n0, h0);
+    orc_coarsest_grid(phi, p0, N, n0);
+    orc_f_cycle(c, p0, f0, n0, h0, N, phi);
+    free(f0);
+    free(p0);
+}
+
+/* ---- harness helpers ---------------------------------------------------- */
+
+/* ||phi - u|| / ||u|| as printed by MultiGridTestRunner.hpp:252-255 */
+double orc_rel_error(const orc_ctx *c, const double *phi, int N)
+{
+    long long L = (long long)N * N;
+    double h = c->a / (N - 1);
+    double *u = orc_alloc(L);
+    double *e = orc_alloc(L);
+    orc_exact(c, u, h, N, N);
+    for (long long i = 0; i < L; ++i)
+        e[i] = phi[i] - u[i];
+    double r = orc_norm(e, L) / orc_norm(u, L);
+    free(u);
+    free(e);
+    return r;
+}
+
+/* sqrt(sum_interior r^2) of the current iterate */
+double orc_residual_norm(const double *phi, const double *f, int N, double h)
+{
+    long long L = (long long)N * N;
+    double *r = orc_alloc(L);
+    orc_residual(r, phi, f, N, N, h);
+    double n = orc_norm(r, L);
+    free(r);
+    return n;
+}
+
+/* FNV-style 64-bit hash over the IEEE words */
+uint64_t orc_hash(const double *v, long long n)
+{
+    uint64_t hsh = 1469598103934665603ULL;
+    for (long long i = 0; i < n; ++i) {
+        uint64_t w;
+        memcpy(&w, &v[i], 8);
+        hsh = (hsh ^ w) * 1099511628211ULL;
+    }
+    return hsh;
+}

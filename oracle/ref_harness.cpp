@@ -1,0 +1,170 @@
+// ref_harness.cpp — drives the REFERENCE's own CPU multigrid (TEST INFRASTRUCTURE).
+//
+// Compiled by oracle/Makefile directly against the reference headers where they lie
+// (/root/reference/2_part_MG/MultiGrid.hpp, Smoother.hpp, DynamicGridUtils.hpp,
+// globals.cpp); output goes to oracle/_ref/ only.  Nothing from the reference is
+// copied into this repository.  Used to generate tests/golden/ and to pin
+// oracle/pgmg_oracle.c bit for bit.
+//
+// Usage: ref_harness <V|W|F> <N> <cycles> <eps> [phi_out.bin]
+// Prints one line per cycle:
+//   cycle <k> relerr <e> res <r> center <phi[(N/2)*N+N/2]> hash <fnv64> sweeps <s> exits <x>
+// and, if given, writes phi after the last cycle as raw little-endian doubles.
+//
+// operator new[] is calloc-backed: the reference reads the never-written
+// boundary of `new double[L]` residual buffers (Smoother.hpp:75-76), which is
+// undefined; zero is what it reads in practice and what we pin.
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <filesystem>
+#include <fstream>
+#include <iomanip>
+#include <iostream>
+#include <new>
+#include <string>
+#include <vector>
+
+void *operator new[](std::size_t n)
+{
+    void *p = std::calloc(n ? n : 1, 1);
+    if (!p) throw std::bad_alloc();
+    return p;
+}
+void operator delete[](void *p) noexcept { std::free(p); }
+void operator delete[](void *p, std::size_t) noexcept { std::free(p); }
+
+#define private public
+#include "2_part_MG/MultiGrid.hpp"
+#undef private
+
+struct CountingJacobi : public JacobiSmoother {
+    using JacobiSmoother::JacobiSmoother;
+    long long sweeps = 0, exits = 0;
+    void smooth(double *x, double *f, int w, int hgt, double h, int num_iter,
+                double *x_true = nullptr, std::vector<double> *residuals = nullptr,
+                std::vector<double> *errors = nullptr) override
+    {
+        (void)residuals;
+        std::vector<double> r;
+        JacobiSmoother::smooth(x, f, w, hgt, h, num_iter, x_true, &r, errors);
+        sweeps += (long long)r.size();
+        if (!r.empty() && r.back() < epsilon) exits++;
+    }
+};
+
+static uint64_t fnv(const double *v, long long n)
+{
+    uint64_t h = 1469598103934665603ULL;
+    for (long long i = 0; i < n; ++i) {
+        uint64_t w;
+        std::memcpy(&w, &v[i], 8);
+        h = (h ^ w) * 1099511628211ULL;
+    }
+    return h;
+}
+
+// Op mode: ref_harness O <N> <h> <eps> <in.bin> <out.bin>
+// in.bin : x[N*N], f[N*N], e[Nc*Nc]  (doubles)
+// out.bin: residual(x,f)[N*N] | restrict(x)[Nc*Nc] | x + P e [N*N] |
+//          smooth(x,f,num_iter=1)[N*N] | smooth(x,f,num_iter=10)[N*N]
+static int op_mode(int argc, char **argv)
+{
+    if (argc < 7) return 2;
+    const int N = std::atoi(argv[2]);
+    const double h = std::atof(argv[3]);
+    const double eps = std::atof(argv[4]);
+    const int Nc = (N - 1) / 2 + 1;
+    const long long L = (long long)N * N, Lc = (long long)Nc * Nc;
+    std::vector<double> in(2 * L + Lc);
+    FILE *fp = std::fopen(argv[5], "rb");
+    if (!fp || std::fread(in.data(), 8, in.size(), fp) != in.size()) return 3;
+    std::fclose(fp);
+    const double *x = in.data(), *f = in.data() + L, *e = in.data() + 2 * L;
+    JacobiSmoother sm(eps);
+    MultigridSolver mg(&sm, 3, N);
+    std::vector<double> out;
+    std::vector<double> r(L, 0.0);
+    DynamicGridUtils::compute_residual(r.data(), x, f, N, N, h);
+    out.insert(out.end(), r.begin(), r.end());
+    std::vector<double> c(Lc, 0.0);
+    mg.restrict_full_weighting(x, c.data(), N, Nc);
+    out.insert(out.end(), c.begin(), c.end());
+    std::vector<double> p(x, x + L);
+    mg.prolongation(p.data(), e, N, Nc);
+    out.insert(out.end(), p.begin(), p.end());
+    for (int it : {1, 10}) {
+        std::vector<double> s(x, x + L);
+        sm.smooth(s.data(), const_cast<double *>(f), N, N, h, it);
+        out.insert(out.end(), s.begin(), s.end());
+    }
+    fp = std::fopen(argv[6], "wb");
+    if (!fp) return 3;
+    std::fwrite(out.data(), 8, out.size(), fp);
+    std::fclose(fp);
+    return 0;
+}
+
+int main(int argc, char **argv)
+{
+    if (argc > 1 && argv[1][0] == 'O') return op_mode(argc, argv);
+    if (argc < 5) {
+        std::fprintf(stderr, "usage: %s <V|W|F> <N> <cycles> <eps> [phi_out.bin]\n", argv[0]);
+        return 2;
+    }
+    const char kind = argv[1][0];
+    const int N = std::atoi(argv[2]);
+    const int cycles = std::atoi(argv[3]);
+    const double eps = std::atof(argv[4]);
+    const long long L = (long long)N * N;
+    const double h = a / (N - 1);
+
+    double *phi = new double[L];
+    double *f = new double[L];
+    double *ex = new double[L];
+    double *r = new double[L];
+    DynamicGridUtils::initialize_zeros(phi, L);
+    DynamicGridUtils::compute_rhs(f, N, N, h);
+    DynamicGridUtils::compute_exact_solution(ex, h, N, N);
+
+    CountingJacobi sm(eps);
+    MultigridSolver mg(&sm, 3, N);
+    const int n0 = mg.N_coarse;
+    const double h0 = 1.0 / (n0 - 1);
+    double *f0 = new double[n0 * n0];
+    DynamicGridUtils::compute_rhs(f0, n0, n0, h0);
+
+    for (int k = 1; k <= cycles; ++k) {
+        if (kind == 'V') {
+            mg.v_cycle(phi, f, N, h);
+        } else if (kind == 'W') {
+            mg.w_cycle(phi, f, N, h);
+        } else {
+            double *p0 = nullptr;
+            mg.compute_coarsest_grid(phi, p0, N, n0);
+            mg.f_cycle(p0, f0, n0, h0);
+            std::memcpy(phi, mg.final_solution, sizeof(double) * L);
+            delete[] p0;
+        }
+        DynamicGridUtils::initialize_zeros(r, L);
+        DynamicGridUtils::compute_residual(r, phi, f, N, N, h);
+        double res = DynamicGridUtils::norm(r, L);
+        double *e = new double[L];
+        DynamicGridUtils::compute_error(e, phi, ex, L);
+        double rel = DynamicGridUtils::norm(e, L) / DynamicGridUtils::norm(ex, L);
+        delete[] e;
+        std::printf("cycle %d relerr %.17g res %.17g center %.17g hash %016llx sweeps %lld exits %lld\n",
+                    k, rel, res, phi[(long long)(N / 2) * N + N / 2],
+                    (unsigned long long)fnv(phi, L), sm.sweeps, sm.exits);
+        std::fflush(stdout);
+    }
+    if (argc > 5) {
+        FILE *fp = std::fopen(argv[5], "wb");
+        if (!fp) return 3;
+        std::fwrite(phi, sizeof(double), (size_t)L, fp);
+        std::fclose(fp);
+    }
+    return 0;
+}
