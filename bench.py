@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""Benchmark: V-cycles/s of the fp64 2D-Poisson geometric-multigrid V-cycle at N=16385
+(16384^2 cells) on MI355X, plus the fine-grid Jacobi sweep's HBM roofline fraction.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 16385]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+A "step" is one V-cycle of the reference's mg_cpu_exec semantics (2+2 Jacobi sweeps
+with the per-sweep residual-norm early exit, full-weighting restriction, the reference
+prolongation, recursion to N=5) on the synthetic problem the reference itself solves:
+phi0 = 0, f = analytic RHS.  All inputs are resident in HBM before the timed region.
+With N GPUs the same grid is split into row strips (strong scaling, RCCL halo exchange);
+value = V-cycles of the whole job per second.
+
+Prints ONE JSON line on rank 0.  See DESIGN.md "Measurement" for every field.
+"""
+import argparse
+import json
+import os
+import pathlib
+import platform
+import shutil
+import subprocess
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
+METRIC = "V-cycles/sec + fine-grid stencil HBM GB/s, 2D Poisson N=16384², fp64"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=16385, help="points per side (2^k+1)")
+    ap.add_argument("--timing", choices=["graph", "events"], default="events",
+                    help="events: eager launches with hipEvents around every fine sweep")
+    ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--cpu-n", type=int, default=0, help="grid for the CPU sample (default = --n)")
+    return ap.parse_args()
+
+
+def cpu_baseline(n, cycles=1):
+    """The oracle (our C restatement of mg_cpu_exec, 1 thread) on the host: a bounded
+    sample of the same workload (one V-cycle at the same N)."""
+    exe = ROOT / "oracle" / "mg_cpu_exec_port"
+    if not exe.exists():
+        subprocess.run(["make", "-C", str(ROOT / "oracle"), "-s",
+                        str(exe)], check=True, capture_output=True)
+    cmd = [str(exe), "V", str(n), str(cycles), "1e-7"]
+    if shutil.which("taskset"):
+        cmd = ["taskset", "-c", "0"] + cmd
+    out = subprocess.run(cmd, check=True, capture_output=True, text=True).stdout
+    secs = [float(l.split("seconds")[1]) for l in out.splitlines() if "seconds" in l]
+    t = sum(secs) / len(secs)
+    model = platform.processor() or ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(1.0 / t, 6), "unit": "V-cycles/s", "cores": 1, "kind": "port",
+            "sample": f"{cycles} V-cycle(s) at N={n}, phi0=0, analytic f; oracle/mg_cpu_exec_port "
+                      f"-O2 single thread (taskset -c 0); {t:.2f} s per V-cycle; host {model}"}
+
+
+def pmc_traffic(n):
+    """HBM bytes per fine-sweep launch from the committed rocprofv3 PMC summary (if any)."""
+    p = ROOT / "profiles" / "pmc_fine_sweep.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())
+        if int(d.get("N", 0)) == n:
+            return d.get("hbm_bytes_per_launch")
+    except (ValueError, OSError):
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch  # noqa: F401  (loads the ROCm runtime first; see _capi.load)
+    import _pkgload
+    pg = _pkgload.load()
+
+    dist = None
+    uid = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("gloo")
+        import ctypes
+        buf = (ctypes.c_ubyte * 128)()
+        if rank == 0:
+            pg._capi.check(pg.load().pgmg_comm_unique_id(buf), "pgmg_comm_unique_id")
+        t = torch.tensor(list(bytes(buf)), dtype=torch.uint8)
+        dist.broadcast(t, 0)
+        uid = (ctypes.c_ubyte * 128)(*t.tolist())
+
+    flags = pg.PGMG_FLAG_TIME_FINE if args.timing == "events" else 0
+    kw = dict(flags=flags, device=local_rank if world > 1 else 0)
+    if world > 1:
+        import ctypes
+        kw.update(rank=rank, world=world, nccl_unique_id=ctypes.cast(uid, ctypes.c_void_p))
+    s = pg.Solver(args.n, **kw)
+    s.set_problem()
+    bulk, tail_top = s.levels()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    # warmup (also builds the hipGraph in graph mode)
+    s.vcycle(max(args.warmup, 0))
+    s.sync()
+    s.fine_sweep_time()  # drop warmup events
+    barrier()
+    s.sync()
+    t0 = time.perf_counter()
+    s.vcycle(args.steps)
+    s.sync()
+    barrier()
+    t1 = time.perf_counter()
+    dt = t1 - t0
+    if dist is not None:
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    dev_ms = s.last_elapsed_ms()
+    nfine, fine_ms = s.fine_sweep_time()
+    if nfine == 0:
+        fine_ms = s.bench_sweep(20)
+        nfine = 20
+    vbytes = s.vcycle_bytes()
+    n = args.n
+    cfg = pg.default_config(n)
+    # algorithmic bytes of one fine sweep on this rank: read x, read f, write x_new
+    N = args.n
+    rows = (N - 2) if world == 1 else None
+    if rows is None:
+        import ctypes
+        p, pitch, r0, nr = (ctypes.c_void_p(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int())
+        pg.load().pgmg_phi_device(s.h, ctypes.byref(p), ctypes.byref(pitch), ctypes.byref(r0),
+                                  ctypes.byref(nr))
+        lo, hi = r0.value, r0.value + nr.value
+        rows = min(hi, N - 1) - max(lo, 1)
+    fine_bytes = 24.0 * rows * (N - 2)
+    achieved = fine_bytes / (fine_ms * 1e-3) / 1e9 if fine_ms > 0 else None
+    traffic = pmc_traffic(N) if world == 1 else None
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and args.cpu_baseline == "auto":
+            try:
+                cpu = cpu_baseline(args.cpu_n or n)
+            except Exception as e:  # reported, not fatal
+                cpu = {"value": None, "unit": "V-cycles/s", "cores": 1, "kind": "port",
+                       "sample": f"failed: {e}"}
+        value = args.steps / dt
+        line = {
+            "metric": METRIC,
+            "value": round(value, 4),
+            "unit": "V-cycles/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: the reference's own problem, phi0=0, f=2*pi^2*sin(pi x)sin(pi y)",
+            "config": {
+                "workload": f"V-cycle N={n} ({n - 1}^2 cells), 2+2 Jacobi (v1=v2=1), 11 coarsest "
+                            f"sweeps, eps=1e-7 early exit, {bulk} bulk levels + one-workgroup LDS "
+                            f"tail from N={tail_top} to N=5",
+                "N": n, "bulk_levels": bulk, "tail_top": tail_top,
+                "parallelism": "single-gpu" if world == 1 else f"row-strips x{world} (RCCL halos)",
+                "timing": args.timing,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_sweep<false,false,true> (finest-level Jacobi sweep)",
+                "achieved": round(achieved, 2) if achieved else None,
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
+                "traffic": traffic,
+                "bytes_per_launch": fine_bytes,
+                "launches_timed": nfine,
+                "ms_per_launch": round(fine_ms, 5),
+            },
+            "vcycle_algorithmic_gbps": round(vbytes / (dt / args.steps) / 1e9, 2),
+            "vcycle_device_ms": round(dev_ms / args.steps, 4),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    s.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

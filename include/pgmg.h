@@ -1,0 +1,170 @@
+/*
+ * pgmg.h — C ABI of the MI355X geometric-multigrid library (libpgmg.so).
+ *
+ * The drop-in boundary for the reference's GPU path.  Every entry point is
+ * extern "C" with plain pointers, sizes and int return codes (0 = success,
+ * negative = error; pgmg_last_error() gives the message).  No C++ exceptions
+ * and no HIP/torch types cross it.  Host code that binds it: the C++ mirror of
+ * the reference interface (host/Parallel_*.hpp, host/ParallelTestRunner.hpp,
+ * host/gpu_exec.cpp) and the Python ctypes plumbing used by tests and bench.py.
+ *
+ * What each entry replaces in the reference (/root/reference/...):
+ *
+ *   cycle level (context API)
+ *     pgmg_create / pgmg_set_problem / pgmg_vcycle / pgmg_get_solution
+ *         ParallelMultiGridSolver::v_cycle(double*, double*, int, double)
+ *             3_part_parallel/Parallel_Mg.cu:21-60, driven by
+ *         ParallelTestRunner::run_v_cycle()  3_part_parallel/ParallelTestRunner.cu:152-186
+ *         (numerics: MultigridSolver::v_cycle, 2_part_MG/MultiGrid.hpp:57-94)
+ *     pgmg_wcycle
+ *         ParallelMultiGridSolver::w_cycle  3_part_parallel/Parallel_Mg.cu:62-102
+ *         (numerics: MultigridSolver::w_cycle, 2_part_MG/MultiGrid.hpp:96-136)
+ *     pgmg_fcycle
+ *         MultigridTestRunner::run_cycle("F-cycle") 2_part_MG/MultiGridTestRunner.hpp:192-205
+ *         + MultigridSolver::f_cycle / compute_coarsest_grid, MultiGrid.hpp:28-55,138-183
+ *
+ *   op level (caller-owned device arrays in the reference's row-major layout,
+ *   element (y, x) at p[y*W + x]; the optional `stream` is a hipStream_t)
+ *     pgmg_jacobi    Parallel::ComputeJacobi       3_part_parallel/Parallel_Method.cu:144-160
+ *                    (numerics of JacobiSmoother::smooth, Smoother.hpp:38-116: v+1
+ *                    out-of-place sweeps with the residual-norm early exit)
+ *     pgmg_residual  Parallel::ComputeResidual     Parallel_Method.cu:162-173
+ *                    (DynamicGridUtils::compute_residual, DynamicGridUtils.hpp:59-69)
+ *     pgmg_restrict  Parallel::ComputeRestriction  Parallel_Method.cu:175-186
+ *                    (MultigridSolver::restrict_full_weighting, MultiGrid.hpp:187-205)
+ *     pgmg_prolong   Parallel::ComputeProlungator  Parallel_Method.cu:188-199
+ *                    (mode 0: MultigridSolver::prolongation, MultiGrid.hpp:208-226;
+ *                     mode 1: the symmetric prolungator_kernel, Parallel_Method.cu:79-138)
+ *     pgmg_norm      DynamicGridUtils::norm        DynamicGridUtils.hpp:21-27
+ *     pgmg_rhs       DynamicGridUtils::compute_rhs DynamicGridUtils.hpp:111-124
+ *
+ * Threading: a context is driven by one host thread; not thread-safe.
+ */
+#ifndef PGMG_H
+#define PGMG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PGMG_OK 0
+#define PGMG_ERR_ARG (-1)     /* bad argument (N not 2^k+1, null pointer, ...) */
+#define PGMG_ERR_HIP (-2)     /* HIP runtime error                              */
+#define PGMG_ERR_NOMEM (-3)   /* device allocation failed                       */
+#define PGMG_ERR_COMM (-4)    /* RCCL error                                     */
+#define PGMG_ERR_STATE (-5)   /* call out of order (e.g. vcycle before set_problem) */
+
+/* prolongation flavours */
+#define PGMG_PROLONG_REFERENCE 0 /* mg_cpu_exec: fine row/col 1 uncorrected */
+#define PGMG_PROLONG_SYMMETRIC 1 /* gpu_exec's prolungator_kernel; fine boundary set 0  */
+
+/* config flags */
+#define PGMG_FLAG_NO_GRAPH 1u    /* launch eagerly instead of replaying a hipGraph */
+#define PGMG_FLAG_TIME_FINE 2u   /* eager launches + hipEvents around every finest-level
+                                    plain Jacobi sweep (see pgmg_fine_sweep_time)   */
+
+typedef struct pgmg_config {
+    int N;             /* points per side incl. boundary; 2^k + 1, k >= 2        */
+    int v1, v2;        /* pre/post smoother num_iter (v+1 sweeps), default 1, 1  */
+    int coarse_iter;   /* num_iter on the coarsest grid, default 10 (11 sweeps)  */
+    int n_coarse;      /* recursion floor N_coarse, default 5                    */
+    int alpha;         /* W-cycle recursion count, default 3                     */
+    double eps;        /* smoother early-exit tolerance, default 1e-7; <0: never */
+    double a, p, q;    /* domain edge and RHS wave numbers, default 1, 1, 1      */
+    int tail_n;        /* levels with N <= tail_n run in one workgroup (<= 65)   */
+    int device;        /* HIP device ordinal, default 0                          */
+    unsigned flags;    /* PGMG_FLAG_*                                            */
+    /* row-strip domain decomposition over `world` ranks (one process per GPU). */
+    int rank, world;   /* default 0, 1                                           */
+    const void *nccl_unique_id;  /* 128-byte ncclUniqueId when world > 1      */
+    int gather_n;      /* levels with N <= gather_n collapse to rank 0 (world>1) */
+} pgmg_config;
+
+typedef struct pgmg_ctx pgmg_ctx;
+
+/* Fill `cfg` with the reference defaults for grid size N. */
+int pgmg_config_default(pgmg_config *cfg, int N);
+
+int pgmg_create(pgmg_ctx **ctx, const pgmg_config *cfg);
+int pgmg_destroy(pgmg_ctx *ctx);
+
+/* Upload phi0 (N*N, NULL -> zeros) and f (N*N, NULL -> the analytic RHS of
+ * DynamicGridUtils::compute_rhs, generated on the device bit-identically from
+ * host libm sine tables).  Host arrays in the reference layout (pitch N).  With
+ * world > 1 every rank passes the full arrays (or NULLs) and keeps its strip. */
+int pgmg_set_problem(pgmg_ctx *ctx, const double *phi0, const double *f);
+
+/* Enqueue `ncycles` cycles on the context's stream (asynchronous). */
+int pgmg_vcycle(pgmg_ctx *ctx, int ncycles);
+int pgmg_wcycle(pgmg_ctx *ctx, int ncycles);
+int pgmg_fcycle(pgmg_ctx *ctx, int ncycles);
+int pgmg_sync(pgmg_ctx *ctx);
+
+/* Download phi (N*N, reference layout).  world > 1: every rank receives the
+ * full grid (strips are gathered to all ranks). */
+int pgmg_get_solution(pgmg_ctx *ctx, double *phi_host);
+
+/* sqrt(sum over interior of r^2) for the current phi (synchronous). */
+int pgmg_residual_norm(pgmg_ctx *ctx, double *out);
+
+/* Cumulative smoother sweeps and early exits since set_problem
+ * (comparable with the oracle's counters). */
+int pgmg_stats(pgmg_ctx *ctx, long long *sweeps, long long *early_exits);
+
+/* Device time of the last pgmg_vcycle/wcycle call in ms (hipEvents on the
+ * context stream; synchronous). */
+int pgmg_last_elapsed_ms(pgmg_ctx *ctx, double *ms);
+
+/* Number of bulk (multi-kernel) levels and the tail's top N. */
+int pgmg_levels(pgmg_ctx *ctx, int *bulk_levels, int *tail_top_n);
+
+/* Algorithmic HBM bytes one V-cycle moves (per rank), summed per kernel. */
+int pgmg_vcycle_bytes(pgmg_ctx *ctx, double *bytes);
+
+/* Raw device pointer and pitch (in doubles) of phi's element (0,0) on this
+ * rank, for callers that want to read it in place. */
+int pgmg_phi_device(pgmg_ctx *ctx, double **ptr, int *pitch, int *row0, int *rows);
+
+/* Count and mean device duration (ms) of the finest-level plain Jacobi sweeps
+ * launched since the last call (needs PGMG_FLAG_TIME_FINE).  Synchronous. */
+int pgmg_fine_sweep_time(pgmg_ctx *ctx, int *count, double *mean_ms);
+
+/* Time `reps` back-to-back fine-grid Jacobi sweeps (the roofline kernel) on the
+ * context's level-0 buffers with hipEvents; returns the mean per sweep in ms.
+ * Leaves phi changed (call set_problem again before parity checks). */
+int pgmg_bench_sweep(pgmg_ctx *ctx, int reps, double *ms_per_sweep);
+
+/* ---- op level (device pointers, reference layout, pitch = W) ------------- */
+/* v+1 sweeps; eps < 0 disables the early exit.  d_tmp: W*H scratch or NULL
+ * (allocated internally).  *sweeps_done (may be NULL) receives the sweep count
+ * (synchronous when non-NULL). */
+int pgmg_jacobi(double *d_x, double *d_tmp, const double *d_f, int H, int W, double h, int v,
+                double eps, int *sweeps_done, void *stream);
+int pgmg_residual(double *d_r, const double *d_x, const double *d_f, int H, int W, double h,
+                  void *stream);
+int pgmg_restrict(const double *d_fine, double *d_coarse, int Nf, int Nc, void *stream);
+int pgmg_prolong(const double *d_coarse, double *d_fine, int Nc, int Nf, int mode, void *stream);
+int pgmg_norm(const double *d_v, long long n, double *result, void *stream);
+int pgmg_rhs(double *d_f, int W, int H, double h, double a, double p, double q, void *stream);
+
+/* ---- device memory helpers (for host code built without HIP headers) ----- */
+int pgmg_device_alloc(void **ptr, size_t bytes);
+int pgmg_device_free(void *ptr);
+int pgmg_memcpy_h2d(void *dst, const void *src, size_t bytes);
+int pgmg_memcpy_d2h(void *dst, const void *src, size_t bytes);
+int pgmg_device_sync(void);
+int pgmg_device_count(int *n);
+
+/* RCCL bootstrap: fill a 128-byte buffer with a fresh ncclUniqueId (rank 0). */
+int pgmg_comm_unique_id(void *out128);
+
+const char *pgmg_last_error(void);
+const char *pgmg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PGMG_H */

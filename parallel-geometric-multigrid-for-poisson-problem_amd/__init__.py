@@ -1,0 +1,197 @@
+"""MI355X-native geometric multigrid for the 2D Poisson problem (fp64).
+
+The hot path (Jacobi smoother, residual + norm, full-weighting restriction,
+prolongation, V/W-cycles) is hand-written HIP for gfx950 in ``csrc/`` behind the C ABI
+of ``include/pgmg.h`` (libpgmg.so).  This Python package is plumbing: a ctypes
+wrapper used by the tests, ``bench.py`` and ``__graft_entry__``.  The C++ mirror of
+the reference's own entry points (``Parallel``, ``ParallelMultiGridSolver``,
+``ParallelTestRunner``, ``gpu_exec``) lives in ``host/``.
+
+Import name: the directory name is not a Python identifier, so load it with
+``_pkgload.load()`` from the repository root (registers it as ``pgmg_amd``).
+"""
+import ctypes as C
+import pathlib
+import subprocess
+
+import numpy as np
+
+from ._capi import (PGMG_FLAG_NO_GRAPH, PGMG_FLAG_TIME_FINE, PGMG_PROLONG_REFERENCE,
+                    PGMG_PROLONG_SYMMETRIC, PgmgConfig, PgmgError, check, load)
+
+PKG_DIR = pathlib.Path(__file__).resolve().parent
+
+__all__ = [
+    "build", "load", "Solver", "PgmgConfig", "PgmgError", "ops",
+    "PGMG_FLAG_NO_GRAPH", "PGMG_FLAG_TIME_FINE", "PGMG_PROLONG_REFERENCE",
+    "PGMG_PROLONG_SYMMETRIC",
+]
+
+
+def build(jobs=8, verbose=False):
+    """Compile libpgmg.so (and host/gpu_exec) for gfx950 in-tree."""
+    cmd = ["make", "-C", str(PKG_DIR), f"-j{jobs}", "all"]
+    r = subprocess.run(cmd, capture_output=not verbose, text=True)
+    if r.returncode != 0:
+        raise PgmgError(f"build failed:\n{r.stdout}\n{r.stderr}")
+    return PKG_DIR / "libpgmg.so"
+
+
+def default_config(N, **kw):
+    cfg = PgmgConfig()
+    check(load().pgmg_config_default(C.byref(cfg), int(N)), "pgmg_config_default")
+    for k, v in kw.items():
+        if not hasattr(cfg, k):
+            raise TypeError(f"unknown config field {k}")
+        setattr(cfg, k, v)
+    return cfg
+
+
+class Solver:
+    """A multigrid context: level pyramid resident in HBM, cycles on a HIP stream.
+
+    Mirrors ParallelTestRunner::run_v_cycle / ParallelMultiGridSolver::v_cycle
+    (3_part_parallel/ParallelTestRunner.cu:152-186, Parallel_Mg.cu:21-60) with the
+    numerics of MultigridSolver (2_part_MG/MultiGrid.hpp:57-136).
+    """
+
+    def __init__(self, N, **cfg):
+        self.lib = load()
+        self.cfg = default_config(N, **cfg)
+        self._keep = None
+        if self.cfg.world > 1 and "nccl_unique_id" in cfg:
+            self._keep = cfg["nccl_unique_id"]
+        h = C.c_void_p()
+        check(self.lib.pgmg_create(C.byref(h), C.byref(self.cfg)), "pgmg_create")
+        self.h = h
+        self.N = int(N)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.pgmg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def set_problem(self, phi0=None, f=None):
+        N = self.N
+        args = []
+        for a in (phi0, f):
+            if a is None:
+                args.append(None)
+            else:
+                a = np.ascontiguousarray(a, dtype=np.float64)
+                assert a.shape == (N, N), a.shape
+                args.append(a)
+        p = [None if a is None else a.ctypes.data_as(C.c_void_p) for a in args]
+        check(self.lib.pgmg_set_problem(self.h, p[0], p[1]), "pgmg_set_problem")
+
+    def vcycle(self, n=1):
+        check(self.lib.pgmg_vcycle(self.h, int(n)), "pgmg_vcycle")
+
+    def wcycle(self, n=1):
+        check(self.lib.pgmg_wcycle(self.h, int(n)), "pgmg_wcycle")
+
+    def fcycle(self, n=1):
+        check(self.lib.pgmg_fcycle(self.h, int(n)), "pgmg_fcycle")
+
+    def sync(self):
+        check(self.lib.pgmg_sync(self.h), "pgmg_sync")
+
+    def solution(self):
+        out = np.empty((self.N, self.N), dtype=np.float64)
+        check(self.lib.pgmg_get_solution(self.h, out.ctypes.data_as(C.c_void_p)),
+              "pgmg_get_solution")
+        return out
+
+    def residual_norm(self):
+        v = C.c_double()
+        check(self.lib.pgmg_residual_norm(self.h, C.byref(v)), "pgmg_residual_norm")
+        return v.value
+
+    def stats(self):
+        s, e = C.c_longlong(), C.c_longlong()
+        check(self.lib.pgmg_stats(self.h, C.byref(s), C.byref(e)), "pgmg_stats")
+        return s.value, e.value
+
+    def last_elapsed_ms(self):
+        v = C.c_double()
+        check(self.lib.pgmg_last_elapsed_ms(self.h, C.byref(v)), "pgmg_last_elapsed_ms")
+        return v.value
+
+    def levels(self):
+        b, t = C.c_int(), C.c_int()
+        check(self.lib.pgmg_levels(self.h, C.byref(b), C.byref(t)), "pgmg_levels")
+        return b.value, t.value
+
+    def vcycle_bytes(self):
+        v = C.c_double()
+        check(self.lib.pgmg_vcycle_bytes(self.h, C.byref(v)), "pgmg_vcycle_bytes")
+        return v.value
+
+    def fine_sweep_time(self):
+        n, m = C.c_int(), C.c_double()
+        check(self.lib.pgmg_fine_sweep_time(self.h, C.byref(n), C.byref(m)),
+              "pgmg_fine_sweep_time")
+        return n.value, m.value
+
+    def bench_sweep(self, reps):
+        m = C.c_double()
+        check(self.lib.pgmg_bench_sweep(self.h, int(reps), C.byref(m)), "pgmg_bench_sweep")
+        return m.value
+
+
+class _Ops:
+    """Op-level entries on caller-owned device buffers (torch tensors or raw pointers),
+    mirroring Parallel::Compute* (3_part_parallel/Parallel_Method.cu:144-199)."""
+
+    @staticmethod
+    def _ptr(t):
+        if t is None:
+            return None
+        if isinstance(t, int):
+            return C.c_void_p(t)
+        return C.c_void_p(t.data_ptr())
+
+    def jacobi(self, x, f, h, v, eps=1e-7, tmp=None, stream=None):
+        H, W = x.shape
+        done = C.c_int()
+        check(load().pgmg_jacobi(self._ptr(x), self._ptr(tmp), self._ptr(f), H, W, float(h),
+                                 int(v), float(eps), C.byref(done), stream), "pgmg_jacobi")
+        return done.value
+
+    def residual(self, r, x, f, h, stream=None):
+        H, W = x.shape
+        check(load().pgmg_residual(self._ptr(r), self._ptr(x), self._ptr(f), H, W, float(h),
+                                   stream), "pgmg_residual")
+
+    def restrict(self, fine, coarse, stream=None):
+        check(load().pgmg_restrict(self._ptr(fine), self._ptr(coarse), fine.shape[0],
+                                   coarse.shape[0], stream), "pgmg_restrict")
+
+    def prolong(self, coarse, fine, mode=PGMG_PROLONG_REFERENCE, stream=None):
+        check(load().pgmg_prolong(self._ptr(coarse), self._ptr(fine), coarse.shape[0],
+                                  fine.shape[0], int(mode), stream), "pgmg_prolong")
+
+    def norm(self, v, stream=None):
+        out = C.c_double()
+        check(load().pgmg_norm(self._ptr(v), v.numel(), C.byref(out), stream), "pgmg_norm")
+        return out.value
+
+    def rhs(self, f, h, a=1.0, p=1.0, q=1.0, stream=None):
+        H, W = f.shape
+        check(load().pgmg_rhs(self._ptr(f), W, H, float(h), float(a), float(p), float(q),
+                              stream), "pgmg_rhs")
+
+
+ops = _Ops()

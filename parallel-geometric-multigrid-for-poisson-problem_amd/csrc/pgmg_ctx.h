@@ -1,0 +1,89 @@
+// pgmg_ctx.h — the context object behind the C ABI (shared by the orchestration
+// in pgmg_ctx.hip and the row-strip communication layer in pgmg_comm.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/pgmg.h"
+#include "pgmg_internal.h"
+
+namespace pgmg {
+
+constexpr int kMaxSweeps = 64;  // early-exit flag slots per smooth call
+
+int set_err(int code, const std::string &msg);
+
+#define PGMG_HIPC(expr)                                                                           \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess)                                                                     \
+            return ::pgmg::set_err(PGMG_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+struct Grid {
+    double *base = nullptr;  // allocation
+    double *o = nullptr;     // virtual origin: element (global row j, col i) at o[j*P + i]
+};
+
+struct Level {
+    int N = 0, P = 0;
+    double h = 0, hh = 0, ih = 0;
+    int lo = 0, hi = 0;      // owned global rows [lo, hi) (row 0 / N-1 belong to the ends)
+    int u0 = 0, u1 = 0;      // interior rows this rank updates: [max(lo,1), min(hi,N-1))
+    Grid A, B, F;            // solution (phi or e), ping-pong, right-hand side (f or rc)
+    bool on_this_rank = true;
+    bool gathered = false;   // the level lives entirely on rank 0
+};
+
+class Comm;
+
+}  // namespace pgmg
+
+struct pgmg_ctx {
+    pgmg_config cfg{};
+    hipStream_t s = nullptr;
+    std::vector<pgmg::Level> lv;  // 0 .. nb-1 bulk levels, nb = the tail's top level
+    int nb = 0;
+    double *partials = nullptr;
+    int partials_cap = 0;
+    unsigned *flags = nullptr;
+    unsigned long long *stats = nullptr;
+    double *scalar = nullptr;
+    hipGraphExec_t gexec = nullptr;
+    bool have_problem = false;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::vector<hipEvent_t> tev;  // fine-sweep timing event pool (PGMG_FLAG_TIME_FINE)
+    int tev_used = 0;
+    pgmg::Comm *comm = nullptr;   // non-null when world > 1
+};
+
+namespace pgmg {
+
+int alloc_grid(Grid &g, const Level &L);
+void free_grid(Grid &g);
+int enqueue_cycle(pgmg_ctx *c, int l, int gamma, bool x0_zero);
+int enqueue_tail(pgmg_ctx *c, int gamma, bool x0_from_global);
+
+// Row-strip domain decomposition over RCCL (one process per GPU).
+class Comm {
+  public:
+    virtual ~Comm() {}
+    // decide ownership (lo/hi/u0/u1, on_this_rank, gathered) for every level
+    virtual int plan(pgmg_ctx *c) = 0;
+    // after allocation: communicators, staging buffers
+    virtual int setup(pgmg_ctx *c) = 0;
+    // exchange `depth` halo rows of the level-l array whose origin is `o`
+    virtual int halo(double *o, const Level &L, int depth, hipStream_t s) = 0;
+    // early-exit decision with a global (all-rank) norm
+    virtual int fixup(const FixupArgs &f, hipStream_t s) = 0;
+    virtual int allreduce_sum(double *d_scalar, hipStream_t s) = 0;
+    // level l is the first gathered level: move rc to rank 0, run the rest there,
+    // move e back
+    virtual int run_gathered(pgmg_ctx *c, int l, int gamma, bool x0_zero) = 0;
+    virtual int gather_solution(pgmg_ctx *c, double *phi_host) = 0;
+    static Comm *create(pgmg_ctx *c, int *rc);
+};
+
+}  // namespace pgmg

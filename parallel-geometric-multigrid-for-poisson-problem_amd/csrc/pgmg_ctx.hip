@@ -1,0 +1,622 @@
+// pgmg_ctx.hip — context, level pyramid, cycle orchestration and the C ABI.
+//
+// Replaces the reference's ParallelMultiGridSolver (3_part_parallel/Parallel_Mg.cu)
+// and the allocation/timing plumbing of ParallelTestRunner::run_v_cycle
+// (3_part_parallel/ParallelTestRunner.cu:152-186), MI355X-first:
+//   * the whole level pyramid is allocated once in HBM (no per-level, per-cycle
+//     cudaMallocManaged, no unified-memory migration, no host sync per kernel);
+//   * each bulk level (N > tail_n) is 2 pre sweeps + fused residual/restriction
+//     + prolongation + 2 post sweeps on ping-pong buffers; the smoother's
+//     per-sweep early exit (Smoother.hpp:75-88) is evaluated on the device by
+//     speculating the next sweep and undoing it when the check fires;
+//   * the coarse end (N <= tail_n) is one LDS-resident workgroup (pgmg_tail.hip);
+//   * a V-cycle is captured once into a hipGraph and replayed.
+//
+// Row strips: every per-level array is addressed through a "virtual origin"
+// pointer o with element (global row j, column i) at o[j*P + i]; a rank only
+// allocates its owned rows plus two halo rows each side, so all kernels work in
+// global row numbers and the fine/coarse row parity (j = 2 jc) is preserved.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "pgmg_ctx.h"
+
+using namespace pgmg;
+
+static thread_local std::string g_err;
+
+int pgmg::set_err(int code, const std::string &msg)
+{
+    g_err = msg;
+    return code;
+}
+
+#define HIPC(expr) PGMG_HIPC(expr)
+
+// ---------------------------------------------------------------------------
+// allocation
+// ---------------------------------------------------------------------------
+int pgmg::alloc_grid(Grid &g, const Level &L)
+{
+    const int rows = (L.hi - L.lo) + 4;  // owned + 2 halo rows each side
+    const size_t n = (size_t)kOff + (size_t)rows * L.P + 64;
+    void *p = nullptr;
+    if (hipMalloc(&p, n * sizeof(double)) != hipSuccess)
+        return set_err(PGMG_ERR_NOMEM, "hipMalloc failed for a level of N=" + std::to_string(L.N));
+    HIPC(hipMemset(p, 0, n * sizeof(double)));
+    g.base = (double *)p;
+    g.o = g.base + kOff + (ptrdiff_t)(2 - L.lo) * L.P;
+    return PGMG_OK;
+}
+
+void pgmg::free_grid(Grid &g)
+{
+    if (g.base) (void)hipFree(g.base);
+    g.base = g.o = nullptr;
+}
+
+// ---------------------------------------------------------------------------
+// kernel sequences
+// ---------------------------------------------------------------------------
+static unsigned *smooth_flags(pgmg_ctx *c, int l, int which)
+{
+    return c->flags + ((size_t)l * 2 + which) * kMaxSweeps;
+}
+
+static double *const kZeroMarker = nullptr;
+
+// one JacobiSmoother::smooth(x = L.A, f = L.F, num_iter = v) on a bulk level
+static int enqueue_smooth(pgmg_ctx *c, int l, int which, int v, bool x0_zero)
+{
+    Level &L = c->lv[l];
+    const int S = v + 1;
+    unsigned *D = smooth_flags(c, l, which);
+    const bool fine = (l == 0);
+    for (int k = 1; k <= S; ++k) {
+        double *in = (k & 1) ? L.A.o : L.B.o;
+        double *out = (k & 1) ? L.B.o : L.A.o;
+        if (c->comm && !(k == 1 && x0_zero)) {
+            int e = c->comm->halo(in, L, 1, c->s);
+            if (e) return e;
+        }
+        SweepArgs a{};
+        a.xin = (k == 1 && x0_zero) ? kZeroMarker : in;
+        a.f = L.F.o;
+        a.xout = out;
+        a.partials = (k >= 2) ? c->partials : nullptr;
+        a.skip = (k >= 2) ? &D[k - 1] : nullptr;
+        a.reset = (k == 1) ? &D[1] : nullptr;
+        a.stats = c->stats;
+        a.hh = L.hh;
+        a.inv_hh = L.ih;
+        a.W = L.N;
+        a.P = L.P;
+        a.row0 = L.u0;
+        a.row1 = L.u1;
+        const bool timed = fine && (c->cfg.flags & PGMG_FLAG_TIME_FINE) && a.partials == nullptr &&
+                           !(k == 1 && x0_zero) && c->tev_used + 2 <= (int)c->tev.size();
+        if (timed) HIPC(hipEventRecord(c->tev[c->tev_used], c->s));
+        launch_sweep(a, k == 1 && x0_zero, l == 0, c->s);
+        if (timed) {
+            HIPC(hipEventRecord(c->tev[c->tev_used + 1], c->s));
+            c->tev_used += 2;
+        }
+        if (k >= 2) {
+            int rpb, gx, gy;
+            const int np = sweep_blocks(L.N, L.u0, L.u1, &rpb, &gx, &gy);
+            FixupArgs f{};
+            f.partials = c->partials;
+            f.np = np;
+            f.eps = c->cfg.eps;
+            f.done_prev = &D[k - 1];
+            f.done_next = &D[k];
+            f.src = in;
+            f.dst = out;
+            f.stats = c->stats;
+            f.W = L.N;
+            f.P = L.P;
+            f.row0 = L.u0;
+            f.row1 = L.u1;
+            if (c->comm) {
+                int e = c->comm->fixup(f, c->s);
+                if (e) return e;
+            } else {
+                launch_fixup(f, c->s);
+            }
+        }
+    }
+    if (S & 1) launch_copy_rows(L.B.o, L.A.o, L.N, L.P, L.u0, L.u1, c->s);
+    return PGMG_OK;
+}
+
+int pgmg::enqueue_tail(pgmg_ctx *c, int gamma, bool x0_from_global)
+{
+    Level &T = c->lv[c->nb];
+    TailArgs t{};
+    t.f_top = T.F.o;
+    t.e_top = T.A.o;
+    t.P_top = T.P;
+    t.N_top = T.N;
+    t.h_top = T.h;
+    t.x0_from_global = x0_from_global ? 1 : 0;
+    t.v1 = c->cfg.v1;
+    t.v2 = c->cfg.v2;
+    t.coarse_iter = c->cfg.coarse_iter;
+    t.n_coarse = c->cfg.n_coarse;
+    t.eps = c->cfg.eps;
+    t.stats = c->stats;
+    HIPC(launch_tail_gamma(t, gamma, c->s));
+    return PGMG_OK;
+}
+
+// MultigridSolver::v_cycle / w_cycle (MultiGrid.hpp:57-136) on level l
+int pgmg::enqueue_cycle(pgmg_ctx *c, int l, int gamma, bool x0_zero)
+{
+    if (l == c->nb) {
+        if (c->comm) return c->comm->run_gathered(c, l, gamma, x0_zero);
+        return enqueue_tail(c, gamma, !x0_zero);
+    }
+    Level &L = c->lv[l];
+    Level &C = c->lv[l + 1];
+    int e = enqueue_smooth(c, l, 0, c->cfg.v1, x0_zero);
+    if (e) return e;
+    if (c->comm) {
+        e = c->comm->halo(L.A.o, L, 2, c->s);
+        if (e) return e;
+        e = c->comm->halo(L.F.o, L, 1, c->s);
+        if (e) return e;
+    }
+    ResRestrictArgs r{};
+    r.x = L.A.o;
+    r.f = L.F.o;
+    r.rc = C.F.o;
+    r.inv_hh = L.ih;
+    r.Wf = L.N;
+    r.Pf = L.P;
+    r.Wc = C.N;
+    r.Pc = C.P;
+    r.jc0 = C.u0;
+    r.jc1 = C.u1;
+    launch_res_restrict(r, c->s);
+    for (int i = 0; i < gamma; ++i) {
+        e = enqueue_cycle(c, l + 1, gamma, i == 0);
+        if (e) return e;
+    }
+    if (c->comm) {
+        e = c->comm->halo(C.A.o, C, 1, c->s);
+        if (e) return e;
+    }
+    ProlongArgs p{};
+    p.c = C.A.o;
+    p.fine = L.A.o;
+    p.Wf = L.N;
+    p.Pf = L.P;
+    p.Wc = C.N;
+    p.Pc = C.P;
+    p.row0 = L.u0 > 2 ? L.u0 : 2;
+    p.row1 = L.u1 < L.N - 1 ? L.u1 : L.N - 1;
+    if (p.row1 > p.row0) launch_prolong(p, c->s);
+    return enqueue_smooth(c, l, 1, c->cfg.v2, false);
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+const char *pgmg_last_error(void) { return g_err.c_str(); }
+const char *pgmg_version(void) { return "pgmg 0.1 (gfx950, fp64, row-strip RCCL)"; }
+
+int pgmg_config_default(pgmg_config *cfg, int N)
+{
+    if (!cfg) return set_err(PGMG_ERR_ARG, "null cfg");
+    std::memset(cfg, 0, sizeof(*cfg));
+    cfg->N = N;
+    cfg->v1 = 1;           // MultiGrid.hpp:15
+    cfg->v2 = 1;           // MultiGrid.hpp:16
+    cfg->coarse_iter = 10; // MultiGrid.hpp:61
+    cfg->n_coarse = 5;     // MultiGrid.hpp:19
+    cfg->alpha = 3;        // 2_part_MG/main.cpp:15
+    cfg->eps = 1e-7;       // 2_part_MG/main.cpp:12
+    cfg->a = 1.0;          // globals.cpp:2-4
+    cfg->p = 1.0;
+    cfg->q = 1.0;
+    cfg->tail_n = kTailMaxN;
+    cfg->device = 0;
+    cfg->flags = 0;
+    cfg->rank = 0;
+    cfg->world = 1;
+    cfg->nccl_unique_id = nullptr;
+    cfg->gather_n = 1025;
+    return PGMG_OK;
+}
+
+static bool is_pow2p1(int N)
+{
+    if (N < 3) return false;
+    const int g = N - 1;
+    return (g & (g - 1)) == 0;
+}
+
+int pgmg_destroy(pgmg_ctx *c)
+{
+    if (!c) return PGMG_OK;
+    if (c->s) (void)hipStreamSynchronize(c->s);
+    if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
+    for (auto &L : c->lv) {
+        free_grid(L.A);
+        free_grid(L.B);
+        free_grid(L.F);
+    }
+    if (c->partials) (void)hipFree(c->partials);
+    if (c->flags) (void)hipFree(c->flags);
+    if (c->stats) (void)hipFree(c->stats);
+    if (c->scalar) (void)hipFree(c->scalar);
+    for (auto e : c->tev) (void)hipEventDestroy(e);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    delete c->comm;
+    if (c->s) (void)hipStreamDestroy(c->s);
+    delete c;
+    return PGMG_OK;
+}
+
+int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
+{
+    if (!out || !cfg) return set_err(PGMG_ERR_ARG, "null argument");
+    *out = nullptr;
+    if (!is_pow2p1(cfg->N) || cfg->N < 5)
+        return set_err(PGMG_ERR_ARG, "N must be 2^k + 1 with N >= 5 (2_part_MG/main.cpp:6)");
+    if (cfg->v1 < 0 || cfg->v2 < 0 || cfg->v1 + 1 >= kMaxSweeps || cfg->v2 + 1 >= kMaxSweeps ||
+        cfg->coarse_iter < 0 || cfg->n_coarse < 3 || cfg->alpha < 1)
+        return set_err(PGMG_ERR_ARG, "bad smoother/cycle parameters");
+    if (cfg->world < 1 || cfg->rank < 0 || cfg->rank >= cfg->world)
+        return set_err(PGMG_ERR_ARG, "bad rank/world");
+    int ndev = 0;
+    HIPC(hipGetDeviceCount(&ndev));
+    if (cfg->device < 0 || cfg->device >= ndev) return set_err(PGMG_ERR_ARG, "bad device ordinal");
+    HIPC(hipSetDevice(cfg->device));
+
+    pgmg_ctx *c = new pgmg_ctx();
+    c->cfg = *cfg;
+    int tail_n = cfg->tail_n;
+    if (tail_n > kTailMaxN) tail_n = kTailMaxN;
+    if (tail_n < cfg->n_coarse) tail_n = cfg->n_coarse;
+    c->cfg.tail_n = tail_n;
+
+    // level sizes: bulk while N > tail_n, then the tail's top level
+    int N = cfg->N;
+    double h = cfg->a / (N - 1);  // MultiGridTestRunner.hpp:131
+    for (;;) {
+        Level L;
+        L.N = N;
+        L.P = pitch_for(N);
+        L.h = h;
+        L.hh = h * h;
+        L.ih = 1.0 / (h * h);
+        L.lo = 0;
+        L.hi = N;
+        L.u0 = 1;
+        L.u1 = N - 1;
+        c->lv.push_back(L);
+        if (N <= tail_n || N <= cfg->n_coarse) break;
+        N = (N - 1) / 2 + 1;
+        h = 2 * h;  // MultiGrid.hpp:83
+    }
+    c->nb = (int)c->lv.size() - 1;
+
+    int rc = PGMG_OK;
+    if (cfg->world > 1) {
+        c->comm = Comm::create(c, &rc);
+        if (!c->comm) {
+            pgmg_destroy(c);
+            return rc;
+        }
+        rc = c->comm->plan(c);
+    }
+
+    for (int l = 0; l < (int)c->lv.size() && rc == PGMG_OK; ++l) {
+        Level &L = c->lv[l];
+        if (!L.on_this_rank) continue;
+        rc = alloc_grid(L.A, L);
+        if (rc == PGMG_OK) rc = alloc_grid(L.F, L);
+        if (rc == PGMG_OK && l < c->nb) rc = alloc_grid(L.B, L);
+    }
+    int maxblocks = 256;
+    for (int l = 0; l < c->nb; ++l) {
+        int rpb, gx, gy;
+        const int nbk = sweep_blocks(c->lv[l].N, c->lv[l].u0, c->lv[l].u1, &rpb, &gx, &gy);
+        if (nbk > maxblocks) maxblocks = nbk;
+    }
+    c->partials_cap = maxblocks;
+    if (rc == PGMG_OK && hipMalloc((void **)&c->partials, sizeof(double) * maxblocks) != hipSuccess)
+        rc = set_err(PGMG_ERR_NOMEM, "partials");
+    const size_t nflags = (size_t)(c->lv.size() + 1) * 2 * kMaxSweeps;
+    if (rc == PGMG_OK && hipMalloc((void **)&c->flags, sizeof(unsigned) * nflags) != hipSuccess)
+        rc = set_err(PGMG_ERR_NOMEM, "flags");
+    if (rc == PGMG_OK && hipMalloc((void **)&c->stats, 4 * sizeof(unsigned long long)) != hipSuccess)
+        rc = set_err(PGMG_ERR_NOMEM, "stats");
+    if (rc == PGMG_OK && hipMalloc((void **)&c->scalar, 8 * sizeof(double)) != hipSuccess)
+        rc = set_err(PGMG_ERR_NOMEM, "scalar");
+    if (rc == PGMG_OK) {
+        if (hipMemset(c->flags, 0, sizeof(unsigned) * nflags) != hipSuccess ||
+            hipMemset(c->stats, 0, 4 * sizeof(unsigned long long)) != hipSuccess ||
+            hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess)
+            rc = set_err(PGMG_ERR_HIP, "stream/event setup failed");
+    }
+    if (rc == PGMG_OK && (cfg->flags & PGMG_FLAG_TIME_FINE)) {
+        c->tev.resize(1024);
+        for (auto &e : c->tev)
+            if (hipEventCreate(&e) != hipSuccess) rc = set_err(PGMG_ERR_HIP, "event pool");
+    }
+    if (rc == PGMG_OK && c->comm) rc = c->comm->setup(c);
+    if (rc != PGMG_OK) {
+        pgmg_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return PGMG_OK;
+}
+
+// host sine tables -> bit-identical compute_rhs on the device
+static void sine_tables(const pgmg_config &cfg, int N, double h, std::vector<double> &sx,
+                        std::vector<double> &sy, double &factor)
+{
+    factor = (M_PI * M_PI / (cfg.a * cfg.a)) * (cfg.p * cfg.p + cfg.q * cfg.q);
+    sx.resize(N);
+    sy.resize(N);
+    for (int i = 0; i < N; ++i) {
+        const double x = i * h;
+        sx[i] = std::sin(cfg.p * M_PI * x / cfg.a);
+        sy[i] = std::sin(cfg.q * M_PI * x / cfg.a);
+    }
+}
+
+int pgmg_set_problem(pgmg_ctx *c, const double *phi0, const double *f)
+{
+    if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
+    Level &L = c->lv[0];
+    const int N = L.N;
+    if (!L.on_this_rank) return set_err(PGMG_ERR_STATE, "level 0 not on this rank");
+    const int r0 = L.lo > 0 ? L.lo - 1 : 0;          // owned rows + one halo row each side
+    const int r1 = L.hi < N ? L.hi + 1 : N;
+    const size_t rows = (size_t)(r1 - r0);
+    HIPC(hipStreamSynchronize(c->s));
+    // phi (and its boundary copy in the ping-pong buffer B)
+    if (phi0) {
+        HIPC(hipMemcpy2D(L.A.o + (size_t)r0 * L.P, L.P * sizeof(double), phi0 + (size_t)r0 * N,
+                         N * sizeof(double), N * sizeof(double), rows, hipMemcpyHostToDevice));
+    } else {
+        HIPC(hipMemset2D(L.A.o + (size_t)r0 * L.P, L.P * sizeof(double), 0, N * sizeof(double), rows));
+    }
+    if (c->nb > 0)
+        HIPC(hipMemcpy2D(L.B.o + (size_t)r0 * L.P, L.P * sizeof(double), L.A.o + (size_t)r0 * L.P,
+                         L.P * sizeof(double), N * sizeof(double), rows, hipMemcpyDeviceToDevice));
+    if (f) {
+        HIPC(hipMemcpy2D(L.F.o + (size_t)r0 * L.P, L.P * sizeof(double), f + (size_t)r0 * N,
+                         N * sizeof(double), N * sizeof(double), rows, hipMemcpyHostToDevice));
+    } else {
+        std::vector<double> sx, sy;
+        double factor;
+        sine_tables(c->cfg, N, L.h, sx, sy, factor);
+        double *d = nullptr;
+        HIPC(hipMalloc((void **)&d, 2 * N * sizeof(double)));
+        HIPC(hipMemcpy(d, sx.data(), N * sizeof(double), hipMemcpyHostToDevice));
+        HIPC(hipMemcpy(d + N, sy.data(), N * sizeof(double), hipMemcpyHostToDevice));
+        launch_rhs(L.F.o, d, d + N, factor, N, L.P, r0, r1, c->s);
+        HIPC(hipGetLastError());
+        HIPC(hipStreamSynchronize(c->s));
+        HIPC(hipFree(d));
+    }
+    HIPC(hipMemset(c->stats, 0, 4 * sizeof(unsigned long long)));
+    HIPC(hipDeviceSynchronize());
+    c->have_problem = true;
+    return PGMG_OK;
+}
+
+static int run_cycles(pgmg_ctx *c, int ncycles, int gamma)
+{
+    if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
+    if (!c->have_problem) return set_err(PGMG_ERR_STATE, "pgmg_set_problem first");
+    if (ncycles <= 0) return PGMG_OK;
+    HIPC(hipEventRecord(c->ev0, c->s));
+    const bool use_graph = gamma == 1 && !(c->cfg.flags & PGMG_FLAG_NO_GRAPH) &&
+                           !(c->cfg.flags & PGMG_FLAG_TIME_FINE) && c->comm == nullptr;
+    if (use_graph && !c->gexec) {
+        // first cycle eagerly (sets kernel attributes), the rest from a captured graph
+        int e = enqueue_cycle(c, 0, 1, false);
+        if (e) return e;
+        HIPC(hipGetLastError());
+        --ncycles;
+        hipGraph_t g = nullptr;
+        HIPC(hipStreamBeginCapture(c->s, hipStreamCaptureModeThreadLocal));
+        e = enqueue_cycle(c, 0, 1, false);
+        hipError_t ce = hipStreamEndCapture(c->s, &g);
+        if (e) return e;
+        if (ce != hipSuccess) return set_err(PGMG_ERR_HIP, std::string("capture: ") + hipGetErrorString(ce));
+        HIPC(hipGraphInstantiate(&c->gexec, g, nullptr, nullptr, 0));
+        HIPC(hipGraphDestroy(g));
+    }
+    for (int k = 0; k < ncycles; ++k) {
+        if (use_graph) {
+            HIPC(hipGraphLaunch(c->gexec, c->s));
+        } else {
+            int e = enqueue_cycle(c, 0, gamma, false);
+            if (e) return e;
+        }
+    }
+    HIPC(hipGetLastError());
+    HIPC(hipEventRecord(c->ev1, c->s));
+    return PGMG_OK;
+}
+
+int pgmg_vcycle(pgmg_ctx *c, int ncycles) { return run_cycles(c, ncycles, 1); }
+int pgmg_wcycle(pgmg_ctx *c, int ncycles) { return run_cycles(c, ncycles, c ? c->cfg.alpha : 1); }
+
+int pgmg_fcycle(pgmg_ctx *c, int ncycles)
+{
+    (void)ncycles;
+    if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
+    return set_err(PGMG_ERR_STATE, "F-cycle (FMG) not implemented yet");
+}
+
+int pgmg_sync(pgmg_ctx *c)
+{
+    if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
+    HIPC(hipStreamSynchronize(c->s));
+    return PGMG_OK;
+}
+
+int pgmg_last_elapsed_ms(pgmg_ctx *c, double *ms)
+{
+    if (!c || !ms) return set_err(PGMG_ERR_ARG, "null argument");
+    HIPC(hipEventSynchronize(c->ev1));
+    float f = 0.f;
+    HIPC(hipEventElapsedTime(&f, c->ev0, c->ev1));
+    *ms = f;
+    return PGMG_OK;
+}
+
+int pgmg_get_solution(pgmg_ctx *c, double *phi)
+{
+    if (!c || !phi) return set_err(PGMG_ERR_ARG, "null argument");
+    HIPC(hipStreamSynchronize(c->s));
+    if (c->comm) return c->comm->gather_solution(c, phi);
+    Level &L = c->lv[0];
+    HIPC(hipMemcpy2D(phi, L.N * sizeof(double), L.A.o, L.P * sizeof(double), L.N * sizeof(double),
+                     L.N, hipMemcpyDeviceToHost));
+    return PGMG_OK;
+}
+
+int pgmg_residual_norm(pgmg_ctx *c, double *out)
+{
+    if (!c || !out) return set_err(PGMG_ERR_ARG, "null argument");
+    Level &L = c->lv[0];
+    int nbk = c->partials_cap < 1024 ? c->partials_cap : 1024;
+    if (c->comm) {
+        int e = c->comm->halo(L.A.o, L, 1, c->s);
+        if (e) return e;
+    }
+    launch_resnorm_partials(L.A.o, L.F.o, c->partials, L.ih, L.N, L.P, L.u0, L.u1, nbk, c->s);
+    launch_sum_partials(c->partials, nbk, c->scalar, c->s);
+    if (c->comm) {
+        int e = c->comm->allreduce_sum(c->scalar, c->s);
+        if (e) return e;
+    }
+    double s = 0.0;
+    HIPC(hipMemcpyAsync(&s, c->scalar, sizeof(double), hipMemcpyDeviceToHost, c->s));
+    HIPC(hipStreamSynchronize(c->s));
+    *out = std::sqrt(s);
+    return PGMG_OK;
+}
+
+int pgmg_stats(pgmg_ctx *c, long long *sweeps, long long *exits)
+{
+    if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
+    unsigned long long h[4];
+    HIPC(hipStreamSynchronize(c->s));
+    HIPC(hipMemcpy(h, c->stats, sizeof(h), hipMemcpyDeviceToHost));
+    if (sweeps) *sweeps = (long long)h[0];
+    if (exits) *exits = (long long)h[1];
+    return PGMG_OK;
+}
+
+int pgmg_levels(pgmg_ctx *c, int *bulk, int *tail_top)
+{
+    if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
+    if (bulk) *bulk = c->nb;
+    if (tail_top) *tail_top = c->lv[c->nb].N;
+    return PGMG_OK;
+}
+
+// algorithmic bytes of one V-cycle on this rank (DESIGN.md "Roofline accounting")
+int pgmg_vcycle_bytes(pgmg_ctx *c, double *bytes)
+{
+    if (!c || !bytes) return set_err(PGMG_ERR_ARG, "null argument");
+    double b = 0.0;
+    for (int l = 0; l < c->nb; ++l) {
+        const Level &L = c->lv[l];
+        const Level &C = c->lv[l + 1];
+        const double n = (double)(L.u1 - L.u0) * (L.N - 2);
+        const double nc = (double)(C.u1 - C.u0) * (C.N - 2);
+        const int S1 = c->cfg.v1 + 1, S2 = c->cfg.v2 + 1;
+        b += (l == 0 ? 24.0 : 16.0) * n + 24.0 * n * (S1 - 1);  // pre-smooth
+        b += 16.0 * n + 8.0 * nc;                                // residual + restriction
+        b += 16.0 * n + 8.0 * nc;                                // prolongation (RMW fine)
+        b += 24.0 * n * S2;                                      // post-smooth
+        if (S1 & 1) b += 16.0 * n;
+        if (S2 & 1) b += 16.0 * n;
+    }
+    const Level &T = c->lv[c->nb];
+    b += 16.0 * (double)T.N * T.N;                               // tail: f in, e out
+    *bytes = b;
+    return PGMG_OK;
+}
+
+int pgmg_phi_device(pgmg_ctx *c, double **ptr, int *pitch, int *row0, int *rows)
+{
+    if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
+    Level &L = c->lv[0];
+    if (ptr) *ptr = L.A.o;
+    if (pitch) *pitch = L.P;
+    if (row0) *row0 = L.lo;
+    if (rows) *rows = L.hi - L.lo;
+    return PGMG_OK;
+}
+
+int pgmg_bench_sweep(pgmg_ctx *c, int reps, double *ms)
+{
+    if (!c || !ms || reps <= 0) return set_err(PGMG_ERR_ARG, "bad argument");
+    if (c->nb == 0) return set_err(PGMG_ERR_STATE, "no bulk level");
+    Level &L = c->lv[0];
+    SweepArgs a{};
+    a.f = L.F.o;
+    a.hh = L.hh;
+    a.inv_hh = L.ih;
+    a.W = L.N;
+    a.P = L.P;
+    a.row0 = L.u0;
+    a.row1 = L.u1;
+    for (int k = 0; k < 2; ++k) {  // warm
+        a.xin = (k & 1) ? L.B.o : L.A.o;
+        a.xout = (k & 1) ? L.A.o : L.B.o;
+        launch_sweep(a, false, true, c->s);
+    }
+    HIPC(hipEventRecord(c->ev0, c->s));
+    for (int k = 0; k < reps; ++k) {
+        a.xin = (k & 1) ? L.B.o : L.A.o;
+        a.xout = (k & 1) ? L.A.o : L.B.o;
+        launch_sweep(a, false, true, c->s);
+    }
+    HIPC(hipEventRecord(c->ev1, c->s));
+    HIPC(hipEventSynchronize(c->ev1));
+    float f = 0.f;
+    HIPC(hipEventElapsedTime(&f, c->ev0, c->ev1));
+    *ms = f / reps;
+    return PGMG_OK;
+}
+
+int pgmg_fine_sweep_time(pgmg_ctx *c, int *count, double *mean_ms)
+{
+    if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
+    HIPC(hipStreamSynchronize(c->s));
+    double tot = 0.0;
+    const int n = c->tev_used / 2;
+    for (int i = 0; i < n; ++i) {
+        float f = 0.f;
+        HIPC(hipEventElapsedTime(&f, c->tev[2 * i], c->tev[2 * i + 1]));
+        tot += f;
+    }
+    if (count) *count = n;
+    if (mean_ms) *mean_ms = n ? tot / n : 0.0;
+    c->tev_used = 0;
+    return PGMG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,198 @@
+// pgmg_ops.hip — op-level C ABI on caller-owned device arrays (reference layout)
+// mirroring Parallel::ComputeJacobi / ComputeResidual / ComputeRestriction /
+// ComputeProlungator (3_part_parallel/Parallel_Method.cu:144-199), plus device
+// memory helpers so host code can drive the library without HIP headers.
+//
+// Unlike the reference kernels, the Jacobi op is out-of-place (ping-pong; the
+// reference's in-place jacobi_kernel races) and applies the CPU
+// smoother's residual-norm early exit when eps >= 0, so its result equals
+// JacobiSmoother::smooth bit for bit.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <vector>
+
+#include "pgmg_ctx.h"
+
+using namespace pgmg;
+
+#define HIPC(expr) PGMG_HIPC(expr)
+
+namespace {
+
+struct OpScratch {
+    double *partials = nullptr;
+    unsigned *flags = nullptr;
+    unsigned long long *stats = nullptr;
+    double *scalar = nullptr;
+    double *tmp = nullptr;
+    size_t tmp_elems = 0;
+};
+
+OpScratch g_op;
+
+int ensure_scratch(size_t tmp_elems)
+{
+    if (!g_op.partials) {
+        HIPC(hipMalloc((void **)&g_op.partials, 4096 * sizeof(double)));
+        HIPC(hipMalloc((void **)&g_op.flags, (kMaxSweeps + 2) * 128 * sizeof(unsigned)));
+        HIPC(hipMalloc((void **)&g_op.stats, 4 * sizeof(unsigned long long)));
+        HIPC(hipMalloc((void **)&g_op.scalar, 4 * sizeof(double)));
+    }
+    if (tmp_elems > g_op.tmp_elems) {
+        if (g_op.tmp) HIPC(hipFree(g_op.tmp));
+        g_op.tmp = nullptr;
+        HIPC(hipMalloc((void **)&g_op.tmp, tmp_elems * sizeof(double)));
+        g_op.tmp_elems = tmp_elems;
+    }
+    return PGMG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pgmg_jacobi(double *d_x, double *d_tmp, const double *d_f, int H, int W, double h, int v,
+                double eps, int *sweeps_done, void *stream)
+{
+    if (!d_x || !d_f || H < 3 || W < 3 || v < 0) return set_err(PGMG_ERR_ARG, "pgmg_jacobi: bad argument");
+    hipStream_t s = (hipStream_t)stream;
+    const size_t L = (size_t)H * W;
+    const int S = v + 1;
+    int e = ensure_scratch(d_tmp ? 0 : L);
+    if (e) return e;
+    double *tmp = d_tmp ? d_tmp : g_op.tmp;
+    const bool check = eps >= 0.0;
+    // flag slots: a fresh block of S+1 words per call would need a ring; the op is
+    // synchronous w.r.t. its own flags because every launch is stream-ordered.
+    unsigned *D = g_op.flags;
+    HIPC(hipMemsetAsync(g_op.stats, 0, 4 * sizeof(unsigned long long), s));
+    launch_g_copy(d_x, tmp, (long long)L, s);  // Smoother.hpp:47 out seeded with x
+    const double hh = h * h, ih = 1.0 / (h * h);
+    const int nb = g_blocks(H, W);
+    for (int k = 1; k <= S; ++k) {
+        const double *in = (k & 1) ? d_x : tmp;
+        double *out = (k & 1) ? tmp : d_x;
+        const bool with_check = check && k >= 2;
+        launch_g_sweep(in, d_f, out, with_check ? g_op.partials : nullptr,
+                       with_check ? &D[k - 1] : nullptr, k == 1 ? &D[1] : nullptr, g_op.stats, hh,
+                       ih, H, W, nb, s);
+        if (with_check)
+            launch_g_fixup(g_op.partials, nb, eps, &D[k - 1], &D[k], in, out, g_op.stats, H, W, s);
+    }
+    if (S & 1) launch_g_copy(tmp, d_x, (long long)L, s);
+    HIPC(hipGetLastError());
+    if (sweeps_done) {
+        unsigned long long st[4];
+        HIPC(hipMemcpyAsync(st, g_op.stats, sizeof(st), hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        *sweeps_done = (int)st[0];
+    }
+    return PGMG_OK;
+}
+
+int pgmg_residual(double *d_r, const double *d_x, const double *d_f, int H, int W, double h,
+                  void *stream)
+{
+    if (!d_r || !d_x || !d_f || H < 3 || W < 3) return set_err(PGMG_ERR_ARG, "pgmg_residual: bad argument");
+    launch_g_residual(d_r, d_x, d_f, 1.0 / (h * h), H, W, (hipStream_t)stream);
+    HIPC(hipGetLastError());
+    return PGMG_OK;
+}
+
+int pgmg_restrict(const double *d_fine, double *d_coarse, int Nf, int Nc, void *stream)
+{
+    if (!d_fine || !d_coarse || Nc < 3 || Nf != 2 * Nc - 1)
+        return set_err(PGMG_ERR_ARG, "pgmg_restrict: need Nf == 2*Nc - 1");
+    launch_g_restrict(d_fine, d_coarse, Nf, Nc, (hipStream_t)stream);
+    HIPC(hipGetLastError());
+    return PGMG_OK;
+}
+
+int pgmg_prolong(const double *d_coarse, double *d_fine, int Nc, int Nf, int mode, void *stream)
+{
+    if (!d_fine || !d_coarse || Nc < 3 || Nf != 2 * Nc - 1 || (mode != 0 && mode != 1))
+        return set_err(PGMG_ERR_ARG, "pgmg_prolong: need Nf == 2*Nc - 1, mode 0|1");
+    launch_g_prolong(d_coarse, d_fine, Nc, Nf, mode, (hipStream_t)stream);
+    HIPC(hipGetLastError());
+    return PGMG_OK;
+}
+
+int pgmg_norm(const double *d_v, long long n, double *result, void *stream)
+{
+    if (!d_v || n < 0 || !result) return set_err(PGMG_ERR_ARG, "pgmg_norm: bad argument");
+    hipStream_t s = (hipStream_t)stream;
+    int e = ensure_scratch(0);
+    if (e) return e;
+    long long nb = (n + kBlock - 1) / kBlock;
+    if (nb > 1024) nb = 1024;
+    if (nb < 1) nb = 1;
+    launch_g_sumsq(d_v, n, g_op.partials, (int)nb, s);
+    launch_sum_partials(g_op.partials, (int)nb, g_op.scalar, s);
+    double sum = 0.0;
+    HIPC(hipMemcpyAsync(&sum, g_op.scalar, sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    *result = std::sqrt(sum);
+    return PGMG_OK;
+}
+
+int pgmg_rhs(double *d_f, int W, int H, double h, double a, double p, double q, void *stream)
+{
+    if (!d_f || W < 1 || H < 1) return set_err(PGMG_ERR_ARG, "pgmg_rhs: bad argument");
+    hipStream_t s = (hipStream_t)stream;
+    const double factor = (M_PI * M_PI / (a * a)) * (p * p + q * q);  // DynamicGridUtils.hpp:113
+    std::vector<double> t(W + H);
+    for (int i = 0; i < W; ++i) t[i] = std::sin(p * M_PI * (i * h) / a);
+    for (int j = 0; j < H; ++j) t[W + j] = std::sin(q * M_PI * (j * h) / a);
+    double *d = nullptr;
+    HIPC(hipMalloc((void **)&d, t.size() * sizeof(double)));
+    HIPC(hipMemcpy(d, t.data(), t.size() * sizeof(double), hipMemcpyHostToDevice));
+    launch_g_rhs(d_f, d, d + W, factor, W, H, s);
+    HIPC(hipStreamSynchronize(s));
+    HIPC(hipFree(d));
+    return PGMG_OK;
+}
+
+int pgmg_device_alloc(void **ptr, size_t bytes)
+{
+    if (!ptr) return set_err(PGMG_ERR_ARG, "null ptr");
+    if (hipMalloc(ptr, bytes) != hipSuccess) return set_err(PGMG_ERR_NOMEM, "hipMalloc failed");
+    return PGMG_OK;
+}
+
+int pgmg_device_free(void *ptr)
+{
+    HIPC(hipFree(ptr));
+    return PGMG_OK;
+}
+
+int pgmg_memcpy_h2d(void *dst, const void *src, size_t bytes)
+{
+    HIPC(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return PGMG_OK;
+}
+
+int pgmg_memcpy_d2h(void *dst, const void *src, size_t bytes)
+{
+    HIPC(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return PGMG_OK;
+}
+
+int pgmg_device_sync(void)
+{
+    HIPC(hipDeviceSynchronize());
+    return PGMG_OK;
+}
+
+int pgmg_device_count(int *n)
+{
+    if (!n) return set_err(PGMG_ERR_ARG, "null n");
+    hipError_t e = hipGetDeviceCount(n);
+    if (e != hipSuccess) {
+        *n = 0;
+        return set_err(PGMG_ERR_HIP, hipGetErrorString(e));
+    }
+    return PGMG_OK;
+}
+
+}  // extern "C"
