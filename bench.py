@@ -70,15 +70,18 @@ def cpu_baseline(n, cycles=1):
                       f"-O2 single thread (taskset -c 0); {t:.2f} s per V-cycle; host {model}"}
 
 
-def pmc_traffic(n):
-    """HBM bytes per fine-sweep launch from the committed rocprofv3 PMC summary (if any)."""
-    p = ROOT / "profiles" / "pmc_fine_sweep.json"
+def pmc_traffic(n, kernel):
+    """HBM bytes per launch of `kernel` at grid n, from the committed rocprofv3 PMC summary
+    (profiles/pmc_fine.json, written by scripts/pmc_summary.py from FETCH_SIZE/WRITE_SIZE
+    passes with the gfx950 corrections of MI355X_MICROARCH.md)."""
+    p = ROOT / "profiles" / "pmc_fine.json"
     if not p.exists():
         return None
     try:
         d = json.loads(p.read_text())
-        if int(d.get("N", 0)) == n:
-            return d.get("hbm_bytes_per_launch")
+        for k in d.get("kernels", []):
+            if int(k.get("N", 0)) == n and k.get("kernel", "").startswith(kernel):
+                return k.get("hbm_bytes_per_launch")
     except (ValueError, OSError):
         pass
     return None
@@ -89,6 +92,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # CPU baseline first, before this process touches the GPU (it runs a child process)
+    cpu = None
+    if world == 1 and rank == 0 and args.cpu_baseline == "auto":
+        try:
+            cpu = cpu_baseline(args.cpu_n or args.n)
+        except Exception as e:  # reported, not fatal
+            cpu = {"value": None, "unit": "V-cycles/s", "cores": 1, "kind": "port",
+                   "sample": f"failed: {e}"}
     import torch  # noqa: F401  (loads the ROCm runtime first; see _capi.load)
     import _pkgload
     pg = _pkgload.load()
@@ -123,7 +134,8 @@ def main():
     # warmup (also builds the hipGraph in graph mode)
     s.vcycle(max(args.warmup, 0))
     s.sync()
-    s.fine_sweep_time()  # drop warmup events
+    for w in (0, 1, 2):  # drop warmup events
+        s.fine_pass_time(w)
     barrier()
     s.sync()
     t0 = time.perf_counter()
@@ -137,35 +149,49 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     dev_ms = s.last_elapsed_ms()
-    nfine, fine_ms = s.fine_sweep_time()
-    if nfine == 0:
-        fine_ms = s.bench_sweep(20)
-        nfine = 20
     vbytes = s.vcycle_bytes()
-    n = args.n
-    cfg = pg.default_config(n)
-    # algorithmic bytes of one fine sweep on this rank: read x, read f, write x_new
-    N = args.n
-    rows = (N - 2) if world == 1 else None
-    if rows is None:
-        import ctypes
-        p, pitch, r0, nr = (ctypes.c_void_p(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int())
-        pg.load().pgmg_phi_device(s.h, ctypes.byref(p), ctypes.byref(pitch), ctypes.byref(r0),
-                                  ctypes.byref(nr))
-        lo, hi = r0.value, r0.value + nr.value
-        rows = min(hi, N - 1) - max(lo, 1)
-    fine_bytes = 24.0 * rows * (N - 2)
-    achieved = fine_bytes / (fine_ms * 1e-3) / 1e9 if fine_ms > 0 else None
-    traffic = pmc_traffic(N) if world == 1 else None
+    n = N = args.n
+    # rows of the finest level this rank updates
+    import ctypes
+    p, pitch, r0, nr = (ctypes.c_void_p(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int())
+    pg._capi.check(pg.load().pgmg_phi_device(s.h, ctypes.byref(p), ctypes.byref(pitch),
+                                             ctypes.byref(r0), ctypes.byref(nr)), "phi_device")
+    rows = min(r0.value + nr.value, N - 1) - max(r0.value, 1)
+    nf = float(rows) * (N - 2)              # fine interior points on this rank
+    nc = nf / 4.0                           # coarse interior points it restricts / prolongs
+    passes = []
+    if s.fused:
+        # k_pre: read x0, f; write x2 (24 B/pt) + write rc; k_post: read phi, f, ec; write x2
+        for which, name, nbytes in ((1, "k_pre<false,true> (finest level: 2 Jacobi sweeps + "
+                                        "residual + restriction, fused)", 24.0 * nf + 8.0 * nc),
+                                    (2, "k_post<true> (finest level: prolongation + 2 Jacobi "
+                                        "sweeps, fused)", 24.0 * nf + 8.0 * nc)):
+            cnt, ms = s.fine_pass_time(which)
+            passes.append((name, nbytes, cnt, ms))
+    else:
+        cnt, ms = s.fine_pass_time(0)
+        passes.append(("k_sweep<false,false,true> (finest-level Jacobi sweep)", 24.0 * nf, cnt, ms))
+    if not passes or passes[0][2] == 0:   # graph mode: time the kernel separately
+        ms = s.bench_sweep(20)
+        passes = [("k_sweep<false,false,true> (finest-level Jacobi sweep, timed apart)",
+                   24.0 * nf, 20, ms)]
+    roof = []
+    for name, nbytes, cnt, ms in passes:
+        ach = nbytes / (ms * 1e-3) / 1e9 if ms > 0 else None
+        roof.append({"bound": "hbm", "kernel": name,
+                     "achieved": round(ach, 2) if ach else None, "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4) if ach else None,
+                     "traffic": pmc_traffic(N, name.split(" ")[0]) if world == 1 else None,
+                     "bytes_per_launch": nbytes, "launches_timed": cnt,
+                     "ms_per_launch": round(ms, 5)})
+    # the dominant kernel: largest total time
+    roof.sort(key=lambda r: -(r["ms_per_launch"] or 0))
+    sweep_eq = None
+    if s.fused and roof[0]["achieved"]:
+        # the same pass counted as the 2 separate 24 B/pt sweeps it replaces
+        sweep_eq = round(2 * 24.0 * nf / (roof[0]["ms_per_launch"] * 1e-3) / 1e9, 2)
 
     if rank == 0:
-        cpu = None
-        if world == 1 and args.cpu_baseline == "auto":
-            try:
-                cpu = cpu_baseline(args.cpu_n or n)
-            except Exception as e:  # reported, not fatal
-                cpu = {"value": None, "unit": "V-cycles/s", "cores": 1, "kind": "port",
-                       "sample": f"failed: {e}"}
         value = args.steps / dt
         line = {
             "metric": METRIC,
@@ -188,18 +214,9 @@ def main():
                 "parallelism": "single-gpu" if world == 1 else f"row-strips x{world} (RCCL halos)",
                 "timing": args.timing,
             },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "k_sweep<false,false,true> (finest-level Jacobi sweep)",
-                "achieved": round(achieved, 2) if achieved else None,
-                "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4) if achieved else None,
-                "traffic": traffic,
-                "bytes_per_launch": fine_bytes,
-                "launches_timed": nfine,
-                "ms_per_launch": round(fine_ms, 5),
-            },
+            "roofline": roof[0],
+            "roofline_other": roof[1:],
+            "fine_sweep_equivalent_gbps": sweep_eq,
             "vcycle_algorithmic_gbps": round(vbytes / (dt / args.steps) / 1e9, 2),
             "vcycle_device_ms": round(dev_ms / args.steps, 4),
             "cpu_baseline": cpu,

@@ -64,7 +64,9 @@ extern "C" {
 /* config flags */
 #define PGMG_FLAG_NO_GRAPH 1u    /* launch eagerly instead of replaying a hipGraph */
 #define PGMG_FLAG_TIME_FINE 2u   /* eager launches + hipEvents around every finest-level
-                                    plain Jacobi sweep (see pgmg_fine_sweep_time)   */
+                                    pass (see pgmg_fine_pass_time)                  */
+#define PGMG_FLAG_UNFUSED 4u     /* one kernel per smoother sweep even when v1 = v2 = 1
+                                    (the general path; same results)                */
 
 typedef struct pgmg_config {
     int N;             /* points per side incl. boundary; 2^k + 1, k >= 2        */
@@ -128,9 +130,15 @@ int pgmg_vcycle_bytes(pgmg_ctx *ctx, double *bytes);
  * rank, for callers that want to read it in place. */
 int pgmg_phi_device(pgmg_ctx *ctx, double **ptr, int *pitch, int *row0, int *rows);
 
-/* Count and mean device duration (ms) of the finest-level plain Jacobi sweeps
- * launched since the last call (needs PGMG_FLAG_TIME_FINE).  Synchronous. */
-int pgmg_fine_sweep_time(pgmg_ctx *ctx, int *count, double *mean_ms);
+/* Count and mean device duration (ms) of the finest-level kernels launched since
+ * the last call (needs PGMG_FLAG_TIME_FINE; synchronous).  pass 0: plain Jacobi
+ * sweep (unfused path), 1: fused pre-smooth+residual+restriction (k_pre),
+ * 2: fused prolongation+post-smooth (k_post). */
+int pgmg_fine_pass_time(pgmg_ctx *ctx, int pass, int *count, double *mean_ms);
+int pgmg_fine_sweep_time(pgmg_ctx *ctx, int *count, double *mean_ms);  /* pass 0 */
+
+/* 1 when the context runs the fused two-pass-per-level cycle (v1 = v2 = 1). */
+int pgmg_fused(pgmg_ctx *ctx, int *fused);
 
 /* Time `reps` back-to-back fine-grid Jacobi sweeps (the roofline kernel) on the
  * context's level-0 buffers with hipEvents; returns the mean per sweep in ms.

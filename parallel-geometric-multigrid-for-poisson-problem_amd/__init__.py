@@ -16,14 +16,14 @@ import subprocess
 
 import numpy as np
 
-from ._capi import (PGMG_FLAG_NO_GRAPH, PGMG_FLAG_TIME_FINE, PGMG_PROLONG_REFERENCE,
+from ._capi import (PGMG_FLAG_NO_GRAPH, PGMG_FLAG_TIME_FINE, PGMG_FLAG_UNFUSED, PGMG_PROLONG_REFERENCE,
                     PGMG_PROLONG_SYMMETRIC, PgmgConfig, PgmgError, check, load)
 
 PKG_DIR = pathlib.Path(__file__).resolve().parent
 
 __all__ = [
     "build", "load", "Solver", "PgmgConfig", "PgmgError", "ops",
-    "PGMG_FLAG_NO_GRAPH", "PGMG_FLAG_TIME_FINE", "PGMG_PROLONG_REFERENCE",
+    "PGMG_FLAG_NO_GRAPH", "PGMG_FLAG_TIME_FINE", "PGMG_FLAG_UNFUSED", "PGMG_PROLONG_REFERENCE",
     "PGMG_PROLONG_SYMMETRIC",
 ]
 
@@ -144,6 +144,19 @@ class Solver:
         check(self.lib.pgmg_fine_sweep_time(self.h, C.byref(n), C.byref(m)),
               "pgmg_fine_sweep_time")
         return n.value, m.value
+
+    def fine_pass_time(self, which):
+        """(count, mean ms) of finest-level kernels: 0 plain sweep, 1 k_pre, 2 k_post."""
+        n, m = C.c_int(), C.c_double()
+        check(self.lib.pgmg_fine_pass_time(self.h, int(which), C.byref(n), C.byref(m)),
+              "pgmg_fine_pass_time")
+        return n.value, m.value
+
+    @property
+    def fused(self):
+        v = C.c_int()
+        check(self.lib.pgmg_fused(self.h, C.byref(v)), "pgmg_fused")
+        return bool(v.value)
 
     def bench_sweep(self, reps):
         m = C.c_double()

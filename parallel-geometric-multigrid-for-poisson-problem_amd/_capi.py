@@ -23,6 +23,7 @@ PGMG_PROLONG_SYMMETRIC = 1
 
 PGMG_FLAG_NO_GRAPH = 1
 PGMG_FLAG_TIME_FINE = 2
+PGMG_FLAG_UNFUSED = 4
 
 
 class PgmgConfig(C.Structure):
@@ -68,6 +69,8 @@ SIGNATURES = [
     ("pgmg_phi_device", C.c_int, [_P, C.POINTER(_P), C.POINTER(C.c_int), C.POINTER(C.c_int),
                                   C.POINTER(C.c_int)]),
     ("pgmg_fine_sweep_time", C.c_int, [_P, C.POINTER(C.c_int), _DP]),
+    ("pgmg_fine_pass_time", C.c_int, [_P, C.c_int, C.POINTER(C.c_int), _DP]),
+    ("pgmg_fused", C.c_int, [_P, C.POINTER(C.c_int)]),
     ("pgmg_bench_sweep", C.c_int, [_P, C.c_int, _DP]),
     ("pgmg_jacobi", C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_double, C.c_int, C.c_double,
                               C.POINTER(C.c_int), _P]),

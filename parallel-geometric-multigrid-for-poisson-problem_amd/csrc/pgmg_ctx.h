@@ -54,8 +54,13 @@ struct pgmg_ctx {
     hipGraphExec_t gexec = nullptr;
     bool have_problem = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    std::vector<hipEvent_t> tev;  // fine-sweep timing event pool (PGMG_FLAG_TIME_FINE)
-    int tev_used = 0;
+    struct EventPool {
+        std::vector<hipEvent_t> ev;
+        int used = 0;
+    };
+    // finest-level kernel timing (PGMG_FLAG_TIME_FINE): 0 plain sweep, 1 k_pre, 2 k_post
+    EventPool tpool[3];
+    bool fused = false;           // v1 = v2 = 1: two fused passes per level
     pgmg::Comm *comm = nullptr;   // non-null when world > 1
 };
 

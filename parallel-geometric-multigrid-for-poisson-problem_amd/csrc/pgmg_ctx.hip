@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "pgmg_ctx.h"
+#include "pgmg_fused.h"
 
 using namespace pgmg;
 
@@ -43,14 +44,16 @@ int pgmg::set_err(int code, const std::string &msg)
 // ---------------------------------------------------------------------------
 int pgmg::alloc_grid(Grid &g, const Level &L)
 {
-    const int rows = (L.hi - L.lo) + 4;  // owned + 2 halo rows each side
-    const size_t n = (size_t)kOff + (size_t)rows * L.P + 64;
+    // owned rows + kHalo halo rows each side (the fused passes read 4 rows past a
+    // segment); the slack covers the last wave tile reading past the row end
+    const int rows = (L.hi - L.lo) + 2 * kHalo;
+    const size_t n = (size_t)kOff + (size_t)rows * L.P + 512;
     void *p = nullptr;
     if (hipMalloc(&p, n * sizeof(double)) != hipSuccess)
         return set_err(PGMG_ERR_NOMEM, "hipMalloc failed for a level of N=" + std::to_string(L.N));
     HIPC(hipMemset(p, 0, n * sizeof(double)));
     g.base = (double *)p;
-    g.o = g.base + kOff + (ptrdiff_t)(2 - L.lo) * L.P;
+    g.o = g.base + kOff + (ptrdiff_t)(kHalo - L.lo) * L.P;
     return PGMG_OK;
 }
 
@@ -69,6 +72,9 @@ static unsigned *smooth_flags(pgmg_ctx *c, int l, int which)
 }
 
 static double *const kZeroMarker = nullptr;
+
+static int timed_begin(pgmg_ctx *c, int slot);
+static int timed_end(pgmg_ctx *c, int slot, int idx);
 
 // one JacobiSmoother::smooth(x = L.A, f = L.F, num_iter = v) on a bulk level
 static int enqueue_smooth(pgmg_ctx *c, int l, int which, int v, bool x0_zero)
@@ -98,14 +104,10 @@ static int enqueue_smooth(pgmg_ctx *c, int l, int which, int v, bool x0_zero)
         a.P = L.P;
         a.row0 = L.u0;
         a.row1 = L.u1;
-        const bool timed = fine && (c->cfg.flags & PGMG_FLAG_TIME_FINE) && a.partials == nullptr &&
-                           !(k == 1 && x0_zero) && c->tev_used + 2 <= (int)c->tev.size();
-        if (timed) HIPC(hipEventRecord(c->tev[c->tev_used], c->s));
+        const int ev = (fine && a.partials == nullptr && !(k == 1 && x0_zero)) ? timed_begin(c, 0) : -1;
         launch_sweep(a, k == 1 && x0_zero, l == 0, c->s);
-        if (timed) {
-            HIPC(hipEventRecord(c->tev[c->tev_used + 1], c->s));
-            c->tev_used += 2;
-        }
+        int te = timed_end(c, 0, ev);
+        if (te) return te;
         if (k >= 2) {
             int rpb, gx, gy;
             const int np = sweep_blocks(L.N, L.u0, L.u1, &rpb, &gx, &gy);
@@ -154,6 +156,87 @@ int pgmg::enqueue_tail(pgmg_ctx *c, int gamma, bool x0_from_global)
     return PGMG_OK;
 }
 
+static int timed_begin(pgmg_ctx *c, int slot)
+{
+    auto &pool = c->tpool[slot];
+    if (!(c->cfg.flags & PGMG_FLAG_TIME_FINE) || pool.used + 2 > (int)pool.ev.size()) return -1;
+    HIPC(hipEventRecord(pool.ev[pool.used], c->s));
+    return pool.used;
+}
+
+static int timed_end(pgmg_ctx *c, int slot, int idx)
+{
+    if (idx < 0) return PGMG_OK;
+    auto &pool = c->tpool[slot];
+    HIPC(hipEventRecord(pool.ev[idx + 1], c->s));
+    pool.used = idx + 2;
+    return PGMG_OK;
+}
+
+// fused level (v1 = v2 = 1): k_pre (+fixup), children, k_post (+fixup)
+static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
+{
+    Level &L = c->lv[l];
+    Level &C = c->lv[l + 1];
+    PreArgs pa{};
+    pa.x0 = L.A.o;
+    pa.f = L.F.o;
+    pa.x2 = L.B.o;
+    pa.rc = C.F.o;
+    pa.partials = c->partials;
+    pa.stats = c->stats;
+    pa.hh = L.hh;
+    pa.ih = L.ih;
+    pa.N = L.N;
+    pa.P = L.P;
+    pa.Nc = C.N;
+    pa.Pc = C.P;
+    pa.jc0 = L.lo / 2;
+    pa.jc1 = (L.hi < L.N ? L.hi : L.N - 1) / 2;
+    pa.row_lo = L.u0;
+    pa.row_hi = L.u1;
+    pa.rc_lo = C.u0;
+    pa.rc_hi = C.u1;
+    FixArgsF fa{};
+    fa.partials = c->partials;
+    fa.np = fused_blocks(L.N, pa.jc0, pa.jc1);
+    fa.eps = c->cfg.eps;
+    fa.stats = c->stats;
+    const bool fine = (l == 0);
+    int ev = fine ? timed_begin(c, 1) : -1;
+    launch_pre(pa, x0_zero, fine, c->s);
+    int e = timed_end(c, 1, ev);
+    if (e) return e;
+    launch_pre_fixup(fa, pa, x0_zero, c->s);
+    for (int i = 0; i < gamma; ++i) {
+        e = enqueue_cycle(c, l + 1, gamma, i == 0);
+        if (e) return e;
+    }
+    PostArgs po{};
+    po.phi = L.B.o;
+    po.ec = C.A.o;
+    po.f = L.F.o;
+    po.x2 = L.A.o;
+    po.partials = c->partials;
+    po.stats = c->stats;
+    po.hh = L.hh;
+    po.ih = L.ih;
+    po.N = L.N;
+    po.P = L.P;
+    po.Nc = C.N;
+    po.Pc = C.P;
+    po.jc0 = pa.jc0;
+    po.jc1 = pa.jc1;
+    po.row_lo = L.u0;
+    po.row_hi = L.u1;
+    ev = fine ? timed_begin(c, 2) : -1;
+    launch_post(po, fine, c->s);
+    e = timed_end(c, 2, ev);
+    if (e) return e;
+    launch_post_fixup(fa, po, c->s);
+    return PGMG_OK;
+}
+
 // MultigridSolver::v_cycle / w_cycle (MultiGrid.hpp:57-136) on level l
 int pgmg::enqueue_cycle(pgmg_ctx *c, int l, int gamma, bool x0_zero)
 {
@@ -161,6 +244,7 @@ int pgmg::enqueue_cycle(pgmg_ctx *c, int l, int gamma, bool x0_zero)
         if (c->comm) return c->comm->run_gathered(c, l, gamma, x0_zero);
         return enqueue_tail(c, gamma, !x0_zero);
     }
+    if (c->fused) return enqueue_fused_level(c, l, gamma, x0_zero);
     Level &L = c->lv[l];
     Level &C = c->lv[l + 1];
     int e = enqueue_smooth(c, l, 0, c->cfg.v1, x0_zero);
@@ -257,7 +341,8 @@ int pgmg_destroy(pgmg_ctx *c)
     if (c->flags) (void)hipFree(c->flags);
     if (c->stats) (void)hipFree(c->stats);
     if (c->scalar) (void)hipFree(c->scalar);
-    for (auto e : c->tev) (void)hipEventDestroy(e);
+    for (auto &pool : c->tpool)
+        for (auto e : pool.ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     delete c->comm;
@@ -327,10 +412,14 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         if (rc == PGMG_OK) rc = alloc_grid(L.F, L);
         if (rc == PGMG_OK && l < c->nb) rc = alloc_grid(L.B, L);
     }
+    c->fused = cfg->v1 == 1 && cfg->v2 == 1 && !(cfg->flags & PGMG_FLAG_UNFUSED);
     int maxblocks = 256;
     for (int l = 0; l < c->nb; ++l) {
         int rpb, gx, gy;
-        const int nbk = sweep_blocks(c->lv[l].N, c->lv[l].u0, c->lv[l].u1, &rpb, &gx, &gy);
+        const Level &L = c->lv[l];
+        int nbk = sweep_blocks(L.N, L.u0, L.u1, &rpb, &gx, &gy);
+        if (nbk > maxblocks) maxblocks = nbk;
+        nbk = fused_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2);
         if (nbk > maxblocks) maxblocks = nbk;
     }
     c->partials_cap = maxblocks;
@@ -351,9 +440,11 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
             rc = set_err(PGMG_ERR_HIP, "stream/event setup failed");
     }
     if (rc == PGMG_OK && (cfg->flags & PGMG_FLAG_TIME_FINE)) {
-        c->tev.resize(1024);
-        for (auto &e : c->tev)
-            if (hipEventCreate(&e) != hipSuccess) rc = set_err(PGMG_ERR_HIP, "event pool");
+        for (auto &pool : c->tpool) {
+            pool.ev.resize(512);
+            for (auto &e : pool.ev)
+                if (hipEventCreate(&e) != hipSuccess) rc = set_err(PGMG_ERR_HIP, "event pool");
+        }
     }
     if (rc == PGMG_OK && c->comm) rc = c->comm->setup(c);
     if (rc != PGMG_OK) {
@@ -545,6 +636,11 @@ int pgmg_vcycle_bytes(pgmg_ctx *c, double *bytes)
         const Level &C = c->lv[l + 1];
         const double n = (double)(L.u1 - L.u0) * (L.N - 2);
         const double nc = (double)(C.u1 - C.u0) * (C.N - 2);
+        if (c->fused) {
+            b += (l == 0 ? 24.0 : 16.0) * n + 8.0 * nc;  // k_pre: x0, f in; x2, rc out
+            b += 24.0 * n + 8.0 * nc;                     // k_post: phi, f, ec in; x2 out
+            continue;
+        }
         const int S1 = c->cfg.v1 + 1, S2 = c->cfg.v2 + 1;
         b += (l == 0 ? 24.0 : 16.0) * n + 24.0 * n * (S1 - 1);  // pre-smooth
         b += 16.0 * n + 8.0 * nc;                                // residual + restriction
@@ -602,20 +698,33 @@ int pgmg_bench_sweep(pgmg_ctx *c, int reps, double *ms)
     return PGMG_OK;
 }
 
-int pgmg_fine_sweep_time(pgmg_ctx *c, int *count, double *mean_ms)
+int pgmg_fine_pass_time(pgmg_ctx *c, int pass, int *count, double *mean_ms)
 {
-    if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
+    if (!c || pass < 0 || pass > 2) return set_err(PGMG_ERR_ARG, "bad argument");
     HIPC(hipStreamSynchronize(c->s));
+    auto &pool = c->tpool[pass];
     double tot = 0.0;
-    const int n = c->tev_used / 2;
+    const int n = pool.used / 2;
     for (int i = 0; i < n; ++i) {
         float f = 0.f;
-        HIPC(hipEventElapsedTime(&f, c->tev[2 * i], c->tev[2 * i + 1]));
+        HIPC(hipEventElapsedTime(&f, pool.ev[2 * i], pool.ev[2 * i + 1]));
         tot += f;
     }
     if (count) *count = n;
     if (mean_ms) *mean_ms = n ? tot / n : 0.0;
-    c->tev_used = 0;
+    pool.used = 0;
+    return PGMG_OK;
+}
+
+int pgmg_fine_sweep_time(pgmg_ctx *c, int *count, double *mean_ms)
+{
+    return pgmg_fine_pass_time(c, 0, count, mean_ms);
+}
+
+int pgmg_fused(pgmg_ctx *c, int *fused)
+{
+    if (!c || !fused) return set_err(PGMG_ERR_ARG, "bad argument");
+    *fused = c->fused ? 1 : 0;
     return PGMG_OK;
 }
 

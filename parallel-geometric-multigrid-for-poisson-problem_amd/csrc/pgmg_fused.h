@@ -1,0 +1,52 @@
+// pgmg_fused.h — argument blocks of the fused smoother passes (pgmg_fused.hip).
+#pragma once
+#include "pgmg_internal.h"
+
+namespace pgmg {
+
+// pre-smooth (2 sweeps) + residual + full-weighting restriction in one pass
+struct PreArgs {
+    const double *x0;           // level solution before smoothing (unused when x0 is zero)
+    const double *f;            // level right-hand side
+    double *x2;                 // result of the two sweeps (ping-pong buffer)
+    double *rc;                 // coarse right-hand side R r(x2)
+    double *partials;           // per block sum r(x1)^2 (early-exit check)
+    unsigned long long *stats;  // [0] sweeps (+2 per launch)
+    double hh, ih;
+    int N, P, Nc, Pc;
+    int jc0, jc1;               // coarse-row segments [jc0, jc1) (fine rows 2jc, 2jc+1)
+    int row_lo, row_hi;         // fine rows whose x2 this rank writes
+    int rc_lo, rc_hi;           // coarse rows whose rc this rank writes
+    int rows_per_block;
+};
+
+// prolongation + post-smooth (2 sweeps) in one pass
+struct PostArgs {
+    const double *phi;          // level solution after pre-smoothing
+    const double *ec;           // coarse-grid correction
+    const double *f;
+    double *x2;                 // result (the level's solution buffer)
+    double *partials;
+    unsigned long long *stats;
+    double hh, ih;
+    int N, P, Nc, Pc;
+    int jc0, jc1;
+    int row_lo, row_hi;
+    int rows_per_block;
+};
+
+struct FixArgsF {
+    const double *partials;
+    int np;
+    double eps;
+    const double *global_sum;   // all-rank sum (multi-GPU) or nullptr: sum the partials
+    unsigned long long *stats;
+};
+
+int fused_blocks(int N, int jc0, int jc1);
+void launch_pre(const PreArgs &a, bool x0_zero, bool fine, hipStream_t s);
+void launch_post(const PostArgs &a, bool fine, hipStream_t s);
+void launch_pre_fixup(const FixArgsF &a, const PreArgs &p, bool x0_zero, hipStream_t s);
+void launch_post_fixup(const FixArgsF &a, const PostArgs &p, hipStream_t s);
+
+}  // namespace pgmg

@@ -1,0 +1,472 @@
+// pgmg_fused.hip — temporally fused smoother passes for the default cycle (v1 = v2 = 1).
+//
+// With v = 1 the reference smoother runs two sweeps and checks ||r(x1)|| < eps after
+// the first (the check after the last sweep cannot change the result).  Instead of
+// six HBM passes per level (2 sweeps, residual+restriction, prolongation, 2 sweeps)
+// a level now costs two:
+//
+//   k_pre : x0, f  -> x1 = J(x0) -> x2 = J(x1) -> r = f - A x2 -> rc = R r
+//           writes x2 (into the ping-pong buffer) and rc; sum r(x1)^2 per block
+//           (MultiGrid.hpp:66-78 + Smoother.hpp:59-88)
+//   k_post: phi, ec, f -> x_eff = phi + P ec -> x1 = J(x_eff) -> x2 = J(x1)
+//           writes x2 (back into the level's solution buffer); sum r(x1)^2
+//           (MultiGrid.hpp:86-89 + Smoother.hpp:59-88)
+//
+// 26 B/point instead of 64 (pre) and 24+2 instead of 64 (post).  Both are
+// speculative in the early exit: when ||r(x1)|| < eps fires (rare; never on fine
+// levels in practice) the fix-up kernels recompute the exact reference result
+// (x1 instead of x2, and rc from r(x1)) from the still-intact inputs.
+//
+// Tiling: a wave owns 120 columns but loads 128 (4-column overlap each side), so
+// every stencil level's horizontal neighbours come from the adjacent lane by DPP
+// and the validity shrinks one column per level: x0 [c0, c0+127] -> x1 [+1,-1] ->
+// x2 [+2,-2] -> r [+3,-3] -> rc centres [+4,-4] = the owned columns.  Rows march
+// down a segment with every stage lagging one row behind the previous one; the
+// pipeline needs 4 rows of x0 above and below the segment (the halo rows are
+// re-read by the neighbouring segment, mostly from L2 / Infinity Cache).
+//
+// Every expression keeps the reference's left-to-right order; built with
+// -ffp-contract=off, so the results are bit-identical to the unfused path.
+#include "pgmg_fused.h"
+
+namespace pgmg {
+
+__device__ __forceinline__ double dpp_prev_f(double v)  // lane i <- lane i-1
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x138, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double dpp_next_f(double v)  // lane i <- lane i+1
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x130, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x130, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__device__ __forceinline__ double2 ldg2(const double *p) { return *reinterpret_cast<const double2 *>(p); }
+__device__ __forceinline__ void stg2(double *p, double2 v) { *reinterpret_cast<double2 *>(p) = v; }
+
+struct Cols {
+    int c;          // odd column of this lane's pair (c, c+1)
+    bool bx, by;    // column c / c+1 is a boundary (or outside) column: passthrough
+    bool own;       // lane owns its pair (lanes 2..61 of the wave tile)
+};
+
+// One Jacobi stage on a row: J(ce) with boundary passthrough.
+__device__ __forceinline__ double2 jstage(double2 up, double2 ce, double2 dn, double2 f, double hh,
+                                          const Cols &k, bool brow)
+{
+    const double l = dpp_prev_f(ce.y);
+    const double r = dpp_next_f(ce.x);
+    double2 o;
+    o.x = 0.25 * ((hh * f.x) + l + ce.y + up.x + dn.x);
+    o.y = 0.25 * ((hh * f.y) + ce.x + r + up.y + dn.y);
+    if (brow || k.bx) o.x = ce.x;
+    if (brow || k.by) o.y = ce.y;
+    return o;
+}
+
+// Residual r = f - (1/h^2)(4x - xl - xr - xu - xd) on a row (DynamicGridUtils.hpp:59-69)
+__device__ __forceinline__ double2 rstage(double2 up, double2 ce, double2 dn, double2 f, double ih)
+{
+    const double l = dpp_prev_f(ce.y);
+    const double r = dpp_next_f(ce.x);
+    double2 o;
+    o.x = f.x - ih * (4 * ce.x - l - ce.y - up.x - dn.x);
+    o.y = f.y - ih * (4 * ce.y - ce.x - r - up.y - dn.y);
+    return o;
+}
+
+__device__ __forceinline__ bool boundary_row(int row, int N) { return row <= 0 || row >= N - 1; }
+
+__device__ __forceinline__ Cols lane_cols(int N)
+{
+    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    Cols k;
+    k.c = 120 * wave - 3 + 2 * lane;
+    k.bx = k.c <= 0 || k.c >= N - 1;
+    k.by = k.c + 1 <= 0 || k.c + 1 >= N - 1;
+    k.own = lane >= 2 && lane <= 61 && k.c <= N - 2;
+    return k;
+}
+
+// deterministic sum over the block (fixed tree) -> thread 0
+__device__ __forceinline__ double fused_block_sum(double v, double *red)
+{
+    #pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double s = 0.0;
+    if (threadIdx.x == 0)
+        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += red[i];
+    return s;
+}
+
+// ---------------------------------------------------------------------------
+// k_pre
+// ---------------------------------------------------------------------------
+template <bool X0_ZERO, bool FINE>
+__global__ __launch_bounds__(256) void k_pre(PreArgs a)
+{
+    __shared__ double red[4];
+    const Cols k = lane_cols(a.N);
+    const int N = a.N;
+    const long long P = a.P;
+    const int jcb = a.jc0 + blockIdx.y * a.rows_per_block;
+    const int jce = min(jcb + a.rows_per_block, a.jc1);
+    const int olo = max(2 * jcb, a.row_lo), ohi = min(2 * jce, a.row_hi);  // x2 rows written
+    const int clo = max(jcb, max(1, a.rc_lo)), chi = min(jce, min(N / 2, a.rc_hi));  // rc rows
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
+        atomicAdd(&a.stats[0], 2ull);
+    const double *__restrict__ X = a.x0 + k.c;
+    const double *__restrict__ F = a.f + k.c;
+    double *__restrict__ O = a.x2 + k.c;
+    const double hh = a.hh, ih = a.ih;
+    const double2 z = make_double2(0.0, 0.0);
+    // windows: x0 rows i-2,i-1 ; x1 rows i-3,i-2 ; x2 rows i-4,i-3 ; r rows i-5,i-4 ;
+    //          f rows i-3,i-2,i-1
+    double2 a0 = z, a1 = z, b0 = z, b1 = z, c0 = z, c1 = z, d0 = z, d1 = z, f0 = z, f1 = z, f2 = z;
+    double acc = 0.0;
+    const int i_begin = 2 * jcb - 4, i_end = 2 * jce + 4;  // steps [i_begin, i_end)
+    double2 nx0 = z, nx1 = z, nf0, nf1;
+    if (!X0_ZERO) {
+        nx0 = ldg2(X + i_begin * P);
+        nx1 = ldg2(X + (i_begin + 1) * P);
+    }
+    nf0 = ldg2(F + i_begin * P);
+    nf1 = ldg2(F + (i_begin + 1) * P);
+    for (int i = i_begin; i < i_end; i += 2) {
+        double2 xe = nx0, xo = nx1, fe = nf0, fo = nf1;
+        if (i + 2 < i_end) {  // prefetch the next pair of rows
+            if (!X0_ZERO) {
+                nx0 = ldg2(X + (i + 2) * P);
+                nx1 = ldg2(X + (i + 3) * P);
+            }
+            nf0 = ldg2(F + (i + 2) * P);
+            nf1 = ldg2(F + (i + 3) * P);
+        }
+        #pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int ii = i + s;
+            const double2 a2 = s ? xo : xe;
+            const double2 f3 = s ? fo : fe;
+            // x1 row ii-1
+            const double2 b2 = jstage(a0, a1, a2, f2, hh, k, boundary_row(ii - 1, N));
+            // r(x1) and x2 on row ii-2
+            {
+                const int row = ii - 2;
+                const double2 r1 = rstage(b0, b1, b2, f1, ih);
+                if (row >= olo && row < ohi && k.own) {
+                    acc += r1.x * r1.x;
+                    if (!k.by) acc += r1.y * r1.y;
+                }
+            }
+            const double2 c2 = jstage(b0, b1, b2, f1, hh, k, boundary_row(ii - 2, N));
+            if (ii - 2 >= olo && ii - 2 < ohi && k.own) stg2(O + (ii - 2) * P, c2);
+            // r(x2) on row ii-3 (0 on boundary rows; never used there)
+            const double2 d2 = rstage(c0, c1, c2, f0, ih);
+            // restriction: rows ii-5, ii-4, ii-3 = 2jc-1, 2jc, 2jc+1 when ii is even
+            if (s == 0) {
+                const int jc = (ii - 4) >> 1;
+                const double m2 = dpp_next_f(d1.x);
+                const double u2 = dpp_next_f(d0.x);
+                const double e2 = dpp_next_f(d2.x);
+                const int ic = (k.c + 1) >> 1;
+                if (jc >= clo && jc < chi && k.own && ic <= a.Nc - 2) {
+                    const double v = 0.25 * d1.y + 0.125 * (m2 + d1.x + d2.y + d0.y) +
+                                     0.0625 * (d0.x + u2 + d2.x + e2);
+                    a.rc[(long long)jc * a.Pc + ic] = v;
+                }
+            }
+            a0 = a1;
+            a1 = a2;
+            b0 = b1;
+            b1 = b2;
+            c0 = c1;
+            c1 = c2;
+            d0 = d1;
+            d1 = d2;
+            f0 = f1;
+            f1 = f2;
+            f2 = f3;
+        }
+    }
+    const double s = fused_block_sum(acc, red);
+    if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = s;
+}
+
+// ---------------------------------------------------------------------------
+// k_post
+// ---------------------------------------------------------------------------
+struct ProlongCols {
+    bool vx, vy;   // column c / c+1 receives a correction
+    int ic;        // coarse column of the odd fine column c: (c-1)/2
+};
+
+__device__ __forceinline__ double2 add_prolong(double2 p, int row, double ca, double cb, double da,
+                                               double db, const ProlongCols &pc, int Nc)
+{
+    // MultiGrid.hpp:219-223; row in [2, Nf-2] <=> its coarse row m in [1, Nc-2]
+    const int m = row >> 1;
+    if (m < 1 || m > Nc - 2) return p;
+    if ((row & 1) == 0) {
+        if (pc.vx) p.x = p.x + 0.5 * (ca + cb);
+        if (pc.vy) p.y = p.y + cb;
+    } else {
+        if (pc.vx) p.x = p.x + 0.25 * (ca + cb + da + db);
+        if (pc.vy) p.y = p.y + 0.5 * (cb + db);
+    }
+    return p;
+}
+
+template <bool FINE>
+__global__ __launch_bounds__(256) void k_post(PostArgs a)
+{
+    __shared__ double red[4];
+    const Cols k = lane_cols(a.N);
+    const int N = a.N, Nc = a.Nc;
+    const long long P = a.P, Pc = a.Pc;
+    const int jcb = a.jc0 + blockIdx.y * a.rows_per_block;
+    const int jce = min(jcb + a.rows_per_block, a.jc1);
+    const int olo = max(2 * jcb, a.row_lo), ohi = min(2 * jce, a.row_hi);
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
+        atomicAdd(&a.stats[0], 2ull);
+    ProlongCols pc;
+    pc.ic = (k.c - 1) >> 1;
+    pc.vx = k.c >= 3 && k.c <= N - 2;
+    pc.vy = k.c + 1 >= 2 && k.c + 1 <= N - 3;
+    const double *__restrict__ X = a.phi + k.c;
+    const double *__restrict__ F = a.f + k.c;
+    const double *__restrict__ E = a.ec + pc.ic;
+    double *__restrict__ O = a.x2 + k.c;
+    const double hh = a.hh, ih = a.ih;
+    const double2 z = make_double2(0.0, 0.0);
+    // windows: x_eff rows i-2,i-1 ; x1 rows i-3,i-2 ; f rows i-2,i-1
+    double2 a0 = z, a1 = z, b0 = z, b1 = z, f1 = z, f2 = z;
+    double acc = 0.0;
+    const int i_begin = 2 * jcb - 2, i_end = 2 * jce + 2;
+    double2 np0 = ldg2(X + i_begin * P), np1 = ldg2(X + (i_begin + 1) * P);
+    double2 nf0 = ldg2(F + i_begin * P), nf1 = ldg2(F + (i_begin + 1) * P);
+    double cm = E[(long long)(i_begin >> 1) * Pc];              // coarse row m = i/2
+    double nc1 = E[(long long)((i_begin >> 1) + 1) * Pc];       // coarse row m+1
+    for (int i = i_begin; i < i_end; i += 2) {
+        const double2 pe = np0, po = np1, fe = nf0, fo = nf1;
+        const double cmA = cm, cmB_row = nc1;
+        if (i + 2 < i_end) {
+            np0 = ldg2(X + (i + 2) * P);
+            np1 = ldg2(X + (i + 3) * P);
+            nf0 = ldg2(F + (i + 2) * P);
+            nf1 = ldg2(F + (i + 3) * P);
+            cm = nc1;
+            nc1 = E[(long long)((i >> 1) + 2) * Pc];
+        }
+        const double ca = cmA, cb = dpp_next_f(cmA);
+        const double da = cmB_row, db = dpp_next_f(cmB_row);
+        #pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int ii = i + s;
+            const double2 a2 = add_prolong(s ? po : pe, ii, ca, cb, da, db, pc, Nc);
+            const double2 f3 = s ? fo : fe;
+            const double2 b2 = jstage(a0, a1, a2, f2, hh, k, boundary_row(ii - 1, N));
+            {
+                const int row = ii - 2;
+                const double2 r1 = rstage(b0, b1, b2, f1, ih);
+                if (row >= olo && row < ohi && k.own) {
+                    acc += r1.x * r1.x;
+                    if (!k.by) acc += r1.y * r1.y;
+                }
+            }
+            const double2 c2 = jstage(b0, b1, b2, f1, hh, k, boundary_row(ii - 2, N));
+            if (ii - 2 >= olo && ii - 2 < ohi && k.own) stg2(O + (ii - 2) * P, c2);
+            a0 = a1;
+            a1 = a2;
+            b0 = b1;
+            b1 = b2;
+            f1 = f2;
+            f2 = f3;
+        }
+    }
+    const double s = fused_block_sum(acc, red);
+    if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = s;
+}
+
+// ---------------------------------------------------------------------------
+// launch geometry
+// ---------------------------------------------------------------------------
+static void fused_geometry(int N, int jc0, int jc1, int *threads, int *gx, int *gy, int *rpb)
+{
+    const int waves = (N - 2 + 119) / 120;
+    const int wpb = waves < 4 ? waves : 4;
+    *threads = 64 * wpb;
+    *gx = (waves + wpb - 1) / wpb;
+    const int rows = jc1 - jc0;   // coarse rows
+    int r = (int)(((long long)rows * *gx + 2047) / 2048);  // >= ~2048 blocks when possible
+    r = r < 8 ? 8 : (r > 64 ? 64 : r);
+    if (r > rows) r = rows;
+    *rpb = r;
+    *gy = (rows + r - 1) / r;
+}
+
+int fused_blocks(int N, int jc0, int jc1)
+{
+    int t, gx, gy, r;
+    fused_geometry(N, jc0, jc1, &t, &gx, &gy, &r);
+    return gx * gy;
+}
+
+// The finest level gets its own kernel symbols (FINE) so rocprofv3 statistics
+// isolate the roofline kernels.
+void launch_pre(const PreArgs &a0, bool x0_zero, bool fine, hipStream_t s)
+{
+    int t, gx, gy, r;
+    fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r);
+    PreArgs a = a0;
+    a.rows_per_block = r;
+    const dim3 g(gx, gy), b(t);
+    if (x0_zero) k_pre<true, false><<<g, b, 0, s>>>(a);
+    else if (fine) k_pre<false, true><<<g, b, 0, s>>>(a);
+    else k_pre<false, false><<<g, b, 0, s>>>(a);
+}
+
+void launch_post(const PostArgs &a0, bool fine, hipStream_t s)
+{
+    int t, gx, gy, r;
+    fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r);
+    PostArgs a = a0;
+    a.rows_per_block = r;
+    const dim3 g(gx, gy), b(t);
+    if (fine) k_post<true><<<g, b, 0, s>>>(a);
+    else k_post<false><<<g, b, 0, s>>>(a);
+}
+
+// ---------------------------------------------------------------------------
+// Fix-ups (rare path): the early-exit check after the first sweep fired.
+// Scalar grid-stride code recomputing the reference result from the inputs
+// the fused pass left untouched.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool fix_decide(const FixArgsF &a, double *red, int *trig)
+{
+    double s = 0.0;
+    for (int k = threadIdx.x; k < a.np; k += blockDim.x) s += a.partials[k];
+    s = fused_block_sum(s, red);
+    if (threadIdx.x == 0) {
+        const double tot = a.global_sum != nullptr ? *a.global_sum : s;
+        *trig = (sqrt(tot) < a.eps) ? 1 : 0;
+    }
+    __syncthreads();
+    const bool t = *trig != 0;
+    if (t && blockIdx.x == 0 && threadIdx.x == 0 && a.stats != nullptr) {
+        atomicAdd(&a.stats[0], (unsigned long long)-1LL);
+        atomicAdd(&a.stats[1], 1ull);
+    }
+    return t;
+}
+
+struct FixCtx {
+    const double *x0, *f;
+    const double *ec;
+    int N, Nc;
+    long long P, Pc;
+    double hh, ih;
+    bool x0_zero;
+};
+
+__device__ __forceinline__ double fx0(const FixCtx &c, int j, int i)
+{
+    return c.x0_zero ? 0.0 : c.x0[(long long)j * c.P + i];
+}
+
+// x_eff = phi + P ec at one fine point (MultiGrid.hpp:208-226)
+__device__ double fxeff(const FixCtx &c, int j, int i)
+{
+    double v = c.x0[(long long)j * c.P + i];
+    if (j < 2 || i < 2 || j > c.N - 2 || i > c.N - 2) return v;
+    const int jc = j >> 1, ic = i >> 1;
+    const double *C0 = c.ec + (long long)jc * c.Pc;
+    double w;
+    if ((j & 1) == 0) {
+        w = ((i & 1) == 0) ? C0[ic] : 0.5 * (C0[ic] + C0[ic + 1]);
+    } else {
+        const double *C1 = C0 + c.Pc;
+        w = ((i & 1) == 0) ? 0.5 * (C0[ic] + C1[ic]) : 0.25 * (C0[ic] + C0[ic + 1] + C1[ic] + C1[ic + 1]);
+    }
+    return v + w;
+}
+
+template <bool POST>
+__device__ double fin(const FixCtx &c, int j, int i)
+{
+    return POST ? fxeff(c, j, i) : fx0(c, j, i);
+}
+
+template <bool POST>
+__device__ double fx1(const FixCtx &c, int j, int i)
+{
+    if (j <= 0 || i <= 0 || j >= c.N - 1 || i >= c.N - 1) return fin<POST>(c, j, i);
+    return 0.25 * ((c.hh * c.f[(long long)j * c.P + i]) + fin<POST>(c, j, i - 1) +
+                   fin<POST>(c, j, i + 1) + fin<POST>(c, j - 1, i) + fin<POST>(c, j + 1, i));
+}
+
+__device__ double fr1(const FixCtx &c, int j, int i)
+{
+    return c.f[(long long)j * c.P + i] -
+           c.ih * (4 * fx1<false>(c, j, i) - fx1<false>(c, j, i - 1) - fx1<false>(c, j, i + 1) -
+                   fx1<false>(c, j - 1, i) - fx1<false>(c, j + 1, i));
+}
+
+__global__ __launch_bounds__(256) void k_pre_fixup(FixArgsF a, PreArgs p, int x0_zero)
+{
+    __shared__ double red[4];
+    __shared__ int trig;
+    if (!fix_decide(a, red, &trig)) return;
+    FixCtx c{p.x0, p.f, nullptr, p.N, p.Nc, p.P, p.Pc, p.hh, p.ih, x0_zero != 0};
+    const long long W = p.N - 2;
+    const long long nrows = (long long)(p.row_hi - p.row_lo);
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < nrows * W; k += stride) {
+        const int j = p.row_lo + (int)(k / W), i = 1 + (int)(k % W);
+        p.x2[(long long)j * p.P + i] = fx1<false>(c, j, i);
+    }
+    const int clo = max(1, p.rc_lo), chi = min(p.Nc - 1, p.rc_hi);
+    const long long Wc = p.Nc - 2;
+    const long long ncr = chi > clo ? (long long)(chi - clo) : 0;
+    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < ncr * Wc; k += stride) {
+        const int jc = clo + (int)(k / Wc), ic = 1 + (int)(k % Wc);
+        const int j = 2 * jc, i = 2 * ic;
+        p.rc[(long long)jc * p.Pc + ic] =
+            0.25 * fr1(c, j, i) + 0.125 * (fr1(c, j, i + 1) + fr1(c, j, i - 1) + fr1(c, j + 1, i) + fr1(c, j - 1, i)) +
+            0.0625 * (fr1(c, j - 1, i - 1) + fr1(c, j - 1, i + 1) + fr1(c, j + 1, i - 1) + fr1(c, j + 1, i + 1));
+    }
+}
+
+__global__ __launch_bounds__(256) void k_post_fixup(FixArgsF a, PostArgs p)
+{
+    __shared__ double red[4];
+    __shared__ int trig;
+    if (!fix_decide(a, red, &trig)) return;
+    FixCtx c{p.phi, p.f, p.ec, p.N, p.Nc, p.P, p.Pc, p.hh, p.ih, false};
+    const long long W = p.N - 2;
+    const long long nrows = (long long)(p.row_hi - p.row_lo);
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < nrows * W; k += stride) {
+        const int j = p.row_lo + (int)(k / W), i = 1 + (int)(k % W);
+        p.x2[(long long)j * p.P + i] = fx1<true>(c, j, i);
+    }
+}
+
+void launch_pre_fixup(const FixArgsF &a, const PreArgs &p, bool x0_zero, hipStream_t s)
+{
+    k_pre_fixup<<<dim3(256), dim3(256), 0, s>>>(a, p, x0_zero ? 1 : 0);
+}
+
+void launch_post_fixup(const FixArgsF &a, const PostArgs &p, hipStream_t s)
+{
+    k_post_fixup<<<dim3(256), dim3(256), 0, s>>>(a, p);
+}
+
+}  // namespace pgmg

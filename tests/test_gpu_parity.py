@@ -82,6 +82,31 @@ def test_full_vectors(pgmg, name):
         assert_bitwise(s.solution(), ref, name)
 
 
+@pytest.mark.parametrize("N,cycles", [(129, 30), (513, 30), (1025, 3)])
+def test_unfused_path_matches_golden(pgmg, oracle_mod, golden_cycles, N, cycles):
+    """One kernel per sweep (the general path) gives the same bits as the fused passes."""
+    case = _golden(golden_cycles, "V", N)
+    case = dict(case, cycles=case["cycles"][:cycles])
+    _run_against_golden(pgmg, oracle_mod, case, flags=pgmg.PGMG_FLAG_UNFUSED)
+    _run_against_golden(pgmg, oracle_mod, case, flags=pgmg.PGMG_FLAG_UNFUSED, tail_n=9)
+
+
+@pytest.mark.parametrize("v1,v2,N", [(2, 0, 257), (0, 3, 129), (3, 2, 129), (2, 2, 65)])
+def test_other_smoothing_counts_against_oracle(pgmg, oracle_mod, v1, v2, N):
+    """v1/v2 != 1 (general path, odd sweep counts, several early-exit checks per call)."""
+    for eps, tail_n in ((1e-7, 65), (1e-7, 9), (5.0, 9)):
+        o = oracle_mod.Oracle(eps=eps, v1=v1, v2=v2)
+        f = o.rhs(N)
+        ref = np.zeros((N, N))
+        with pgmg.Solver(N, v1=v1, v2=v2, eps=eps, tail_n=tail_n) as s:
+            s.set_problem()
+            for k in range(4):
+                o.v_cycle(ref, f)
+                s.vcycle(1)
+                assert_bitwise(s.solution(), ref, f"v1={v1} v2={v2} eps={eps} tail={tail_n} k={k}")
+                assert s.stats()[0] == o.sweeps
+
+
 def test_graph_replay_equals_eager(pgmg):
     out = []
     for flags in (0, pgmg.PGMG_FLAG_NO_GRAPH, pgmg.PGMG_FLAG_TIME_FINE):
