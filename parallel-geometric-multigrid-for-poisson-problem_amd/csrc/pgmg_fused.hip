@@ -27,6 +27,8 @@
 //
 // Every expression keeps the reference's left-to-right order; built with
 // -ffp-contract=off, so the results are bit-identical to the unfused path.
+#include <cstdlib>
+
 #include "pgmg_fused.h"
 
 namespace pgmg {
@@ -110,9 +112,10 @@ __device__ __forceinline__ double fused_block_sum(double v, double *red)
 // ---------------------------------------------------------------------------
 // k_pre
 // ---------------------------------------------------------------------------
-template <bool X0_ZERO, bool FINE>
+template <bool X0_ZERO, bool FINE, int PAIRS>
 __global__ __launch_bounds__(256) void k_pre(PreArgs a)
 {
+    constexpr int R = 2 * PAIRS;  // rows loaded per iteration (and prefetched ahead)
     __shared__ double red[4];
     const Cols k = lane_cols(a.N);
     const int N = a.N;
@@ -132,29 +135,35 @@ __global__ __launch_bounds__(256) void k_pre(PreArgs a)
     //          f rows i-3,i-2,i-1
     double2 a0 = z, a1 = z, b0 = z, b1 = z, c0 = z, c1 = z, d0 = z, d1 = z, f0 = z, f1 = z, f2 = z;
     double acc = 0.0;
-    const int i_begin = 2 * jcb - 4, i_end = 2 * jce + 4;  // steps [i_begin, i_end)
-    double2 nx0 = z, nx1 = z, nf0, nf1;
-    if (!X0_ZERO) {
-        nx0 = ldg2(X + i_begin * P);
-        nx1 = ldg2(X + (i_begin + 1) * P);
+    // steps [i_begin, i_end): rows 2jcb-4 .. 2jce+3, rounded up to whole iterations
+    // (the extra rows are computed but never stored; kHalo covers their loads)
+    const int i_begin = 2 * jcb - 4;
+    const int i_end = i_begin + ((2 * (jce - jcb) + 8 + R - 1) / R) * R;
+    double2 nx[R], nf[R];
+    #pragma unroll
+    for (int q = 0; q < R; ++q) {
+        nx[q] = X0_ZERO ? z : ldg2(X + (i_begin + q) * P);
+        nf[q] = ldg2(F + (i_begin + q) * P);
     }
-    nf0 = ldg2(F + i_begin * P);
-    nf1 = ldg2(F + (i_begin + 1) * P);
-    for (int i = i_begin; i < i_end; i += 2) {
-        double2 xe = nx0, xo = nx1, fe = nf0, fo = nf1;
-        if (i + 2 < i_end) {  // prefetch the next pair of rows
-            if (!X0_ZERO) {
-                nx0 = ldg2(X + (i + 2) * P);
-                nx1 = ldg2(X + (i + 3) * P);
+    for (int i = i_begin; i < i_end; i += R) {
+        double2 cx[R], cf[R];
+        #pragma unroll
+        for (int q = 0; q < R; ++q) {
+            cx[q] = nx[q];
+            cf[q] = nf[q];
+        }
+        if (i + R < i_end) {  // prefetch the next R rows
+            #pragma unroll
+            for (int q = 0; q < R; ++q) {
+                if (!X0_ZERO) nx[q] = ldg2(X + (i + R + q) * P);
+                nf[q] = ldg2(F + (i + R + q) * P);
             }
-            nf0 = ldg2(F + (i + 2) * P);
-            nf1 = ldg2(F + (i + 3) * P);
         }
         #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < R; ++s) {
             const int ii = i + s;
-            const double2 a2 = s ? xo : xe;
-            const double2 f3 = s ? fo : fe;
+            const double2 a2 = cx[s];
+            const double2 f3 = cf[s];
             // x1 row ii-1
             const double2 b2 = jstage(a0, a1, a2, f2, hh, k, boundary_row(ii - 1, N));
             // r(x1) and x2 on row ii-2
@@ -168,10 +177,10 @@ __global__ __launch_bounds__(256) void k_pre(PreArgs a)
             }
             const double2 c2 = jstage(b0, b1, b2, f1, hh, k, boundary_row(ii - 2, N));
             if (ii - 2 >= olo && ii - 2 < ohi && k.own) stg2(O + (ii - 2) * P, c2);
-            // r(x2) on row ii-3 (0 on boundary rows; never used there)
+            // r(x2) on row ii-3 (garbage on boundary rows; never used there)
             const double2 d2 = rstage(c0, c1, c2, f0, ih);
             // restriction: rows ii-5, ii-4, ii-3 = 2jc-1, 2jc, 2jc+1 when ii is even
-            if (s == 0) {
+            if ((s & 1) == 0) {
                 const int jc = (ii - 4) >> 1;
                 const double m2 = dpp_next_f(d1.x);
                 const double u2 = dpp_next_f(d0.x);
@@ -196,8 +205,8 @@ __global__ __launch_bounds__(256) void k_pre(PreArgs a)
             f2 = f3;
         }
     }
-    const double s = fused_block_sum(acc, red);
-    if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = s;
+    const double sum = fused_block_sum(acc, red);
+    if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = sum;
 }
 
 // ---------------------------------------------------------------------------
@@ -224,9 +233,10 @@ __device__ __forceinline__ double2 add_prolong(double2 p, int row, double ca, do
     return p;
 }
 
-template <bool FINE>
+template <bool FINE, int PAIRS>
 __global__ __launch_bounds__(256) void k_post(PostArgs a)
 {
+    constexpr int R = 2 * PAIRS;
     __shared__ double red[4];
     const Cols k = lane_cols(a.N);
     const int N = a.N, Nc = a.Nc;
@@ -249,29 +259,47 @@ __global__ __launch_bounds__(256) void k_post(PostArgs a)
     // windows: x_eff rows i-2,i-1 ; x1 rows i-3,i-2 ; f rows i-2,i-1
     double2 a0 = z, a1 = z, b0 = z, b1 = z, f1 = z, f2 = z;
     double acc = 0.0;
-    const int i_begin = 2 * jcb - 2, i_end = 2 * jce + 2;
-    double2 np0 = ldg2(X + i_begin * P), np1 = ldg2(X + (i_begin + 1) * P);
-    double2 nf0 = ldg2(F + i_begin * P), nf1 = ldg2(F + (i_begin + 1) * P);
-    double cm = E[(long long)(i_begin >> 1) * Pc];              // coarse row m = i/2
-    double nc1 = E[(long long)((i_begin >> 1) + 1) * Pc];       // coarse row m+1
-    for (int i = i_begin; i < i_end; i += 2) {
-        const double2 pe = np0, po = np1, fe = nf0, fo = nf1;
-        const double cmA = cm, cmB_row = nc1;
-        if (i + 2 < i_end) {
-            np0 = ldg2(X + (i + 2) * P);
-            np1 = ldg2(X + (i + 3) * P);
-            nf0 = ldg2(F + (i + 2) * P);
-            nf1 = ldg2(F + (i + 3) * P);
-            cm = nc1;
-            nc1 = E[(long long)((i >> 1) + 2) * Pc];
-        }
-        const double ca = cmA, cb = dpp_next_f(cmA);
-        const double da = cmB_row, db = dpp_next_f(cmB_row);
+    const int i_begin = 2 * jcb - 2;
+    const int i_end = i_begin + ((2 * (jce - jcb) + 4 + R - 1) / R) * R;
+    // coarse row m = ii/2 of fine row ii; an iteration of R rows uses coarse rows
+    // i/2 .. i/2 + PAIRS
+    double2 np_[R], nf[R];
+    double ncr[PAIRS + 1];
+    #pragma unroll
+    for (int q = 0; q < R; ++q) {
+        np_[q] = ldg2(X + (i_begin + q) * P);
+        nf[q] = ldg2(F + (i_begin + q) * P);
+    }
+    #pragma unroll
+    for (int q = 0; q <= PAIRS; ++q) ncr[q] = E[(long long)((i_begin >> 1) + q) * Pc];
+    for (int i = i_begin; i < i_end; i += R) {
+        double2 cp[R], cf[R];
+        double cr[PAIRS + 1];
         #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int q = 0; q < R; ++q) {
+            cp[q] = np_[q];
+            cf[q] = nf[q];
+        }
+        #pragma unroll
+        for (int q = 0; q <= PAIRS; ++q) cr[q] = ncr[q];
+        if (i + R < i_end) {
+            #pragma unroll
+            for (int q = 0; q < R; ++q) {
+                np_[q] = ldg2(X + (i + R + q) * P);
+                nf[q] = ldg2(F + (i + R + q) * P);
+            }
+            #pragma unroll
+            for (int q = 0; q <= PAIRS; ++q) ncr[q] = E[(long long)(((i + R) >> 1) + q) * Pc];
+        }
+        double crn[PAIRS + 1];
+        #pragma unroll
+        for (int q = 0; q <= PAIRS; ++q) crn[q] = dpp_next_f(cr[q]);
+        #pragma unroll
+        for (int s = 0; s < R; ++s) {
             const int ii = i + s;
-            const double2 a2 = add_prolong(s ? po : pe, ii, ca, cb, da, db, pc, Nc);
-            const double2 f3 = s ? fo : fe;
+            const int pq = s >> 1;
+            const double2 a2 = add_prolong(cp[s], ii, cr[pq], crn[pq], cr[pq + 1], crn[pq + 1], pc, Nc);
+            const double2 f3 = cf[s];
             const double2 b2 = jstage(a0, a1, a2, f2, hh, k, boundary_row(ii - 1, N));
             {
                 const int row = ii - 2;
@@ -291,13 +319,22 @@ __global__ __launch_bounds__(256) void k_post(PostArgs a)
             f2 = f3;
         }
     }
-    const double s = fused_block_sum(acc, red);
-    if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = s;
+    const double sum = fused_block_sum(acc, red);
+    if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = sum;
 }
 
 // ---------------------------------------------------------------------------
 // launch geometry
 // ---------------------------------------------------------------------------
+// Launch geometry.  Blocks march down long row bands: the grid is sized to about
+// the number of workgroups resident at once (tunable: PGMG_FUSED_BLOCKS), so the
+// 8 halo rows per band are a small fraction and there is no tail wave of blocks.
+static int env_int(const char *name, int dflt)
+{
+    const char *v = getenv(name);
+    return (v && *v) ? atoi(v) : dflt;
+}
+
 static void fused_geometry(int N, int jc0, int jc1, int *threads, int *gx, int *gy, int *rpb)
 {
     const int waves = (N - 2 + 119) / 120;
@@ -305,12 +342,18 @@ static void fused_geometry(int N, int jc0, int jc1, int *threads, int *gx, int *
     *threads = 64 * wpb;
     *gx = (waves + wpb - 1) / wpb;
     const int rows = jc1 - jc0;   // coarse rows
-    int r = (int)(((long long)rows * *gx + 2047) / 2048);  // >= ~2048 blocks when possible
-    r = r < 8 ? 8 : (r > 64 ? 64 : r);
+    const int target = env_int("PGMG_FUSED_BLOCKS", 2048);  // tuned r01: tune_fused.py
+    const int rmin = env_int("PGMG_FUSED_MIN_ROWS", 8);
+    const int rmax = env_int("PGMG_FUSED_MAX_ROWS", 512);
+    int r = (int)(((long long)rows * *gx + target - 1) / target);
+    r = r < rmin ? rmin : (r > rmax ? rmax : r);
     if (r > rows) r = rows;
+    if (r < 1) r = 1;
     *rpb = r;
     *gy = (rows + r - 1) / r;
 }
+
+static int fused_pairs() { return env_int("PGMG_FUSED_PAIRS", 2) >= 2 ? 2 : 1; }
 
 int fused_blocks(int N, int jc0, int jc1)
 {
@@ -328,9 +371,15 @@ void launch_pre(const PreArgs &a0, bool x0_zero, bool fine, hipStream_t s)
     PreArgs a = a0;
     a.rows_per_block = r;
     const dim3 g(gx, gy), b(t);
-    if (x0_zero) k_pre<true, false><<<g, b, 0, s>>>(a);
-    else if (fine) k_pre<false, true><<<g, b, 0, s>>>(a);
-    else k_pre<false, false><<<g, b, 0, s>>>(a);
+    if (fused_pairs() == 2) {
+        if (x0_zero) k_pre<true, false, 2><<<g, b, 0, s>>>(a);
+        else if (fine) k_pre<false, true, 2><<<g, b, 0, s>>>(a);
+        else k_pre<false, false, 2><<<g, b, 0, s>>>(a);
+    } else {
+        if (x0_zero) k_pre<true, false, 1><<<g, b, 0, s>>>(a);
+        else if (fine) k_pre<false, true, 1><<<g, b, 0, s>>>(a);
+        else k_pre<false, false, 1><<<g, b, 0, s>>>(a);
+    }
 }
 
 void launch_post(const PostArgs &a0, bool fine, hipStream_t s)
@@ -340,8 +389,13 @@ void launch_post(const PostArgs &a0, bool fine, hipStream_t s)
     PostArgs a = a0;
     a.rows_per_block = r;
     const dim3 g(gx, gy), b(t);
-    if (fine) k_post<true><<<g, b, 0, s>>>(a);
-    else k_post<false><<<g, b, 0, s>>>(a);
+    if (fused_pairs() == 2) {
+        if (fine) k_post<true, 2><<<g, b, 0, s>>>(a);
+        else k_post<false, 2><<<g, b, 0, s>>>(a);
+    } else {
+        if (fine) k_post<true, 1><<<g, b, 0, s>>>(a);
+        else k_post<false, 1><<<g, b, 0, s>>>(a);
+    }
 }
 
 // ---------------------------------------------------------------------------

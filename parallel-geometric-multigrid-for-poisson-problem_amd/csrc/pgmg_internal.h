@@ -16,7 +16,7 @@
 namespace pgmg {
 
 constexpr int kOff = 15;          // doubles between allocation base and element (0,0)
-constexpr int kHalo = 4;          // halo rows allocated above and below a level's rows
+constexpr int kHalo = 6;          // halo rows allocated above and below a level's rows
 constexpr int kBlock = 256;       // threads per block for streaming kernels (4 waves)
 constexpr int kTailThreads = 1024;
 constexpr int kTailMaxN = 65;     // largest level the LDS-resident tail holds
