@@ -110,19 +110,14 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
         dist.init_process_group("gloo")
-        import ctypes
-        buf = (ctypes.c_ubyte * 128)()
-        if rank == 0:
-            pg._capi.check(pg.load().pgmg_comm_unique_id(buf), "pgmg_comm_unique_id")
-        t = torch.tensor(list(bytes(buf)), dtype=torch.uint8)
+        t = torch.tensor(list(pg.unique_id()) if rank == 0 else [0] * 128, dtype=torch.uint8)
         dist.broadcast(t, 0)
-        uid = (ctypes.c_ubyte * 128)(*t.tolist())
+        uid = bytes(t.tolist())
 
     flags = pg.PGMG_FLAG_TIME_FINE if args.timing == "events" else 0
     kw = dict(flags=flags, device=local_rank if world > 1 else 0)
     if world > 1:
-        import ctypes
-        kw.update(rank=rank, world=world, nccl_unique_id=ctypes.cast(uid, ctypes.c_void_p))
+        kw.update(rank=rank, world=world, uid=uid)
     s = pg.Solver(args.n, **kw)
     s.set_problem()
     bulk, tail_top = s.levels()

@@ -67,6 +67,9 @@ extern "C" {
                                     pass (see pgmg_fine_pass_time)                  */
 #define PGMG_FLAG_UNFUSED 4u     /* one kernel per smoother sweep even when v1 = v2 = 1
                                     (the general path; same results)                */
+#define PGMG_FLAG_LOOPBACK 8u    /* world > 1 with ranks as threads of one process on
+                                    one GPU: nccl_unique_id is a pgmg_loopback hub
+                                    (test transport for the strip decomposition)    */
 
 typedef struct pgmg_config {
     int N;             /* points per side incl. boundary; 2^k + 1, k >= 2        */
@@ -168,6 +171,15 @@ int pgmg_device_count(int *n);
 
 /* RCCL bootstrap: fill a 128-byte buffer with a fresh ncclUniqueId (rank 0). */
 int pgmg_comm_unique_id(void *out128);
+
+/* In-process rank hub for PGMG_FLAG_LOOPBACK (tests of the strip decomposition). */
+int pgmg_loopback_create(int world, void **hub);
+int pgmg_loopback_destroy(void *hub);
+
+/* Host-only strip plan: the finest-level rows [lo, hi) rank `rank` owns and the
+ * number of strip-distributed levels (0: too small to split, replicas). */
+int pgmg_plan_strips(int N, int world, int rank, int tail_n, int gather_n, int *lo, int *hi,
+                     int *dist_levels);
 
 const char *pgmg_last_error(void);
 const char *pgmg_version(void);

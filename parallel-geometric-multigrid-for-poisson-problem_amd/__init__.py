@@ -16,14 +16,16 @@ import subprocess
 
 import numpy as np
 
-from ._capi import (PGMG_FLAG_NO_GRAPH, PGMG_FLAG_TIME_FINE, PGMG_FLAG_UNFUSED, PGMG_PROLONG_REFERENCE,
+from ._capi import (PGMG_FLAG_LOOPBACK, PGMG_FLAG_NO_GRAPH, PGMG_FLAG_TIME_FINE,
+                    PGMG_FLAG_UNFUSED, PGMG_PROLONG_REFERENCE,
                     PGMG_PROLONG_SYMMETRIC, PgmgConfig, PgmgError, check, load)
 
 PKG_DIR = pathlib.Path(__file__).resolve().parent
 
 __all__ = [
     "build", "load", "Solver", "PgmgConfig", "PgmgError", "ops",
-    "PGMG_FLAG_NO_GRAPH", "PGMG_FLAG_TIME_FINE", "PGMG_FLAG_UNFUSED", "PGMG_PROLONG_REFERENCE",
+    "PGMG_FLAG_NO_GRAPH", "PGMG_FLAG_TIME_FINE", "PGMG_FLAG_UNFUSED", "PGMG_FLAG_LOOPBACK",
+    "PGMG_PROLONG_REFERENCE", "plan_strips", "LoopbackHub", "unique_id",
     "PGMG_PROLONG_SYMMETRIC",
 ]
 
@@ -47,6 +49,38 @@ def default_config(N, **kw):
     return cfg
 
 
+def plan_strips(N, world, rank, tail_n=65, gather_n=1025):
+    """Finest-level rows [lo, hi) owned by `rank` and the number of strip-distributed
+    levels (host arithmetic of the row-strip decomposition; no GPU needed)."""
+    lo, hi, nd = C.c_int(), C.c_int(), C.c_int()
+    check(load().pgmg_plan_strips(int(N), int(world), int(rank), int(tail_n), int(gather_n),
+                                  C.byref(lo), C.byref(hi), C.byref(nd)), "pgmg_plan_strips")
+    return lo.value, hi.value, nd.value
+
+
+def unique_id():
+    """A fresh 128-byte RCCL unique id (rank 0 creates it, then broadcasts it)."""
+    buf = (C.c_ubyte * 128)()
+    check(load().pgmg_comm_unique_id(buf), "pgmg_comm_unique_id")
+    return bytes(buf)
+
+
+class LoopbackHub:
+    """In-process rank hub: `world` Solvers in threads of one process share one GPU
+    (test transport for the strip decomposition; RCCL refuses two ranks per device)."""
+
+    def __init__(self, world):
+        h = C.c_void_p()
+        check(load().pgmg_loopback_create(int(world), C.byref(h)), "pgmg_loopback_create")
+        self.h = h
+        self.world = world
+
+    def close(self):
+        if self.h:
+            load().pgmg_loopback_destroy(self.h)
+            self.h = None
+
+
 class Solver:
     """A multigrid context: level pyramid resident in HBM, cycles on a HIP stream.
 
@@ -55,12 +89,17 @@ class Solver:
     numerics of MultigridSolver (2_part_MG/MultiGrid.hpp:57-136).
     """
 
-    def __init__(self, N, **cfg):
+    def __init__(self, N, hub=None, uid=None, **cfg):
+        """hub: LoopbackHub (ranks as threads on one GPU); uid: 128-byte RCCL unique id."""
         self.lib = load()
+        if hub is not None:
+            cfg["flags"] = cfg.get("flags", 0) | PGMG_FLAG_LOOPBACK
+            cfg["world"] = hub.world
+            cfg["nccl_unique_id"] = hub.h
+        elif uid is not None:
+            self._uid = (C.c_ubyte * 128)(*uid)
+            cfg["nccl_unique_id"] = C.cast(self._uid, C.c_void_p)
         self.cfg = default_config(N, **cfg)
-        self._keep = None
-        if self.cfg.world > 1 and "nccl_unique_id" in cfg:
-            self._keep = cfg["nccl_unique_id"]
         h = C.c_void_p()
         check(self.lib.pgmg_create(C.byref(h), C.byref(self.cfg)), "pgmg_create")
         self.h = h

@@ -24,6 +24,7 @@ PGMG_PROLONG_SYMMETRIC = 1
 PGMG_FLAG_NO_GRAPH = 1
 PGMG_FLAG_TIME_FINE = 2
 PGMG_FLAG_UNFUSED = 4
+PGMG_FLAG_LOOPBACK = 8
 
 
 class PgmgConfig(C.Structure):
@@ -87,6 +88,10 @@ SIGNATURES = [
     ("pgmg_device_sync", C.c_int, []),
     ("pgmg_device_count", C.c_int, [C.POINTER(C.c_int)]),
     ("pgmg_comm_unique_id", C.c_int, [_P]),
+    ("pgmg_loopback_create", C.c_int, [C.c_int, C.POINTER(_P)]),
+    ("pgmg_loopback_destroy", C.c_int, [_P]),
+    ("pgmg_plan_strips", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                   C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("pgmg_last_error", C.c_char_p, []),
     ("pgmg_version", C.c_char_p, []),
 ]

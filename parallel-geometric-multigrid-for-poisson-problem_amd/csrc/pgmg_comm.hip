@@ -1,20 +1,477 @@
-// pgmg_comm.hip — row-strip domain decomposition over RCCL (one process per GPU).
-// (placeholder until the strip exchange lands; world == 1 never reaches here)
+// pgmg_comm.hip — row-strip domain decomposition of the level pyramid over ranks.
+//
+// One process per GPU (BASELINE north star: "partitioned across the 8 GPUs ... halo
+// exchange as RCCL point-to-point ... the coarsest levels collapsing to rank 0").
+// The reference has no multi-GPU path; this is new.
+//
+//  * Split points s_r of the finest level are multiples of 2^Ld, so level l < Ld
+//    splits at s_r >> l and the coarse row jc sits on the rank owning fine row 2jc.
+//    Rank r owns rows [s_r, s_{r+1}) (rank 0 also row 0, the last rank row N-1).
+//  * Every kernel is pointwise with a bounded neighbourhood, so halo rows make the
+//    strip computation bit-identical to one GPU.  Halo depths (rows): k_pre reads
+//    x0/f 4 rows past its strip (two sweeps + residual + restriction), k_post reads
+//    phi 2 rows and the coarse correction 1-2 rows.
+//  * The smoother's early-exit norm is a global sum: a local partial sum, then one
+//    allreduce of a single double (all ranks take the same decision).
+//  * Levels with N <= gather_n (or strips thinner than kMinRows) are "gathered":
+//    each rank sends its rows of the coarse right-hand side to rank 0, rank 0 runs
+//    the remaining cycle (bulk kernels + LDS tail) alone, then sends each rank the
+//    rows of the correction its prolongation reads.
+//  * Transport: RCCL grouped ncclSend/ncclRecv + ncclAllReduce on the context's
+//    stream (RCCL over xGMI on MI355X).  Tests use an in-process loopback
+//    transport (ranks = host threads sharing one GPU; RCCL refuses two ranks per
+//    device) that gives the same message semantics.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
 #include "pgmg_ctx.h"
 
 namespace pgmg {
 
+namespace {
+
+constexpr int kMinRows = 16;  // thinnest strip a distributed level may have
+
+#define NCCLC(expr)                                                                        \
+    do {                                                                                   \
+        ncclResult_t r_ = (expr);                                                          \
+        if (r_ != ncclSuccess)                                                             \
+            return set_err(PGMG_ERR_COMM, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// transports
+// ---------------------------------------------------------------------------
+class Transport {
+  public:
+    virtual ~Transport() {}
+    virtual int group_start() = 0;
+    virtual int send(const void *buf, size_t bytes, int peer, hipStream_t s) = 0;
+    virtual int recv(void *buf, size_t bytes, int peer, hipStream_t s) = 0;
+    virtual int group_end(hipStream_t s) = 0;
+    virtual int allreduce_sum(double *d, int n, hipStream_t s) = 0;
+};
+
+class RcclTransport : public Transport {
+  public:
+    ncclComm_t comm = nullptr;
+    ~RcclTransport() override
+    {
+        if (comm) ncclCommDestroy(comm);
+    }
+    int init(const void *uid, int world, int rank)
+    {
+        ncclUniqueId id;
+        std::memcpy(&id, uid, sizeof(id));
+        NCCLC(ncclCommInitRank(&comm, world, id, rank));
+        return PGMG_OK;
+    }
+    int group_start() override
+    {
+        NCCLC(ncclGroupStart());
+        return PGMG_OK;
+    }
+    int send(const void *buf, size_t bytes, int peer, hipStream_t s) override
+    {
+        NCCLC(ncclSend(buf, bytes, ncclChar, peer, comm, s));
+        return PGMG_OK;
+    }
+    int recv(void *buf, size_t bytes, int peer, hipStream_t s) override
+    {
+        NCCLC(ncclRecv(buf, bytes, ncclChar, peer, comm, s));
+        return PGMG_OK;
+    }
+    int group_end(hipStream_t) override
+    {
+        NCCLC(ncclGroupEnd());
+        return PGMG_OK;
+    }
+    int allreduce_sum(double *d, int n, hipStream_t s) override
+    {
+        NCCLC(ncclAllReduce(d, d, n, ncclDouble, ncclSum, comm, s));
+        return PGMG_OK;
+    }
+};
+
+}  // namespace
+
+// In-process hub for the loopback transport (test infrastructure for the strip
+// decomposition on a single GPU).  Message matching by (src, dst, sequence).
+struct LoopbackHub {
+    int world = 0;
+    std::mutex m;
+    std::condition_variable cv;
+    struct Msg {
+        const void *src = nullptr;
+        size_t bytes = 0;
+        hipEvent_t ready = nullptr;  // recorded on the sender's stream
+        hipEvent_t done = nullptr;   // recorded on the receiver's stream after the copy
+        bool posted = false, copied = false;
+    };
+    std::map<std::tuple<int, int, long long>, Msg> box;
+    std::map<std::pair<int, int>, long long> seq_send, seq_recv;
+    // allreduce rendezvous
+    long long ar_round[64] = {0};
+    std::map<long long, std::vector<double>> ar_vals;
+    std::map<long long, int> ar_count, ar_taken;
+};
+
+namespace {
+
+class LoopbackTransport : public Transport {
+  public:
+    LoopbackHub *hub;
+    int me;
+    struct Pend {
+        bool is_send;
+        void *buf;
+        size_t bytes;
+        int peer;
+    };
+    std::vector<Pend> pend;
+    LoopbackTransport(LoopbackHub *h, int rank) : hub(h), me(rank) {}
+    int group_start() override
+    {
+        pend.clear();
+        return PGMG_OK;
+    }
+    int send(const void *buf, size_t bytes, int peer, hipStream_t) override
+    {
+        pend.push_back({true, const_cast<void *>(buf), bytes, peer});
+        return PGMG_OK;
+    }
+    int recv(void *buf, size_t bytes, int peer, hipStream_t) override
+    {
+        pend.push_back({false, buf, bytes, peer});
+        return PGMG_OK;
+    }
+    int group_end(hipStream_t s) override
+    {
+        std::vector<std::tuple<int, int, long long>> my_sends;
+        // 1. post sends (data ready when the sender's stream reaches this point)
+        for (auto &p : pend) {
+            if (!p.is_send) continue;
+            hipEvent_t ready, done;
+            PGMG_HIPC(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+            PGMG_HIPC(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+            PGMG_HIPC(hipEventRecord(ready, s));
+            std::lock_guard<std::mutex> g(hub->m);
+            const long long q = hub->seq_send[{me, p.peer}]++;
+            auto key = std::make_tuple(me, p.peer, q);
+            auto &msg = hub->box[key];
+            msg.src = p.buf;
+            msg.bytes = p.bytes;
+            msg.ready = ready;
+            msg.done = done;
+            msg.posted = true;
+            my_sends.push_back(key);
+            hub->cv.notify_all();
+        }
+        // 2. receive: wait for the matching send, copy on this stream
+        for (auto &p : pend) {
+            if (p.is_send) continue;
+            std::unique_lock<std::mutex> g(hub->m);
+            const long long q = hub->seq_recv[{p.peer, me}]++;
+            auto key = std::make_tuple(p.peer, me, q);
+            hub->cv.wait(g, [&] { return hub->box.count(key) && hub->box[key].posted; });
+            auto msg = hub->box[key];
+            g.unlock();
+            if (msg.bytes != p.bytes) return set_err(PGMG_ERR_COMM, "loopback size mismatch");
+            PGMG_HIPC(hipStreamWaitEvent(s, msg.ready, 0));
+            PGMG_HIPC(hipMemcpyAsync(p.buf, msg.src, p.bytes, hipMemcpyDeviceToDevice, s));
+            PGMG_HIPC(hipEventRecord(msg.done, s));
+            g.lock();
+            hub->box[key].copied = true;
+            hub->cv.notify_all();
+        }
+        // 3. the sender may not overwrite its buffer before the receiver copied it
+        for (auto &key : my_sends) {
+            std::unique_lock<std::mutex> g(hub->m);
+            hub->cv.wait(g, [&] { return hub->box[key].copied; });
+            auto msg = hub->box[key];
+            hub->box.erase(key);
+            g.unlock();
+            PGMG_HIPC(hipStreamWaitEvent(s, msg.done, 0));
+            (void)hipEventDestroy(msg.ready);
+            // `done` is destroyed lazily: the wait above holds a reference
+            (void)hipEventDestroy(msg.done);
+        }
+        pend.clear();
+        return PGMG_OK;
+    }
+    int allreduce_sum(double *d, int n, hipStream_t s) override
+    {
+        std::vector<double> v(n);
+        PGMG_HIPC(hipMemcpyAsync(v.data(), d, n * sizeof(double), hipMemcpyDeviceToHost, s));
+        PGMG_HIPC(hipStreamSynchronize(s));
+        std::vector<double> tot;
+        {
+            std::unique_lock<std::mutex> g(hub->m);
+            const long long r = hub->ar_round[me]++;
+            auto &vals = hub->ar_vals[r];
+            if (vals.empty()) vals.assign((size_t)hub->world * n, 0.0);
+            std::copy(v.begin(), v.end(), vals.begin() + (size_t)me * n);
+            hub->ar_count[r]++;
+            hub->cv.notify_all();
+            hub->cv.wait(g, [&] { return hub->ar_count[r] == hub->world; });
+            tot.assign(n, 0.0);
+            for (int k = 0; k < hub->world; ++k)  // rank order: deterministic
+                for (int i = 0; i < n; ++i) tot[i] += vals[(size_t)k * n + i];
+            if (++hub->ar_taken[r] == hub->world) {
+                hub->ar_vals.erase(r);
+                hub->ar_count.erase(r);
+                hub->ar_taken.erase(r);
+            }
+        }
+        PGMG_HIPC(hipMemcpyAsync(d, tot.data(), n * sizeof(double), hipMemcpyHostToDevice, s));
+        PGMG_HIPC(hipStreamSynchronize(s));
+        return PGMG_OK;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// strip decomposition
+// ---------------------------------------------------------------------------
+class StripComm : public Comm {
+  public:
+    Transport *t = nullptr;
+    int me = 0, world = 1;
+    int Ld = 0;                  // levels 0..Ld-1 distributed; Ld = first gathered level
+    std::vector<int> split;      // finest-level split points s_0 .. s_world
+
+    ~StripComm() override { delete t; }
+    int gathered_level() const override { return Ld; }
+    int rank() const override { return me; }
+
+    int strip_lo(int r, int l) const { return split[r] >> l; }
+    int strip_hi(int r, int l, int N) const { return r == world - 1 ? N : (split[r + 1] >> l); }
+
+    int plan(pgmg_ctx *c) override
+    {
+        const int N0 = c->lv[0].N;
+        const int G = N0 - 1;
+        const int gather_n = std::max(c->cfg.gather_n, c->lv[c->nb].N);
+        // distributed levels: N_l > gather_n and every strip at least kMinRows rows
+        Ld = 0;
+        for (int l = 0; l < c->nb; ++l) {
+            const int Nl = c->lv[l].N;
+            if (Nl <= gather_n || (Nl - 1) / world < kMinRows) break;
+            Ld = l + 1;
+        }
+        if (Ld == 0) return 1;  // too small to split: every rank runs its own replica
+        const int align = 1 << Ld;
+        split.assign(world + 1, 0);
+        for (int r = 1; r < world; ++r)
+            split[r] = (int)(((long long)r * G / world) / align * align);
+        split[world] = N0;
+        for (int r = 0; r < world; ++r)
+            if (split[r + 1] - split[r] < kMinRows * (1 << (Ld - 1)) && r + 1 < world)
+                return set_err(PGMG_ERR_ARG, "grid too small for this many ranks");
+        for (int l = 0; l < (int)c->lv.size(); ++l) {
+            Level &L = c->lv[l];
+            if (l < Ld) {
+                L.lo = strip_lo(me, l);
+                L.hi = strip_hi(me, l, L.N);
+                L.on_this_rank = true;
+                L.gathered = false;
+            } else {
+                L.lo = 0;
+                L.hi = L.N;
+                L.gathered = true;
+                L.on_this_rank = (l == Ld) || me == 0;  // receive buffers for the correction
+            }
+            L.u0 = std::max(L.lo, 1);
+            L.u1 = std::min(L.hi, L.N - 1);
+        }
+        return PGMG_OK;
+    }
+
+    int setup(pgmg_ctx *) override { return PGMG_OK; }
+
+    int halo(double *o, const Level &L, int depth, hipStream_t s) override
+    {
+        const size_t row = (size_t)L.P * sizeof(double);
+        int e = t->group_start();
+        if (e) return e;
+        if (me > 0) {
+            if ((e = t->send(o + (size_t)L.lo * L.P, depth * row, me - 1, s))) return e;
+            if ((e = t->recv(o + (ptrdiff_t)(L.lo - depth) * L.P, depth * row, me - 1, s))) return e;
+        }
+        if (me < world - 1) {
+            if ((e = t->send(o + (ptrdiff_t)(L.hi - depth) * L.P, depth * row, me + 1, s))) return e;
+            if ((e = t->recv(o + (size_t)L.hi * L.P, depth * row, me + 1, s))) return e;
+        }
+        return t->group_end(s);
+    }
+
+    int allreduce_sum(double *d, hipStream_t s) override { return t->allreduce_sum(d, 1, s); }
+
+    int run_gathered(pgmg_ctx *c, int l, int gamma, int repeats) override
+    {
+        Level &L = c->lv[l];
+        const size_t row = (size_t)L.P * sizeof(double);
+        // 1. rows of the coarse right-hand side -> rank 0
+        int e = t->group_start();
+        if (e) return e;
+        for (int r = 0; r < world; ++r) {
+            const int a = std::max(strip_lo(r, l), 1), b = std::min(strip_hi(r, l, L.N), L.N - 1);
+            if (b <= a || r == 0) continue;
+            if (me == r && (e = t->send(L.F.o + (size_t)a * L.P, (b - a) * row, 0, c->s))) return e;
+            if (me == 0 && (e = t->recv(L.F.o + (size_t)a * L.P, (b - a) * row, r, c->s))) return e;
+        }
+        if ((e = t->group_end(c->s))) return e;
+        // 2. rank 0 runs the rest of the hierarchy alone
+        if (me == 0) {
+            for (int i = 0; i < repeats; ++i)
+                if ((e = enqueue_cycle(c, l, gamma, i == 0))) return e;
+        }
+        // 3. the correction rows each strip's prolongation reads -> every rank
+        if ((e = t->group_start())) return e;
+        for (int r = 1; r < world; ++r) {
+            const int a = std::max(strip_lo(r, l) - 2, 0);
+            const int b = std::min(strip_hi(r, l, L.N) + 2, L.N);
+            if (me == 0 && (e = t->send(L.A.o + (size_t)a * L.P, (b - a) * row, r, c->s))) return e;
+            if (me == r && (e = t->recv(L.A.o + (size_t)a * L.P, (b - a) * row, 0, c->s))) return e;
+        }
+        return t->group_end(c->s);
+    }
+
+    int gather_solution(pgmg_ctx *c, double *phi) override
+    {
+        Level &L = c->lv[0];
+        const int N = L.N;
+        double *full = nullptr;
+        PGMG_HIPC(hipMalloc((void **)&full, (size_t)N * L.P * sizeof(double)));
+        PGMG_HIPC(hipMemcpy2DAsync(full + (size_t)L.lo * L.P, L.P * sizeof(double),
+                                   L.A.o + (size_t)L.lo * L.P, L.P * sizeof(double),
+                                   N * sizeof(double), L.hi - L.lo, hipMemcpyDeviceToDevice, c->s));
+        const size_t row = (size_t)L.P * sizeof(double);
+        int e = t->group_start();
+        for (int r = 0; r < world && !e; ++r) {
+            if (r == me) continue;
+            e = t->send(L.A.o + (size_t)L.lo * L.P, (L.hi - L.lo) * row, r, c->s);
+            if (!e) {
+                const int a = strip_lo(r, 0), b = strip_hi(r, 0, N);
+                e = t->recv(full + (size_t)a * L.P, (b - a) * row, r, c->s);
+            }
+        }
+        if (!e) e = t->group_end(c->s);
+        if (!e) {
+            hipError_t he = hipMemcpy2DAsync(phi, N * sizeof(double), full, L.P * sizeof(double),
+                                             N * sizeof(double), N, hipMemcpyDeviceToHost, c->s);
+            if (he == hipSuccess) he = hipStreamSynchronize(c->s);
+            if (he != hipSuccess) e = set_err(PGMG_ERR_HIP, hipGetErrorString(he));
+        }
+        (void)hipFree(full);
+        return e;
+    }
+};
+
+}  // namespace
+
 Comm *Comm::create(pgmg_ctx *c, int *rc)
 {
-    (void)c;
-    *rc = set_err(PGMG_ERR_STATE, "world > 1 not available in this build");
-    return nullptr;
+    *rc = PGMG_OK;
+    const pgmg_config &cfg = c->cfg;
+    if (!cfg.nccl_unique_id) {
+        *rc = set_err(PGMG_ERR_ARG, "world > 1 needs nccl_unique_id (or a loopback hub)");
+        return nullptr;
+    }
+    auto *sc = new StripComm();
+    sc->me = cfg.rank;
+    sc->world = cfg.world;
+    if (cfg.flags & PGMG_FLAG_LOOPBACK) {
+        auto *hub = (LoopbackHub *)cfg.nccl_unique_id;
+        if (hub->world != cfg.world) {
+            *rc = set_err(PGMG_ERR_ARG, "loopback hub world mismatch");
+            delete sc;
+            return nullptr;
+        }
+        sc->t = new LoopbackTransport(hub, cfg.rank);
+    } else {
+        auto *rt = new RcclTransport();
+        sc->t = rt;
+        *rc = rt->init(cfg.nccl_unique_id, cfg.world, cfg.rank);
+        if (*rc) {
+            delete sc;
+            return nullptr;
+        }
+    }
+    return sc;
 }
 
 }  // namespace pgmg
 
-extern "C" int pgmg_comm_unique_id(void *out128)
+extern "C" {
+
+int pgmg_comm_unique_id(void *out128)
 {
-    (void)out128;
-    return pgmg::set_err(PGMG_ERR_STATE, "RCCL bootstrap not available in this build");
+    if (!out128) return pgmg::set_err(PGMG_ERR_ARG, "null buffer");
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return pgmg::set_err(PGMG_ERR_COMM, ncclGetErrorString(r));
+    std::memcpy(out128, &id, sizeof(id) < 128 ? sizeof(id) : 128);
+    return PGMG_OK;
 }
+
+int pgmg_loopback_create(int world, void **hub)
+{
+    if (!hub || world < 1 || world > 64) return pgmg::set_err(PGMG_ERR_ARG, "bad argument");
+    auto *h = new pgmg::LoopbackHub();
+    h->world = world;
+    *hub = h;
+    return PGMG_OK;
+}
+
+int pgmg_loopback_destroy(void *hub)
+{
+    delete (pgmg::LoopbackHub *)hub;
+    return PGMG_OK;
+}
+
+// Host-only: the finest-level row strip [lo, hi) of `rank` and the number of
+// strip-distributed levels for an N-point grid over `world` ranks (0 levels: too
+// small, every rank runs a replica).  Pure arithmetic, no GPU needed.
+int pgmg_plan_strips(int N, int world, int rank, int tail_n, int gather_n, int *lo, int *hi,
+                     int *dist_levels)
+{
+    if (world < 1 || rank < 0 || rank >= world || N < 5)
+        return pgmg::set_err(PGMG_ERR_ARG, "bad argument");
+    std::vector<int> Ns;
+    for (int n = N;; n = (n - 1) / 2 + 1) {
+        Ns.push_back(n);
+        if (n <= tail_n || n <= 5) break;
+    }
+    const int nb = (int)Ns.size() - 1;
+    const int gn = std::max(gather_n, Ns[nb]);
+    int Ld = 0;
+    if (world > 1)
+        for (int l = 0; l < nb; ++l) {
+            if (Ns[l] <= gn || (Ns[l] - 1) / world < pgmg::kMinRows) break;
+            Ld = l + 1;
+        }
+    if (Ld == 0) {
+        *lo = 0;
+        *hi = N;
+        *dist_levels = 0;
+        return PGMG_OK;
+    }
+    const int align = 1 << Ld, G = N - 1;
+    auto sp = [&](int r) {
+        return r == 0 ? 0 : (r == world ? N : (int)(((long long)r * G / world) / align * align));
+    };
+    *lo = sp(rank);
+    *hi = sp(rank + 1);
+    *dist_levels = Ld;
+    return PGMG_OK;
+}
+
+}  // extern "C"

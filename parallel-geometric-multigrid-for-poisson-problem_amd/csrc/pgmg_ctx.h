@@ -71,24 +71,35 @@ void free_grid(Grid &g);
 int enqueue_cycle(pgmg_ctx *c, int l, int gamma, bool x0_zero);
 int enqueue_tail(pgmg_ctx *c, int gamma, bool x0_from_global);
 
-// Row-strip domain decomposition over RCCL (one process per GPU).
+// Row-strip domain decomposition (one process per GPU, RCCL), pgmg_comm.hip.
+// Levels 0 .. gathered_level()-1 are split into row strips with halo exchange;
+// the first gathered level and everything below it run on rank 0 alone.
 class Comm {
   public:
     virtual ~Comm() {}
-    // decide ownership (lo/hi/u0/u1, on_this_rank, gathered) for every level
+    // ownership (lo/hi/u0/u1, on_this_rank, gathered) for every level, before allocation
     virtual int plan(pgmg_ctx *c) = 0;
-    // after allocation: communicators, staging buffers
+    // after allocation
     virtual int setup(pgmg_ctx *c) = 0;
-    // exchange `depth` halo rows of the level-l array whose origin is `o`
+    virtual int gathered_level() const = 0;
+    virtual int rank() const = 0;
+    // exchange `depth` halo rows of a strip-distributed level-l array (origin `o`)
     virtual int halo(double *o, const Level &L, int depth, hipStream_t s) = 0;
-    // early-exit decision with a global (all-rank) norm
-    virtual int fixup(const FixupArgs &f, hipStream_t s) = 0;
+    // in-place sum of one device double over all ranks
     virtual int allreduce_sum(double *d_scalar, hipStream_t s) = 0;
-    // level l is the first gathered level: move rc to rank 0, run the rest there,
-    // move e back
-    virtual int run_gathered(pgmg_ctx *c, int l, int gamma, bool x0_zero) = 0;
+    // the parent produced rc of gathered level l: move it to rank 0, run `repeats`
+    // cycles there, bring the correction back to every rank's strip
+    virtual int run_gathered(pgmg_ctx *c, int l, int gamma, int repeats) = 0;
     virtual int gather_solution(pgmg_ctx *c, double *phi_host) = 0;
     static Comm *create(pgmg_ctx *c, int *rc);
 };
 
+// true when level l is split across ranks (halos, global norms)
+inline bool is_dist(const pgmg_ctx *c, int l);
+
 }  // namespace pgmg
+
+inline bool pgmg::is_dist(const pgmg_ctx *c, int l)
+{
+    return c->comm != nullptr && l < c->comm->gathered_level();
+}

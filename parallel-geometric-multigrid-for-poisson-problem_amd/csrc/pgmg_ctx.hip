@@ -75,6 +75,7 @@ static double *const kZeroMarker = nullptr;
 
 static int timed_begin(pgmg_ctx *c, int slot);
 static int timed_end(pgmg_ctx *c, int slot, int idx);
+static int enqueue_children(pgmg_ctx *c, int l, int gamma);
 
 // one JacobiSmoother::smooth(x = L.A, f = L.F, num_iter = v) on a bulk level
 static int enqueue_smooth(pgmg_ctx *c, int l, int which, int v, bool x0_zero)
@@ -86,7 +87,7 @@ static int enqueue_smooth(pgmg_ctx *c, int l, int which, int v, bool x0_zero)
     for (int k = 1; k <= S; ++k) {
         double *in = (k & 1) ? L.A.o : L.B.o;
         double *out = (k & 1) ? L.B.o : L.A.o;
-        if (c->comm && !(k == 1 && x0_zero)) {
+        if (is_dist(c, l) && !(k == 1 && x0_zero)) {
             int e = c->comm->halo(in, L, 1, c->s);
             if (e) return e;
         }
@@ -124,12 +125,14 @@ static int enqueue_smooth(pgmg_ctx *c, int l, int which, int v, bool x0_zero)
             f.P = L.P;
             f.row0 = L.u0;
             f.row1 = L.u1;
-            if (c->comm) {
-                int e = c->comm->fixup(f, c->s);
+            f.global_sum = nullptr;
+            if (is_dist(c, l)) {
+                launch_sum_partials(c->partials, np, c->scalar, c->s);
+                int e = c->comm->allreduce_sum(c->scalar, c->s);
                 if (e) return e;
-            } else {
-                launch_fixup(f, c->s);
+                f.global_sum = c->scalar;
             }
+            launch_fixup(f, c->s);
         }
     }
     if (S & 1) launch_copy_rows(L.B.o, L.A.o, L.N, L.P, L.u0, L.u1, c->s);
@@ -173,11 +176,38 @@ static int timed_end(pgmg_ctx *c, int slot, int idx)
     return PGMG_OK;
 }
 
+// children of level l: gamma cycles on level l+1 (on rank 0 alone if it is gathered)
+static int enqueue_children(pgmg_ctx *c, int l, int gamma)
+{
+    if (c->comm && l + 1 == c->comm->gathered_level())
+        return c->comm->run_gathered(c, l + 1, gamma, gamma);
+    for (int i = 0; i < gamma; ++i) {
+        int e = enqueue_cycle(c, l + 1, gamma, i == 0);
+        if (e) return e;
+    }
+    return PGMG_OK;
+}
+
+// global early-exit sum for a distributed level: local partial sum, then all ranks
+static int global_sum(pgmg_ctx *c, int np, const double **out)
+{
+    launch_sum_partials(c->partials, np, c->scalar, c->s);
+    int e = c->comm->allreduce_sum(c->scalar, c->s);
+    *out = c->scalar;
+    return e;
+}
+
 // fused level (v1 = v2 = 1): k_pre (+fixup), children, k_post (+fixup)
 static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
 {
     Level &L = c->lv[l];
     Level &C = c->lv[l + 1];
+    const bool dist = is_dist(c, l);
+    int e;
+    if (dist) {
+        if (!x0_zero && (e = c->comm->halo(L.A.o, L, 4, c->s))) return e;
+        if (l > 0 && (e = c->comm->halo(L.F.o, L, 4, c->s))) return e;
+    }
     PreArgs pa{};
     pa.x0 = L.A.o;
     pa.f = L.F.o;
@@ -195,8 +225,9 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
     pa.jc1 = (L.hi < L.N ? L.hi : L.N - 1) / 2;
     pa.row_lo = L.u0;
     pa.row_hi = L.u1;
-    pa.rc_lo = C.u0;
-    pa.rc_hi = C.u1;
+    // coarse rows this rank restricts into (its strip's rows; the fix-up honours them too)
+    pa.rc_lo = pa.jc0 > 1 ? pa.jc0 : 1;
+    pa.rc_hi = pa.jc1 < C.N - 1 ? pa.jc1 : C.N - 1;
     FixArgsF fa{};
     fa.partials = c->partials;
     fa.np = fused_blocks(L.N, pa.jc0, pa.jc1);
@@ -205,12 +236,13 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
     const bool fine = (l == 0);
     int ev = fine ? timed_begin(c, 1) : -1;
     launch_pre(pa, x0_zero, fine, c->s);
-    int e = timed_end(c, 1, ev);
-    if (e) return e;
+    if ((e = timed_end(c, 1, ev))) return e;
+    if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
     launch_pre_fixup(fa, pa, x0_zero, c->s);
-    for (int i = 0; i < gamma; ++i) {
-        e = enqueue_cycle(c, l + 1, gamma, i == 0);
-        if (e) return e;
+    if ((e = enqueue_children(c, l, gamma))) return e;
+    if (dist) {
+        if ((e = c->comm->halo(L.B.o, L, 2, c->s))) return e;
+        if (is_dist(c, l + 1) && (e = c->comm->halo(C.A.o, C, 2, c->s))) return e;
     }
     PostArgs po{};
     po.phi = L.B.o;
@@ -231,8 +263,9 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
     po.row_hi = L.u1;
     ev = fine ? timed_begin(c, 2) : -1;
     launch_post(po, fine, c->s);
-    e = timed_end(c, 2, ev);
-    if (e) return e;
+    if ((e = timed_end(c, 2, ev))) return e;
+    fa.global_sum = nullptr;
+    if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
     launch_post_fixup(fa, po, c->s);
     return PGMG_OK;
 }
@@ -240,21 +273,16 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
 // MultigridSolver::v_cycle / w_cycle (MultiGrid.hpp:57-136) on level l
 int pgmg::enqueue_cycle(pgmg_ctx *c, int l, int gamma, bool x0_zero)
 {
-    if (l == c->nb) {
-        if (c->comm) return c->comm->run_gathered(c, l, gamma, x0_zero);
-        return enqueue_tail(c, gamma, !x0_zero);
-    }
+    if (l == c->nb) return enqueue_tail(c, gamma, !x0_zero);
     if (c->fused) return enqueue_fused_level(c, l, gamma, x0_zero);
     Level &L = c->lv[l];
     Level &C = c->lv[l + 1];
-    int e = enqueue_smooth(c, l, 0, c->cfg.v1, x0_zero);
+    const bool dist = is_dist(c, l);
+    int e;
+    if (dist && l > 0 && (e = c->comm->halo(L.F.o, L, 1, c->s))) return e;
+    e = enqueue_smooth(c, l, 0, c->cfg.v1, x0_zero);
     if (e) return e;
-    if (c->comm) {
-        e = c->comm->halo(L.A.o, L, 2, c->s);
-        if (e) return e;
-        e = c->comm->halo(L.F.o, L, 1, c->s);
-        if (e) return e;
-    }
+    if (dist && (e = c->comm->halo(L.A.o, L, 2, c->s))) return e;
     ResRestrictArgs r{};
     r.x = L.A.o;
     r.f = L.F.o;
@@ -264,17 +292,12 @@ int pgmg::enqueue_cycle(pgmg_ctx *c, int l, int gamma, bool x0_zero)
     r.Pf = L.P;
     r.Wc = C.N;
     r.Pc = C.P;
-    r.jc0 = C.u0;
-    r.jc1 = C.u1;
+    // coarse rows jc whose centre fine row 2jc this rank owns
+    r.jc0 = L.lo / 2 > 1 ? L.lo / 2 : 1;
+    r.jc1 = (L.hi + 1) / 2 < C.N - 1 ? (L.hi + 1) / 2 : C.N - 1;
     launch_res_restrict(r, c->s);
-    for (int i = 0; i < gamma; ++i) {
-        e = enqueue_cycle(c, l + 1, gamma, i == 0);
-        if (e) return e;
-    }
-    if (c->comm) {
-        e = c->comm->halo(C.A.o, C, 1, c->s);
-        if (e) return e;
-    }
+    if ((e = enqueue_children(c, l, gamma))) return e;
+    if (dist && is_dist(c, l + 1) && (e = c->comm->halo(C.A.o, C, 2, c->s))) return e;
     ProlongArgs p{};
     p.c = C.A.o;
     p.fine = L.A.o;
@@ -403,6 +426,11 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
             return rc;
         }
         rc = c->comm->plan(c);
+        if (rc == 1) {  // grid too small to split: every rank runs an independent replica
+            delete c->comm;
+            c->comm = nullptr;
+            rc = PGMG_OK;
+        }
     }
 
     for (int l = 0; l < (int)c->lv.size() && rc == PGMG_OK; ++l) {
@@ -475,8 +503,9 @@ int pgmg_set_problem(pgmg_ctx *c, const double *phi0, const double *f)
     Level &L = c->lv[0];
     const int N = L.N;
     if (!L.on_this_rank) return set_err(PGMG_ERR_STATE, "level 0 not on this rank");
-    const int r0 = L.lo > 0 ? L.lo - 1 : 0;          // owned rows + one halo row each side
-    const int r1 = L.hi < N ? L.hi + 1 : N;
+    // owned rows + the halo rows the fused passes read (every rank has the full host arrays)
+    const int r0 = L.lo - kHalo > 0 ? L.lo - kHalo : 0;
+    const int r1 = L.hi + kHalo < N ? L.hi + kHalo : N;
     const size_t rows = (size_t)(r1 - r0);
     HIPC(hipStreamSynchronize(c->s));
     // phi (and its boundary copy in the ping-pong buffer B)

@@ -71,6 +71,7 @@ struct FixupArgs {
     double *dst;                // buffer the speculative sweep k wrote
     unsigned long long *stats;
     int W, P, row0, row1;       // region copied on trigger
+    const double *global_sum;   // all-rank sum of the partials (multi-GPU) or nullptr
 };
 
 // The whole V-cycle at and below a level with N <= 65, in LDS, one workgroup.

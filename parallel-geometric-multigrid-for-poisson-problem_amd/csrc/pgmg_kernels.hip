@@ -357,7 +357,10 @@ __global__ __launch_bounds__(kBlock) void k_fixup(FixupArgs a)
     double s = 0.0;
     for (int k = threadIdx.x; k < a.np; k += kBlock) s += a.partials[k];
     s = block_sum<kBlock>(s, red);
-    if (threadIdx.x == 0) trig = (sqrt(s) < a.eps) ? 1 : 0;
+    if (threadIdx.x == 0) {
+        const double tot = a.global_sum != nullptr ? *a.global_sum : s;
+        trig = (sqrt(tot) < a.eps) ? 1 : 0;
+    }
     __syncthreads();
     if (leader) {
         *a.done_next = trig ? 1u : 0u;
