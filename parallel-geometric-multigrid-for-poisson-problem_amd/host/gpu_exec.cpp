@@ -1,0 +1,49 @@
+// gpu_exec.cpp — the reference's `gpu_exec` entry (3_part_parallel/main.cu:5-50) on
+// MI355X: same default run (N = 33 ... 2049, 3 cycles, alpha = 3, V then W per N),
+// same stdout and OUTPUT_RESULT/timings_parallel_{v,w}_cycle.txt.
+//
+//   gpu_exec                       # the reference's default run
+//   gpu_exec --n 513,1025 --cycles 1 --alpha 3 [--ops]
+// --ops additionally runs the per-op timing study (plotTimeSequentialVsParallel).
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <sstream>
+#include <vector>
+
+#include "ParallelTestRunner.hpp"
+
+int main(int argc, char **argv)
+{
+    std::vector<int> N_list = {33, 65, 129, 257, 513, 1025, 2049};  // main.cu:3
+    std::vector<int> N_thread_list = {16, 32};                        // main.cu:4
+    int mg_max_iterations = 3;                                        // main.cu:17
+    int alpha = 3;                                                    // main.cu:15
+    bool ops = false;
+    for (int i = 1; i < argc; ++i) {
+        if (!std::strcmp(argv[i], "--n") && i + 1 < argc) {
+            N_list.clear();
+            std::stringstream ss(argv[++i]);
+            std::string tok;
+            while (std::getline(ss, tok, ',')) N_list.push_back(std::atoi(tok.c_str()));
+        } else if (!std::strcmp(argv[i], "--cycles") && i + 1 < argc) {
+            mg_max_iterations = std::atoi(argv[++i]);
+        } else if (!std::strcmp(argv[i], "--alpha") && i + 1 < argc) {
+            alpha = std::atoi(argv[++i]);
+        } else if (!std::strcmp(argv[i], "--ops")) {
+            ops = true;
+        } else {
+            std::cerr << "usage: " << argv[0] << " [--n 33,65,...] [--cycles K] [--alpha A] [--ops]\n";
+            return 2;
+        }
+    }
+    try {
+        ParallelTestRunner parallel_runner(0, mg_max_iterations, alpha);
+        if (ops) parallel_runner.plotTimeSequentialVsParallel(N_list, N_thread_list);
+        parallel_runner.run_all_cycles(N_list);
+    } catch (const std::exception &e) {
+        std::cerr << "gpu_exec: " << e.what() << "\n";
+        return 1;
+    }
+    return 0;
+}
