@@ -67,6 +67,8 @@ extern "C" {
                                     pass (see pgmg_fine_pass_time)                  */
 #define PGMG_FLAG_UNFUSED 4u     /* one kernel per smoother sweep even when v1 = v2 = 1
                                     (the general path; same results)                */
+#define PGMG_FLAG_NO_CROSS 16u   /* do not fuse the finest level's post-smooth with the
+                                    next cycle's pre-smooth (same results)           */
 #define PGMG_FLAG_LOOPBACK 8u    /* world > 1 with ranks as threads of one process on
                                     one GPU: nccl_unique_id is a pgmg_loopback hub
                                     (test transport for the strip decomposition)    */
@@ -119,6 +121,10 @@ int pgmg_residual_norm(pgmg_ctx *ctx, double *out);
  * (comparable with the oracle's counters). */
 int pgmg_stats(pgmg_ctx *ctx, long long *sweeps, long long *early_exits);
 
+/* [0] sweeps, [1] early exits, [2] k_postpre post-check rare paths taken (-1 when
+ * cross-cycle fusion is off), [3] k_postpre pre-check rare paths taken. */
+int pgmg_stats_detail(pgmg_ctx *ctx, long long *out4);
+
 /* Device time of the last pgmg_vcycle/wcycle call in ms (hipEvents on the
  * context stream; synchronous). */
 int pgmg_last_elapsed_ms(pgmg_ctx *ctx, double *ms);
@@ -136,7 +142,7 @@ int pgmg_phi_device(pgmg_ctx *ctx, double **ptr, int *pitch, int *row0, int *row
 /* Count and mean device duration (ms) of the finest-level kernels launched since
  * the last call (needs PGMG_FLAG_TIME_FINE; synchronous).  pass 0: plain Jacobi
  * sweep (unfused path), 1: fused pre-smooth+residual+restriction (k_pre),
- * 2: fused prolongation+post-smooth (k_post). */
+ * 2: fused prolongation+post-smooth (k_post), 3: cross-cycle k_postpre. */
 int pgmg_fine_pass_time(pgmg_ctx *ctx, int pass, int *count, double *mean_ms);
 int pgmg_fine_sweep_time(pgmg_ctx *ctx, int *count, double *mean_ms);  /* pass 0 */
 

@@ -16,7 +16,8 @@ import subprocess
 
 import numpy as np
 
-from ._capi import (PGMG_FLAG_LOOPBACK, PGMG_FLAG_NO_GRAPH, PGMG_FLAG_TIME_FINE,
+from ._capi import (PGMG_FLAG_LOOPBACK, PGMG_FLAG_NO_CROSS, PGMG_FLAG_NO_GRAPH,
+                    PGMG_FLAG_TIME_FINE,
                     PGMG_FLAG_UNFUSED, PGMG_PROLONG_REFERENCE,
                     PGMG_PROLONG_SYMMETRIC, PgmgConfig, PgmgError, check, load)
 
@@ -24,7 +25,7 @@ PKG_DIR = pathlib.Path(__file__).resolve().parent
 
 __all__ = [
     "build", "load", "Solver", "PgmgConfig", "PgmgError", "ops",
-    "PGMG_FLAG_NO_GRAPH", "PGMG_FLAG_TIME_FINE", "PGMG_FLAG_UNFUSED", "PGMG_FLAG_LOOPBACK",
+    "PGMG_FLAG_NO_GRAPH", "PGMG_FLAG_TIME_FINE", "PGMG_FLAG_UNFUSED", "PGMG_FLAG_LOOPBACK", "PGMG_FLAG_NO_CROSS",
     "PGMG_PROLONG_REFERENCE", "plan_strips", "LoopbackHub", "unique_id",
     "PGMG_PROLONG_SYMMETRIC",
 ]
@@ -162,6 +163,13 @@ class Solver:
         s, e = C.c_longlong(), C.c_longlong()
         check(self.lib.pgmg_stats(self.h, C.byref(s), C.byref(e)), "pgmg_stats")
         return s.value, e.value
+
+    def stats_detail(self):
+        """[sweeps, early exits, k_postpre post-check rare paths (-1: not cross-fused),
+        k_postpre pre-check rare paths]"""
+        v = (C.c_longlong * 4)()
+        check(self.lib.pgmg_stats_detail(self.h, v), "pgmg_stats_detail")
+        return list(v)
 
     def last_elapsed_ms(self):
         v = C.c_double()

@@ -25,6 +25,7 @@ PGMG_FLAG_NO_GRAPH = 1
 PGMG_FLAG_TIME_FINE = 2
 PGMG_FLAG_UNFUSED = 4
 PGMG_FLAG_LOOPBACK = 8
+PGMG_FLAG_NO_CROSS = 16
 
 
 class PgmgConfig(C.Structure):
@@ -64,6 +65,7 @@ SIGNATURES = [
     ("pgmg_get_solution", C.c_int, [_P, _P]),
     ("pgmg_residual_norm", C.c_int, [_P, _DP]),
     ("pgmg_stats", C.c_int, [_P, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]),
+    ("pgmg_stats_detail", C.c_int, [_P, C.POINTER(C.c_longlong)]),
     ("pgmg_last_elapsed_ms", C.c_int, [_P, _DP]),
     ("pgmg_levels", C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("pgmg_vcycle_bytes", C.c_int, [_P, _DP]),

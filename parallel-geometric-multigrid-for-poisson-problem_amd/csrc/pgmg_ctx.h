@@ -59,8 +59,12 @@ struct pgmg_ctx {
         int used = 0;
     };
     // finest-level kernel timing (PGMG_FLAG_TIME_FINE): 0 plain sweep, 1 k_pre, 2 k_post
-    EventPool tpool[3];
+    EventPool tpool[4];           // 3: k_postpre
     bool fused = false;           // v1 = v2 = 1: two fused passes per level
+    bool cross = false;           // finest level fuses post(k) with pre(k+1) across cycles
+    pgmg::Grid S;                 // finest-level scratch for k_postpre's rare paths
+    double *partials2 = nullptr;  // second partials buffer (k_postpre's pre check)
+    unsigned *ppflags = nullptr;  // k_postpre_decide flags
     pgmg::Comm *comm = nullptr;   // non-null when world > 1
 };
 

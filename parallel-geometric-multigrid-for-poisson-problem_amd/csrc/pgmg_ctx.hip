@@ -20,8 +20,10 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "pgmg_ctx.h"
@@ -270,6 +272,148 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
     return PGMG_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Cross-cycle fusion of the finest level (single GPU, v1 = v2 = 1): for n
+// consecutive cycles the finest level runs k_pre, (children, k_postpre) x (n-1),
+// children, k_post.  k_postpre reads the pre-smoothed solution of cycle k from one
+// level-0 buffer and writes that of cycle k+1 into the other, so the buffers
+// alternate; at the end the solution is moved back under L.A by swapping the
+// host pointers (B always mirrors A's boundary, so either may play either role).
+// ---------------------------------------------------------------------------
+static PreArgs make_pre(pgmg_ctx *c, const double *x0, double *x2)
+{
+    Level &L = c->lv[0], &C = c->lv[1];
+    PreArgs pa{};
+    pa.x0 = x0;
+    pa.f = L.F.o;
+    pa.x2 = x2;
+    pa.rc = C.F.o;
+    pa.partials = c->partials;
+    pa.stats = c->stats;
+    pa.hh = L.hh;
+    pa.ih = L.ih;
+    pa.N = L.N;
+    pa.P = L.P;
+    pa.Nc = C.N;
+    pa.Pc = C.P;
+    pa.jc0 = 0;
+    pa.jc1 = (L.N - 1) / 2;
+    pa.row_lo = 1;
+    pa.row_hi = L.N - 1;
+    pa.rc_lo = 1;
+    pa.rc_hi = C.N - 1;
+    return pa;
+}
+
+static PostArgs make_post(pgmg_ctx *c, const double *phi, double *x2)
+{
+    Level &L = c->lv[0], &C = c->lv[1];
+    PostArgs po{};
+    po.phi = phi;
+    po.ec = C.A.o;
+    po.f = L.F.o;
+    po.x2 = x2;
+    po.partials = c->partials;
+    po.stats = c->stats;
+    po.hh = L.hh;
+    po.ih = L.ih;
+    po.N = L.N;
+    po.P = L.P;
+    po.Nc = C.N;
+    po.Pc = C.P;
+    po.jc0 = 0;
+    po.jc1 = (L.N - 1) / 2;
+    po.row_lo = 1;
+    po.row_hi = L.N - 1;
+    return po;
+}
+
+static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
+{
+    Level &L = c->lv[0], &C = c->lv[1];
+    double *A = L.A.o, *B = L.B.o;
+    const int np = fused_blocks(L.N, 0, (L.N - 1) / 2);
+    FixArgsF fa{};
+    fa.partials = c->partials;
+    fa.np = np;
+    fa.eps = c->cfg.eps;
+    fa.stats = c->stats;
+    int e;
+    // cycle 1: pre-smooth (+ residual, restriction) A -> B
+    PreArgs pa = make_pre(c, A, B);
+    int ev = timed_begin(c, 1);
+    launch_pre(pa, false, true, c->s);
+    if ((e = timed_end(c, 1, ev))) return e;
+    launch_pre_fixup(fa, pa, false, c->s);
+    double *pr = B;  // pre-smoothed solution of the current cycle
+    if ((e = enqueue_children(c, 0, gamma))) return e;
+    for (int k = 1; k < n; ++k) {
+        double *nx = (pr == A) ? B : A;
+        PostPreArgs q{};
+        q.phi = pr;
+        q.ec = C.A.o;
+        q.f = L.F.o;
+        q.x4 = nx;
+        q.rc = C.F.o;
+        q.partials1 = c->partials;
+        q.partials2 = c->partials2;
+        q.stats = c->stats;
+        q.hh = L.hh;
+        q.ih = L.ih;
+        q.N = L.N;
+        q.P = L.P;
+        q.Nc = C.N;
+        q.Pc = C.P;
+        q.jc0 = 0;
+        q.jc1 = (L.N - 1) / 2;
+        q.row_lo = 1;
+        q.row_hi = L.N - 1;
+        q.rc_lo = 1;
+        q.rc_hi = C.N - 1;
+        ev = timed_begin(c, 3);
+        launch_postpre(q, c->s);
+        if ((e = timed_end(c, 3, ev))) return e;
+        launch_postpre_decide(q, postpre_blocks(L.N, 0, (L.N - 1) / 2), c->cfg.eps, c->ppflags, c->s);
+        // rare path 1 (post check fired): S = x1 of the post-smooth, then a full
+        // pre-smooth from S (conditional k_pre + its own fix-up)
+        PostArgs po = make_post(c, pr, c->S.o);
+        FixArgsF f1 = fa;
+        f1.cond = &c->ppflags[0];
+        f1.force = 1;
+        f1.stats = nullptr;
+        launch_post_fixup(f1, po, c->s);
+        PreArgs p1 = make_pre(c, c->S.o, nx);
+        p1.cond = &c->ppflags[0];
+        launch_pre(p1, false, false, c->s);
+        FixArgsF f1b = fa;
+        f1b.cond = &c->ppflags[0];
+        launch_pre_fixup(f1b, p1, false, c->s);
+        // rare path 2 (only the pre check fired): S = x2 of the post-smooth, then the
+        // pre-smooth result is J(S) and rc = R r(J(S))
+        PostArgs p2 = make_post(c, pr, c->S.o);
+        p2.cond = &c->ppflags[1];
+        p2.stats = nullptr;
+        launch_post(p2, false, c->s);
+        PreArgs p3 = make_pre(c, c->S.o, nx);
+        FixArgsF f2 = fa;
+        f2.cond = &c->ppflags[1];
+        f2.force = 1;
+        f2.stats = nullptr;
+        launch_pre_fixup(f2, p3, false, c->s);
+        pr = nx;
+        if ((e = enqueue_children(c, 0, gamma))) return e;
+    }
+    // last cycle: post-smooth
+    double *out = (pr == A) ? B : A;
+    PostArgs po = make_post(c, pr, out);
+    ev = timed_begin(c, 2);
+    launch_post(po, true, c->s);
+    if ((e = timed_end(c, 2, ev))) return e;
+    launch_post_fixup(fa, po, c->s);
+    if (out != A) std::swap(L.A, L.B);
+    return PGMG_OK;
+}
+
 // MultigridSolver::v_cycle / w_cycle (MultiGrid.hpp:57-136) on level l
 int pgmg::enqueue_cycle(pgmg_ctx *c, int l, int gamma, bool x0_zero)
 {
@@ -361,6 +505,9 @@ int pgmg_destroy(pgmg_ctx *c)
         free_grid(L.F);
     }
     if (c->partials) (void)hipFree(c->partials);
+    if (c->partials2) (void)hipFree(c->partials2);
+    if (c->ppflags) (void)hipFree(c->ppflags);
+    free_grid(c->S);
     if (c->flags) (void)hipFree(c->flags);
     if (c->stats) (void)hipFree(c->stats);
     if (c->scalar) (void)hipFree(c->scalar);
@@ -441,6 +588,12 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         if (rc == PGMG_OK && l < c->nb) rc = alloc_grid(L.B, L);
     }
     c->fused = cfg->v1 == 1 && cfg->v2 == 1 && !(cfg->flags & PGMG_FLAG_UNFUSED);
+    {
+        const char *ev = getenv("PGMG_CROSS_MIN_N");
+        const int cross_min = (ev && *ev) ? atoi(ev) : 2049;
+        c->cross = c->fused && c->comm == nullptr && c->nb >= 1 && c->lv[0].N >= cross_min &&
+                   !(cfg->flags & PGMG_FLAG_NO_CROSS);
+    }
     int maxblocks = 256;
     for (int l = 0; l < c->nb; ++l) {
         int rpb, gx, gy;
@@ -449,6 +602,14 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         if (nbk > maxblocks) maxblocks = nbk;
         nbk = fused_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2);
         if (nbk > maxblocks) maxblocks = nbk;
+        nbk = postpre_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2);
+        if (nbk > maxblocks) maxblocks = nbk;
+    }
+    if (rc == PGMG_OK && c->cross) {
+        rc = alloc_grid(c->S, c->lv[0]);
+        if (rc == PGMG_OK && (hipMalloc((void **)&c->partials2, sizeof(double) * maxblocks) != hipSuccess ||
+                              hipMalloc((void **)&c->ppflags, 4 * sizeof(unsigned)) != hipSuccess))
+            rc = set_err(PGMG_ERR_NOMEM, "cross-cycle buffers");
     }
     c->partials_cap = maxblocks;
     if (rc == PGMG_OK && hipMalloc((void **)&c->partials, sizeof(double) * maxblocks) != hipSuccess)
@@ -547,7 +708,8 @@ static int run_cycles(pgmg_ctx *c, int ncycles, int gamma)
     if (ncycles <= 0) return PGMG_OK;
     HIPC(hipEventRecord(c->ev0, c->s));
     const bool use_graph = gamma == 1 && !(c->cfg.flags & PGMG_FLAG_NO_GRAPH) &&
-                           !(c->cfg.flags & PGMG_FLAG_TIME_FINE) && c->comm == nullptr;
+                           !(c->cfg.flags & PGMG_FLAG_TIME_FINE) && c->comm == nullptr &&
+                           !c->cross;
     if (use_graph && !c->gexec) {
         // first cycle eagerly (sets kernel attributes), the rest from a captured graph
         int e = enqueue_cycle(c, 0, 1, false);
@@ -562,6 +724,13 @@ static int run_cycles(pgmg_ctx *c, int ncycles, int gamma)
         if (ce != hipSuccess) return set_err(PGMG_ERR_HIP, std::string("capture: ") + hipGetErrorString(ce));
         HIPC(hipGraphInstantiate(&c->gexec, g, nullptr, nullptr, 0));
         HIPC(hipGraphDestroy(g));
+    }
+    if (c->cross && !use_graph) {
+        int e = enqueue_cross_cycles(c, ncycles, gamma);
+        if (e) return e;
+        HIPC(hipGetLastError());
+        HIPC(hipEventRecord(c->ev1, c->s));
+        return PGMG_OK;
     }
     for (int k = 0; k < ncycles; ++k) {
         if (use_graph) {
@@ -647,6 +816,17 @@ int pgmg_stats(pgmg_ctx *c, long long *sweeps, long long *exits)
     return PGMG_OK;
 }
 
+int pgmg_stats_detail(pgmg_ctx *c, long long *out4)
+{
+    if (!c || !out4) return set_err(PGMG_ERR_ARG, "null argument");
+    unsigned long long h[4];
+    HIPC(hipStreamSynchronize(c->s));
+    HIPC(hipMemcpy(h, c->stats, sizeof(h), hipMemcpyDeviceToHost));
+    for (int i = 0; i < 4; ++i) out4[i] = (long long)h[i];
+    out4[2] = c->cross ? out4[2] : -1;
+    return PGMG_OK;
+}
+
 int pgmg_levels(pgmg_ctx *c, int *bulk, int *tail_top)
 {
     if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
@@ -666,6 +846,10 @@ int pgmg_vcycle_bytes(pgmg_ctx *c, double *bytes)
         const double n = (double)(L.u1 - L.u0) * (L.N - 2);
         const double nc = (double)(C.u1 - C.u0) * (C.N - 2);
         if (c->fused) {
+            if (l == 0 && c->cross) {                     // steady state: one k_postpre
+                b += 24.0 * n + 16.0 * nc;                // phi, f, ec in; x4, rc out
+                continue;
+            }
             b += (l == 0 ? 24.0 : 16.0) * n + 8.0 * nc;  // k_pre: x0, f in; x2, rc out
             b += 24.0 * n + 8.0 * nc;                     // k_post: phi, f, ec in; x2 out
             continue;
@@ -729,7 +913,7 @@ int pgmg_bench_sweep(pgmg_ctx *c, int reps, double *ms)
 
 int pgmg_fine_pass_time(pgmg_ctx *c, int pass, int *count, double *mean_ms)
 {
-    if (!c || pass < 0 || pass > 2) return set_err(PGMG_ERR_ARG, "bad argument");
+    if (!c || pass < 0 || pass > 3) return set_err(PGMG_ERR_ARG, "bad argument");
     HIPC(hipStreamSynchronize(c->s));
     auto &pool = c->tpool[pass];
     double tot = 0.0;

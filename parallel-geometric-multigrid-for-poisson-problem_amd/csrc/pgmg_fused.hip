@@ -84,17 +84,22 @@ __device__ __forceinline__ double2 rstage(double2 up, double2 ce, double2 dn, do
 
 __device__ __forceinline__ bool boundary_row(int row, int N) { return row <= 0 || row >= N - 1; }
 
-__device__ __forceinline__ Cols lane_cols(int N)
+// Wave tile: STRIDE owned columns, loaded window starts MARGIN columns to the left;
+// lanes [MARGIN/2, 63 - (64*2 - STRIDE - MARGIN)/2] own their pair.
+template <int STRIDE, int MARGIN>
+__device__ __forceinline__ Cols lane_cols_t(int N)
 {
     const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     Cols k;
-    k.c = 120 * wave - 3 + 2 * lane;
+    k.c = STRIDE * wave + 1 - MARGIN + 2 * lane;
     k.bx = k.c <= 0 || k.c >= N - 1;
     k.by = k.c + 1 <= 0 || k.c + 1 >= N - 1;
-    k.own = lane >= 2 && lane <= 61 && k.c <= N - 2;
+    k.own = lane >= MARGIN / 2 && lane < MARGIN / 2 + STRIDE / 2 && k.c <= N - 2;
     return k;
 }
+
+__device__ __forceinline__ Cols lane_cols(int N) { return lane_cols_t<120, 4>(N); }
 
 // deterministic sum over the block (fixed tree) -> thread 0
 __device__ __forceinline__ double fused_block_sum(double v, double *red)
@@ -117,6 +122,7 @@ __global__ __launch_bounds__(256) void k_pre(PreArgs a)
 {
     constexpr int R = 2 * PAIRS;  // rows loaded per iteration (and prefetched ahead)
     __shared__ double red[4];
+    if (a.cond != nullptr && *a.cond == 0u) return;  // conditional (rare-path) launch
     const Cols k = lane_cols(a.N);
     const int N = a.N;
     const long long P = a.P;
@@ -238,6 +244,7 @@ __global__ __launch_bounds__(256) void k_post(PostArgs a)
 {
     constexpr int R = 2 * PAIRS;
     __shared__ double red[4];
+    if (a.cond != nullptr && *a.cond == 0u) return;  // conditional (rare-path) launch
     const Cols k = lane_cols(a.N);
     const int N = a.N, Nc = a.Nc;
     const long long P = a.P, Pc = a.Pc;
@@ -324,6 +331,183 @@ __global__ __launch_bounds__(256) void k_post(PostArgs a)
 }
 
 // ---------------------------------------------------------------------------
+// k_postpre: the finest level between two consecutive cycles of one call.
+//   xe = phi + P ec -> x1 -> x2 (post-smooth of cycle k, never stored)
+//   -> x3 -> x4 (pre-smooth of cycle k+1, stored) -> r(x4) -> rc (cycle k+1)
+// Checks: ||r(x1)|| (post) and ||r(x3)|| (pre), both speculative (partials1/2).
+// Read phi, f, ec; write x4, rc: 24 B per fine point + 16 B per coarse point,
+// replacing k_post + k_pre (48 + 16).  Wave tile: 114 owned columns of 128
+// (validity shrinks 6 columns per side through 6 stencil levels + restriction).
+// Stage lags behind the loaded row i: xe i, x1 i-1, x2 i-2, x3 i-3, x4 i-4,
+// r(x4) i-5, rc when i-5 = 2jc+1.
+// ---------------------------------------------------------------------------
+constexpr int kPPStride = 114, kPPMargin = 6;
+
+template <int PAIRS>
+__global__ __launch_bounds__(256) void k_postpre(PostPreArgs a)
+{
+    constexpr int R = 2 * PAIRS;
+    __shared__ double red[4];
+    const Cols k = lane_cols_t<kPPStride, kPPMargin>(a.N);
+    const int N = a.N, Nc = a.Nc;
+    const long long P = a.P, Pc = a.Pc;
+    const int jcb = a.jc0 + blockIdx.y * a.rows_per_block;
+    const int jce = min(jcb + a.rows_per_block, a.jc1);
+    const int olo = max(2 * jcb, a.row_lo), ohi = min(2 * jce, a.row_hi);
+    const int clo = max(jcb, max(1, a.rc_lo)), chi = min(jce, min(N / 2, a.rc_hi));
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
+        atomicAdd(&a.stats[0], 4ull);
+    ProlongCols pc;
+    pc.ic = (k.c - 1) >> 1;
+    pc.vx = k.c >= 3 && k.c <= N - 2;
+    pc.vy = k.c + 1 >= 2 && k.c + 1 <= N - 3;
+    const double *__restrict__ X = a.phi + k.c;
+    const double *__restrict__ F = a.f + k.c;
+    const double *__restrict__ E = a.ec + pc.ic;
+    double *__restrict__ O = a.x4 + k.c;
+    const double hh = a.hh, ih = a.ih;
+    const double2 z = make_double2(0.0, 0.0);
+    // windows (two previous rows each) and f rows i-5 .. i-1
+    double2 e0 = z, e1 = z, b0 = z, b1 = z, c0 = z, c1 = z, g0 = z, g1 = z, h0 = z, h1 = z,
+            d0 = z, d1 = z;
+    double2 f1 = z, f2 = z, f3 = z, f4 = z, f5 = z;  // f[i-1], f[i-2], ..., f[i-5]
+    double acc1 = 0.0, acc2 = 0.0;
+    const int i_begin = 2 * jcb - 6;
+    const int i_end = i_begin + ((2 * (jce - jcb) + 11 + R - 1) / R) * R;
+    double2 np_[R], nf[R];
+    double ncr[PAIRS + 1];
+    #pragma unroll
+    for (int q = 0; q < R; ++q) {
+        np_[q] = ldg2(X + (i_begin + q) * P);
+        nf[q] = ldg2(F + (i_begin + q) * P);
+    }
+    #pragma unroll
+    for (int q = 0; q <= PAIRS; ++q) ncr[q] = E[(long long)((i_begin >> 1) + q) * Pc];
+    for (int i = i_begin; i < i_end; i += R) {
+        double2 cp[R], cf[R];
+        double cr[PAIRS + 1];
+        #pragma unroll
+        for (int q = 0; q < R; ++q) {
+            cp[q] = np_[q];
+            cf[q] = nf[q];
+        }
+        #pragma unroll
+        for (int q = 0; q <= PAIRS; ++q) cr[q] = ncr[q];
+        if (i + R < i_end) {
+            #pragma unroll
+            for (int q = 0; q < R; ++q) {
+                np_[q] = ldg2(X + (i + R + q) * P);
+                nf[q] = ldg2(F + (i + R + q) * P);
+            }
+            #pragma unroll
+            for (int q = 0; q <= PAIRS; ++q) ncr[q] = E[(long long)(((i + R) >> 1) + q) * Pc];
+        }
+        double crn[PAIRS + 1];
+        #pragma unroll
+        for (int q = 0; q <= PAIRS; ++q) crn[q] = dpp_next_f(cr[q]);
+        #pragma unroll
+        for (int s = 0; s < R; ++s) {
+            const int ii = i + s;
+            const int pq = s >> 1;
+            const double2 e2 = add_prolong(cp[s], ii, cr[pq], crn[pq], cr[pq + 1], crn[pq + 1], pc, Nc);
+            const double2 f0 = cf[s];  // f[ii]
+            // post-smooth sweep 1: x1 row ii-1
+            const double2 b2 = jstage(e0, e1, e2, f1, hh, k, boundary_row(ii - 1, N));
+            {   // post check: r(x1) on row ii-2
+                const double2 r1 = rstage(b0, b1, b2, f2, ih);
+                const int row = ii - 2;
+                if (row >= olo && row < ohi && k.own) {
+                    acc1 += r1.x * r1.x;
+                    if (!k.by) acc1 += r1.y * r1.y;
+                }
+            }
+            // post-smooth sweep 2: x2 row ii-2 (= phi of cycle k+1)
+            const double2 c2 = jstage(b0, b1, b2, f2, hh, k, boundary_row(ii - 2, N));
+            // pre-smooth sweep 1: x3 row ii-3
+            const double2 g2 = jstage(c0, c1, c2, f3, hh, k, boundary_row(ii - 3, N));
+            {   // pre check: r(x3) on row ii-4
+                const double2 r3 = rstage(g0, g1, g2, f4, ih);
+                const int row = ii - 4;
+                if (row >= olo && row < ohi && k.own) {
+                    acc2 += r3.x * r3.x;
+                    if (!k.by) acc2 += r3.y * r3.y;
+                }
+            }
+            // pre-smooth sweep 2: x4 row ii-4 (stored)
+            const double2 h2 = jstage(g0, g1, g2, f4, hh, k, boundary_row(ii - 4, N));
+            if (ii - 4 >= olo && ii - 4 < ohi && k.own) stg2(O + (ii - 4) * P, h2);
+            // r(x4) on row ii-5
+            const double2 d2 = rstage(h0, h1, h2, f5, ih);
+            // restriction: rows ii-7, ii-6, ii-5 = 2jc-1, 2jc, 2jc+1 when ii is even
+            if ((s & 1) == 0) {
+                const int jc = (ii - 6) >> 1;
+                const double m2 = dpp_next_f(d1.x);
+                const double u2 = dpp_next_f(d0.x);
+                const double w2 = dpp_next_f(d2.x);
+                const int ic = (k.c + 1) >> 1;
+                if (jc >= clo && jc < chi && k.own && ic <= Nc - 2) {
+                    const double v = 0.25 * d1.y + 0.125 * (m2 + d1.x + d2.y + d0.y) +
+                                     0.0625 * (d0.x + u2 + d2.x + w2);
+                    a.rc[(long long)jc * Pc + ic] = v;
+                }
+            }
+            e0 = e1; e1 = e2;
+            b0 = b1; b1 = b2;
+            c0 = c1; c1 = c2;
+            g0 = g1; g1 = g2;
+            h0 = h1; h1 = h2;
+            d0 = d1; d1 = d2;
+            f5 = f4; f4 = f3; f3 = f2; f2 = f1; f1 = f0;
+        }
+    }
+    const int slot = blockIdx.y * gridDim.x + blockIdx.x;
+    const double s1 = fused_block_sum(acc1, red);
+    __syncthreads();
+    const double s2 = fused_block_sum(acc2, red);
+    if (threadIdx.x == 0) {
+        a.partials1[slot] = s1;
+        a.partials2[slot] = s2;
+    }
+}
+
+// one block: both decisions, stats, flags for the conditional rare-path kernels
+__global__ __launch_bounds__(256) void k_postpre_decide(const double *p1, const double *p2, int np,
+                                                        double eps, unsigned *flags,
+                                                        unsigned long long *stats)
+{
+    __shared__ double red[4];
+    double s1 = 0.0, s2 = 0.0;
+    for (int k = threadIdx.x; k < np; k += blockDim.x) {
+        s1 += p1[k];
+        s2 += p2[k];
+    }
+    s1 = fused_block_sum(s1, red);
+    __syncthreads();
+    s2 = fused_block_sum(s2, red);
+    if (threadIdx.x == 0) {
+        const unsigned t1 = sqrt(s1) < eps ? 1u : 0u;
+        const unsigned t2 = (!t1 && sqrt(s2) < eps) ? 1u : 0u;
+        flags[0] = t1;
+        flags[1] = t2;
+        if (stats != nullptr) {
+            // t1: the post-smooth stopped after 1 sweep and the pre-smooth is redone from
+            //     x1 by the conditional k_pre (which counts its own sweeps): -1 - 2
+            // t2: the pre-smooth stopped after 1 sweep: -1
+            if (t1) {
+                atomicAdd(&stats[0], (unsigned long long)-3LL);
+                atomicAdd(&stats[1], 1ull);
+                atomicAdd(&stats[2], 1ull);
+            }
+            if (t2) {
+                atomicAdd(&stats[0], (unsigned long long)-1LL);
+                atomicAdd(&stats[1], 1ull);
+                atomicAdd(&stats[3], 1ull);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // launch geometry
 // ---------------------------------------------------------------------------
 // Launch geometry.  Blocks march down long row bands: the grid is sized to about
@@ -335,9 +519,10 @@ static int env_int(const char *name, int dflt)
     return (v && *v) ? atoi(v) : dflt;
 }
 
-static void fused_geometry(int N, int jc0, int jc1, int *threads, int *gx, int *gy, int *rpb)
+static void fused_geometry(int N, int jc0, int jc1, int *threads, int *gx, int *gy, int *rpb,
+                           int stride = 120)
 {
-    const int waves = (N - 2 + 119) / 120;
+    const int waves = (N - 2 + stride - 1) / stride;
     const int wpb = waves < 4 ? waves : 4;
     *threads = 64 * wpb;
     *gx = (waves + wpb - 1) / wpb;
@@ -398,6 +583,30 @@ void launch_post(const PostArgs &a0, bool fine, hipStream_t s)
     }
 }
 
+int postpre_blocks(int N, int jc0, int jc1)
+{
+    int t, gx, gy, r;
+    fused_geometry(N, jc0, jc1, &t, &gx, &gy, &r, kPPStride);
+    return gx * gy;
+}
+
+void launch_postpre(const PostPreArgs &a0, hipStream_t s)
+{
+    int t, gx, gy, r;
+    fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, kPPStride);
+    PostPreArgs a = a0;
+    a.rows_per_block = r;
+    const dim3 g(gx, gy), b(t);
+    if (env_int("PGMG_PP_PAIRS", 1) >= 2) k_postpre<2><<<g, b, 0, s>>>(a);
+    else k_postpre<1><<<g, b, 0, s>>>(a);
+}
+
+void launch_postpre_decide(const PostPreArgs &a, int np, double eps, unsigned *flags, hipStream_t s)
+{
+    k_postpre_decide<<<dim3(1), dim3(256), 0, s>>>(a.partials1, a.partials2, np, eps, flags,
+                                                  a.stats);
+}
+
 // ---------------------------------------------------------------------------
 // Fix-ups (rare path): the early-exit check after the first sweep fired.
 // Scalar grid-stride code recomputing the reference result from the inputs
@@ -405,6 +614,8 @@ void launch_post(const PostArgs &a0, bool fine, hipStream_t s)
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ bool fix_decide(const FixArgsF &a, double *red, int *trig)
 {
+    if (a.cond != nullptr && *a.cond == 0u) return false;  // uniform
+    if (a.force) return true;  // recompute requested by k_postpre_decide (stats done there)
     double s = 0.0;
     for (int k = threadIdx.x; k < a.np; k += blockDim.x) s += a.partials[k];
     s = fused_block_sum(s, red);

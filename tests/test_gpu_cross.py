@@ -1,0 +1,96 @@
+"""GPU: cross-cycle fusion of the finest level (k_postpre: post-smooth of cycle k and
+pre-smooth + residual + restriction of cycle k+1 in one pass) is bit-identical to the
+reference over multi-cycle calls, including both speculative early-exit rare paths.
+
+PGMG_CROSS_MIN_N lowers the grid size from which the finest level is cross-fused so
+small grids exercise it (default 2049)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import assert_bitwise
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def cross_everywhere():
+    old = os.environ.get("PGMG_CROSS_MIN_N")
+    os.environ["PGMG_CROSS_MIN_N"] = "9"
+    yield
+    if old is None:
+        os.environ.pop("PGMG_CROSS_MIN_N")
+    else:
+        os.environ["PGMG_CROSS_MIN_N"] = old
+
+
+def _golden(golden_cycles, kind, N, eps=1e-7):
+    return next(c for c in golden_cycles if c["kind"] == kind and c["N"] == N and c["eps"] == eps)
+
+
+@pytest.mark.parametrize("N,eps,tail_n", [(129, 1e-7, 65), (129, 1e-7, 9), (513, 1e-7, 65),
+                                          (33, 1e-7, 17), (129, 1e3, 65), (257, 1.0, 9),
+                                          (65, 0.0, 33), (257, 1e-7, 17)])
+def test_cross_multicycle_call_matches_golden(pgmg, oracle_mod, golden_cycles, cross_everywhere,
+                                              N, eps, tail_n):
+    case = _golden(golden_cycles, "V", N, eps)
+    with pgmg.Solver(N, eps=eps, tail_n=tail_n) as s:
+        assert s.stats_detail()[2] >= 0, "cross-cycle fusion not active"
+        s.set_problem()
+        k = len(case["cycles"])
+        s.vcycle(k)                     # ONE call: k_pre, (children, k_postpre) x k-1, k_post
+        phi = s.solution()
+        assert oracle_mod.fnv_hash(phi) == case["cycles"][-1]["hash"]
+        assert s.stats()[0] == case["cycles"][-1]["sweeps"]
+        # and the context continues correctly after the buffer rotation
+        if k >= 2:
+            s.set_problem()
+            s.vcycle(k - 1)
+            s.vcycle(1)
+            assert oracle_mod.fnv_hash(s.solution()) == case["cycles"][-1]["hash"]
+
+
+def test_cross_rare_paths_fire_and_match_oracle(pgmg, oracle_mod, cross_everywhere):
+    """Sweep eps on a random problem until both rare paths of k_postpre have fired."""
+    rng = np.random.default_rng(3)
+    N = 129
+    phi0 = rng.uniform(-1, 1, (N, N))
+    f = rng.uniform(-1, 1, (N, N)) * 1e-3
+    for a in (phi0, f):
+        a[0, :] = a[-1, :] = a[:, 0] = a[:, -1] = 0.0
+    seen = [0, 0]
+    for eps in [10 ** (k / 12.0) for k in range(96, -24, -1)]:
+        if seen[0] > 0 and seen[1] > 0:
+            break
+        o = oracle_mod.Oracle(eps=eps)
+        ref = phi0.copy()
+        for _ in range(6):
+            o.v_cycle(ref, f)
+        with pgmg.Solver(N, eps=eps, tail_n=17) as s:
+            s.set_problem(phi0, f)
+            s.vcycle(6)
+            assert_bitwise(s.solution(), ref, f"eps={eps}")
+            d = s.stats_detail()
+            assert d[0] == o.sweeps, (eps, d, o.sweeps)
+            seen[0] += d[2]
+            seen[1] += d[3]
+    assert seen[0] > 0 and seen[1] > 0, seen
+
+
+def test_cross_wcycle(pgmg, oracle_mod, golden_cycles, cross_everywhere):
+    case = _golden(golden_cycles, "W", 129)
+    with pgmg.Solver(129, tail_n=17) as s:
+        s.set_problem()
+        s.wcycle(3)
+        assert oracle_mod.fnv_hash(s.solution()) == case["cycles"][-1]["hash"]
+
+
+def test_cross_default_threshold_large_grid(pgmg, oracle_mod, golden_cycles):
+    case = _golden(golden_cycles, "V", 4097)
+    with pgmg.Solver(4097) as s:
+        assert s.stats_detail()[2] >= 0
+        s.set_problem()
+        s.vcycle(3)
+        assert oracle_mod.fnv_hash(s.solution()) == case["cycles"][-1]["hash"]
+        assert s.stats()[0] == case["cycles"][-1]["sweeps"]
