@@ -66,6 +66,11 @@ struct pgmg_ctx {
     double *partials2 = nullptr;  // second partials buffer (k_postpre's pre check)
     unsigned *ppflags = nullptr;  // k_postpre_decide flags
     pgmg::Comm *comm = nullptr;   // non-null when world > 1
+    // F-cycle (pgmg_fcycle): analytic level-0 RHS of the FMG h chain, and the sine
+    // tables of every level (built on the first call)
+    pgmg::Grid Ffmg;
+    double *fmg_tab = nullptr;
+    std::vector<int> fmg_off;     // per level 0..nb then tail levels below nb: sx offset
 };
 
 namespace pgmg {

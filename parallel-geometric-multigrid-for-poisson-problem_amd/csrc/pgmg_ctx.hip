@@ -508,6 +508,8 @@ int pgmg_destroy(pgmg_ctx *c)
     if (c->partials2) (void)hipFree(c->partials2);
     if (c->ppflags) (void)hipFree(c->ppflags);
     free_grid(c->S);
+    free_grid(c->Ffmg);
+    if (c->fmg_tab) (void)hipFree(c->fmg_tab);
     if (c->flags) (void)hipFree(c->flags);
     if (c->stats) (void)hipFree(c->stats);
     if (c->scalar) (void)hipFree(c->scalar);
@@ -748,11 +750,138 @@ static int run_cycles(pgmg_ctx *c, int ncycles, int gamma)
 int pgmg_vcycle(pgmg_ctx *c, int ncycles) { return run_cycles(c, ncycles, 1); }
 int pgmg_wcycle(pgmg_ctx *c, int ncycles) { return run_cycles(c, ncycles, c ? c->cfg.alpha : 1); }
 
+// h of an N-point grid in the F-cycle's chain: 1/(n_coarse-1) halved once per level
+// (MultiGridTestRunner.hpp:195, MultiGrid.hpp:171) — differs from a/(N-1) when a != 1
+static double fmg_h(const pgmg_config &cfg, int N)
+{
+    double h = 1.0 / (cfg.n_coarse - 1);
+    for (int n = cfg.n_coarse; n < N; n = 2 * n - 1) h /= 2;
+    return h;
+}
+
+// sine tables of every level the F-cycle visits: bulk 0..nb-1, then the tail levels
+static int fmg_tables(pgmg_ctx *c)
+{
+    if (c->fmg_tab) return PGMG_OK;
+    std::vector<int> Ns;
+    for (int l = 0; l < c->nb; ++l) Ns.push_back(c->lv[l].N);
+    for (int N = c->lv[c->nb].N;; N = (N - 1) / 2 + 1) {
+        Ns.push_back(N);
+        if (N <= c->cfg.n_coarse) break;
+    }
+    std::vector<double> tab;
+    c->fmg_off.clear();
+    for (int N : Ns) {
+        std::vector<double> sx, sy;
+        double factor;
+        sine_tables(c->cfg, N, fmg_h(c->cfg, N), sx, sy, factor);
+        c->fmg_off.push_back((int)tab.size());
+        tab.insert(tab.end(), sx.begin(), sx.end());
+        tab.insert(tab.end(), sy.begin(), sy.end());
+    }
+    HIPC(hipMalloc((void **)&c->fmg_tab, tab.size() * sizeof(double)));
+    HIPC(hipMemcpy(c->fmg_tab, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice));
+    return PGMG_OK;
+}
+
+// One outer F-cycle (MultiGridTestRunner.hpp:192-205 -> MultigridSolver::f_cycle,
+// MultiGrid.hpp:138-183) on the current solution A_0:
+//   restrict phi to n_coarse (compute_coarsest_grid); then from the coarsest level up:
+//   smooth(3); phi_fine = 0 + P phi; f_fine = analytic RHS; one V-cycle on the finer level.
+// The levels at or below the tail's top run inside one k_tail launch; the bulk levels use
+// the V-cycle kernels with the level's F replaced by the analytic RHS of the FMG chain.
+static int enqueue_fcycle(pgmg_ctx *c)
+{
+    const int nb = c->nb;
+    double factor;
+    {
+        std::vector<double> sx, sy;
+        sine_tables(c->cfg, 1, 1.0, sx, sy, factor);
+    }
+    for (int l = 0; l < nb; ++l) {
+        const Level &L = c->lv[l], &C = c->lv[l + 1];
+        launch_restrict_values(L.A.o, L.N, L.P, C.A.o, C.N, C.P, c->s);
+    }
+    {
+        Level &T = c->lv[nb];
+        TailArgs t{};
+        t.f_top = T.F.o;
+        t.e_top = T.A.o;
+        t.P_top = T.P;
+        t.N_top = T.N;
+        t.h_top = T.h;
+        t.x0_from_global = 1;
+        t.v1 = c->cfg.v1;
+        t.v2 = c->cfg.v2;
+        t.coarse_iter = c->cfg.coarse_iter;
+        t.n_coarse = c->cfg.n_coarse;
+        t.eps = c->cfg.eps;
+        t.stats = c->stats;
+        t.fmg = 1;
+        t.fmg_smooth_top = nb > 0 ? 1 : 0;
+        t.fmg_tab = c->fmg_tab;
+        for (int k = 0; k < 8 && nb + k < (int)c->fmg_off.size(); ++k)
+            t.fmg_tab_off[k] = c->fmg_off[nb + k];
+        t.fmg_factor = factor;
+        HIPC(launch_tail_gamma(t, 1, c->s));
+    }
+    for (int l = nb - 1; l >= 0; --l) {
+        Level &L = c->lv[l];
+        const Level &C = c->lv[l + 1];
+        const double *sx = c->fmg_tab + c->fmg_off[l];
+        launch_rhs(L.F.o, sx, sx + L.N, factor, L.N, L.P, 0, L.N, c->s);
+        launch_fill_rows(L.A.o, L.P, 0, L.N, 0.0, c->s);
+        launch_fill_rows(L.B.o, L.P, 0, L.N, 0.0, c->s);
+        ProlongArgs p{};
+        p.c = C.A.o;
+        p.fine = L.A.o;
+        p.Wf = L.N;
+        p.Pf = L.P;
+        p.Wc = C.N;
+        p.Pc = C.P;
+        p.row0 = 2;
+        p.row1 = L.N - 1;
+        launch_prolong(p, c->s);
+        int e = enqueue_cycle(c, l, 1, false);
+        if (e) return e;
+        if (l > 0 && (e = enqueue_smooth(c, l, 0, 3, false))) return e;
+    }
+    return PGMG_OK;
+}
+
 int pgmg_fcycle(pgmg_ctx *c, int ncycles)
 {
-    (void)ncycles;
     if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
-    return set_err(PGMG_ERR_STATE, "F-cycle (FMG) not implemented yet");
+    if (!c->have_problem) return set_err(PGMG_ERR_STATE, "pgmg_set_problem first");
+    if (c->comm) return set_err(PGMG_ERR_STATE, "F-cycle runs on one GPU (world > 1: use replicas)");
+    if (ncycles <= 0) return PGMG_OK;
+    int e = fmg_tables(c);
+    if (e) return e;
+    Level &L0 = c->lv[0];
+    if (c->nb > 0 && !c->Ffmg.base && (e = alloc_grid(c->Ffmg, L0))) return e;
+    // the F-cycle's levels use the FMG h chain and (level 0) the analytic RHS of that chain
+    // (every level including the tail's top, whose h enqueue_tail passes on)
+    std::vector<Level> saved(c->lv);
+    for (int l = 0; l <= c->nb; ++l) {
+        Level &L = c->lv[l];
+        const double h = fmg_h(c->cfg, L.N);
+        L.h = h;
+        L.hh = h * h;
+        L.ih = 1.0 / (h * h);
+    }
+    if (c->nb > 0) std::swap(L0.F, c->Ffmg);
+    HIPC(hipEventRecord(c->ev0, c->s));
+    for (int k = 0; k < ncycles && !e; ++k) e = enqueue_fcycle(c);
+    if (c->nb > 0) std::swap(L0.F, c->Ffmg);
+    for (int l = 0; l <= c->nb; ++l) {
+        c->lv[l].h = saved[l].h;
+        c->lv[l].hh = saved[l].hh;
+        c->lv[l].ih = saved[l].ih;
+    }
+    if (e) return e;
+    HIPC(hipGetLastError());
+    HIPC(hipEventRecord(c->ev1, c->s));
+    return PGMG_OK;
 }
 
 int pgmg_sync(pgmg_ctx *c)

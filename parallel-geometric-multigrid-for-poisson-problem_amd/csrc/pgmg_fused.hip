@@ -144,12 +144,16 @@ __global__ __launch_bounds__(256) void k_pre(PreArgs a)
     // steps [i_begin, i_end): rows 2jcb-4 .. 2jce+3, rounded up to whole iterations
     // (the extra rows are computed but never stored; kHalo covers their loads)
     const int i_begin = 2 * jcb - 4;
-    const int i_end = i_begin + ((2 * (jce - jcb) + 8 + R - 1) / R) * R;
+    // a wave whose owned columns all lie past the grid (the last block's spare
+    // waves) streams nothing; it still joins the block reduction below
+    const bool idle = (k.c - 2 * (threadIdx.x & 63) + 4) > N - 2;
+    const int i_end = idle ? i_begin
+                           : i_begin + ((2 * (jce - jcb) + 8 + R - 1) / R) * R;
     double2 nx[R], nf[R];
     #pragma unroll
     for (int q = 0; q < R; ++q) {
-        nx[q] = X0_ZERO ? z : ldg2(X + (i_begin + q) * P);
-        nf[q] = ldg2(F + (i_begin + q) * P);
+        nx[q] = (X0_ZERO || idle) ? z : ldg2(X + (i_begin + q) * P);
+        nf[q] = idle ? z : ldg2(F + (i_begin + q) * P);
     }
     for (int i = i_begin; i < i_end; i += R) {
         double2 cx[R], cf[R];
@@ -267,18 +271,20 @@ __global__ __launch_bounds__(256) void k_post(PostArgs a)
     double2 a0 = z, a1 = z, b0 = z, b1 = z, f1 = z, f2 = z;
     double acc = 0.0;
     const int i_begin = 2 * jcb - 2;
-    const int i_end = i_begin + ((2 * (jce - jcb) + 4 + R - 1) / R) * R;
+    const bool idle = (k.c - 2 * (threadIdx.x & 63) + 4) > N - 2;  // spare wave
+    const int i_end = idle ? i_begin
+                           : i_begin + ((2 * (jce - jcb) + 4 + R - 1) / R) * R;
     // coarse row m = ii/2 of fine row ii; an iteration of R rows uses coarse rows
     // i/2 .. i/2 + PAIRS
     double2 np_[R], nf[R];
     double ncr[PAIRS + 1];
     #pragma unroll
     for (int q = 0; q < R; ++q) {
-        np_[q] = ldg2(X + (i_begin + q) * P);
-        nf[q] = ldg2(F + (i_begin + q) * P);
+        np_[q] = idle ? z : ldg2(X + (i_begin + q) * P);
+        nf[q] = idle ? z : ldg2(F + (i_begin + q) * P);
     }
     #pragma unroll
-    for (int q = 0; q <= PAIRS; ++q) ncr[q] = E[(long long)((i_begin >> 1) + q) * Pc];
+    for (int q = 0; q <= PAIRS; ++q) ncr[q] = idle ? 0.0 : E[(long long)((i_begin >> 1) + q) * Pc];
     for (int i = i_begin; i < i_end; i += R) {
         double2 cp[R], cf[R];
         double cr[PAIRS + 1];
@@ -373,16 +379,18 @@ __global__ __launch_bounds__(256) void k_postpre(PostPreArgs a)
     double2 f1 = z, f2 = z, f3 = z, f4 = z, f5 = z;  // f[i-1], f[i-2], ..., f[i-5]
     double acc1 = 0.0, acc2 = 0.0;
     const int i_begin = 2 * jcb - 6;
-    const int i_end = i_begin + ((2 * (jce - jcb) + 11 + R - 1) / R) * R;
+    const bool idle = (k.c - 2 * (threadIdx.x & 63) + kPPMargin) > N - 2;  // spare wave
+    const int i_end = idle ? i_begin
+                           : i_begin + ((2 * (jce - jcb) + 11 + R - 1) / R) * R;
     double2 np_[R], nf[R];
     double ncr[PAIRS + 1];
     #pragma unroll
     for (int q = 0; q < R; ++q) {
-        np_[q] = ldg2(X + (i_begin + q) * P);
-        nf[q] = ldg2(F + (i_begin + q) * P);
+        np_[q] = idle ? z : ldg2(X + (i_begin + q) * P);
+        nf[q] = idle ? z : ldg2(F + (i_begin + q) * P);
     }
     #pragma unroll
-    for (int q = 0; q <= PAIRS; ++q) ncr[q] = E[(long long)((i_begin >> 1) + q) * Pc];
+    for (int q = 0; q <= PAIRS; ++q) ncr[q] = idle ? 0.0 : E[(long long)((i_begin >> 1) + q) * Pc];
     for (int i = i_begin; i < i_end; i += R) {
         double2 cp[R], cf[R];
         double cr[PAIRS + 1];

@@ -85,6 +85,14 @@ struct TailArgs {
     int v1, v2, coarse_iter, n_coarse;
     double eps;
     unsigned long long *stats;
+    // F-cycle (full multigrid) mode, MultiGrid.hpp:138-183: e_top holds phi on entry;
+    // restrict it to the coarsest level, then climb with smooth(3) -> prolong into a
+    // zeroed finer grid -> analytic RHS -> V-cycle; result back into e_top.
+    int fmg;
+    int fmg_smooth_top;          // also run the smooth(3) on the top level (a finer level follows)
+    const double *fmg_tab;       // per tail level: sx[N], sy[N] sine tables (host libm)
+    int fmg_tab_off[8];          // offset of level t's sx in fmg_tab (sy follows)
+    double fmg_factor;           // (pi^2/a^2)(p^2+q^2)
 };
 
 // sweeps on the finest level use a distinct kernel symbol (kFine) so that
@@ -102,6 +110,10 @@ hipError_t launch_tail_gamma(const TailArgs &a, int gamma, hipStream_t s);
 size_t tail_lds_doubles(int N_top, int n_coarse);
 void launch_rhs(double *f, const double *sx, const double *sy, double factor, int W, int P,
                 int row0, int row1, hipStream_t s);
+// coarse = R fine on interior coarse points (values, not residuals): compute_coarsest_grid
+void launch_restrict_values(const double *fine, int Nf, int Pf, double *coarse, int Nc, int Pc,
+                            hipStream_t s);
+void launch_fill_rows(double *o, int P, int row0, int row1, double v, hipStream_t s);
 void launch_resnorm_partials(const double *x, const double *f, double *partials, double inv_hh,
                              int W, int P, int row0, int row1, int nblocks, hipStream_t s);
 void launch_sum_partials(const double *partials, int np, double *out, hipStream_t s);

@@ -430,6 +430,46 @@ void launch_rhs(double *f, const double *sx, const double *sy, double factor, in
                                                                   row0, row1);
 }
 
+// MultiGrid.hpp:187-205 applied to values (compute_coarsest_grid, MultiGrid.hpp:28-55)
+__global__ void k_restrict_values(const double *Fn, int Nf, long long Pf, double *C, int Nc,
+                                  long long Pc)
+{
+    const long long n = (long long)(Nc - 2) * (Nc - 2);
+    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n;
+         k += (long long)gridDim.x * blockDim.x) {
+        const long long jc = 1 + k / (Nc - 2), ic = 1 + k % (Nc - 2);
+        const long long q = (2 * jc) * Pf + 2 * ic;
+        C[jc * Pc + ic] = 0.25 * Fn[q] + 0.125 * (Fn[q + 1] + Fn[q - 1] + Fn[q + Pf] + Fn[q - Pf]) +
+                          0.0625 * (Fn[q - Pf - 1] + Fn[q - Pf + 1] + Fn[q + Pf - 1] + Fn[q + Pf + 1]);
+    }
+}
+
+void launch_restrict_values(const double *fine, int Nf, int Pf, double *coarse, int Nc, int Pc,
+                            hipStream_t s)
+{
+    long long nb = ((long long)(Nc - 2) * (Nc - 2) + 255) / 256;
+    if (nb > 4096) nb = 4096;
+    if (nb < 1) nb = 1;
+    k_restrict_values<<<dim3((unsigned)nb), dim3(256), 0, s>>>(fine, Nf, Pf, coarse, Nc, Pc);
+}
+
+__global__ void k_fill_rows(double *o, long long P, int row0, int row1, double v)
+{
+    const long long n = (long long)(row1 - row0) * P;
+    double *base = o + (long long)row0 * P;
+    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n;
+         k += (long long)gridDim.x * blockDim.x)
+        base[k] = v;
+}
+
+void launch_fill_rows(double *o, int P, int row0, int row1, double v, hipStream_t s)
+{
+    long long nb = ((long long)(row1 - row0) * P + 255) / 256;
+    if (nb > 8192) nb = 8192;
+    if (nb < 1) nb = 1;
+    k_fill_rows<<<dim3((unsigned)nb), dim3(256), 0, s>>>(o, P, row0, row1, v);
+}
+
 // sum r(x)^2 over rows [row0,row1), interior columns — reporting only
 __global__ __launch_bounds__(kBlock) void k_resnorm(const double *x, const double *f,
                                                     double *partials, double ih, int W,

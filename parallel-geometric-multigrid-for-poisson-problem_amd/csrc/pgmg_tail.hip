@@ -157,6 +157,77 @@ __device__ void tail_prolong(double *x, const TailLevel &Lf, const double *e, co
     __syncthreads();
 }
 
+// gamma-cycle (MultiGrid.hpp:57-136) whose top is tail level `top`; levels top.. last
+__device__ void tail_gcycle(const TailArgsDev &d, int top, double *E, double *F, double *T,
+                            double *red, long long &sweeps, long long &exits)
+{
+    const TailArgs &a = d.a;
+    int visits[kTailMaxLevels];
+    for (int i = 0; i < kTailMaxLevels; ++i) visits[i] = 0;
+    int l = top;
+    bool descending = true;
+    const int last = d.nl - 1;
+    for (;;) {
+        if (descending) {
+            if (l == last) {
+                tail_smooth(E + d.lv[l].off, F + d.lv[l].off, d.lv[l], a.coarse_iter, a.eps, T,
+                            red, sweeps, exits);
+                descending = false;
+            } else {
+                tail_smooth(E + d.lv[l].off, F + d.lv[l].off, d.lv[l], a.v1, a.eps, T, red,
+                            sweeps, exits);
+                tail_res_restrict(E + d.lv[l].off, F + d.lv[l].off, d.lv[l], F + d.lv[l + 1].off,
+                                  E + d.lv[l + 1].off, d.lv[l + 1], T);
+                visits[l + 1] = 0;
+                ++l;
+            }
+        } else {
+            if (l == top) break;
+            const int p = l - 1;
+            if (++visits[l] < d.gamma) {
+                descending = true;   // call the cycle on level l again
+            } else {
+                tail_prolong(E + d.lv[p].off, d.lv[p], E + d.lv[l].off, d.lv[l]);
+                tail_smooth(E + d.lv[p].off, F + d.lv[p].off, d.lv[p], a.v2, a.eps, T, red,
+                            sweeps, exits);
+                l = p;
+            }
+        }
+    }
+}
+
+// analytic right-hand side of tail level t from host sine tables (DynamicGridUtils.hpp:111-124)
+__device__ void tail_rhs(const TailArgsDev &d, int t, double *F)
+{
+    const int N = d.lv[t].N, n = N * N;
+    const double *sx = d.a.fmg_tab + d.a.fmg_tab_off[t];
+    const double *sy = sx + N;
+    for (int k = threadIdx.x; k < n; k += kTailThreads) {
+        const int j = k / N;
+        const int i = k - j * N;
+        F[k] = d.a.fmg_factor * sx[i] * sy[j];
+    }
+}
+
+// values restriction (compute_coarsest_grid) fine level t -> t+1, coarse boundary 0
+__device__ void tail_restrict_values(const double *x, const TailLevel &Lf, double *xc,
+                                     const TailLevel &Lc)
+{
+    const int N = Lf.N, Nc = Lc.N, nc = Nc * Nc;
+    for (int q = threadIdx.x; q < nc; q += kTailThreads) {
+        const int jc = q / Nc;
+        const int ic = q - jc * Nc;
+        if (ic == 0 || jc == 0 || ic == Nc - 1 || jc == Nc - 1) {
+            xc[q] = 0.0;
+            continue;
+        }
+        const int k = (2 * jc) * N + 2 * ic;
+        xc[q] = 0.25 * x[k] + 0.125 * (x[k + 1] + x[k - 1] + x[k + N] + x[k - N]) +
+                0.0625 * (x[k - N - 1] + x[k - N + 1] + x[k + N - 1] + x[k + N + 1]);
+    }
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(kTailThreads) void k_tail(TailArgsDev d)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -175,43 +246,35 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(TailArgsDev d)
         for (int k = threadIdx.x; k < n; k += kTailThreads) {
             const int j = k / N;
             const int i = k - j * N;
-            F[k] = a.f_top[j * P + i];
-            if (a.x0_from_global) E[k] = a.e_top[j * P + i];
+            if (!a.fmg) F[k] = a.f_top[j * P + i];
+            if (a.x0_from_global || a.fmg) E[k] = a.e_top[j * P + i];
         }
     }
     __syncthreads();
 
     long long sweeps = 0, exits = 0;
-    int visits[kTailMaxLevels];
-    for (int i = 0; i < kTailMaxLevels; ++i) visits[i] = 0;
-    int l = 0;
-    bool descending = true;
     const int last = d.nl - 1;
-    for (;;) {
-        if (descending) {
-            if (l == last) {
-                tail_smooth(E + d.lv[l].off, F + d.lv[l].off, d.lv[l], a.coarse_iter, a.eps, T,
-                            red, sweeps, exits);
-                descending = false;
+    if (!a.fmg) {
+        tail_gcycle(d, 0, E, F, T, red, sweeps, exits);
+    } else {
+        // compute_coarsest_grid: restrict phi down to the coarsest level
+        for (int t = 0; t < last; ++t)
+            tail_restrict_values(E + d.lv[t].off, d.lv[t], E + d.lv[t + 1].off, d.lv[t + 1]);
+        for (int t = last; t >= 0; --t) {
+            double *Et = E + d.lv[t].off;
+            double *Ft = F + d.lv[t].off;
+            tail_rhs(d, t, Ft);                      // f_fine = compute_rhs (MultiGrid.hpp:162)
+            if (t < last) {
+                const int n = d.lv[t].N * d.lv[t].N;
+                for (int k = threadIdx.x; k < n; k += kTailThreads) Et[k] = 0.0;
+                __syncthreads();
+                tail_prolong(Et, d.lv[t], E + d.lv[t + 1].off, d.lv[t + 1]);   // :164
+                tail_gcycle(d, t, E, F, T, red, sweeps, exits);              // :167 v_cycle
             } else {
-                tail_smooth(E + d.lv[l].off, F + d.lv[l].off, d.lv[l], a.v1, a.eps, T, red,
-                            sweeps, exits);
-                tail_res_restrict(E + d.lv[l].off, F + d.lv[l].off, d.lv[l], F + d.lv[l + 1].off,
-                                  E + d.lv[l + 1].off, d.lv[l + 1], T);
-                visits[l + 1] = 0;
-                ++l;
+                __syncthreads();
             }
-        } else {
-            if (l == 0) break;
-            const int p = l - 1;
-            if (++visits[l] < d.gamma) {
-                descending = true;   // call the cycle on level l again
-            } else {
-                tail_prolong(E + d.lv[p].off, d.lv[p], E + d.lv[l].off, d.lv[l]);
-                tail_smooth(E + d.lv[p].off, F + d.lv[p].off, d.lv[p], a.v2, a.eps, T, red,
-                            sweeps, exits);
-                l = p;
-            }
+            if (t > 0 || a.fmg_smooth_top)                                   // :153 smooth(3)
+                tail_smooth(Et, Ft, d.lv[t], 3, a.eps, T, red, sweeps, exits);
         }
     }
 

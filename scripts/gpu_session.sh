@@ -23,6 +23,7 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run tests 900 python -m pytest tests -m gpu -q -rf ;;
     strips) run strips 400 python -m pytest tests/test_gpu_strips.py -m gpu -q -rf -x ;;
+    fcycle) run fcycle 600 python -m pytest tests/test_gpu_fcycle.py -m gpu -q -rf ;;
     tests-fast) run tests 600 python -m pytest tests -m "gpu and not slow" -q -rf ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
     bench-graph) run bench_graph 600 python bench.py --steps 20 --warmup 3 --timing graph --cpu-baseline off ;;

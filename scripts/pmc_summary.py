@@ -53,9 +53,10 @@ def main(tag, N=16385):
             stats[norm_name(r["Name"])] = float(r["AverageNs"]) / 1e6
     kernels = []
     for k, v in sorted(vals.items()):
-        if "true" not in k or not (k.startswith("k_pre") or k.startswith("k_post") or
-                                   k.startswith("k_sweep")):
-            continue  # finest-level symbols only (FINE template argument)
+        finest = k.startswith("k_postpre<") or (k.endswith("true>") and (
+            k.startswith("k_pre<") or k.startswith("k_post<") or k.startswith("k_sweep<")))
+        if not finest:
+            continue  # finest-level symbols only (FINE template argument; k_postpre always)
         if not v.get("FETCH_SIZE") or not v.get("WRITE_SIZE"):
             continue
         fetch = sum(v["FETCH_SIZE"]) / len(v["FETCH_SIZE"])
