@@ -62,6 +62,7 @@ struct pgmg_ctx {
     EventPool tpool[4];           // 3: k_postpre
     bool fused = false;           // v1 = v2 = 1: two fused passes per level
     bool cross = false;           // finest level fuses post(k) with pre(k+1) across cycles
+    bool recompute = true;        // levels entered with x0 = 0 recompute x2 in k_post
     pgmg::Grid S;                 // finest-level scratch for k_postpre's rare paths
     double *partials2 = nullptr;  // second partials buffer (k_postpre's pre check)
     unsigned *ppflags = nullptr;  // k_postpre_decide flags

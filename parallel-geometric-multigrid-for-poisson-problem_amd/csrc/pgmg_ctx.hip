@@ -205,6 +205,10 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
     Level &L = c->lv[l];
     Level &C = c->lv[l + 1];
     const bool dist = is_dist(c, l);
+    // entered with x0 = 0: the pre-smoothed iterate is a function of f alone, so k_pre
+    // does not store it and k_post recomputes it (x1 = J(0) is pointwise)
+    const bool recomp = x0_zero && l > 0 && c->recompute;
+    unsigned *fired = smooth_flags(c, l, 0) + (kMaxSweeps - 1);
     int e;
     if (dist) {
         if (!x0_zero && (e = c->comm->halo(L.A.o, L, 4, c->s))) return e;
@@ -213,7 +217,8 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
     PreArgs pa{};
     pa.x0 = L.A.o;
     pa.f = L.F.o;
-    pa.x2 = L.B.o;
+    pa.x2 = recomp ? nullptr : L.B.o;
+    pa.fired = recomp ? fired : nullptr;
     pa.rc = C.F.o;
     pa.partials = c->partials;
     pa.stats = c->stats;
@@ -243,11 +248,12 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
     launch_pre_fixup(fa, pa, x0_zero, c->s);
     if ((e = enqueue_children(c, l, gamma))) return e;
     if (dist) {
-        if ((e = c->comm->halo(L.B.o, L, 2, c->s))) return e;
+        if (!recomp && (e = c->comm->halo(L.B.o, L, 2, c->s))) return e;
         if (is_dist(c, l + 1) && (e = c->comm->halo(C.A.o, C, 2, c->s))) return e;
     }
     PostArgs po{};
     po.phi = L.B.o;
+    po.pre_fired = recomp ? fired : nullptr;
     po.ec = C.A.o;
     po.f = L.F.o;
     po.x2 = L.A.o;
@@ -590,6 +596,10 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         if (rc == PGMG_OK && l < c->nb) rc = alloc_grid(L.B, L);
     }
     c->fused = cfg->v1 == 1 && cfg->v2 == 1 && !(cfg->flags & PGMG_FLAG_UNFUSED);
+    {
+        const char *ev = getenv("PGMG_RECOMPUTE");
+        c->recompute = !(ev && *ev == '0');
+    }
     {
         const char *ev = getenv("PGMG_CROSS_MIN_N");
         const int cross_min = (ev && *ev) ? atoi(ev) : 2049;
@@ -977,6 +987,11 @@ int pgmg_vcycle_bytes(pgmg_ctx *c, double *bytes)
         if (c->fused) {
             if (l == 0 && c->cross) {                     // steady state: one k_postpre
                 b += 24.0 * n + 16.0 * nc;                // phi, f, ec in; x4, rc out
+                continue;
+            }
+            if (l > 0 && c->recompute) {                  // x0 = 0, x2 recomputed
+                b += 8.0 * n + 8.0 * nc;                  // k_pre: f in; rc out
+                b += 16.0 * n + 8.0 * nc;                 // k_post: f, ec in; x2 out
                 continue;
             }
             b += (l == 0 ? 24.0 : 16.0) * n + 8.0 * nc;  // k_pre: x0, f in; x2, rc out

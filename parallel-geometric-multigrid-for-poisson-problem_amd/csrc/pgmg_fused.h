@@ -8,7 +8,8 @@ namespace pgmg {
 struct PreArgs {
     const double *x0;           // level solution before smoothing (unused when x0 is zero)
     const double *f;            // level right-hand side
-    double *x2;                 // result of the two sweeps (ping-pong buffer)
+    double *x2;                 // result of the two sweeps (ping-pong buffer); nullptr: not
+                                // stored (x0 = 0: k_post recomputes it from f)
     double *rc;                 // coarse right-hand side R r(x2)
     double *partials;           // per block sum r(x1)^2 (early-exit check)
     unsigned long long *stats;  // [0] sweeps (+2 per launch)
@@ -19,6 +20,7 @@ struct PreArgs {
     int rc_lo, rc_hi;           // coarse rows whose rc this rank writes
     int rows_per_block;
     const unsigned *cond;       // non-null: run only when *cond != 0
+    unsigned *fired;            // non-null: the fix-up records whether the check fired
 };
 
 // prolongation + post-smooth (2 sweeps) in one pass
@@ -35,6 +37,9 @@ struct PostArgs {
     int row_lo, row_hi;
     int rows_per_block;
     const unsigned *cond;
+    // non-null: phi is not read but recomputed from f as the pre-smoothed iterate of
+    // x0 = 0 (x1 = J(0), phi = *pre_fired ? x1 : J(x1)); PreArgs::fired of the same level
+    const unsigned *pre_fired;
 };
 
 // post-smooth of cycle k + pre-smooth/residual/restriction of cycle k+1 in one pass

@@ -134,6 +134,7 @@ __global__ __launch_bounds__(256) void k_pre(PreArgs a)
         atomicAdd(&a.stats[0], 2ull);
     const double *__restrict__ X = a.x0 + k.c;
     const double *__restrict__ F = a.f + k.c;
+    const bool store = a.x2 != nullptr;
     double *__restrict__ O = a.x2 + k.c;
     const double hh = a.hh, ih = a.ih;
     const double2 z = make_double2(0.0, 0.0);
@@ -186,7 +187,7 @@ __global__ __launch_bounds__(256) void k_pre(PreArgs a)
                 }
             }
             const double2 c2 = jstage(b0, b1, b2, f1, hh, k, boundary_row(ii - 2, N));
-            if (ii - 2 >= olo && ii - 2 < ohi && k.own) stg2(O + (ii - 2) * P, c2);
+            if (store && ii - 2 >= olo && ii - 2 < ohi && k.own) stg2(O + (ii - 2) * P, c2);
             // r(x2) on row ii-3 (garbage on boundary rows; never used there)
             const double2 d2 = rstage(c0, c1, c2, f0, ih);
             // restriction: rows ii-5, ii-4, ii-3 = 2jc-1, 2jc, 2jc+1 when ii is even
@@ -243,7 +244,10 @@ __device__ __forceinline__ double2 add_prolong(double2 p, int row, double ca, do
     return p;
 }
 
-template <bool FINE, int PAIRS>
+// RECOMP (levels entered with x0 = 0): phi is not read.  The loaded row is f[ii+1];
+// x1 = J(0) is pointwise, so x1 row ii+1 -> phi row ii = J(x1) (or x1 when the pre
+// check fired) -> x_eff row ii: one more row of lag than reading phi, 16 B/point less.
+template <bool FINE, int PAIRS, bool RECOMP>
 __global__ __launch_bounds__(256) void k_post(PostArgs a)
 {
     constexpr int R = 2 * PAIRS;
@@ -261,19 +265,29 @@ __global__ __launch_bounds__(256) void k_post(PostArgs a)
     pc.ic = (k.c - 1) >> 1;
     pc.vx = k.c >= 3 && k.c <= N - 2;
     pc.vy = k.c + 1 >= 2 && k.c + 1 <= N - 3;
-    const double *__restrict__ X = a.phi + k.c;
     const double *__restrict__ F = a.f + k.c;
+    // the streamed array: phi, or f one row ahead (RECOMP)
+    const double *__restrict__ X = RECOMP ? F + P : a.phi + k.c;
     const double *__restrict__ E = a.ec + pc.ic;
     double *__restrict__ O = a.x2 + k.c;
     const double hh = a.hh, ih = a.ih;
     const double2 z = make_double2(0.0, 0.0);
     // windows: x_eff rows i-2,i-1 ; x1 rows i-3,i-2 ; f rows i-2,i-1
     double2 a0 = z, a1 = z, b0 = z, b1 = z, f1 = z, f2 = z;
+    // RECOMP: pre-smooth x1 rows ii-1, ii ; f row ii
+    double2 g0 = z, g1 = z, fc = z;
     double acc = 0.0;
     const int i_begin = 2 * jcb - 2;
     const bool idle = (k.c - 2 * (threadIdx.x & 63) + 4) > N - 2;  // spare wave
     const int i_end = idle ? i_begin
                            : i_begin + ((2 * (jce - jcb) + 4 + R - 1) / R) * R;
+    const bool pfired = RECOMP && *a.pre_fired != 0u;
+    if (RECOMP && !idle) {
+        const double2 fm = ldg2(F + (i_begin - 1) * P);
+        fc = ldg2(F + i_begin * P);
+        g0 = jstage(z, z, z, fm, hh, k, boundary_row(i_begin - 1, N));
+        g1 = jstage(z, z, z, fc, hh, k, boundary_row(i_begin, N));
+    }
     // coarse row m = ii/2 of fine row ii; an iteration of R rows uses coarse rows
     // i/2 .. i/2 + PAIRS
     double2 np_[R], nf[R];
@@ -281,7 +295,7 @@ __global__ __launch_bounds__(256) void k_post(PostArgs a)
     #pragma unroll
     for (int q = 0; q < R; ++q) {
         np_[q] = idle ? z : ldg2(X + (i_begin + q) * P);
-        nf[q] = idle ? z : ldg2(F + (i_begin + q) * P);
+        if (!RECOMP) nf[q] = idle ? z : ldg2(F + (i_begin + q) * P);
     }
     #pragma unroll
     for (int q = 0; q <= PAIRS; ++q) ncr[q] = idle ? 0.0 : E[(long long)((i_begin >> 1) + q) * Pc];
@@ -291,7 +305,7 @@ __global__ __launch_bounds__(256) void k_post(PostArgs a)
         #pragma unroll
         for (int q = 0; q < R; ++q) {
             cp[q] = np_[q];
-            cf[q] = nf[q];
+            if (!RECOMP) cf[q] = nf[q];
         }
         #pragma unroll
         for (int q = 0; q <= PAIRS; ++q) cr[q] = ncr[q];
@@ -299,7 +313,7 @@ __global__ __launch_bounds__(256) void k_post(PostArgs a)
             #pragma unroll
             for (int q = 0; q < R; ++q) {
                 np_[q] = ldg2(X + (i + R + q) * P);
-                nf[q] = ldg2(F + (i + R + q) * P);
+                if (!RECOMP) nf[q] = ldg2(F + (i + R + q) * P);
             }
             #pragma unroll
             for (int q = 0; q <= PAIRS; ++q) ncr[q] = E[(long long)(((i + R) >> 1) + q) * Pc];
@@ -311,8 +325,20 @@ __global__ __launch_bounds__(256) void k_post(PostArgs a)
         for (int s = 0; s < R; ++s) {
             const int ii = i + s;
             const int pq = s >> 1;
-            const double2 a2 = add_prolong(cp[s], ii, cr[pq], crn[pq], cr[pq + 1], crn[pq + 1], pc, Nc);
-            const double2 f3 = cf[s];
+            double2 ph, f3;
+            if (RECOMP) {
+                const double2 fn = cp[s];  // f row ii+1
+                const double2 g2 = jstage(z, z, z, fn, hh, k, boundary_row(ii + 1, N));
+                ph = pfired ? g1 : jstage(g0, g1, g2, fc, hh, k, boundary_row(ii, N));
+                f3 = fc;
+                g0 = g1;
+                g1 = g2;
+                fc = fn;
+            } else {
+                ph = cp[s];
+                f3 = cf[s];
+            }
+            const double2 a2 = add_prolong(ph, ii, cr[pq], crn[pq], cr[pq + 1], crn[pq + 1], pc, Nc);
             const double2 b2 = jstage(a0, a1, a2, f2, hh, k, boundary_row(ii - 1, N));
             {
                 const int row = ii - 2;
@@ -582,12 +608,15 @@ void launch_post(const PostArgs &a0, bool fine, hipStream_t s)
     PostArgs a = a0;
     a.rows_per_block = r;
     const dim3 g(gx, gy), b(t);
+    const bool rec = a.pre_fired != nullptr;
     if (fused_pairs() == 2) {
-        if (fine) k_post<true, 2><<<g, b, 0, s>>>(a);
-        else k_post<false, 2><<<g, b, 0, s>>>(a);
+        if (fine) k_post<true, 2, false><<<g, b, 0, s>>>(a);
+        else if (rec) k_post<false, 2, true><<<g, b, 0, s>>>(a);
+        else k_post<false, 2, false><<<g, b, 0, s>>>(a);
     } else {
-        if (fine) k_post<true, 1><<<g, b, 0, s>>>(a);
-        else k_post<false, 1><<<g, b, 0, s>>>(a);
+        if (fine) k_post<true, 1, false><<<g, b, 0, s>>>(a);
+        else if (rec) k_post<false, 1, true><<<g, b, 0, s>>>(a);
+        else k_post<false, 1, false><<<g, b, 0, s>>>(a);
     }
 }
 
@@ -647,6 +676,7 @@ struct FixCtx {
     long long P, Pc;
     double hh, ih;
     bool x0_zero;
+    const unsigned *pre_fired;  // non-null: phi (x0 of fxeff) is recomputed from f
 };
 
 __device__ __forceinline__ double fx0(const FixCtx &c, int j, int i)
@@ -654,10 +684,25 @@ __device__ __forceinline__ double fx0(const FixCtx &c, int j, int i)
     return c.x0_zero ? 0.0 : c.x0[(long long)j * c.P + i];
 }
 
+template <bool POST>
+__device__ double fx1(const FixCtx &c, int j, int i);
+
+// pre-smoothed iterate of x0 = 0 (k_post RECOMP): x1 = J(0), phi = fired ? x1 : J(x1)
+__device__ double fphi0(const FixCtx &c, int j, int i)
+{
+    FixCtx z = c;
+    z.x0_zero = true;
+    z.pre_fired = nullptr;
+    if (*c.pre_fired != 0u || j <= 0 || i <= 0 || j >= c.N - 1 || i >= c.N - 1)
+        return fx1<false>(z, j, i);
+    return 0.25 * ((c.hh * c.f[(long long)j * c.P + i]) + fx1<false>(z, j, i - 1) +
+                   fx1<false>(z, j, i + 1) + fx1<false>(z, j - 1, i) + fx1<false>(z, j + 1, i));
+}
+
 // x_eff = phi + P ec at one fine point (MultiGrid.hpp:208-226)
 __device__ double fxeff(const FixCtx &c, int j, int i)
 {
-    double v = c.x0[(long long)j * c.P + i];
+    double v = c.pre_fired != nullptr ? fphi0(c, j, i) : c.x0[(long long)j * c.P + i];
     if (j < 2 || i < 2 || j > c.N - 2 || i > c.N - 2) return v;
     const int jc = j >> 1, ic = i >> 1;
     const double *C0 = c.ec + (long long)jc * c.Pc;
@@ -696,10 +741,12 @@ __global__ __launch_bounds__(256) void k_pre_fixup(FixArgsF a, PreArgs p, int x0
 {
     __shared__ double red[4];
     __shared__ int trig;
-    if (!fix_decide(a, red, &trig)) return;
-    FixCtx c{p.x0, p.f, nullptr, p.N, p.Nc, p.P, p.Pc, p.hh, p.ih, x0_zero != 0};
+    const bool t = fix_decide(a, red, &trig);
+    if (p.fired != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *p.fired = t ? 1u : 0u;
+    if (!t) return;
+    FixCtx c{p.x0, p.f, nullptr, p.N, p.Nc, p.P, p.Pc, p.hh, p.ih, x0_zero != 0, nullptr};
     const long long W = p.N - 2;
-    const long long nrows = (long long)(p.row_hi - p.row_lo);
+    const long long nrows = p.x2 != nullptr ? (long long)(p.row_hi - p.row_lo) : 0;
     const long long stride = (long long)gridDim.x * blockDim.x;
     for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < nrows * W; k += stride) {
         const int j = p.row_lo + (int)(k / W), i = 1 + (int)(k % W);
@@ -722,7 +769,7 @@ __global__ __launch_bounds__(256) void k_post_fixup(FixArgsF a, PostArgs p)
     __shared__ double red[4];
     __shared__ int trig;
     if (!fix_decide(a, red, &trig)) return;
-    FixCtx c{p.phi, p.f, p.ec, p.N, p.Nc, p.P, p.Pc, p.hh, p.ih, false};
+    FixCtx c{p.phi, p.f, p.ec, p.N, p.Nc, p.P, p.Pc, p.hh, p.ih, false, p.pre_fired};
     const long long W = p.N - 2;
     const long long nrows = (long long)(p.row_hi - p.row_lo);
     const long long stride = (long long)gridDim.x * blockDim.x;
