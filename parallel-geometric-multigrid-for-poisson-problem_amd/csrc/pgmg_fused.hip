@@ -375,12 +375,29 @@ __global__ __launch_bounds__(256) void k_post(PostArgs a)
 // ---------------------------------------------------------------------------
 constexpr int kPPStride = 114, kPPMargin = 6;
 
-template <int PAIRS>
-__global__ __launch_bounds__(256) void k_postpre(PostPreArgs a)
+// MODE 0: the real pass.  MODE 1 (PGMG_PP_VARIANT=1, measurement only): the same loads
+// and stores with the stencil arithmetic replaced by one add, to separate the memory
+// ceiling of this access pattern from the instruction cost.
+template <int MODE>
+__device__ __forceinline__ double2 js(double2 up, double2 ce, double2 dn, double2 f, double hh,
+                                      const Cols &k, bool brow)
+{
+    if (MODE == 1) return make_double2(ce.x + f.x, ce.y + up.y + dn.y);
+    return jstage(up, ce, dn, f, hh, k, brow);
+}
+template <int MODE>
+__device__ __forceinline__ double2 rs(double2 up, double2 ce, double2 dn, double2 f, double ih)
+{
+    if (MODE == 1) return make_double2(f.x + ce.x, f.y);
+    return rstage(up, ce, dn, f, ih);
+}
+
+template <int PAIRS, int MODE, int STRIDE = kPPStride, int MARGIN = kPPMargin>
+__device__ __forceinline__ void postpre_body(const PostPreArgs &a)
 {
     constexpr int R = 2 * PAIRS;
     __shared__ double red[4];
-    const Cols k = lane_cols_t<kPPStride, kPPMargin>(a.N);
+    const Cols k = lane_cols_t<STRIDE, MARGIN>(a.N);
     const int N = a.N, Nc = a.Nc;
     const long long P = a.P, Pc = a.Pc;
     const int jcb = a.jc0 + blockIdx.y * a.rows_per_block;
@@ -405,7 +422,7 @@ __global__ __launch_bounds__(256) void k_postpre(PostPreArgs a)
     double2 f1 = z, f2 = z, f3 = z, f4 = z, f5 = z;  // f[i-1], f[i-2], ..., f[i-5]
     double acc1 = 0.0, acc2 = 0.0;
     const int i_begin = 2 * jcb - 6;
-    const bool idle = (k.c - 2 * (threadIdx.x & 63) + kPPMargin) > N - 2;  // spare wave
+    const bool idle = (k.c - 2 * (threadIdx.x & 63) + MARGIN) > N - 2;  // spare wave
     const int i_end = idle ? i_begin
                            : i_begin + ((2 * (jce - jcb) + 11 + R - 1) / R) * R;
     double2 np_[R], nf[R];
@@ -445,6 +462,192 @@ __global__ __launch_bounds__(256) void k_postpre(PostPreArgs a)
             const int pq = s >> 1;
             const double2 e2 = add_prolong(cp[s], ii, cr[pq], crn[pq], cr[pq + 1], crn[pq + 1], pc, Nc);
             const double2 f0 = cf[s];  // f[ii]
+            // post-smooth sweep 1: x1 row ii-1
+            const double2 b2 = js<MODE>(e0, e1, e2, f1, hh, k, boundary_row(ii - 1, N));
+            {   // post check: r(x1) on row ii-2
+                const double2 r1 = rs<MODE>(b0, b1, b2, f2, ih);
+                const int row = ii - 2;
+                if (row >= olo && row < ohi && k.own) {
+                    acc1 += r1.x * r1.x;
+                    if (!k.by) acc1 += r1.y * r1.y;
+                }
+            }
+            // post-smooth sweep 2: x2 row ii-2 (= phi of cycle k+1)
+            const double2 c2 = js<MODE>(b0, b1, b2, f2, hh, k, boundary_row(ii - 2, N));
+            // pre-smooth sweep 1: x3 row ii-3
+            const double2 g2 = js<MODE>(c0, c1, c2, f3, hh, k, boundary_row(ii - 3, N));
+            {   // pre check: r(x3) on row ii-4
+                const double2 r3 = rs<MODE>(g0, g1, g2, f4, ih);
+                const int row = ii - 4;
+                if (row >= olo && row < ohi && k.own) {
+                    acc2 += r3.x * r3.x;
+                    if (!k.by) acc2 += r3.y * r3.y;
+                }
+            }
+            // pre-smooth sweep 2: x4 row ii-4 (stored)
+            const double2 h2 = js<MODE>(g0, g1, g2, f4, hh, k, boundary_row(ii - 4, N));
+            if (ii - 4 >= olo && ii - 4 < ohi && k.own) stg2(O + (ii - 4) * P, h2);
+            // r(x4) on row ii-5
+            const double2 d2 = rs<MODE>(h0, h1, h2, f5, ih);
+            // restriction: rows ii-7, ii-6, ii-5 = 2jc-1, 2jc, 2jc+1 when ii is even
+            if ((s & 1) == 0) {
+                const int jc = (ii - 6) >> 1;
+                const double m2 = dpp_next_f(d1.x);
+                const double u2 = dpp_next_f(d0.x);
+                const double w2 = dpp_next_f(d2.x);
+                const int ic = (k.c + 1) >> 1;
+                if (jc >= clo && jc < chi && k.own && ic <= Nc - 2) {
+                    const double v = 0.25 * d1.y + 0.125 * (m2 + d1.x + d2.y + d0.y) +
+                                     0.0625 * (d0.x + u2 + d2.x + w2);
+                    a.rc[(long long)jc * Pc + ic] = v;
+                }
+            }
+            e0 = e1; e1 = e2;
+            b0 = b1; b1 = b2;
+            c0 = c1; c1 = c2;
+            g0 = g1; g1 = g2;
+            h0 = h1; h1 = h2;
+            d0 = d1; d1 = d2;
+            f5 = f4; f4 = f3; f3 = f2; f2 = f1; f1 = f0;
+        }
+    }
+    const int slot = blockIdx.y * gridDim.x + blockIdx.x;
+    const double s1 = fused_block_sum(acc1, red);
+    __syncthreads();
+    const double s2 = fused_block_sum(acc2, red);
+    if (threadIdx.x == 0) {
+        a.partials1[slot] = s1;
+        a.partials2[slot] = s2;
+    }
+}
+
+template <int PAIRS, int MODE, int STRIDE = kPPStride, int MARGIN = kPPMargin>
+__global__ __launch_bounds__(256) void k_postpre(PostPreArgs a)
+{
+    postpre_body<PAIRS, MODE, STRIDE, MARGIN>(a);
+}
+
+// PGMG_PP_VARIANT=2: at most 128 VGPRs (4 waves per SIMD)
+template <int PAIRS>
+__global__ __launch_bounds__(256, 4) void k_postpre_o4(PostPreArgs a)
+{
+    postpre_body<PAIRS, 0>(a);
+}
+
+// ---------------------------------------------------------------------------
+// k_postpre_lds (default): the same pass, but the rows of phi, f and ec are staged
+// once per block in LDS.  A block's 4 wave tiles overlap by 12 columns each; loading
+// every tile from HBM re-reads 14 of each 128 columns (12 %).  Here the block's
+// 256 lanes load its 468-column window (4 x 114 owned + 2 x 6 margin) exactly once
+// per row (one 16-byte load per lane), and each wave reads its 128-column window
+// (and the coarse correction, with its right neighbour) from LDS.  Double-buffered
+// by row pairs: while the waves compute pair g from one slot, the loads of pair g+2
+// are in flight in registers and pair g+1 sits in the other slot; one barrier per
+// row pair.  Coarse rows live in a ring of 3 (pair g reads coarse rows g and g+1).
+// ---------------------------------------------------------------------------
+constexpr int kPPLdsRow = 4 * kPPStride + 2 * kPPMargin + 4;     // 472 doubles per row
+constexpr int kPPLdsCoarse = 2 * kPPStride + kPPMargin + 8;      // 242 doubles per coarse row
+
+__device__ __forceinline__ double2 lds2(const double *p) { return *reinterpret_cast<const double2 *>(p); }
+
+__global__ __launch_bounds__(256) void k_postpre_lds(PostPreArgs a)
+{
+    constexpr int R = 2;
+    __shared__ double red[4];
+    __shared__ __attribute__((aligned(16))) double sx[2][R][kPPLdsRow];
+    __shared__ __attribute__((aligned(16))) double sf[2][R][kPPLdsRow];
+    __shared__ __attribute__((aligned(16))) double se[3][kPPLdsCoarse];
+    const Cols k = lane_cols_t<kPPStride, kPPMargin>(a.N);
+    const int N = a.N, Nc = a.Nc;
+    const long long P = a.P, Pc = a.Pc;
+    const int jcb = a.jc0 + blockIdx.y * a.rows_per_block;
+    const int jce = min(jcb + a.rows_per_block, a.jc1);
+    const int olo = max(2 * jcb, a.row_lo), ohi = min(2 * jce, a.row_hi);
+    const int clo = max(jcb, max(1, a.rc_lo)), chi = min(jce, min(N / 2, a.rc_hi));
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
+        atomicAdd(&a.stats[0], 4ull);
+    ProlongCols pc;
+    pc.ic = (k.c - 1) >> 1;
+    pc.vx = k.c >= 3 && k.c <= N - 2;
+    pc.vy = k.c + 1 >= 2 && k.c + 1 <= N - 3;
+    double *__restrict__ O = a.x4 + k.c;
+    const double hh = a.hh, ih = a.ih;
+    const double2 z = make_double2(0.0, 0.0);
+
+    // loader geometry: the block window starts at column L0 (odd: 16-byte aligned pairs)
+    const int wpb = blockDim.x >> 6;
+    const int t = threadIdx.x;
+    const int L0 = kPPStride * wpb * blockIdx.x + 1 - kPPMargin;
+    const int npairs = (kPPStride * wpb + 2 * kPPMargin) / 2;
+    const bool ldr = t < npairs && L0 + 2 * t <= N - 1;      // columns >= N never matter
+    const int cc0 = (L0 - 1) >> 1;                               // first coarse column
+    const int ncc = (kPPStride / 2) * wpb + kPPMargin + 2;
+    const bool cldr = t < ncc && cc0 + t <= Nc - 1;
+    const double *__restrict__ GX = a.phi + L0 + 2 * t;
+    const double *__restrict__ GF = a.f + L0 + 2 * t;
+    const double *__restrict__ GE = a.ec + cc0 + t;
+    // this wave's window in the LDS rows
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int xo = kPPStride * w + 2 * lane;
+    const int co = (kPPStride / 2) * w + lane;
+
+    double2 e0 = z, e1 = z, b0 = z, b1 = z, c0 = z, c1 = z, g0 = z, g1 = z, h0 = z, h1 = z,
+            d0 = z, d1 = z;
+    double2 f1 = z, f2 = z, f3 = z, f4 = z, f5 = z;  // f[i-1], f[i-2], ..., f[i-5]
+    double acc1 = 0.0, acc2 = 0.0;
+    const int i_begin = 2 * jcb - 6;
+    const int ng = (2 * (jce - jcb) + 11 + R - 1) / R;   // row pairs (uniform over the block)
+    const int m0 = i_begin >> 1;                          // coarse row of the first pair
+    auto ring = [](int m) { return (m + 3 * 4096) % 3; };  // m >= -3
+
+    if (t < 2 * R * 4) {   // the 4 pad doubles past the window (read by spare lanes only)
+        const int sl = t >> 3, q = (t >> 2) & 1, j = kPPLdsRow - 4 + (t & 3);
+        sx[sl][q][j] = 0.0;
+        sf[sl][q][j] = 0.0;
+    }
+    // two register sets: pair p's loads go to set p & 1, issued two pairs ahead
+    double2 pxA[R], pfA[R], pxB[R], pfB[R];
+    double peA = 0.0, peB = 0.0;
+    auto load_pair = [&](int p, double2 (&px)[R], double2 (&pf)[R], double &pe) {
+        #pragma unroll
+        for (int q = 0; q < R; ++q) {
+            px[q] = ldr ? ldg2(GX + (i_begin + p * R + q) * P) : z;
+            pf[q] = ldr ? ldg2(GF + (i_begin + p * R + q) * P) : z;
+        }
+        pe = cldr ? GE[(long long)(m0 + p + 1) * Pc] : 0.0;   // the pair's second coarse row
+    };
+    auto store_pair = [&](int p, const double2 (&px)[R], const double2 (&pf)[R], double pe) {
+        if (t < npairs) {
+            #pragma unroll
+            for (int q = 0; q < R; ++q) {
+                *reinterpret_cast<double2 *>(&sx[p & 1][q][2 * t]) = px[q];
+                *reinterpret_cast<double2 *>(&sf[p & 1][q][2 * t]) = pf[q];
+            }
+        }
+        if (t < ncc) se[ring(m0 + p + 1)][t] = pe;
+    };
+    // prologue: pair 0 (+ its first coarse row) into slot 0; pairs 1, 2 in flight
+    load_pair(0, pxA, pfA, peA);
+    if (t < ncc) se[ring(m0)][t] = cldr ? GE[(long long)m0 * Pc] : 0.0;
+    store_pair(0, pxA, pfA, peA);
+    if (ng > 1) load_pair(1, pxB, pfB, peB);
+    if (ng > 2) load_pair(2, pxA, pfA, peA);
+    __syncthreads();
+
+    // pair gi: compute from slot gi & 1; pair gi+1 (set (gi+1) & 1) -> the other slot;
+    // issue pair gi+3 into the set just freed; one barrier
+    auto step = [&](int gi, double2 (&px)[R], double2 (&pf)[R], double &pe) {
+        const int slot = gi & 1;
+        const int i = i_begin + gi * R;
+        const int m = m0 + gi;
+        const double *E0 = se[ring(m)], *E1 = se[ring(m + 1)];
+        const double cr0 = E0[co], crn0 = E0[co + 1], cr1 = E1[co], crn1 = E1[co + 1];
+        #pragma unroll
+        for (int s = 0; s < R; ++s) {
+            const int ii = i + s;
+            const double2 xr = lds2(&sx[slot][s][xo]);
+            const double2 f0 = lds2(&sf[slot][s][xo]);   // f[ii]
+            const double2 e2 = add_prolong(xr, ii, cr0, crn0, cr1, crn1, pc, Nc);
             // post-smooth sweep 1: x1 row ii-1
             const double2 b2 = jstage(e0, e1, e2, f1, hh, k, boundary_row(ii - 1, N));
             {   // post check: r(x1) on row ii-2
@@ -493,6 +696,13 @@ __global__ __launch_bounds__(256) void k_postpre(PostPreArgs a)
             d0 = d1; d1 = d2;
             f5 = f4; f4 = f3; f3 = f2; f2 = f1; f1 = f0;
         }
+        if (gi + 1 < ng) store_pair(gi + 1, px, pf, pe);
+        if (gi + 3 < ng) load_pair(gi + 3, px, pf, pe);
+        __syncthreads();
+    };
+    for (int gi = 0; gi < ng; gi += 2) {
+        step(gi, pxB, pfB, peB);
+        if (gi + 1 < ng) step(gi + 1, pxA, pfA, peA);
     }
     const int slot = blockIdx.y * gridDim.x + blockIdx.x;
     const double s1 = fused_block_sum(acc1, red);
@@ -630,12 +840,18 @@ int postpre_blocks(int N, int jc0, int jc1)
 void launch_postpre(const PostPreArgs &a0, hipStream_t s)
 {
     int t, gx, gy, r;
-    fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, kPPStride);
+    const int variant = env_int("PGMG_PP_VARIANT", 0);
+    fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, variant == 3 ? 128 : kPPStride);
     PostPreArgs a = a0;
     a.rows_per_block = r;
     const dim3 g(gx, gy), b(t);
-    if (env_int("PGMG_PP_PAIRS", 1) >= 2) k_postpre<2><<<g, b, 0, s>>>(a);
-    else k_postpre<1><<<g, b, 0, s>>>(a);
+    if (variant == 0) k_postpre_lds<<<g, b, 0, s>>>(a);
+    else if (variant == 4) k_postpre<1, 0><<<g, b, 0, s>>>(a);    // per-wave loads (r01)
+    else if (variant == 1) k_postpre<1, 1><<<g, b, 0, s>>>(a);
+    else if (variant == 3) k_postpre<1, 1, 128, 0><<<g, b, 0, s>>>(a);  // no column overlap
+    else if (variant == 2) k_postpre_o4<1><<<g, b, 0, s>>>(a);
+    else if (env_int("PGMG_PP_PAIRS", 1) >= 2) k_postpre<2, 0><<<g, b, 0, s>>>(a);
+    else k_postpre<1, 0><<<g, b, 0, s>>>(a);
 }
 
 void launch_postpre_decide(const PostPreArgs &a, int np, double eps, unsigned *flags, hipStream_t s)
