@@ -41,6 +41,8 @@ def parse():
                     help="events: eager launches with hipEvents around every fine sweep")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-n", type=int, default=0, help="grid for the CPU sample (default = --n)")
+    ap.add_argument("--dtype", choices=["f64", "f32"], default="f64",
+                    help="f64: the reference's precision (the headline); f32: the fp32 variant")
     return ap.parse_args()
 
 
@@ -94,7 +96,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # CPU baseline first, before this process touches the GPU (it runs a child process)
     cpu = None
-    if world == 1 and rank == 0 and args.cpu_baseline == "auto":
+    if world == 1 and rank == 0 and args.cpu_baseline == "auto" and args.dtype == "f64":
         try:
             cpu = cpu_baseline(args.cpu_n or args.n)
         except Exception as e:  # reported, not fatal
@@ -115,7 +117,7 @@ def main():
         uid = bytes(t.tolist())
 
     flags = pg.PGMG_FLAG_TIME_FINE if args.timing == "events" else 0
-    kw = dict(flags=flags, device=local_rank if world > 1 else 0)
+    kw = dict(flags=flags, device=local_rank if world > 1 else 0, dtype=args.dtype)
     if world > 1:
         kw.update(rank=rank, world=world, uid=uid)
     s = pg.Solver(args.n, **kw)
@@ -154,32 +156,35 @@ def main():
     rows = min(r0.value + nr.value, N - 1) - max(r0.value, 1)
     nf = float(rows) * (N - 2)              # fine interior points on this rank
     nc = nf / 4.0                           # coarse interior points it restricts / prolongs
+    es = s.elem_bytes / 8.0                 # the per-point byte figures below are fp64
     passes = []
     if s.fused:
         # k_pre: read x0, f; write x2 (24 B/pt) + write rc; k_post: read phi, f, ec; write x2
         for which, name, nbytes in ((3, "k_postpre (finest level, between cycles: prolongation "
                                         "+ 2+2 Jacobi sweeps + residual + restriction, fused)",
-                                     24.0 * nf + 16.0 * nc),
+                                     (24.0 * nf + 16.0 * nc) * es),
                                     (1, "k_pre<false,true> (finest level: 2 Jacobi sweeps + "
-                                        "residual + restriction, fused)", 24.0 * nf + 8.0 * nc),
+                                        "residual + restriction, fused)", (24.0 * nf + 8.0 * nc) * es),
                                     (2, "k_post<true> (finest level: prolongation + 2 Jacobi "
-                                        "sweeps, fused)", 24.0 * nf + 8.0 * nc)):
+                                        "sweeps, fused)", (24.0 * nf + 8.0 * nc) * es)):
             cnt, ms = s.fine_pass_time(which)
             passes.append((name, nbytes, cnt, ms))
     else:
         cnt, ms = s.fine_pass_time(0)
-        passes.append(("k_sweep<false,false,true> (finest-level Jacobi sweep)", 24.0 * nf, cnt, ms))
+        passes.append(("k_sweep<false,false,true> (finest-level Jacobi sweep)", 24.0 * nf * es,
+                       cnt, ms))
     if not passes or passes[0][2] == 0:   # graph mode: time the kernel separately
         ms = s.bench_sweep(20)
         passes = [("k_sweep<false,false,true> (finest-level Jacobi sweep, timed apart)",
-                   24.0 * nf, 20, ms)]
+                   24.0 * nf * es, 20, ms)]
     roof = []
     for name, nbytes, cnt, ms in passes:
         ach = nbytes / (ms * 1e-3) / 1e9 if ms > 0 else None
         roof.append({"bound": "hbm", "kernel": name,
                      "achieved": round(ach, 2) if ach else None, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4) if ach else None,
-                     "traffic": pmc_traffic(N, name.split(" ")[0]) if world == 1 else None,
+                     "traffic": (pmc_traffic(N, name.split(" ")[0])
+                                 if world == 1 and args.dtype == "f64" else None),
                      "bytes_per_launch": nbytes, "launches_timed": cnt,
                      "ms_per_launch": round(ms, 5)})
     # the dominant kernel: largest total time over the timed region
@@ -189,12 +194,12 @@ def main():
     if s.fused and roof and roof[0]["achieved"]:
         # the same pass counted as the separate 24 B/pt sweeps it replaces
         nsw = 4 if roof[0]["kernel"].startswith("k_postpre") else 2
-        sweep_eq = round(nsw * 24.0 * nf / (roof[0]["ms_per_launch"] * 1e-3) / 1e9, 2)
+        sweep_eq = round(nsw * 24.0 * nf * es / (roof[0]["ms_per_launch"] * 1e-3) / 1e9, 2)
 
     if rank == 0:
         value = args.steps / dt
         line = {
-            "metric": METRIC,
+            "metric": METRIC if args.dtype == "f64" else METRIC.replace(", fp64", ", fp32 variant"),
             "value": round(value, 4),
             "unit": "V-cycles/s",
             "n_gpus": world,
@@ -204,7 +209,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": args.dtype,
             "data": "synthetic: the reference's own problem, phi0=0, f=2*pi^2*sin(pi x)sin(pi y)",
             "config": {
                 "workload": f"V-cycle N={n} ({n - 1}^2 cells), 2+2 Jacobi (v1=v2=1), 11 coarsest "

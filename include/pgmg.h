@@ -61,6 +61,13 @@ extern "C" {
 #define PGMG_PROLONG_REFERENCE 0 /* mg_cpu_exec: fine row/col 1 uncorrected */
 #define PGMG_PROLONG_SYMMETRIC 1 /* gpu_exec's prolungator_kernel; fine boundary set 0  */
 
+/* element type of every level grid (pgmg_config.precision) */
+#define PGMG_PRECISION_FP64 0    /* bit-identical to mg_cpu_exec (the default)            */
+#define PGMG_PRECISION_FP32 1    /* fp32 storage and arithmetic, half the HBM bytes; norms
+                                    accumulated in fp64; parity stated as a tolerance
+                                    against fp64 (the reference is fp64-only).
+                                    Host arrays at the ABI stay double.                     */
+
 /* config flags */
 #define PGMG_FLAG_NO_GRAPH 1u    /* launch eagerly instead of replaying a hipGraph */
 #define PGMG_FLAG_TIME_FINE 2u   /* eager launches + hipEvents around every finest-level
@@ -88,6 +95,7 @@ typedef struct pgmg_config {
     int rank, world;   /* default 0, 1                                           */
     const void *nccl_unique_id;  /* 128-byte ncclUniqueId when world > 1      */
     int gather_n;      /* levels with N <= gather_n collapse to rank 0 (world>1) */
+    int precision;     /* PGMG_PRECISION_FP64 (default) or PGMG_PRECISION_FP32    */
 } pgmg_config;
 
 typedef struct pgmg_ctx pgmg_ctx;
@@ -139,9 +147,13 @@ int pgmg_levels(pgmg_ctx *ctx, int *bulk_levels, int *tail_top_n);
 /* Algorithmic HBM bytes one V-cycle moves (per rank), summed per kernel. */
 int pgmg_vcycle_bytes(pgmg_ctx *ctx, double *bytes);
 
-/* Raw device pointer and pitch (in doubles) of phi's element (0,0) on this
- * rank, for callers that want to read it in place. */
+/* Raw device pointer and pitch (in elements) of phi's element (0,0) on this
+ * rank, for callers that want to read it in place.  The elements are double, or
+ * float when the context was created with PGMG_PRECISION_FP32 (pgmg_precision). */
 int pgmg_phi_device(pgmg_ctx *ctx, double **ptr, int *pitch, int *row0, int *rows);
+
+/* The context's PGMG_PRECISION_* and its grid element size in bytes (8 or 4). */
+int pgmg_precision(pgmg_ctx *ctx, int *precision, int *elem_bytes);
 
 /* Count and mean device duration (ms) of the finest-level kernels launched since
  * the last call (needs PGMG_FLAG_TIME_FINE; synchronous).  pass 0: plain Jacobi

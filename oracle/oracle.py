@@ -11,6 +11,7 @@ import numpy as np
 
 HERE = pathlib.Path(__file__).resolve().parent
 LIB = HERE / "liboracle.so"
+LIB_F32 = HERE / "liboracle_f32.so"   # -DORC_REAL=float: checker of the fp32 variant
 
 
 class OrcCtx(C.Structure):
@@ -30,7 +31,7 @@ class OrcCtx(C.Structure):
     ]
 
 
-_lib = None
+_libs = {}
 _DP = C.POINTER(C.c_double)
 
 
@@ -38,12 +39,18 @@ def build():
     subprocess.run(["make", "-C", str(HERE), "-s", "all"], check=True)
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not LIB.exists():
+def _np_dtype(dtype):
+    return np.float32 if dtype in ("f32", np.float32) else np.float64
+
+
+def lib(dtype="f64"):
+    """liboracle.so (fp64, pinned to the reference) or liboracle_f32.so (dtype="f32")."""
+    key = "f32" if _np_dtype(dtype) is np.float32 else "f64"
+    if key not in _libs:
+        path = LIB_F32 if key == "f32" else LIB
+        if not path.exists():
             build()
-        L = C.CDLL(str(LIB))
+        L = C.CDLL(str(path))
         P = C.c_void_p
         sig = {
             "orc_ctx_init": (None, [P]),
@@ -61,14 +68,16 @@ def lib():
             "orc_rel_error": (C.c_double, [P, P, C.c_int]),
             "orc_residual_norm": (C.c_double, [P, P, C.c_int, C.c_double]),
             "orc_hash": (C.c_uint64, [P, C.c_longlong]),
+            "orc_real_size": (C.c_int, []),
         }
         for k, (r, a) in sig.items():
             fn = getattr(L, k)
             fn.restype = r
             fn.argtypes = a
         assert L.orc_ctx_size() == C.sizeof(OrcCtx), "OrcCtx layout mismatch"
-        _lib = L
-    return _lib
+        assert L.orc_real_size() == (4 if key == "f32" else 8), "oracle element type"
+        _libs[key] = L
+    return _libs[key]
 
 
 def _p(a):
@@ -78,9 +87,11 @@ def _p(a):
 class Oracle:
     """Sequential CPU multigrid with the reference's exact semantics."""
 
-    def __init__(self, eps=1e-7, **kw):
+    def __init__(self, eps=1e-7, dtype="f64", **kw):
+        self.dt = _np_dtype(dtype)
+        self.L = lib(dtype)
         self.c = OrcCtx()
-        lib().orc_ctx_init(C.byref(self.c))
+        self.L.orc_ctx_init(C.byref(self.c))
         self.c.eps = eps
         for k, v in kw.items():
             setattr(self.c, k, v)
@@ -95,35 +106,45 @@ class Oracle:
 
     def rhs(self, N, h=None):
         h = 1.0 / (N - 1) * self.c.a if h is None else h
-        f = np.zeros((N, N))
-        lib().orc_rhs(C.byref(self.c), _p(f), N, N, h)
+        f = np.zeros((N, N), dtype=self.dt)
+        self.L.orc_rhs(C.byref(self.c), _p(f), N, N, h)
         return f
 
     def exact(self, N):
         u = np.zeros((N, N))
-        lib().orc_exact(C.byref(self.c), _p(u), self.c.a / (N - 1), N, N)
+        self.L.orc_exact(C.byref(self.c), _p(u), self.c.a / (N - 1), N, N)
         return u
 
     def v_cycle(self, phi, f, h=None):
         N = phi.shape[0]
         h = self.c.a / (N - 1) if h is None else h
-        lib().orc_v_cycle(C.byref(self.c), _p(phi), _p(f), N, h)
+        self._chk(phi, f)
+        self.L.orc_v_cycle(C.byref(self.c), _p(phi), _p(f), N, h)
 
     def w_cycle(self, phi, f, h=None):
         N = phi.shape[0]
         h = self.c.a / (N - 1) if h is None else h
-        lib().orc_w_cycle(C.byref(self.c), _p(phi), _p(f), N, h)
+        self._chk(phi, f)
+        self.L.orc_w_cycle(C.byref(self.c), _p(phi), _p(f), N, h)
 
     def f_cycle_outer(self, phi):
-        lib().orc_f_cycle_outer(C.byref(self.c), _p(phi), phi.shape[0])
+        self._chk(phi)
+        self.L.orc_f_cycle_outer(C.byref(self.c), _p(phi), phi.shape[0])
 
     def smooth(self, x, f, h, num_iter):
         N = x.shape[0]
-        work = np.zeros(2 * N * N)
-        return lib().orc_jacobi_smooth(C.byref(self.c), _p(x), _p(f), N, N, h, num_iter, _p(work))
+        self._chk(x, f)
+        work = np.zeros(2 * N * N, dtype=self.dt)
+        return self.L.orc_jacobi_smooth(C.byref(self.c), _p(x), _p(f), N, N, h, num_iter,
+                                        _p(work))
 
     def rel_error(self, phi):
-        return lib().orc_rel_error(C.byref(self.c), _p(phi), phi.shape[0])
+        phi = np.ascontiguousarray(phi, dtype=self.dt)
+        return self.L.orc_rel_error(C.byref(self.c), _p(phi), phi.shape[0])
+
+    def _chk(self, *arrays):
+        for a in arrays:
+            assert a.dtype == self.dt and a.flags.c_contiguous, (a.dtype, self.dt)
 
 
 def residual(x, f, h):
@@ -157,11 +178,12 @@ def fnv_hash(a):
     return "%016x" % lib().orc_hash(_p(a), a.size)
 
 
-def run_cycles(kind, N, cycles, eps=1e-7):
-    """phi after `cycles` cycles from phi=0, f=analytic RHS (mg_cpu_exec's setup)."""
-    o = Oracle(eps=eps)
+def run_cycles(kind, N, cycles, eps=1e-7, dtype="f64"):
+    """phi after `cycles` cycles from phi=0, f=analytic RHS (mg_cpu_exec's setup).
+    dtype="f32": the fp32 restatement (float grids and arithmetic)."""
+    o = Oracle(eps=eps, dtype=dtype)
     f = o.rhs(N)
-    phi = np.zeros((N, N))
+    phi = np.zeros((N, N), dtype=o.dt)
     for _ in range(cycles):
         if kind == "V":
             o.v_cycle(phi, f)

@@ -23,6 +23,14 @@
  *     prolongation incl. the skipped fine row/col 1 (:208-226)
  * Floating point: compiled with -ffp-contract=off so every expression rounds
  * exactly as the reference's plain C++ does (no FMA contraction).
+ *
+ * Element type: `real` = double (liboracle.so, the pinned restatement) or, with
+ * -DORC_REAL=float, float (liboracle_f32.so): the same algorithm with every grid
+ * value and every arithmetic operation in fp32, h*h and 1/(h*h) rounded once from
+ * fp64, the RHS computed in fp64 and rounded, squares of the norms accumulated in
+ * fp64.  That is the checker of the library's PGMG_PRECISION_FP32 variant (SURVEY
+ * §8 f3; the reference itself is fp64-only).  For real = double every expression
+ * below is the one the reference evaluates.
  */
 #include <math.h>
 #include <stdint.h>
@@ -32,6 +40,13 @@
 #ifndef M_PI
 #define M_PI 3.14159265358979323846
 #endif
+
+#ifndef ORC_REAL
+#define ORC_REAL double
+#endif
+typedef ORC_REAL real;
+
+int orc_real_size(void) { return (int)sizeof(real); }
 
 typedef struct orc_ctx {
     double eps;        /* smoother tolerance (MultiGridTestRunner.hpp:144 -> 1e-7) */
@@ -66,43 +81,43 @@ int orc_ctx_size(void) { return (int)sizeof(orc_ctx); }
 
 /* ---- grid utilities (DynamicGridUtils.hpp) ---------------------------- */
 
-void orc_zero(double *x, long long n)
+void orc_zero(real *x, long long n)
 {
     for (long long i = 0; i < n; ++i)
-        x[i] = 0.0;
+        x[i] = 0;
 }
 
 /* DynamicGridUtils.hpp:21-27 — sequential sum of squares over l entries */
-double orc_norm(const double *v, long long l)
+double orc_norm(const real *v, long long l)
 {
     double s = 0.0;
     for (long long i = 0; i < l; ++i)
-        s += v[i] * v[i];
+        s += (double)v[i] * (double)v[i];
     return sqrt(s);
 }
 
 /* DynamicGridUtils.hpp:59-69 — interior only; boundary of r untouched */
-void orc_residual(double *r, const double *x, const double *f, int W, int H, double h)
+void orc_residual(real *r, const real *x, const real *f, int W, int H, double h)
 {
+    const real ih = (real)(1.0 / (h * h));
     for (int y = 1; y < H - 1; ++y) {
         for (int xi = 1; xi < W - 1; ++xi) {
             long long k = (long long)y * W + xi;
-            r[k] = f[k] - (1.0 / (h * h)) *
-                              (4 * x[k] - x[k - 1] - x[k + 1] - x[k - W] - x[k + W]);
+            r[k] = f[k] - ih * (4 * x[k] - x[k - 1] - x[k + 1] - x[k - W] - x[k + W]);
         }
     }
 }
 
 /* DynamicGridUtils.hpp:111-124 */
-void orc_rhs(const orc_ctx *c, double *f, int W, int H, double h)
+void orc_rhs(const orc_ctx *c, real *f, int W, int H, double h)
 {
     double factor = (M_PI * M_PI / (c->a * c->a)) * (c->p * c->p + c->q * c->q);
     for (int j = 0; j < H; ++j) {
         for (int i = 0; i < W; ++i) {
             double xx = i * h;
             double yy = j * h;
-            f[(long long)j * W + i] = factor * sin(c->p * M_PI * xx / c->a) *
-                                      sin(c->q * M_PI * yy / c->a);
+            f[(long long)j * W + i] = (real)(factor * sin(c->p * M_PI * xx / c->a) *
+                                             sin(c->q * M_PI * yy / c->a));
         }
     }
 }
@@ -120,15 +135,16 @@ void orc_exact(const orc_ctx *c, double *u, double h, int W, int H)
 }
 
 /* ---- Jacobi smoother (Smoother.hpp:38-116) ------------------------------
- * Returns the number of sweeps performed.  `work` must hold 2*W*H doubles.
+ * Returns the number of sweeps performed.  `work` must hold 2*W*H elements.
  */
-int orc_jacobi_smooth(orc_ctx *c, double *x, const double *f, int W, int H, double h,
-                      int num_iter, double *work)
+int orc_jacobi_smooth(orc_ctx *c, real *x, const real *f, int W, int H, double h,
+                      int num_iter, real *work)
 {
     long long L = (long long)W * H;
-    double *out = work;     /* Smoother.hpp:46-47: seeded with x */
-    double *r = work + L;   /* Smoother.hpp:75: residual buffer, boundary 0 */
-    memcpy(out, x, sizeof(double) * L);
+    real *out = work;       /* Smoother.hpp:46-47: seeded with x */
+    real *r = work + L;     /* Smoother.hpp:75: residual buffer, boundary 0 */
+    const real hh = (real)(h * h);
+    memcpy(out, x, sizeof(real) * L);
     orc_zero(r, L);
     int done = 0;
     c->smooth_calls++;
@@ -136,10 +152,10 @@ int orc_jacobi_smooth(orc_ctx *c, double *x, const double *f, int W, int H, doub
         for (int y = 1; y < H - 1; ++y) {
             for (int xi = 1; xi < W - 1; ++xi) {
                 long long k = (long long)y * W + xi;
-                out[k] = 0.25 * ((h * h * f[k]) + x[k - 1] + x[k + 1] + x[k - W] + x[k + W]);
+                out[k] = (real)0.25 * ((hh * f[k]) + x[k - 1] + x[k + 1] + x[k - W] + x[k + W]);
             }
         }
-        memcpy(x, out, sizeof(double) * L);
+        memcpy(x, out, sizeof(real) * L);
         ++done;
         c->sweeps++;
         orc_residual(r, x, f, W, H, h);
@@ -154,56 +170,56 @@ int orc_jacobi_smooth(orc_ctx *c, double *x, const double *f, int W, int H, doub
 
 /* ---- transfer operators (MultiGrid.hpp:187-226) ------------------------ */
 
-void orc_restrict(const double *F, double *C, int Nf, int Nc)
+void orc_restrict(const real *F, real *C, int Nf, int Nc)
 {
     for (int jc = 1; jc < Nc - 1; ++jc) {
         for (int ic = 1; ic < Nc - 1; ++ic) {
             long long c = (long long)jc * Nc + ic;
             long long k = (long long)(2 * jc) * Nf + 2 * ic;
-            C[c] = 0.25 * F[k] +
-                   0.125 * (F[k + 1] + F[k - 1] + F[k + Nf] + F[k - Nf]) +
-                   0.0625 * (F[k - Nf - 1] + F[k - Nf + 1] + F[k + Nf - 1] + F[k + Nf + 1]);
+            C[c] = (real)0.25 * F[k] +
+                   (real)0.125 * (F[k + 1] + F[k - 1] + F[k + Nf] + F[k - Nf]) +
+                   (real)0.0625 * (F[k - Nf - 1] + F[k - Nf + 1] + F[k + Nf - 1] + F[k + Nf + 1]);
         }
     }
 }
 
 /* fine += P * coarse; the loop bounds never touch fine row/col 1 (MultiGrid.hpp:210-225) */
-void orc_prolong(double *F, const double *C, int Nf, int Nc)
+void orc_prolong(real *F, const real *C, int Nf, int Nc)
 {
     for (int jc = 1; jc < Nc - 1; ++jc) {
         for (int ic = 1; ic < Nc - 1; ++ic) {
             long long c = (long long)jc * Nc + ic;
             long long J = 2 * jc, I = 2 * ic;
             F[J * Nf + I] += C[c];
-            F[(J + 1) * Nf + I] += 0.5 * (C[c] + C[c + Nc]);
-            F[J * Nf + I + 1] += 0.5 * (C[c] + C[c + 1]);
-            F[(J + 1) * Nf + I + 1] += 0.25 * (C[c] + C[c + 1] + C[c + Nc] + C[c + Nc + 1]);
+            F[(J + 1) * Nf + I] += (real)0.5 * (C[c] + C[c + Nc]);
+            F[J * Nf + I + 1] += (real)0.5 * (C[c] + C[c + 1]);
+            F[(J + 1) * Nf + I + 1] += (real)0.25 * (C[c] + C[c + 1] + C[c + Nc] + C[c + Nc + 1]);
         }
     }
 }
 
 /* ---- cycles ------------------------------------------------------------- */
 
-static double *orc_alloc(long long n) { return (double *)calloc((size_t)n, sizeof(double)); }
+static real *orc_alloc(long long n) { return (real *)calloc((size_t)n, sizeof(real)); }
 
 /* MultiGrid.hpp:57-94 */
-void orc_v_cycle(orc_ctx *c, double *phi, const double *f, int N, double h)
+void orc_v_cycle(orc_ctx *c, real *phi, const real *f, int N, double h)
 {
     long long L = (long long)N * N;
-    double *work = orc_alloc(2 * L);
+    real *work = orc_alloc(2 * L);
     if (N <= c->n_coarse) {
         orc_jacobi_smooth(c, phi, f, N, N, h, c->coarse_iter, work);
         free(work);
         return;
     }
     orc_jacobi_smooth(c, phi, f, N, N, h, c->v1, work);
-    double *res = orc_alloc(L);
+    real *res = orc_alloc(L);
     orc_residual(res, phi, f, N, N, h);
     int Nc = (N - 1) / 2 + 1;
     long long Lc = (long long)Nc * Nc;
-    double *rc = orc_alloc(Lc);
+    real *rc = orc_alloc(Lc);
     orc_restrict(res, rc, N, Nc);
-    double *ec = orc_alloc(Lc);
+    real *ec = orc_alloc(Lc);
     orc_v_cycle(c, ec, rc, Nc, 2 * h);
     orc_prolong(phi, ec, N, Nc);
     orc_jacobi_smooth(c, phi, f, N, N, h, c->v2, work);
@@ -214,23 +230,23 @@ void orc_v_cycle(orc_ctx *c, double *phi, const double *f, int N, double h)
 }
 
 /* MultiGrid.hpp:96-136 */
-void orc_w_cycle(orc_ctx *c, double *phi, const double *f, int N, double h)
+void orc_w_cycle(orc_ctx *c, real *phi, const real *f, int N, double h)
 {
     long long L = (long long)N * N;
-    double *work = orc_alloc(2 * L);
+    real *work = orc_alloc(2 * L);
     if (N <= c->n_coarse) {
         orc_jacobi_smooth(c, phi, f, N, N, h, c->coarse_iter, work);
         free(work);
         return;
     }
     orc_jacobi_smooth(c, phi, f, N, N, h, c->v1, work);
-    double *res = orc_alloc(L);
+    real *res = orc_alloc(L);
     orc_residual(res, phi, f, N, N, h);
     int Nc = (N - 1) / 2 + 1;
     long long Lc = (long long)Nc * Nc;
-    double *rc = orc_alloc(Lc);
+    real *rc = orc_alloc(Lc);
     orc_restrict(res, rc, N, Nc);
-    double *ec = orc_alloc(Lc);
+    real *ec = orc_alloc(Lc);
     for (int i = 0; i < c->alpha; ++i)
         orc_w_cycle(c, ec, rc, Nc, 2.0 * h);
     orc_prolong(phi, ec, N, Nc);
@@ -243,44 +259,44 @@ void orc_w_cycle(orc_ctx *c, double *phi, const double *f, int N, double h)
 
 /* MultiGrid.hpp:28-55 — restrict `fine` repeatedly down to N_coarsest.
  * Writes the coarsest grid into `out` (N_coarsest^2 doubles). */
-void orc_coarsest_grid(const double *fine, double *out, int N_fine, int N_coarsest)
+void orc_coarsest_grid(const real *fine, real *out, int N_fine, int N_coarsest)
 {
     int Nc = N_fine;
-    double *cur = orc_alloc((long long)Nc * Nc);
-    memcpy(cur, fine, sizeof(double) * (size_t)((long long)Nc * Nc));
+    real *cur = orc_alloc((long long)Nc * Nc);
+    memcpy(cur, fine, sizeof(real) * (size_t)((long long)Nc * Nc));
     while (Nc > N_coarsest) {
         int Nn = (Nc - 1) / 2 + 1;
-        double *nx = orc_alloc((long long)Nn * Nn);
+        real *nx = orc_alloc((long long)Nn * Nn);
         orc_restrict(cur, nx, Nc, Nn);
         free(cur);
         cur = nx;
         Nc = Nn;
     }
-    memcpy(out, cur, sizeof(double) * (size_t)((long long)Nc * Nc));
+    memcpy(out, cur, sizeof(real) * (size_t)((long long)Nc * Nc));
     free(cur);
 }
 
 /* MultiGrid.hpp:138-183 — full multigrid from N_init up to N_final; the
  * result (N_final^2) goes to `final_solution`.  The finer RHS is regenerated
  * analytically on every level (MultiGrid.hpp:162). */
-void orc_f_cycle(orc_ctx *c, const double *phi, const double *f, int N_init, double h_init,
-                 int N_final, double *final_solution)
+void orc_f_cycle(orc_ctx *c, const real *phi, const real *f, int N_init, double h_init,
+                 int N_final, real *final_solution)
 {
     int N = N_init;
     double h = h_init;
     long long L = (long long)N * N;
-    double *phic = orc_alloc(L);
-    double *fc = orc_alloc(L);
-    memcpy(phic, phi, sizeof(double) * (size_t)L);
-    memcpy(fc, f, sizeof(double) * (size_t)L);
+    real *phic = orc_alloc(L);
+    real *fc = orc_alloc(L);
+    memcpy(phic, phi, sizeof(real) * (size_t)L);
+    memcpy(fc, f, sizeof(real) * (size_t)L);
     while (N < N_final) {
-        double *work = orc_alloc(2 * (long long)N * N);
+        real *work = orc_alloc(2 * (long long)N * N);
         orc_jacobi_smooth(c, phic, fc, N, N, h, 3, work);
         free(work);
         int Nf = 2 * N - 1;
         long long Lf = (long long)Nf * Nf;
-        double *phif = orc_alloc(Lf);
-        double *ff = orc_alloc(Lf);
+        real *phif = orc_alloc(Lf);
+        real *ff = orc_alloc(Lf);
         orc_rhs(c, ff, Nf, Nf, h / 2);
         orc_prolong(phif, phic, Nf, N);
         orc_v_cycle(c, phif, ff, Nf, h / 2);
@@ -291,7 +307,7 @@ void orc_f_cycle(orc_ctx *c, const double *phi, const double *f, int N_init, dou
         N = Nf;
         h /= 2;
     }
-    memcpy(final_solution, phic, sizeof(double) * (size_t)((long long)N * N));
+    memcpy(final_solution, phic, sizeof(real) * (size_t)((long long)N * N));
     free(phic);
     free(fc);
 }
@@ -299,12 +315,12 @@ void orc_f_cycle(orc_ctx *c, const double *phi, const double *f, int N_init, dou
 /* One outer iteration of MultiGridTestRunner::run_cycle("F-cycle")
  * (MultiGridTestRunner.hpp:192-205): restrict phi to N_coarse, run f_cycle
  * from there with the analytic coarse RHS, copy the result into phi. */
-void orc_f_cycle_outer(orc_ctx *c, double *phi, int N)
+void orc_f_cycle_outer(orc_ctx *c, real *phi, int N)
 {
     int n0 = c->n_coarse;
     double h0 = 1.0 / (n0 - 1);
-    double *f0 = orc_alloc((long long)n0 * n0);
-    double *p0 = orc_alloc((long long)n0 * n0);
+    real *f0 = orc_alloc((long long)n0 * n0);
+    real *p0 = orc_alloc((long long)n0 * n0);
     orc_rhs(c, f0, n0, n0, h0);
     orc_coarsest_grid(phi, p0, N, n0);
     orc_f_cycle(c, p0, f0, n0, h0, N, phi);
@@ -315,26 +331,29 @@ void orc_f_cycle_outer(orc_ctx *c, double *phi, int N)
 /* ---- harness helpers ---------------------------------------------------- */
 
 /* ||phi - u|| / ||u|| as printed by MultiGridTestRunner.hpp:252-255 */
-double orc_rel_error(const orc_ctx *c, const double *phi, int N)
+double orc_rel_error(const orc_ctx *c, const real *phi, int N)
 {
-    long long L = (long long)N * N;
+    /* sequential sums in fp64 over the exact solution of orc_exact (fp32: phi widened) */
     double h = c->a / (N - 1);
-    double *u = orc_alloc(L);
-    double *e = orc_alloc(L);
-    orc_exact(c, u, h, N, N);
-    for (long long i = 0; i < L; ++i)
-        e[i] = phi[i] - u[i];
-    double r = orc_norm(e, L) / orc_norm(u, L);
-    free(u);
-    free(e);
-    return r;
+    double se = 0.0, su = 0.0;
+    for (int j = 0; j < N; ++j) {
+        for (int i = 0; i < N; ++i) {
+            double xx = i * h;
+            double yy = j * h;
+            double u = sin(c->p * M_PI * xx / c->a) * sin(c->q * M_PI * yy / c->a);
+            double e = (double)phi[(long long)j * N + i] - u;
+            se += e * e;
+            su += u * u;
+        }
+    }
+    return sqrt(se) / sqrt(su);
 }
 
 /* sqrt(sum_interior r^2) of the current iterate */
-double orc_residual_norm(const double *phi, const double *f, int N, double h)
+double orc_residual_norm(const real *phi, const real *f, int N, double h)
 {
     long long L = (long long)N * N;
-    double *r = orc_alloc(L);
+    real *r = orc_alloc(L);
     orc_residual(r, phi, f, N, N, h);
     double n = orc_norm(r, L);
     free(r);
@@ -342,12 +361,12 @@ double orc_residual_norm(const double *phi, const double *f, int N, double h)
 }
 
 /* FNV-style 64-bit hash over the IEEE words */
-uint64_t orc_hash(const double *v, long long n)
+uint64_t orc_hash(const real *v, long long n)
 {
     uint64_t hsh = 1469598103934665603ULL;
     for (long long i = 0; i < n; ++i) {
-        uint64_t w;
-        memcpy(&w, &v[i], 8);
+        uint64_t w = 0;
+        memcpy(&w, &v[i], sizeof(real));
         hsh = (hsh ^ w) * 1099511628211ULL;
     }
     return hsh;

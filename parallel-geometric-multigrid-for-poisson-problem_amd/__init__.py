@@ -1,4 +1,4 @@
-"""MI355X-native geometric multigrid for the 2D Poisson problem (fp64).
+"""MI355X-native geometric multigrid for the 2D Poisson problem (fp64; fp32 variant).
 
 The hot path (Jacobi smoother, residual + norm, full-weighting restriction,
 prolongation, V/W-cycles) is hand-written HIP for gfx950 in ``csrc/`` behind the C ABI
@@ -17,7 +17,7 @@ import subprocess
 import numpy as np
 
 from ._capi import (PGMG_FLAG_LOOPBACK, PGMG_FLAG_NO_CROSS, PGMG_FLAG_NO_GRAPH,
-                    PGMG_FLAG_TIME_FINE,
+                    PGMG_FLAG_TIME_FINE, PGMG_PRECISION_FP32, PGMG_PRECISION_FP64,
                     PGMG_FLAG_UNFUSED, PGMG_PROLONG_REFERENCE,
                     PGMG_PROLONG_SYMMETRIC, PgmgConfig, PgmgError, check, load)
 
@@ -27,7 +27,7 @@ __all__ = [
     "build", "load", "Solver", "PgmgConfig", "PgmgError", "ops",
     "PGMG_FLAG_NO_GRAPH", "PGMG_FLAG_TIME_FINE", "PGMG_FLAG_UNFUSED", "PGMG_FLAG_LOOPBACK", "PGMG_FLAG_NO_CROSS",
     "PGMG_PROLONG_REFERENCE", "plan_strips", "LoopbackHub", "unique_id",
-    "PGMG_PROLONG_SYMMETRIC",
+    "PGMG_PROLONG_SYMMETRIC", "PGMG_PRECISION_FP64", "PGMG_PRECISION_FP32",
 ]
 
 
@@ -90,9 +90,13 @@ class Solver:
     numerics of MultigridSolver (2_part_MG/MultiGrid.hpp:57-136).
     """
 
-    def __init__(self, N, hub=None, uid=None, **cfg):
-        """hub: LoopbackHub (ranks as threads on one GPU); uid: 128-byte RCCL unique id."""
+    def __init__(self, N, hub=None, uid=None, dtype="f64", **cfg):
+        """hub: LoopbackHub (ranks as threads on one GPU); uid: 128-byte RCCL unique id;
+        dtype: "f64" (bit-exact to mg_cpu_exec) or "f32" (PGMG_PRECISION_FP32)."""
         self.lib = load()
+        if dtype not in ("f64", "f32"):
+            raise ValueError(f"dtype must be 'f64' or 'f32', not {dtype!r}")
+        cfg.setdefault("precision", PGMG_PRECISION_FP32 if dtype == "f32" else PGMG_PRECISION_FP64)
         if hub is not None:
             cfg["flags"] = cfg.get("flags", 0) | PGMG_FLAG_LOOPBACK
             cfg["world"] = hub.world
@@ -204,6 +208,13 @@ class Solver:
         v = C.c_int()
         check(self.lib.pgmg_fused(self.h, C.byref(v)), "pgmg_fused")
         return bool(v.value)
+
+    @property
+    def elem_bytes(self):
+        """8 (fp64) or 4 (fp32): bytes per grid element on the device."""
+        p, e = C.c_int(), C.c_int()
+        check(self.lib.pgmg_precision(self.h, C.byref(p), C.byref(e)), "pgmg_precision")
+        return e.value
 
     def bench_sweep(self, reps):
         m = C.c_double()

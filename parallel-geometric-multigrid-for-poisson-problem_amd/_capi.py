@@ -27,6 +27,9 @@ PGMG_FLAG_UNFUSED = 4
 PGMG_FLAG_LOOPBACK = 8
 PGMG_FLAG_NO_CROSS = 16
 
+PGMG_PRECISION_FP64 = 0
+PGMG_PRECISION_FP32 = 1
+
 
 class PgmgConfig(C.Structure):
     _fields_ = [
@@ -47,6 +50,7 @@ class PgmgConfig(C.Structure):
         ("world", C.c_int),
         ("nccl_unique_id", C.c_void_p),
         ("gather_n", C.c_int),
+        ("precision", C.c_int),
     ]
 
 
@@ -74,6 +78,7 @@ SIGNATURES = [
     ("pgmg_fine_sweep_time", C.c_int, [_P, C.POINTER(C.c_int), _DP]),
     ("pgmg_fine_pass_time", C.c_int, [_P, C.c_int, C.POINTER(C.c_int), _DP]),
     ("pgmg_fused", C.c_int, [_P, C.POINTER(C.c_int)]),
+    ("pgmg_precision", C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("pgmg_bench_sweep", C.c_int, [_P, C.c_int, _DP]),
     ("pgmg_jacobi", C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_double, C.c_int, C.c_double,
                               C.POINTER(C.c_int), _P]),

@@ -296,18 +296,18 @@ class StripComm : public Comm {
 
     int setup(pgmg_ctx *) override { return PGMG_OK; }
 
-    int halo(double *o, const Level &L, int depth, hipStream_t s) override
+    int halo(const Grid &g, const Level &L, int depth, hipStream_t s) override
     {
-        const size_t row = (size_t)L.P * sizeof(double);
+        const size_t row = (size_t)L.P * L.es;
         int e = t->group_start();
         if (e) return e;
         if (me > 0) {
-            if ((e = t->send(o + (size_t)L.lo * L.P, depth * row, me - 1, s))) return e;
-            if ((e = t->recv(o + (ptrdiff_t)(L.lo - depth) * L.P, depth * row, me - 1, s))) return e;
+            if ((e = t->send(row_ptr(g, L.lo, L.P, L.es), depth * row, me - 1, s))) return e;
+            if ((e = t->recv(row_ptr(g, L.lo - depth, L.P, L.es), depth * row, me - 1, s))) return e;
         }
         if (me < world - 1) {
-            if ((e = t->send(o + (ptrdiff_t)(L.hi - depth) * L.P, depth * row, me + 1, s))) return e;
-            if ((e = t->recv(o + (size_t)L.hi * L.P, depth * row, me + 1, s))) return e;
+            if ((e = t->send(row_ptr(g, L.hi - depth, L.P, L.es), depth * row, me + 1, s))) return e;
+            if ((e = t->recv(row_ptr(g, L.hi, L.P, L.es), depth * row, me + 1, s))) return e;
         }
         return t->group_end(s);
     }
@@ -317,15 +317,15 @@ class StripComm : public Comm {
     int run_gathered(pgmg_ctx *c, int l, int gamma, int repeats) override
     {
         Level &L = c->lv[l];
-        const size_t row = (size_t)L.P * sizeof(double);
+        const size_t row = (size_t)L.P * L.es;
         // 1. rows of the coarse right-hand side -> rank 0
         int e = t->group_start();
         if (e) return e;
         for (int r = 0; r < world; ++r) {
             const int a = std::max(strip_lo(r, l), 1), b = std::min(strip_hi(r, l, L.N), L.N - 1);
             if (b <= a || r == 0) continue;
-            if (me == r && (e = t->send(L.F.o + (size_t)a * L.P, (b - a) * row, 0, c->s))) return e;
-            if (me == 0 && (e = t->recv(L.F.o + (size_t)a * L.P, (b - a) * row, r, c->s))) return e;
+            if (me == r && (e = t->send(row_ptr(L.F, a, L.P, L.es), (b - a) * row, 0, c->s))) return e;
+            if (me == 0 && (e = t->recv(row_ptr(L.F, a, L.P, L.es), (b - a) * row, r, c->s))) return e;
         }
         if ((e = t->group_end(c->s))) return e;
         // 2. rank 0 runs the rest of the hierarchy alone
@@ -338,8 +338,8 @@ class StripComm : public Comm {
         for (int r = 1; r < world; ++r) {
             const int a = std::max(strip_lo(r, l) - 2, 0);
             const int b = std::min(strip_hi(r, l, L.N) + 2, L.N);
-            if (me == 0 && (e = t->send(L.A.o + (size_t)a * L.P, (b - a) * row, r, c->s))) return e;
-            if (me == r && (e = t->recv(L.A.o + (size_t)a * L.P, (b - a) * row, 0, c->s))) return e;
+            if (me == 0 && (e = t->send(row_ptr(L.A, a, L.P, L.es), (b - a) * row, r, c->s))) return e;
+            if (me == r && (e = t->recv(row_ptr(L.A, a, L.P, L.es), (b - a) * row, 0, c->s))) return e;
         }
         return t->group_end(c->s);
     }
@@ -348,29 +348,25 @@ class StripComm : public Comm {
     {
         Level &L = c->lv[0];
         const int N = L.N;
-        double *full = nullptr;
-        PGMG_HIPC(hipMalloc((void **)&full, (size_t)N * L.P * sizeof(double)));
-        PGMG_HIPC(hipMemcpy2DAsync(full + (size_t)L.lo * L.P, L.P * sizeof(double),
-                                   L.A.o + (size_t)L.lo * L.P, L.P * sizeof(double),
-                                   N * sizeof(double), L.hi - L.lo, hipMemcpyDeviceToDevice, c->s));
-        const size_t row = (size_t)L.P * sizeof(double);
+        const size_t row = (size_t)L.P * L.es;
+        Grid full;
+        PGMG_HIPC(hipMalloc(&full.base, (size_t)N * row));
+        full.o = full.base;
+        PGMG_HIPC(hipMemcpyAsync(row_ptr(full, L.lo, L.P, L.es), row_ptr(L.A, L.lo, L.P, L.es),
+                                 (L.hi - L.lo) * row, hipMemcpyDeviceToDevice, c->s));
         int e = t->group_start();
         for (int r = 0; r < world && !e; ++r) {
             if (r == me) continue;
-            e = t->send(L.A.o + (size_t)L.lo * L.P, (L.hi - L.lo) * row, r, c->s);
+            e = t->send(row_ptr(L.A, L.lo, L.P, L.es), (L.hi - L.lo) * row, r, c->s);
             if (!e) {
                 const int a = strip_lo(r, 0), b = strip_hi(r, 0, N);
-                e = t->recv(full + (size_t)a * L.P, (b - a) * row, r, c->s);
+                e = t->recv(row_ptr(full, a, L.P, L.es), (b - a) * row, r, c->s);
             }
         }
         if (!e) e = t->group_end(c->s);
-        if (!e) {
-            hipError_t he = hipMemcpy2DAsync(phi, N * sizeof(double), full, L.P * sizeof(double),
-                                             N * sizeof(double), N, hipMemcpyDeviceToHost, c->s);
-            if (he == hipSuccess) he = hipStreamSynchronize(c->s);
-            if (he != hipSuccess) e = set_err(PGMG_ERR_HIP, hipGetErrorString(he));
-        }
-        (void)hipFree(full);
+        if (!e) e = download_grid(c, full.o, L.P, N, phi);
+        (void)hipStreamSynchronize(c->s);
+        (void)hipFree(full.base);
         return e;
     }
 };

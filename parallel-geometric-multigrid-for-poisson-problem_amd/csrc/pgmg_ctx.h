@@ -23,12 +23,21 @@ int set_err(int code, const std::string &msg);
     } while (0)
 
 struct Grid {
-    double *base = nullptr;  // allocation
-    double *o = nullptr;     // virtual origin: element (global row j, col i) at o[j*P + i]
+    void *base = nullptr;    // allocation
+    void *o = nullptr;       // virtual origin: element (global row j, col i) at o[j*P + i]
 };
 
+// typed view of a grid's origin (T = the context's element type)
+template <class T> inline T *G(const Grid &g) { return static_cast<T *>(g.o); }
+// element (row, 0) of a grid with element size es and pitch P, as bytes
+inline char *row_ptr(const Grid &g, long long row, int P, int es)
+{
+    return static_cast<char *>(g.o) + row * (long long)P * es;
+}
+
 struct Level {
-    int N = 0, P = 0;
+    int N = 0, P = 0;        // points per side, row pitch (elements)
+    int es = 8;              // element bytes: 8 (fp64) or 4 (fp32)
     double h = 0, hh = 0, ih = 0;
     int lo = 0, hi = 0;      // owned global rows [lo, hi) (row 0 / N-1 belong to the ends)
     int u0 = 0, u1 = 0;      // interior rows this rank updates: [max(lo,1), min(hi,N-1))
@@ -43,6 +52,7 @@ class Comm;
 
 struct pgmg_ctx {
     pgmg_config cfg{};
+    bool fp32 = false;            // PGMG_PRECISION_FP32: every level grid stores float
     hipStream_t s = nullptr;
     std::vector<pgmg::Level> lv;  // 0 .. nb-1 bulk levels, nb = the tail's top level
     int nb = 0;
@@ -78,8 +88,12 @@ namespace pgmg {
 
 int alloc_grid(Grid &g, const Level &L);
 void free_grid(Grid &g);
+// dispatch on the context's element type
 int enqueue_cycle(pgmg_ctx *c, int l, int gamma, bool x0_zero);
 int enqueue_tail(pgmg_ctx *c, int gamma, bool x0_from_global);
+// copy rows [0, N) of a level-0-shaped grid (origin o, pitch P, the context's element
+// type) to a dense host array of doubles (synchronous)
+int download_grid(pgmg_ctx *c, const void *o, int P, int N, double *host);
 
 // Row-strip domain decomposition (one process per GPU, RCCL), pgmg_comm.hip.
 // Levels 0 .. gathered_level()-1 are split into row strips with halo exchange;
@@ -94,7 +108,7 @@ class Comm {
     virtual int gathered_level() const = 0;
     virtual int rank() const = 0;
     // exchange `depth` halo rows of a strip-distributed level-l array (origin `o`)
-    virtual int halo(double *o, const Level &L, int depth, hipStream_t s) = 0;
+    virtual int halo(const Grid &g, const Level &L, int depth, hipStream_t s) = 0;
     // in-place sum of one device double over all ranks
     virtual int allreduce_sum(double *d_scalar, hipStream_t s) = 0;
     // the parent produced rc of gathered level l: move it to rank 0, run `repeats`

@@ -49,13 +49,15 @@ int pgmg::alloc_grid(Grid &g, const Level &L)
     // owned rows + kHalo halo rows each side (the fused passes read 4 rows past a
     // segment); the slack covers the last wave tile reading past the row end
     const int rows = (L.hi - L.lo) + 2 * kHalo;
-    const size_t n = (size_t)kOff + (size_t)rows * L.P + 512;
+    // column 1 of every row on a 128-byte boundary: 128/es - 1 elements before (0,0)
+    const size_t off = (size_t)(128 / L.es - 1);
+    const size_t n = off + (size_t)rows * L.P + 512;
     void *p = nullptr;
-    if (hipMalloc(&p, n * sizeof(double)) != hipSuccess)
+    if (hipMalloc(&p, n * L.es) != hipSuccess)
         return set_err(PGMG_ERR_NOMEM, "hipMalloc failed for a level of N=" + std::to_string(L.N));
-    HIPC(hipMemset(p, 0, n * sizeof(double)));
-    g.base = (double *)p;
-    g.o = g.base + kOff + (ptrdiff_t)(kHalo - L.lo) * L.P;
+    HIPC(hipMemset(p, 0, n * L.es));
+    g.base = p;
+    g.o = static_cast<char *>(p) + (off + (ptrdiff_t)(kHalo - L.lo) * L.P) * L.es;
     return PGMG_OK;
 }
 
@@ -73,13 +75,13 @@ static unsigned *smooth_flags(pgmg_ctx *c, int l, int which)
     return c->flags + ((size_t)l * 2 + which) * kMaxSweeps;
 }
 
-static double *const kZeroMarker = nullptr;
-
 static int timed_begin(pgmg_ctx *c, int slot);
 static int timed_end(pgmg_ctx *c, int slot, int idx);
-static int enqueue_children(pgmg_ctx *c, int l, int gamma);
+template <class T> static int enqueue_children(pgmg_ctx *c, int l, int gamma);
+template <class T> static int enqueue_cycle_t(pgmg_ctx *c, int l, int gamma, bool x0_zero);
 
 // one JacobiSmoother::smooth(x = L.A, f = L.F, num_iter = v) on a bulk level
+template <class T>
 static int enqueue_smooth(pgmg_ctx *c, int l, int which, int v, bool x0_zero)
 {
     Level &L = c->lv[l];
@@ -87,22 +89,22 @@ static int enqueue_smooth(pgmg_ctx *c, int l, int which, int v, bool x0_zero)
     unsigned *D = smooth_flags(c, l, which);
     const bool fine = (l == 0);
     for (int k = 1; k <= S; ++k) {
-        double *in = (k & 1) ? L.A.o : L.B.o;
-        double *out = (k & 1) ? L.B.o : L.A.o;
+        T *in = G<T>((k & 1) ? L.A : L.B);
+        T *out = G<T>((k & 1) ? L.B : L.A);
         if (is_dist(c, l) && !(k == 1 && x0_zero)) {
-            int e = c->comm->halo(in, L, 1, c->s);
+            int e = c->comm->halo((k & 1) ? L.A : L.B, L, 1, c->s);
             if (e) return e;
         }
-        SweepArgs a{};
-        a.xin = (k == 1 && x0_zero) ? kZeroMarker : in;
-        a.f = L.F.o;
+        SweepArgsT<T> a{};
+        a.xin = (k == 1 && x0_zero) ? nullptr : in;
+        a.f = G<T>(L.F);
         a.xout = out;
         a.partials = (k >= 2) ? c->partials : nullptr;
         a.skip = (k >= 2) ? &D[k - 1] : nullptr;
         a.reset = (k == 1) ? &D[1] : nullptr;
         a.stats = c->stats;
-        a.hh = L.hh;
-        a.inv_hh = L.ih;
+        a.hh = (T)L.hh;
+        a.inv_hh = (T)L.ih;
         a.W = L.N;
         a.P = L.P;
         a.row0 = L.u0;
@@ -114,7 +116,7 @@ static int enqueue_smooth(pgmg_ctx *c, int l, int which, int v, bool x0_zero)
         if (k >= 2) {
             int rpb, gx, gy;
             const int np = sweep_blocks(L.N, L.u0, L.u1, &rpb, &gx, &gy);
-            FixupArgs f{};
+            FixupArgsT<T> f{};
             f.partials = c->partials;
             f.np = np;
             f.eps = c->cfg.eps;
@@ -137,19 +139,20 @@ static int enqueue_smooth(pgmg_ctx *c, int l, int which, int v, bool x0_zero)
             launch_fixup(f, c->s);
         }
     }
-    if (S & 1) launch_copy_rows(L.B.o, L.A.o, L.N, L.P, L.u0, L.u1, c->s);
+    if (S & 1) launch_copy_rows(G<T>(L.B), G<T>(L.A), L.N, L.P, L.u0, L.u1, c->s);
     return PGMG_OK;
 }
 
-int pgmg::enqueue_tail(pgmg_ctx *c, int gamma, bool x0_from_global)
+template <class T>
+static int enqueue_tail_t(pgmg_ctx *c, int gamma, bool x0_from_global)
 {
-    Level &T = c->lv[c->nb];
-    TailArgs t{};
-    t.f_top = T.F.o;
-    t.e_top = T.A.o;
-    t.P_top = T.P;
-    t.N_top = T.N;
-    t.h_top = T.h;
+    Level &Lt = c->lv[c->nb];
+    TailArgsT<T> t{};
+    t.f_top = G<T>(Lt.F);
+    t.e_top = G<T>(Lt.A);
+    t.P_top = Lt.P;
+    t.N_top = Lt.N;
+    t.h_top = Lt.h;
     t.x0_from_global = x0_from_global ? 1 : 0;
     t.v1 = c->cfg.v1;
     t.v2 = c->cfg.v2;
@@ -159,6 +162,12 @@ int pgmg::enqueue_tail(pgmg_ctx *c, int gamma, bool x0_from_global)
     t.stats = c->stats;
     HIPC(launch_tail_gamma(t, gamma, c->s));
     return PGMG_OK;
+}
+
+int pgmg::enqueue_tail(pgmg_ctx *c, int gamma, bool x0_from_global)
+{
+    return c->fp32 ? enqueue_tail_t<float>(c, gamma, x0_from_global)
+                   : enqueue_tail_t<double>(c, gamma, x0_from_global);
 }
 
 static int timed_begin(pgmg_ctx *c, int slot)
@@ -179,12 +188,13 @@ static int timed_end(pgmg_ctx *c, int slot, int idx)
 }
 
 // children of level l: gamma cycles on level l+1 (on rank 0 alone if it is gathered)
+template <class T>
 static int enqueue_children(pgmg_ctx *c, int l, int gamma)
 {
     if (c->comm && l + 1 == c->comm->gathered_level())
         return c->comm->run_gathered(c, l + 1, gamma, gamma);
     for (int i = 0; i < gamma; ++i) {
-        int e = enqueue_cycle(c, l + 1, gamma, i == 0);
+        int e = enqueue_cycle_t<T>(c, l + 1, gamma, i == 0);
         if (e) return e;
     }
     return PGMG_OK;
@@ -200,6 +210,7 @@ static int global_sum(pgmg_ctx *c, int np, const double **out)
 }
 
 // fused level (v1 = v2 = 1): k_pre (+fixup), children, k_post (+fixup)
+template <class T>
 static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
 {
     Level &L = c->lv[l];
@@ -211,19 +222,19 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
     unsigned *fired = smooth_flags(c, l, 0) + (kMaxSweeps - 1);
     int e;
     if (dist) {
-        if (!x0_zero && (e = c->comm->halo(L.A.o, L, 4, c->s))) return e;
-        if (l > 0 && (e = c->comm->halo(L.F.o, L, 4, c->s))) return e;
+        if (!x0_zero && (e = c->comm->halo(L.A, L, 4, c->s))) return e;
+        if (l > 0 && (e = c->comm->halo(L.F, L, 4, c->s))) return e;
     }
-    PreArgs pa{};
-    pa.x0 = L.A.o;
-    pa.f = L.F.o;
-    pa.x2 = recomp ? nullptr : L.B.o;
+    PreArgsT<T> pa{};
+    pa.x0 = G<T>(L.A);
+    pa.f = G<T>(L.F);
+    pa.x2 = recomp ? nullptr : G<T>(L.B);
     pa.fired = recomp ? fired : nullptr;
-    pa.rc = C.F.o;
+    pa.rc = G<T>(C.F);
     pa.partials = c->partials;
     pa.stats = c->stats;
-    pa.hh = L.hh;
-    pa.ih = L.ih;
+    pa.hh = (T)L.hh;
+    pa.ih = (T)L.ih;
     pa.N = L.N;
     pa.P = L.P;
     pa.Nc = C.N;
@@ -246,21 +257,21 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
     if ((e = timed_end(c, 1, ev))) return e;
     if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
     launch_pre_fixup(fa, pa, x0_zero, c->s);
-    if ((e = enqueue_children(c, l, gamma))) return e;
+    if ((e = enqueue_children<T>(c, l, gamma))) return e;
     if (dist) {
-        if (!recomp && (e = c->comm->halo(L.B.o, L, 2, c->s))) return e;
-        if (is_dist(c, l + 1) && (e = c->comm->halo(C.A.o, C, 2, c->s))) return e;
+        if (!recomp && (e = c->comm->halo(L.B, L, 2, c->s))) return e;
+        if (is_dist(c, l + 1) && (e = c->comm->halo(C.A, C, 2, c->s))) return e;
     }
-    PostArgs po{};
-    po.phi = L.B.o;
+    PostArgsT<T> po{};
+    po.phi = G<T>(L.B);
     po.pre_fired = recomp ? fired : nullptr;
-    po.ec = C.A.o;
-    po.f = L.F.o;
-    po.x2 = L.A.o;
+    po.ec = G<T>(C.A);
+    po.f = G<T>(L.F);
+    po.x2 = G<T>(L.A);
     po.partials = c->partials;
     po.stats = c->stats;
-    po.hh = L.hh;
-    po.ih = L.ih;
+    po.hh = (T)L.hh;
+    po.ih = (T)L.ih;
     po.N = L.N;
     po.P = L.P;
     po.Nc = C.N;
@@ -286,18 +297,19 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
 // alternate; at the end the solution is moved back under L.A by swapping the
 // host pointers (B always mirrors A's boundary, so either may play either role).
 // ---------------------------------------------------------------------------
-static PreArgs make_pre(pgmg_ctx *c, const double *x0, double *x2)
+template <class T>
+static PreArgsT<T> make_pre(pgmg_ctx *c, const T *x0, T *x2)
 {
     Level &L = c->lv[0], &C = c->lv[1];
-    PreArgs pa{};
+    PreArgsT<T> pa{};
     pa.x0 = x0;
-    pa.f = L.F.o;
+    pa.f = G<T>(L.F);
     pa.x2 = x2;
-    pa.rc = C.F.o;
+    pa.rc = G<T>(C.F);
     pa.partials = c->partials;
     pa.stats = c->stats;
-    pa.hh = L.hh;
-    pa.ih = L.ih;
+    pa.hh = (T)L.hh;
+    pa.ih = (T)L.ih;
     pa.N = L.N;
     pa.P = L.P;
     pa.Nc = C.N;
@@ -311,18 +323,19 @@ static PreArgs make_pre(pgmg_ctx *c, const double *x0, double *x2)
     return pa;
 }
 
-static PostArgs make_post(pgmg_ctx *c, const double *phi, double *x2)
+template <class T>
+static PostArgsT<T> make_post(pgmg_ctx *c, const T *phi, T *x2)
 {
     Level &L = c->lv[0], &C = c->lv[1];
-    PostArgs po{};
+    PostArgsT<T> po{};
     po.phi = phi;
-    po.ec = C.A.o;
-    po.f = L.F.o;
+    po.ec = G<T>(C.A);
+    po.f = G<T>(L.F);
     po.x2 = x2;
     po.partials = c->partials;
     po.stats = c->stats;
-    po.hh = L.hh;
-    po.ih = L.ih;
+    po.hh = (T)L.hh;
+    po.ih = (T)L.ih;
     po.N = L.N;
     po.P = L.P;
     po.Nc = C.N;
@@ -334,10 +347,12 @@ static PostArgs make_post(pgmg_ctx *c, const double *phi, double *x2)
     return po;
 }
 
+template <class T>
 static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
 {
     Level &L = c->lv[0], &C = c->lv[1];
-    double *A = L.A.o, *B = L.B.o;
+    T *A = G<T>(L.A), *B = G<T>(L.B);
+    T *S = G<T>(c->S);
     const int np = fused_blocks(L.N, 0, (L.N - 1) / 2);
     FixArgsF fa{};
     fa.partials = c->partials;
@@ -346,26 +361,26 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
     fa.stats = c->stats;
     int e;
     // cycle 1: pre-smooth (+ residual, restriction) A -> B
-    PreArgs pa = make_pre(c, A, B);
+    PreArgsT<T> pa = make_pre<T>(c, A, B);
     int ev = timed_begin(c, 1);
     launch_pre(pa, false, true, c->s);
     if ((e = timed_end(c, 1, ev))) return e;
     launch_pre_fixup(fa, pa, false, c->s);
-    double *pr = B;  // pre-smoothed solution of the current cycle
-    if ((e = enqueue_children(c, 0, gamma))) return e;
+    T *pr = B;  // pre-smoothed solution of the current cycle
+    if ((e = enqueue_children<T>(c, 0, gamma))) return e;
     for (int k = 1; k < n; ++k) {
-        double *nx = (pr == A) ? B : A;
-        PostPreArgs q{};
+        T *nx = (pr == A) ? B : A;
+        PostPreArgsT<T> q{};
         q.phi = pr;
-        q.ec = C.A.o;
-        q.f = L.F.o;
+        q.ec = G<T>(C.A);
+        q.f = G<T>(L.F);
         q.x4 = nx;
-        q.rc = C.F.o;
+        q.rc = G<T>(C.F);
         q.partials1 = c->partials;
         q.partials2 = c->partials2;
         q.stats = c->stats;
-        q.hh = L.hh;
-        q.ih = L.ih;
+        q.hh = (T)L.hh;
+        q.ih = (T)L.ih;
         q.N = L.N;
         q.P = L.P;
         q.Nc = C.N;
@@ -379,16 +394,17 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         ev = timed_begin(c, 3);
         launch_postpre(q, c->s);
         if ((e = timed_end(c, 3, ev))) return e;
-        launch_postpre_decide(q, postpre_blocks(L.N, 0, (L.N - 1) / 2), c->cfg.eps, c->ppflags, c->s);
+        launch_postpre_decide(q.partials1, q.partials2, q.stats, postpre_blocks(L.N, 0, (L.N - 1) / 2),
+                              c->cfg.eps, c->ppflags, c->s);
         // rare path 1 (post check fired): S = x1 of the post-smooth, then a full
         // pre-smooth from S (conditional k_pre + its own fix-up)
-        PostArgs po = make_post(c, pr, c->S.o);
+        PostArgsT<T> po = make_post<T>(c, pr, S);
         FixArgsF f1 = fa;
         f1.cond = &c->ppflags[0];
         f1.force = 1;
         f1.stats = nullptr;
         launch_post_fixup(f1, po, c->s);
-        PreArgs p1 = make_pre(c, c->S.o, nx);
+        PreArgsT<T> p1 = make_pre<T>(c, S, nx);
         p1.cond = &c->ppflags[0];
         launch_pre(p1, false, false, c->s);
         FixArgsF f1b = fa;
@@ -396,22 +412,22 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         launch_pre_fixup(f1b, p1, false, c->s);
         // rare path 2 (only the pre check fired): S = x2 of the post-smooth, then the
         // pre-smooth result is J(S) and rc = R r(J(S))
-        PostArgs p2 = make_post(c, pr, c->S.o);
+        PostArgsT<T> p2 = make_post<T>(c, pr, S);
         p2.cond = &c->ppflags[1];
         p2.stats = nullptr;
         launch_post(p2, false, c->s);
-        PreArgs p3 = make_pre(c, c->S.o, nx);
+        PreArgsT<T> p3 = make_pre<T>(c, S, nx);
         FixArgsF f2 = fa;
         f2.cond = &c->ppflags[1];
         f2.force = 1;
         f2.stats = nullptr;
         launch_pre_fixup(f2, p3, false, c->s);
         pr = nx;
-        if ((e = enqueue_children(c, 0, gamma))) return e;
+        if ((e = enqueue_children<T>(c, 0, gamma))) return e;
     }
     // last cycle: post-smooth
-    double *out = (pr == A) ? B : A;
-    PostArgs po = make_post(c, pr, out);
+    T *out = (pr == A) ? B : A;
+    PostArgsT<T> po = make_post<T>(c, pr, out);
     ev = timed_begin(c, 2);
     launch_post(po, true, c->s);
     if ((e = timed_end(c, 2, ev))) return e;
@@ -421,23 +437,24 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
 }
 
 // MultigridSolver::v_cycle / w_cycle (MultiGrid.hpp:57-136) on level l
-int pgmg::enqueue_cycle(pgmg_ctx *c, int l, int gamma, bool x0_zero)
+template <class T>
+static int enqueue_cycle_t(pgmg_ctx *c, int l, int gamma, bool x0_zero)
 {
-    if (l == c->nb) return enqueue_tail(c, gamma, !x0_zero);
-    if (c->fused) return enqueue_fused_level(c, l, gamma, x0_zero);
+    if (l == c->nb) return enqueue_tail_t<T>(c, gamma, !x0_zero);
+    if (c->fused) return enqueue_fused_level<T>(c, l, gamma, x0_zero);
     Level &L = c->lv[l];
     Level &C = c->lv[l + 1];
     const bool dist = is_dist(c, l);
     int e;
-    if (dist && l > 0 && (e = c->comm->halo(L.F.o, L, 1, c->s))) return e;
-    e = enqueue_smooth(c, l, 0, c->cfg.v1, x0_zero);
+    if (dist && l > 0 && (e = c->comm->halo(L.F, L, 1, c->s))) return e;
+    e = enqueue_smooth<T>(c, l, 0, c->cfg.v1, x0_zero);
     if (e) return e;
-    if (dist && (e = c->comm->halo(L.A.o, L, 2, c->s))) return e;
-    ResRestrictArgs r{};
-    r.x = L.A.o;
-    r.f = L.F.o;
-    r.rc = C.F.o;
-    r.inv_hh = L.ih;
+    if (dist && (e = c->comm->halo(L.A, L, 2, c->s))) return e;
+    ResRestrictArgsT<T> r{};
+    r.x = G<T>(L.A);
+    r.f = G<T>(L.F);
+    r.rc = G<T>(C.F);
+    r.inv_hh = (T)L.ih;
     r.Wf = L.N;
     r.Pf = L.P;
     r.Wc = C.N;
@@ -446,11 +463,11 @@ int pgmg::enqueue_cycle(pgmg_ctx *c, int l, int gamma, bool x0_zero)
     r.jc0 = L.lo / 2 > 1 ? L.lo / 2 : 1;
     r.jc1 = (L.hi + 1) / 2 < C.N - 1 ? (L.hi + 1) / 2 : C.N - 1;
     launch_res_restrict(r, c->s);
-    if ((e = enqueue_children(c, l, gamma))) return e;
-    if (dist && is_dist(c, l + 1) && (e = c->comm->halo(C.A.o, C, 2, c->s))) return e;
-    ProlongArgs p{};
-    p.c = C.A.o;
-    p.fine = L.A.o;
+    if ((e = enqueue_children<T>(c, l, gamma))) return e;
+    if (dist && is_dist(c, l + 1) && (e = c->comm->halo(C.A, C, 2, c->s))) return e;
+    ProlongArgsT<T> p{};
+    p.c = G<T>(C.A);
+    p.fine = G<T>(L.A);
     p.Wf = L.N;
     p.Pf = L.P;
     p.Wc = C.N;
@@ -458,7 +475,13 @@ int pgmg::enqueue_cycle(pgmg_ctx *c, int l, int gamma, bool x0_zero)
     p.row0 = L.u0 > 2 ? L.u0 : 2;
     p.row1 = L.u1 < L.N - 1 ? L.u1 : L.N - 1;
     if (p.row1 > p.row0) launch_prolong(p, c->s);
-    return enqueue_smooth(c, l, 1, c->cfg.v2, false);
+    return enqueue_smooth<T>(c, l, 1, c->cfg.v2, false);
+}
+
+int pgmg::enqueue_cycle(pgmg_ctx *c, int l, int gamma, bool x0_zero)
+{
+    return c->fp32 ? enqueue_cycle_t<float>(c, l, gamma, x0_zero)
+                   : enqueue_cycle_t<double>(c, l, gamma, x0_zero);
 }
 
 // ---------------------------------------------------------------------------
@@ -467,7 +490,7 @@ int pgmg::enqueue_cycle(pgmg_ctx *c, int l, int gamma, bool x0_zero)
 extern "C" {
 
 const char *pgmg_last_error(void) { return g_err.c_str(); }
-const char *pgmg_version(void) { return "pgmg 0.1 (gfx950, fp64, row-strip RCCL)"; }
+const char *pgmg_version(void) { return "pgmg 0.2 (gfx950, fp64 | fp32, row-strip RCCL)"; }
 
 int pgmg_config_default(pgmg_config *cfg, int N)
 {
@@ -490,6 +513,7 @@ int pgmg_config_default(pgmg_config *cfg, int N)
     cfg->world = 1;
     cfg->nccl_unique_id = nullptr;
     cfg->gather_n = 1025;
+    cfg->precision = PGMG_PRECISION_FP64;
     return PGMG_OK;
 }
 
@@ -540,6 +564,8 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         return set_err(PGMG_ERR_ARG, "bad smoother/cycle parameters");
     if (cfg->world < 1 || cfg->rank < 0 || cfg->rank >= cfg->world)
         return set_err(PGMG_ERR_ARG, "bad rank/world");
+    if (cfg->precision != PGMG_PRECISION_FP64 && cfg->precision != PGMG_PRECISION_FP32)
+        return set_err(PGMG_ERR_ARG, "precision must be PGMG_PRECISION_FP64 or _FP32");
     int ndev = 0;
     HIPC(hipGetDeviceCount(&ndev));
     if (cfg->device < 0 || cfg->device >= ndev) return set_err(PGMG_ERR_ARG, "bad device ordinal");
@@ -547,6 +573,7 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
 
     pgmg_ctx *c = new pgmg_ctx();
     c->cfg = *cfg;
+    c->fp32 = cfg->precision == PGMG_PRECISION_FP32;
     int tail_n = cfg->tail_n;
     if (tail_n > kTailMaxN) tail_n = kTailMaxN;
     if (tail_n < cfg->n_coarse) tail_n = cfg->n_coarse;
@@ -558,7 +585,8 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
     for (;;) {
         Level L;
         L.N = N;
-        L.P = pitch_for(N);
+        L.es = c->fp32 ? 4 : 8;
+        L.P = c->fp32 ? pitch_elems<float>(N) : pitch_elems<double>(N);
         L.h = h;
         L.hh = h * h;
         L.ih = 1.0 / (h * h);
@@ -670,6 +698,50 @@ static void sine_tables(const pgmg_config &cfg, int N, double h, std::vector<dou
     }
 }
 
+}  // extern "C"
+
+// rows [r0, r1) of a dense host array (pitch N) -> grid g (the context's element type)
+static int upload_rows(pgmg_ctx *c, const Level &L, const Grid &g, const double *host, int r0,
+                       int r1)
+{
+    const int N = L.N;
+    const size_t rows = (size_t)(r1 - r0);
+    if (!c->fp32) {
+        HIPC(hipMemcpy2D(row_ptr(g, r0, L.P, 8), L.P * sizeof(double), host + (size_t)r0 * N,
+                         N * sizeof(double), N * sizeof(double), rows, hipMemcpyHostToDevice));
+        return PGMG_OK;
+    }
+    // fp32: stage the doubles on the device, narrow there
+    double *d = nullptr;
+    HIPC(hipMalloc((void **)&d, rows * N * sizeof(double)));
+    HIPC(hipMemcpy(d, host + (size_t)r0 * N, rows * N * sizeof(double), hipMemcpyHostToDevice));
+    launch_from_double(d - (size_t)r0 * N, N, G<float>(g), L.P, r0, r1, c->s);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(c->s));
+    HIPC(hipFree(d));
+    return PGMG_OK;
+}
+
+int pgmg::download_grid(pgmg_ctx *c, const void *o, int P, int N, double *host)
+{
+    if (!c->fp32) {
+        HIPC(hipMemcpy2DAsync(host, N * sizeof(double), o, P * sizeof(double), N * sizeof(double),
+                              N, hipMemcpyDeviceToHost, c->s));
+        HIPC(hipStreamSynchronize(c->s));
+        return PGMG_OK;
+    }
+    double *d = nullptr;
+    HIPC(hipMalloc((void **)&d, (size_t)N * N * sizeof(double)));
+    launch_to_double(static_cast<const float *>(o), P, d, N, 0, N, c->s);
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(host, d, (size_t)N * N * sizeof(double), hipMemcpyDeviceToHost, c->s));
+    HIPC(hipStreamSynchronize(c->s));
+    HIPC(hipFree(d));
+    return PGMG_OK;
+}
+
+extern "C" {
+
 int pgmg_set_problem(pgmg_ctx *c, const double *phi0, const double *f)
 {
     if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
@@ -680,20 +752,20 @@ int pgmg_set_problem(pgmg_ctx *c, const double *phi0, const double *f)
     const int r0 = L.lo - kHalo > 0 ? L.lo - kHalo : 0;
     const int r1 = L.hi + kHalo < N ? L.hi + kHalo : N;
     const size_t rows = (size_t)(r1 - r0);
+    const size_t pitch = (size_t)L.P * L.es, width = (size_t)N * L.es;
+    int e;
     HIPC(hipStreamSynchronize(c->s));
     // phi (and its boundary copy in the ping-pong buffer B)
     if (phi0) {
-        HIPC(hipMemcpy2D(L.A.o + (size_t)r0 * L.P, L.P * sizeof(double), phi0 + (size_t)r0 * N,
-                         N * sizeof(double), N * sizeof(double), rows, hipMemcpyHostToDevice));
+        if ((e = upload_rows(c, L, L.A, phi0, r0, r1))) return e;
     } else {
-        HIPC(hipMemset2D(L.A.o + (size_t)r0 * L.P, L.P * sizeof(double), 0, N * sizeof(double), rows));
+        HIPC(hipMemset2D(row_ptr(L.A, r0, L.P, L.es), pitch, 0, width, rows));
     }
     if (c->nb > 0)
-        HIPC(hipMemcpy2D(L.B.o + (size_t)r0 * L.P, L.P * sizeof(double), L.A.o + (size_t)r0 * L.P,
-                         L.P * sizeof(double), N * sizeof(double), rows, hipMemcpyDeviceToDevice));
+        HIPC(hipMemcpy2D(row_ptr(L.B, r0, L.P, L.es), pitch, row_ptr(L.A, r0, L.P, L.es), pitch,
+                         width, rows, hipMemcpyDeviceToDevice));
     if (f) {
-        HIPC(hipMemcpy2D(L.F.o + (size_t)r0 * L.P, L.P * sizeof(double), f + (size_t)r0 * N,
-                         N * sizeof(double), N * sizeof(double), rows, hipMemcpyHostToDevice));
+        if ((e = upload_rows(c, L, L.F, f, r0, r1))) return e;
     } else {
         std::vector<double> sx, sy;
         double factor;
@@ -702,7 +774,8 @@ int pgmg_set_problem(pgmg_ctx *c, const double *phi0, const double *f)
         HIPC(hipMalloc((void **)&d, 2 * N * sizeof(double)));
         HIPC(hipMemcpy(d, sx.data(), N * sizeof(double), hipMemcpyHostToDevice));
         HIPC(hipMemcpy(d + N, sy.data(), N * sizeof(double), hipMemcpyHostToDevice));
-        launch_rhs(L.F.o, d, d + N, factor, N, L.P, r0, r1, c->s);
+        if (c->fp32) launch_rhs(G<float>(L.F), d, d + N, factor, N, L.P, r0, r1, c->s);
+        else launch_rhs(G<double>(L.F), d, d + N, factor, N, L.P, r0, r1, c->s);
         HIPC(hipGetLastError());
         HIPC(hipStreamSynchronize(c->s));
         HIPC(hipFree(d));
@@ -738,7 +811,8 @@ static int run_cycles(pgmg_ctx *c, int ncycles, int gamma)
         HIPC(hipGraphDestroy(g));
     }
     if (c->cross && !use_graph) {
-        int e = enqueue_cross_cycles(c, ncycles, gamma);
+        int e = c->fp32 ? enqueue_cross_cycles<float>(c, ncycles, gamma)
+                        : enqueue_cross_cycles<double>(c, ncycles, gamma);
         if (e) return e;
         HIPC(hipGetLastError());
         HIPC(hipEventRecord(c->ev1, c->s));
@@ -800,6 +874,9 @@ static int fmg_tables(pgmg_ctx *c)
 //   smooth(3); phi_fine = 0 + P phi; f_fine = analytic RHS; one V-cycle on the finer level.
 // The levels at or below the tail's top run inside one k_tail launch; the bulk levels use
 // the V-cycle kernels with the level's F replaced by the analytic RHS of the FMG chain.
+}  // extern "C"
+
+template <class T>
 static int enqueue_fcycle(pgmg_ctx *c)
 {
     const int nb = c->nb;
@@ -810,16 +887,16 @@ static int enqueue_fcycle(pgmg_ctx *c)
     }
     for (int l = 0; l < nb; ++l) {
         const Level &L = c->lv[l], &C = c->lv[l + 1];
-        launch_restrict_values(L.A.o, L.N, L.P, C.A.o, C.N, C.P, c->s);
+        launch_restrict_values(G<T>(L.A), L.N, L.P, G<T>(C.A), C.N, C.P, c->s);
     }
     {
-        Level &T = c->lv[nb];
-        TailArgs t{};
-        t.f_top = T.F.o;
-        t.e_top = T.A.o;
-        t.P_top = T.P;
-        t.N_top = T.N;
-        t.h_top = T.h;
+        Level &Lt = c->lv[nb];
+        TailArgsT<T> t{};
+        t.f_top = G<T>(Lt.F);
+        t.e_top = G<T>(Lt.A);
+        t.P_top = Lt.P;
+        t.N_top = Lt.N;
+        t.h_top = Lt.h;
         t.x0_from_global = 1;
         t.v1 = c->cfg.v1;
         t.v2 = c->cfg.v2;
@@ -839,12 +916,12 @@ static int enqueue_fcycle(pgmg_ctx *c)
         Level &L = c->lv[l];
         const Level &C = c->lv[l + 1];
         const double *sx = c->fmg_tab + c->fmg_off[l];
-        launch_rhs(L.F.o, sx, sx + L.N, factor, L.N, L.P, 0, L.N, c->s);
-        launch_fill_rows(L.A.o, L.P, 0, L.N, 0.0, c->s);
-        launch_fill_rows(L.B.o, L.P, 0, L.N, 0.0, c->s);
-        ProlongArgs p{};
-        p.c = C.A.o;
-        p.fine = L.A.o;
+        launch_rhs(G<T>(L.F), sx, sx + L.N, factor, L.N, L.P, 0, L.N, c->s);
+        launch_fill_rows(G<T>(L.A), L.P, 0, L.N, c->s);
+        launch_fill_rows(G<T>(L.B), L.P, 0, L.N, c->s);
+        ProlongArgsT<T> p{};
+        p.c = G<T>(C.A);
+        p.fine = G<T>(L.A);
         p.Wf = L.N;
         p.Pf = L.P;
         p.Wc = C.N;
@@ -852,12 +929,14 @@ static int enqueue_fcycle(pgmg_ctx *c)
         p.row0 = 2;
         p.row1 = L.N - 1;
         launch_prolong(p, c->s);
-        int e = enqueue_cycle(c, l, 1, false);
+        int e = enqueue_cycle_t<T>(c, l, 1, false);
         if (e) return e;
-        if (l > 0 && (e = enqueue_smooth(c, l, 0, 3, false))) return e;
+        if (l > 0 && (e = enqueue_smooth<T>(c, l, 0, 3, false))) return e;
     }
     return PGMG_OK;
 }
+
+extern "C" {
 
 int pgmg_fcycle(pgmg_ctx *c, int ncycles)
 {
@@ -881,7 +960,8 @@ int pgmg_fcycle(pgmg_ctx *c, int ncycles)
     }
     if (c->nb > 0) std::swap(L0.F, c->Ffmg);
     HIPC(hipEventRecord(c->ev0, c->s));
-    for (int k = 0; k < ncycles && !e; ++k) e = enqueue_fcycle(c);
+    for (int k = 0; k < ncycles && !e; ++k)
+        e = c->fp32 ? enqueue_fcycle<float>(c) : enqueue_fcycle<double>(c);
     if (c->nb > 0) std::swap(L0.F, c->Ffmg);
     for (int l = 0; l <= c->nb; ++l) {
         c->lv[l].h = saved[l].h;
@@ -917,9 +997,7 @@ int pgmg_get_solution(pgmg_ctx *c, double *phi)
     HIPC(hipStreamSynchronize(c->s));
     if (c->comm) return c->comm->gather_solution(c, phi);
     Level &L = c->lv[0];
-    HIPC(hipMemcpy2D(phi, L.N * sizeof(double), L.A.o, L.P * sizeof(double), L.N * sizeof(double),
-                     L.N, hipMemcpyDeviceToHost));
-    return PGMG_OK;
+    return download_grid(c, L.A.o, L.P, L.N, phi);
 }
 
 int pgmg_residual_norm(pgmg_ctx *c, double *out)
@@ -928,10 +1006,15 @@ int pgmg_residual_norm(pgmg_ctx *c, double *out)
     Level &L = c->lv[0];
     int nbk = c->partials_cap < 1024 ? c->partials_cap : 1024;
     if (c->comm) {
-        int e = c->comm->halo(L.A.o, L, 1, c->s);
+        int e = c->comm->halo(L.A, L, 1, c->s);
         if (e) return e;
     }
-    launch_resnorm_partials(L.A.o, L.F.o, c->partials, L.ih, L.N, L.P, L.u0, L.u1, nbk, c->s);
+    if (c->fp32)
+        launch_resnorm_partials(G<float>(L.A), G<float>(L.F), c->partials, (float)L.ih, L.N, L.P,
+                                L.u0, L.u1, nbk, c->s);
+    else
+        launch_resnorm_partials(G<double>(L.A), G<double>(L.F), c->partials, L.ih, L.N, L.P, L.u0,
+                                L.u1, nbk, c->s);
     launch_sum_partials(c->partials, nbk, c->scalar, c->s);
     if (c->comm) {
         int e = c->comm->allreduce_sum(c->scalar, c->s);
@@ -1006,9 +1089,17 @@ int pgmg_vcycle_bytes(pgmg_ctx *c, double *bytes)
         if (S1 & 1) b += 16.0 * n;
         if (S2 & 1) b += 16.0 * n;
     }
-    const Level &T = c->lv[c->nb];
-    b += 16.0 * (double)T.N * T.N;                               // tail: f in, e out
-    *bytes = b;
+    const Level &Lt = c->lv[c->nb];
+    b += 16.0 * (double)Lt.N * Lt.N;                             // tail: f in, e out
+    *bytes = b * (c->lv[0].es / 8.0);                            // per-point figures are fp64
+    return PGMG_OK;
+}
+
+int pgmg_precision(pgmg_ctx *c, int *precision, int *elem_bytes)
+{
+    if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
+    if (precision) *precision = c->fp32 ? PGMG_PRECISION_FP32 : PGMG_PRECISION_FP64;
+    if (elem_bytes) *elem_bytes = c->lv[0].es;
     return PGMG_OK;
 }
 
@@ -1016,37 +1107,44 @@ int pgmg_phi_device(pgmg_ctx *c, double **ptr, int *pitch, int *row0, int *rows)
 {
     if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
     Level &L = c->lv[0];
-    if (ptr) *ptr = L.A.o;
+    if (ptr) *ptr = static_cast<double *>(L.A.o);
     if (pitch) *pitch = L.P;
     if (row0) *row0 = L.lo;
     if (rows) *rows = L.hi - L.lo;
     return PGMG_OK;
 }
 
-int pgmg_bench_sweep(pgmg_ctx *c, int reps, double *ms)
+}  // extern "C"
+
+template <class T>
+static void bench_sweeps(pgmg_ctx *c, int reps)
 {
-    if (!c || !ms || reps <= 0) return set_err(PGMG_ERR_ARG, "bad argument");
-    if (c->nb == 0) return set_err(PGMG_ERR_STATE, "no bulk level");
     Level &L = c->lv[0];
-    SweepArgs a{};
-    a.f = L.F.o;
-    a.hh = L.hh;
-    a.inv_hh = L.ih;
+    SweepArgsT<T> a{};
+    a.f = G<T>(L.F);
+    a.hh = (T)L.hh;
+    a.inv_hh = (T)L.ih;
     a.W = L.N;
     a.P = L.P;
     a.row0 = L.u0;
     a.row1 = L.u1;
-    for (int k = 0; k < 2; ++k) {  // warm
-        a.xin = (k & 1) ? L.B.o : L.A.o;
-        a.xout = (k & 1) ? L.A.o : L.B.o;
-        launch_sweep(a, false, true, c->s);
-    }
-    HIPC(hipEventRecord(c->ev0, c->s));
     for (int k = 0; k < reps; ++k) {
-        a.xin = (k & 1) ? L.B.o : L.A.o;
-        a.xout = (k & 1) ? L.A.o : L.B.o;
+        a.xin = G<T>((k & 1) ? L.B : L.A);
+        a.xout = G<T>((k & 1) ? L.A : L.B);
         launch_sweep(a, false, true, c->s);
     }
+}
+
+extern "C" {
+
+int pgmg_bench_sweep(pgmg_ctx *c, int reps, double *ms)
+{
+    if (!c || !ms || reps <= 0) return set_err(PGMG_ERR_ARG, "bad argument");
+    if (c->nb == 0) return set_err(PGMG_ERR_STATE, "no bulk level");
+    auto run = [&](int n) { c->fp32 ? bench_sweeps<float>(c, n) : bench_sweeps<double>(c, n); };
+    run(2);  // warm
+    HIPC(hipEventRecord(c->ev0, c->s));
+    run(reps);
     HIPC(hipEventRecord(c->ev1, c->s));
     HIPC(hipEventSynchronize(c->ev1));
     float f = 0.f;

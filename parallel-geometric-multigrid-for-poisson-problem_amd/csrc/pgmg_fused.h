@@ -1,19 +1,22 @@
 // pgmg_fused.h — argument blocks of the fused smoother passes (pgmg_fused.hip).
+// Templates on the grid element type T (double, or float for the fp32 variant);
+// partial sums and eps stay double.
 #pragma once
 #include "pgmg_internal.h"
 
 namespace pgmg {
 
 // pre-smooth (2 sweeps) + residual + full-weighting restriction in one pass
-struct PreArgs {
-    const double *x0;           // level solution before smoothing (unused when x0 is zero)
-    const double *f;            // level right-hand side
-    double *x2;                 // result of the two sweeps (ping-pong buffer); nullptr: not
+template <class T>
+struct PreArgsT {
+    const T *x0;                // level solution before smoothing (unused when x0 is zero)
+    const T *f;                 // level right-hand side
+    T *x2;                      // result of the two sweeps (ping-pong buffer); nullptr: not
                                 // stored (x0 = 0: k_post recomputes it from f)
-    double *rc;                 // coarse right-hand side R r(x2)
+    T *rc;                      // coarse right-hand side R r(x2)
     double *partials;           // per block sum r(x1)^2 (early-exit check)
     unsigned long long *stats;  // [0] sweeps (+2 per launch)
-    double hh, ih;
+    T hh, ih;
     int N, P, Nc, Pc;
     int jc0, jc1;               // coarse-row segments [jc0, jc1) (fine rows 2jc, 2jc+1)
     int row_lo, row_hi;         // fine rows whose x2 this rank writes
@@ -24,14 +27,15 @@ struct PreArgs {
 };
 
 // prolongation + post-smooth (2 sweeps) in one pass
-struct PostArgs {
-    const double *phi;          // level solution after pre-smoothing
-    const double *ec;           // coarse-grid correction
-    const double *f;
-    double *x2;                 // result (the level's solution buffer)
+template <class T>
+struct PostArgsT {
+    const T *phi;               // level solution after pre-smoothing
+    const T *ec;                // coarse-grid correction
+    const T *f;
+    T *x2;                      // result (the level's solution buffer)
     double *partials;
     unsigned long long *stats;
-    double hh, ih;
+    T hh, ih;
     int N, P, Nc, Pc;
     int jc0, jc1;
     int row_lo, row_hi;
@@ -44,16 +48,17 @@ struct PostArgs {
 
 // post-smooth of cycle k + pre-smooth/residual/restriction of cycle k+1 in one pass
 // (the finest level between consecutive cycles of one pgmg_vcycle call)
-struct PostPreArgs {
-    const double *phi;          // pre-smoothed solution of cycle k
-    const double *ec;           // coarse correction of cycle k
-    const double *f;
-    double *x4;                 // pre-smoothed solution of cycle k+1
-    double *rc;                 // coarse right-hand side of cycle k+1
+template <class T>
+struct PostPreArgsT {
+    const T *phi;               // pre-smoothed solution of cycle k
+    const T *ec;                // coarse correction of cycle k
+    const T *f;
+    T *x4;                      // pre-smoothed solution of cycle k+1
+    T *rc;                      // coarse right-hand side of cycle k+1
     double *partials1;          // sum r(x1)^2 (post-smooth check)
     double *partials2;          // sum r(x3)^2 (pre-smooth check)
     unsigned long long *stats;
-    double hh, ih;
+    T hh, ih;
     int N, P, Nc, Pc;
     int jc0, jc1;
     int row_lo, row_hi;
@@ -71,15 +76,21 @@ struct FixArgsF {
     int force;                  // recompute without deciding (rare path of k_postpre)
 };
 
+using PreArgs = PreArgsT<double>;
+using PostArgs = PostArgsT<double>;
+using PostPreArgs = PostPreArgsT<double>;
+
 int fused_blocks(int N, int jc0, int jc1);
-void launch_pre(const PreArgs &a, bool x0_zero, bool fine, hipStream_t s);
-void launch_post(const PostArgs &a, bool fine, hipStream_t s);
-void launch_pre_fixup(const FixArgsF &a, const PreArgs &p, bool x0_zero, hipStream_t s);
-void launch_post_fixup(const FixArgsF &a, const PostArgs &p, hipStream_t s);
+template <class T> void launch_pre(const PreArgsT<T> &a, bool x0_zero, bool fine, hipStream_t s);
+template <class T> void launch_post(const PostArgsT<T> &a, bool fine, hipStream_t s);
+template <class T>
+void launch_pre_fixup(const FixArgsF &a, const PreArgsT<T> &p, bool x0_zero, hipStream_t s);
+template <class T> void launch_post_fixup(const FixArgsF &a, const PostArgsT<T> &p, hipStream_t s);
 int postpre_blocks(int N, int jc0, int jc1);
-void launch_postpre(const PostPreArgs &a, hipStream_t s);
+template <class T> void launch_postpre(const PostPreArgsT<T> &a, hipStream_t s);
 // flags[0] = post check fired; flags[1] = pre check fired (and post did not)
-void launch_postpre_decide(const PostPreArgs &a, int np, double eps, unsigned *flags,
+void launch_postpre_decide(const double *partials1, const double *partials2,
+                           unsigned long long *stats, int np, double eps, unsigned *flags,
                            hipStream_t s);
 
 }  // namespace pgmg

@@ -28,28 +28,11 @@
 // Every expression keeps the reference's left-to-right order; built with
 // -ffp-contract=off, so the results are bit-identical to the unfused path.
 #include <cstdlib>
+#include <type_traits>
 
 #include "pgmg_fused.h"
 
 namespace pgmg {
-
-__device__ __forceinline__ double dpp_prev_f(double v)  // lane i <- lane i-1
-{
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x138, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xF, 0xF, false);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-__device__ __forceinline__ double dpp_next_f(double v)  // lane i <- lane i+1
-{
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x130, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x130, 0xF, 0xF, false);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-
-__device__ __forceinline__ double2 ldg2(const double *p) { return *reinterpret_cast<const double2 *>(p); }
-__device__ __forceinline__ void stg2(double *p, double2 v) { *reinterpret_cast<double2 *>(p) = v; }
 
 struct Cols {
     int c;          // odd column of this lane's pair (c, c+1)
@@ -58,27 +41,29 @@ struct Cols {
 };
 
 // One Jacobi stage on a row: J(ce) with boundary passthrough.
-__device__ __forceinline__ double2 jstage(double2 up, double2 ce, double2 dn, double2 f, double hh,
+template <class T>
+__device__ __forceinline__ V2<T> jstage(V2<T> up, V2<T> ce, V2<T> dn, V2<T> f, T hh,
                                           const Cols &k, bool brow)
 {
-    const double l = dpp_prev_f(ce.y);
-    const double r = dpp_next_f(ce.x);
-    double2 o;
-    o.x = 0.25 * ((hh * f.x) + l + ce.y + up.x + dn.x);
-    o.y = 0.25 * ((hh * f.y) + ce.x + r + up.y + dn.y);
+    const T l = dpp_shr(ce.y);
+    const T r = dpp_shl(ce.x);
+    V2<T> o;
+    o.x = T(0.25) * ((hh * f.x) + l + ce.y + up.x + dn.x);
+    o.y = T(0.25) * ((hh * f.y) + ce.x + r + up.y + dn.y);
     if (brow || k.bx) o.x = ce.x;
     if (brow || k.by) o.y = ce.y;
     return o;
 }
 
 // Residual r = f - (1/h^2)(4x - xl - xr - xu - xd) on a row (DynamicGridUtils.hpp:59-69)
-__device__ __forceinline__ double2 rstage(double2 up, double2 ce, double2 dn, double2 f, double ih)
+template <class T>
+__device__ __forceinline__ V2<T> rstage(V2<T> up, V2<T> ce, V2<T> dn, V2<T> f, T ih)
 {
-    const double l = dpp_prev_f(ce.y);
-    const double r = dpp_next_f(ce.x);
-    double2 o;
-    o.x = f.x - ih * (4 * ce.x - l - ce.y - up.x - dn.x);
-    o.y = f.y - ih * (4 * ce.y - ce.x - r - up.y - dn.y);
+    const T l = dpp_shr(ce.y);
+    const T r = dpp_shl(ce.x);
+    V2<T> o;
+    o.x = f.x - ih * (T(4) * ce.x - l - ce.y - up.x - dn.x);
+    o.y = f.y - ih * (T(4) * ce.y - ce.x - r - up.y - dn.y);
     return o;
 }
 
@@ -117,8 +102,8 @@ __device__ __forceinline__ double fused_block_sum(double v, double *red)
 // ---------------------------------------------------------------------------
 // k_pre
 // ---------------------------------------------------------------------------
-template <bool X0_ZERO, bool FINE, int PAIRS>
-__global__ __launch_bounds__(256) void k_pre(PreArgs a)
+template <class T, bool X0_ZERO, bool FINE, int PAIRS>
+__global__ __launch_bounds__(256) void k_pre(PreArgsT<T> a)
 {
     constexpr int R = 2 * PAIRS;  // rows loaded per iteration (and prefetched ahead)
     __shared__ double red[4];
@@ -132,15 +117,15 @@ __global__ __launch_bounds__(256) void k_pre(PreArgs a)
     const int clo = max(jcb, max(1, a.rc_lo)), chi = min(jce, min(N / 2, a.rc_hi));  // rc rows
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
         atomicAdd(&a.stats[0], 2ull);
-    const double *__restrict__ X = a.x0 + k.c;
-    const double *__restrict__ F = a.f + k.c;
+    const T *__restrict__ X = a.x0 + k.c;
+    const T *__restrict__ F = a.f + k.c;
     const bool store = a.x2 != nullptr;
-    double *__restrict__ O = a.x2 + k.c;
-    const double hh = a.hh, ih = a.ih;
-    const double2 z = make_double2(0.0, 0.0);
+    T *__restrict__ O = a.x2 + k.c;
+    const T hh = a.hh, ih = a.ih;
+    const V2<T> z = zero2<T>();
     // windows: x0 rows i-2,i-1 ; x1 rows i-3,i-2 ; x2 rows i-4,i-3 ; r rows i-5,i-4 ;
     //          f rows i-3,i-2,i-1
-    double2 a0 = z, a1 = z, b0 = z, b1 = z, c0 = z, c1 = z, d0 = z, d1 = z, f0 = z, f1 = z, f2 = z;
+    V2<T> a0 = z, a1 = z, b0 = z, b1 = z, c0 = z, c1 = z, d0 = z, d1 = z, f0 = z, f1 = z, f2 = z;
     double acc = 0.0;
     // steps [i_begin, i_end): rows 2jcb-4 .. 2jce+3, rounded up to whole iterations
     // (the extra rows are computed but never stored; kHalo covers their loads)
@@ -150,14 +135,14 @@ __global__ __launch_bounds__(256) void k_pre(PreArgs a)
     const bool idle = (k.c - 2 * (threadIdx.x & 63) + 4) > N - 2;
     const int i_end = idle ? i_begin
                            : i_begin + ((2 * (jce - jcb) + 8 + R - 1) / R) * R;
-    double2 nx[R], nf[R];
+    V2<T> nx[R], nf[R];
     #pragma unroll
     for (int q = 0; q < R; ++q) {
-        nx[q] = (X0_ZERO || idle) ? z : ldg2(X + (i_begin + q) * P);
-        nf[q] = idle ? z : ldg2(F + (i_begin + q) * P);
+        nx[q] = (X0_ZERO || idle) ? z : ldv(X + (i_begin + q) * P);
+        nf[q] = idle ? z : ldv(F + (i_begin + q) * P);
     }
     for (int i = i_begin; i < i_end; i += R) {
-        double2 cx[R], cf[R];
+        V2<T> cx[R], cf[R];
         #pragma unroll
         for (int q = 0; q < R; ++q) {
             cx[q] = nx[q];
@@ -166,40 +151,40 @@ __global__ __launch_bounds__(256) void k_pre(PreArgs a)
         if (i + R < i_end) {  // prefetch the next R rows
             #pragma unroll
             for (int q = 0; q < R; ++q) {
-                if (!X0_ZERO) nx[q] = ldg2(X + (i + R + q) * P);
-                nf[q] = ldg2(F + (i + R + q) * P);
+                if (!X0_ZERO) nx[q] = ldv(X + (i + R + q) * P);
+                nf[q] = ldv(F + (i + R + q) * P);
             }
         }
         #pragma unroll
         for (int s = 0; s < R; ++s) {
             const int ii = i + s;
-            const double2 a2 = cx[s];
-            const double2 f3 = cf[s];
+            const V2<T> a2 = cx[s];
+            const V2<T> f3 = cf[s];
             // x1 row ii-1
-            const double2 b2 = jstage(a0, a1, a2, f2, hh, k, boundary_row(ii - 1, N));
+            const V2<T> b2 = jstage(a0, a1, a2, f2, hh, k, boundary_row(ii - 1, N));
             // r(x1) and x2 on row ii-2
             {
                 const int row = ii - 2;
-                const double2 r1 = rstage(b0, b1, b2, f1, ih);
+                const V2<T> r1 = rstage(b0, b1, b2, f1, ih);
                 if (row >= olo && row < ohi && k.own) {
-                    acc += r1.x * r1.x;
-                    if (!k.by) acc += r1.y * r1.y;
+                    acc += sq(r1.x);
+                    if (!k.by) acc += sq(r1.y);
                 }
             }
-            const double2 c2 = jstage(b0, b1, b2, f1, hh, k, boundary_row(ii - 2, N));
-            if (store && ii - 2 >= olo && ii - 2 < ohi && k.own) stg2(O + (ii - 2) * P, c2);
+            const V2<T> c2 = jstage(b0, b1, b2, f1, hh, k, boundary_row(ii - 2, N));
+            if (store && ii - 2 >= olo && ii - 2 < ohi && k.own) stv(O + (ii - 2) * P, c2);
             // r(x2) on row ii-3 (garbage on boundary rows; never used there)
-            const double2 d2 = rstage(c0, c1, c2, f0, ih);
+            const V2<T> d2 = rstage(c0, c1, c2, f0, ih);
             // restriction: rows ii-5, ii-4, ii-3 = 2jc-1, 2jc, 2jc+1 when ii is even
             if ((s & 1) == 0) {
                 const int jc = (ii - 4) >> 1;
-                const double m2 = dpp_next_f(d1.x);
-                const double u2 = dpp_next_f(d0.x);
-                const double e2 = dpp_next_f(d2.x);
+                const T m2 = dpp_shl(d1.x);
+                const T u2 = dpp_shl(d0.x);
+                const T e2 = dpp_shl(d2.x);
                 const int ic = (k.c + 1) >> 1;
                 if (jc >= clo && jc < chi && k.own && ic <= a.Nc - 2) {
-                    const double v = 0.25 * d1.y + 0.125 * (m2 + d1.x + d2.y + d0.y) +
-                                     0.0625 * (d0.x + u2 + d2.x + e2);
+                    const T v = T(0.25) * d1.y + T(0.125) * (m2 + d1.x + d2.y + d0.y) +
+                                     T(0.0625) * (d0.x + u2 + d2.x + e2);
                     a.rc[(long long)jc * a.Pc + ic] = v;
                 }
             }
@@ -228,18 +213,18 @@ struct ProlongCols {
     int ic;        // coarse column of the odd fine column c: (c-1)/2
 };
 
-__device__ __forceinline__ double2 add_prolong(double2 p, int row, double ca, double cb, double da,
-                                               double db, const ProlongCols &pc, int Nc)
+template <class T>
+__device__ __forceinline__ V2<T> add_prolong(V2<T> p, int row, T ca, T cb, T da, T db, const ProlongCols &pc, int Nc)
 {
     // MultiGrid.hpp:219-223; row in [2, Nf-2] <=> its coarse row m in [1, Nc-2]
     const int m = row >> 1;
     if (m < 1 || m > Nc - 2) return p;
     if ((row & 1) == 0) {
-        if (pc.vx) p.x = p.x + 0.5 * (ca + cb);
+        if (pc.vx) p.x = p.x + T(0.5) * (ca + cb);
         if (pc.vy) p.y = p.y + cb;
     } else {
-        if (pc.vx) p.x = p.x + 0.25 * (ca + cb + da + db);
-        if (pc.vy) p.y = p.y + 0.5 * (cb + db);
+        if (pc.vx) p.x = p.x + T(0.25) * (ca + cb + da + db);
+        if (pc.vy) p.y = p.y + T(0.5) * (cb + db);
     }
     return p;
 }
@@ -247,8 +232,8 @@ __device__ __forceinline__ double2 add_prolong(double2 p, int row, double ca, do
 // RECOMP (levels entered with x0 = 0): phi is not read.  The loaded row is f[ii+1];
 // x1 = J(0) is pointwise, so x1 row ii+1 -> phi row ii = J(x1) (or x1 when the pre
 // check fired) -> x_eff row ii: one more row of lag than reading phi, 16 B/point less.
-template <bool FINE, int PAIRS, bool RECOMP>
-__global__ __launch_bounds__(256) void k_post(PostArgs a)
+template <class T, bool FINE, int PAIRS, bool RECOMP>
+__global__ __launch_bounds__(256) void k_post(PostArgsT<T> a)
 {
     constexpr int R = 2 * PAIRS;
     __shared__ double red[4];
@@ -265,17 +250,17 @@ __global__ __launch_bounds__(256) void k_post(PostArgs a)
     pc.ic = (k.c - 1) >> 1;
     pc.vx = k.c >= 3 && k.c <= N - 2;
     pc.vy = k.c + 1 >= 2 && k.c + 1 <= N - 3;
-    const double *__restrict__ F = a.f + k.c;
+    const T *__restrict__ F = a.f + k.c;
     // the streamed array: phi, or f one row ahead (RECOMP)
-    const double *__restrict__ X = RECOMP ? F + P : a.phi + k.c;
-    const double *__restrict__ E = a.ec + pc.ic;
-    double *__restrict__ O = a.x2 + k.c;
-    const double hh = a.hh, ih = a.ih;
-    const double2 z = make_double2(0.0, 0.0);
+    const T *__restrict__ X = RECOMP ? F + P : a.phi + k.c;
+    const T *__restrict__ E = a.ec + pc.ic;
+    T *__restrict__ O = a.x2 + k.c;
+    const T hh = a.hh, ih = a.ih;
+    const V2<T> z = zero2<T>();
     // windows: x_eff rows i-2,i-1 ; x1 rows i-3,i-2 ; f rows i-2,i-1
-    double2 a0 = z, a1 = z, b0 = z, b1 = z, f1 = z, f2 = z;
+    V2<T> a0 = z, a1 = z, b0 = z, b1 = z, f1 = z, f2 = z;
     // RECOMP: pre-smooth x1 rows ii-1, ii ; f row ii
-    double2 g0 = z, g1 = z, fc = z;
+    V2<T> g0 = z, g1 = z, fc = z;
     double acc = 0.0;
     const int i_begin = 2 * jcb - 2;
     const bool idle = (k.c - 2 * (threadIdx.x & 63) + 4) > N - 2;  // spare wave
@@ -283,25 +268,25 @@ __global__ __launch_bounds__(256) void k_post(PostArgs a)
                            : i_begin + ((2 * (jce - jcb) + 4 + R - 1) / R) * R;
     const bool pfired = RECOMP && *a.pre_fired != 0u;
     if (RECOMP && !idle) {
-        const double2 fm = ldg2(F + (i_begin - 1) * P);
-        fc = ldg2(F + i_begin * P);
+        const V2<T> fm = ldv(F + (i_begin - 1) * P);
+        fc = ldv(F + i_begin * P);
         g0 = jstage(z, z, z, fm, hh, k, boundary_row(i_begin - 1, N));
         g1 = jstage(z, z, z, fc, hh, k, boundary_row(i_begin, N));
     }
     // coarse row m = ii/2 of fine row ii; an iteration of R rows uses coarse rows
     // i/2 .. i/2 + PAIRS
-    double2 np_[R], nf[R];
-    double ncr[PAIRS + 1];
+    V2<T> np_[R], nf[R];
+    T ncr[PAIRS + 1];
     #pragma unroll
     for (int q = 0; q < R; ++q) {
-        np_[q] = idle ? z : ldg2(X + (i_begin + q) * P);
-        if (!RECOMP) nf[q] = idle ? z : ldg2(F + (i_begin + q) * P);
+        np_[q] = idle ? z : ldv(X + (i_begin + q) * P);
+        if (!RECOMP) nf[q] = idle ? z : ldv(F + (i_begin + q) * P);
     }
     #pragma unroll
-    for (int q = 0; q <= PAIRS; ++q) ncr[q] = idle ? 0.0 : E[(long long)((i_begin >> 1) + q) * Pc];
+    for (int q = 0; q <= PAIRS; ++q) ncr[q] = idle ? T(0) : E[(long long)((i_begin >> 1) + q) * Pc];
     for (int i = i_begin; i < i_end; i += R) {
-        double2 cp[R], cf[R];
-        double cr[PAIRS + 1];
+        V2<T> cp[R], cf[R];
+        T cr[PAIRS + 1];
         #pragma unroll
         for (int q = 0; q < R; ++q) {
             cp[q] = np_[q];
@@ -312,23 +297,23 @@ __global__ __launch_bounds__(256) void k_post(PostArgs a)
         if (i + R < i_end) {
             #pragma unroll
             for (int q = 0; q < R; ++q) {
-                np_[q] = ldg2(X + (i + R + q) * P);
-                if (!RECOMP) nf[q] = ldg2(F + (i + R + q) * P);
+                np_[q] = ldv(X + (i + R + q) * P);
+                if (!RECOMP) nf[q] = ldv(F + (i + R + q) * P);
             }
             #pragma unroll
             for (int q = 0; q <= PAIRS; ++q) ncr[q] = E[(long long)(((i + R) >> 1) + q) * Pc];
         }
-        double crn[PAIRS + 1];
+        T crn[PAIRS + 1];
         #pragma unroll
-        for (int q = 0; q <= PAIRS; ++q) crn[q] = dpp_next_f(cr[q]);
+        for (int q = 0; q <= PAIRS; ++q) crn[q] = dpp_shl(cr[q]);
         #pragma unroll
         for (int s = 0; s < R; ++s) {
             const int ii = i + s;
             const int pq = s >> 1;
-            double2 ph, f3;
+            V2<T> ph, f3;
             if (RECOMP) {
-                const double2 fn = cp[s];  // f row ii+1
-                const double2 g2 = jstage(z, z, z, fn, hh, k, boundary_row(ii + 1, N));
+                const V2<T> fn = cp[s];  // f row ii+1
+                const V2<T> g2 = jstage(z, z, z, fn, hh, k, boundary_row(ii + 1, N));
                 ph = pfired ? g1 : jstage(g0, g1, g2, fc, hh, k, boundary_row(ii, N));
                 f3 = fc;
                 g0 = g1;
@@ -338,18 +323,18 @@ __global__ __launch_bounds__(256) void k_post(PostArgs a)
                 ph = cp[s];
                 f3 = cf[s];
             }
-            const double2 a2 = add_prolong(ph, ii, cr[pq], crn[pq], cr[pq + 1], crn[pq + 1], pc, Nc);
-            const double2 b2 = jstage(a0, a1, a2, f2, hh, k, boundary_row(ii - 1, N));
+            const V2<T> a2 = add_prolong(ph, ii, cr[pq], crn[pq], cr[pq + 1], crn[pq + 1], pc, Nc);
+            const V2<T> b2 = jstage(a0, a1, a2, f2, hh, k, boundary_row(ii - 1, N));
             {
                 const int row = ii - 2;
-                const double2 r1 = rstage(b0, b1, b2, f1, ih);
+                const V2<T> r1 = rstage(b0, b1, b2, f1, ih);
                 if (row >= olo && row < ohi && k.own) {
-                    acc += r1.x * r1.x;
-                    if (!k.by) acc += r1.y * r1.y;
+                    acc += sq(r1.x);
+                    if (!k.by) acc += sq(r1.y);
                 }
             }
-            const double2 c2 = jstage(b0, b1, b2, f1, hh, k, boundary_row(ii - 2, N));
-            if (ii - 2 >= olo && ii - 2 < ohi && k.own) stg2(O + (ii - 2) * P, c2);
+            const V2<T> c2 = jstage(b0, b1, b2, f1, hh, k, boundary_row(ii - 2, N));
+            if (ii - 2 >= olo && ii - 2 < ohi && k.own) stv(O + (ii - 2) * P, c2);
             a0 = a1;
             a1 = a2;
             b0 = b1;
@@ -378,22 +363,22 @@ constexpr int kPPStride = 114, kPPMargin = 6;
 // MODE 0: the real pass.  MODE 1 (PGMG_PP_VARIANT=1, measurement only): the same loads
 // and stores with the stencil arithmetic replaced by one add, to separate the memory
 // ceiling of this access pattern from the instruction cost.
-template <int MODE>
-__device__ __forceinline__ double2 js(double2 up, double2 ce, double2 dn, double2 f, double hh,
+template <int MODE, class T>
+__device__ __forceinline__ V2<T> js(V2<T> up, V2<T> ce, V2<T> dn, V2<T> f, T hh,
                                       const Cols &k, bool brow)
 {
-    if (MODE == 1) return make_double2(ce.x + f.x, ce.y + up.y + dn.y);
+    if (MODE == 1) return mk2<T>(ce.x + f.x, ce.y + up.y + dn.y);
     return jstage(up, ce, dn, f, hh, k, brow);
 }
-template <int MODE>
-__device__ __forceinline__ double2 rs(double2 up, double2 ce, double2 dn, double2 f, double ih)
+template <int MODE, class T>
+__device__ __forceinline__ V2<T> rs(V2<T> up, V2<T> ce, V2<T> dn, V2<T> f, T ih)
 {
-    if (MODE == 1) return make_double2(f.x + ce.x, f.y);
+    if (MODE == 1) return mk2<T>(f.x + ce.x, f.y);
     return rstage(up, ce, dn, f, ih);
 }
 
-template <int PAIRS, int MODE, int STRIDE = kPPStride, int MARGIN = kPPMargin>
-__device__ __forceinline__ void postpre_body(const PostPreArgs &a)
+template <class T, int PAIRS, int MODE, int STRIDE = kPPStride, int MARGIN = kPPMargin>
+__device__ __forceinline__ void postpre_body(const PostPreArgsT<T> &a)
 {
     constexpr int R = 2 * PAIRS;
     __shared__ double red[4];
@@ -410,33 +395,33 @@ __device__ __forceinline__ void postpre_body(const PostPreArgs &a)
     pc.ic = (k.c - 1) >> 1;
     pc.vx = k.c >= 3 && k.c <= N - 2;
     pc.vy = k.c + 1 >= 2 && k.c + 1 <= N - 3;
-    const double *__restrict__ X = a.phi + k.c;
-    const double *__restrict__ F = a.f + k.c;
-    const double *__restrict__ E = a.ec + pc.ic;
-    double *__restrict__ O = a.x4 + k.c;
-    const double hh = a.hh, ih = a.ih;
-    const double2 z = make_double2(0.0, 0.0);
+    const T *__restrict__ X = a.phi + k.c;
+    const T *__restrict__ F = a.f + k.c;
+    const T *__restrict__ E = a.ec + pc.ic;
+    T *__restrict__ O = a.x4 + k.c;
+    const T hh = a.hh, ih = a.ih;
+    const V2<T> z = zero2<T>();
     // windows (two previous rows each) and f rows i-5 .. i-1
-    double2 e0 = z, e1 = z, b0 = z, b1 = z, c0 = z, c1 = z, g0 = z, g1 = z, h0 = z, h1 = z,
+    V2<T> e0 = z, e1 = z, b0 = z, b1 = z, c0 = z, c1 = z, g0 = z, g1 = z, h0 = z, h1 = z,
             d0 = z, d1 = z;
-    double2 f1 = z, f2 = z, f3 = z, f4 = z, f5 = z;  // f[i-1], f[i-2], ..., f[i-5]
+    V2<T> f1 = z, f2 = z, f3 = z, f4 = z, f5 = z;  // f[i-1], f[i-2], ..., f[i-5]
     double acc1 = 0.0, acc2 = 0.0;
     const int i_begin = 2 * jcb - 6;
     const bool idle = (k.c - 2 * (threadIdx.x & 63) + MARGIN) > N - 2;  // spare wave
     const int i_end = idle ? i_begin
                            : i_begin + ((2 * (jce - jcb) + 11 + R - 1) / R) * R;
-    double2 np_[R], nf[R];
-    double ncr[PAIRS + 1];
+    V2<T> np_[R], nf[R];
+    T ncr[PAIRS + 1];
     #pragma unroll
     for (int q = 0; q < R; ++q) {
-        np_[q] = idle ? z : ldg2(X + (i_begin + q) * P);
-        nf[q] = idle ? z : ldg2(F + (i_begin + q) * P);
+        np_[q] = idle ? z : ldv(X + (i_begin + q) * P);
+        nf[q] = idle ? z : ldv(F + (i_begin + q) * P);
     }
     #pragma unroll
-    for (int q = 0; q <= PAIRS; ++q) ncr[q] = idle ? 0.0 : E[(long long)((i_begin >> 1) + q) * Pc];
+    for (int q = 0; q <= PAIRS; ++q) ncr[q] = idle ? T(0) : E[(long long)((i_begin >> 1) + q) * Pc];
     for (int i = i_begin; i < i_end; i += R) {
-        double2 cp[R], cf[R];
-        double cr[PAIRS + 1];
+        V2<T> cp[R], cf[R];
+        T cr[PAIRS + 1];
         #pragma unroll
         for (int q = 0; q < R; ++q) {
             cp[q] = np_[q];
@@ -447,58 +432,58 @@ __device__ __forceinline__ void postpre_body(const PostPreArgs &a)
         if (i + R < i_end) {
             #pragma unroll
             for (int q = 0; q < R; ++q) {
-                np_[q] = ldg2(X + (i + R + q) * P);
-                nf[q] = ldg2(F + (i + R + q) * P);
+                np_[q] = ldv(X + (i + R + q) * P);
+                nf[q] = ldv(F + (i + R + q) * P);
             }
             #pragma unroll
             for (int q = 0; q <= PAIRS; ++q) ncr[q] = E[(long long)(((i + R) >> 1) + q) * Pc];
         }
-        double crn[PAIRS + 1];
+        T crn[PAIRS + 1];
         #pragma unroll
-        for (int q = 0; q <= PAIRS; ++q) crn[q] = dpp_next_f(cr[q]);
+        for (int q = 0; q <= PAIRS; ++q) crn[q] = dpp_shl(cr[q]);
         #pragma unroll
         for (int s = 0; s < R; ++s) {
             const int ii = i + s;
             const int pq = s >> 1;
-            const double2 e2 = add_prolong(cp[s], ii, cr[pq], crn[pq], cr[pq + 1], crn[pq + 1], pc, Nc);
-            const double2 f0 = cf[s];  // f[ii]
+            const V2<T> e2 = add_prolong(cp[s], ii, cr[pq], crn[pq], cr[pq + 1], crn[pq + 1], pc, Nc);
+            const V2<T> f0 = cf[s];  // f[ii]
             // post-smooth sweep 1: x1 row ii-1
-            const double2 b2 = js<MODE>(e0, e1, e2, f1, hh, k, boundary_row(ii - 1, N));
+            const V2<T> b2 = js<MODE, T>(e0, e1, e2, f1, hh, k, boundary_row(ii - 1, N));
             {   // post check: r(x1) on row ii-2
-                const double2 r1 = rs<MODE>(b0, b1, b2, f2, ih);
+                const V2<T> r1 = rs<MODE, T>(b0, b1, b2, f2, ih);
                 const int row = ii - 2;
                 if (row >= olo && row < ohi && k.own) {
-                    acc1 += r1.x * r1.x;
-                    if (!k.by) acc1 += r1.y * r1.y;
+                    acc1 += sq(r1.x);
+                    if (!k.by) acc1 += sq(r1.y);
                 }
             }
             // post-smooth sweep 2: x2 row ii-2 (= phi of cycle k+1)
-            const double2 c2 = js<MODE>(b0, b1, b2, f2, hh, k, boundary_row(ii - 2, N));
+            const V2<T> c2 = js<MODE, T>(b0, b1, b2, f2, hh, k, boundary_row(ii - 2, N));
             // pre-smooth sweep 1: x3 row ii-3
-            const double2 g2 = js<MODE>(c0, c1, c2, f3, hh, k, boundary_row(ii - 3, N));
+            const V2<T> g2 = js<MODE, T>(c0, c1, c2, f3, hh, k, boundary_row(ii - 3, N));
             {   // pre check: r(x3) on row ii-4
-                const double2 r3 = rs<MODE>(g0, g1, g2, f4, ih);
+                const V2<T> r3 = rs<MODE, T>(g0, g1, g2, f4, ih);
                 const int row = ii - 4;
                 if (row >= olo && row < ohi && k.own) {
-                    acc2 += r3.x * r3.x;
-                    if (!k.by) acc2 += r3.y * r3.y;
+                    acc2 += sq(r3.x);
+                    if (!k.by) acc2 += sq(r3.y);
                 }
             }
             // pre-smooth sweep 2: x4 row ii-4 (stored)
-            const double2 h2 = js<MODE>(g0, g1, g2, f4, hh, k, boundary_row(ii - 4, N));
-            if (ii - 4 >= olo && ii - 4 < ohi && k.own) stg2(O + (ii - 4) * P, h2);
+            const V2<T> h2 = js<MODE, T>(g0, g1, g2, f4, hh, k, boundary_row(ii - 4, N));
+            if (ii - 4 >= olo && ii - 4 < ohi && k.own) stv(O + (ii - 4) * P, h2);
             // r(x4) on row ii-5
-            const double2 d2 = rs<MODE>(h0, h1, h2, f5, ih);
+            const V2<T> d2 = rs<MODE, T>(h0, h1, h2, f5, ih);
             // restriction: rows ii-7, ii-6, ii-5 = 2jc-1, 2jc, 2jc+1 when ii is even
             if ((s & 1) == 0) {
                 const int jc = (ii - 6) >> 1;
-                const double m2 = dpp_next_f(d1.x);
-                const double u2 = dpp_next_f(d0.x);
-                const double w2 = dpp_next_f(d2.x);
+                const T m2 = dpp_shl(d1.x);
+                const T u2 = dpp_shl(d0.x);
+                const T w2 = dpp_shl(d2.x);
                 const int ic = (k.c + 1) >> 1;
                 if (jc >= clo && jc < chi && k.own && ic <= Nc - 2) {
-                    const double v = 0.25 * d1.y + 0.125 * (m2 + d1.x + d2.y + d0.y) +
-                                     0.0625 * (d0.x + u2 + d2.x + w2);
+                    const T v = T(0.25) * d1.y + T(0.125) * (m2 + d1.x + d2.y + d0.y) +
+                                     T(0.0625) * (d0.x + u2 + d2.x + w2);
                     a.rc[(long long)jc * Pc + ic] = v;
                 }
             }
@@ -521,17 +506,17 @@ __device__ __forceinline__ void postpre_body(const PostPreArgs &a)
     }
 }
 
-template <int PAIRS, int MODE, int STRIDE = kPPStride, int MARGIN = kPPMargin>
-__global__ __launch_bounds__(256) void k_postpre(PostPreArgs a)
+template <class T, int PAIRS, int MODE, int STRIDE = kPPStride, int MARGIN = kPPMargin>
+__global__ __launch_bounds__(256) void k_postpre(PostPreArgsT<T> a)
 {
-    postpre_body<PAIRS, MODE, STRIDE, MARGIN>(a);
+    postpre_body<T, PAIRS, MODE, STRIDE, MARGIN>(a);
 }
 
 // PGMG_PP_VARIANT=2: at most 128 VGPRs (4 waves per SIMD)
-template <int PAIRS>
-__global__ __launch_bounds__(256, 4) void k_postpre_o4(PostPreArgs a)
+template <class T, int PAIRS>
+__global__ __launch_bounds__(256, 4) void k_postpre_o4(PostPreArgsT<T> a)
 {
-    postpre_body<PAIRS, 0>(a);
+    postpre_body<T, PAIRS, 0>(a);
 }
 
 // ---------------------------------------------------------------------------
@@ -548,15 +533,14 @@ __global__ __launch_bounds__(256, 4) void k_postpre_o4(PostPreArgs a)
 constexpr int kPPLdsRow = 4 * kPPStride + 2 * kPPMargin + 4;     // 472 doubles per row
 constexpr int kPPLdsCoarse = 2 * kPPStride + kPPMargin + 8;      // 242 doubles per coarse row
 
-__device__ __forceinline__ double2 lds2(const double *p) { return *reinterpret_cast<const double2 *>(p); }
-
-__global__ __launch_bounds__(256) void k_postpre_lds(PostPreArgs a)
+template <class T>
+__global__ __launch_bounds__(256) void k_postpre_lds(PostPreArgsT<T> a)
 {
     constexpr int R = 2;
     __shared__ double red[4];
-    __shared__ __attribute__((aligned(16))) double sx[2][R][kPPLdsRow];
-    __shared__ __attribute__((aligned(16))) double sf[2][R][kPPLdsRow];
-    __shared__ __attribute__((aligned(16))) double se[3][kPPLdsCoarse];
+    __shared__ __attribute__((aligned(16))) T sx[2][R][kPPLdsRow];
+    __shared__ __attribute__((aligned(16))) T sf[2][R][kPPLdsRow];
+    __shared__ __attribute__((aligned(16))) T se[3][kPPLdsCoarse];
     const Cols k = lane_cols_t<kPPStride, kPPMargin>(a.N);
     const int N = a.N, Nc = a.Nc;
     const long long P = a.P, Pc = a.Pc;
@@ -570,9 +554,9 @@ __global__ __launch_bounds__(256) void k_postpre_lds(PostPreArgs a)
     pc.ic = (k.c - 1) >> 1;
     pc.vx = k.c >= 3 && k.c <= N - 2;
     pc.vy = k.c + 1 >= 2 && k.c + 1 <= N - 3;
-    double *__restrict__ O = a.x4 + k.c;
-    const double hh = a.hh, ih = a.ih;
-    const double2 z = make_double2(0.0, 0.0);
+    T *__restrict__ O = a.x4 + k.c;
+    const T hh = a.hh, ih = a.ih;
+    const V2<T> z = zero2<T>();
 
     // loader geometry: the block window starts at column L0 (odd: 16-byte aligned pairs)
     const int wpb = blockDim.x >> 6;
@@ -583,17 +567,17 @@ __global__ __launch_bounds__(256) void k_postpre_lds(PostPreArgs a)
     const int cc0 = (L0 - 1) >> 1;                               // first coarse column
     const int ncc = (kPPStride / 2) * wpb + kPPMargin + 2;
     const bool cldr = t < ncc && cc0 + t <= Nc - 1;
-    const double *__restrict__ GX = a.phi + L0 + 2 * t;
-    const double *__restrict__ GF = a.f + L0 + 2 * t;
-    const double *__restrict__ GE = a.ec + cc0 + t;
+    const T *__restrict__ GX = a.phi + L0 + 2 * t;
+    const T *__restrict__ GF = a.f + L0 + 2 * t;
+    const T *__restrict__ GE = a.ec + cc0 + t;
     // this wave's window in the LDS rows
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int xo = kPPStride * w + 2 * lane;
     const int co = (kPPStride / 2) * w + lane;
 
-    double2 e0 = z, e1 = z, b0 = z, b1 = z, c0 = z, c1 = z, g0 = z, g1 = z, h0 = z, h1 = z,
+    V2<T> e0 = z, e1 = z, b0 = z, b1 = z, c0 = z, c1 = z, g0 = z, g1 = z, h0 = z, h1 = z,
             d0 = z, d1 = z;
-    double2 f1 = z, f2 = z, f3 = z, f4 = z, f5 = z;  // f[i-1], f[i-2], ..., f[i-5]
+    V2<T> f1 = z, f2 = z, f3 = z, f4 = z, f5 = z;  // f[i-1], f[i-2], ..., f[i-5]
     double acc1 = 0.0, acc2 = 0.0;
     const int i_begin = 2 * jcb - 6;
     const int ng = (2 * (jce - jcb) + 11 + R - 1) / R;   // row pairs (uniform over the block)
@@ -602,33 +586,33 @@ __global__ __launch_bounds__(256) void k_postpre_lds(PostPreArgs a)
 
     if (t < 2 * R * 4) {   // the 4 pad doubles past the window (read by spare lanes only)
         const int sl = t >> 3, q = (t >> 2) & 1, j = kPPLdsRow - 4 + (t & 3);
-        sx[sl][q][j] = 0.0;
-        sf[sl][q][j] = 0.0;
+        sx[sl][q][j] = T(0);
+        sf[sl][q][j] = T(0);
     }
     // two register sets: pair p's loads go to set p & 1, issued two pairs ahead
-    double2 pxA[R], pfA[R], pxB[R], pfB[R];
-    double peA = 0.0, peB = 0.0;
-    auto load_pair = [&](int p, double2 (&px)[R], double2 (&pf)[R], double &pe) {
+    V2<T> pxA[R], pfA[R], pxB[R], pfB[R];
+    T peA = T(0), peB = T(0);
+    auto load_pair = [&](int p, V2<T> (&px)[R], V2<T> (&pf)[R], T &pe) {
         #pragma unroll
         for (int q = 0; q < R; ++q) {
-            px[q] = ldr ? ldg2(GX + (i_begin + p * R + q) * P) : z;
-            pf[q] = ldr ? ldg2(GF + (i_begin + p * R + q) * P) : z;
+            px[q] = ldr ? ldv(GX + (i_begin + p * R + q) * P) : z;
+            pf[q] = ldr ? ldv(GF + (i_begin + p * R + q) * P) : z;
         }
-        pe = cldr ? GE[(long long)(m0 + p + 1) * Pc] : 0.0;   // the pair's second coarse row
+        pe = cldr ? GE[(long long)(m0 + p + 1) * Pc] : T(0);   // the pair's second coarse row
     };
-    auto store_pair = [&](int p, const double2 (&px)[R], const double2 (&pf)[R], double pe) {
+    auto store_pair = [&](int p, const V2<T> (&px)[R], const V2<T> (&pf)[R], T pe) {
         if (t < npairs) {
             #pragma unroll
             for (int q = 0; q < R; ++q) {
-                *reinterpret_cast<double2 *>(&sx[p & 1][q][2 * t]) = px[q];
-                *reinterpret_cast<double2 *>(&sf[p & 1][q][2 * t]) = pf[q];
+                *reinterpret_cast<V2<T> *>(&sx[p & 1][q][2 * t]) = px[q];
+                *reinterpret_cast<V2<T> *>(&sf[p & 1][q][2 * t]) = pf[q];
             }
         }
         if (t < ncc) se[ring(m0 + p + 1)][t] = pe;
     };
     // prologue: pair 0 (+ its first coarse row) into slot 0; pairs 1, 2 in flight
     load_pair(0, pxA, pfA, peA);
-    if (t < ncc) se[ring(m0)][t] = cldr ? GE[(long long)m0 * Pc] : 0.0;
+    if (t < ncc) se[ring(m0)][t] = cldr ? GE[(long long)m0 * Pc] : T(0);
     store_pair(0, pxA, pfA, peA);
     if (ng > 1) load_pair(1, pxB, pfB, peB);
     if (ng > 2) load_pair(2, pxA, pfA, peA);
@@ -636,55 +620,55 @@ __global__ __launch_bounds__(256) void k_postpre_lds(PostPreArgs a)
 
     // pair gi: compute from slot gi & 1; pair gi+1 (set (gi+1) & 1) -> the other slot;
     // issue pair gi+3 into the set just freed; one barrier
-    auto step = [&](int gi, double2 (&px)[R], double2 (&pf)[R], double &pe) {
+    auto step = [&](int gi, V2<T> (&px)[R], V2<T> (&pf)[R], T &pe) {
         const int slot = gi & 1;
         const int i = i_begin + gi * R;
         const int m = m0 + gi;
-        const double *E0 = se[ring(m)], *E1 = se[ring(m + 1)];
-        const double cr0 = E0[co], crn0 = E0[co + 1], cr1 = E1[co], crn1 = E1[co + 1];
+        const T *E0 = se[ring(m)], *E1 = se[ring(m + 1)];
+        const T cr0 = E0[co], crn0 = E0[co + 1], cr1 = E1[co], crn1 = E1[co + 1];
         #pragma unroll
         for (int s = 0; s < R; ++s) {
             const int ii = i + s;
-            const double2 xr = lds2(&sx[slot][s][xo]);
-            const double2 f0 = lds2(&sf[slot][s][xo]);   // f[ii]
-            const double2 e2 = add_prolong(xr, ii, cr0, crn0, cr1, crn1, pc, Nc);
+            const V2<T> xr = ldv(&sx[slot][s][xo]);
+            const V2<T> f0 = ldv(&sf[slot][s][xo]);   // f[ii]
+            const V2<T> e2 = add_prolong(xr, ii, cr0, crn0, cr1, crn1, pc, Nc);
             // post-smooth sweep 1: x1 row ii-1
-            const double2 b2 = jstage(e0, e1, e2, f1, hh, k, boundary_row(ii - 1, N));
+            const V2<T> b2 = jstage(e0, e1, e2, f1, hh, k, boundary_row(ii - 1, N));
             {   // post check: r(x1) on row ii-2
-                const double2 r1 = rstage(b0, b1, b2, f2, ih);
+                const V2<T> r1 = rstage(b0, b1, b2, f2, ih);
                 const int row = ii - 2;
                 if (row >= olo && row < ohi && k.own) {
-                    acc1 += r1.x * r1.x;
-                    if (!k.by) acc1 += r1.y * r1.y;
+                    acc1 += sq(r1.x);
+                    if (!k.by) acc1 += sq(r1.y);
                 }
             }
             // post-smooth sweep 2: x2 row ii-2 (= phi of cycle k+1)
-            const double2 c2 = jstage(b0, b1, b2, f2, hh, k, boundary_row(ii - 2, N));
+            const V2<T> c2 = jstage(b0, b1, b2, f2, hh, k, boundary_row(ii - 2, N));
             // pre-smooth sweep 1: x3 row ii-3
-            const double2 g2 = jstage(c0, c1, c2, f3, hh, k, boundary_row(ii - 3, N));
+            const V2<T> g2 = jstage(c0, c1, c2, f3, hh, k, boundary_row(ii - 3, N));
             {   // pre check: r(x3) on row ii-4
-                const double2 r3 = rstage(g0, g1, g2, f4, ih);
+                const V2<T> r3 = rstage(g0, g1, g2, f4, ih);
                 const int row = ii - 4;
                 if (row >= olo && row < ohi && k.own) {
-                    acc2 += r3.x * r3.x;
-                    if (!k.by) acc2 += r3.y * r3.y;
+                    acc2 += sq(r3.x);
+                    if (!k.by) acc2 += sq(r3.y);
                 }
             }
             // pre-smooth sweep 2: x4 row ii-4 (stored)
-            const double2 h2 = jstage(g0, g1, g2, f4, hh, k, boundary_row(ii - 4, N));
-            if (ii - 4 >= olo && ii - 4 < ohi && k.own) stg2(O + (ii - 4) * P, h2);
+            const V2<T> h2 = jstage(g0, g1, g2, f4, hh, k, boundary_row(ii - 4, N));
+            if (ii - 4 >= olo && ii - 4 < ohi && k.own) stv(O + (ii - 4) * P, h2);
             // r(x4) on row ii-5
-            const double2 d2 = rstage(h0, h1, h2, f5, ih);
+            const V2<T> d2 = rstage(h0, h1, h2, f5, ih);
             // restriction: rows ii-7, ii-6, ii-5 = 2jc-1, 2jc, 2jc+1 when ii is even
             if ((s & 1) == 0) {
                 const int jc = (ii - 6) >> 1;
-                const double m2 = dpp_next_f(d1.x);
-                const double u2 = dpp_next_f(d0.x);
-                const double w2 = dpp_next_f(d2.x);
+                const T m2 = dpp_shl(d1.x);
+                const T u2 = dpp_shl(d0.x);
+                const T w2 = dpp_shl(d2.x);
                 const int ic = (k.c + 1) >> 1;
                 if (jc >= clo && jc < chi && k.own && ic <= Nc - 2) {
-                    const double v = 0.25 * d1.y + 0.125 * (m2 + d1.x + d2.y + d0.y) +
-                                     0.0625 * (d0.x + u2 + d2.x + w2);
+                    const T v = T(0.25) * d1.y + T(0.125) * (m2 + d1.x + d2.y + d0.y) +
+                                     T(0.0625) * (d0.x + u2 + d2.x + w2);
                     a.rc[(long long)jc * Pc + ic] = v;
                 }
             }
@@ -793,40 +777,42 @@ int fused_blocks(int N, int jc0, int jc1)
 
 // The finest level gets its own kernel symbols (FINE) so rocprofv3 statistics
 // isolate the roofline kernels.
-void launch_pre(const PreArgs &a0, bool x0_zero, bool fine, hipStream_t s)
+template <class T>
+void launch_pre(const PreArgsT<T> &a0, bool x0_zero, bool fine, hipStream_t s)
 {
     int t, gx, gy, r;
     fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r);
-    PreArgs a = a0;
+    PreArgsT<T> a = a0;
     a.rows_per_block = r;
     const dim3 g(gx, gy), b(t);
     if (fused_pairs() == 2) {
-        if (x0_zero) k_pre<true, false, 2><<<g, b, 0, s>>>(a);
-        else if (fine) k_pre<false, true, 2><<<g, b, 0, s>>>(a);
-        else k_pre<false, false, 2><<<g, b, 0, s>>>(a);
+        if (x0_zero) k_pre<T, true, false, 2><<<g, b, 0, s>>>(a);
+        else if (fine) k_pre<T, false, true, 2><<<g, b, 0, s>>>(a);
+        else k_pre<T, false, false, 2><<<g, b, 0, s>>>(a);
     } else {
-        if (x0_zero) k_pre<true, false, 1><<<g, b, 0, s>>>(a);
-        else if (fine) k_pre<false, true, 1><<<g, b, 0, s>>>(a);
-        else k_pre<false, false, 1><<<g, b, 0, s>>>(a);
+        if (x0_zero) k_pre<T, true, false, 1><<<g, b, 0, s>>>(a);
+        else if (fine) k_pre<T, false, true, 1><<<g, b, 0, s>>>(a);
+        else k_pre<T, false, false, 1><<<g, b, 0, s>>>(a);
     }
 }
 
-void launch_post(const PostArgs &a0, bool fine, hipStream_t s)
+template <class T>
+void launch_post(const PostArgsT<T> &a0, bool fine, hipStream_t s)
 {
     int t, gx, gy, r;
     fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r);
-    PostArgs a = a0;
+    PostArgsT<T> a = a0;
     a.rows_per_block = r;
     const dim3 g(gx, gy), b(t);
     const bool rec = a.pre_fired != nullptr;
     if (fused_pairs() == 2) {
-        if (fine) k_post<true, 2, false><<<g, b, 0, s>>>(a);
-        else if (rec) k_post<false, 2, true><<<g, b, 0, s>>>(a);
-        else k_post<false, 2, false><<<g, b, 0, s>>>(a);
+        if (fine) k_post<T, true, 2, false><<<g, b, 0, s>>>(a);
+        else if (rec) k_post<T, false, 2, true><<<g, b, 0, s>>>(a);
+        else k_post<T, false, 2, false><<<g, b, 0, s>>>(a);
     } else {
-        if (fine) k_post<true, 1, false><<<g, b, 0, s>>>(a);
-        else if (rec) k_post<false, 1, true><<<g, b, 0, s>>>(a);
-        else k_post<false, 1, false><<<g, b, 0, s>>>(a);
+        if (fine) k_post<T, true, 1, false><<<g, b, 0, s>>>(a);
+        else if (rec) k_post<T, false, 1, true><<<g, b, 0, s>>>(a);
+        else k_post<T, false, 1, false><<<g, b, 0, s>>>(a);
     }
 }
 
@@ -837,27 +823,31 @@ int postpre_blocks(int N, int jc0, int jc1)
     return gx * gy;
 }
 
-void launch_postpre(const PostPreArgs &a0, hipStream_t s)
+// PGMG_PP_VARIANT (fp64 only, measurement): 1 trivial arithmetic, 2 <= 128 VGPRs,
+// 3 no column overlap, 4 per-wave HBM loads (no LDS staging)
+template <class T>
+void launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
 {
     int t, gx, gy, r;
-    const int variant = env_int("PGMG_PP_VARIANT", 0);
+    const int variant = std::is_same<T, double>::value ? env_int("PGMG_PP_VARIANT", 0) : 0;
     fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, variant == 3 ? 128 : kPPStride);
-    PostPreArgs a = a0;
+    PostPreArgsT<T> a = a0;
     a.rows_per_block = r;
     const dim3 g(gx, gy), b(t);
-    if (variant == 0) k_postpre_lds<<<g, b, 0, s>>>(a);
-    else if (variant == 4) k_postpre<1, 0><<<g, b, 0, s>>>(a);    // per-wave loads (r01)
-    else if (variant == 1) k_postpre<1, 1><<<g, b, 0, s>>>(a);
-    else if (variant == 3) k_postpre<1, 1, 128, 0><<<g, b, 0, s>>>(a);  // no column overlap
-    else if (variant == 2) k_postpre_o4<1><<<g, b, 0, s>>>(a);
-    else if (env_int("PGMG_PP_PAIRS", 1) >= 2) k_postpre<2, 0><<<g, b, 0, s>>>(a);
-    else k_postpre<1, 0><<<g, b, 0, s>>>(a);
+    if constexpr (std::is_same<T, double>::value) {
+        if (variant == 4) k_postpre<T, 1, 0><<<g, b, 0, s>>>(a);    // per-wave loads (r01)
+        else if (variant == 1) k_postpre<T, 1, 1><<<g, b, 0, s>>>(a);
+        else if (variant == 3) k_postpre<T, 1, 1, 128, 0><<<g, b, 0, s>>>(a);  // no column overlap
+        else if (variant == 2) k_postpre_o4<T, 1><<<g, b, 0, s>>>(a);
+        if (variant != 0) return;
+    }
+    k_postpre_lds<T><<<g, b, 0, s>>>(a);
 }
 
-void launch_postpre_decide(const PostPreArgs &a, int np, double eps, unsigned *flags, hipStream_t s)
+void launch_postpre_decide(const double *partials1, const double *partials2, unsigned long long *stats,
+                           int np, double eps, unsigned *flags, hipStream_t s)
 {
-    k_postpre_decide<<<dim3(1), dim3(256), 0, s>>>(a.partials1, a.partials2, np, eps, flags,
-                                                  a.stats);
+    k_postpre_decide<<<dim3(1), dim3(256), 0, s>>>(partials1, partials2, np, eps, flags, stats);
 }
 
 // ---------------------------------------------------------------------------
@@ -885,82 +875,88 @@ __device__ __forceinline__ bool fix_decide(const FixArgsF &a, double *red, int *
     return t;
 }
 
+template <class T>
 struct FixCtx {
-    const double *x0, *f;
-    const double *ec;
+    const T *x0, *f;
+    const T *ec;
     int N, Nc;
     long long P, Pc;
-    double hh, ih;
+    T hh, ih;
     bool x0_zero;
     const unsigned *pre_fired;  // non-null: phi (x0 of fxeff) is recomputed from f
 };
 
-__device__ __forceinline__ double fx0(const FixCtx &c, int j, int i)
+template <class T>
+__device__ __forceinline__ T fx0(const FixCtx<T> &c, int j, int i)
 {
-    return c.x0_zero ? 0.0 : c.x0[(long long)j * c.P + i];
+    return c.x0_zero ? T(0) : c.x0[(long long)j * c.P + i];
 }
 
-template <bool POST>
-__device__ double fx1(const FixCtx &c, int j, int i);
+template <bool POST, class T>
+__device__ T fx1(const FixCtx<T> &c, int j, int i);
 
 // pre-smoothed iterate of x0 = 0 (k_post RECOMP): x1 = J(0), phi = fired ? x1 : J(x1)
-__device__ double fphi0(const FixCtx &c, int j, int i)
+template <class T>
+__device__ T fphi0(const FixCtx<T> &c, int j, int i)
 {
-    FixCtx z = c;
+    FixCtx<T> z = c;
     z.x0_zero = true;
     z.pre_fired = nullptr;
     if (*c.pre_fired != 0u || j <= 0 || i <= 0 || j >= c.N - 1 || i >= c.N - 1)
         return fx1<false>(z, j, i);
-    return 0.25 * ((c.hh * c.f[(long long)j * c.P + i]) + fx1<false>(z, j, i - 1) +
+    return T(0.25) * ((c.hh * c.f[(long long)j * c.P + i]) + fx1<false>(z, j, i - 1) +
                    fx1<false>(z, j, i + 1) + fx1<false>(z, j - 1, i) + fx1<false>(z, j + 1, i));
 }
 
 // x_eff = phi + P ec at one fine point (MultiGrid.hpp:208-226)
-__device__ double fxeff(const FixCtx &c, int j, int i)
+template <class T>
+__device__ T fxeff(const FixCtx<T> &c, int j, int i)
 {
-    double v = c.pre_fired != nullptr ? fphi0(c, j, i) : c.x0[(long long)j * c.P + i];
+    T v = c.pre_fired != nullptr ? fphi0(c, j, i) : c.x0[(long long)j * c.P + i];
     if (j < 2 || i < 2 || j > c.N - 2 || i > c.N - 2) return v;
     const int jc = j >> 1, ic = i >> 1;
-    const double *C0 = c.ec + (long long)jc * c.Pc;
-    double w;
+    const T *C0 = c.ec + (long long)jc * c.Pc;
+    T w;
     if ((j & 1) == 0) {
-        w = ((i & 1) == 0) ? C0[ic] : 0.5 * (C0[ic] + C0[ic + 1]);
+        w = ((i & 1) == 0) ? C0[ic] : T(0.5) * (C0[ic] + C0[ic + 1]);
     } else {
-        const double *C1 = C0 + c.Pc;
-        w = ((i & 1) == 0) ? 0.5 * (C0[ic] + C1[ic]) : 0.25 * (C0[ic] + C0[ic + 1] + C1[ic] + C1[ic + 1]);
+        const T *C1 = C0 + c.Pc;
+        w = ((i & 1) == 0) ? T(0.5) * (C0[ic] + C1[ic]) : T(0.25) * (C0[ic] + C0[ic + 1] + C1[ic] + C1[ic + 1]);
     }
     return v + w;
 }
 
-template <bool POST>
-__device__ double fin(const FixCtx &c, int j, int i)
+template <bool POST, class T>
+__device__ T fin(const FixCtx<T> &c, int j, int i)
 {
     return POST ? fxeff(c, j, i) : fx0(c, j, i);
 }
 
-template <bool POST>
-__device__ double fx1(const FixCtx &c, int j, int i)
+template <bool POST, class T>
+__device__ T fx1(const FixCtx<T> &c, int j, int i)
 {
     if (j <= 0 || i <= 0 || j >= c.N - 1 || i >= c.N - 1) return fin<POST>(c, j, i);
-    return 0.25 * ((c.hh * c.f[(long long)j * c.P + i]) + fin<POST>(c, j, i - 1) +
+    return T(0.25) * ((c.hh * c.f[(long long)j * c.P + i]) + fin<POST>(c, j, i - 1) +
                    fin<POST>(c, j, i + 1) + fin<POST>(c, j - 1, i) + fin<POST>(c, j + 1, i));
 }
 
-__device__ double fr1(const FixCtx &c, int j, int i)
+template <class T>
+__device__ T fr1(const FixCtx<T> &c, int j, int i)
 {
     return c.f[(long long)j * c.P + i] -
-           c.ih * (4 * fx1<false>(c, j, i) - fx1<false>(c, j, i - 1) - fx1<false>(c, j, i + 1) -
+           c.ih * (T(4) * fx1<false>(c, j, i) - fx1<false>(c, j, i - 1) - fx1<false>(c, j, i + 1) -
                    fx1<false>(c, j - 1, i) - fx1<false>(c, j + 1, i));
 }
 
-__global__ __launch_bounds__(256) void k_pre_fixup(FixArgsF a, PreArgs p, int x0_zero)
+template <class T>
+__global__ __launch_bounds__(256) void k_pre_fixup(FixArgsF a, PreArgsT<T> p, int x0_zero)
 {
     __shared__ double red[4];
     __shared__ int trig;
     const bool t = fix_decide(a, red, &trig);
     if (p.fired != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *p.fired = t ? 1u : 0u;
     if (!t) return;
-    FixCtx c{p.x0, p.f, nullptr, p.N, p.Nc, p.P, p.Pc, p.hh, p.ih, x0_zero != 0, nullptr};
+    FixCtx<T> c{p.x0, p.f, nullptr, p.N, p.Nc, p.P, p.Pc, p.hh, p.ih, x0_zero != 0, nullptr};
     const long long W = p.N - 2;
     const long long nrows = p.x2 != nullptr ? (long long)(p.row_hi - p.row_lo) : 0;
     const long long stride = (long long)gridDim.x * blockDim.x;
@@ -975,17 +971,18 @@ __global__ __launch_bounds__(256) void k_pre_fixup(FixArgsF a, PreArgs p, int x0
         const int jc = clo + (int)(k / Wc), ic = 1 + (int)(k % Wc);
         const int j = 2 * jc, i = 2 * ic;
         p.rc[(long long)jc * p.Pc + ic] =
-            0.25 * fr1(c, j, i) + 0.125 * (fr1(c, j, i + 1) + fr1(c, j, i - 1) + fr1(c, j + 1, i) + fr1(c, j - 1, i)) +
-            0.0625 * (fr1(c, j - 1, i - 1) + fr1(c, j - 1, i + 1) + fr1(c, j + 1, i - 1) + fr1(c, j + 1, i + 1));
+            T(0.25) * fr1(c, j, i) + T(0.125) * (fr1(c, j, i + 1) + fr1(c, j, i - 1) + fr1(c, j + 1, i) + fr1(c, j - 1, i)) +
+            T(0.0625) * (fr1(c, j - 1, i - 1) + fr1(c, j - 1, i + 1) + fr1(c, j + 1, i - 1) + fr1(c, j + 1, i + 1));
     }
 }
 
-__global__ __launch_bounds__(256) void k_post_fixup(FixArgsF a, PostArgs p)
+template <class T>
+__global__ __launch_bounds__(256) void k_post_fixup(FixArgsF a, PostArgsT<T> p)
 {
     __shared__ double red[4];
     __shared__ int trig;
     if (!fix_decide(a, red, &trig)) return;
-    FixCtx c{p.phi, p.f, p.ec, p.N, p.Nc, p.P, p.Pc, p.hh, p.ih, false, p.pre_fired};
+    FixCtx<T> c{p.phi, p.f, p.ec, p.N, p.Nc, p.P, p.Pc, p.hh, p.ih, false, p.pre_fired};
     const long long W = p.N - 2;
     const long long nrows = (long long)(p.row_hi - p.row_lo);
     const long long stride = (long long)gridDim.x * blockDim.x;
@@ -995,14 +992,26 @@ __global__ __launch_bounds__(256) void k_post_fixup(FixArgsF a, PostArgs p)
     }
 }
 
-void launch_pre_fixup(const FixArgsF &a, const PreArgs &p, bool x0_zero, hipStream_t s)
+template <class T>
+void launch_pre_fixup(const FixArgsF &a, const PreArgsT<T> &p, bool x0_zero, hipStream_t s)
 {
-    k_pre_fixup<<<dim3(256), dim3(256), 0, s>>>(a, p, x0_zero ? 1 : 0);
+    k_pre_fixup<T><<<dim3(256), dim3(256), 0, s>>>(a, p, x0_zero ? 1 : 0);
 }
 
-void launch_post_fixup(const FixArgsF &a, const PostArgs &p, hipStream_t s)
+template <class T>
+void launch_post_fixup(const FixArgsF &a, const PostArgsT<T> &p, hipStream_t s)
 {
-    k_post_fixup<<<dim3(256), dim3(256), 0, s>>>(a, p);
+    k_post_fixup<T><<<dim3(256), dim3(256), 0, s>>>(a, p);
 }
+
+#define PGMG_INSTANTIATE(T)                                                                       \
+    template void launch_pre<T>(const PreArgsT<T> &, bool, bool, hipStream_t);                   \
+    template void launch_post<T>(const PostArgsT<T> &, bool, hipStream_t);                       \
+    template void launch_postpre<T>(const PostPreArgsT<T> &, hipStream_t);                       \
+    template void launch_pre_fixup<T>(const FixArgsF &, const PreArgsT<T> &, bool, hipStream_t);  \
+    template void launch_post_fixup<T>(const FixArgsF &, const PostArgsT<T> &, hipStream_t);
+PGMG_INSTANTIATE(double)
+PGMG_INSTANTIATE(float)
+#undef PGMG_INSTANTIATE
 
 }  // namespace pgmg

@@ -7,15 +7,19 @@
 //   lane t owns is one aligned 16-byte load and a wave's 64 pairs are exactly
 //   eight 128-byte lines.
 //
-// All kernels compute in fp64 with -ffp-contract=off and keep the reference's
-// left-to-right expression order, so results are bit-identical to mg_cpu_exec.
+// All kernels keep the reference's left-to-right expression order and are built with
+// -ffp-contract=off, so the fp64 instantiations are bit-identical to mg_cpu_exec.  Level
+// kernels are templates on the element type T (double, or float for the fp32 variant,
+// pgmg_real.h); the argument blocks below are templated alike (XxxArgsT<T>).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "pgmg_real.h"
+
 namespace pgmg {
 
-constexpr int kOff = 15;          // doubles between allocation base and element (0,0)
+constexpr int kOff = 15;          // doubles between allocation base and element (0,0) (fp64)
 constexpr int kHalo = 6;          // halo rows allocated above and below a level's rows
 constexpr int kBlock = 256;       // threads per block for streaming kernels (4 waves)
 constexpr int kTailThreads = 1024;
@@ -27,57 +31,62 @@ inline size_t alloc_elems(int rows, int N) { return (size_t)kOff + (size_t)rows 
 // One sweep x_out = J(x_in) over interior rows [row0,row1) of a W-column grid.
 // With partials != nullptr it also accumulates sum r(x_in)^2 over the same points
 // per block: the smoother's early-exit norm of the PREVIOUS sweep, fused.
-struct SweepArgs {
-    const double *xin;      // origin pointer (element (0,0)); unused when x0 is zero
-    const double *f;
-    double *xout;
+template <class T>
+struct SweepArgsT {
+    const T *xin;           // origin pointer (element (0,0)); unused when x0 is zero
+    const T *f;
+    T *xout;
     double *partials;       // one double per block, or nullptr
     const unsigned *skip;   // non-null and *skip != 0: the kernel does nothing
     unsigned *reset;        // non-null: block 0 writes 0 here (start of a smooth call)
     unsigned long long *stats;  // [0] sweeps performed (block 0 adds 1)
-    double hh, inv_hh;      // h*h and 1.0/(h*h), rounded once on the host
-    int W, P;               // columns, pitch (doubles)
+    T hh, inv_hh;           // h*h and 1.0/(h*h), rounded once on the host
+    int W, P;               // columns, pitch (elements)
     int row0, row1;         // rows to update (local indexing)
     int rows_per_block;
 };
 
 // rc = R r(x) on coarse rows [jc0, jc1); the residual is never materialised.
-struct ResRestrictArgs {
-    const double *x, *f;
-    double *rc;
-    double inv_hh;
+template <class T>
+struct ResRestrictArgsT {
+    const T *x, *f;
+    T *rc;
+    T inv_hh;
     int Wf, Pf, Wc, Pc;
     int jc0, jc1;
     int rows_per_block;     // coarse rows per block
 };
 
 // fine += P coarse (reference flavour: fine row/col 1 never corrected).
-struct ProlongArgs {
-    const double *c;
-    double *fine;
+template <class T>
+struct ProlongArgsT {
+    const T *c;
+    T *fine;
     int Wf, Pf, Wc, Pc;
     int row0, row1;         // fine rows to update, inside [2, Nf-2]
     int rows_per_block;
 };
 
 // Early-exit decision for one smoother check plus the undo of the speculative sweep.
-struct FixupArgs {
+template <class T>
+struct FixupArgsT {
     const double *partials;
     int np;
     double eps;
     const unsigned *done_prev;  // smoother already exited before this sweep
     unsigned *done_next;        // written: done_prev || (norm < eps)
-    const double *src;          // buffer holding x_{k-1}
-    double *dst;                // buffer the speculative sweep k wrote
+    const T *src;               // buffer holding x_{k-1}
+    T *dst;                     // buffer the speculative sweep k wrote
     unsigned long long *stats;
     int W, P, row0, row1;       // region copied on trigger
     const double *global_sum;   // all-rank sum of the partials (multi-GPU) or nullptr
 };
 
 // The whole V-cycle at and below a level with N <= 65, in LDS, one workgroup.
-struct TailArgs {
-    const double *f_top;    // rhs of the tail's top level (global origin pointer)
-    double *e_top;          // solution of the tail's top level (global origin pointer)
+template <class T>
+struct TailArgsT {
+    const T *f_top;         // rhs of the tail's top level (global origin pointer)
+    T *e_top;               // solution of the tail's top level (global origin pointer)
     int P_top;              // pitch of f_top / e_top
     int N_top;
     double h_top;
@@ -95,28 +104,42 @@ struct TailArgs {
     double fmg_factor;           // (pi^2/a^2)(p^2+q^2)
 };
 
+using SweepArgs = SweepArgsT<double>;
+using ResRestrictArgs = ResRestrictArgsT<double>;
+using ProlongArgs = ProlongArgsT<double>;
+using FixupArgs = FixupArgsT<double>;
+using TailArgs = TailArgsT<double>;
+
 // sweeps on the finest level use a distinct kernel symbol (kFine) so that
 // rocprofv3's per-kernel statistics isolate the roofline kernel.
-void launch_sweep(const SweepArgs &a, bool x0_zero, bool fine_level, hipStream_t s);
+template <class T> void launch_sweep(const SweepArgsT<T> &a, bool x0_zero, bool fine_level, hipStream_t s);
 int sweep_blocks(int W, int row0, int row1, int *rows_per_block, int *gx, int *gy);
-void launch_res_restrict(const ResRestrictArgs &a, hipStream_t s);
+template <class T> void launch_res_restrict(const ResRestrictArgsT<T> &a, hipStream_t s);
 int res_restrict_rows_per_block(int Wc, int nrows);
-void launch_prolong(const ProlongArgs &a, hipStream_t s);
-void launch_fixup(const FixupArgs &a, hipStream_t s);
-void launch_copy_rows(const double *src, double *dst, int W, int P, int row0, int row1,
-                      hipStream_t s);
-hipError_t launch_tail(const TailArgs &a, hipStream_t s);
-hipError_t launch_tail_gamma(const TailArgs &a, int gamma, hipStream_t s);
-size_t tail_lds_doubles(int N_top, int n_coarse);
-void launch_rhs(double *f, const double *sx, const double *sy, double factor, int W, int P,
-                int row0, int row1, hipStream_t s);
+template <class T> void launch_prolong(const ProlongArgsT<T> &a, hipStream_t s);
+template <class T> void launch_fixup(const FixupArgsT<T> &a, hipStream_t s);
+template <class T>
+void launch_copy_rows(const T *src, T *dst, int W, int P, int row0, int row1, hipStream_t s);
+template <class T> hipError_t launch_tail_gamma(const TailArgsT<T> &a, int gamma, hipStream_t s);
+template <class T> size_t tail_lds_bytes(int N_top, int n_coarse);
+// f = (factor * sx[i]) * sy[j] in double, stored as T
+template <class T>
+void launch_rhs(T *f, const double *sx, const double *sy, double factor, int W, int P, int row0,
+                int row1, hipStream_t s);
 // coarse = R fine on interior coarse points (values, not residuals): compute_coarsest_grid
-void launch_restrict_values(const double *fine, int Nf, int Pf, double *coarse, int Nc, int Pc,
+template <class T>
+void launch_restrict_values(const T *fine, int Nf, int Pf, T *coarse, int Nc, int Pc,
                             hipStream_t s);
-void launch_fill_rows(double *o, int P, int row0, int row1, double v, hipStream_t s);
-void launch_resnorm_partials(const double *x, const double *f, double *partials, double inv_hh,
-                             int W, int P, int row0, int row1, int nblocks, hipStream_t s);
+template <class T> void launch_fill_rows(T *o, int P, int row0, int row1, hipStream_t s);
+template <class T>
+void launch_resnorm_partials(const T *x, const T *f, double *partials, T inv_hh, int W, int P,
+                             int row0, int row1, int nblocks, hipStream_t s);
 void launch_sum_partials(const double *partials, int np, double *out, hipStream_t s);
+// widen / narrow a level's rows between T storage and a double staging array (pitch N)
+template <class T>
+void launch_to_double(const T *src, int P, double *dst, int N, int row0, int row1, hipStream_t s);
+template <class T>
+void launch_from_double(const double *src, int N, T *dst, int P, int row0, int row1, hipStream_t s);
 
 // reference-layout (pitch = W, any alignment) op kernels
 void launch_g_sweep(const double *xin, const double *f, double *xout, double *partials,

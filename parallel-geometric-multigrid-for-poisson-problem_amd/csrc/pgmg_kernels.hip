@@ -18,27 +18,6 @@
 
 namespace pgmg {
 
-// ---------------------------------------------------------------------------
-// lane exchange: wave64 DPP moves on the two dword halves of a double
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ double dpp_prev(double v)  // lane i <- lane i-1 (wave_shr:1)
-{
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x138, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xF, 0xF, false);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-__device__ __forceinline__ double dpp_next(double v)  // lane i <- lane i+1 (wave_shl:1)
-{
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x130, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x130, 0xF, 0xF, false);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-
-__device__ __forceinline__ double2 ld2(const double *p) { return *reinterpret_cast<const double2 *>(p); }
-__device__ __forceinline__ void st2(double *p, double2 v) { *reinterpret_cast<double2 *>(p) = v; }
-
 // deterministic block sum (fixed tree) of one double per thread; result valid in thread 0
 template <int NT>
 __device__ __forceinline__ double block_sum(double v, double *red)
@@ -64,8 +43,8 @@ __device__ __forceinline__ double block_sum(double v, double *red)
 // ---------------------------------------------------------------------------
 constexpr int kU = 4;  // rows in flight per wave
 
-template <bool X0_ZERO, bool NORM, bool FINE>
-__global__ __launch_bounds__(kBlock) void k_sweep(SweepArgs a)
+template <class T, bool X0_ZERO, bool NORM, bool FINE>
+__global__ __launch_bounds__(kBlock) void k_sweep(SweepArgsT<T> a)
 {
     __shared__ double red[kBlock / 64];
     if (a.skip != nullptr && *a.skip != 0u) return;  // smoother already exited (uniform)
@@ -84,57 +63,58 @@ __global__ __launch_bounds__(kBlock) void k_sweep(SweepArgs a)
     const int jb = a.row0 + blockIdx.y * a.rows_per_block;
     const int je = min(jb + a.rows_per_block, a.row1);
     const long long P = a.P;
-    const double *__restrict__ X = a.xin;
-    const double *__restrict__ F = a.f;
-    double *__restrict__ O = a.xout;
-    const double hh = a.hh, ih = a.inv_hh;
+    using D2 = V2<T>;
+    const T *__restrict__ X = a.xin;
+    const T *__restrict__ F = a.f;
+    T *__restrict__ O = a.xout;
+    const T hh = a.hh, ih = a.inv_hh;
     double acc = 0.0;
 
-    double2 w0 = make_double2(0.0, 0.0), w1 = make_double2(0.0, 0.0);
+    D2 w0 = zero2<T>(), w1 = zero2<T>();
     if (!X0_ZERO) {
-        w0 = ld2(X + (jb - 1) * P + c);
-        w1 = ld2(X + jb * P + c);
+        w0 = ldv(X + (jb - 1) * P + c);
+        w1 = ldv(X + jb * P + c);
     }
     for (int j = jb; j < je; j += kU) {
-        double2 xn[kU], fv[kU];
-        double el[kU], er[kU];
+        D2 xn[kU], fv[kU];
+        T el[kU], er[kU];
         #pragma unroll
         for (int u = 0; u < kU; ++u) {
             const int r = min(j + u, je - 1);
-            fv[u] = ld2(F + r * P + c);
-            el[u] = 0.0;
-            er[u] = 0.0;
+            fv[u] = ldv(F + r * P + c);
+            el[u] = T(0);
+            er[u] = T(0);
             if (!X0_ZERO) {
-                xn[u] = ld2(X + (r + 1) * P + c);
+                xn[u] = ldv(X + (r + 1) * P + c);
                 if (lane == 0) el[u] = X[r * P + c - 1];
                 if (lane == 63) er[u] = X[r * P + c + 2];
             } else {
-                xn[u] = make_double2(0.0, 0.0);
+                xn[u] = zero2<T>();
             }
         }
         #pragma unroll
         for (int u = 0; u < kU; ++u) {
             const int r = j + u;
-            const double2 up = (u == 0) ? w0 : (u == 1 ? w1 : xn[u - 2]);
-            const double2 ce = (u == 0) ? w1 : xn[u - 1];
-            const double2 dn = xn[u];
-            double left = dpp_prev(ce.y);
-            double right = dpp_next(ce.x);
+            const D2 up = (u == 0) ? w0 : (u == 1 ? w1 : xn[u - 2]);
+            const D2 ce = (u == 0) ? w1 : xn[u - 1];
+            const D2 dn = xn[u];
+            T left = dpp_shr(ce.y);
+            T right = dpp_shl(ce.x);
             if (lane == 0) left = el[u];
             if (lane == 63) right = er[u];
-            double2 o;
-            o.x = 0.25 * ((hh * fv[u].x) + left + ce.y + up.x + dn.x);
-            o.y = second ? 0.25 * ((hh * fv[u].y) + ce.x + right + up.y + dn.y) : ce.y;
+            D2 o;
+            o.x = T(0.25) * ((hh * fv[u].x) + left + ce.y + up.x + dn.x);
+            o.y = second ? T(0.25) * ((hh * fv[u].y) + ce.x + right + up.y + dn.y) : ce.y;
             const bool live = act && r < je;
             if (NORM) {
-                const double r0 = fv[u].x - ih * (4 * ce.x - left - ce.y - up.x - dn.x);
-                const double r1 = fv[u].y - ih * (4 * ce.y - ce.x - right - up.y - dn.y);
+                const T r0 = fv[u].x - ih * (T(4) * ce.x - left - ce.y - up.x - dn.x);
+                const T r1 = fv[u].y - ih * (T(4) * ce.y - ce.x - right - up.y - dn.y);
                 if (live) {
-                    acc += r0 * r0;
-                    if (second) acc += r1 * r1;
+                    acc += sq(r0);
+                    if (second) acc += sq(r1);
                 }
             }
-            if (live) st2(O + r * P + c, o);
+            if (live) stv(O + r * P + c, o);
         }
         w0 = xn[kU - 2];
         w1 = xn[kU - 1];
@@ -161,22 +141,23 @@ int sweep_blocks(int W, int row0, int row1, int *rows_per_block, int *gx, int *g
     return bx * by;
 }
 
-void launch_sweep(const SweepArgs &a, bool x0_zero, bool fine, hipStream_t s)
+template <class T>
+void launch_sweep(const SweepArgsT<T> &a, bool x0_zero, bool fine, hipStream_t s)
 {
     int rpb, gx, gy;
     sweep_blocks(a.W, a.row0, a.row1, &rpb, &gx, &gy);
-    SweepArgs b = a;
+    SweepArgsT<T> b = a;
     b.rows_per_block = rpb;
     const dim3 grid(gx, gy), blk(kBlock);
     const bool norm = a.partials != nullptr;
     if (fine) {
-        if (x0_zero) k_sweep<true, false, true><<<grid, blk, 0, s>>>(b);
-        else if (norm) k_sweep<false, true, true><<<grid, blk, 0, s>>>(b);
-        else k_sweep<false, false, true><<<grid, blk, 0, s>>>(b);
+        if (x0_zero) k_sweep<T, true, false, true><<<grid, blk, 0, s>>>(b);
+        else if (norm) k_sweep<T, false, true, true><<<grid, blk, 0, s>>>(b);
+        else k_sweep<T, false, false, true><<<grid, blk, 0, s>>>(b);
     } else {
-        if (x0_zero) k_sweep<true, false, false><<<grid, blk, 0, s>>>(b);
-        else if (norm) k_sweep<false, true, false><<<grid, blk, 0, s>>>(b);
-        else k_sweep<false, false, false><<<grid, blk, 0, s>>>(b);
+        if (x0_zero) k_sweep<T, true, false, false><<<grid, blk, 0, s>>>(b);
+        else if (norm) k_sweep<T, false, true, false><<<grid, blk, 0, s>>>(b);
+        else k_sweep<T, false, false, false><<<grid, blk, 0, s>>>(b);
     }
 }
 
@@ -188,39 +169,44 @@ void launch_sweep(const SweepArgs &a, bool x0_zero, bool fine, hipStream_t s)
 // with F = r computed on the fly (never written to HBM).  Lane t produces coarse
 // column ic = t+1, whose fine centre column is c+1 (c = 2t+1).
 // ---------------------------------------------------------------------------
+template <class T>
 struct XRow {
-    double2 own;   // x at (c, c+1)
-    double2 nxt;   // x at (c+2, c+3)
-    double lft;    // x at c-1
+    V2<T> own;   // x at (c, c+1)
+    V2<T> nxt;   // x at (c+2, c+3)
+    T lft;       // x at c-1
 };
 
-__device__ __forceinline__ XRow load_xrow(const double *X, long long off, int c, int lane)
+template <class T>
+__device__ __forceinline__ XRow<T> load_xrow(const T *X, long long off, int c, int lane)
 {
-    XRow r;
-    r.own = ld2(X + off + c);
-    r.nxt.x = dpp_next(r.own.x);
-    r.nxt.y = dpp_next(r.own.y);
-    r.lft = dpp_prev(r.own.y);
-    if (lane == 63) r.nxt = ld2(X + off + c + 2);
+    XRow<T> r;
+    r.own = ldv(X + off + c);
+    r.nxt.x = dpp_shl(r.own.x);
+    r.nxt.y = dpp_shl(r.own.y);
+    r.lft = dpp_shr(r.own.y);
+    if (lane == 63) r.nxt = ldv(X + off + c + 2);
     if (lane == 0) r.lft = X[off + c - 1];
     return r;
 }
 
+template <class T>
 struct RTriple {
-    double r0, r1, r2;  // residual at columns c, c+1, c+2
+    T r0, r1, r2;  // residual at columns c, c+1, c+2
 };
 
-__device__ __forceinline__ RTriple resid3(const XRow &u, const XRow &m, const XRow &d, double2 fo,
-                                          double fn, double ih)
+template <class T>
+__device__ __forceinline__ RTriple<T> resid3(const XRow<T> &u, const XRow<T> &m, const XRow<T> &d,
+                                             V2<T> fo, T fn, T ih)
 {
-    RTriple r;
-    r.r0 = fo.x - ih * (4 * m.own.x - m.lft - m.own.y - u.own.x - d.own.x);
-    r.r1 = fo.y - ih * (4 * m.own.y - m.own.x - m.nxt.x - u.own.y - d.own.y);
-    r.r2 = fn - ih * (4 * m.nxt.x - m.own.y - m.nxt.y - u.nxt.x - d.nxt.x);
+    RTriple<T> r;
+    r.r0 = fo.x - ih * (T(4) * m.own.x - m.lft - m.own.y - u.own.x - d.own.x);
+    r.r1 = fo.y - ih * (T(4) * m.own.y - m.own.x - m.nxt.x - u.own.y - d.own.y);
+    r.r2 = fn - ih * (T(4) * m.nxt.x - m.own.y - m.nxt.y - u.nxt.x - d.nxt.x);
     return r;
 }
 
-__global__ __launch_bounds__(kBlock) void k_res_restrict(ResRestrictArgs a)
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_res_restrict(ResRestrictArgsT<T> a)
 {
     const int lane = threadIdx.x & 63;
     const int nact = a.Wc - 2;                   // coarse interior columns
@@ -232,34 +218,34 @@ __global__ __launch_bounds__(kBlock) void k_res_restrict(ResRestrictArgs a)
     const int jce = min(jcb + a.rows_per_block, a.jc1);
     if (jcb >= jce) return;
     const long long Pf = a.Pf, Pc = a.Pc;
-    const double *__restrict__ X = a.x;
-    const double *__restrict__ F = a.f;
-    const double ih = a.inv_hh;
+    const T *__restrict__ X = a.x;
+    const T *__restrict__ F = a.f;
+    const T ih = a.inv_hh;
 
     // window: x rows 2jc-1 (A) and 2jc (B); r row 2jc-1 (up)
-    XRow xz = load_xrow(X, (2LL * jcb - 2) * Pf, c, lane);
-    XRow xa = load_xrow(X, (2LL * jcb - 1) * Pf, c, lane);
-    XRow xb = load_xrow(X, (2LL * jcb) * Pf, c, lane);
-    double2 fo = ld2(F + (2LL * jcb - 1) * Pf + c);
-    double fn = dpp_next(fo.x);
+    XRow<T> xz = load_xrow(X, (2LL * jcb - 2) * Pf, c, lane);
+    XRow<T> xa = load_xrow(X, (2LL * jcb - 1) * Pf, c, lane);
+    XRow<T> xb = load_xrow(X, (2LL * jcb) * Pf, c, lane);
+    V2<T> fo = ldv(F + (2LL * jcb - 1) * Pf + c);
+    T fn = dpp_shl(fo.x);
     if (lane == 63) fn = F[(2LL * jcb - 1) * Pf + c + 2];
-    RTriple up = resid3(xz, xa, xb, fo, fn, ih);
+    RTriple<T> up = resid3(xz, xa, xb, fo, fn, ih);
 
     for (int jc = jcb; jc < jce; ++jc) {
         const long long rm = 2LL * jc, rd = rm + 1;
-        const XRow xc = load_xrow(X, rd * Pf, c, lane);
-        const XRow xd = load_xrow(X, (rd + 1) * Pf, c, lane);
-        const double2 fm = ld2(F + rm * Pf + c);
-        const double2 fd = ld2(F + rd * Pf + c);
-        double fmn = dpp_next(fm.x), fdn = dpp_next(fd.x);
+        const XRow<T> xc = load_xrow(X, rd * Pf, c, lane);
+        const XRow<T> xd = load_xrow(X, (rd + 1) * Pf, c, lane);
+        const V2<T> fm = ldv(F + rm * Pf + c);
+        const V2<T> fd = ldv(F + rd * Pf + c);
+        T fmn = dpp_shl(fm.x), fdn = dpp_shl(fd.x);
         if (lane == 63) {
             fmn = F[rm * Pf + c + 2];
             fdn = F[rd * Pf + c + 2];
         }
-        const RTriple mid = resid3(xa, xb, xc, fm, fmn, ih);
-        const RTriple dn = resid3(xb, xc, xd, fd, fdn, ih);
-        const double v = 0.25 * mid.r1 + 0.125 * (mid.r2 + mid.r0 + dn.r1 + up.r1) +
-                         0.0625 * (up.r0 + up.r2 + dn.r0 + dn.r2);
+        const RTriple<T> mid = resid3(xa, xb, xc, fm, fmn, ih);
+        const RTriple<T> dn = resid3(xb, xc, xd, fd, fdn, ih);
+        const T v = T(0.25) * mid.r1 + T(0.125) * (mid.r2 + mid.r0 + dn.r1 + up.r1) +
+                    T(0.0625) * (up.r0 + up.r2 + dn.r0 + dn.r2);
         if (act) a.rc[jc * Pc + (t + 1)] = v;
         up = dn;
         xa = xc;
@@ -274,14 +260,15 @@ int res_restrict_rows_per_block(int Wc, int nrows)
     return rpb < 2 ? 2 : (rpb > 32 ? 32 : rpb);
 }
 
-void launch_res_restrict(const ResRestrictArgs &a, hipStream_t s)
+template <class T>
+void launch_res_restrict(const ResRestrictArgsT<T> &a, hipStream_t s)
 {
     const int bx = (a.Wc - 2 + kBlock - 1) / kBlock;
     const int rows = a.jc1 - a.jc0;
-    ResRestrictArgs b = a;
+    ResRestrictArgsT<T> b = a;
     b.rows_per_block = res_restrict_rows_per_block(a.Wc, rows);
     const int by = (rows + b.rows_per_block - 1) / b.rows_per_block;
-    k_res_restrict<<<dim3(bx, by), dim3(kBlock), 0, s>>>(b);
+    k_res_restrict<T><<<dim3(bx, by), dim3(kBlock), 0, s>>>(b);
 }
 
 // ---------------------------------------------------------------------------
@@ -293,7 +280,8 @@ void launch_res_restrict(const ResRestrictArgs &a, hipStream_t s)
 // for ic, jc in [1, Nc-2]: every fine point in [2, Nf-2]^2 is written exactly
 // once, fine row/col 1 never.  Each lane gathers its own value.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_prolong(ProlongArgs a)
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_prolong(ProlongArgsT<T> a)
 {
     const int npairs = (a.Wf - 1) >> 1;
     const int t_raw = blockIdx.x * kBlock + threadIdx.x;
@@ -307,33 +295,34 @@ __global__ __launch_bounds__(kBlock) void k_prolong(ProlongArgs a)
     const long long Pf = a.Pf, Pc = a.Pc;
     for (int j = jb; j < je; ++j) {
         const int jc = j >> 1;
-        const double *C0 = a.c + jc * Pc;
-        const double c00 = C0[t], c01 = C0[t + 1];
-        double2 v = ld2(a.fine + j * Pf + c);
+        const T *C0 = a.c + jc * Pc;
+        const T c00 = C0[t], c01 = C0[t + 1];
+        V2<T> v = ldv(a.fine + j * Pf + c);
         if ((j & 1) == 0) {
-            if (okx) v.x = v.x + 0.5 * (c00 + c01);
+            if (okx) v.x = v.x + T(0.5) * (c00 + c01);
             if (oky) v.y = v.y + c01;
         } else {
-            const double *C1 = C0 + Pc;
-            const double c10 = C1[t], c11 = C1[t + 1];
-            if (okx) v.x = v.x + 0.25 * (c00 + c01 + c10 + c11);
-            if (oky) v.y = v.y + 0.5 * (c01 + c11);
+            const T *C1 = C0 + Pc;
+            const T c10 = C1[t], c11 = C1[t + 1];
+            if (okx) v.x = v.x + T(0.25) * (c00 + c01 + c10 + c11);
+            if (oky) v.y = v.y + T(0.5) * (c01 + c11);
         }
-        if (act) st2(a.fine + j * Pf + c, v);
+        if (act) stv(a.fine + j * Pf + c, v);
     }
 }
 
-void launch_prolong(const ProlongArgs &a, hipStream_t s)
+template <class T>
+void launch_prolong(const ProlongArgsT<T> &a, hipStream_t s)
 {
     const int npairs = (a.Wf - 1) / 2;
     const int bx = (npairs + kBlock - 1) / kBlock;
     const int rows = a.row1 - a.row0;
     int rpb = (int)(((long long)rows * bx + 4095) / 4096);
     rpb = rpb < 2 ? 2 : (rpb > 32 ? 32 : rpb);
-    ProlongArgs b = a;
+    ProlongArgsT<T> b = a;
     b.rows_per_block = rpb;
     const int by = (rows + rpb - 1) / rpb;
-    k_prolong<<<dim3(bx, by), dim3(kBlock), 0, s>>>(b);
+    k_prolong<T><<<dim3(bx, by), dim3(kBlock), 0, s>>>(b);
 }
 
 // ---------------------------------------------------------------------------
@@ -345,7 +334,8 @@ void launch_prolong(const ProlongArgs &a, hipStream_t s)
 // ---------------------------------------------------------------------------
 constexpr int kFixBlocks = 256;
 
-__global__ __launch_bounds__(kBlock) void k_fixup(FixupArgs a)
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_fixup(FixupArgsT<T> a)
 {
     __shared__ double red[kBlock / 64];
     __shared__ int trig;
@@ -378,17 +368,19 @@ __global__ __launch_bounds__(kBlock) void k_fixup(FixupArgs a)
         const int r = a.row0 + (int)(k / npairs);
         const int t = (int)(k % npairs);
         const int c = 1 + 2 * t;
-        st2(a.dst + r * P + c, ld2(a.src + r * P + c));
+        stv(a.dst + r * P + c, ldv(a.src + r * P + c));
     }
 }
 
-void launch_fixup(const FixupArgs &a, hipStream_t s)
+template <class T>
+void launch_fixup(const FixupArgsT<T> &a, hipStream_t s)
 {
-    k_fixup<<<dim3(kFixBlocks), dim3(kBlock), 0, s>>>(a);
+    k_fixup<T><<<dim3(kFixBlocks), dim3(kBlock), 0, s>>>(a);
 }
 
-__global__ __launch_bounds__(kBlock) void k_copy_rows(const double *src, double *dst, int W,
-                                                      long long P, int row0, int row1)
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_copy_rows(const T *src, T *dst, int W, long long P,
+                                                      int row0, int row1)
 {
     const int npairs = (W - 1) >> 1;
     const long long total = (long long)(row1 - row0) * npairs;
@@ -396,84 +388,88 @@ __global__ __launch_bounds__(kBlock) void k_copy_rows(const double *src, double 
          k += (long long)gridDim.x * kBlock) {
         const int r = row0 + (int)(k / npairs);
         const int c = 1 + 2 * (int)(k % npairs);
-        st2(dst + r * P + c, ld2(src + r * P + c));
+        stv(dst + r * P + c, ldv(src + r * P + c));
     }
 }
 
-void launch_copy_rows(const double *src, double *dst, int W, int P, int row0, int row1,
-                      hipStream_t s)
+template <class T>
+void launch_copy_rows(const T *src, T *dst, int W, int P, int row0, int row1, hipStream_t s)
 {
     const long long total = (long long)(row1 - row0) * ((W - 1) / 2);
     long long nb = (total + kBlock - 1) / kBlock;
     if (nb > 4096) nb = 4096;
     if (nb < 1) nb = 1;
-    k_copy_rows<<<dim3((unsigned)nb), dim3(kBlock), 0, s>>>(src, dst, W, P, row0, row1);
+    k_copy_rows<T><<<dim3((unsigned)nb), dim3(kBlock), 0, s>>>(src, dst, W, P, row0, row1);
 }
 
 // ---------------------------------------------------------------------------
 // RHS from separable host sine tables: f = factor * sin(p*pi*x/a) * sin(q*pi*y/a)
 // (DynamicGridUtils.hpp:111-124) = (factor * sx[i]) * sy[j], same IEEE ops.
 // ---------------------------------------------------------------------------
-__global__ void k_rhs(double *f, const double *sx, const double *sy, double factor, int W,
+template <class T>
+__global__ void k_rhs(T *f, const double *sx, const double *sy, double factor, int W,
                       long long P, int row0, int row1)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int j = row0 + blockIdx.y;
     if (i >= W || j >= row1) return;
-    f[j * P + i] = factor * sx[i] * sy[j];
+    f[j * P + i] = (T)(factor * sx[i] * sy[j]);
 }
 
-void launch_rhs(double *f, const double *sx, const double *sy, double factor, int W, int P,
-                int row0, int row1, hipStream_t s)
+template <class T>
+void launch_rhs(T *f, const double *sx, const double *sy, double factor, int W, int P, int row0,
+                int row1, hipStream_t s)
 {
-    k_rhs<<<dim3((W + 255) / 256, row1 - row0), dim3(256), 0, s>>>(f, sx, sy, factor, W, P,
+    k_rhs<T><<<dim3((W + 255) / 256, row1 - row0), dim3(256), 0, s>>>(f, sx, sy, factor, W, P,
                                                                   row0, row1);
 }
 
 // MultiGrid.hpp:187-205 applied to values (compute_coarsest_grid, MultiGrid.hpp:28-55)
-__global__ void k_restrict_values(const double *Fn, int Nf, long long Pf, double *C, int Nc,
-                                  long long Pc)
+template <class T>
+__global__ void k_restrict_values(const T *Fn, int Nf, long long Pf, T *C, int Nc, long long Pc)
 {
     const long long n = (long long)(Nc - 2) * (Nc - 2);
     for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n;
          k += (long long)gridDim.x * blockDim.x) {
         const long long jc = 1 + k / (Nc - 2), ic = 1 + k % (Nc - 2);
         const long long q = (2 * jc) * Pf + 2 * ic;
-        C[jc * Pc + ic] = 0.25 * Fn[q] + 0.125 * (Fn[q + 1] + Fn[q - 1] + Fn[q + Pf] + Fn[q - Pf]) +
-                          0.0625 * (Fn[q - Pf - 1] + Fn[q - Pf + 1] + Fn[q + Pf - 1] + Fn[q + Pf + 1]);
+        C[jc * Pc + ic] = T(0.25) * Fn[q] + T(0.125) * (Fn[q + 1] + Fn[q - 1] + Fn[q + Pf] + Fn[q - Pf]) +
+                          T(0.0625) * (Fn[q - Pf - 1] + Fn[q - Pf + 1] + Fn[q + Pf - 1] + Fn[q + Pf + 1]);
     }
 }
 
-void launch_restrict_values(const double *fine, int Nf, int Pf, double *coarse, int Nc, int Pc,
-                            hipStream_t s)
+template <class T>
+void launch_restrict_values(const T *fine, int Nf, int Pf, T *coarse, int Nc, int Pc, hipStream_t s)
 {
     long long nb = ((long long)(Nc - 2) * (Nc - 2) + 255) / 256;
     if (nb > 4096) nb = 4096;
     if (nb < 1) nb = 1;
-    k_restrict_values<<<dim3((unsigned)nb), dim3(256), 0, s>>>(fine, Nf, Pf, coarse, Nc, Pc);
+    k_restrict_values<T><<<dim3((unsigned)nb), dim3(256), 0, s>>>(fine, Nf, Pf, coarse, Nc, Pc);
 }
 
-__global__ void k_fill_rows(double *o, long long P, int row0, int row1, double v)
+template <class T>
+__global__ void k_fill_rows(T *o, long long P, int row0, int row1)
 {
     const long long n = (long long)(row1 - row0) * P;
-    double *base = o + (long long)row0 * P;
+    T *base = o + (long long)row0 * P;
     for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n;
          k += (long long)gridDim.x * blockDim.x)
-        base[k] = v;
+        base[k] = T(0);
 }
 
-void launch_fill_rows(double *o, int P, int row0, int row1, double v, hipStream_t s)
+template <class T>
+void launch_fill_rows(T *o, int P, int row0, int row1, hipStream_t s)
 {
     long long nb = ((long long)(row1 - row0) * P + 255) / 256;
     if (nb > 8192) nb = 8192;
     if (nb < 1) nb = 1;
-    k_fill_rows<<<dim3((unsigned)nb), dim3(256), 0, s>>>(o, P, row0, row1, v);
+    k_fill_rows<T><<<dim3((unsigned)nb), dim3(256), 0, s>>>(o, P, row0, row1);
 }
 
 // sum r(x)^2 over rows [row0,row1), interior columns — reporting only
-__global__ __launch_bounds__(kBlock) void k_resnorm(const double *x, const double *f,
-                                                    double *partials, double ih, int W,
-                                                    long long P, int row0, int row1)
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_resnorm(const T *x, const T *f, double *partials,
+                                                    T ih, int W, long long P, int row0, int row1)
 {
     __shared__ double red[kBlock / 64];
     const long long n = (long long)(row1 - row0) * (W - 2);
@@ -483,17 +479,18 @@ __global__ __launch_bounds__(kBlock) void k_resnorm(const double *x, const doubl
         const int j = row0 + (int)(k / (W - 2));
         const int i = 1 + (int)(k % (W - 2));
         const long long q = j * P + i;
-        const double r = f[q] - ih * (4 * x[q] - x[q - 1] - x[q + 1] - x[q - P] - x[q + P]);
-        acc += r * r;
+        const T r = f[q] - ih * (T(4) * x[q] - x[q - 1] - x[q + 1] - x[q - P] - x[q + P]);
+        acc += sq(r);
     }
     const double s = block_sum<kBlock>(acc, red);
     if (threadIdx.x == 0) partials[blockIdx.x] = s;
 }
 
-void launch_resnorm_partials(const double *x, const double *f, double *partials, double inv_hh,
-                             int W, int P, int row0, int row1, int nblocks, hipStream_t s)
+template <class T>
+void launch_resnorm_partials(const T *x, const T *f, double *partials, T inv_hh, int W, int P,
+                             int row0, int row1, int nblocks, hipStream_t s)
 {
-    k_resnorm<<<dim3(nblocks), dim3(kBlock), 0, s>>>(x, f, partials, inv_hh, W, P, row0, row1);
+    k_resnorm<T><<<dim3(nblocks), dim3(kBlock), 0, s>>>(x, f, partials, inv_hh, W, P, row0, row1);
 }
 
 __global__ __launch_bounds__(kBlock) void k_sum_partials(const double *partials, int np,
@@ -510,5 +507,56 @@ void launch_sum_partials(const double *partials, int np, double *out, hipStream_
 {
     k_sum_partials<<<dim3(1), dim3(kBlock), 0, s>>>(partials, np, out);
 }
+
+// widen / narrow rows between T storage (pitch P) and a dense double array (pitch N)
+template <class T>
+__global__ void k_to_double(const T *src, long long P, double *dst, int N, int row0, int row1)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int j = row0 + blockIdx.y;
+    if (i >= N || j >= row1) return;
+    dst[(long long)j * N + i] = (double)src[j * P + i];
+}
+
+template <class T>
+__global__ void k_from_double(const double *src, int N, T *dst, long long P, int row0, int row1)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int j = row0 + blockIdx.y;
+    if (i >= N || j >= row1) return;
+    dst[j * P + i] = (T)src[(long long)j * N + i];
+}
+
+template <class T>
+void launch_to_double(const T *src, int P, double *dst, int N, int row0, int row1, hipStream_t s)
+{
+    if (row1 > row0)
+        k_to_double<T><<<dim3((N + 255) / 256, row1 - row0), dim3(256), 0, s>>>(src, P, dst, N, row0, row1);
+}
+
+template <class T>
+void launch_from_double(const double *src, int N, T *dst, int P, int row0, int row1, hipStream_t s)
+{
+    if (row1 > row0)
+        k_from_double<T><<<dim3((N + 255) / 256, row1 - row0), dim3(256), 0, s>>>(src, N, dst, P, row0, row1);
+}
+
+#define PGMG_INSTANTIATE(T)                                                                        \
+    template void launch_sweep<T>(const SweepArgsT<T> &, bool, bool, hipStream_t);                \
+    template void launch_res_restrict<T>(const ResRestrictArgsT<T> &, hipStream_t);                \
+    template void launch_prolong<T>(const ProlongArgsT<T> &, hipStream_t);                         \
+    template void launch_fixup<T>(const FixupArgsT<T> &, hipStream_t);                             \
+    template void launch_copy_rows<T>(const T *, T *, int, int, int, int, hipStream_t);            \
+    template void launch_rhs<T>(T *, const double *, const double *, double, int, int, int, int,   \
+                                hipStream_t);                                                      \
+    template void launch_restrict_values<T>(const T *, int, int, T *, int, int, hipStream_t);      \
+    template void launch_fill_rows<T>(T *, int, int, int, hipStream_t);                            \
+    template void launch_resnorm_partials<T>(const T *, const T *, double *, T, int, int, int, int, \
+                                             int, hipStream_t);                                    \
+    template void launch_to_double<T>(const T *, int, double *, int, int, int, hipStream_t);      \
+    template void launch_from_double<T>(const double *, int, T *, int, int, int, hipStream_t);
+PGMG_INSTANTIATE(double)
+PGMG_INSTANTIATE(float)
+#undef PGMG_INSTANTIATE
 
 }  // namespace pgmg

@@ -1,0 +1,70 @@
+// pgmg_real.h — element-type plumbing shared by the level kernels.
+//
+// Every level kernel is a template on the grid element type T: double (the
+// bit-exact default, PGMG_PRECISION_FP64) or float (PGMG_PRECISION_FP32, SURVEY §8 f3:
+// half the bytes, parity stated as a tolerance against the fp64 results).  A lane
+// always owns a column pair, so a lane moves V2<T> (16 B for double, 8 B for float) per
+// row and array.  Norm partial sums are accumulated in double for both types.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace pgmg {
+
+template <class T> struct Vec2;
+template <> struct Vec2<double> { using type = double2; };
+template <> struct Vec2<float> { using type = float2; };
+template <class T> using V2 = typename Vec2<T>::type;
+
+template <class T>
+__device__ __forceinline__ V2<T> ldv(const T *p) { return *reinterpret_cast<const V2<T> *>(p); }
+template <class T>
+__device__ __forceinline__ void stv(T *p, V2<T> v) { *reinterpret_cast<V2<T> *>(p) = v; }
+template <class T>
+__device__ __forceinline__ V2<T> mk2(T a, T b)
+{
+    V2<T> v;
+    v.x = a;
+    v.y = b;
+    return v;
+}
+template <class T> __device__ __forceinline__ V2<T> zero2() { return mk2<T>(T(0), T(0)); }
+
+// r*r accumulated in double (identical to r*r for T = double)
+template <class T> __device__ __forceinline__ double sq(T r) { return (double)r * (double)r; }
+
+// wave64 DPP lane moves: wave_shr:1 (lane i <- lane i-1), wave_shl:1 (lane i <- lane i+1);
+// the edge lane receives 0
+__device__ __forceinline__ double dpp_shr(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x138, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double dpp_shl(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x130, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x130, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ float dpp_shr(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float dpp_shl(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xF, 0xF, false));
+}
+
+// elements between an allocation's base and element (0,0): column 1 of every row on a
+// 128-byte boundary (15 doubles, 31 floats)
+template <class T> constexpr int off_elems() { return 128 / (int)sizeof(T) - 1; }
+// row pitch in elements: whole 128-byte lines
+template <class T> inline int pitch_elems(int N)
+{
+    const int q = 128 / (int)sizeof(T);
+    return (N + q - 1) / q * q;
+}
+
+}  // namespace pgmg

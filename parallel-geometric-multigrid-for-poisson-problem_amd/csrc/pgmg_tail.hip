@@ -15,18 +15,21 @@
 namespace pgmg {
 
 constexpr int kTailMaxLevels = 8;
+constexpr int kTailRed = kTailThreads / 64 + 2;  // doubles of reduction scratch at the LDS base
 
+template <class Real>
 struct TailLevel {
     int N;
-    int off;       // offset of this level's E and F grids (pitch N, no padding)
-    double hh, ih; // h*h and 1.0/(h*h) rounded on the host
+    int off;         // offset of this level's E and F grids (pitch N, no padding)
+    Real hh, ih;     // h*h and 1.0/(h*h) rounded on the host
 };
 
+template <class Real>
 struct TailArgsDev {
-    TailArgs a;
+    TailArgsT<Real> a;
     int nl;
-    int S;         // doubles per pyramid
-    TailLevel lv[kTailMaxLevels];
+    int S;           // elements per pyramid
+    TailLevel<Real> lv[kTailMaxLevels];
     int gamma;
 };
 
@@ -50,9 +53,9 @@ __device__ __forceinline__ double tail_sum(double v, double *red)
 }
 
 // out = J(cur) on all points (boundary copied); optionally sum r(cur)^2
-template <bool NORM>
-__device__ __forceinline__ double tail_jacobi(const double *cur, double *out, const double *f,
-                                              int N, double hh, double ih)
+template <class Real, bool NORM>
+__device__ __forceinline__ double tail_jacobi(const Real *cur, Real *out, const Real *f, int N,
+                                              Real hh, Real ih)
 {
     double acc = 0.0;
     const int n = N * N;
@@ -63,11 +66,11 @@ __device__ __forceinline__ double tail_jacobi(const double *cur, double *out, co
             out[k] = cur[k];
             continue;
         }
-        out[k] = 0.25 * ((hh * f[k]) + cur[k - 1] + cur[k + 1] + cur[k - N] + cur[k + N]);
+        out[k] = Real(0.25) * ((hh * f[k]) + cur[k - 1] + cur[k + 1] + cur[k - N] + cur[k + N]);
         if (NORM) {
-            const double r =
-                f[k] - ih * (4 * cur[k] - cur[k - 1] - cur[k + 1] - cur[k - N] - cur[k + N]);
-            acc += r * r;
+            const Real r =
+                f[k] - ih * (Real(4) * cur[k] - cur[k - 1] - cur[k + 1] - cur[k - N] - cur[k + N]);
+            acc += sq(r);
         }
     }
     return acc;
@@ -76,19 +79,20 @@ __device__ __forceinline__ double tail_jacobi(const double *cur, double *out, co
 // JacobiSmoother::smooth(x, f, N, N, h, num_iter): num_iter+1 sweeps, break as
 // soon as ||r(x_k)|| < eps.  The check of x_k is fused into sweep k+1 (which
 // reads the same neighbourhood); when it fires, sweep k+1's output is dropped.
-__device__ void tail_smooth(double *x, const double *f, const TailLevel &L, int num_iter,
-                            double eps, double *T, double *red, long long &sweeps,
+template <class Real>
+__device__ void tail_smooth(Real *x, const Real *f, const TailLevel<Real> &L, int num_iter,
+                            double eps, Real *T, double *red, long long &sweeps,
                             long long &exits)
 {
-    double *cur = x, *oth = T;
-    tail_jacobi<false>(cur, oth, f, L.N, L.hh, L.ih);
+    Real *cur = x, *oth = T;
+    tail_jacobi<Real, false>(cur, oth, f, L.N, L.hh, L.ih);
     __syncthreads();
-    double *tmp = cur;
+    Real *tmp = cur;
     cur = oth;
     oth = tmp;
     ++sweeps;
     for (int k = 2; k <= num_iter + 1; ++k) {
-        const double acc = tail_jacobi<true>(cur, oth, f, L.N, L.hh, L.ih);
+        const double acc = tail_jacobi<Real, true>(cur, oth, f, L.N, L.hh, L.ih);
         const double s = tail_sum(acc, red);   // also orders the writes of oth
         if (sqrt(s) < eps) {
             ++exits;
@@ -107,35 +111,38 @@ __device__ void tail_smooth(double *x, const double *f, const TailLevel &L, int 
 }
 
 // T = r(x) on the interior, 0 on the boundary; then fc = R T (MultiGrid.hpp:70-78)
-__device__ void tail_res_restrict(const double *x, const double *f, const TailLevel &Lf,
-                                  double *fc, double *ec, const TailLevel &Lc, double *T)
+template <class Real>
+__device__ void tail_res_restrict(const Real *x, const Real *f, const TailLevel<Real> &Lf, Real *fc,
+                                  Real *ec, const TailLevel<Real> &Lc, Real *T)
 {
     const int N = Lf.N, n = N * N;
     for (int k = threadIdx.x; k < n; k += kTailThreads) {
         const int j = k / N;
         const int i = k - j * N;
         if (i == 0 || j == 0 || i == N - 1 || j == N - 1) {
-            T[k] = 0.0;
+            T[k] = Real(0);
             continue;
         }
-        T[k] = f[k] - Lf.ih * (4 * x[k] - x[k - 1] - x[k + 1] - x[k - N] - x[k + N]);
+        T[k] = f[k] - Lf.ih * (Real(4) * x[k] - x[k - 1] - x[k + 1] - x[k - N] - x[k + N]);
     }
     __syncthreads();
     const int Nc = Lc.N, nc = Nc * Nc;
     for (int q = threadIdx.x; q < nc; q += kTailThreads) {
         const int jc = q / Nc;
         const int ic = q - jc * Nc;
-        ec[q] = 0.0;  // MultiGrid.hpp:81-82 e_coarse = 0
+        ec[q] = Real(0);  // MultiGrid.hpp:81-82 e_coarse = 0
         if (ic == 0 || jc == 0 || ic == Nc - 1 || jc == Nc - 1) continue;
         const int k = (2 * jc) * N + 2 * ic;
-        fc[q] = 0.25 * T[k] + 0.125 * (T[k + 1] + T[k - 1] + T[k + N] + T[k - N]) +
-                0.0625 * (T[k - N - 1] + T[k - N + 1] + T[k + N - 1] + T[k + N + 1]);
+        fc[q] = Real(0.25) * T[k] + Real(0.125) * (T[k + 1] + T[k - 1] + T[k + N] + T[k - N]) +
+                Real(0.0625) * (T[k - N - 1] + T[k - N + 1] + T[k + N - 1] + T[k + N + 1]);
     }
     __syncthreads();
 }
 
 // x += P e (MultiGrid.hpp:208-226): fine points in [2, Nf-2]^2 only
-__device__ void tail_prolong(double *x, const TailLevel &Lf, const double *e, const TailLevel &Lc)
+template <class Real>
+__device__ void tail_prolong(Real *x, const TailLevel<Real> &Lf, const Real *e,
+                             const TailLevel<Real> &Lc)
 {
     const int N = Lf.N, Nc = Lc.N, n = N * N;
     for (int k = threadIdx.x; k < n; k += kTailThreads) {
@@ -143,14 +150,14 @@ __device__ void tail_prolong(double *x, const TailLevel &Lf, const double *e, co
         const int i = k - j * N;
         if (i < 2 || j < 2 || i > N - 2 || j > N - 2) continue;
         const int jc = j >> 1, ic = i >> 1;
-        const double *C0 = e + jc * Nc;
-        double v;
+        const Real *C0 = e + jc * Nc;
+        Real v;
         if ((j & 1) == 0) {
-            v = ((i & 1) == 0) ? C0[ic] : 0.5 * (C0[ic] + C0[ic + 1]);
+            v = ((i & 1) == 0) ? C0[ic] : Real(0.5) * (C0[ic] + C0[ic + 1]);
         } else {
-            const double *C1 = C0 + Nc;
-            v = ((i & 1) == 0) ? 0.5 * (C0[ic] + C1[ic])
-                               : 0.25 * (C0[ic] + C0[ic + 1] + C1[ic] + C1[ic + 1]);
+            const Real *C1 = C0 + Nc;
+            v = ((i & 1) == 0) ? Real(0.5) * (C0[ic] + C1[ic])
+                               : Real(0.25) * (C0[ic] + C0[ic + 1] + C1[ic] + C1[ic + 1]);
         }
         x[k] = x[k] + v;
     }
@@ -158,10 +165,11 @@ __device__ void tail_prolong(double *x, const TailLevel &Lf, const double *e, co
 }
 
 // gamma-cycle (MultiGrid.hpp:57-136) whose top is tail level `top`; levels top.. last
-__device__ void tail_gcycle(const TailArgsDev &d, int top, double *E, double *F, double *T,
+template <class Real>
+__device__ void tail_gcycle(const TailArgsDev<Real> &d, int top, Real *E, Real *F, Real *T,
                             double *red, long long &sweeps, long long &exits)
 {
-    const TailArgs &a = d.a;
+    const TailArgsT<Real> &a = d.a;
     int visits[kTailMaxLevels];
     for (int i = 0; i < kTailMaxLevels; ++i) visits[i] = 0;
     int l = top;
@@ -197,7 +205,8 @@ __device__ void tail_gcycle(const TailArgsDev &d, int top, double *E, double *F,
 }
 
 // analytic right-hand side of tail level t from host sine tables (DynamicGridUtils.hpp:111-124)
-__device__ void tail_rhs(const TailArgsDev &d, int t, double *F)
+template <class Real>
+__device__ void tail_rhs(const TailArgsDev<Real> &d, int t, Real *F)
 {
     const int N = d.lv[t].N, n = N * N;
     const double *sx = d.a.fmg_tab + d.a.fmg_tab_off[t];
@@ -205,40 +214,42 @@ __device__ void tail_rhs(const TailArgsDev &d, int t, double *F)
     for (int k = threadIdx.x; k < n; k += kTailThreads) {
         const int j = k / N;
         const int i = k - j * N;
-        F[k] = d.a.fmg_factor * sx[i] * sy[j];
+        F[k] = (Real)(d.a.fmg_factor * sx[i] * sy[j]);
     }
 }
 
 // values restriction (compute_coarsest_grid) fine level t -> t+1, coarse boundary 0
-__device__ void tail_restrict_values(const double *x, const TailLevel &Lf, double *xc,
-                                     const TailLevel &Lc)
+template <class Real>
+__device__ void tail_restrict_values(const Real *x, const TailLevel<Real> &Lf, Real *xc,
+                                     const TailLevel<Real> &Lc)
 {
     const int N = Lf.N, Nc = Lc.N, nc = Nc * Nc;
     for (int q = threadIdx.x; q < nc; q += kTailThreads) {
         const int jc = q / Nc;
         const int ic = q - jc * Nc;
         if (ic == 0 || jc == 0 || ic == Nc - 1 || jc == Nc - 1) {
-            xc[q] = 0.0;
+            xc[q] = Real(0);
             continue;
         }
         const int k = (2 * jc) * N + 2 * ic;
-        xc[q] = 0.25 * x[k] + 0.125 * (x[k + 1] + x[k - 1] + x[k + N] + x[k - N]) +
-                0.0625 * (x[k - N - 1] + x[k - N + 1] + x[k + N - 1] + x[k + N + 1]);
+        xc[q] = Real(0.25) * x[k] + Real(0.125) * (x[k + 1] + x[k - 1] + x[k + N] + x[k - N]) +
+                Real(0.0625) * (x[k - N - 1] + x[k - N + 1] + x[k + N - 1] + x[k + N + 1]);
     }
     __syncthreads();
 }
 
-__global__ __launch_bounds__(kTailThreads) void k_tail(TailArgsDev d)
+template <class Real>
+__global__ __launch_bounds__(kTailThreads) void k_tail(TailArgsDev<Real> d)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    const TailArgs &a = d.a;
+    const TailArgsT<Real> &a = d.a;
     const int S = d.S;
-    double *E = lds;
-    double *F = lds + S;
-    double *T = lds + 2 * S;
-    double *red = T + d.lv[0].N * d.lv[0].N;
+    double *red = lds;                                   // kTailThreads / 64 + 1 partial sums
+    Real *E = reinterpret_cast<Real *>(lds + kTailRed);
+    Real *F = E + S;
+    Real *T = E + 2 * S;
 
-    for (int k = threadIdx.x; k < 2 * S; k += kTailThreads) lds[k] = 0.0;
+    for (int k = threadIdx.x; k < 2 * S; k += kTailThreads) E[k] = Real(0);
     __syncthreads();
     {
         const int N = d.lv[0].N, n = N * N;
@@ -261,12 +272,12 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(TailArgsDev d)
         for (int t = 0; t < last; ++t)
             tail_restrict_values(E + d.lv[t].off, d.lv[t], E + d.lv[t + 1].off, d.lv[t + 1]);
         for (int t = last; t >= 0; --t) {
-            double *Et = E + d.lv[t].off;
-            double *Ft = F + d.lv[t].off;
+            Real *Et = E + d.lv[t].off;
+            Real *Ft = F + d.lv[t].off;
             tail_rhs(d, t, Ft);                      // f_fine = compute_rhs (MultiGrid.hpp:162)
             if (t < last) {
                 const int n = d.lv[t].N * d.lv[t].N;
-                for (int k = threadIdx.x; k < n; k += kTailThreads) Et[k] = 0.0;
+                for (int k = threadIdx.x; k < n; k += kTailThreads) Et[k] = Real(0);
                 __syncthreads();
                 tail_prolong(Et, d.lv[t], E + d.lv[t + 1].off, d.lv[t + 1]);   // :164
                 tail_gcycle(d, t, E, F, T, red, sweeps, exits);              // :167 v_cycle
@@ -293,7 +304,8 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(TailArgsDev d)
     }
 }
 
-size_t tail_lds_doubles(int N_top, int n_coarse)
+template <class Real>
+size_t tail_lds_bytes(int N_top, int n_coarse)
 {
     size_t S = 0;
     int N = N_top;
@@ -302,14 +314,14 @@ size_t tail_lds_doubles(int N_top, int n_coarse)
         if (N <= n_coarse) break;
         N = (N - 1) / 2 + 1;
     }
-    return 2 * S + (size_t)N_top * N_top + kTailThreads / 64 + 8;
+    return kTailRed * sizeof(double) + (2 * S + (size_t)N_top * N_top) * sizeof(Real);
 }
 
-static bool g_tail_attr_set = false;
-
-hipError_t launch_tail_gamma(const TailArgs &a, int gamma, hipStream_t s)
+template <class Real>
+hipError_t launch_tail_gamma(const TailArgsT<Real> &a, int gamma, hipStream_t s)
 {
-    TailArgsDev d;
+    static bool attr_set = false;
+    TailArgsDev<Real> d;
     d.a = a;
     d.gamma = gamma;
     int N = a.N_top;
@@ -318,8 +330,8 @@ hipError_t launch_tail_gamma(const TailArgs &a, int gamma, hipStream_t s)
     for (; nl < kTailMaxLevels; ++nl) {
         d.lv[nl].N = N;
         d.lv[nl].off = off;
-        d.lv[nl].hh = h * h;
-        d.lv[nl].ih = 1.0 / (h * h);
+        d.lv[nl].hh = (Real)(h * h);
+        d.lv[nl].ih = (Real)(1.0 / (h * h));
         off += N * N;
         if (N <= a.n_coarse) {
             ++nl;
@@ -330,17 +342,20 @@ hipError_t launch_tail_gamma(const TailArgs &a, int gamma, hipStream_t s)
     }
     d.nl = nl;
     d.S = off;
-    const size_t bytes = tail_lds_doubles(a.N_top, a.n_coarse) * sizeof(double);
-    if (!g_tail_attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void *)k_tail,
+    const size_t bytes = tail_lds_bytes<Real>(a.N_top, a.n_coarse);
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void *)k_tail<Real>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
-        g_tail_attr_set = true;
+        attr_set = true;
     }
-    k_tail<<<dim3(1), dim3(kTailThreads), bytes, s>>>(d);
+    k_tail<Real><<<dim3(1), dim3(kTailThreads), bytes, s>>>(d);
     return hipGetLastError();
 }
 
-hipError_t launch_tail(const TailArgs &a, hipStream_t s) { return launch_tail_gamma(a, 1, s); }
+template hipError_t launch_tail_gamma<double>(const TailArgsT<double> &, int, hipStream_t);
+template hipError_t launch_tail_gamma<float>(const TailArgsT<float> &, int, hipStream_t);
+template size_t tail_lds_bytes<double>(int, int);
+template size_t tail_lds_bytes<float>(int, int);
 
 }  // namespace pgmg

@@ -2,7 +2,7 @@
 # One guarded GPU session on the MI355X box (run through gpurun from the repo root).
 # Every GPU step has its own time limit; the script stops at the first step that
 # faults, aborts, segfaults or times out (anything but exit 0 / pytest's 1).
-#   scripts/gpu_session.sh [steps...]   steps: smoke tests bench prof pmc
+#   scripts/gpu_session.sh [steps...]   steps: smoke tests bench prof pmc fp32 bench32 sweep ...
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -26,6 +26,9 @@ for s in $STEPS; do
     fcycle) run fcycle 600 python -m pytest tests/test_gpu_fcycle.py -m gpu -q -rf ;;
     tests-fast) run tests 600 python -m pytest tests -m "gpu and not slow" -q -rf ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
+    fp32) run fp32 600 python -m pytest tests/test_gpu_fp32.py -m gpu -q -rf ;;
+    bench32) run bench32 600 python bench.py --steps 20 --warmup 3 --dtype f32 --cpu-baseline off ;;
+    sweep) run sweep 900 python scripts/fp32_sweep.py --out gpurun_out/fp32_sweep.json ;;
     bench-graph) run bench_graph 600 python bench.py --steps 20 --warmup 3 --timing graph --cpu-baseline off ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 10 --warmup 2 --cpu-baseline off ;;
     pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline off
