@@ -296,23 +296,30 @@ class StripComm : public Comm {
 
     int setup(pgmg_ctx *) override { return PGMG_OK; }
 
-    int halo(const Grid &g, const Level &L, int depth, hipStream_t s) override
+    int halos(const HaloReq *reqs, int n, hipStream_t s) override
     {
-        const size_t row = (size_t)L.P * L.es;
         int e = t->group_start();
         if (e) return e;
-        if (me > 0) {
-            if ((e = t->send(row_ptr(g, L.lo, L.P, L.es), depth * row, me - 1, s))) return e;
-            if ((e = t->recv(row_ptr(g, L.lo - depth, L.P, L.es), depth * row, me - 1, s))) return e;
-        }
-        if (me < world - 1) {
-            if ((e = t->send(row_ptr(g, L.hi - depth, L.P, L.es), depth * row, me + 1, s))) return e;
-            if ((e = t->recv(row_ptr(g, L.hi, L.P, L.es), depth * row, me + 1, s))) return e;
+        for (int k = 0; k < n; ++k) {
+            const Grid &g = *reqs[k].g;
+            const Level &L = *reqs[k].L;
+            const int depth = reqs[k].depth;
+            const size_t row = (size_t)L.P * L.es;
+            if (me > 0) {
+                if ((e = t->send(row_ptr(g, L.lo, L.P, L.es), depth * row, me - 1, s))) return e;
+                if ((e = t->recv(row_ptr(g, L.lo - depth, L.P, L.es), depth * row, me - 1, s)))
+                    return e;
+            }
+            if (me < world - 1) {
+                if ((e = t->send(row_ptr(g, L.hi - depth, L.P, L.es), depth * row, me + 1, s)))
+                    return e;
+                if ((e = t->recv(row_ptr(g, L.hi, L.P, L.es), depth * row, me + 1, s))) return e;
+            }
         }
         return t->group_end(s);
     }
 
-    int allreduce_sum(double *d, hipStream_t s) override { return t->allreduce_sum(d, 1, s); }
+    int allreduce_sum(double *d, int n, hipStream_t s) override { return t->allreduce_sum(d, n, s); }
 
     int run_gathered(pgmg_ctx *c, int l, int gamma, int repeats) override
     {
@@ -333,11 +340,12 @@ class StripComm : public Comm {
             for (int i = 0; i < repeats; ++i)
                 if ((e = enqueue_cycle(c, l, gamma, i == 0))) return e;
         }
-        // 3. the correction rows each strip's prolongation reads -> every rank
+        // 3. the correction rows each strip's prolongation reads -> every rank (4 rows past
+        //    the strip: k_postpre reads 3 above and 4 below, its rare paths one more)
         if ((e = t->group_start())) return e;
         for (int r = 1; r < world; ++r) {
-            const int a = std::max(strip_lo(r, l) - 2, 0);
-            const int b = std::min(strip_hi(r, l, L.N) + 2, L.N);
+            const int a = std::max(strip_lo(r, l) - 4, 0);
+            const int b = std::min(strip_hi(r, l, L.N) + 4, L.N);
             if (me == 0 && (e = t->send(row_ptr(L.A, a, L.P, L.es), (b - a) * row, r, c->s))) return e;
             if (me == r && (e = t->recv(row_ptr(L.A, a, L.P, L.es), (b - a) * row, 0, c->s))) return e;
         }

@@ -48,6 +48,13 @@ struct Level {
 
 class Comm;
 
+// one array's halo exchange inside a grouped exchange (Comm::halos)
+struct HaloReq {
+    const Grid *g;
+    const Level *L;
+    int depth;
+};
+
 }  // namespace pgmg
 
 struct pgmg_ctx {
@@ -75,6 +82,7 @@ struct pgmg_ctx {
     bool recompute = true;        // levels entered with x0 = 0 recompute x2 in k_post
     pgmg::Grid S;                 // finest-level scratch for k_postpre's rare paths
     double *partials2 = nullptr;  // second partials buffer (k_postpre's pre check)
+    double *partials3 = nullptr;  // third (row strips: k_postpre's pre check from x1)
     unsigned *ppflags = nullptr;  // k_postpre_decide flags
     pgmg::Comm *comm = nullptr;   // non-null when world > 1
     // F-cycle (pgmg_fcycle): analytic level-0 RHS of the FMG h chain, and the sine
@@ -107,10 +115,15 @@ class Comm {
     virtual int setup(pgmg_ctx *c) = 0;
     virtual int gathered_level() const = 0;
     virtual int rank() const = 0;
-    // exchange `depth` halo rows of a strip-distributed level-l array (origin `o`)
-    virtual int halo(const Grid &g, const Level &L, int depth, hipStream_t s) = 0;
-    // in-place sum of one device double over all ranks
-    virtual int allreduce_sum(double *d_scalar, hipStream_t s) = 0;
+    // exchange `depth` halo rows of strip-distributed arrays, all in one group
+    virtual int halos(const HaloReq *reqs, int n, hipStream_t s) = 0;
+    int halo(const Grid &g, const Level &L, int depth, hipStream_t s)
+    {
+        const HaloReq r{&g, &L, depth};
+        return halos(&r, 1, s);
+    }
+    // in-place sum of n device doubles over all ranks
+    virtual int allreduce_sum(double *d, int n, hipStream_t s) = 0;
     // the parent produced rc of gathered level l: move it to rank 0, run `repeats`
     // cycles there, bring the correction back to every rank's strip
     virtual int run_gathered(pgmg_ctx *c, int l, int gamma, int repeats) = 0;

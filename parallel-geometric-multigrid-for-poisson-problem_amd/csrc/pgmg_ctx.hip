@@ -132,7 +132,7 @@ static int enqueue_smooth(pgmg_ctx *c, int l, int which, int v, bool x0_zero)
             f.global_sum = nullptr;
             if (is_dist(c, l)) {
                 launch_sum_partials(c->partials, np, c->scalar, c->s);
-                int e = c->comm->allreduce_sum(c->scalar, c->s);
+                int e = c->comm->allreduce_sum(c->scalar, 1, c->s);
                 if (e) return e;
                 f.global_sum = c->scalar;
             }
@@ -204,7 +204,7 @@ static int enqueue_children(pgmg_ctx *c, int l, int gamma)
 static int global_sum(pgmg_ctx *c, int np, const double **out)
 {
     launch_sum_partials(c->partials, np, c->scalar, c->s);
-    int e = c->comm->allreduce_sum(c->scalar, c->s);
+    int e = c->comm->allreduce_sum(c->scalar, 1, c->s);
     *out = c->scalar;
     return e;
 }
@@ -290,17 +290,47 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
 }
 
 // ---------------------------------------------------------------------------
-// Cross-cycle fusion of the finest level (single GPU, v1 = v2 = 1): for n
-// consecutive cycles the finest level runs k_pre, (children, k_postpre) x (n-1),
-// children, k_post.  k_postpre reads the pre-smoothed solution of cycle k from one
-// level-0 buffer and writes that of cycle k+1 into the other, so the buffers
-// alternate; at the end the solution is moved back under L.A by swapping the
-// host pointers (B always mirrors A's boundary, so either may play either role).
+// Cross-cycle fusion of the finest level (v1 = v2 = 1): for n consecutive cycles
+// the finest level runs k_pre, (children, k_postpre) x (n-1), children, k_post.
+// k_postpre reads the pre-smoothed solution of cycle k from one level-0 buffer and
+// writes that of cycle k+1 into the other, so the buffers alternate; at the end the
+// solution is moved back under L.A by swapping the host pointers (B always mirrors
+// A's boundary, so either may play either role).
+//
+// Row strips (level 0 distributed): every pass covers the rank's rows; before
+// k_postpre one grouped exchange brings 6 halo rows of phi and 4 of the coarse
+// correction; k_postpre also sums r(x2)^2 (the pre check of rare path 1, which
+// restarts the pre-smooth from x1: J(x1) = x2), so ONE allreduce of three sums
+// decides every rare path on every rank.  The rare paths rebuild their scratch
+// iterate S on the rows the following k_pre reads (4 past the strip) from the
+// exchanged halos instead of exchanging S.
 // ---------------------------------------------------------------------------
+struct StripRows {
+    int jc0, jc1;         // coarse-row segments [jc0, jc1)
+    int row_lo, row_hi;   // fine rows this rank writes
+    int rc_lo, rc_hi;     // coarse rows this rank restricts into
+    int x_lo, x_hi;       // rows of the rare-path scratch S (row_lo - 4 .. row_hi + 4)
+};
+
+static StripRows strip_rows(const Level &L, const Level &C)
+{
+    StripRows r;
+    r.jc0 = L.lo / 2;
+    r.jc1 = (L.hi < L.N ? L.hi : L.N - 1) / 2;
+    r.row_lo = L.u0;
+    r.row_hi = L.u1;
+    r.rc_lo = r.jc0 > 1 ? r.jc0 : 1;
+    r.rc_hi = r.jc1 < C.N - 1 ? r.jc1 : C.N - 1;
+    r.x_lo = L.u0 - 4 > 1 ? L.u0 - 4 : 1;
+    r.x_hi = L.u1 + 4 < L.N - 1 ? L.u1 + 4 : L.N - 1;
+    return r;
+}
+
 template <class T>
 static PreArgsT<T> make_pre(pgmg_ctx *c, const T *x0, T *x2)
 {
     Level &L = c->lv[0], &C = c->lv[1];
+    const StripRows sr = strip_rows(L, C);
     PreArgsT<T> pa{};
     pa.x0 = x0;
     pa.f = G<T>(L.F);
@@ -314,12 +344,12 @@ static PreArgsT<T> make_pre(pgmg_ctx *c, const T *x0, T *x2)
     pa.P = L.P;
     pa.Nc = C.N;
     pa.Pc = C.P;
-    pa.jc0 = 0;
-    pa.jc1 = (L.N - 1) / 2;
-    pa.row_lo = 1;
-    pa.row_hi = L.N - 1;
-    pa.rc_lo = 1;
-    pa.rc_hi = C.N - 1;
+    pa.jc0 = sr.jc0;
+    pa.jc1 = sr.jc1;
+    pa.row_lo = sr.row_lo;
+    pa.row_hi = sr.row_hi;
+    pa.rc_lo = sr.rc_lo;
+    pa.rc_hi = sr.rc_hi;
     return pa;
 }
 
@@ -327,6 +357,7 @@ template <class T>
 static PostArgsT<T> make_post(pgmg_ctx *c, const T *phi, T *x2)
 {
     Level &L = c->lv[0], &C = c->lv[1];
+    const StripRows sr = strip_rows(L, C);
     PostArgsT<T> po{};
     po.phi = phi;
     po.ec = G<T>(C.A);
@@ -340,10 +371,10 @@ static PostArgsT<T> make_post(pgmg_ctx *c, const T *phi, T *x2)
     po.P = L.P;
     po.Nc = C.N;
     po.Pc = C.P;
-    po.jc0 = 0;
-    po.jc1 = (L.N - 1) / 2;
-    po.row_lo = 1;
-    po.row_hi = L.N - 1;
+    po.jc0 = sr.jc0;
+    po.jc1 = sr.jc1;
+    po.row_lo = sr.row_lo;
+    po.row_hi = sr.row_hi;
     return po;
 }
 
@@ -351,9 +382,14 @@ template <class T>
 static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
 {
     Level &L = c->lv[0], &C = c->lv[1];
-    T *A = G<T>(L.A), *B = G<T>(L.B);
+    const bool dist = is_dist(c, 0);
+    const bool cdist = is_dist(c, 1);
+    const StripRows sr = strip_rows(L, C);
+    Grid gA = L.A, gB = L.B;
+    T *A = G<T>(gA), *B = G<T>(gB);
     T *S = G<T>(c->S);
-    const int np = fused_blocks(L.N, 0, (L.N - 1) / 2);
+    const int np = fused_blocks(L.N, sr.jc0, sr.jc1);
+    const int npp = postpre_blocks(L.N, sr.jc0, sr.jc1);
     FixArgsF fa{};
     fa.partials = c->partials;
     fa.np = np;
@@ -361,15 +397,22 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
     fa.stats = c->stats;
     int e;
     // cycle 1: pre-smooth (+ residual, restriction) A -> B
+    if (dist && (e = c->comm->halo(gA, L, 4, c->s))) return e;
     PreArgsT<T> pa = make_pre<T>(c, A, B);
     int ev = timed_begin(c, 1);
     launch_pre(pa, false, true, c->s);
     if ((e = timed_end(c, 1, ev))) return e;
+    if (dist && (e = global_sum(c, np, &fa.global_sum))) return e;
     launch_pre_fixup(fa, pa, false, c->s);
+    fa.global_sum = nullptr;
     T *pr = B;  // pre-smoothed solution of the current cycle
     if ((e = enqueue_children<T>(c, 0, gamma))) return e;
     for (int k = 1; k < n; ++k) {
         T *nx = (pr == A) ? B : A;
+        if (dist) {
+            const HaloReq h[2] = {{pr == A ? &gA : &gB, &L, 6}, {&C.A, &C, 4}};
+            if ((e = c->comm->halos(h, cdist ? 2 : 1, c->s))) return e;
+        }
         PostPreArgsT<T> q{};
         q.phi = pr;
         q.ec = G<T>(C.A);
@@ -378,6 +421,7 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         q.rc = G<T>(C.F);
         q.partials1 = c->partials;
         q.partials2 = c->partials2;
+        q.partials3 = dist ? c->partials3 : nullptr;
         q.stats = c->stats;
         q.hh = (T)L.hh;
         q.ih = (T)L.ih;
@@ -385,20 +429,30 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         q.P = L.P;
         q.Nc = C.N;
         q.Pc = C.P;
-        q.jc0 = 0;
-        q.jc1 = (L.N - 1) / 2;
-        q.row_lo = 1;
-        q.row_hi = L.N - 1;
-        q.rc_lo = 1;
-        q.rc_hi = C.N - 1;
+        q.jc0 = sr.jc0;
+        q.jc1 = sr.jc1;
+        q.row_lo = sr.row_lo;
+        q.row_hi = sr.row_hi;
+        q.rc_lo = sr.rc_lo;
+        q.rc_hi = sr.rc_hi;
         ev = timed_begin(c, 3);
         launch_postpre(q, c->s);
         if ((e = timed_end(c, 3, ev))) return e;
-        launch_postpre_decide(q.partials1, q.partials2, q.stats, postpre_blocks(L.N, 0, (L.N - 1) / 2),
-                              c->cfg.eps, c->ppflags, c->s);
+        const double *g3 = nullptr;   // all-rank {post, pre, pre-from-x1} sums
+        if (dist) {
+            launch_sum_partials(q.partials1, npp, c->scalar, c->s);
+            launch_sum_partials(q.partials2, npp, c->scalar + 1, c->s);
+            launch_sum_partials(q.partials3, npp, c->scalar + 2, c->s);
+            if ((e = c->comm->allreduce_sum(c->scalar, 3, c->s))) return e;
+            g3 = c->scalar;
+        }
+        launch_postpre_decide(q.partials1, q.partials2, q.stats, npp, g3, c->cfg.eps, c->ppflags,
+                              c->s);
         // rare path 1 (post check fired): S = x1 of the post-smooth, then a full
         // pre-smooth from S (conditional k_pre + its own fix-up)
         PostArgsT<T> po = make_post<T>(c, pr, S);
+        po.row_lo = sr.x_lo;
+        po.row_hi = sr.x_hi;
         FixArgsF f1 = fa;
         f1.cond = &c->ppflags[0];
         f1.force = 1;
@@ -409,13 +463,25 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         launch_pre(p1, false, false, c->s);
         FixArgsF f1b = fa;
         f1b.cond = &c->ppflags[0];
+        f1b.global_sum = dist ? c->scalar + 2 : nullptr;
         launch_pre_fixup(f1b, p1, false, c->s);
         // rare path 2 (only the pre check fired): S = x2 of the post-smooth, then the
         // pre-smooth result is J(S) and rc = R r(J(S))
         PostArgsT<T> p2 = make_post<T>(c, pr, S);
-        p2.cond = &c->ppflags[1];
-        p2.stats = nullptr;
-        launch_post(p2, false, c->s);
+        if (dist) {   // x2 on the strip and 4 rows past it, from the exchanged halos
+            p2.row_lo = sr.x_lo;
+            p2.row_hi = sr.x_hi;
+            p2.fix_sweeps = 2;
+            FixArgsF f2a = fa;
+            f2a.cond = &c->ppflags[1];
+            f2a.force = 1;
+            f2a.stats = nullptr;
+            launch_post_fixup(f2a, p2, c->s);
+        } else {
+            p2.cond = &c->ppflags[1];
+            p2.stats = nullptr;
+            launch_post(p2, false, c->s);
+        }
         PreArgsT<T> p3 = make_pre<T>(c, S, nx);
         FixArgsF f2 = fa;
         f2.cond = &c->ppflags[1];
@@ -427,10 +493,15 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
     }
     // last cycle: post-smooth
     T *out = (pr == A) ? B : A;
+    if (dist) {
+        const HaloReq h[2] = {{pr == A ? &gA : &gB, &L, 2}, {&C.A, &C, 2}};
+        if ((e = c->comm->halos(h, cdist ? 2 : 1, c->s))) return e;
+    }
     PostArgsT<T> po = make_post<T>(c, pr, out);
     ev = timed_begin(c, 2);
     launch_post(po, true, c->s);
     if ((e = timed_end(c, 2, ev))) return e;
+    if (dist && (e = global_sum(c, np, &fa.global_sum))) return e;
     launch_post_fixup(fa, po, c->s);
     if (out != A) std::swap(L.A, L.B);
     return PGMG_OK;
@@ -536,6 +607,7 @@ int pgmg_destroy(pgmg_ctx *c)
     }
     if (c->partials) (void)hipFree(c->partials);
     if (c->partials2) (void)hipFree(c->partials2);
+    if (c->partials3) (void)hipFree(c->partials3);
     if (c->ppflags) (void)hipFree(c->ppflags);
     free_grid(c->S);
     free_grid(c->Ffmg);
@@ -631,7 +703,7 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
     {
         const char *ev = getenv("PGMG_CROSS_MIN_N");
         const int cross_min = (ev && *ev) ? atoi(ev) : 2049;
-        c->cross = c->fused && c->comm == nullptr && c->nb >= 1 && c->lv[0].N >= cross_min &&
+        c->cross = c->fused && c->nb >= 1 && c->lv[0].N >= cross_min &&
                    !(cfg->flags & PGMG_FLAG_NO_CROSS);
     }
     int maxblocks = 256;
@@ -648,6 +720,7 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
     if (rc == PGMG_OK && c->cross) {
         rc = alloc_grid(c->S, c->lv[0]);
         if (rc == PGMG_OK && (hipMalloc((void **)&c->partials2, sizeof(double) * maxblocks) != hipSuccess ||
+                              hipMalloc((void **)&c->partials3, sizeof(double) * maxblocks) != hipSuccess ||
                               hipMalloc((void **)&c->ppflags, 4 * sizeof(unsigned)) != hipSuccess))
             rc = set_err(PGMG_ERR_NOMEM, "cross-cycle buffers");
     }
@@ -763,6 +836,11 @@ int pgmg_set_problem(pgmg_ctx *c, const double *phi0, const double *f)
     }
     if (c->nb > 0)
         HIPC(hipMemcpy2D(row_ptr(L.B, r0, L.P, L.es), pitch, row_ptr(L.A, r0, L.P, L.es), pitch,
+                         width, rows, hipMemcpyDeviceToDevice));
+    // the cross-cycle rare-path scratch S mirrors phi's boundary too (its passes never
+    // write boundary rows/columns, the k_pre that reads it passes them through)
+    if (c->S.base)
+        HIPC(hipMemcpy2D(row_ptr(c->S, r0, L.P, L.es), pitch, row_ptr(L.A, r0, L.P, L.es), pitch,
                          width, rows, hipMemcpyDeviceToDevice));
     if (f) {
         if ((e = upload_rows(c, L, L.F, f, r0, r1))) return e;
@@ -1017,7 +1095,7 @@ int pgmg_residual_norm(pgmg_ctx *c, double *out)
                                 L.u1, nbk, c->s);
     launch_sum_partials(c->partials, nbk, c->scalar, c->s);
     if (c->comm) {
-        int e = c->comm->allreduce_sum(c->scalar, c->s);
+        int e = c->comm->allreduce_sum(c->scalar, 1, c->s);
         if (e) return e;
     }
     double s = 0.0;

@@ -44,6 +44,7 @@ struct PostArgsT {
     // non-null: phi is not read but recomputed from f as the pre-smoothed iterate of
     // x0 = 0 (x1 = J(0), phi = *pre_fired ? x1 : J(x1)); PreArgs::fired of the same level
     const unsigned *pre_fired;
+    int fix_sweeps;             // k_post_fixup: 0/1 -> x1 (the check fired), 2 -> x2
 };
 
 // post-smooth of cycle k + pre-smooth/residual/restriction of cycle k+1 in one pass
@@ -57,6 +58,7 @@ struct PostPreArgsT {
     T *rc;                      // coarse right-hand side of cycle k+1
     double *partials1;          // sum r(x1)^2 (post-smooth check)
     double *partials2;          // sum r(x3)^2 (pre-smooth check)
+    double *partials3;          // non-null (row strips): sum r(x2)^2 (pre check from x1)
     unsigned long long *stats;
     T hh, ih;
     int N, P, Nc, Pc;
@@ -88,9 +90,10 @@ void launch_pre_fixup(const FixArgsF &a, const PreArgsT<T> &p, bool x0_zero, hip
 template <class T> void launch_post_fixup(const FixArgsF &a, const PostArgsT<T> &p, hipStream_t s);
 int postpre_blocks(int N, int jc0, int jc1);
 template <class T> void launch_postpre(const PostPreArgsT<T> &a, hipStream_t s);
-// flags[0] = post check fired; flags[1] = pre check fired (and post did not)
+// flags[0] = post check fired; flags[1] = pre check fired (and post did not).
+// global != nullptr: all-rank sums {post, pre} (row strips) instead of the partials.
 void launch_postpre_decide(const double *partials1, const double *partials2,
-                           unsigned long long *stats, int np, double eps, unsigned *flags,
-                           hipStream_t s);
+                           unsigned long long *stats, int np, const double *global, double eps,
+                           unsigned *flags, hipStream_t s);
 
 }  // namespace pgmg

@@ -533,7 +533,10 @@ __global__ __launch_bounds__(256, 4) void k_postpre_o4(PostPreArgsT<T> a)
 constexpr int kPPLdsRow = 4 * kPPStride + 2 * kPPMargin + 4;     // 472 doubles per row
 constexpr int kPPLdsCoarse = 2 * kPPStride + kPPMargin + 8;      // 242 doubles per coarse row
 
-template <class T>
+// R2 (row strips): also sum r(x2)^2 into partials3.  When the post check fires the
+// pre-smooth restarts from x1 and its first check is ||r(J(x1))|| = ||r(x2)||; having it
+// here lets one allreduce of three sums decide every rare path.
+template <class T, bool R2>
 __global__ __launch_bounds__(256) void k_postpre_lds(PostPreArgsT<T> a)
 {
     constexpr int R = 2;
@@ -578,7 +581,7 @@ __global__ __launch_bounds__(256) void k_postpre_lds(PostPreArgsT<T> a)
     V2<T> e0 = z, e1 = z, b0 = z, b1 = z, c0 = z, c1 = z, g0 = z, g1 = z, h0 = z, h1 = z,
             d0 = z, d1 = z;
     V2<T> f1 = z, f2 = z, f3 = z, f4 = z, f5 = z;  // f[i-1], f[i-2], ..., f[i-5]
-    double acc1 = 0.0, acc2 = 0.0;
+    double acc1 = 0.0, acc2 = 0.0, acc3 = 0.0;
     const int i_begin = 2 * jcb - 6;
     const int ng = (2 * (jce - jcb) + 11 + R - 1) / R;   // row pairs (uniform over the block)
     const int m0 = i_begin >> 1;                          // coarse row of the first pair
@@ -644,6 +647,14 @@ __global__ __launch_bounds__(256) void k_postpre_lds(PostPreArgsT<T> a)
             }
             // post-smooth sweep 2: x2 row ii-2 (= phi of cycle k+1)
             const V2<T> c2 = jstage(b0, b1, b2, f2, hh, k, boundary_row(ii - 2, N));
+            if (R2) {   // r(x2) on row ii-3
+                const V2<T> r2 = rstage(c0, c1, c2, f3, ih);
+                const int row = ii - 3;
+                if (row >= olo && row < ohi && k.own) {
+                    acc3 += sq(r2.x);
+                    if (!k.by) acc3 += sq(r2.y);
+                }
+            }
             // pre-smooth sweep 1: x3 row ii-3
             const V2<T> g2 = jstage(c0, c1, c2, f3, hh, k, boundary_row(ii - 3, N));
             {   // pre check: r(x3) on row ii-4
@@ -692,6 +703,11 @@ __global__ __launch_bounds__(256) void k_postpre_lds(PostPreArgsT<T> a)
     const double s1 = fused_block_sum(acc1, red);
     __syncthreads();
     const double s2 = fused_block_sum(acc2, red);
+    if (R2) {
+        __syncthreads();
+        const double s3 = fused_block_sum(acc3, red);
+        if (threadIdx.x == 0) a.partials3[slot] = s3;
+    }
     if (threadIdx.x == 0) {
         a.partials1[slot] = s1;
         a.partials2[slot] = s2;
@@ -699,8 +715,10 @@ __global__ __launch_bounds__(256) void k_postpre_lds(PostPreArgsT<T> a)
 }
 
 // one block: both decisions, stats, flags for the conditional rare-path kernels
+// global != nullptr (row strips): the all-rank sums {post, pre} instead of the partials
 __global__ __launch_bounds__(256) void k_postpre_decide(const double *p1, const double *p2, int np,
-                                                        double eps, unsigned *flags,
+                                                        const double *global, double eps,
+                                                        unsigned *flags,
                                                         unsigned long long *stats)
 {
     __shared__ double red[4];
@@ -712,6 +730,10 @@ __global__ __launch_bounds__(256) void k_postpre_decide(const double *p1, const 
     s1 = fused_block_sum(s1, red);
     __syncthreads();
     s2 = fused_block_sum(s2, red);
+    if (threadIdx.x == 0 && global != nullptr) {
+        s1 = global[0];
+        s2 = global[1];
+    }
     if (threadIdx.x == 0) {
         const unsigned t1 = sqrt(s1) < eps ? 1u : 0u;
         const unsigned t2 = (!t1 && sqrt(s2) < eps) ? 1u : 0u;
@@ -835,19 +857,22 @@ void launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
     a.rows_per_block = r;
     const dim3 g(gx, gy), b(t);
     if constexpr (std::is_same<T, double>::value) {
+        if (a.partials3 != nullptr && variant != 0) return;   // measurement variants: 1 GPU only
         if (variant == 4) k_postpre<T, 1, 0><<<g, b, 0, s>>>(a);    // per-wave loads (r01)
         else if (variant == 1) k_postpre<T, 1, 1><<<g, b, 0, s>>>(a);
         else if (variant == 3) k_postpre<T, 1, 1, 128, 0><<<g, b, 0, s>>>(a);  // no column overlap
         else if (variant == 2) k_postpre_o4<T, 1><<<g, b, 0, s>>>(a);
         if (variant != 0) return;
     }
-    k_postpre_lds<T><<<g, b, 0, s>>>(a);
+    if (a.partials3 != nullptr) k_postpre_lds<T, true><<<g, b, 0, s>>>(a);
+    else k_postpre_lds<T, false><<<g, b, 0, s>>>(a);
 }
 
 void launch_postpre_decide(const double *partials1, const double *partials2, unsigned long long *stats,
-                           int np, double eps, unsigned *flags, hipStream_t s)
+                           int np, const double *global, double eps, unsigned *flags, hipStream_t s)
 {
-    k_postpre_decide<<<dim3(1), dim3(256), 0, s>>>(partials1, partials2, np, eps, flags, stats);
+    k_postpre_decide<<<dim3(1), dim3(256), 0, s>>>(partials1, partials2, np, global, eps, flags,
+                                                  stats);
 }
 
 // ---------------------------------------------------------------------------
@@ -940,6 +965,15 @@ __device__ T fx1(const FixCtx<T> &c, int j, int i)
                    fin<POST>(c, j, i + 1) + fin<POST>(c, j - 1, i) + fin<POST>(c, j + 1, i));
 }
 
+// two post-smooth sweeps from x_eff (row-strip rare path: x2 on rows past the strip)
+template <class T>
+__device__ T fx2post(const FixCtx<T> &c, int j, int i)
+{
+    if (j <= 0 || i <= 0 || j >= c.N - 1 || i >= c.N - 1) return fxeff(c, j, i);
+    return T(0.25) * ((c.hh * c.f[(long long)j * c.P + i]) + fx1<true>(c, j, i - 1) +
+                      fx1<true>(c, j, i + 1) + fx1<true>(c, j - 1, i) + fx1<true>(c, j + 1, i));
+}
+
 template <class T>
 __device__ T fr1(const FixCtx<T> &c, int j, int i)
 {
@@ -988,7 +1022,7 @@ __global__ __launch_bounds__(256) void k_post_fixup(FixArgsF a, PostArgsT<T> p)
     const long long stride = (long long)gridDim.x * blockDim.x;
     for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < nrows * W; k += stride) {
         const int j = p.row_lo + (int)(k / W), i = 1 + (int)(k % W);
-        p.x2[(long long)j * p.P + i] = fx1<true>(c, j, i);
+        p.x2[(long long)j * p.P + i] = p.fix_sweeps == 2 ? fx2post(c, j, i) : fx1<true>(c, j, i);
     }
 }
 

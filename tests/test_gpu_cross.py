@@ -94,3 +94,28 @@ def test_cross_default_threshold_large_grid(pgmg, oracle_mod, golden_cycles):
         s.vcycle(3)
         assert oracle_mod.fnv_hash(s.solution()) == case["cycles"][-1]["hash"]
         assert s.stats()[0] == case["cycles"][-1]["sweeps"]
+
+
+def test_cross_rare_paths_nonzero_boundary(pgmg, oracle_mod, cross_everywhere):
+    """The rare paths rebuild the iterate in the scratch grid S; S must carry phi's
+    Dirichlet boundary (set_problem mirrors it), or a non-zero boundary goes wrong."""
+    rng = np.random.default_rng(5)
+    N = 129
+    phi0 = rng.uniform(-1, 1, (N, N))          # boundary included
+    f = rng.uniform(-1, 1, (N, N)) * 1e-3
+    seen = [0, 0]
+    for eps in [10 ** (k / 12.0) for k in range(96, -24, -1)]:
+        if seen[0] > 0 and seen[1] > 0:
+            break
+        o = oracle_mod.Oracle(eps=eps)
+        ref = phi0.copy()
+        for _ in range(6):
+            o.v_cycle(ref, f)
+        with pgmg.Solver(N, eps=eps, tail_n=17) as s:
+            s.set_problem(phi0, f)
+            s.vcycle(6)
+            assert_bitwise(s.solution(), ref, f"eps={eps}")
+            d = s.stats_detail()
+            seen[0] += d[2]
+            seen[1] += d[3]
+    assert seen[0] > 0 and seen[1] > 0, seen
