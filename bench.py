@@ -72,17 +72,18 @@ def cpu_baseline(n, cycles=1):
                       f"-O2 single thread (taskset -c 0); {t:.2f} s per V-cycle; host {model}"}
 
 
-def pmc_traffic(n, kernel):
-    """HBM bytes per launch of `kernel` at grid n, from the committed rocprofv3 PMC summary
-    (profiles/pmc_fine.json, written by scripts/pmc_summary.py from FETCH_SIZE/WRITE_SIZE
-    passes with the gfx950 corrections of MI355X_MICROARCH.md)."""
+def pmc_traffic(n, key):
+    """HBM bytes per launch of the kernel symbol `key` (normalised as scripts/pmc_summary.py
+    does, e.g. k_postpre_lds<double,false,true>) at grid n, from the committed rocprofv3 PMC
+    summary (profiles/pmc_fine.json: FETCH_SIZE/WRITE_SIZE passes with the gfx950
+    corrections of MI355X_MICROARCH.md)."""
     p = ROOT / "profiles" / "pmc_fine.json"
     if not p.exists():
         return None
     try:
         d = json.loads(p.read_text())
         for k in d.get("kernels", []):
-            if int(k.get("N", 0)) == n and k.get("kernel", "").startswith(kernel):
+            if int(k.get("N", 0)) == n and k.get("kernel", "") == key:
                 return k.get("hbm_bytes_per_launch")
     except (ValueError, OSError):
         pass
@@ -148,43 +149,38 @@ def main():
     dev_ms = s.last_elapsed_ms()
     vbytes = s.vcycle_bytes()
     n = N = args.n
-    # rows of the finest level this rank updates
-    import ctypes
-    p, pitch, r0, nr = (ctypes.c_void_p(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int())
-    pg._capi.check(pg.load().pgmg_phi_device(s.h, ctypes.byref(p), ctypes.byref(pitch),
-                                             ctypes.byref(r0), ctypes.byref(nr)), "phi_device")
-    rows = min(r0.value + nr.value, N - 1) - max(r0.value, 1)
-    nf = float(rows) * (N - 2)              # fine interior points on this rank
-    nc = nf / 4.0                           # coarse interior points it restricts / prolongs
-    es = s.elem_bytes / 8.0                 # the per-point byte figures below are fp64
+    gen = s.fused and s.fine_pass_bytes(3) < s.fine_pass_bytes(2)   # f regenerated in-kernel
+    T = "double" if args.dtype == "f64" else "float"
     passes = []
     if s.fused:
-        # k_pre: read x0, f; write x2 (24 B/pt) + write rc; k_post: read phi, f, ec; write x2
-        for which, name, nbytes in ((3, "k_postpre (finest level, between cycles: prolongation "
-                                        "+ 2+2 Jacobi sweeps + residual + restriction, fused)",
-                                     (24.0 * nf + 16.0 * nc) * es),
-                                    (1, "k_pre<false,true> (finest level: 2 Jacobi sweeps + "
-                                        "residual + restriction, fused)", (24.0 * nf + 8.0 * nc) * es),
-                                    (2, "k_post<true> (finest level: prolongation + 2 Jacobi "
-                                        "sweeps, fused)", (24.0 * nf + 8.0 * nc) * es)):
+        # algorithmic bytes per launch from the library (pgmg_fine_pass_bytes): each input
+        # read once, each output written once
+        for which, name, key in (
+                (3, "k_postpre (finest level, between cycles: prolongation + 2+2 Jacobi sweeps "
+                    "+ residual + restriction, fused" + ("; f regenerated in-kernel" if gen else "")
+                    + ")", f"k_postpre_lds<{T},{'true' if world > 1 else 'false'},"
+                           f"{'true' if gen else 'false'}>"),
+                (1, "k_pre<false,true> (finest level: 2 Jacobi sweeps + residual + restriction, "
+                    "fused)", f"k_pre<{T},false,true>"),
+                (2, "k_post<true> (finest level: prolongation + 2 Jacobi sweeps, fused)",
+                 f"k_post<{T},true,2,false>")):
             cnt, ms = s.fine_pass_time(which)
-            passes.append((name, nbytes, cnt, ms))
+            passes.append((name, s.fine_pass_bytes(which), cnt, ms, key))
     else:
         cnt, ms = s.fine_pass_time(0)
-        passes.append(("k_sweep<false,false,true> (finest-level Jacobi sweep)", 24.0 * nf * es,
-                       cnt, ms))
+        passes.append(("k_sweep<false,false,true> (finest-level Jacobi sweep)",
+                       s.fine_pass_bytes(0), cnt, ms, f"k_sweep<{T},false,false,true>"))
     if not passes or passes[0][2] == 0:   # graph mode: time the kernel separately
         ms = s.bench_sweep(20)
         passes = [("k_sweep<false,false,true> (finest-level Jacobi sweep, timed apart)",
-                   24.0 * nf * es, 20, ms)]
+                   s.fine_pass_bytes(0), 20, ms, f"k_sweep<{T},false,false,true>")]
     roof = []
-    for name, nbytes, cnt, ms in passes:
+    for name, nbytes, cnt, ms, key in passes:
         ach = nbytes / (ms * 1e-3) / 1e9 if ms > 0 else None
-        roof.append({"bound": "hbm", "kernel": name,
+        roof.append({"bound": "hbm", "kernel": name, "symbol": key,
                      "achieved": round(ach, 2) if ach else None, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4) if ach else None,
-                     "traffic": (pmc_traffic(N, name.split(" ")[0])
-                                 if world == 1 and args.dtype == "f64" else None),
+                     "traffic": (pmc_traffic(N, key) if world == 1 else None),
                      "bytes_per_launch": nbytes, "launches_timed": cnt,
                      "ms_per_launch": round(ms, 5)})
     # the dominant kernel: largest total time over the timed region
@@ -194,7 +190,7 @@ def main():
     if s.fused and roof and roof[0]["achieved"]:
         # the same pass counted as the separate 24 B/pt sweeps it replaces
         nsw = 4 if roof[0]["kernel"].startswith("k_postpre") else 2
-        sweep_eq = round(nsw * 24.0 * nf * es / (roof[0]["ms_per_launch"] * 1e-3) / 1e9, 2)
+        sweep_eq = round(nsw * s.fine_pass_bytes(0) / (roof[0]["ms_per_launch"] * 1e-3) / 1e9, 2)
 
     if rank == 0:
         value = args.steps / dt

@@ -76,6 +76,10 @@ extern "C" {
                                     (the general path; same results)                */
 #define PGMG_FLAG_NO_CROSS 16u   /* do not fuse the finest level's post-smooth with the
                                     next cycle's pre-smooth (same results)           */
+#define PGMG_FLAG_STORED_RHS 32u /* always stream f from HBM; by default, when f is the
+                                    analytic RHS (set_problem f = NULL), the finest-level
+                                    cross-cycle pass regenerates it in-kernel from two
+                                    sine tables (bitwise the same values, 8 B/pt less) */
 #define PGMG_FLAG_LOOPBACK 8u    /* world > 1 with ranks as threads of one process on
                                     one GPU: nccl_unique_id is a pgmg_loopback hub
                                     (test transport for the strip decomposition)    */
@@ -151,6 +155,12 @@ int pgmg_vcycle_bytes(pgmg_ctx *ctx, double *bytes);
  * rank, for callers that want to read it in place.  The elements are double, or
  * float when the context was created with PGMG_PRECISION_FP32 (pgmg_precision). */
 int pgmg_phi_device(pgmg_ctx *ctx, double **ptr, int *pitch, int *row0, int *rows);
+
+/* Algorithmic HBM bytes of one launch of finest-level pass `pass` (numbering of
+ * pgmg_fine_pass_time) on this rank: every input read once, every output written once
+ * (24 B per fine point for x, f -> x; +8 B per coarse point per coarse array; 16 B when
+ * k_postpre regenerates the analytic f in-kernel), times elem_bytes / 8. */
+int pgmg_fine_pass_bytes(pgmg_ctx *ctx, int pass, double *bytes);
 
 /* The context's PGMG_PRECISION_* and its grid element size in bytes (8 or 4). */
 int pgmg_precision(pgmg_ctx *ctx, int *precision, int *elem_bytes);

@@ -17,6 +17,7 @@ import subprocess
 import numpy as np
 
 from ._capi import (PGMG_FLAG_LOOPBACK, PGMG_FLAG_NO_CROSS, PGMG_FLAG_NO_GRAPH,
+                    PGMG_FLAG_STORED_RHS,
                     PGMG_FLAG_TIME_FINE, PGMG_PRECISION_FP32, PGMG_PRECISION_FP64,
                     PGMG_FLAG_UNFUSED, PGMG_PROLONG_REFERENCE,
                     PGMG_PROLONG_SYMMETRIC, PgmgConfig, PgmgError, check, load)
@@ -28,6 +29,7 @@ __all__ = [
     "PGMG_FLAG_NO_GRAPH", "PGMG_FLAG_TIME_FINE", "PGMG_FLAG_UNFUSED", "PGMG_FLAG_LOOPBACK", "PGMG_FLAG_NO_CROSS",
     "PGMG_PROLONG_REFERENCE", "plan_strips", "LoopbackHub", "unique_id",
     "PGMG_PROLONG_SYMMETRIC", "PGMG_PRECISION_FP64", "PGMG_PRECISION_FP32",
+    "PGMG_FLAG_STORED_RHS",
 ]
 
 
@@ -208,6 +210,12 @@ class Solver:
         v = C.c_int()
         check(self.lib.pgmg_fused(self.h, C.byref(v)), "pgmg_fused")
         return bool(v.value)
+
+    def fine_pass_bytes(self, which):
+        """Algorithmic HBM bytes of one launch of finest-level pass `which` on this rank."""
+        v = C.c_double()
+        check(self.lib.pgmg_fine_pass_bytes(self.h, int(which), C.byref(v)), "pgmg_fine_pass_bytes")
+        return v.value
 
     @property
     def elem_bytes(self):

@@ -83,6 +83,11 @@ struct pgmg_ctx {
     pgmg::Grid S;                 // finest-level scratch for k_postpre's rare paths
     double *partials2 = nullptr;  // second partials buffer (k_postpre's pre check)
     double *partials3 = nullptr;  // third (row strips: k_postpre's pre check from x1)
+    // analytic RHS (set_problem with f = NULL): level-0 passes may regenerate f in-kernel
+    // as gfx[i] * gsy[j] instead of streaming it (bitwise the stored values)
+    double *rhs_tab = nullptr;
+    const double *gfx = nullptr, *gsy = nullptr;   // valid for indices -8 ..
+    bool gen_rhs = false;
     unsigned *ppflags = nullptr;  // k_postpre_decide flags
     pgmg::Comm *comm = nullptr;   // non-null when world > 1
     // F-cycle (pgmg_fcycle): analytic level-0 RHS of the FMG h chain, and the sine

@@ -422,6 +422,8 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         q.partials1 = c->partials;
         q.partials2 = c->partials2;
         q.partials3 = dist ? c->partials3 : nullptr;
+        q.gfx = c->gen_rhs ? c->gfx : nullptr;
+        q.gsy = c->gen_rhs ? c->gsy : nullptr;
         q.stats = c->stats;
         q.hh = (T)L.hh;
         q.ih = (T)L.ih;
@@ -608,6 +610,7 @@ int pgmg_destroy(pgmg_ctx *c)
     if (c->partials) (void)hipFree(c->partials);
     if (c->partials2) (void)hipFree(c->partials2);
     if (c->partials3) (void)hipFree(c->partials3);
+    if (c->rhs_tab) (void)hipFree(c->rhs_tab);
     if (c->ppflags) (void)hipFree(c->ppflags);
     free_grid(c->S);
     free_grid(c->Ffmg);
@@ -842,6 +845,7 @@ int pgmg_set_problem(pgmg_ctx *c, const double *phi0, const double *f)
     if (c->S.base)
         HIPC(hipMemcpy2D(row_ptr(c->S, r0, L.P, L.es), pitch, row_ptr(L.A, r0, L.P, L.es), pitch,
                          width, rows, hipMemcpyDeviceToDevice));
+    c->gen_rhs = false;
     if (f) {
         if ((e = upload_rows(c, L, L.F, f, r0, r1))) return e;
     } else {
@@ -857,6 +861,22 @@ int pgmg_set_problem(pgmg_ctx *c, const double *phi0, const double *f)
         HIPC(hipGetLastError());
         HIPC(hipStreamSynchronize(c->s));
         HIPC(hipFree(d));
+        // tables for regenerating f inside the level-0 passes: fx[i] = factor * sx[i]
+        // (the first product of k_rhs's factor * sx[i] * sy[j]) and sy[j], zero-padded
+        // past the grid (columns / rows -8 .. N + 1024 / N + 16, like the stored f's
+        // zero padding)
+        if (!(c->cfg.flags & PGMG_FLAG_STORED_RHS)) {
+            const int nx = 8 + N + 1024, ny = 8 + N + 16;
+            std::vector<double> tab((size_t)nx + ny, 0.0);
+            for (int i = 0; i < N; ++i) tab[8 + i] = factor * sx[i];
+            for (int j = 0; j < N; ++j) tab[(size_t)nx + 8 + j] = sy[j];
+            if (!c->rhs_tab) HIPC(hipMalloc((void **)&c->rhs_tab, tab.size() * sizeof(double)));
+            HIPC(hipMemcpy(c->rhs_tab, tab.data(), tab.size() * sizeof(double),
+                           hipMemcpyHostToDevice));
+            c->gfx = c->rhs_tab + 8;
+            c->gsy = c->rhs_tab + nx + 8;
+            c->gen_rhs = true;
+        }
     }
     HIPC(hipMemset(c->stats, 0, 4 * sizeof(unsigned long long)));
     HIPC(hipDeviceSynchronize());
@@ -1147,7 +1167,7 @@ int pgmg_vcycle_bytes(pgmg_ctx *c, double *bytes)
         const double nc = (double)(C.u1 - C.u0) * (C.N - 2);
         if (c->fused) {
             if (l == 0 && c->cross) {                     // steady state: one k_postpre
-                b += 24.0 * n + 16.0 * nc;                // phi, f, ec in; x4, rc out
+                b += (c->gen_rhs ? 16.0 : 24.0) * n + 16.0 * nc;  // phi, (f,) ec in; x4, rc out
                 continue;
             }
             if (l > 0 && c->recompute) {                  // x0 = 0, x2 recomputed
@@ -1170,6 +1190,25 @@ int pgmg_vcycle_bytes(pgmg_ctx *c, double *bytes)
     const Level &Lt = c->lv[c->nb];
     b += 16.0 * (double)Lt.N * Lt.N;                             // tail: f in, e out
     *bytes = b * (c->lv[0].es / 8.0);                            // per-point figures are fp64
+    return PGMG_OK;
+}
+
+int pgmg_fine_pass_bytes(pgmg_ctx *c, int pass, double *bytes)
+{
+    if (!c || !bytes || pass < 0 || pass > 3) return set_err(PGMG_ERR_ARG, "bad argument");
+    if (c->nb == 0) return set_err(PGMG_ERR_STATE, "no bulk level");
+    const Level &L = c->lv[0], &C = c->lv[1];
+    const double n = (double)(L.u1 - L.u0) * (L.N - 2);
+    const StripRows sr = strip_rows(L, C);
+    const double nc = (double)(sr.rc_hi > sr.rc_lo ? sr.rc_hi - sr.rc_lo : 0) * (C.N - 2);
+    double b = 0.0;
+    switch (pass) {
+    case 0: b = 24.0 * n; break;                               // x, f in; x out
+    case 1: b = 24.0 * n + 8.0 * nc; break;                    // x0, f in; x2, rc out
+    case 2: b = 24.0 * n + 8.0 * nc; break;                    // phi, f, ec in; x2 out
+    case 3: b = (c->gen_rhs ? 16.0 : 24.0) * n + 16.0 * nc; break;  // phi, (f,) ec; x4, rc
+    }
+    *bytes = b * (L.es / 8.0);
     return PGMG_OK;
 }
 

@@ -59,6 +59,9 @@ struct PostPreArgsT {
     double *partials1;          // sum r(x1)^2 (post-smooth check)
     double *partials2;          // sum r(x3)^2 (pre-smooth check)
     double *partials3;          // non-null (row strips): sum r(x2)^2 (pre check from x1)
+    // non-null: f is the analytic RHS, regenerated as (T)(gfx[i] * gsy[j]) (gfx[i] =
+    // factor*sx[i]); both tables valid for indices -8 .. (gfx: P + 248, gsy: N + 8)
+    const double *gfx, *gsy;
     unsigned long long *stats;
     T hh, ih;
     int N, P, Nc, Pc;

@@ -38,10 +38,12 @@ struct Cols {
     int c;          // odd column of this lane's pair (c, c+1)
     bool bx, by;    // column c / c+1 is a boundary (or outside) column: passthrough
     bool own;       // lane owns its pair (lanes 2..61 of the wave tile)
+    bool edge;      // wave-uniform: some lane of this wave has a boundary/outside column
 };
 
-// One Jacobi stage on a row: J(ce) with boundary passthrough.
-template <class T>
+// One Jacobi stage on a row: J(ce) with boundary passthrough.  EDGE = false: the caller
+// guarantees that neither the row nor any column of the wave is a boundary (no selects).
+template <class T, bool EDGE = true>
 __device__ __forceinline__ V2<T> jstage(V2<T> up, V2<T> ce, V2<T> dn, V2<T> f, T hh,
                                           const Cols &k, bool brow)
 {
@@ -50,8 +52,10 @@ __device__ __forceinline__ V2<T> jstage(V2<T> up, V2<T> ce, V2<T> dn, V2<T> f, T
     V2<T> o;
     o.x = T(0.25) * ((hh * f.x) + l + ce.y + up.x + dn.x);
     o.y = T(0.25) * ((hh * f.y) + ce.x + r + up.y + dn.y);
-    if (brow || k.bx) o.x = ce.x;
-    if (brow || k.by) o.y = ce.y;
+    if constexpr (EDGE) {
+        if (brow || k.bx) o.x = ce.x;
+        if (brow || k.by) o.y = ce.y;
+    }
     return o;
 }
 
@@ -81,6 +85,9 @@ __device__ __forceinline__ Cols lane_cols_t(int N)
     k.bx = k.c <= 0 || k.c >= N - 1;
     k.by = k.c + 1 <= 0 || k.c + 1 >= N - 1;
     k.own = lane >= MARGIN / 2 && lane < MARGIN / 2 + STRIDE / 2 && k.c <= N - 2;
+    // the wave's columns are [c0, c0 + 127]: uniform, kept in a scalar register
+    const int c0 = __builtin_amdgcn_readfirstlane(STRIDE * wave + 1 - MARGIN);
+    k.edge = c0 <= 0 || c0 + 127 >= N - 1;
     return k;
 }
 
@@ -167,8 +174,8 @@ __global__ __launch_bounds__(256) void k_pre(PreArgsT<T> a)
                 const int row = ii - 2;
                 const V2<T> r1 = rstage(b0, b1, b2, f1, ih);
                 if (row >= olo && row < ohi && k.own) {
-                    acc += sq(r1.x);
-                    if (!k.by) acc += sq(r1.y);
+                    acc = sqacc(acc, r1.x);
+                    if (!k.by) acc = sqacc(acc, r1.y);
                 }
             }
             const V2<T> c2 = jstage(b0, b1, b2, f1, hh, k, boundary_row(ii - 2, N));
@@ -329,8 +336,8 @@ __global__ __launch_bounds__(256) void k_post(PostArgsT<T> a)
                 const int row = ii - 2;
                 const V2<T> r1 = rstage(b0, b1, b2, f1, ih);
                 if (row >= olo && row < ohi && k.own) {
-                    acc += sq(r1.x);
-                    if (!k.by) acc += sq(r1.y);
+                    acc = sqacc(acc, r1.x);
+                    if (!k.by) acc = sqacc(acc, r1.y);
                 }
             }
             const V2<T> c2 = jstage(b0, b1, b2, f1, hh, k, boundary_row(ii - 2, N));
@@ -363,12 +370,12 @@ constexpr int kPPStride = 114, kPPMargin = 6;
 // MODE 0: the real pass.  MODE 1 (PGMG_PP_VARIANT=1, measurement only): the same loads
 // and stores with the stencil arithmetic replaced by one add, to separate the memory
 // ceiling of this access pattern from the instruction cost.
-template <int MODE, class T>
+template <int MODE, class T, bool EDGE = true>
 __device__ __forceinline__ V2<T> js(V2<T> up, V2<T> ce, V2<T> dn, V2<T> f, T hh,
                                       const Cols &k, bool brow)
 {
     if (MODE == 1) return mk2<T>(ce.x + f.x, ce.y + up.y + dn.y);
-    return jstage(up, ce, dn, f, hh, k, brow);
+    return jstage<T, EDGE>(up, ce, dn, f, hh, k, brow);
 }
 template <int MODE, class T>
 __device__ __forceinline__ V2<T> rs(V2<T> up, V2<T> ce, V2<T> dn, V2<T> f, T ih)
@@ -453,8 +460,8 @@ __device__ __forceinline__ void postpre_body(const PostPreArgsT<T> &a)
                 const V2<T> r1 = rs<MODE, T>(b0, b1, b2, f2, ih);
                 const int row = ii - 2;
                 if (row >= olo && row < ohi && k.own) {
-                    acc1 += sq(r1.x);
-                    if (!k.by) acc1 += sq(r1.y);
+                    acc1 = sqacc(acc1, r1.x);
+                    if (!k.by) acc1 = sqacc(acc1, r1.y);
                 }
             }
             // post-smooth sweep 2: x2 row ii-2 (= phi of cycle k+1)
@@ -465,8 +472,8 @@ __device__ __forceinline__ void postpre_body(const PostPreArgsT<T> &a)
                 const V2<T> r3 = rs<MODE, T>(g0, g1, g2, f4, ih);
                 const int row = ii - 4;
                 if (row >= olo && row < ohi && k.own) {
-                    acc2 += sq(r3.x);
-                    if (!k.by) acc2 += sq(r3.y);
+                    acc2 = sqacc(acc2, r3.x);
+                    if (!k.by) acc2 = sqacc(acc2, r3.y);
                 }
             }
             // pre-smooth sweep 2: x4 row ii-4 (stored)
@@ -536,15 +543,26 @@ constexpr int kPPLdsCoarse = 2 * kPPStride + kPPMargin + 8;      // 242 doubles 
 // R2 (row strips): also sum r(x2)^2 into partials3.  When the post check fires the
 // pre-smooth restarts from x1 and its first check is ||r(J(x1))|| = ||r(x2)||; having it
 // here lets one allreduce of three sums decide every rare path.
-template <class T, bool R2>
-__global__ __launch_bounds__(256) void k_postpre_lds(PostPreArgsT<T> a)
+// GENF (the problem's f is the analytic RHS of compute_rhs): f is not streamed from HBM
+// but regenerated per point as (T)(fx[i] * sy[j]) with fx[i] = factor*sin(p pi x_i / a)
+// (per lane, in registers) and sy[j] = sin(q pi y_j / a) (per row, a scalar load) — the
+// same IEEE operations as k_rhs, so the values are identical to the stored f.  One
+// multiply per point replaces 8 bytes per point of the pass (28 -> 20 B/pt).
+// D: row pairs of loads in flight per lane (register sets); OCC: waves per SIMD the
+// register allocation must allow (1 = compiler's choice).
+// MODE 1 (measurement only): stencil arithmetic replaced by one add (js/rs), to separate
+// the memory/LDS cost of the pass from its VALU cost.
+constexpr int kPPR = 2;   // rows per LDS slot (a row pair)
+
+// The body of k_postpre_lds for one block.  EDGE = false: no row of the block's band and
+// no column of this wave is a boundary, so the Jacobi stages carry no passthrough selects.
+template <class T, bool R2, bool GENF, int D, int MODE, bool EDGE>
+__device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const Cols &k,
+                                                double *red, T (&sx)[2][kPPR][kPPLdsRow],
+                                                T (&sf)[2][kPPR][GENF ? 1 : kPPLdsRow],
+                                                T (&se)[3][kPPLdsCoarse])
 {
-    constexpr int R = 2;
-    __shared__ double red[4];
-    __shared__ __attribute__((aligned(16))) T sx[2][R][kPPLdsRow];
-    __shared__ __attribute__((aligned(16))) T sf[2][R][kPPLdsRow];
-    __shared__ __attribute__((aligned(16))) T se[3][kPPLdsCoarse];
-    const Cols k = lane_cols_t<kPPStride, kPPMargin>(a.N);
+    constexpr int R = kPPR;
     const int N = a.N, Nc = a.Nc;
     const long long P = a.P, Pc = a.Pc;
     const int jcb = a.jc0 + blockIdx.y * a.rows_per_block;
@@ -573,6 +591,8 @@ __global__ __launch_bounds__(256) void k_postpre_lds(PostPreArgsT<T> a)
     const T *__restrict__ GX = a.phi + L0 + 2 * t;
     const T *__restrict__ GF = a.f + L0 + 2 * t;
     const T *__restrict__ GE = a.ec + cc0 + t;
+    // GENF: this lane's columns of fx (tables padded: valid for columns/rows -8 ..)
+    const double fxa = GENF ? a.gfx[k.c] : 0.0, fxb = GENF ? a.gfx[k.c + 1] : 0.0;
     // this wave's window in the LDS rows
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int xo = kPPStride * w + 2 * lane;
@@ -590,16 +610,16 @@ __global__ __launch_bounds__(256) void k_postpre_lds(PostPreArgsT<T> a)
     if (t < 2 * R * 4) {   // the 4 pad doubles past the window (read by spare lanes only)
         const int sl = t >> 3, q = (t >> 2) & 1, j = kPPLdsRow - 4 + (t & 3);
         sx[sl][q][j] = T(0);
-        sf[sl][q][j] = T(0);
+        if constexpr (!GENF) sf[sl][q][j] = T(0);
     }
-    // two register sets: pair p's loads go to set p & 1, issued two pairs ahead
-    V2<T> pxA[R], pfA[R], pxB[R], pfB[R];
-    T peA = T(0), peB = T(0);
+    // D register sets: pair p's loads go to set p % D, issued D pairs ahead
+    V2<T> pxA[R], pfA[R], pxB[R], pfB[R], pxC[R], pfC[R];
+    T peA = T(0), peB = T(0), peC = T(0);
     auto load_pair = [&](int p, V2<T> (&px)[R], V2<T> (&pf)[R], T &pe) {
         #pragma unroll
         for (int q = 0; q < R; ++q) {
             px[q] = ldr ? ldv(GX + (i_begin + p * R + q) * P) : z;
-            pf[q] = ldr ? ldv(GF + (i_begin + p * R + q) * P) : z;
+            if constexpr (!GENF) pf[q] = ldr ? ldv(GF + (i_begin + p * R + q) * P) : z;
         }
         pe = cldr ? GE[(long long)(m0 + p + 1) * Pc] : T(0);   // the pair's second coarse row
     };
@@ -608,17 +628,22 @@ __global__ __launch_bounds__(256) void k_postpre_lds(PostPreArgsT<T> a)
             #pragma unroll
             for (int q = 0; q < R; ++q) {
                 *reinterpret_cast<V2<T> *>(&sx[p & 1][q][2 * t]) = px[q];
-                *reinterpret_cast<V2<T> *>(&sf[p & 1][q][2 * t]) = pf[q];
+                if constexpr (!GENF) *reinterpret_cast<V2<T> *>(&sf[p & 1][q][2 * t]) = pf[q];
             }
         }
         if (t < ncc) se[ring(m0 + p + 1)][t] = pe;
     };
-    // prologue: pair 0 (+ its first coarse row) into slot 0; pairs 1, 2 in flight
+    // prologue: pair 0 (+ its first coarse row) into slot 0; pairs 1 .. D in flight
     load_pair(0, pxA, pfA, peA);
     if (t < ncc) se[ring(m0)][t] = cldr ? GE[(long long)m0 * Pc] : T(0);
     store_pair(0, pxA, pfA, peA);
     if (ng > 1) load_pair(1, pxB, pfB, peB);
-    if (ng > 2) load_pair(2, pxA, pfA, peA);
+    if constexpr (D == 2) {
+        if (ng > 2) load_pair(2, pxA, pfA, peA);
+    } else {
+        if (ng > 2) load_pair(2, pxC, pfC, peC);
+        if (ng > 3) load_pair(3, pxA, pfA, peA);
+    }
     __syncthreads();
 
     // pair gi: compute from slot gi & 1; pair gi+1 (set (gi+1) & 1) -> the other slot;
@@ -633,43 +658,49 @@ __global__ __launch_bounds__(256) void k_postpre_lds(PostPreArgsT<T> a)
         for (int s = 0; s < R; ++s) {
             const int ii = i + s;
             const V2<T> xr = ldv(&sx[slot][s][xo]);
-            const V2<T> f0 = ldv(&sf[slot][s][xo]);   // f[ii]
+            V2<T> f0;   // f[ii]
+            if constexpr (GENF) {
+                const double sy = a.gsy[ii];
+                f0 = mk2<T>((T)(fxa * sy), (T)(fxb * sy));
+            } else {
+                f0 = ldv(&sf[slot][s][xo]);
+            }
             const V2<T> e2 = add_prolong(xr, ii, cr0, crn0, cr1, crn1, pc, Nc);
             // post-smooth sweep 1: x1 row ii-1
-            const V2<T> b2 = jstage(e0, e1, e2, f1, hh, k, boundary_row(ii - 1, N));
+            const V2<T> b2 = js<MODE, T, EDGE>(e0, e1, e2, f1, hh, k, boundary_row(ii - 1, N));
             {   // post check: r(x1) on row ii-2
-                const V2<T> r1 = rstage(b0, b1, b2, f2, ih);
+                const V2<T> r1 = rs<MODE, T>(b0, b1, b2, f2, ih);
                 const int row = ii - 2;
                 if (row >= olo && row < ohi && k.own) {
-                    acc1 += sq(r1.x);
-                    if (!k.by) acc1 += sq(r1.y);
+                    acc1 = sqacc(acc1, r1.x);
+                    if (!k.by) acc1 = sqacc(acc1, r1.y);
                 }
             }
             // post-smooth sweep 2: x2 row ii-2 (= phi of cycle k+1)
-            const V2<T> c2 = jstage(b0, b1, b2, f2, hh, k, boundary_row(ii - 2, N));
+            const V2<T> c2 = js<MODE, T, EDGE>(b0, b1, b2, f2, hh, k, boundary_row(ii - 2, N));
             if (R2) {   // r(x2) on row ii-3
-                const V2<T> r2 = rstage(c0, c1, c2, f3, ih);
+                const V2<T> r2 = rs<MODE, T>(c0, c1, c2, f3, ih);
                 const int row = ii - 3;
                 if (row >= olo && row < ohi && k.own) {
-                    acc3 += sq(r2.x);
-                    if (!k.by) acc3 += sq(r2.y);
+                    acc3 = sqacc(acc3, r2.x);
+                    if (!k.by) acc3 = sqacc(acc3, r2.y);
                 }
             }
             // pre-smooth sweep 1: x3 row ii-3
-            const V2<T> g2 = jstage(c0, c1, c2, f3, hh, k, boundary_row(ii - 3, N));
+            const V2<T> g2 = js<MODE, T, EDGE>(c0, c1, c2, f3, hh, k, boundary_row(ii - 3, N));
             {   // pre check: r(x3) on row ii-4
-                const V2<T> r3 = rstage(g0, g1, g2, f4, ih);
+                const V2<T> r3 = rs<MODE, T>(g0, g1, g2, f4, ih);
                 const int row = ii - 4;
                 if (row >= olo && row < ohi && k.own) {
-                    acc2 += sq(r3.x);
-                    if (!k.by) acc2 += sq(r3.y);
+                    acc2 = sqacc(acc2, r3.x);
+                    if (!k.by) acc2 = sqacc(acc2, r3.y);
                 }
             }
             // pre-smooth sweep 2: x4 row ii-4 (stored)
-            const V2<T> h2 = jstage(g0, g1, g2, f4, hh, k, boundary_row(ii - 4, N));
+            const V2<T> h2 = js<MODE, T, EDGE>(g0, g1, g2, f4, hh, k, boundary_row(ii - 4, N));
             if (ii - 4 >= olo && ii - 4 < ohi && k.own) stv(O + (ii - 4) * P, h2);
             // r(x4) on row ii-5
-            const V2<T> d2 = rstage(h0, h1, h2, f5, ih);
+            const V2<T> d2 = rs<MODE, T>(h0, h1, h2, f5, ih);
             // restriction: rows ii-7, ii-6, ii-5 = 2jc-1, 2jc, 2jc+1 when ii is even
             if ((s & 1) == 0) {
                 const int jc = (ii - 6) >> 1;
@@ -692,12 +723,20 @@ __global__ __launch_bounds__(256) void k_postpre_lds(PostPreArgsT<T> a)
             f5 = f4; f4 = f3; f3 = f2; f2 = f1; f1 = f0;
         }
         if (gi + 1 < ng) store_pair(gi + 1, px, pf, pe);
-        if (gi + 3 < ng) load_pair(gi + 3, px, pf, pe);
+        if (gi + 1 + D < ng) load_pair(gi + 1 + D, px, pf, pe);
         __syncthreads();
     };
-    for (int gi = 0; gi < ng; gi += 2) {
-        step(gi, pxB, pfB, peB);
-        if (gi + 1 < ng) step(gi + 1, pxA, pfA, peA);
+    if constexpr (D == 2) {
+        for (int gi = 0; gi < ng; gi += 2) {
+            step(gi, pxB, pfB, peB);
+            if (gi + 1 < ng) step(gi + 1, pxA, pfA, peA);
+        }
+    } else {
+        for (int gi = 0; gi < ng; gi += 3) {
+            step(gi, pxB, pfB, peB);
+            if (gi + 1 < ng) step(gi + 1, pxC, pfC, peC);
+            if (gi + 2 < ng) step(gi + 2, pxA, pfA, peA);
+        }
     }
     const int slot = blockIdx.y * gridDim.x + blockIdx.x;
     const double s1 = fused_block_sum(acc1, red);
@@ -712,6 +751,26 @@ __global__ __launch_bounds__(256) void k_postpre_lds(PostPreArgsT<T> a)
         a.partials1[slot] = s1;
         a.partials2[slot] = s2;
     }
+}
+
+
+template <class T, bool R2, bool GENF, int D = 2, int OCC = 1, int MODE = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC)))
+void k_postpre_lds(PostPreArgsT<T> a)
+{
+    __shared__ double red[4];
+    __shared__ __attribute__((aligned(16))) T sx[2][kPPR][kPPLdsRow];
+    __shared__ __attribute__((aligned(16))) T sf[2][kPPR][GENF ? 1 : kPPLdsRow];
+    __shared__ __attribute__((aligned(16))) T se[3][kPPLdsCoarse];
+    const Cols k = lane_cols_t<kPPStride, kPPMargin>(a.N);
+    // the band's rows 2jcb-6 .. 2jce+5 (see postpre_lds_run): does it reach row 0 or N-1?
+    const int jcb = a.jc0 + blockIdx.y * a.rows_per_block;
+    const int jce = min(jcb + a.rows_per_block, a.jc1);
+    const bool edge_rows = 2 * jcb - 6 <= 0 || 2 * jce + 6 >= a.N - 1;
+    if (k.edge || edge_rows)
+        postpre_lds_run<T, R2, GENF, D, MODE, true>(a, k, red, sx, sf, se);
+    else
+        postpre_lds_run<T, R2, GENF, D, MODE, false>(a, k, red, sx, sf, se);
 }
 
 // one block: both decisions, stats, flags for the conditional rare-path kernels
@@ -857,15 +916,36 @@ void launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
     a.rows_per_block = r;
     const dim3 g(gx, gy), b(t);
     if constexpr (std::is_same<T, double>::value) {
-        if (a.partials3 != nullptr && variant != 0) return;   // measurement variants: 1 GPU only
+        if ((a.partials3 != nullptr || a.gfx != nullptr) && variant != 0) return;   // 1 GPU, stored f
         if (variant == 4) k_postpre<T, 1, 0><<<g, b, 0, s>>>(a);    // per-wave loads (r01)
         else if (variant == 1) k_postpre<T, 1, 1><<<g, b, 0, s>>>(a);
         else if (variant == 3) k_postpre<T, 1, 1, 128, 0><<<g, b, 0, s>>>(a);  // no column overlap
         else if (variant == 2) k_postpre_o4<T, 1><<<g, b, 0, s>>>(a);
         if (variant != 0) return;
     }
-    if (a.partials3 != nullptr) k_postpre_lds<T, true><<<g, b, 0, s>>>(a);
-    else k_postpre_lds<T, false><<<g, b, 0, s>>>(a);
+    const bool genf = a.gfx != nullptr;
+    if constexpr (std::is_same<T, double>::value) {
+        // measurement knobs for the default pass (1 GPU, regenerated f)
+        const int depth = env_int("PGMG_PP_DEPTH", 2), occ = env_int("PGMG_PP_OCC", 1);
+        const int mode = env_int("PGMG_PP_LDS_MODE", 0);
+        if (genf && a.partials3 == nullptr && mode == 1) {
+            k_postpre_lds<T, false, true, 2, 1, 1><<<g, b, 0, s>>>(a);
+            return;
+        }
+        if (genf && a.partials3 == nullptr && (depth != 2 || occ != 1)) {
+            if (depth == 3 && occ == 3) k_postpre_lds<T, false, true, 3, 3><<<g, b, 0, s>>>(a);
+            else if (depth == 3) k_postpre_lds<T, false, true, 3, 1><<<g, b, 0, s>>>(a);
+            else k_postpre_lds<T, false, true, 2, 3><<<g, b, 0, s>>>(a);
+            return;
+        }
+    }
+    if (a.partials3 != nullptr) {
+        if (genf) k_postpre_lds<T, true, true><<<g, b, 0, s>>>(a);
+        else k_postpre_lds<T, true, false><<<g, b, 0, s>>>(a);
+    } else {
+        if (genf) k_postpre_lds<T, false, true><<<g, b, 0, s>>>(a);
+        else k_postpre_lds<T, false, false><<<g, b, 0, s>>>(a);
+    }
 }
 
 void launch_postpre_decide(const double *partials1, const double *partials2, unsigned long long *stats,

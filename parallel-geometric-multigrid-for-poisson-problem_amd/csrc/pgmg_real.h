@@ -31,31 +31,34 @@ template <class T> __device__ __forceinline__ V2<T> zero2() { return mk2<T>(T(0)
 
 // r*r accumulated in double (identical to r*r for T = double)
 template <class T> __device__ __forceinline__ double sq(T r) { return (double)r * (double)r; }
+// acc + r*r with one fused multiply-add: the early-exit partial sums are order-dependent
+// anyway (parallel reduction), so their rounding is not part of the bitwise contract
+template <class T> __device__ __forceinline__ double sqacc(double acc, T r)
+{
+    return __builtin_fma((double)r, (double)r, acc);
+}
 
 // wave64 DPP lane moves: wave_shr:1 (lane i <- lane i-1), wave_shl:1 (lane i <- lane i+1);
-// the edge lane receives 0
+// the edge lane receives 0.  bound_ctrl = true: lanes without a source lane read 0, so
+// no "old" operand has to be materialised (one v_mov_b32_dpp per dword, no extra move).
+__device__ __forceinline__ int dpp_shr_i(int v) { return __builtin_amdgcn_mov_dpp(v, 0x138, 0xF, 0xF, true); }
+__device__ __forceinline__ int dpp_shl_i(int v) { return __builtin_amdgcn_mov_dpp(v, 0x130, 0xF, 0xF, true); }
 __device__ __forceinline__ double dpp_shr(double v)
 {
     const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x138, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xF, 0xF, false);
+    const int lo = dpp_shr_i((int)b);
+    const int hi = dpp_shr_i((int)(b >> 32));
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 __device__ __forceinline__ double dpp_shl(double v)
 {
     const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x130, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x130, 0xF, 0xF, false);
+    const int lo = dpp_shl_i((int)b);
+    const int hi = dpp_shl_i((int)(b >> 32));
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
-__device__ __forceinline__ float dpp_shr(float v)
-{
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float dpp_shl(float v)
-{
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xF, 0xF, false));
-}
+__device__ __forceinline__ float dpp_shr(float v) { return __int_as_float(dpp_shr_i(__float_as_int(v))); }
+__device__ __forceinline__ float dpp_shl(float v) { return __int_as_float(dpp_shl_i(__float_as_int(v))); }
 
 // elements between an allocation's base and element (0,0): column 1 of every row on a
 // 128-byte boundary (15 doubles, 31 floats)

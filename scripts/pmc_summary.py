@@ -30,6 +30,14 @@ def norm_name(n):
     return m.group(1) + t
 
 
+def is_finest(k):
+    """Finest-level kernel symbols (normalised): k_postpre*, k_pre<T,false,true>,
+    k_post<T,true,PAIRS,false>, k_sweep<T,X0,NORM,true>."""
+    return bool(k.startswith("k_postpre") or re.match(r"k_pre<\w+,false,true>$", k) or
+                re.match(r"k_post<\w+,true,\d+,false>$", k) or
+                re.match(r"k_sweep<\w+,\w+,\w+,true>$", k))
+
+
 def main(tag, N=16385):
     dst = ROOT / "profiles" / tag
     dst.mkdir(parents=True, exist_ok=True)
@@ -53,9 +61,7 @@ def main(tag, N=16385):
             stats[norm_name(r["Name"])] = float(r["AverageNs"]) / 1e6
     kernels = []
     for k, v in sorted(vals.items()):
-        finest = k.startswith("k_postpre<") or (k.endswith("true>") and (
-            k.startswith("k_pre<") or k.startswith("k_post<") or k.startswith("k_sweep<")))
-        if not finest:
+        if not is_finest(k):
             continue  # finest-level symbols only (FINE template argument; k_postpre always)
         if not v.get("FETCH_SIZE") or not v.get("WRITE_SIZE"):
             continue

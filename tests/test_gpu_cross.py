@@ -119,3 +119,46 @@ def test_cross_rare_paths_nonzero_boundary(pgmg, oracle_mod, cross_everywhere):
             seen[0] += d[2]
             seen[1] += d[3]
     assert seen[0] > 0 and seen[1] > 0, seen
+
+
+@pytest.mark.parametrize("N,dtype", [(513, "f64"), (2049, "f64"), (513, "f32")])
+def test_regenerated_rhs_equals_stored_rhs(pgmg, cross_everywhere, N, dtype):
+    """With the analytic RHS, k_postpre regenerates f in-kernel (fx[i] * sy[j]); the same
+    multi-cycle call with PGMG_FLAG_STORED_RHS streams the stored f: identical words."""
+    out = []
+    for flags in (0, pgmg.PGMG_FLAG_STORED_RHS):
+        with pgmg.Solver(N, dtype=dtype, flags=flags) as s:
+            s.set_problem()
+            gen = s.fine_pass_bytes(3) < s.fine_pass_bytes(2)
+            assert gen == (flags == 0)
+            s.vcycle(4)
+            out.append((s.solution(), s.stats_detail()))
+    assert_bitwise(out[0][0], out[1][0], f"regenerated vs stored f, N={N} {dtype}")
+    assert out[0][1] == out[1][1]
+
+
+def test_regenerated_rhs_rare_paths(pgmg, oracle_mod, cross_everywhere):
+    """Analytic f (regenerated in k_postpre) with a random phi0 and eps swept until both
+    k_postpre rare paths fire: bitwise to the oracle."""
+    rng = np.random.default_rng(9)
+    N = 129
+    phi0 = rng.uniform(-1, 1, (N, N)) * 1e-3
+    phi0[0, :] = phi0[-1, :] = phi0[:, 0] = phi0[:, -1] = 0.0
+    seen = [0, 0]
+    for eps in [10 ** (k / 12.0) for k in range(72, -36, -1)]:
+        if seen[0] > 0 and seen[1] > 0:
+            break
+        o = oracle_mod.Oracle(eps=eps)
+        f = o.rhs(N)
+        ref = phi0.copy()
+        for _ in range(6):
+            o.v_cycle(ref, f)
+        with pgmg.Solver(N, eps=eps, tail_n=17) as s:
+            s.set_problem(phi0, None)
+            s.vcycle(6)
+            assert_bitwise(s.solution(), ref, f"eps={eps}")
+            d = s.stats_detail()
+            assert d[0] == o.sweeps, (eps, d, o.sweeps)
+            seen[0] += d[2]
+            seen[1] += d[3]
+    assert seen[0] > 0 and seen[1] > 0, seen
