@@ -149,7 +149,7 @@ def main():
     dev_ms = s.last_elapsed_ms()
     vbytes = s.vcycle_bytes()
     n = N = args.n
-    gen = s.fused and s.fine_pass_bytes(3) < s.fine_pass_bytes(2)   # f regenerated in-kernel
+    gen = s.fused and s.fine_pass_bytes(3) < s.fine_pass_bytes(0)   # f regenerated in-kernel
     T = "double" if args.dtype == "f64" else "float"
     passes = []
     if s.fused:
@@ -161,9 +161,9 @@ def main():
                     + ")", f"k_postpre_lds<{T},{'true' if world > 1 else 'false'},"
                            f"{'true' if gen else 'false'}>"),
                 (1, "k_pre<false,true> (finest level: 2 Jacobi sweeps + residual + restriction, "
-                    "fused)", f"k_pre<{T},false,true>"),
+                    "fused)", f"k_pre<{T},false,true,2,true>" if gen else f"k_pre<{T},false,true>"),
                 (2, "k_post<true> (finest level: prolongation + 2 Jacobi sweeps, fused)",
-                 f"k_post<{T},true,2,false>")):
+                 f"k_post<{T},true,2,false,true>" if gen else f"k_post<{T},true,2,false>")):
             cnt, ms = s.fine_pass_time(which)
             passes.append((name, s.fine_pass_bytes(which), cnt, ms, key))
     else:

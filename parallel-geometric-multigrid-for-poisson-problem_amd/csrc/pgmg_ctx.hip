@@ -350,6 +350,8 @@ static PreArgsT<T> make_pre(pgmg_ctx *c, const T *x0, T *x2)
     pa.row_hi = sr.row_hi;
     pa.rc_lo = sr.rc_lo;
     pa.rc_hi = sr.rc_hi;
+    pa.gfx = c->gen_rhs ? c->gfx : nullptr;
+    pa.gsy = c->gen_rhs ? c->gsy : nullptr;
     return pa;
 }
 
@@ -375,6 +377,8 @@ static PostArgsT<T> make_post(pgmg_ctx *c, const T *phi, T *x2)
     po.jc1 = sr.jc1;
     po.row_lo = sr.row_lo;
     po.row_hi = sr.row_hi;
+    po.gfx = c->gen_rhs ? c->gfx : nullptr;
+    po.gsy = c->gen_rhs ? c->gsy : nullptr;
     return po;
 }
 
@@ -1202,11 +1206,13 @@ int pgmg_fine_pass_bytes(pgmg_ctx *c, int pass, double *bytes)
     const StripRows sr = strip_rows(L, C);
     const double nc = (double)(sr.rc_hi > sr.rc_lo ? sr.rc_hi - sr.rc_lo : 0) * (C.N - 2);
     double b = 0.0;
+    // f is regenerated in-kernel (not read) by the cross-fused level-0 passes
+    const double fb = (c->cross && c->gen_rhs) ? 0.0 : 8.0;
     switch (pass) {
     case 0: b = 24.0 * n; break;                               // x, f in; x out
-    case 1: b = 24.0 * n + 8.0 * nc; break;                    // x0, f in; x2, rc out
-    case 2: b = 24.0 * n + 8.0 * nc; break;                    // phi, f, ec in; x2 out
-    case 3: b = (c->gen_rhs ? 16.0 : 24.0) * n + 16.0 * nc; break;  // phi, (f,) ec; x4, rc
+    case 1: b = (16.0 + fb) * n + 8.0 * nc; break;             // x0, (f) in; x2, rc out
+    case 2: b = (16.0 + fb) * n + 8.0 * nc; break;             // phi, (f,) ec in; x2 out
+    case 3: b = (16.0 + fb) * n + 16.0 * nc; break;            // phi, (f,) ec; x4, rc
     }
     *bytes = b * (L.es / 8.0);
     return PGMG_OK;

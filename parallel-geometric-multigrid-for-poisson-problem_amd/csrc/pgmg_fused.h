@@ -24,6 +24,8 @@ struct PreArgsT {
     int rows_per_block;
     const unsigned *cond;       // non-null: run only when *cond != 0
     unsigned *fired;            // non-null: the fix-up records whether the check fired
+    // non-null: f is the analytic RHS, regenerated as (T)(gfx[i] * gsy[j]) (level 0 only)
+    const double *gfx, *gsy;
 };
 
 // prolongation + post-smooth (2 sweeps) in one pass
@@ -45,6 +47,8 @@ struct PostArgsT {
     // x0 = 0 (x1 = J(0), phi = *pre_fired ? x1 : J(x1)); PreArgs::fired of the same level
     const unsigned *pre_fired;
     int fix_sweeps;             // k_post_fixup: 0/1 -> x1 (the check fired), 2 -> x2
+    // non-null: f is the analytic RHS, regenerated as (T)(gfx[i] * gsy[j]) (level 0 only)
+    const double *gfx, *gsy;
 };
 
 // post-smooth of cycle k + pre-smooth/residual/restriction of cycle k+1 in one pass

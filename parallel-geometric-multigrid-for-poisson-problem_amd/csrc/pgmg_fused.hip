@@ -109,7 +109,8 @@ __device__ __forceinline__ double fused_block_sum(double v, double *red)
 // ---------------------------------------------------------------------------
 // k_pre
 // ---------------------------------------------------------------------------
-template <class T, bool X0_ZERO, bool FINE, int PAIRS>
+// GENF: f is the analytic RHS, regenerated per row from the gfx/gsy tables (see k_postpre_lds)
+template <class T, bool X0_ZERO, bool FINE, int PAIRS, bool GENF = false>
 __global__ __launch_bounds__(256) void k_pre(PreArgsT<T> a)
 {
     constexpr int R = 2 * PAIRS;  // rows loaded per iteration (and prefetched ahead)
@@ -126,6 +127,7 @@ __global__ __launch_bounds__(256) void k_pre(PreArgsT<T> a)
         atomicAdd(&a.stats[0], 2ull);
     const T *__restrict__ X = a.x0 + k.c;
     const T *__restrict__ F = a.f + k.c;
+    const double fxa = GENF ? a.gfx[k.c] : 0.0, fxb = GENF ? a.gfx[k.c + 1] : 0.0;
     const bool store = a.x2 != nullptr;
     T *__restrict__ O = a.x2 + k.c;
     const T hh = a.hh, ih = a.ih;
@@ -146,27 +148,33 @@ __global__ __launch_bounds__(256) void k_pre(PreArgsT<T> a)
     #pragma unroll
     for (int q = 0; q < R; ++q) {
         nx[q] = (X0_ZERO || idle) ? z : ldv(X + (i_begin + q) * P);
-        nf[q] = idle ? z : ldv(F + (i_begin + q) * P);
+        if constexpr (!GENF) nf[q] = idle ? z : ldv(F + (i_begin + q) * P);
     }
     for (int i = i_begin; i < i_end; i += R) {
         V2<T> cx[R], cf[R];
         #pragma unroll
         for (int q = 0; q < R; ++q) {
             cx[q] = nx[q];
-            cf[q] = nf[q];
+            if constexpr (!GENF) cf[q] = nf[q];
         }
         if (i + R < i_end) {  // prefetch the next R rows
             #pragma unroll
             for (int q = 0; q < R; ++q) {
                 if (!X0_ZERO) nx[q] = ldv(X + (i + R + q) * P);
-                nf[q] = ldv(F + (i + R + q) * P);
+                if constexpr (!GENF) nf[q] = ldv(F + (i + R + q) * P);
             }
         }
         #pragma unroll
         for (int s = 0; s < R; ++s) {
             const int ii = i + s;
             const V2<T> a2 = cx[s];
-            const V2<T> f3 = cf[s];
+            V2<T> f3;
+            if constexpr (GENF) {
+                const double sy = a.gsy[ii];
+                f3 = mk2<T>((T)(fxa * sy), (T)(fxb * sy));
+            } else {
+                f3 = cf[s];
+            }
             // x1 row ii-1
             const V2<T> b2 = jstage(a0, a1, a2, f2, hh, k, boundary_row(ii - 1, N));
             // r(x1) and x2 on row ii-2
@@ -220,18 +228,20 @@ struct ProlongCols {
     int ic;        // coarse column of the odd fine column c: (c-1)/2
 };
 
-template <class T>
+// EDGE = false: the caller guarantees row in [2, Nf-2] and both columns in [2, Nf-2]
+// (interior bands and wave tiles), so no masks
+template <class T, bool EDGE = true>
 __device__ __forceinline__ V2<T> add_prolong(V2<T> p, int row, T ca, T cb, T da, T db, const ProlongCols &pc, int Nc)
 {
     // MultiGrid.hpp:219-223; row in [2, Nf-2] <=> its coarse row m in [1, Nc-2]
     const int m = row >> 1;
-    if (m < 1 || m > Nc - 2) return p;
+    if (EDGE && (m < 1 || m > Nc - 2)) return p;
     if ((row & 1) == 0) {
-        if (pc.vx) p.x = p.x + T(0.5) * (ca + cb);
-        if (pc.vy) p.y = p.y + cb;
+        if (!EDGE || pc.vx) p.x = p.x + T(0.5) * (ca + cb);
+        if (!EDGE || pc.vy) p.y = p.y + cb;
     } else {
-        if (pc.vx) p.x = p.x + T(0.25) * (ca + cb + da + db);
-        if (pc.vy) p.y = p.y + T(0.5) * (cb + db);
+        if (!EDGE || pc.vx) p.x = p.x + T(0.25) * (ca + cb + da + db);
+        if (!EDGE || pc.vy) p.y = p.y + T(0.5) * (cb + db);
     }
     return p;
 }
@@ -239,7 +249,7 @@ __device__ __forceinline__ V2<T> add_prolong(V2<T> p, int row, T ca, T cb, T da,
 // RECOMP (levels entered with x0 = 0): phi is not read.  The loaded row is f[ii+1];
 // x1 = J(0) is pointwise, so x1 row ii+1 -> phi row ii = J(x1) (or x1 when the pre
 // check fired) -> x_eff row ii: one more row of lag than reading phi, 16 B/point less.
-template <class T, bool FINE, int PAIRS, bool RECOMP>
+template <class T, bool FINE, int PAIRS, bool RECOMP, bool GENF = false>
 __global__ __launch_bounds__(256) void k_post(PostArgsT<T> a)
 {
     constexpr int R = 2 * PAIRS;
@@ -258,6 +268,7 @@ __global__ __launch_bounds__(256) void k_post(PostArgsT<T> a)
     pc.vx = k.c >= 3 && k.c <= N - 2;
     pc.vy = k.c + 1 >= 2 && k.c + 1 <= N - 3;
     const T *__restrict__ F = a.f + k.c;
+    const double fxa = GENF ? a.gfx[k.c] : 0.0, fxb = GENF ? a.gfx[k.c + 1] : 0.0;
     // the streamed array: phi, or f one row ahead (RECOMP)
     const T *__restrict__ X = RECOMP ? F + P : a.phi + k.c;
     const T *__restrict__ E = a.ec + pc.ic;
@@ -287,7 +298,7 @@ __global__ __launch_bounds__(256) void k_post(PostArgsT<T> a)
     #pragma unroll
     for (int q = 0; q < R; ++q) {
         np_[q] = idle ? z : ldv(X + (i_begin + q) * P);
-        if (!RECOMP) nf[q] = idle ? z : ldv(F + (i_begin + q) * P);
+        if (!RECOMP && !GENF) nf[q] = idle ? z : ldv(F + (i_begin + q) * P);
     }
     #pragma unroll
     for (int q = 0; q <= PAIRS; ++q) ncr[q] = idle ? T(0) : E[(long long)((i_begin >> 1) + q) * Pc];
@@ -297,7 +308,7 @@ __global__ __launch_bounds__(256) void k_post(PostArgsT<T> a)
         #pragma unroll
         for (int q = 0; q < R; ++q) {
             cp[q] = np_[q];
-            if (!RECOMP) cf[q] = nf[q];
+            if (!RECOMP && !GENF) cf[q] = nf[q];
         }
         #pragma unroll
         for (int q = 0; q <= PAIRS; ++q) cr[q] = ncr[q];
@@ -305,7 +316,7 @@ __global__ __launch_bounds__(256) void k_post(PostArgsT<T> a)
             #pragma unroll
             for (int q = 0; q < R; ++q) {
                 np_[q] = ldv(X + (i + R + q) * P);
-                if (!RECOMP) nf[q] = ldv(F + (i + R + q) * P);
+                if (!RECOMP && !GENF) nf[q] = ldv(F + (i + R + q) * P);
             }
             #pragma unroll
             for (int q = 0; q <= PAIRS; ++q) ncr[q] = E[(long long)(((i + R) >> 1) + q) * Pc];
@@ -328,7 +339,12 @@ __global__ __launch_bounds__(256) void k_post(PostArgsT<T> a)
                 fc = fn;
             } else {
                 ph = cp[s];
-                f3 = cf[s];
+                if constexpr (GENF) {
+                    const double sy = a.gsy[ii];
+                    f3 = mk2<T>((T)(fxa * sy), (T)(fxb * sy));
+                } else {
+                    f3 = cf[s];
+                }
             }
             const V2<T> a2 = add_prolong(ph, ii, cr[pq], crn[pq], cr[pq + 1], crn[pq + 1], pc, Nc);
             const V2<T> b2 = jstage(a0, a1, a2, f2, hh, k, boundary_row(ii - 1, N));
@@ -370,6 +386,39 @@ constexpr int kPPStride = 114, kPPMargin = 6;
 // MODE 0: the real pass.  MODE 1 (PGMG_PP_VARIANT=1, measurement only): the same loads
 // and stores with the stencil arithmetic replaced by one add, to separate the memory
 // ceiling of this access pattern from the instruction cost.
+// Horizontal neighbours of a row's column pair (left of c, right of c+1), shared by the
+// stages that use the same centre row (a Jacobi sweep and a residual of the same iterate).
+template <class T> struct Nbr {
+    T l, r;
+};
+template <class T> __device__ __forceinline__ Nbr<T> nbr(V2<T> ce)
+{
+    return Nbr<T>{dpp_shr(ce.y), dpp_shl(ce.x)};
+}
+template <int MODE, class T, bool EDGE>
+__device__ __forceinline__ V2<T> jsn(V2<T> up, V2<T> ce, V2<T> dn, Nbr<T> n, V2<T> f, T hh,
+                                       const Cols &k, bool brow)
+{
+    if (MODE == 1) return mk2<T>(ce.x + f.x, ce.y + up.y + dn.y);
+    V2<T> o;
+    o.x = T(0.25) * ((hh * f.x) + n.l + ce.y + up.x + dn.x);
+    o.y = T(0.25) * ((hh * f.y) + ce.x + n.r + up.y + dn.y);
+    if constexpr (EDGE) {
+        if (brow || k.bx) o.x = ce.x;
+        if (brow || k.by) o.y = ce.y;
+    }
+    return o;
+}
+template <int MODE, class T>
+__device__ __forceinline__ V2<T> rsn(V2<T> up, V2<T> ce, V2<T> dn, Nbr<T> n, V2<T> f, T ih)
+{
+    if (MODE == 1) return mk2<T>(f.x + ce.x, f.y);
+    V2<T> o;
+    o.x = f.x - ih * (T(4) * ce.x - n.l - ce.y - up.x - dn.x);
+    o.y = f.y - ih * (T(4) * ce.y - ce.x - n.r - up.y - dn.y);
+    return o;
+}
+
 template <int MODE, class T, bool EDGE = true>
 __device__ __forceinline__ V2<T> js(V2<T> up, V2<T> ce, V2<T> dn, V2<T> f, T hh,
                                       const Cols &k, bool brow)
@@ -556,7 +605,7 @@ constexpr int kPPR = 2;   // rows per LDS slot (a row pair)
 
 // The body of k_postpre_lds for one block.  EDGE = false: no row of the block's band and
 // no column of this wave is a boundary, so the Jacobi stages carry no passthrough selects.
-template <class T, bool R2, bool GENF, int D, int MODE, bool EDGE>
+template <class T, bool R2, bool GENF, int D, int MODE, bool EDGE, bool FRECOMP>
 __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const Cols &k,
                                                 double *red, T (&sx)[2][kPPR][kPPLdsRow],
                                                 T (&sf)[2][kPPR][GENF ? 1 : kPPLdsRow],
@@ -648,6 +697,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
 
     // pair gi: compute from slot gi & 1; pair gi+1 (set (gi+1) & 1) -> the other slot;
     // issue pair gi+3 into the set just freed; one barrier
+    T wprev = T(0);   // dpp_shl(d2.x) of the previous restriction row (d0 starts as zero)
     auto step = [&](int gi, V2<T> (&px)[R], V2<T> (&pf)[R], T &pe) {
         const int slot = gi & 1;
         const int i = i_begin + gi * R;
@@ -658,18 +708,33 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
         for (int s = 0; s < R; ++s) {
             const int ii = i + s;
             const V2<T> xr = ldv(&sx[slot][s][xo]);
-            V2<T> f0;   // f[ii]
-            if constexpr (GENF) {
+            // f[ii]; GENF: f of the row each stage needs is regenerated where it is used
+            // (one multiply per value; no window of f rows is carried across rows)
+            // f[ii]: from LDS, or (GENF) generated once here and carried in the f window.
+            // FRECOMP (measurement): regenerate f at every use instead of carrying the
+            // window (fewer VGPRs, 8 more multiplies per row: measured slower, r01)
+            V2<T> f0 = z;
+            if constexpr (!GENF) f0 = ldv(&sf[slot][s][xo]);
+            if constexpr (GENF && !FRECOMP) {
                 const double sy = a.gsy[ii];
                 f0 = mk2<T>((T)(fxa * sy), (T)(fxb * sy));
-            } else {
-                f0 = ldv(&sf[slot][s][xo]);
             }
-            const V2<T> e2 = add_prolong(xr, ii, cr0, crn0, cr1, crn1, pc, Nc);
+            auto fr = [&](int row, const V2<T> &win) -> V2<T> {
+                if constexpr (GENF && FRECOMP) {
+                    const double sy = a.gsy[row];
+                    return mk2<T>((T)(fxa * sy), (T)(fxb * sy));
+                } else {
+                    return win;
+                }
+            };
+            const V2<T> fq1 = fr(ii - 1, f1), fq2 = fr(ii - 2, f2), fq3 = fr(ii - 3, f3),
+                        fq4 = fr(ii - 4, f4), fq5 = fr(ii - 5, f5);
+            const V2<T> e2 = add_prolong<T, EDGE>(xr, ii, cr0, crn0, cr1, crn1, pc, Nc);
             // post-smooth sweep 1: x1 row ii-1
-            const V2<T> b2 = js<MODE, T, EDGE>(e0, e1, e2, f1, hh, k, boundary_row(ii - 1, N));
+            const V2<T> b2 = jsn<MODE, T, EDGE>(e0, e1, e2, nbr<T>(e1), fq1, hh, k, boundary_row(ii - 1, N));
+            const Nbr<T> nb1 = nbr<T>(b1), nc1 = nbr<T>(c1), ng1 = nbr<T>(g1);
             {   // post check: r(x1) on row ii-2
-                const V2<T> r1 = rs<MODE, T>(b0, b1, b2, f2, ih);
+                const V2<T> r1 = rsn<MODE, T>(b0, b1, b2, nb1, fq2, ih);
                 const int row = ii - 2;
                 if (row >= olo && row < ohi && k.own) {
                     acc1 = sqacc(acc1, r1.x);
@@ -677,9 +742,9 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                 }
             }
             // post-smooth sweep 2: x2 row ii-2 (= phi of cycle k+1)
-            const V2<T> c2 = js<MODE, T, EDGE>(b0, b1, b2, f2, hh, k, boundary_row(ii - 2, N));
+            const V2<T> c2 = jsn<MODE, T, EDGE>(b0, b1, b2, nb1, fq2, hh, k, boundary_row(ii - 2, N));
             if (R2) {   // r(x2) on row ii-3
-                const V2<T> r2 = rs<MODE, T>(c0, c1, c2, f3, ih);
+                const V2<T> r2 = rsn<MODE, T>(c0, c1, c2, nc1, fq3, ih);
                 const int row = ii - 3;
                 if (row >= olo && row < ohi && k.own) {
                     acc3 = sqacc(acc3, r2.x);
@@ -687,9 +752,9 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                 }
             }
             // pre-smooth sweep 1: x3 row ii-3
-            const V2<T> g2 = js<MODE, T, EDGE>(c0, c1, c2, f3, hh, k, boundary_row(ii - 3, N));
+            const V2<T> g2 = jsn<MODE, T, EDGE>(c0, c1, c2, nc1, fq3, hh, k, boundary_row(ii - 3, N));
             {   // pre check: r(x3) on row ii-4
-                const V2<T> r3 = rs<MODE, T>(g0, g1, g2, f4, ih);
+                const V2<T> r3 = rsn<MODE, T>(g0, g1, g2, ng1, fq4, ih);
                 const int row = ii - 4;
                 if (row >= olo && row < ohi && k.own) {
                     acc2 = sqacc(acc2, r3.x);
@@ -697,16 +762,17 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                 }
             }
             // pre-smooth sweep 2: x4 row ii-4 (stored)
-            const V2<T> h2 = js<MODE, T, EDGE>(g0, g1, g2, f4, hh, k, boundary_row(ii - 4, N));
+            const V2<T> h2 = jsn<MODE, T, EDGE>(g0, g1, g2, ng1, fq4, hh, k, boundary_row(ii - 4, N));
             if (ii - 4 >= olo && ii - 4 < ohi && k.own) stv(O + (ii - 4) * P, h2);
             // r(x4) on row ii-5
-            const V2<T> d2 = rs<MODE, T>(h0, h1, h2, f5, ih);
+            const V2<T> d2 = rsn<MODE, T>(h0, h1, h2, nbr<T>(h1), fq5, ih);
             // restriction: rows ii-7, ii-6, ii-5 = 2jc-1, 2jc, 2jc+1 when ii is even
             if ((s & 1) == 0) {
                 const int jc = (ii - 6) >> 1;
                 const T m2 = dpp_shl(d1.x);
-                const T u2 = dpp_shl(d0.x);
+                const T u2 = wprev;               // = dpp_shl(d0.x): row ii-7 was d2 two rows ago
                 const T w2 = dpp_shl(d2.x);
+                wprev = w2;
                 const int ic = (k.c + 1) >> 1;
                 if (jc >= clo && jc < chi && k.own && ic <= Nc - 2) {
                     const T v = T(0.25) * d1.y + T(0.125) * (m2 + d1.x + d2.y + d0.y) +
@@ -720,7 +786,9 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
             g0 = g1; g1 = g2;
             h0 = h1; h1 = h2;
             d0 = d1; d1 = d2;
-            f5 = f4; f4 = f3; f3 = f2; f2 = f1; f1 = f0;
+            if constexpr (!GENF || !FRECOMP) {
+                f5 = f4; f4 = f3; f3 = f2; f2 = f1; f1 = f0;
+            }
         }
         if (gi + 1 < ng) store_pair(gi + 1, px, pf, pe);
         if (gi + 1 + D < ng) load_pair(gi + 1 + D, px, pf, pe);
@@ -754,7 +822,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
 }
 
 
-template <class T, bool R2, bool GENF, int D = 2, int OCC = 1, int MODE = 0>
+template <class T, bool R2, bool GENF, int D = 2, int OCC = 1, int MODE = 0, bool FRECOMP = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC)))
 void k_postpre_lds(PostPreArgsT<T> a)
 {
@@ -768,9 +836,9 @@ void k_postpre_lds(PostPreArgsT<T> a)
     const int jce = min(jcb + a.rows_per_block, a.jc1);
     const bool edge_rows = 2 * jcb - 6 <= 0 || 2 * jce + 6 >= a.N - 1;
     if (k.edge || edge_rows)
-        postpre_lds_run<T, R2, GENF, D, MODE, true>(a, k, red, sx, sf, se);
+        postpre_lds_run<T, R2, GENF, D, MODE, true, FRECOMP>(a, k, red, sx, sf, se);
     else
-        postpre_lds_run<T, R2, GENF, D, MODE, false>(a, k, red, sx, sf, se);
+        postpre_lds_run<T, R2, GENF, D, MODE, false, FRECOMP>(a, k, red, sx, sf, se);
 }
 
 // one block: both decisions, stats, flags for the conditional rare-path kernels
@@ -829,14 +897,14 @@ static int env_int(const char *name, int dflt)
 }
 
 static void fused_geometry(int N, int jc0, int jc1, int *threads, int *gx, int *gy, int *rpb,
-                           int stride = 120)
+                           int stride = 120, int target = 0)
 {
     const int waves = (N - 2 + stride - 1) / stride;
     const int wpb = waves < 4 ? waves : 4;
     *threads = 64 * wpb;
     *gx = (waves + wpb - 1) / wpb;
     const int rows = jc1 - jc0;   // coarse rows
-    const int target = env_int("PGMG_FUSED_BLOCKS", 2048);  // tuned r01: tune_fused.py
+    if (target <= 0) target = env_int("PGMG_FUSED_BLOCKS", 2048);  // tuned r01: tune_fused.py
     const int rmin = env_int("PGMG_FUSED_MIN_ROWS", 8);
     const int rmax = env_int("PGMG_FUSED_MAX_ROWS", 512);
     int r = (int)(((long long)rows * *gx + target - 1) / target);
@@ -868,7 +936,9 @@ void launch_pre(const PreArgsT<T> &a0, bool x0_zero, bool fine, hipStream_t s)
     const dim3 g(gx, gy), b(t);
     if (fused_pairs() == 2) {
         if (x0_zero) k_pre<T, true, false, 2><<<g, b, 0, s>>>(a);
+        else if (fine && a.gfx != nullptr) k_pre<T, false, true, 2, true><<<g, b, 0, s>>>(a);
         else if (fine) k_pre<T, false, true, 2><<<g, b, 0, s>>>(a);
+        else if (a.gfx != nullptr) k_pre<T, false, false, 2, true><<<g, b, 0, s>>>(a);
         else k_pre<T, false, false, 2><<<g, b, 0, s>>>(a);
     } else {
         if (x0_zero) k_pre<T, true, false, 1><<<g, b, 0, s>>>(a);
@@ -887,8 +957,10 @@ void launch_post(const PostArgsT<T> &a0, bool fine, hipStream_t s)
     const dim3 g(gx, gy), b(t);
     const bool rec = a.pre_fired != nullptr;
     if (fused_pairs() == 2) {
-        if (fine) k_post<T, true, 2, false><<<g, b, 0, s>>>(a);
+        if (fine && a.gfx != nullptr) k_post<T, true, 2, false, true><<<g, b, 0, s>>>(a);
+        else if (fine) k_post<T, true, 2, false><<<g, b, 0, s>>>(a);
         else if (rec) k_post<T, false, 2, true><<<g, b, 0, s>>>(a);
+        else if (a.gfx != nullptr) k_post<T, false, 2, false, true><<<g, b, 0, s>>>(a);
         else k_post<T, false, 2, false><<<g, b, 0, s>>>(a);
     } else {
         if (fine) k_post<T, true, 1, false><<<g, b, 0, s>>>(a);
@@ -897,10 +969,15 @@ void launch_post(const PostArgsT<T> &a0, bool fine, hipStream_t s)
     }
 }
 
+// k_postpre's grid target: 3072 workgroups = 6 full rounds of the 512 that are resident
+// at once (2 per CU at its ~200 VGPRs); measured r01 against 2048 .. 8192
+// (PGMG_PP_BLOCKS): 2048 1.30 ms, 3072 1.18 ms, 4096 1.25 ms, 8192 1.28 ms at N = 16385.
+static int pp_target() { return env_int("PGMG_PP_BLOCKS", 3072); }
+
 int postpre_blocks(int N, int jc0, int jc1)
 {
     int t, gx, gy, r;
-    fused_geometry(N, jc0, jc1, &t, &gx, &gy, &r, kPPStride);
+    fused_geometry(N, jc0, jc1, &t, &gx, &gy, &r, kPPStride, pp_target());
     return gx * gy;
 }
 
@@ -911,7 +988,8 @@ void launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
 {
     int t, gx, gy, r;
     const int variant = std::is_same<T, double>::value ? env_int("PGMG_PP_VARIANT", 0) : 0;
-    fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, variant == 3 ? 128 : kPPStride);
+    fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, variant == 3 ? 128 : kPPStride,
+                   pp_target());
     PostPreArgsT<T> a = a0;
     a.rows_per_block = r;
     const dim3 g(gx, gy), b(t);
@@ -930,6 +1008,10 @@ void launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
         const int mode = env_int("PGMG_PP_LDS_MODE", 0);
         if (genf && a.partials3 == nullptr && mode == 1) {
             k_postpre_lds<T, false, true, 2, 1, 1><<<g, b, 0, s>>>(a);
+            return;
+        }
+        if (genf && a.partials3 == nullptr && mode == 2) {   // f regenerated at every use
+            k_postpre_lds<T, false, true, 2, 1, 0, true><<<g, b, 0, s>>>(a);
             return;
         }
         if (genf && a.partials3 == nullptr && (depth != 2 || occ != 1)) {

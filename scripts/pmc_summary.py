@@ -27,14 +27,16 @@ def norm_name(n):
     t = (m.group(2) or "").replace(" ", "")
     # drop the prefetch-depth template argument (last int) for k_pre/k_post
     t = re.sub(r",\d+>$", ">", t)
+    if m.group(1) == "k_postpre_lds":   # <T, R2, GENF, depth, occupancy, mode, frecomp>
+        t = "<" + ",".join(t.strip("<>").split(",")[:3]) + ">"
     return m.group(1) + t
 
 
 def is_finest(k):
     """Finest-level kernel symbols (normalised): k_postpre*, k_pre<T,false,true>,
     k_post<T,true,PAIRS,false>, k_sweep<T,X0,NORM,true>."""
-    return bool(k.startswith("k_postpre") or re.match(r"k_pre<\w+,false,true>$", k) or
-                re.match(r"k_post<\w+,true,\d+,false>$", k) or
+    return bool(k.startswith("k_postpre") or re.match(r"k_pre<\w+,false,true[,>]", k) or
+                re.match(r"k_post<\w+,true,\d+,false[,>]", k) or
                 re.match(r"k_sweep<\w+,\w+,\w+,true>$", k))
 
 
