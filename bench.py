@@ -41,19 +41,21 @@ def parse():
                     help="events: eager launches with hipEvents around every fine sweep")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-n", type=int, default=0, help="grid for the CPU sample (default = --n)")
+    ap.add_argument("--cycle", choices=["V", "W", "F"], default="V",
+                    help="V (the headline), W (alpha=3 recursions) or F (full multigrid) cycles")
     ap.add_argument("--dtype", choices=["f64", "f32"], default="f64",
                     help="f64: the reference's precision (the headline); f32: the fp32 variant")
     return ap.parse_args()
 
 
-def cpu_baseline(n, cycles=1):
+def cpu_baseline(n, cycles=1, kind="V"):
     """The oracle (our C restatement of mg_cpu_exec, 1 thread) on the host: a bounded
-    sample of the same workload (one V-cycle at the same N)."""
+    sample of the same workload (one cycle of the same kind at the same N)."""
     exe = ROOT / "oracle" / "mg_cpu_exec_port"
     if not exe.exists():
         subprocess.run(["make", "-C", str(ROOT / "oracle"), "-s",
                         str(exe)], check=True, capture_output=True)
-    cmd = [str(exe), "V", str(n), str(cycles), "1e-7"]
+    cmd = [str(exe), kind, str(n), str(cycles), "1e-7"]
     if shutil.which("taskset"):
         cmd = ["taskset", "-c", "0"] + cmd
     out = subprocess.run(cmd, check=True, capture_output=True, text=True).stdout
@@ -67,9 +69,9 @@ def cpu_baseline(n, cycles=1):
                 break
     except OSError:
         pass
-    return {"value": round(1.0 / t, 6), "unit": "V-cycles/s", "cores": 1, "kind": "port",
-            "sample": f"{cycles} V-cycle(s) at N={n}, phi0=0, analytic f; oracle/mg_cpu_exec_port "
-                      f"-O2 single thread (taskset -c 0); {t:.2f} s per V-cycle; host {model}"}
+    return {"value": round(1.0 / t, 6), "unit": f"{kind}-cycles/s", "cores": 1, "kind": "port",
+            "sample": f"{cycles} {kind}-cycle(s) at N={n}, phi0=0, analytic f; oracle/mg_cpu_exec_port "
+                      f"-O2 single thread (taskset -c 0); {t:.2f} s per {kind}-cycle; host {model}"}
 
 
 def pmc_traffic(n, key):
@@ -99,7 +101,7 @@ def main():
     cpu = None
     if world == 1 and rank == 0 and args.cpu_baseline == "auto" and args.dtype == "f64":
         try:
-            cpu = cpu_baseline(args.cpu_n or args.n)
+            cpu = cpu_baseline(args.cpu_n or args.n, kind=args.cycle)
         except Exception as e:  # reported, not fatal
             cpu = {"value": None, "unit": "V-cycles/s", "cores": 1, "kind": "port",
                    "sample": f"failed: {e}"}
@@ -130,14 +132,15 @@ def main():
             dist.barrier()
 
     # warmup (also builds the hipGraph in graph mode)
-    s.vcycle(max(args.warmup, 0))
+    run = {"V": s.vcycle, "W": s.wcycle, "F": s.fcycle}[args.cycle]
+    run(max(args.warmup, 0))
     s.sync()
     for w in (0, 1, 2, 3):  # drop warmup events
         s.fine_pass_time(w)
     barrier()
     s.sync()
     t0 = time.perf_counter()
-    s.vcycle(args.steps)
+    run(args.steps)
     s.sync()
     barrier()
     t1 = time.perf_counter()
@@ -194,10 +197,13 @@ def main():
 
     if rank == 0:
         value = args.steps / dt
+        metric = METRIC if args.dtype == "f64" else METRIC.replace(", fp64", ", fp32 variant")
+        if args.cycle != "V":
+            metric = metric.replace("V-cycles/sec", f"{args.cycle}-cycles/sec")
         line = {
-            "metric": METRIC if args.dtype == "f64" else METRIC.replace(", fp64", ", fp32 variant"),
+            "metric": metric,
             "value": round(value, 4),
-            "unit": "V-cycles/s",
+            "unit": f"{args.cycle}-cycles/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -208,7 +214,7 @@ def main():
             "dtype": args.dtype,
             "data": "synthetic: the reference's own problem, phi0=0, f=2*pi^2*sin(pi x)sin(pi y)",
             "config": {
-                "workload": f"V-cycle N={n} ({n - 1}^2 cells), 2+2 Jacobi (v1=v2=1), 11 coarsest "
+                "workload": f"{args.cycle}-cycle N={n} ({n - 1}^2 cells), 2+2 Jacobi (v1=v2=1), 11 coarsest "
                             f"sweeps, eps=1e-7 early exit, {bulk} bulk levels + one-workgroup LDS "
                             f"tail from N={tail_top} to N=5",
                 "N": n, "bulk_levels": bulk, "tail_top": tail_top,

@@ -96,8 +96,7 @@ __device__ __forceinline__ Cols lane_cols(int N) { return lane_cols_t<120, 4>(N)
 // deterministic sum over the block (fixed tree) -> thread 0
 __device__ __forceinline__ double fused_block_sum(double v, double *red)
 {
-    #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    v = wave_sum(v);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
     double s = 0.0;

@@ -11,8 +11,7 @@ namespace pgmg {
 template <int NT>
 __device__ __forceinline__ double gblock_sum(double v, double *red)
 {
-    #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    v = wave_sum(v);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
     double s = 0.0;

@@ -22,8 +22,7 @@ namespace pgmg {
 template <int NT>
 __device__ __forceinline__ double block_sum(double v, double *red)
 {
-    #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    v = wave_sum(v);
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) red[w] = v;
     __syncthreads();

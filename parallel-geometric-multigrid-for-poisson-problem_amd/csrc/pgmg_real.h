@@ -60,6 +60,35 @@ __device__ __forceinline__ double dpp_shl(double v)
 __device__ __forceinline__ float dpp_shr(float v) { return __int_as_float(dpp_shr_i(__float_as_int(v))); }
 __device__ __forceinline__ float dpp_shl(float v) { return __int_as_float(dpp_shl_i(__float_as_int(v))); }
 
+// Sum of one double over the 64 lanes of a wave, returned (bitwise identical) in every
+// lane.  DPP row_shr:1,2,4,8 (a Hillis-Steele scan inside each row of 16 lanes, VALU
+// latency only) then the four row totals read out with v_readlane: ~10 dependent VALU
+// ops instead of six __shfl_xor rounds through the LDS crossbar (ds_bpermute, ~100+
+// cycles each), which dominated the per-sweep cost of the LDS tail.  All 64 lanes must
+// be active.
+template <int CTRL> __device__ __forceinline__ double dpp64(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, true);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double readlane64(double v, int lane)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, lane);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double wave_sum(double v)
+{
+    v += dpp64<0x111>(v);   // row_shr:1
+    v += dpp64<0x112>(v);   // row_shr:2
+    v += dpp64<0x114>(v);   // row_shr:4
+    v += dpp64<0x118>(v);   // row_shr:8  -> lane 16r+15 holds the total of row r
+    return (readlane64(v, 15) + readlane64(v, 31)) + (readlane64(v, 47) + readlane64(v, 63));
+}
+
 // elements between an allocation's base and element (0,0): column 1 of every row on a
 // 128-byte boundary (15 doubles, 31 floats)
 template <class T> constexpr int off_elems() { return 128 / (int)sizeof(T) - 1; }

@@ -10,18 +10,22 @@
 // Semantics are exactly MultigridSolver::v_cycle / w_cycle (MultiGrid.hpp:57-136)
 // with JacobiSmoother::smooth (Smoother.hpp:38-116), including the per-sweep
 // residual-norm early exit, evaluated sequentially (no speculation needed here).
+#include <cstdlib>
+
 #include "pgmg_internal.h"
 
 namespace pgmg {
 
 constexpr int kTailMaxLevels = 8;
-constexpr int kTailRed = kTailThreads / 64 + 2;  // doubles of reduction scratch at the LDS base
+constexpr int kTailWaves = kTailThreads / 64;
+constexpr int kTailRed = 2 * kTailWaves + 2;  // doubles of reduction scratch at the LDS base
 
 template <class Real>
 struct TailLevel {
     int N;
     int off;         // offset of this level's E and F grids (pitch N, no padding)
     Real hh, ih;     // h*h and 1.0/(h*h) rounded on the host
+    float rN;        // 1.0f / N: row of a flat index k as int((k + 0.5f) * rN), exact for N <= 65
 };
 
 template <class Real>
@@ -31,36 +35,62 @@ struct TailArgsDev {
     int S;           // elements per pyramid
     TailLevel<Real> lv[kTailMaxLevels];
     int gamma;
+    int wave_n;      // levels with N <= wave_n run on wave 0 alone (no workgroup barriers)
 };
 
-__device__ __forceinline__ double tail_sum(double v, double *red)
-{
-    #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) red[w] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
+// Two execution teams for the same level code.  BlockTeam: the whole 1024-thread
+// workgroup, stages separated by __syncthreads.  WaveTeam: wave 0 alone; LDS operations
+// of one wavefront are performed in program order (AMDGPU memory model), so a stage
+// boundary only has to stop the compiler from moving LDS accesses across it.  The deep,
+// tiny levels of a W-cycle (3^l visits of a few hundred points) run as a WaveTeam: a
+// stage there costs a few dozen cycles instead of a 16-wave barrier.
+struct BlockTeam {
+    static constexpr int size = kTailThreads;
+    __device__ static int tid() { return threadIdx.x; }
+    __device__ static void sync() { __syncthreads(); }
+    // deterministic total of one double per thread (wave sums in wave order), valid in
+    // every thread; one barrier, alternating scratch halves (par)
+    __device__ static double sum(double v, double *red, int &par)
+    {
+        v = wave_sum(v);
+        double *r = red + par * kTailWaves;
+        if ((threadIdx.x & 63) == 0) r[threadIdx.x >> 6] = v;
+        __syncthreads();
         double s = 0.0;
         #pragma unroll
-        for (int i = 0; i < kTailThreads / 64; ++i) s += red[i];
-        red[kTailThreads / 64] = s;
+        for (int i = 0; i < kTailWaves; ++i) s += r[i];
+        par ^= 1;
+        return s;
     }
-    __syncthreads();
-    const double s = red[kTailThreads / 64];
-    __syncthreads();
-    return s;
-}
+};
+
+struct WaveTeam {
+    static constexpr int size = 64;
+    __device__ static int tid() { return threadIdx.x & 63; }
+    __device__ static void sync()
+    {
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __builtin_amdgcn_wave_barrier();
+    }
+    __device__ static double sum(double v, double *, int &)
+    {
+        v = wave_sum(v);
+        return v;
+    }
+};
+
+__device__ __forceinline__ int tail_row(int k, float rN) { return (int)(((float)k + 0.5f) * rN); }
 
 // out = J(cur) on all points (boundary copied); optionally sum r(cur)^2
-template <class Real, bool NORM>
-__device__ __forceinline__ double tail_jacobi(const Real *cur, Real *out, const Real *f, int N,
-                                              Real hh, Real ih)
+template <class Team, class Real, bool NORM>
+__device__ __forceinline__ double tail_jacobi(const Real *cur, Real *out, const Real *f,
+                                              const TailLevel<Real> &L)
 {
     double acc = 0.0;
-    const int n = N * N;
-    for (int k = threadIdx.x; k < n; k += kTailThreads) {
-        const int j = k / N;
+    const int N = L.N, n = N * N;
+    const Real hh = L.hh, ih = L.ih;
+    for (int k = Team::tid(); k < n; k += Team::size) {
+        const int j = tail_row(k, L.rN);
         const int i = k - j * N;
         if (i == 0 || j == 0 || i == N - 1 || j == N - 1) {
             out[k] = cur[k];
@@ -79,21 +109,22 @@ __device__ __forceinline__ double tail_jacobi(const Real *cur, Real *out, const 
 // JacobiSmoother::smooth(x, f, N, N, h, num_iter): num_iter+1 sweeps, break as
 // soon as ||r(x_k)|| < eps.  The check of x_k is fused into sweep k+1 (which
 // reads the same neighbourhood); when it fires, sweep k+1's output is dropped.
-template <class Real>
+template <class Team, class Real>
 __device__ void tail_smooth(Real *x, const Real *f, const TailLevel<Real> &L, int num_iter,
-                            double eps, Real *T, double *red, long long &sweeps,
+                            double eps, Real *T, double *red, int &par, long long &sweeps,
                             long long &exits)
 {
     Real *cur = x, *oth = T;
-    tail_jacobi<Real, false>(cur, oth, f, L.N, L.hh, L.ih);
-    __syncthreads();
+    tail_jacobi<Team, Real, false>(cur, oth, f, L);
+    Team::sync();
     Real *tmp = cur;
     cur = oth;
     oth = tmp;
     ++sweeps;
     for (int k = 2; k <= num_iter + 1; ++k) {
-        const double acc = tail_jacobi<Real, true>(cur, oth, f, L.N, L.hh, L.ih);
-        const double s = tail_sum(acc, red);   // also orders the writes of oth
+        const double acc = tail_jacobi<Team, Real, true>(cur, oth, f, L);
+        const double s = Team::sum(acc, red, par);   // also orders the writes of oth
+        if (Team::size != kTailThreads) Team::sync();  // (the block sum has its barrier)
         if (sqrt(s) < eps) {
             ++exits;
             break;
@@ -105,19 +136,19 @@ __device__ void tail_smooth(Real *x, const Real *f, const TailLevel<Real> &L, in
     }
     if (cur != x) {
         const int n = L.N * L.N;
-        for (int k = threadIdx.x; k < n; k += kTailThreads) x[k] = cur[k];
+        for (int k = Team::tid(); k < n; k += Team::size) x[k] = cur[k];
     }
-    __syncthreads();
+    Team::sync();
 }
 
 // T = r(x) on the interior, 0 on the boundary; then fc = R T (MultiGrid.hpp:70-78)
-template <class Real>
+template <class Team, class Real>
 __device__ void tail_res_restrict(const Real *x, const Real *f, const TailLevel<Real> &Lf, Real *fc,
                                   Real *ec, const TailLevel<Real> &Lc, Real *T)
 {
     const int N = Lf.N, n = N * N;
-    for (int k = threadIdx.x; k < n; k += kTailThreads) {
-        const int j = k / N;
+    for (int k = Team::tid(); k < n; k += Team::size) {
+        const int j = tail_row(k, Lf.rN);
         const int i = k - j * N;
         if (i == 0 || j == 0 || i == N - 1 || j == N - 1) {
             T[k] = Real(0);
@@ -125,10 +156,10 @@ __device__ void tail_res_restrict(const Real *x, const Real *f, const TailLevel<
         }
         T[k] = f[k] - Lf.ih * (Real(4) * x[k] - x[k - 1] - x[k + 1] - x[k - N] - x[k + N]);
     }
-    __syncthreads();
+    Team::sync();
     const int Nc = Lc.N, nc = Nc * Nc;
-    for (int q = threadIdx.x; q < nc; q += kTailThreads) {
-        const int jc = q / Nc;
+    for (int q = Team::tid(); q < nc; q += Team::size) {
+        const int jc = tail_row(q, Lc.rN);
         const int ic = q - jc * Nc;
         ec[q] = Real(0);  // MultiGrid.hpp:81-82 e_coarse = 0
         if (ic == 0 || jc == 0 || ic == Nc - 1 || jc == Nc - 1) continue;
@@ -136,17 +167,17 @@ __device__ void tail_res_restrict(const Real *x, const Real *f, const TailLevel<
         fc[q] = Real(0.25) * T[k] + Real(0.125) * (T[k + 1] + T[k - 1] + T[k + N] + T[k - N]) +
                 Real(0.0625) * (T[k - N - 1] + T[k - N + 1] + T[k + N - 1] + T[k + N + 1]);
     }
-    __syncthreads();
+    Team::sync();
 }
 
 // x += P e (MultiGrid.hpp:208-226): fine points in [2, Nf-2]^2 only
-template <class Real>
+template <class Team, class Real>
 __device__ void tail_prolong(Real *x, const TailLevel<Real> &Lf, const Real *e,
                              const TailLevel<Real> &Lc)
 {
     const int N = Lf.N, Nc = Lc.N, n = N * N;
-    for (int k = threadIdx.x; k < n; k += kTailThreads) {
-        const int j = k / N;
+    for (int k = Team::tid(); k < n; k += Team::size) {
+        const int j = tail_row(k, Lf.rN);
         const int i = k - j * N;
         if (i < 2 || j < 2 || i > N - 2 || j > N - 2) continue;
         const int jc = j >> 1, ic = i >> 1;
@@ -161,43 +192,61 @@ __device__ void tail_prolong(Real *x, const TailLevel<Real> &Lf, const Real *e,
         }
         x[k] = x[k] + v;
     }
-    __syncthreads();
+    Team::sync();
 }
 
-// gamma-cycle (MultiGrid.hpp:57-136) whose top is tail level `top`; levels top.. last
-template <class Real>
-__device__ void tail_gcycle(const TailArgsDev<Real> &d, int top, Real *E, Real *F, Real *T,
-                            double *red, long long &sweeps, long long &exits)
+// `reps` gamma-cycles (MultiGrid.hpp:57-136) whose top is tail level `top`; levels
+// top .. last.  A BlockTeam hands every sub-hierarchy whose top has N <= wave_n to wave 0
+// (all gamma visits of it at once) and waits at a barrier.
+template <class Team, class Real>
+__device__ void tail_gcycle(const TailArgsDev<Real> &d, int top, int reps, Real *E, Real *F,
+                            Real *T, double *red, int &par, long long &sweeps, long long &exits)
 {
+    constexpr bool kBlock = Team::size == kTailThreads;
     const TailArgsT<Real> &a = d.a;
     int visits[kTailMaxLevels];
     for (int i = 0; i < kTailMaxLevels; ++i) visits[i] = 0;
-    int l = top;
+    int l = top, done = 0;
     bool descending = true;
     const int last = d.nl - 1;
     for (;;) {
         if (descending) {
+            if (kBlock && l != top && d.lv[l].N <= d.wave_n) {
+                // the whole gamma-recursion of level l on wave 0
+                if (threadIdx.x < 64)
+                    tail_gcycle<WaveTeam, Real>(d, l, d.gamma, E, F, T, red, par, sweeps, exits);
+                __syncthreads();
+                visits[l] = d.gamma - 1;
+                descending = false;
+                continue;
+            }
             if (l == last) {
-                tail_smooth(E + d.lv[l].off, F + d.lv[l].off, d.lv[l], a.coarse_iter, a.eps, T,
-                            red, sweeps, exits);
+                tail_smooth<Team>(E + d.lv[l].off, F + d.lv[l].off, d.lv[l], a.coarse_iter, a.eps, T,
+                                  red, par, sweeps, exits);
                 descending = false;
             } else {
-                tail_smooth(E + d.lv[l].off, F + d.lv[l].off, d.lv[l], a.v1, a.eps, T, red,
-                            sweeps, exits);
-                tail_res_restrict(E + d.lv[l].off, F + d.lv[l].off, d.lv[l], F + d.lv[l + 1].off,
-                                  E + d.lv[l + 1].off, d.lv[l + 1], T);
+                tail_smooth<Team>(E + d.lv[l].off, F + d.lv[l].off, d.lv[l], a.v1, a.eps, T, red,
+                                  par, sweeps, exits);
+                tail_res_restrict<Team>(E + d.lv[l].off, F + d.lv[l].off, d.lv[l],
+                                        F + d.lv[l + 1].off, E + d.lv[l + 1].off, d.lv[l + 1], T);
                 visits[l + 1] = 0;
                 ++l;
             }
         } else {
-            if (l == top) break;
+            if (l == top) {
+                if (++done < reps) {
+                    descending = true;   // the caller's next visit of the top level
+                    continue;
+                }
+                break;
+            }
             const int p = l - 1;
             if (++visits[l] < d.gamma) {
                 descending = true;   // call the cycle on level l again
             } else {
-                tail_prolong(E + d.lv[p].off, d.lv[p], E + d.lv[l].off, d.lv[l]);
-                tail_smooth(E + d.lv[p].off, F + d.lv[p].off, d.lv[p], a.v2, a.eps, T, red,
-                            sweeps, exits);
+                tail_prolong<Team>(E + d.lv[p].off, d.lv[p], E + d.lv[l].off, d.lv[l]);
+                tail_smooth<Team>(E + d.lv[p].off, F + d.lv[p].off, d.lv[p], a.v2, a.eps, T, red,
+                                  par, sweeps, exits);
                 l = p;
             }
         }
@@ -264,9 +313,10 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(TailArgsDev<Real> d)
     __syncthreads();
 
     long long sweeps = 0, exits = 0;
+    int par = 0;
     const int last = d.nl - 1;
     if (!a.fmg) {
-        tail_gcycle(d, 0, E, F, T, red, sweeps, exits);
+        tail_gcycle<BlockTeam>(d, 0, 1, E, F, T, red, par, sweeps, exits);
     } else {
         // compute_coarsest_grid: restrict phi down to the coarsest level
         for (int t = 0; t < last; ++t)
@@ -279,13 +329,13 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(TailArgsDev<Real> d)
                 const int n = d.lv[t].N * d.lv[t].N;
                 for (int k = threadIdx.x; k < n; k += kTailThreads) Et[k] = Real(0);
                 __syncthreads();
-                tail_prolong(Et, d.lv[t], E + d.lv[t + 1].off, d.lv[t + 1]);   // :164
-                tail_gcycle(d, t, E, F, T, red, sweeps, exits);              // :167 v_cycle
+                tail_prolong<BlockTeam>(Et, d.lv[t], E + d.lv[t + 1].off, d.lv[t + 1]);   // :164
+                tail_gcycle<BlockTeam>(d, t, 1, E, F, T, red, par, sweeps, exits);  // :167 v_cycle
             } else {
                 __syncthreads();
             }
             if (t > 0 || a.fmg_smooth_top)                                   // :153 smooth(3)
-                tail_smooth(Et, Ft, d.lv[t], 3, a.eps, T, red, sweeps, exits);
+                tail_smooth<BlockTeam>(Et, Ft, d.lv[t], 3, a.eps, T, red, par, sweeps, exits);
         }
     }
 
@@ -332,6 +382,7 @@ hipError_t launch_tail_gamma(const TailArgsT<Real> &a, int gamma, hipStream_t s)
         d.lv[nl].off = off;
         d.lv[nl].hh = (Real)(h * h);
         d.lv[nl].ih = (Real)(1.0 / (h * h));
+        d.lv[nl].rN = 1.0f / (float)N;
         off += N * N;
         if (N <= a.n_coarse) {
             ++nl;
@@ -342,6 +393,13 @@ hipError_t launch_tail_gamma(const TailArgsT<Real> &a, int gamma, hipStream_t s)
     }
     d.nl = nl;
     d.S = off;
+    {
+        static const int wave_n = [] {
+            const char *v = getenv("PGMG_TAIL_WAVE_N");
+            return (v && *v) ? atoi(v) : 17;
+        }();
+        d.wave_n = wave_n;
+    }
     const size_t bytes = tail_lds_bytes<Real>(a.N_top, a.n_coarse);
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute((const void *)k_tail<Real>,
