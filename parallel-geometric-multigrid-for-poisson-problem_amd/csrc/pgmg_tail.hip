@@ -396,7 +396,7 @@ hipError_t launch_tail_gamma(const TailArgsT<Real> &a, int gamma, hipStream_t s)
     {
         static const int wave_n = [] {
             const char *v = getenv("PGMG_TAIL_WAVE_N");
-            return (v && *v) ? atoi(v) : 17;
+            return (v && *v) ? atoi(v) : 9;
         }();
         d.wave_n = wave_n;
     }
