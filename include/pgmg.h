@@ -80,6 +80,10 @@ extern "C" {
                                     analytic RHS (set_problem f = NULL), the finest-level
                                     cross-cycle pass regenerates it in-kernel from two
                                     sine tables (bitwise the same values, 8 B/pt less) */
+#define PGMG_FLAG_EXACT_DIST 64u /* row strips: decide every smoother early-exit check of a
+                                    distributed level with its own allreduce instead of
+                                    speculatively (validated once per call, rollback on
+                                    doubt; same results)                              */
 #define PGMG_FLAG_LOOPBACK 8u    /* world > 1 with ranks as threads of one process on
                                     one GPU: nccl_unique_id is a pgmg_loopback hub
                                     (test transport for the strip decomposition)    */
@@ -161,6 +165,10 @@ int pgmg_phi_device(pgmg_ctx *ctx, double **ptr, int *pitch, int *row0, int *row
  * (24 B per fine point for x, f -> x; +8 B per coarse point per coarse array; 16 B when
  * k_postpre regenerates the analytic f in-kernel), times elem_bytes / 8. */
 int pgmg_fine_pass_bytes(pgmg_ctx *ctx, int pass, double *bytes);
+
+/* Row strips: whether the early-exit checks are decided speculatively (1) or with one
+ * allreduce each (0), and how many calls had to be rolled back and rerun exactly. */
+int pgmg_dist_info(pgmg_ctx *ctx, int *speculative, long long *rollbacks);
 
 /* The context's PGMG_PRECISION_* and its grid element size in bytes (8 or 4). */
 int pgmg_precision(pgmg_ctx *ctx, int *precision, int *elem_bytes);

@@ -27,6 +27,7 @@ PGMG_FLAG_UNFUSED = 4
 PGMG_FLAG_LOOPBACK = 8
 PGMG_FLAG_NO_CROSS = 16
 PGMG_FLAG_STORED_RHS = 32
+PGMG_FLAG_EXACT_DIST = 64
 
 PGMG_PRECISION_FP64 = 0
 PGMG_PRECISION_FP32 = 1
@@ -81,6 +82,7 @@ SIGNATURES = [
     ("pgmg_fused", C.c_int, [_P, C.POINTER(C.c_int)]),
     ("pgmg_precision", C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("pgmg_fine_pass_bytes", C.c_int, [_P, C.c_int, _DP]),
+    ("pgmg_dist_info", C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_longlong)]),
     ("pgmg_bench_sweep", C.c_int, [_P, C.c_int, _DP]),
     ("pgmg_jacobi", C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_double, C.c_int, C.c_double,
                               C.POINTER(C.c_int), _P]),

@@ -58,6 +58,7 @@ class Transport {
     virtual int recv(void *buf, size_t bytes, int peer, hipStream_t s) = 0;
     virtual int group_end(hipStream_t s) = 0;
     virtual int allreduce_sum(double *d, int n, hipStream_t s) = 0;
+    virtual int allreduce_min_u32(unsigned *d, int n, hipStream_t s) = 0;
 };
 
 class RcclTransport : public Transport {
@@ -97,6 +98,11 @@ class RcclTransport : public Transport {
     int allreduce_sum(double *d, int n, hipStream_t s) override
     {
         NCCLC(ncclAllReduce(d, d, n, ncclDouble, ncclSum, comm, s));
+        return PGMG_OK;
+    }
+    int allreduce_min_u32(unsigned *d, int n, hipStream_t s) override
+    {
+        NCCLC(ncclAllReduce(d, d, n, ncclUint32, ncclMin, comm, s));
         return PGMG_OK;
     }
 };
@@ -206,6 +212,28 @@ class LoopbackTransport : public Transport {
         }
         pend.clear();
         return PGMG_OK;
+    }
+    int allreduce_min_u32(unsigned *d, int n, hipStream_t s) override
+    {
+        // through the double rendezvous: values 0/1 (exact in double), min = -sum(-x)...
+        // simplest exact form: each rank contributes x, the minimum of 0/1 flags over the
+        // world is 1 iff their sum equals the world size
+        std::vector<unsigned> u(n);
+        PGMG_HIPC(hipMemcpyAsync(u.data(), d, n * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+        PGMG_HIPC(hipStreamSynchronize(s));
+        double *tmp = nullptr;
+        PGMG_HIPC(hipMalloc((void **)&tmp, n * sizeof(double)));
+        std::vector<double> v(u.begin(), u.end());
+        for (auto &x : v) x = x ? 1.0 : 0.0;
+        PGMG_HIPC(hipMemcpy(tmp, v.data(), n * sizeof(double), hipMemcpyHostToDevice));
+        int e = allreduce_sum(tmp, n, s);
+        if (!e) {
+            PGMG_HIPC(hipMemcpy(v.data(), tmp, n * sizeof(double), hipMemcpyDeviceToHost));
+            for (int i = 0; i < n; ++i) u[i] = v[i] == (double)hub->world ? 1u : 0u;
+            PGMG_HIPC(hipMemcpy(d, u.data(), n * sizeof(unsigned), hipMemcpyHostToDevice));
+        }
+        (void)hipFree(tmp);
+        return e;
     }
     int allreduce_sum(double *d, int n, hipStream_t s) override
     {
@@ -320,6 +348,10 @@ class StripComm : public Comm {
     }
 
     int allreduce_sum(double *d, int n, hipStream_t s) override { return t->allreduce_sum(d, n, s); }
+    int allreduce_min_u32(unsigned *d, int n, hipStream_t s) override
+    {
+        return t->allreduce_min_u32(d, n, s);
+    }
 
     int run_gathered(pgmg_ctx *c, int l, int gamma, int repeats) override
     {

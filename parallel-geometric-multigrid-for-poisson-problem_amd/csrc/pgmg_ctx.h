@@ -25,6 +25,7 @@ int set_err(int code, const std::string &msg);
 struct Grid {
     void *base = nullptr;    // allocation
     void *o = nullptr;       // virtual origin: element (global row j, col i) at o[j*P + i]
+    size_t bytes = 0;        // allocation size
 };
 
 // typed view of a grid's origin (T = the context's element type)
@@ -88,6 +89,14 @@ struct pgmg_ctx {
     double *rhs_tab = nullptr;
     const double *gfx = nullptr, *gsy = nullptr;   // valid for indices -8 ..
     bool gen_rhs = false;
+    // row strips, speculative early-exit decisions (pgmg_ctx.hip "speculative decisions")
+    bool spec = false;            // enabled for this context (world > 1, fused cycle)
+    bool spec_now = false;        // the cycles being enqueued decide speculatively
+    unsigned *uflags = nullptr;   // one flag per distributed check of the current call
+    int uflags_cap = 0, uidx = 0;
+    pgmg::Grid bk;                // level-0 solution at the start of the call (rollback)
+    unsigned long long *stats_bk = nullptr;
+    long long rollbacks = 0;
     unsigned *ppflags = nullptr;  // k_postpre_decide flags
     pgmg::Comm *comm = nullptr;   // non-null when world > 1
     // F-cycle (pgmg_fcycle): analytic level-0 RHS of the FMG h chain, and the sine
@@ -129,6 +138,8 @@ class Comm {
     }
     // in-place sum of n device doubles over all ranks
     virtual int allreduce_sum(double *d, int n, hipStream_t s) = 0;
+    // in-place element-wise minimum of n device unsigned ints over all ranks
+    virtual int allreduce_min_u32(unsigned *d, int n, hipStream_t s) = 0;
     // the parent produced rc of gathered level l: move it to rank 0, run `repeats`
     // cycles there, bring the correction back to every rank's strip
     virtual int run_gathered(pgmg_ctx *c, int l, int gamma, int repeats) = 0;

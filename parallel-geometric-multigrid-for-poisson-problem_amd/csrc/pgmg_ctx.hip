@@ -57,6 +57,7 @@ int pgmg::alloc_grid(Grid &g, const Level &L)
         return set_err(PGMG_ERR_NOMEM, "hipMalloc failed for a level of N=" + std::to_string(L.N));
     HIPC(hipMemset(p, 0, n * L.es));
     g.base = p;
+    g.bytes = n * L.es;
     g.o = static_cast<char *>(p) + (off + (ptrdiff_t)(kHalo - L.lo) * L.P) * L.es;
     return PGMG_OK;
 }
@@ -65,6 +66,17 @@ void pgmg::free_grid(Grid &g)
 {
     if (g.base) (void)hipFree(g.base);
     g.base = g.o = nullptr;
+    g.bytes = 0;
+}
+
+// Row strips, speculative decisions: the next n flags of the current call (nullptr when
+// the cycles being enqueued decide exactly)
+static unsigned *spec_slot(pgmg_ctx *c, int n)
+{
+    if (!c->spec_now) return nullptr;
+    unsigned *p = c->uflags + c->uidx;
+    c->uidx += n;
+    return p;
 }
 
 // ---------------------------------------------------------------------------
@@ -255,8 +267,10 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
     int ev = fine ? timed_begin(c, 1) : -1;
     launch_pre(pa, x0_zero, fine, c->s);
     if ((e = timed_end(c, 1, ev))) return e;
-    if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
+    if (dist && c->spec_now) fa.spec = spec_slot(c, 1);
+    else if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
     launch_pre_fixup(fa, pa, x0_zero, c->s);
+    fa.spec = nullptr;
     if ((e = enqueue_children<T>(c, l, gamma))) return e;
     if (dist) {
         if (!recomp && (e = c->comm->halo(L.B, L, 2, c->s))) return e;
@@ -284,7 +298,8 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
     launch_post(po, fine, c->s);
     if ((e = timed_end(c, 2, ev))) return e;
     fa.global_sum = nullptr;
-    if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
+    if (dist && c->spec_now) fa.spec = spec_slot(c, 1);
+    else if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
     launch_post_fixup(fa, po, c->s);
     return PGMG_OK;
 }
@@ -406,9 +421,12 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
     int ev = timed_begin(c, 1);
     launch_pre(pa, false, true, c->s);
     if ((e = timed_end(c, 1, ev))) return e;
-    if (dist && (e = global_sum(c, np, &fa.global_sum))) return e;
+    if (dist && c->spec_now) fa.spec = spec_slot(c, 1);
+    else if (dist && (e = global_sum(c, np, &fa.global_sum))) return e;
     launch_pre_fixup(fa, pa, false, c->s);
     fa.global_sum = nullptr;
+    fa.spec = nullptr;
+    const bool spec = dist && c->spec_now;   // no rare path can run (decisions deferred)
     T *pr = B;  // pre-smoothed solution of the current cycle
     if ((e = enqueue_children<T>(c, 0, gamma))) return e;
     for (int k = 1; k < n; ++k) {
@@ -445,6 +463,13 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         launch_postpre(q, c->s);
         if ((e = timed_end(c, 3, ev))) return e;
         const double *g3 = nullptr;   // all-rank {post, pre, pre-from-x1} sums
+        if (spec) {
+            launch_postpre_decide(q.partials1, q.partials2, q.stats, npp, nullptr, c->cfg.eps,
+                                  c->ppflags, spec_slot(c, 2), c->s);
+            pr = nx;
+            if ((e = enqueue_children<T>(c, 0, gamma))) return e;
+            continue;
+        }
         if (dist) {
             launch_sum_partials(q.partials1, npp, c->scalar, c->s);
             launch_sum_partials(q.partials2, npp, c->scalar + 1, c->s);
@@ -453,7 +478,7 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
             g3 = c->scalar;
         }
         launch_postpre_decide(q.partials1, q.partials2, q.stats, npp, g3, c->cfg.eps, c->ppflags,
-                              c->s);
+                              nullptr, c->s);
         // rare path 1 (post check fired): S = x1 of the post-smooth, then a full
         // pre-smooth from S (conditional k_pre + its own fix-up)
         PostArgsT<T> po = make_post<T>(c, pr, S);
@@ -507,7 +532,8 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
     ev = timed_begin(c, 2);
     launch_post(po, true, c->s);
     if ((e = timed_end(c, 2, ev))) return e;
-    if (dist && (e = global_sum(c, np, &fa.global_sum))) return e;
+    if (spec) fa.spec = spec_slot(c, 1);
+    else if (dist && (e = global_sum(c, np, &fa.global_sum))) return e;
     launch_post_fixup(fa, po, c->s);
     if (out != A) std::swap(L.A, L.B);
     return PGMG_OK;
@@ -615,6 +641,9 @@ int pgmg_destroy(pgmg_ctx *c)
     if (c->partials2) (void)hipFree(c->partials2);
     if (c->partials3) (void)hipFree(c->partials3);
     if (c->rhs_tab) (void)hipFree(c->rhs_tab);
+    if (c->uflags) (void)hipFree(c->uflags);
+    if (c->stats_bk) (void)hipFree(c->stats_bk);
+    free_grid(c->bk);
     if (c->ppflags) (void)hipFree(c->ppflags);
     free_grid(c->S);
     free_grid(c->Ffmg);
@@ -756,6 +785,7 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         }
     }
     if (rc == PGMG_OK && c->comm) rc = c->comm->setup(c);
+    c->spec = c->comm != nullptr && c->fused && !(cfg->flags & PGMG_FLAG_EXACT_DIST);
     if (rc != PGMG_OK) {
         pgmg_destroy(c);
         return rc;
@@ -888,11 +918,8 @@ int pgmg_set_problem(pgmg_ctx *c, const double *phi0, const double *f)
     return PGMG_OK;
 }
 
-static int run_cycles(pgmg_ctx *c, int ncycles, int gamma)
+static int run_cycles_plain(pgmg_ctx *c, int ncycles, int gamma)
 {
-    if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
-    if (!c->have_problem) return set_err(PGMG_ERR_STATE, "pgmg_set_problem first");
-    if (ncycles <= 0) return PGMG_OK;
     HIPC(hipEventRecord(c->ev0, c->s));
     const bool use_graph = gamma == 1 && !(c->cfg.flags & PGMG_FLAG_NO_GRAPH) &&
                            !(c->cfg.flags & PGMG_FLAG_TIME_FINE) && c->comm == nullptr &&
@@ -930,6 +957,85 @@ static int run_cycles(pgmg_ctx *c, int ncycles, int gamma)
     }
     HIPC(hipGetLastError());
     HIPC(hipEventRecord(c->ev1, c->s));
+    return PGMG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Speculative decisions (row strips).  Every smoother early-exit check on a distributed
+// level needs the all-rank residual norm; an allreduce per check is the most latency-
+// bound operation of a cycle.  A partial sum is a lower bound of the global sum (a sum of
+// non-negative doubles never rounds below one of its terms, and sqrt is monotonic), so a
+// rank whose own partial already gives sqrt(partial) >= eps knows the global check does
+// not fire.  The cycles of a call are therefore enqueued with every distributed check
+// decided "does not fire", each rank recording whether it could NOT rule the check out
+// locally.  After the call one allreduce(min) of these flags finds the checks that no
+// rank could rule out; if there is one (never at these grid sizes in practice), the
+// call is rolled back (level-0 solution and statistics restored) and run again with exact
+// per-check allreduces.  Results are therefore identical to the exact path.
+// ---------------------------------------------------------------------------
+static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
+{
+    Level &L0 = c->lv[0];
+    // flags needed: level 0 at most 3 per cycle, level l < Ld two per visit (gamma^l)
+    long long per = 3, v = 1;
+    for (int l = 1; l < c->comm->gathered_level(); ++l) {
+        v *= gamma;
+        per += 2 * v;
+    }
+    const long long need = (long long)ncycles * (per + 2) + 16;
+    if (need > (long long)1 << 28) return run_cycles_plain(c, ncycles, gamma);
+    if (need > c->uflags_cap) {
+        HIPC(hipStreamSynchronize(c->s));
+        if (c->uflags) HIPC(hipFree(c->uflags));
+        HIPC(hipMalloc((void **)&c->uflags, (need + 1) * sizeof(unsigned)));
+        c->uflags_cap = (int)need;
+    }
+    if (!c->bk.base) {
+        int e = alloc_grid(c->bk, L0);
+        if (e) return e;
+        HIPC(hipMalloc((void **)&c->stats_bk, 4 * sizeof(unsigned long long)));
+    }
+    const Grid A0 = L0.A, B0 = L0.B;
+    HIPC(hipMemcpyAsync(c->bk.base, L0.A.base, L0.A.bytes, hipMemcpyDeviceToDevice, c->s));
+    HIPC(hipMemcpyAsync(c->stats_bk, c->stats, 4 * sizeof(unsigned long long),
+                        hipMemcpyDeviceToDevice, c->s));
+    c->uidx = 0;
+    c->spec_now = true;
+    int e = run_cycles_plain(c, ncycles, gamma);
+    c->spec_now = false;
+    if (e) return e;
+    if (c->uidx == 0) return PGMG_OK;
+    unsigned *any = c->uflags + c->uflags_cap;   // one spare slot past the flags
+    if ((e = c->comm->allreduce_min_u32(c->uflags, c->uidx, c->s))) return e;
+    launch_any_flag(c->uflags, c->uidx, any, c->s);
+    unsigned h = 0;
+    HIPC(hipMemcpyAsync(&h, any, sizeof(unsigned), hipMemcpyDeviceToHost, c->s));
+    HIPC(hipStreamSynchronize(c->s));
+    if (!h) return PGMG_OK;
+    // some check could fire: roll back and decide every check exactly
+    ++c->rollbacks;
+    L0.A = A0;
+    L0.B = B0;
+    HIPC(hipMemcpyAsync(L0.A.base, c->bk.base, L0.A.bytes, hipMemcpyDeviceToDevice, c->s));
+    HIPC(hipMemcpyAsync(c->stats, c->stats_bk, 4 * sizeof(unsigned long long),
+                        hipMemcpyDeviceToDevice, c->s));
+    return run_cycles_plain(c, ncycles, gamma);
+}
+
+static int run_cycles(pgmg_ctx *c, int ncycles, int gamma)
+{
+    if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
+    if (!c->have_problem) return set_err(PGMG_ERR_STATE, "pgmg_set_problem first");
+    if (ncycles <= 0) return PGMG_OK;
+    if (c->spec && c->comm) return run_cycles_spec(c, ncycles, gamma);
+    return run_cycles_plain(c, ncycles, gamma);
+}
+
+int pgmg_dist_info(pgmg_ctx *c, int *speculative, long long *rollbacks)
+{
+    if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
+    if (speculative) *speculative = (c->spec && c->comm) ? 1 : 0;
+    if (rollbacks) *rollbacks = c->rollbacks;
     return PGMG_OK;
 }
 

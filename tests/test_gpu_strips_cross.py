@@ -117,3 +117,59 @@ def test_strips_cross_fp32(pgmg):
     outs = _ranks(pgmg, 4, 1025, 3, gather_n=65, dtype="f32")
     for r, (phi, _) in enumerate(outs):
         assert_bitwise(phi, ref[0], f"fp32 rank {r}")
+
+
+def _ranks_info(pgmg, world, N, cycles, problem=(None, None), **cfg):
+    hub = pgmg.LoopbackHub(world)
+    out, err = [None] * world, [None] * world
+
+    def work(r):
+        try:
+            with pgmg.Solver(N, hub=hub, rank=r, **cfg) as s:
+                s.set_problem(*problem)
+                s.vcycle(cycles)
+                out[r] = (s.solution(), s.stats_detail(), s.dist_info())
+        except Exception as e:  # surfaced below
+            err[r] = e
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=600)
+    hub.close()
+    for e in err:
+        if e is not None:
+            raise e
+    return out
+
+
+def test_speculative_decisions_no_rollback_and_exact_mode(pgmg):
+    """The reference problem: every distributed check is ruled out locally (huge norms),
+    so the speculative call is never rolled back; PGMG_FLAG_EXACT_DIST (one allreduce per
+    check) gives the same words and statistics."""
+    ref = _single(pgmg, 2049, 4)
+    spec = _ranks_info(pgmg, 4, 2049, 4, gather_n=129)
+    exact = _ranks_info(pgmg, 4, 2049, 4, gather_n=129, flags=pgmg.PGMG_FLAG_EXACT_DIST)
+    for r in range(4):
+        assert spec[r][2] == (True, 0), spec[r][2]
+        assert exact[r][2] == (False, 0), exact[r][2]
+        assert_bitwise(spec[r][0], ref[0], f"speculative rank {r}")
+        assert_bitwise(exact[r][0], ref[0], f"exact rank {r}")
+    assert spec[0][1][:2] == exact[0][1][:2] == ref[1][:2]
+
+
+def test_speculative_rollback_when_a_check_can_fire(pgmg, oracle_mod):
+    """eps above every norm: every check fires, no rank can rule any out, the call is
+    rolled back and rerun exactly; the result is the oracle's."""
+    N, eps = 513, 1e9
+    o = oracle_mod.Oracle(eps=eps)
+    f = o.rhs(N)
+    ref = np.zeros((N, N))
+    for _ in range(3):
+        o.v_cycle(ref, f)
+    outs = _ranks_info(pgmg, 2, N, 3, eps=eps, tail_n=17, gather_n=33)
+    for r, (phi, det, info) in enumerate(outs):
+        assert_bitwise(phi, ref, f"rank {r}")
+        assert info[0] and info[1] >= 1, info
+    assert outs[0][1][0] == o.sweeps
