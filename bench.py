@@ -141,6 +141,7 @@ def main():
     s.sync()
     t0 = time.perf_counter()
     run(args.steps)
+    t_enq = time.perf_counter()   # host time to enqueue the steps (asynchronous launches)
     s.sync()
     barrier()
     t1 = time.perf_counter()
@@ -154,6 +155,7 @@ def main():
     n = N = args.n
     gen = s.fused and s.fine_pass_bytes(3) < s.fine_pass_bytes(0)   # f regenerated in-kernel
     T = "double" if args.dtype == "f64" else "float"
+    r2 = world > 1 and not s.dist_info()[0]   # k_postpre sums r(x2)^2: exact strip decisions
     passes = []
     if s.fused:
         # algorithmic bytes per launch from the library (pgmg_fine_pass_bytes): each input
@@ -161,7 +163,7 @@ def main():
         for which, name, key in (
                 (3, "k_postpre (finest level, between cycles: prolongation + 2+2 Jacobi sweeps "
                     "+ residual + restriction, fused" + ("; f regenerated in-kernel" if gen else "")
-                    + ")", f"k_postpre_lds<{T},{'true' if world > 1 else 'false'},"
+                    + ")", f"k_postpre_lds<{T},{'true' if r2 else 'false'},"
                            f"{'true' if gen else 'false'}>"),
                 (1, "k_pre<false,true> (finest level: 2 Jacobi sweeps + residual + restriction, "
                     "fused)", f"k_pre<{T},false,true,2,true>" if gen else f"k_pre<{T},false,true>"),
@@ -226,6 +228,7 @@ def main():
             "fine_sweep_equivalent_gbps": sweep_eq,
             "vcycle_algorithmic_gbps": round(vbytes / (dt / args.steps) / 1e9, 2),
             "vcycle_device_ms": round(dev_ms / args.steps, 4),
+            "host_enqueue_ms_per_step": round((t_enq - t0) * 1e3 / args.steps, 4),
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

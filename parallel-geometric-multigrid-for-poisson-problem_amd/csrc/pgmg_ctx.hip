@@ -443,7 +443,7 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         q.rc = G<T>(C.F);
         q.partials1 = c->partials;
         q.partials2 = c->partials2;
-        q.partials3 = dist ? c->partials3 : nullptr;
+        q.partials3 = (dist && !spec) ? c->partials3 : nullptr;   // spec: no rare path runs
         q.gfx = c->gen_rhs ? c->gfx : nullptr;
         q.gsy = c->gen_rhs ? c->gsy : nullptr;
         q.stats = c->stats;
