@@ -1219,16 +1219,28 @@ __global__ __launch_bounds__(256) void k_post_fixup(FixArgsF a, PostArgsT<T> p)
     }
 }
 
+// Fix-up grid: every block re-reduces the partials (the decision) and the grid-stride
+// recompute only runs when a check fired, so small levels get few blocks (a 256-block
+// launch costs ~2 us more than a 1-block one on a latency-bound level); 256 blocks from
+// 2^20 points up (a fired recompute on the finest levels then still has the whole chip).
+static int fixup_blocks(int N, int row_lo, int row_hi)
+{
+    const long long pts = (long long)(row_hi > row_lo ? row_hi - row_lo : 0) * N;
+    long long b = pts >> 12;
+    return (int)(b < 1 ? 1 : (b > 256 ? 256 : b));
+}
+
 template <class T>
 void launch_pre_fixup(const FixArgsF &a, const PreArgsT<T> &p, bool x0_zero, hipStream_t s)
 {
-    k_pre_fixup<T><<<dim3(256), dim3(256), 0, s>>>(a, p, x0_zero ? 1 : 0);
+    k_pre_fixup<T><<<dim3(fixup_blocks(p.N, p.row_lo, p.row_hi)), dim3(256), 0, s>>>(
+        a, p, x0_zero ? 1 : 0);
 }
 
 template <class T>
 void launch_post_fixup(const FixArgsF &a, const PostArgsT<T> &p, hipStream_t s)
 {
-    k_post_fixup<T><<<dim3(256), dim3(256), 0, s>>>(a, p);
+    k_post_fixup<T><<<dim3(fixup_blocks(p.N, p.row_lo, p.row_hi)), dim3(256), 0, s>>>(a, p);
 }
 
 #define PGMG_INSTANTIATE(T)                                                                       \
