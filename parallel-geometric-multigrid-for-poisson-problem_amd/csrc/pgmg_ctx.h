@@ -89,6 +89,10 @@ struct pgmg_ctx {
     double *rhs_tab = nullptr;
     const double *gfx = nullptr, *gsy = nullptr;   // valid for indices -8 ..
     bool gen_rhs = false;
+    // the tables matching the CURRENT level-0 F (gfx/gsy, or the F-cycle's own during
+    // pgmg_fcycle), nullptr when level-0 f must be streamed
+    const double *rgfx = nullptr, *rgsy = nullptr;
+    double *fmg_gtab = nullptr;   // fx/sy tables of the F-cycle's level-0 RHS
     // row strips, speculative early-exit decisions (pgmg_ctx.hip "speculative decisions")
     bool spec = false;            // enabled for this context (world > 1, fused cycle)
     bool spec_now = false;        // the cycles being enqueued decide speculatively
@@ -102,6 +106,7 @@ struct pgmg_ctx {
     // F-cycle (pgmg_fcycle): analytic level-0 RHS of the FMG h chain, and the sine
     // tables of every level (built on the first call)
     pgmg::Grid Ffmg;
+    bool fmg_rhs_ready = false;   // Ffmg holds the level-0 analytic RHS of the FMG h chain
     double *fmg_tab = nullptr;
     std::vector<int> fmg_off;     // per level 0..nb then tail levels below nb: sx offset
 };

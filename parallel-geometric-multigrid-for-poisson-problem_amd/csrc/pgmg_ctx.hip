@@ -258,6 +258,8 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
     // coarse rows this rank restricts into (its strip's rows; the fix-up honours them too)
     pa.rc_lo = pa.jc0 > 1 ? pa.jc0 : 1;
     pa.rc_hi = pa.jc1 < C.N - 1 ? pa.jc1 : C.N - 1;
+    pa.gfx = l == 0 ? c->rgfx : nullptr;   // level 0 with an analytic RHS: regenerate f
+    pa.gsy = l == 0 ? c->rgsy : nullptr;
     FixArgsF fa{};
     fa.partials = c->partials;
     fa.np = fused_blocks(L.N, pa.jc0, pa.jc1);
@@ -294,6 +296,8 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
     po.jc1 = pa.jc1;
     po.row_lo = L.u0;
     po.row_hi = L.u1;
+    po.gfx = l == 0 ? c->rgfx : nullptr;
+    po.gsy = l == 0 ? c->rgsy : nullptr;
     ev = fine ? timed_begin(c, 2) : -1;
     launch_post(po, fine, c->s);
     if ((e = timed_end(c, 2, ev))) return e;
@@ -365,8 +369,8 @@ static PreArgsT<T> make_pre(pgmg_ctx *c, const T *x0, T *x2)
     pa.row_hi = sr.row_hi;
     pa.rc_lo = sr.rc_lo;
     pa.rc_hi = sr.rc_hi;
-    pa.gfx = c->gen_rhs ? c->gfx : nullptr;
-    pa.gsy = c->gen_rhs ? c->gsy : nullptr;
+    pa.gfx = c->rgfx;
+    pa.gsy = c->rgsy;
     return pa;
 }
 
@@ -392,8 +396,8 @@ static PostArgsT<T> make_post(pgmg_ctx *c, const T *phi, T *x2)
     po.jc1 = sr.jc1;
     po.row_lo = sr.row_lo;
     po.row_hi = sr.row_hi;
-    po.gfx = c->gen_rhs ? c->gfx : nullptr;
-    po.gsy = c->gen_rhs ? c->gsy : nullptr;
+    po.gfx = c->rgfx;
+    po.gsy = c->rgsy;
     return po;
 }
 
@@ -444,8 +448,8 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         q.partials1 = c->partials;
         q.partials2 = c->partials2;
         q.partials3 = (dist && !spec) ? c->partials3 : nullptr;   // spec: no rare path runs
-        q.gfx = c->gen_rhs ? c->gfx : nullptr;
-        q.gsy = c->gen_rhs ? c->gsy : nullptr;
+        q.gfx = c->rgfx;
+        q.gsy = c->rgsy;
         q.stats = c->stats;
         q.hh = (T)L.hh;
         q.ih = (T)L.ih;
@@ -641,6 +645,7 @@ int pgmg_destroy(pgmg_ctx *c)
     if (c->partials2) (void)hipFree(c->partials2);
     if (c->partials3) (void)hipFree(c->partials3);
     if (c->rhs_tab) (void)hipFree(c->rhs_tab);
+    if (c->fmg_gtab) (void)hipFree(c->fmg_gtab);
     if (c->uflags) (void)hipFree(c->uflags);
     if (c->stats_bk) (void)hipFree(c->stats_bk);
     free_grid(c->bk);
@@ -880,6 +885,7 @@ int pgmg_set_problem(pgmg_ctx *c, const double *phi0, const double *f)
         HIPC(hipMemcpy2D(row_ptr(c->S, r0, L.P, L.es), pitch, row_ptr(L.A, r0, L.P, L.es), pitch,
                          width, rows, hipMemcpyDeviceToDevice));
     c->gen_rhs = false;
+    c->rgfx = c->rgsy = nullptr;
     if (f) {
         if ((e = upload_rows(c, L, L.F, f, r0, r1))) return e;
     } else {
@@ -910,6 +916,8 @@ int pgmg_set_problem(pgmg_ctx *c, const double *phi0, const double *f)
             c->gfx = c->rhs_tab + 8;
             c->gsy = c->rhs_tab + nx + 8;
             c->gen_rhs = true;
+            c->rgfx = c->gfx;
+            c->rgsy = c->gsy;
         }
     }
     HIPC(hipMemset(c->stats, 0, 4 * sizeof(unsigned long long)));
@@ -1073,6 +1081,19 @@ static int fmg_tables(pgmg_ctx *c)
     }
     HIPC(hipMalloc((void **)&c->fmg_tab, tab.size() * sizeof(double)));
     HIPC(hipMemcpy(c->fmg_tab, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice));
+    // the level-0 RHS of the FMG chain, regenerated in the level-0 passes like set_problem's
+    if (c->nb > 0) {
+        const int N = c->lv[0].N;
+        std::vector<double> sx, sy;
+        double factor;
+        sine_tables(c->cfg, N, fmg_h(c->cfg, N), sx, sy, factor);
+        const int nx = 8 + N + 1024, ny = 8 + N + 16;
+        std::vector<double> g((size_t)nx + ny, 0.0);
+        for (int i = 0; i < N; ++i) g[8 + i] = factor * sx[i];
+        for (int j = 0; j < N; ++j) g[(size_t)nx + 8 + j] = sy[j];
+        HIPC(hipMalloc((void **)&c->fmg_gtab, g.size() * sizeof(double)));
+        HIPC(hipMemcpy(c->fmg_gtab, g.data(), g.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
     return PGMG_OK;
 }
 
@@ -1124,9 +1145,14 @@ static int enqueue_fcycle(pgmg_ctx *c)
         Level &L = c->lv[l];
         const Level &C = c->lv[l + 1];
         const double *sx = c->fmg_tab + c->fmg_off[l];
-        launch_rhs(G<T>(L.F), sx, sx + L.N, factor, L.N, L.P, 0, L.N, c->s);
-        launch_fill_rows(G<T>(L.A), L.P, 0, L.N, c->s);
-        launch_fill_rows(G<T>(L.B), L.P, 0, L.N, c->s);
+        // level 0's F is the F-cycle's own analytic RHS (Ffmg): the same on every call
+        if (l > 0 || !c->fmg_rhs_ready)
+            launch_rhs(G<T>(L.F), sx, sx + L.N, factor, L.N, L.P, 0, L.N, c->s);
+        // phi_fine = 0 + P phi_coarse (MultiGrid.hpp:159-164): the prolongation assigns the
+        // interior, the frame (boundary, and row/column 1 the reference never corrects) is
+        // zeroed; the ping-pong buffer's frame mirrors it
+        launch_zero_frame(G<T>(L.A), L.P, L.N, c->s);
+        launch_zero_frame(G<T>(L.B), L.P, L.N, c->s);
         ProlongArgsT<T> p{};
         p.c = G<T>(C.A);
         p.fine = G<T>(L.A);
@@ -1136,6 +1162,7 @@ static int enqueue_fcycle(pgmg_ctx *c)
         p.Pc = C.P;
         p.row0 = 2;
         p.row1 = L.N - 1;
+        p.assign = 1;
         launch_prolong(p, c->s);
         int e = enqueue_cycle_t<T>(c, l, 1, false);
         if (e) return e;
@@ -1167,10 +1194,18 @@ int pgmg_fcycle(pgmg_ctx *c, int ncycles)
         L.ih = 1.0 / (h * h);
     }
     if (c->nb > 0) std::swap(L0.F, c->Ffmg);
+    const double *sgx = c->rgfx, *sgy = c->rgsy;
+    const bool gen = c->nb > 0 && !(c->cfg.flags & PGMG_FLAG_STORED_RHS);
+    c->rgfx = gen ? c->fmg_gtab + 8 : nullptr;
+    c->rgsy = gen ? c->fmg_gtab + (8 + L0.N + 1024) + 8 : nullptr;
     HIPC(hipEventRecord(c->ev0, c->s));
-    for (int k = 0; k < ncycles && !e; ++k)
+    for (int k = 0; k < ncycles && !e; ++k) {
         e = c->fp32 ? enqueue_fcycle<float>(c) : enqueue_fcycle<double>(c);
+        c->fmg_rhs_ready = true;
+    }
     if (c->nb > 0) std::swap(L0.F, c->Ffmg);
+    c->rgfx = sgx;
+    c->rgsy = sgy;
     for (int l = 0; l <= c->nb; ++l) {
         c->lv[l].h = saved[l].h;
         c->lv[l].hh = saved[l].hh;
@@ -1277,7 +1312,7 @@ int pgmg_vcycle_bytes(pgmg_ctx *c, double *bytes)
         const double nc = (double)(C.u1 - C.u0) * (C.N - 2);
         if (c->fused) {
             if (l == 0 && c->cross) {                     // steady state: one k_postpre
-                b += (c->gen_rhs ? 16.0 : 24.0) * n + 16.0 * nc;  // phi, (f,) ec in; x4, rc out
+                b += (c->rgfx ? 16.0 : 24.0) * n + 16.0 * nc;     // phi, (f,) ec in; x4, rc out
                 continue;
             }
             if (l > 0 && c->recompute) {                  // x0 = 0, x2 recomputed
@@ -1285,8 +1320,9 @@ int pgmg_vcycle_bytes(pgmg_ctx *c, double *bytes)
                 b += 16.0 * n + 8.0 * nc;                 // k_post: f, ec in; x2 out
                 continue;
             }
-            b += (l == 0 ? 24.0 : 16.0) * n + 8.0 * nc;  // k_pre: x0, f in; x2, rc out
-            b += 24.0 * n + 8.0 * nc;                     // k_post: phi, f, ec in; x2 out
+            const double fb = (l == 0 && c->rgfx) ? 0.0 : 8.0;  // level 0: f regenerated
+            b += (l == 0 ? 16.0 + fb : 16.0) * n + 8.0 * nc;   // k_pre: x0, f in; x2, rc out
+            b += (16.0 + fb) * n + 8.0 * nc;                    // k_post: phi, f, ec in; x2 out
             continue;
         }
         const int S1 = c->cfg.v1 + 1, S2 = c->cfg.v2 + 1;
@@ -1312,8 +1348,8 @@ int pgmg_fine_pass_bytes(pgmg_ctx *c, int pass, double *bytes)
     const StripRows sr = strip_rows(L, C);
     const double nc = (double)(sr.rc_hi > sr.rc_lo ? sr.rc_hi - sr.rc_lo : 0) * (C.N - 2);
     double b = 0.0;
-    // f is regenerated in-kernel (not read) by the cross-fused level-0 passes
-    const double fb = (c->cross && c->gen_rhs) ? 0.0 : 8.0;
+    // f is regenerated in-kernel (not read) by the level-0 passes
+    const double fb = c->rgfx != nullptr ? 0.0 : 8.0;
     switch (pass) {
     case 0: b = 24.0 * n; break;                               // x, f in; x out
     case 1: b = (16.0 + fb) * n + 8.0 * nc; break;             // x0, (f) in; x2, rc out

@@ -65,6 +65,7 @@ struct ProlongArgsT {
     int Wf, Pf, Wc, Pc;
     int row0, row1;         // fine rows to update, inside [2, Nf-2]
     int rows_per_block;
+    int assign;             // fine = (+0) + P coarse (prolongation into a zeroed grid)
 };
 
 // Early-exit decision for one smoother check plus the undo of the speculative sweep.
@@ -131,6 +132,9 @@ template <class T>
 void launch_restrict_values(const T *fine, int Nf, int Pf, T *coarse, int Nc, int Pc,
                             hipStream_t s);
 template <class T> void launch_fill_rows(T *o, int P, int row0, int row1, hipStream_t s);
+// zero rows 0, 1, N-1 and columns 0, N-1 of an N x N grid (what a prolongation with
+// assign = 1 over rows [2, N-2] leaves unwritten)
+template <class T> void launch_zero_frame(T *o, int P, int N, hipStream_t s);
 template <class T>
 void launch_resnorm_partials(const T *x, const T *f, double *partials, T inv_hh, int W, int P,
                              int row0, int row1, int nblocks, hipStream_t s);

@@ -296,7 +296,8 @@ __global__ __launch_bounds__(kBlock) void k_prolong(ProlongArgsT<T> a)
         const int jc = j >> 1;
         const T *C0 = a.c + jc * Pc;
         const T c00 = C0[t], c01 = C0[t + 1];
-        V2<T> v = ldv(a.fine + j * Pf + c);
+        // assign: start from +0.0 — the same additions as into a zeroed grid
+        V2<T> v = a.assign ? zero2<T>() : ldv(a.fine + j * Pf + c);
         if ((j & 1) == 0) {
             if (okx) v.x = v.x + T(0.5) * (c00 + c01);
             if (oky) v.y = v.y + c01;
@@ -465,6 +466,31 @@ void launch_fill_rows(T *o, int P, int row0, int row1, hipStream_t s)
     k_fill_rows<T><<<dim3((unsigned)nb), dim3(256), 0, s>>>(o, P, row0, row1);
 }
 
+template <class T>
+__global__ void k_zero_frame(T *o, long long P, int N)
+{
+    const int n = 3 * N + 2 * (N - 3);   // rows 0, 1, N-1; columns 0, N-1 of rows 2..N-2
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        long long q;
+        if (k < N) q = k;
+        else if (k < 2 * N) q = P + (k - N);
+        else if (k < 3 * N) q = (long long)(N - 1) * P + (k - 2 * N);
+        else {
+            const int r = k - 3 * N;            // 0 .. 2(N-3)-1
+            const long long j = 2 + (r >> 1);
+            q = j * P + ((r & 1) ? N - 1 : 0);
+        }
+        o[q] = T(0);
+    }
+}
+
+template <class T>
+void launch_zero_frame(T *o, int P, int N, hipStream_t s)
+{
+    const int n = 3 * N + 2 * (N - 3);
+    k_zero_frame<T><<<dim3((n + 255) / 256), dim3(256), 0, s>>>(o, P, N);
+}
+
 // sum r(x)^2 over rows [row0,row1), interior columns — reporting only
 template <class T>
 __global__ __launch_bounds__(kBlock) void k_resnorm(const T *x, const T *f, double *partials,
@@ -550,6 +576,7 @@ void launch_from_double(const double *src, int N, T *dst, int P, int row0, int r
                                 hipStream_t);                                                      \
     template void launch_restrict_values<T>(const T *, int, int, T *, int, int, hipStream_t);      \
     template void launch_fill_rows<T>(T *, int, int, int, hipStream_t);                            \
+    template void launch_zero_frame<T>(T *, int, int, hipStream_t);                                \
     template void launch_resnorm_partials<T>(const T *, const T *, double *, T, int, int, int, int, \
                                              int, hipStream_t);                                    \
     template void launch_to_double<T>(const T *, int, double *, int, int, int, hipStream_t);      \

@@ -155,3 +155,19 @@ def test_fcycle_4097_vs_oracle(pgmg, oracle_mod):
         got = s.solution()
         assert s.stats()[0] == o.sweeps
     assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
+@pytest.mark.parametrize("N", [129, 2049])
+def test_fcycle_regenerated_rhs_equals_stored(pgmg, N):
+    """The F-cycle's level-0 passes regenerate the FMG chain's analytic RHS in-kernel;
+    PGMG_FLAG_STORED_RHS streams it: identical words over repeated F-cycles (the cached
+    level-0 RHS, the assigned prolongation and the zeroed frames included)."""
+    out = []
+    for flags in (0, pgmg.PGMG_FLAG_STORED_RHS):
+        with pgmg.Solver(N, flags=flags) as s:
+            s.set_problem()
+            s.fcycle(2)
+            s.vcycle(1)       # the V-cycle after an F-cycle uses the problem's own f again
+            out.append((s.solution(), s.stats()))
+    assert np.array_equal(out[0][0].view(np.uint64), out[1][0].view(np.uint64))
+    assert out[0][1] == out[1][1]
