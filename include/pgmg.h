@@ -102,7 +102,8 @@ typedef struct pgmg_config {
     /* row-strip domain decomposition over `world` ranks (one process per GPU). */
     int rank, world;   /* default 0, 1                                           */
     const void *nccl_unique_id;  /* 128-byte ncclUniqueId when world > 1      */
-    int gather_n;      /* levels with N <= gather_n collapse to rank 0 (world>1) */
+    int gather_n;      /* levels with N <= gather_n collapse to one grid, replicated
+                          on every rank (world > 1)                               */
     int precision;     /* PGMG_PRECISION_FP64 (default) or PGMG_PRECISION_FP32    */
 } pgmg_config;
 

@@ -13,10 +13,11 @@
 //    phi 2 rows and the coarse correction 1-2 rows.
 //  * The smoother's early-exit norm is a global sum: a local partial sum, then one
 //    allreduce of a single double (all ranks take the same decision).
-//  * Levels with N <= gather_n (or strips thinner than kMinRows) are "gathered":
-//    each rank sends its rows of the coarse right-hand side to rank 0, rank 0 runs
-//    the remaining cycle (bulk kernels + LDS tail) alone, then sends each rank the
-//    rows of the correction its prolongation reads.
+//  * Levels with N <= gather_n (or strips thinner than kMinRows) are "gathered" and
+//    replicated: every rank sends its rows of the coarse right-hand side to every other
+//    rank (one grouped exchange), then every rank runs the remaining cycle (bulk kernels
+//    + LDS tail) on its full copy — identical work and results on every rank, so no
+//    scatter of the correction is needed (one collective step instead of two).
 //  * Transport: RCCL grouped ncclSend/ncclRecv + ncclAllReduce on the context's
 //    stream (RCCL over xGMI on MI355X).  Tests use an in-process loopback
 //    transport (ranks = host threads sharing one GPU; RCCL refuses two ranks per
@@ -314,7 +315,7 @@ class StripComm : public Comm {
                 L.lo = 0;
                 L.hi = L.N;
                 L.gathered = true;
-                L.on_this_rank = (l == Ld) || me == 0;  // receive buffers for the correction
+                L.on_this_rank = true;  // the coarse levels are replicated on every rank
             }
             L.u0 = std::max(L.lo, 1);
             L.u1 = std::min(L.hi, L.N - 1);
@@ -357,31 +358,27 @@ class StripComm : public Comm {
     {
         Level &L = c->lv[l];
         const size_t row = (size_t)L.P * L.es;
-        // 1. rows of the coarse right-hand side -> rank 0
+        // 1. every rank's rows of the coarse right-hand side -> every rank (one group)
         int e = t->group_start();
         if (e) return e;
         for (int r = 0; r < world; ++r) {
             const int a = std::max(strip_lo(r, l), 1), b = std::min(strip_hi(r, l, L.N), L.N - 1);
-            if (b <= a || r == 0) continue;
-            if (me == r && (e = t->send(row_ptr(L.F, a, L.P, L.es), (b - a) * row, 0, c->s))) return e;
-            if (me == 0 && (e = t->recv(row_ptr(L.F, a, L.P, L.es), (b - a) * row, r, c->s))) return e;
+            if (b <= a) continue;
+            if (r == me) {
+                for (int q = 0; q < world && !e; ++q)
+                    if (q != me) e = t->send(row_ptr(L.F, a, L.P, L.es), (b - a) * row, q, c->s);
+                if (e) return e;
+            } else if ((e = t->recv(row_ptr(L.F, a, L.P, L.es), (b - a) * row, r, c->s))) {
+                return e;
+            }
         }
         if ((e = t->group_end(c->s))) return e;
-        // 2. rank 0 runs the rest of the hierarchy alone
-        if (me == 0) {
-            for (int i = 0; i < repeats; ++i)
-                if ((e = enqueue_cycle(c, l, gamma, i == 0))) return e;
-        }
-        // 3. the correction rows each strip's prolongation reads -> every rank (4 rows past
-        //    the strip: k_postpre reads 3 above and 4 below, its rare paths one more)
-        if ((e = t->group_start())) return e;
-        for (int r = 1; r < world; ++r) {
-            const int a = std::max(strip_lo(r, l) - 4, 0);
-            const int b = std::min(strip_hi(r, l, L.N) + 4, L.N);
-            if (me == 0 && (e = t->send(row_ptr(L.A, a, L.P, L.es), (b - a) * row, r, c->s))) return e;
-            if (me == r && (e = t->recv(row_ptr(L.A, a, L.P, L.es), (b - a) * row, 0, c->s))) return e;
-        }
-        return t->group_end(c->s);
+        // 2. every rank runs the rest of the hierarchy on its full copy: identical inputs,
+        //    identical (pointwise, deterministic) results, so the parent's prolongation reads
+        //    the correction from its own copy and no scatter is needed
+        for (int i = 0; i < repeats; ++i)
+            if ((e = enqueue_cycle(c, l, gamma, i == 0))) return e;
+        return PGMG_OK;
     }
 
     int gather_solution(pgmg_ctx *c, double *phi) override

@@ -44,7 +44,7 @@ struct Level {
     int u0 = 0, u1 = 0;      // interior rows this rank updates: [max(lo,1), min(hi,N-1))
     Grid A, B, F;            // solution (phi or e), ping-pong, right-hand side (f or rc)
     bool on_this_rank = true;
-    bool gathered = false;   // the level lives entirely on rank 0
+    bool gathered = false;   // the level is not split: every rank holds and computes all of it
 };
 
 class Comm;
@@ -124,7 +124,7 @@ int download_grid(pgmg_ctx *c, const void *o, int P, int N, double *host);
 
 // Row-strip domain decomposition (one process per GPU, RCCL), pgmg_comm.hip.
 // Levels 0 .. gathered_level()-1 are split into row strips with halo exchange;
-// the first gathered level and everything below it run on rank 0 alone.
+// the first gathered level and everything below it are collapsed to one (replicated) grid.
 class Comm {
   public:
     virtual ~Comm() {}
@@ -145,8 +145,8 @@ class Comm {
     virtual int allreduce_sum(double *d, int n, hipStream_t s) = 0;
     // in-place element-wise minimum of n device unsigned ints over all ranks
     virtual int allreduce_min_u32(unsigned *d, int n, hipStream_t s) = 0;
-    // the parent produced rc of gathered level l: move it to rank 0, run `repeats`
-    // cycles there, bring the correction back to every rank's strip
+    // the parent produced rc of gathered level l: gather it on every rank, run `repeats`
+    // cycles on every rank's full copy (identical results; no scatter needed)
     virtual int run_gathered(pgmg_ctx *c, int l, int gamma, int repeats) = 0;
     virtual int gather_solution(pgmg_ctx *c, double *phi_host) = 0;
     static Comm *create(pgmg_ctx *c, int *rc);
