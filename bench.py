@@ -202,6 +202,8 @@ def main():
         metric = METRIC if args.dtype == "f64" else METRIC.replace(", fp64", ", fp32 variant")
         if args.cycle != "V":
             metric = metric.replace("V-cycles/sec", f"{args.cycle}-cycles/sec")
+        if args.n != 16385:
+            metric = metric.replace("16384²", f"{args.n - 1}²")
         line = {
             "metric": metric,
             "value": round(value, 4),

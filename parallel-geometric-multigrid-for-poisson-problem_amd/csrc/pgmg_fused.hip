@@ -940,6 +940,16 @@ void launch_pre(const PreArgsT<T> &a0, bool x0_zero, bool fine, hipStream_t s)
     PreArgsT<T> a = a0;
     a.rows_per_block = r;
     const dim3 g(gx, gy), b(t);
+    // x0 = 0 (coarse levels): only f streams, so more rows in flight per lane
+    static const int p0 = env_int("PGMG_PRE0_PAIRS", 3);   // r01 sweep: 3 >= 2, 4
+    if (x0_zero && p0 == 4) {
+        k_pre<T, true, false, 4><<<g, b, 0, s>>>(a);
+        return;
+    }
+    if (x0_zero && p0 == 3) {
+        k_pre<T, true, false, 3><<<g, b, 0, s>>>(a);
+        return;
+    }
     if (fused_pairs() == 2) {
         if (x0_zero) k_pre<T, true, false, 2><<<g, b, 0, s>>>(a);
         else if (fine && a.gfx != nullptr) k_pre<T, false, true, 2, true><<<g, b, 0, s>>>(a);
@@ -962,6 +972,12 @@ void launch_post(const PostArgsT<T> &a0, bool fine, hipStream_t s)
     a.rows_per_block = r;
     const dim3 g(gx, gy), b(t);
     const bool rec = a.pre_fired != nullptr;
+    static const int pr = env_int("PGMG_POSTR_PAIRS", 2);
+    if (!fine && rec && (pr == 3 || pr == 4)) {
+        if (pr == 4) k_post<T, false, 4, true><<<g, b, 0, s>>>(a);
+        else k_post<T, false, 3, true><<<g, b, 0, s>>>(a);
+        return;
+    }
     if (fused_pairs() == 2) {
         if (fine && a.gfx != nullptr) k_post<T, true, 2, false, true><<<g, b, 0, s>>>(a);
         else if (fine) k_post<T, true, 2, false><<<g, b, 0, s>>>(a);
