@@ -9,7 +9,8 @@ import os
 import pathlib
 
 PKG_DIR = pathlib.Path(__file__).resolve().parent
-LIB_PATH = PKG_DIR / "libpgmg.so"
+# PGMG_LIB: another build of the library (A/B measurements of compile-time variants)
+LIB_PATH = pathlib.Path(os.environ["PGMG_LIB"]) if os.environ.get("PGMG_LIB") else PKG_DIR / "libpgmg.so"
 
 PGMG_OK = 0
 PGMG_ERR_ARG = -1
