@@ -80,10 +80,10 @@ extern "C" {
                                     analytic RHS (set_problem f = NULL), the finest-level
                                     cross-cycle pass regenerates it in-kernel from two
                                     sine tables (bitwise the same values, 8 B/pt less) */
-#define PGMG_FLAG_EXACT_DIST 64u /* row strips: decide every smoother early-exit check of a
-                                    distributed level with its own allreduce instead of
-                                    speculatively (validated once per call, rollback on
-                                    doubt; same results)                              */
+#define PGMG_FLAG_EXACT_DIST 64u /* decide every smoother early-exit check in-stream (a
+                                    fix-up launch per check; on row strips an allreduce
+                                    each) instead of speculatively (validated once per
+                                    call, rollback on doubt; same results)            */
 #define PGMG_FLAG_LOOPBACK 8u    /* world > 1 with ranks as threads of one process on
                                     one GPU: nccl_unique_id is a pgmg_loopback hub
                                     (test transport for the strip decomposition)    */
@@ -121,7 +121,8 @@ int pgmg_destroy(pgmg_ctx *ctx);
  * world > 1 every rank passes the full arrays (or NULLs) and keeps its strip. */
 int pgmg_set_problem(pgmg_ctx *ctx, const double *phi0, const double *f);
 
-/* Enqueue `ncycles` cycles on the context's stream (asynchronous).
+/* Enqueue `ncycles` cycles on the context's stream (asynchronous; a speculative call,
+ * see pgmg_dist_info, returns after the device has finished it).
  * pgmg_fcycle: one F-cycle = restrict phi to n_coarse, then per level up smooth(3),
  * prolongation into a zeroed finer grid, analytic RHS of that grid (h chain starting at
  * 1/(n_coarse-1)), one V-cycle; the f given to pgmg_set_problem is left untouched
@@ -167,9 +168,17 @@ int pgmg_phi_device(pgmg_ctx *ctx, double **ptr, int *pitch, int *row0, int *row
  * k_postpre regenerates the analytic f in-kernel), times elem_bytes / 8. */
 int pgmg_fine_pass_bytes(pgmg_ctx *ctx, int pass, double *bytes);
 
-/* Row strips: whether the early-exit checks are decided speculatively (1) or with one
- * allreduce each (0), and how many calls had to be rolled back and rerun exactly. */
+/* Whether V/W-cycle calls decide the smoother early-exit checks speculatively (1: the
+ * checks are recorded, validated once after the call, and the call is rolled back and
+ * rerun with in-stream decisions when one could fire; cross-fused or row-strip contexts
+ * without PGMG_FLAG_EXACT_DIST) or in-stream (0), and how many calls were rolled back.
+ * After a rollback the context decides in-stream until the next pgmg_set_problem. */
 int pgmg_dist_info(pgmg_ctx *ctx, int *speculative, long long *rollbacks);
+
+/* Which bulk levels decide their early-exit checks in-stream in the next speculative call:
+ * bit l (l >= 1) = level l's checks fired or are predicted to fire soon; bit 0 = no
+ * speculation at all (disabled, or a finest-level check fires). */
+int pgmg_spec_levels(pgmg_ctx *ctx, unsigned long long *in_stream);
 
 /* The context's PGMG_PRECISION_* and its grid element size in bytes (8 or 4). */
 int pgmg_precision(pgmg_ctx *ctx, int *precision, int *elem_bytes);

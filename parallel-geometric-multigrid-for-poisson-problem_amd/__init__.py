@@ -218,10 +218,18 @@ class Solver:
         return v.value
 
     def dist_info(self):
-        """(speculative early-exit decisions on strips?, calls rolled back and rerun)"""
+        """(speculative early-exit checks (recorded, validated after the call)?, calls
+        rolled back and rerun with in-stream decisions)"""
         sp, rb = C.c_int(), C.c_longlong()
         check(self.lib.pgmg_dist_info(self.h, C.byref(sp), C.byref(rb)), "pgmg_dist_info")
         return bool(sp.value), rb.value
+
+    def spec_levels(self):
+        """Bit mask: bit l = bulk level l decides its checks in-stream; bit 0 = no
+        speculation at all."""
+        m = C.c_ulonglong()
+        check(self.lib.pgmg_spec_levels(self.h, C.byref(m)), "pgmg_spec_levels")
+        return m.value
 
     @property
     def elem_bytes(self):

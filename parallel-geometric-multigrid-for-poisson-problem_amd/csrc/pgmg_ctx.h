@@ -93,11 +93,23 @@ struct pgmg_ctx {
     // pgmg_fcycle), nullptr when level-0 f must be streamed
     const double *rgfx = nullptr, *rgsy = nullptr;
     double *fmg_gtab = nullptr;   // fx/sy tables of the F-cycle's level-0 RHS
-    // row strips, speculative early-exit decisions (pgmg_ctx.hip "speculative decisions")
-    bool spec = false;            // enabled for this context (world > 1, fused cycle)
-    bool spec_now = false;        // the cycles being enqueued decide speculatively
-    unsigned *uflags = nullptr;   // one flag per distributed check of the current call
-    int uflags_cap = 0, uidx = 0;
+    // speculative calls (pgmg_ctx.hip "speculative calls"): the early-exit checks of a
+    // call are recorded instead of decided in-stream, validated once after the call
+    bool spec = false;            // enabled for this context (fused cycle, no EXACT flag)
+    bool spec_off = false;        // switched off: a finest-level check fires
+    std::vector<char> lvl_exact;  // per bulk level: its checks fire (soon): decide in-stream
+    std::vector<std::vector<double>> lvl_hist;   // per bulk level: its last check norms
+    double *chk_norm = nullptr;   // per-check norms of the last validation
+    unsigned *mark_dev = nullptr; // row strips: per-level marks agreed by allreduce
+    std::vector<double> hnorm;
+    std::vector<unsigned> hflag;
+    bool lean = false;            // the cycles being enqueued record their checks
+    double *plog = nullptr;       // partials of every recorded check of the current call
+    long long plog_cap = 0, plog_used = 0;
+    std::vector<pgmg::CheckRef> chks;
+    pgmg::CheckRef *chk_dev = nullptr;
+    unsigned *uflags = nullptr;   // per-check verdicts (+ one spare word: any)
+    long long chk_cap = 0;
     pgmg::Grid bk;                // level-0 solution at the start of the call (rollback)
     unsigned long long *stats_bk = nullptr;
     long long rollbacks = 0;

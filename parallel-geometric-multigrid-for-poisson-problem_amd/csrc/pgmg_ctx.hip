@@ -69,13 +69,21 @@ void pgmg::free_grid(Grid &g)
     g.bytes = 0;
 }
 
-// Row strips, speculative decisions: the next n flags of the current call (nullptr when
-// the cycles being enqueued decide exactly)
-static unsigned *spec_slot(pgmg_ctx *c, int n)
+// Speculative call: a fresh slice of the partials log for one early-exit check, recorded
+// for the validation after the call (nullptr when the cycles being enqueued decide every
+// check in-stream).  The log is sized beforehand (spec_need); running past it would be a
+// bug: the check then writes the shared partials and the call is treated as failed
+// validation (rolled back), never read out of bounds.
+static double *chk_partials(pgmg_ctx *c, int np, int level)
 {
-    if (!c->spec_now) return nullptr;
-    unsigned *p = c->uflags + c->uidx;
-    c->uidx += n;
+    if (!c->lean || c->lvl_exact[level]) return nullptr;
+    if (c->plog_used + np > c->plog_cap) {
+        c->chks.push_back({nullptr, -1, level, 0});
+        return c->partials;
+    }
+    double *p = c->plog + c->plog_used;
+    c->plog_used += np;
+    c->chks.push_back({p, np, level, 0});
     return p;
 }
 
@@ -266,13 +274,15 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
     fa.eps = c->cfg.eps;
     fa.stats = c->stats;
     const bool fine = (l == 0);
+    double *lp = chk_partials(c, fa.np, l);   // speculative call: record the check, no fix-up
+    if (lp) pa.partials = lp;
     int ev = fine ? timed_begin(c, 1) : -1;
     launch_pre(pa, x0_zero, fine, c->s);
     if ((e = timed_end(c, 1, ev))) return e;
-    if (dist && c->spec_now) fa.spec = spec_slot(c, 1);
-    else if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
-    launch_pre_fixup(fa, pa, x0_zero, c->s);
-    fa.spec = nullptr;
+    if (!lp) {
+        if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
+        launch_pre_fixup(fa, pa, x0_zero, c->s);
+    }
     if ((e = enqueue_children<T>(c, l, gamma))) return e;
     if (dist) {
         if (!recomp && (e = c->comm->halo(L.B, L, 2, c->s))) return e;
@@ -298,13 +308,16 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
     po.row_hi = L.u1;
     po.gfx = l == 0 ? c->rgfx : nullptr;
     po.gsy = l == 0 ? c->rgsy : nullptr;
+    lp = chk_partials(c, fa.np, l);
+    if (lp) po.partials = lp;
     ev = fine ? timed_begin(c, 2) : -1;
     launch_post(po, fine, c->s);
     if ((e = timed_end(c, 2, ev))) return e;
-    fa.global_sum = nullptr;
-    if (dist && c->spec_now) fa.spec = spec_slot(c, 1);
-    else if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
-    launch_post_fixup(fa, po, c->s);
+    if (!lp) {
+        fa.global_sum = nullptr;
+        if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
+        launch_post_fixup(fa, po, c->s);
+    }
     return PGMG_OK;
 }
 
@@ -408,9 +421,15 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
     const bool dist = is_dist(c, 0);
     const bool cdist = is_dist(c, 1);
     const StripRows sr = strip_rows(L, C);
-    Grid gA = L.A, gB = L.B;
+    Grid gA = L.A, gB = L.B, gS = c->S;
     T *A = G<T>(gA), *B = G<T>(gB);
-    T *S = G<T>(c->S);
+    T *S = G<T>(gS);
+    // speculative call: no rare path can run, so the scratch S is free and the level-0
+    // buffers rotate through B and S; A (the call's input) is never written and a
+    // rollback restarts from it
+    const bool lean = c->lean;
+    auto grid_of = [&](const T *p) -> const Grid * { return p == A ? &gA : p == B ? &gB : &gS; };
+    auto next_of = [&](const T *p) -> T * { return lean ? (p == B ? S : B) : (p == A ? B : A); };
     const int np = fused_blocks(L.N, sr.jc0, sr.jc1);
     const int npp = postpre_blocks(L.N, sr.jc0, sr.jc1);
     FixArgsF fa{};
@@ -422,21 +441,22 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
     // cycle 1: pre-smooth (+ residual, restriction) A -> B
     if (dist && (e = c->comm->halo(gA, L, 4, c->s))) return e;
     PreArgsT<T> pa = make_pre<T>(c, A, B);
+    double *lp = chk_partials(c, np, 0);
+    if (lp) pa.partials = lp;
     int ev = timed_begin(c, 1);
     launch_pre(pa, false, true, c->s);
     if ((e = timed_end(c, 1, ev))) return e;
-    if (dist && c->spec_now) fa.spec = spec_slot(c, 1);
-    else if (dist && (e = global_sum(c, np, &fa.global_sum))) return e;
-    launch_pre_fixup(fa, pa, false, c->s);
-    fa.global_sum = nullptr;
-    fa.spec = nullptr;
-    const bool spec = dist && c->spec_now;   // no rare path can run (decisions deferred)
+    if (!lp) {
+        if (dist && (e = global_sum(c, np, &fa.global_sum))) return e;
+        launch_pre_fixup(fa, pa, false, c->s);
+        fa.global_sum = nullptr;
+    }
     T *pr = B;  // pre-smoothed solution of the current cycle
     if ((e = enqueue_children<T>(c, 0, gamma))) return e;
     for (int k = 1; k < n; ++k) {
-        T *nx = (pr == A) ? B : A;
+        T *nx = next_of(pr);
         if (dist) {
-            const HaloReq h[2] = {{pr == A ? &gA : &gB, &L, 6}, {&C.A, &C, 4}};
+            const HaloReq h[2] = {{grid_of(pr), &L, 6}, {&C.A, &C, 4}};
             if ((e = c->comm->halos(h, cdist ? 2 : 1, c->s))) return e;
         }
         PostPreArgsT<T> q{};
@@ -445,9 +465,9 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         q.f = G<T>(L.F);
         q.x4 = nx;
         q.rc = G<T>(C.F);
-        q.partials1 = c->partials;
-        q.partials2 = c->partials2;
-        q.partials3 = (dist && !spec) ? c->partials3 : nullptr;   // spec: no rare path runs
+        q.partials1 = lean ? chk_partials(c, npp, 0) : c->partials;
+        q.partials2 = lean ? chk_partials(c, npp, 0) : c->partials2;
+        q.partials3 = (dist && !lean) ? c->partials3 : nullptr;   // lean: no rare path runs
         q.gfx = c->rgfx;
         q.gsy = c->rgsy;
         q.stats = c->stats;
@@ -467,9 +487,7 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         launch_postpre(q, c->s);
         if ((e = timed_end(c, 3, ev))) return e;
         const double *g3 = nullptr;   // all-rank {post, pre, pre-from-x1} sums
-        if (spec) {
-            launch_postpre_decide(q.partials1, q.partials2, q.stats, npp, nullptr, c->cfg.eps,
-                                  c->ppflags, spec_slot(c, 2), c->s);
+        if (lean) {
             pr = nx;
             if ((e = enqueue_children<T>(c, 0, gamma))) return e;
             continue;
@@ -482,7 +500,7 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
             g3 = c->scalar;
         }
         launch_postpre_decide(q.partials1, q.partials2, q.stats, npp, g3, c->cfg.eps, c->ppflags,
-                              nullptr, c->s);
+                              c->s);
         // rare path 1 (post check fired): S = x1 of the post-smooth, then a full
         // pre-smooth from S (conditional k_pre + its own fix-up)
         PostArgsT<T> po = make_post<T>(c, pr, S);
@@ -527,19 +545,30 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         if ((e = enqueue_children<T>(c, 0, gamma))) return e;
     }
     // last cycle: post-smooth
-    T *out = (pr == A) ? B : A;
+    T *out = next_of(pr);
     if (dist) {
-        const HaloReq h[2] = {{pr == A ? &gA : &gB, &L, 2}, {&C.A, &C, 2}};
+        const HaloReq h[2] = {{grid_of(pr), &L, 2}, {&C.A, &C, 2}};
         if ((e = c->comm->halos(h, cdist ? 2 : 1, c->s))) return e;
     }
     PostArgsT<T> po = make_post<T>(c, pr, out);
+    lp = chk_partials(c, np, 0);
+    if (lp) po.partials = lp;
     ev = timed_begin(c, 2);
     launch_post(po, true, c->s);
     if ((e = timed_end(c, 2, ev))) return e;
-    if (spec) fa.spec = spec_slot(c, 1);
-    else if (dist && (e = global_sum(c, np, &fa.global_sum))) return e;
-    launch_post_fixup(fa, po, c->s);
-    if (out != A) std::swap(L.A, L.B);
+    if (!lp) {
+        if (dist && (e = global_sum(c, np, &fa.global_sum))) return e;
+        launch_post_fixup(fa, po, c->s);
+    }
+    // the solution's buffer becomes L.A (all three mirror the boundary)
+    if (lean) {
+        const Grid go = *grid_of(out), gp = *grid_of(pr);
+        L.A = go;
+        L.B = gA;
+        c->S = gp;
+    } else if (out != A) {
+        std::swap(L.A, L.B);
+    }
     return PGMG_OK;
 }
 
@@ -647,6 +676,10 @@ int pgmg_destroy(pgmg_ctx *c)
     if (c->rhs_tab) (void)hipFree(c->rhs_tab);
     if (c->fmg_gtab) (void)hipFree(c->fmg_gtab);
     if (c->uflags) (void)hipFree(c->uflags);
+    if (c->plog) (void)hipFree(c->plog);
+    if (c->chk_dev) (void)hipFree(c->chk_dev);
+    if (c->chk_norm) (void)hipFree(c->chk_norm);
+    if (c->mark_dev) (void)hipFree(c->mark_dev);
     if (c->stats_bk) (void)hipFree(c->stats_bk);
     free_grid(c->bk);
     if (c->ppflags) (void)hipFree(c->ppflags);
@@ -790,7 +823,11 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         }
     }
     if (rc == PGMG_OK && c->comm) rc = c->comm->setup(c);
-    c->spec = c->comm != nullptr && c->fused && !(cfg->flags & PGMG_FLAG_EXACT_DIST);
+    {
+        const char *ev = getenv("PGMG_SPEC");
+        c->spec = c->fused && (c->cross || c->comm != nullptr) &&
+                  !(cfg->flags & PGMG_FLAG_EXACT_DIST) && !(ev && *ev == '0');
+    }
     if (rc != PGMG_OK) {
         pgmg_destroy(c);
         return rc;
@@ -923,12 +960,15 @@ int pgmg_set_problem(pgmg_ctx *c, const double *phi0, const double *f)
     HIPC(hipMemset(c->stats, 0, 4 * sizeof(unsigned long long)));
     HIPC(hipDeviceSynchronize());
     c->have_problem = true;
+    c->spec_off = false;   // a new problem: speculate again, every level
+    c->lvl_exact.assign(c->nb + 1, 0);
+    c->lvl_hist.assign(c->nb + 1, std::vector<double>());
     return PGMG_OK;
 }
 
-static int run_cycles_plain(pgmg_ctx *c, int ncycles, int gamma)
+static int run_cycles_plain(pgmg_ctx *c, int ncycles, int gamma, bool rec0 = true)
 {
-    HIPC(hipEventRecord(c->ev0, c->s));
+    if (rec0) HIPC(hipEventRecord(c->ev0, c->s));
     const bool use_graph = gamma == 1 && !(c->cfg.flags & PGMG_FLAG_NO_GRAPH) &&
                            !(c->cfg.flags & PGMG_FLAG_TIME_FINE) && c->comm == nullptr &&
                            !c->cross;
@@ -969,65 +1009,205 @@ static int run_cycles_plain(pgmg_ctx *c, int ncycles, int gamma)
 }
 
 // ---------------------------------------------------------------------------
-// Speculative decisions (row strips).  Every smoother early-exit check on a distributed
-// level needs the all-rank residual norm; an allreduce per check is the most latency-
-// bound operation of a cycle.  A partial sum is a lower bound of the global sum (a sum of
-// non-negative doubles never rounds below one of its terms, and sqrt is monotonic), so a
-// rank whose own partial already gives sqrt(partial) >= eps knows the global check does
-// not fire.  The cycles of a call are therefore enqueued with every distributed check
-// decided "does not fire", each rank recording whether it could NOT rule the check out
-// locally.  After the call one allreduce(min) of these flags finds the checks that no
-// rank could rule out; if there is one (never at these grid sizes in practice), the
-// call is rolled back (level-0 solution and statistics restored) and run again with exact
-// per-check allreduces.  Results are therefore identical to the exact path.
+// Speculative calls.  Every smoother's early-exit check (MultiGrid.hpp via Smoother.hpp:
+// 75-88, ||r(x1)|| < eps after the first of the two sweeps) needs a grid-wide sum, so the
+// exact path follows each fused pass with a fix-up launch that reduces the pass's per-
+// block partials, decides, and recomputes the reference result when the check fired
+// (plus, at level 0 between cycles, a decision kernel and four conditional rare-path
+// launches): ~22 launches per V-cycle of a few microseconds each that almost never do
+// work.  A speculative call instead enqueues all its cycles with every check decided
+// "does not fire": each pass writes its partials into a fresh slice of a per-call log and
+// no fix-up is launched.  After the call one kernel re-reduces every recorded check
+// exactly as the fix-ups would and flags those that could fire; on row strips a rank's
+// partial is a lower bound of the all-rank sum (a sum of non-negative doubles never
+// rounds below one of its terms, sqrt is monotonic), so one allreduce(min) of the flags
+// finds the checks no rank could rule out.  If any check could fire, the call is rolled
+// back (the level-0 solution -- untouched: the cross-fused cycles rotate through the
+// scratch buffer S instead of writing A -- buffer roles and statistics restored) and run
+// again with in-stream decisions, and the context stops speculating (a fired check means
+// the solver is near convergence, where checks keep firing).  Results and statistics
+// are therefore always the exact path's.  The call ends with one host synchronisation.
 // ---------------------------------------------------------------------------
+
+// log doubles and checks of one visit of level l >= 1 (the tail decides in-kernel)
+static void spec_need_level(pgmg_ctx *c, int l, int gamma, long long *dbl, long long *nchk)
+{
+    *dbl = 0;
+    *nchk = 0;
+    if (l >= c->nb) return;
+    const Level &L = c->lv[l];
+    const int np = fused_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2);
+    long long d, k;
+    spec_need_level(c, l + 1, gamma, &d, &k);
+    *dbl = 2LL * np + gamma * d;
+    *nchk = 2 + gamma * k;
+}
+
+static int spec_reserve(pgmg_ctx *c, long long dbl, long long nchk)
+{
+    if (dbl > c->plog_cap || nchk > c->chk_cap) {
+        HIPC(hipStreamSynchronize(c->s));
+        if (dbl > c->plog_cap) {
+            if (c->plog) HIPC(hipFree(c->plog));
+            c->plog = nullptr;
+            HIPC(hipMalloc((void **)&c->plog, dbl * sizeof(double)));
+            c->plog_cap = dbl;
+        }
+        if (nchk > c->chk_cap) {
+            if (c->chk_dev) HIPC(hipFree(c->chk_dev));
+            if (c->uflags) HIPC(hipFree(c->uflags));
+            if (c->chk_norm) HIPC(hipFree(c->chk_norm));
+            c->chk_dev = nullptr;
+            c->uflags = nullptr;
+            c->chk_norm = nullptr;
+            HIPC(hipMalloc((void **)&c->chk_dev, nchk * sizeof(CheckRef)));
+            HIPC(hipMalloc((void **)&c->uflags, (nchk + 1) * sizeof(unsigned)));
+            HIPC(hipMalloc((void **)&c->chk_norm, nchk * sizeof(double)));
+            c->chk_cap = nchk;
+        }
+    }
+    if (!c->stats_bk) HIPC(hipMalloc((void **)&c->stats_bk, 4 * sizeof(unsigned long long)));
+    if (c->comm && !c->mark_dev) HIPC(hipMalloc((void **)&c->mark_dev, (c->nb + 1) * sizeof(unsigned)));
+    return PGMG_OK;
+}
+
+// Per-level policy.  Residual norms of a level fall geometrically over the V-cycles (after
+// a few cycles of growth from phi = 0) until they level off, and on the reference problem
+// the levels just above the tail reach eps after ~27 cycles at every N >= 2049
+// (scripts/spec_fire_probe.py, spec_trace.py: 0.32-0.35 per cycle in the steady phase).
+// A rollback costs a whole segment, so a coarse level whose checks are predicted to fire
+// within the next segment -- last norm x rho^cycles < 100 eps with rho = min(0.4, its
+// measured decay) -- or did fire decides in-stream from then on (its two fix-ups per visit
+// come back); the others keep speculating.  The finest
+// level is not predicted (its norm levels off far above eps at these sizes: round-off of
+// 1/h^2-scaled sums); if one of its checks does fire the context stops speculating.
+// Row strips: each rank predicts from its own partials (a lower bound of the global norm,
+// so earlier), then the ranks agree on the union of the marks (one allreduce).
+static int spec_mark_levels(pgmg_ctx *c, int cycles)
+{
+    const double lim = c->cfg.eps * 100.0;
+    std::vector<unsigned> keep(c->nb + 1, 1u);   // 1 = keep speculating
+    for (int l = 1; l < c->nb; ++l) {
+        const std::vector<double> &h = c->lvl_hist[l];
+        const size_t m = h.size();
+        if (c->lvl_exact[l] || m < 2) continue;
+        const double last = std::min(h[m - 1], h[m - 2]);   // min over the last visit
+        double rho = 0.4;
+        if (m >= 4) {
+            const double prev = std::min(h[m - 3], h[m - 4]);
+            if (prev > 0.0) rho = std::min(rho, std::max(1e-3, last / prev));
+        }
+        if (!(last * std::pow(rho, (double)cycles) >= lim)) keep[l] = 0u;
+        if (getenv("PGMG_SPEC_TRACE"))
+            fprintf(stderr, "spec level %d N=%d norms[-4..] %.3e %.3e %.3e %.3e rho %.3f next %d -> %s\n",
+                    l, c->lv[l].N, m >= 4 ? h[m - 4] : -1.0, m >= 3 ? h[m - 3] : -1.0, h[m - 2],
+                    h[m - 1], rho, cycles, keep[l] ? "speculate" : "in-stream");
+    }
+    if (c->comm) {
+        HIPC(hipMemcpyAsync(c->mark_dev, keep.data(), (c->nb + 1) * sizeof(unsigned),
+                            hipMemcpyHostToDevice, c->s));
+        int e = c->comm->allreduce_min_u32(c->mark_dev, c->nb + 1, c->s);
+        if (e) return e;
+        HIPC(hipMemcpyAsync(keep.data(), c->mark_dev, (c->nb + 1) * sizeof(unsigned),
+                            hipMemcpyDeviceToHost, c->s));
+        HIPC(hipStreamSynchronize(c->s));
+    }
+    for (int l = 1; l < c->nb; ++l)
+        if (!keep[l]) c->lvl_exact[l] = 1;
+    return PGMG_OK;
+}
+
+static void spec_record_norms(pgmg_ctx *c, int n)
+{
+    for (int i = 0; i < n; ++i) {
+        std::vector<double> &h = c->lvl_hist[c->chks[i].level];
+        h.push_back(c->hnorm[i]);
+        if (h.size() > 8) h.erase(h.begin(), h.end() - 4);
+    }
+}
+
 static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
 {
     Level &L0 = c->lv[0];
-    // flags needed: level 0 at most 3 per cycle, level l < Ld two per visit (gamma^l)
-    long long per = 3, v = 1;
-    for (int l = 1; l < c->comm->gathered_level(); ++l) {
-        v *= gamma;
-        per += 2 * v;
+    const int np0 = fused_blocks(L0.N, L0.lo / 2, (L0.hi < L0.N ? L0.hi : L0.N - 1) / 2);
+    const int npp = c->cross ? postpre_blocks(L0.N, L0.lo / 2, (L0.hi < L0.N ? L0.hi : L0.N - 1) / 2) : 0;
+    long long d1, k1;
+    spec_need_level(c, 1, gamma, &d1, &k1);
+    const long long per_dbl = 2LL * std::max(np0, npp) + d1, per_chk = 2 + k1;
+    // segments of at most 2^27 logged doubles (1 GiB) / 2^22 checks
+    long long seg_max = std::min(((1LL << 27) - 2LL * np0) / per_dbl, ((1LL << 22) - 2) / per_chk);
+    {
+        const char *ev = getenv("PGMG_SPEC_SEG");   // tests: cycles per validated segment
+        if (ev && *ev && atoi(ev) > 0) seg_max = std::min<long long>(seg_max, atoi(ev));
     }
-    const long long need = (long long)ncycles * (per + 2) + 16;
-    if (need > (long long)1 << 28) return run_cycles_plain(c, ncycles, gamma);
-    if (need > c->uflags_cap) {
-        HIPC(hipStreamSynchronize(c->s));
-        if (c->uflags) HIPC(hipFree(c->uflags));
-        HIPC(hipMalloc((void **)&c->uflags, (need + 1) * sizeof(unsigned)));
-        c->uflags_cap = (int)need;
-    }
-    if (!c->bk.base) {
-        int e = alloc_grid(c->bk, L0);
+    if (seg_max < 1) return run_cycles_plain(c, ncycles, gamma);
+    // the cross-fused cycles keep A intact (rotation through S); otherwise copy it
+    const bool rotate = c->cross && c->S.base != nullptr;
+    bool first = true;
+    while (ncycles > 0) {
+        const int seg = (int)std::min<long long>(ncycles, seg_max);
+        int e = spec_reserve(c, seg * per_dbl + 2LL * np0 + 64, seg * per_chk + 4);
         if (e) return e;
-        HIPC(hipMalloc((void **)&c->stats_bk, 4 * sizeof(unsigned long long)));
+        if ((e = spec_mark_levels(c, seg))) return e;
+        if (c->spec_off) return run_cycles_plain(c, ncycles, gamma, first);
+        const Grid A0 = L0.A, B0 = L0.B, S0 = c->S;
+        if (!rotate) {
+            if (!c->bk.base && (e = alloc_grid(c->bk, L0))) return e;
+            HIPC(hipMemcpyAsync(c->bk.base, L0.A.base, L0.A.bytes, hipMemcpyDeviceToDevice, c->s));
+        }
+        HIPC(hipMemcpyAsync(c->stats_bk, c->stats, 4 * sizeof(unsigned long long),
+                            hipMemcpyDeviceToDevice, c->s));
+        // the coarse levels' "pre-smooth fired" flags (written by the skipped fix-ups) = 0
+        HIPC(hipMemsetAsync(c->flags, 0, sizeof(unsigned) * (c->lv.size() + 1) * 2 * kMaxSweeps, c->s));
+        c->lean = true;
+        c->plog_used = 0;
+        c->chks.clear();
+        e = run_cycles_plain(c, seg, gamma, first);
+        c->lean = false;
+        first = false;
+        if (e) return e;
+        const int n = (int)c->chks.size();
+        bool overflow = false;
+        for (const CheckRef &k : c->chks) overflow |= k.np < 0;
+        unsigned h = overflow ? 1u : 0u;
+        c->hnorm.assign(n, 0.0);
+        c->hflag.assign(n, 1u);
+        if (n > 0 && !overflow) {
+            unsigned *any = c->uflags + c->chk_cap;   // the spare word past the verdicts
+            HIPC(hipMemcpyAsync(c->chk_dev, c->chks.data(), n * sizeof(CheckRef),
+                                hipMemcpyHostToDevice, c->s));
+            launch_verify_checks(c->chk_dev, n, c->cfg.eps, c->uflags, c->chk_norm, c->s);
+            if (c->comm && (e = c->comm->allreduce_min_u32(c->uflags, n, c->s))) return e;
+            launch_any_flag(c->uflags, n, any, c->s);
+            HIPC(hipMemcpyAsync(&h, any, sizeof(unsigned), hipMemcpyDeviceToHost, c->s));
+            HIPC(hipMemcpyAsync(c->hnorm.data(), c->chk_norm, n * sizeof(double),
+                                hipMemcpyDeviceToHost, c->s));
+            HIPC(hipMemcpyAsync(c->hflag.data(), c->uflags, n * sizeof(unsigned),
+                                hipMemcpyDeviceToHost, c->s));
+        }
+        HIPC(hipStreamSynchronize(c->s));
+        if (h) {
+            // some check could fire: roll back this segment, rerun the rest of the call with
+            // in-stream decisions; the levels whose checks could fire stay in-stream
+            ++c->rollbacks;
+            for (int i = 0; i < n; ++i)
+                if (c->hflag[i] || overflow) {
+                    if (c->chks[i].level == 0) c->spec_off = true;
+                    else c->lvl_exact[c->chks[i].level] = 1;
+                }
+            L0.A = A0;
+            L0.B = B0;
+            c->S = S0;
+            if (!rotate)
+                HIPC(hipMemcpyAsync(L0.A.base, c->bk.base, L0.A.bytes, hipMemcpyDeviceToDevice, c->s));
+            HIPC(hipMemcpyAsync(c->stats, c->stats_bk, 4 * sizeof(unsigned long long),
+                                hipMemcpyDeviceToDevice, c->s));
+            return run_cycles_plain(c, ncycles, gamma, false);
+        }
+        spec_record_norms(c, n);
+        ncycles -= seg;
     }
-    const Grid A0 = L0.A, B0 = L0.B;
-    HIPC(hipMemcpyAsync(c->bk.base, L0.A.base, L0.A.bytes, hipMemcpyDeviceToDevice, c->s));
-    HIPC(hipMemcpyAsync(c->stats_bk, c->stats, 4 * sizeof(unsigned long long),
-                        hipMemcpyDeviceToDevice, c->s));
-    c->uidx = 0;
-    c->spec_now = true;
-    int e = run_cycles_plain(c, ncycles, gamma);
-    c->spec_now = false;
-    if (e) return e;
-    if (c->uidx == 0) return PGMG_OK;
-    unsigned *any = c->uflags + c->uflags_cap;   // one spare slot past the flags
-    if ((e = c->comm->allreduce_min_u32(c->uflags, c->uidx, c->s))) return e;
-    launch_any_flag(c->uflags, c->uidx, any, c->s);
-    unsigned h = 0;
-    HIPC(hipMemcpyAsync(&h, any, sizeof(unsigned), hipMemcpyDeviceToHost, c->s));
-    HIPC(hipStreamSynchronize(c->s));
-    if (!h) return PGMG_OK;
-    // some check could fire: roll back and decide every check exactly
-    ++c->rollbacks;
-    L0.A = A0;
-    L0.B = B0;
-    HIPC(hipMemcpyAsync(L0.A.base, c->bk.base, L0.A.bytes, hipMemcpyDeviceToDevice, c->s));
-    HIPC(hipMemcpyAsync(c->stats, c->stats_bk, 4 * sizeof(unsigned long long),
-                        hipMemcpyDeviceToDevice, c->s));
-    return run_cycles_plain(c, ncycles, gamma);
+    return PGMG_OK;
 }
 
 static int run_cycles(pgmg_ctx *c, int ncycles, int gamma)
@@ -1035,15 +1215,27 @@ static int run_cycles(pgmg_ctx *c, int ncycles, int gamma)
     if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
     if (!c->have_problem) return set_err(PGMG_ERR_STATE, "pgmg_set_problem first");
     if (ncycles <= 0) return PGMG_OK;
-    if (c->spec && c->comm) return run_cycles_spec(c, ncycles, gamma);
+    // V-cycles only: W-cycles revisit the coarse levels until their checks fire (the
+    // reference's W-cycle at 129 exits 147 times in its first cycle), a rollback per call
+    if (c->spec && !c->spec_off && gamma == 1) return run_cycles_spec(c, ncycles, gamma);
     return run_cycles_plain(c, ncycles, gamma);
 }
 
 int pgmg_dist_info(pgmg_ctx *c, int *speculative, long long *rollbacks)
 {
     if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
-    if (speculative) *speculative = (c->spec && c->comm) ? 1 : 0;
+    if (speculative) *speculative = c->spec ? 1 : 0;
     if (rollbacks) *rollbacks = c->rollbacks;
+    return PGMG_OK;
+}
+
+int pgmg_spec_levels(pgmg_ctx *c, unsigned long long *in_stream)
+{
+    if (!c || !in_stream) return set_err(PGMG_ERR_ARG, "null argument");
+    unsigned long long m = (!c->spec || c->spec_off) ? 1ull : 0ull;
+    for (int l = 1; l < (int)c->lvl_exact.size() && l < 64; ++l)
+        if (c->lvl_exact[l]) m |= 1ull << l;
+    *in_stream = m;
     return PGMG_OK;
 }
 
@@ -1153,6 +1345,7 @@ static int enqueue_fcycle(pgmg_ctx *c)
         // zeroed; the ping-pong buffer's frame mirrors it
         launch_zero_frame(G<T>(L.A), L.P, L.N, c->s);
         launch_zero_frame(G<T>(L.B), L.P, L.N, c->s);
+        if (l == 0 && c->S.base) launch_zero_frame(G<T>(c->S), L.P, L.N, c->s);   // S mirrors too
         ProlongArgsT<T> p{};
         p.c = G<T>(C.A);
         p.fine = G<T>(L.A);

@@ -83,11 +83,8 @@ struct FixArgsF {
     unsigned long long *stats;
     const unsigned *cond;       // non-null: run only when *cond != 0
     int force;                  // recompute without deciding (rare path of k_postpre)
-    // non-null (row strips, speculative global decisions): record whether THIS rank's
-    // partial sum alone would let the check fire (sqrt(local) < eps) and do not fire; the
-    // call is validated afterwards (see pgmg_ctx.hip, "speculative decisions")
-    unsigned *spec;
 };
+
 
 using PreArgs = PreArgsT<double>;
 using PostArgs = PostArgsT<double>;
@@ -103,11 +100,13 @@ int postpre_blocks(int N, int jc0, int jc1);
 template <class T> void launch_postpre(const PostPreArgsT<T> &a, hipStream_t s);
 // flags[0] = post check fired; flags[1] = pre check fired (and post did not).
 // global != nullptr: all-rank sums {post, pre} (row strips) instead of the partials.
-// spec != nullptr (row strips, speculative): flags = 0, spec[0..1] = local post / pre
-// checks would fire (see FixArgsF::spec)
 void launch_postpre_decide(const double *partials1, const double *partials2,
                            unsigned long long *stats, int np, const double *global, double eps,
-                           unsigned *flags, unsigned *spec, hipStream_t s);
+                           unsigned *flags, hipStream_t s);
+// out[i] = 1 when check i could fire: sqrt(sum of its partials) < eps * (1 + 1e-12), the
+// sum taken in the fix-ups' order (one workgroup per check); norm[i] = that sqrt
+void launch_verify_checks(const CheckRef *checks, int n, double eps, unsigned *out, double *norm,
+                          hipStream_t s);
 
 void launch_any_flag(const unsigned *flags, int n, unsigned *out, hipStream_t s);
 

@@ -844,7 +844,7 @@ void k_postpre_lds(PostPreArgsT<T> a)
 // global != nullptr (row strips): the all-rank sums {post, pre} instead of the partials
 __global__ __launch_bounds__(256) void k_postpre_decide(const double *p1, const double *p2, int np,
                                                         const double *global, double eps,
-                                                        unsigned *flags, unsigned *spec,
+                                                        unsigned *flags,
                                                         unsigned long long *stats)
 {
     __shared__ double red[4];
@@ -859,13 +859,6 @@ __global__ __launch_bounds__(256) void k_postpre_decide(const double *p1, const 
     if (threadIdx.x == 0 && global != nullptr) {
         s1 = global[0];
         s2 = global[1];
-    }
-    if (threadIdx.x == 0 && spec != nullptr) {   // speculative (row strips): no rare path
-        spec[0] = sqrt(s1) < eps ? 1u : 0u;
-        spec[1] = sqrt(s2) < eps ? 1u : 0u;
-        flags[0] = 0u;
-        flags[1] = 0u;
-        return;
     }
     if (threadIdx.x == 0) {
         const unsigned t1 = sqrt(s1) < eps ? 1u : 0u;
@@ -1053,15 +1046,40 @@ void launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
 }
 
 void launch_postpre_decide(const double *partials1, const double *partials2, unsigned long long *stats,
-                           int np, const double *global, double eps, unsigned *flags, unsigned *spec,
-                           hipStream_t s)
+                           int np, const double *global, double eps, unsigned *flags, hipStream_t s)
 {
     k_postpre_decide<<<dim3(1), dim3(256), 0, s>>>(partials1, partials2, np, global, eps, flags,
-                                                  spec, stats);
+                                                  stats);
 }
 
-// OR over n flags (after the all-rank MIN): out = 1 when any check was undecidable locally
-// on every rank
+// Validation of a speculative call: one workgroup per recorded check re-reduces its
+// partials exactly as fix_decide / k_postpre_decide do (256 threads, strided, then the
+// block sum) and flags the checks that could fire.  The 1e-12 margin makes the flag a
+// superset of "fires" whatever order the exact path sums in (an all-rank sum of row
+// strips goes through launch_sum_partials + allreduce: relative differences below
+// ~4e-13 for the <= 3072 non-negative terms of one rank).
+__global__ __launch_bounds__(256) void k_verify_checks(const CheckRef *checks, double eps,
+                                                       unsigned *out, double *norm)
+{
+    __shared__ double red[4];
+    const CheckRef c = checks[blockIdx.x];
+    double s = 0.0;
+    for (long long k = threadIdx.x; k < c.np; k += blockDim.x) s += c.partials[k];
+    s = fused_block_sum(s, red);
+    if (threadIdx.x == 0) {
+        out[blockIdx.x] = (sqrt(s) < eps * (1.0 + 1e-12)) ? 1u : 0u;
+        norm[blockIdx.x] = sqrt(s);
+    }
+}
+
+void launch_verify_checks(const CheckRef *checks, int n, double eps, unsigned *out, double *norm,
+                          hipStream_t s)
+{
+    if (n > 0) k_verify_checks<<<dim3(n), dim3(256), 0, s>>>(checks, eps, out, norm);
+}
+
+// OR over n flags (after the all-rank MIN): out = 1 when any check could fire on every
+// rank
 __global__ __launch_bounds__(256) void k_any_flag(const unsigned *f, int n, unsigned *out)
 {
     __shared__ unsigned any;
@@ -1092,13 +1110,8 @@ __device__ __forceinline__ bool fix_decide(const FixArgsF &a, double *red, int *
     for (int k = threadIdx.x; k < a.np; k += blockDim.x) s += a.partials[k];
     s = fused_block_sum(s, red);
     if (threadIdx.x == 0) {
-        if (a.spec != nullptr) {   // speculative: never fire here, record the local verdict
-            if (blockIdx.x == 0) *a.spec = (sqrt(s) < a.eps) ? 1u : 0u;
-            *trig = 0;
-        } else {
-            const double tot = a.global_sum != nullptr ? *a.global_sum : s;
-            *trig = (sqrt(tot) < a.eps) ? 1 : 0;
-        }
+        const double tot = a.global_sum != nullptr ? *a.global_sum : s;
+        *trig = (sqrt(tot) < a.eps) ? 1 : 0;
     }
     __syncthreads();
     const bool t = *trig != 0;

@@ -19,6 +19,15 @@
 
 namespace pgmg {
 
+// one early-exit check recorded by a speculative call: the producing pass's per-block
+// partial sums of r^2 (see pgmg_ctx.hip, "speculative calls")
+struct CheckRef {
+    const double *partials;
+    long long np;
+    int level;   // host bookkeeping (per-level speculation policy)
+    int pad;
+};
+
 constexpr int kOff = 15;          // doubles between allocation base and element (0,0) (fp64)
 constexpr int kHalo = 6;          // halo rows allocated above and below a level's rows
 constexpr int kBlock = 256;       // threads per block for streaming kernels (4 waves)
