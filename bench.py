@@ -151,6 +151,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     dev_ms = s.last_elapsed_ms()
+    spec_info, spec_mask = s.dist_info(), s.spec_levels()
     vbytes = s.vcycle_bytes()
     n = N = args.n
     gen = s.fused and s.fine_pass_bytes(3) < s.fine_pass_bytes(0)   # f regenerated in-kernel
@@ -231,6 +232,9 @@ def main():
             "vcycle_algorithmic_gbps": round(vbytes / (dt / args.steps) / 1e9, 2),
             "vcycle_device_ms": round(dev_ms / args.steps, 4),
             "host_enqueue_ms_per_step": round((t_enq - t0) * 1e3 / args.steps, 4),
+            # early-exit checks recorded and validated after each call (DESIGN.md §3 point 8)
+            "speculative_checks": {"enabled": spec_info[0], "rollbacks": spec_info[1],
+                                   "in_stream_level_mask": spec_mask},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -27,6 +27,7 @@
 //
 // Every expression keeps the reference's left-to-right order; built with
 // -ffp-contract=off, so the results are bit-identical to the unfused path.
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -903,7 +904,13 @@ static void fused_geometry(int N, int jc0, int jc1, int *threads, int *gx, int *
     *threads = 64 * wpb;
     *gx = (waves + wpb - 1) / wpb;
     const int rows = jc1 - jc0;   // coarse rows
-    if (target <= 0) target = env_int("PGMG_FUSED_BLOCKS", 2048);  // tuned r01: tune_fused.py
+    // ~22k fine points per workgroup, 256 .. 3072 workgroups: measured per level at N =
+    // 16385 (scripts/level_sweep.sh): 8193 best at 3072, 4097 at 768 (band halos), and
+    // the finest level's first/last passes at 3072 (6 rounds of the 512 resident)
+    if (target <= 0) {
+        const long long pts = 2LL * rows * N;
+        target = env_int("PGMG_FUSED_BLOCKS", (int)std::min(3072LL, std::max(256LL, pts / 21845)));
+    }
     const int rmin = env_int("PGMG_FUSED_MIN_ROWS", 8);
     const int rmax = env_int("PGMG_FUSED_MAX_ROWS", 512);
     int r = (int)(((long long)rows * *gx + target - 1) / target);
@@ -934,7 +941,8 @@ void launch_pre(const PreArgsT<T> &a0, bool x0_zero, bool fine, hipStream_t s)
     a.rows_per_block = r;
     const dim3 g(gx, gy), b(t);
     // x0 = 0 (coarse levels): only f streams, so more rows in flight per lane
-    static const int p0 = env_int("PGMG_PRE0_PAIRS", 3);   // r01 sweep: 3 >= 2, 4
+    // r01 sweeps: 2 as fast as 3 on 8193, faster below (4097: 52 vs 56 us), 4 slower
+    static const int p0 = env_int("PGMG_PRE0_PAIRS", 2);
     if (x0_zero && p0 == 4) {
         k_pre<T, true, false, 4><<<g, b, 0, s>>>(a);
         return;
