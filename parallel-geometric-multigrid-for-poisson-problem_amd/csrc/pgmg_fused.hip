@@ -841,6 +841,228 @@ void k_postpre_lds(PostPreArgsT<T> a)
         postpre_lds_run<T, R2, GENF, D, MODE, false, FRECOMP>(a, k, red, sx, sf, se);
 }
 
+// ---------------------------------------------------------------------------
+// k_postpre_glds: k_postpre_lds with the rows brought into LDS by LDS-DMA
+// (global_load_lds_dwordx4 / _dword: no VGPR destination) instead of register staging.
+// One finest-level configuration (fp64, analytic f regenerated in-kernel, one GPU):
+// the register sets that held the prefetched rows (16 VGPRs) are gone, and the rows of
+// THREE pairs ahead are in flight per wave (a 4-slot LDS ring) where register staging
+// afforded two.  The DMA stays in flight across the per-pair barrier: a raw s_barrier
+// after a counted `s_waitcnt vmcnt(n)` that retires only the next pair (vector-memory
+// loads return in order, so at most n outstanding means every older load has landed;
+// stores in between only make the wait stricter).  __syncthreads() would drain it.
+// All LDS is one array (a second __shared__ object makes hipcc wait vmcnt(0) before
+// LDS reads).  Arithmetic identical to postpre_lds_run.
+// ---------------------------------------------------------------------------
+constexpr int kGlRow = 512;                   // doubles per fine LDS row (4 waves x 64 lanes x 2)
+constexpr int kGlSlots = 4;                   // row-pair slots (3 pairs in flight)
+constexpr int kGlCRow = 256;                  // doubles per coarse LDS row (2 dword DMAs per wave)
+constexpr int kGlCRing = 6;                   // coarse rows m-1 .. m+4 live
+constexpr int kGlLds = kGlSlots * kPPR * kGlRow + kGlCRing * kGlCRow + 8;   // doubles (40 KiB)
+
+// LDS-DMA in inline asm: hipcc's own bookkeeping would wait vmcnt(0) before every LDS read
+// of the staging array (it cannot tell the slots apart); the waits are counted by hand.
+// M0 = the wave-uniform LDS byte address, written in the same statement.
+__device__ __forceinline__ unsigned lds_addr(const double *p)
+{
+    return (unsigned)(unsigned long long)(const __attribute__((address_space(3))) double *)p;
+}
+
+__device__ __forceinline__ void glds16(const void *g, const double *lds_wave_base)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_wave_base)))
+                 : "memory");
+}
+
+__device__ __forceinline__ void glds4(const void *g, const double *lds_wave_base)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_wave_base)))
+                 : "memory");
+}
+
+// wait until at most n (0, 4 or 8) vector-memory operations of this wave are outstanding
+__device__ __forceinline__ void vm_wait(int n)
+{
+    if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__device__ __forceinline__ void raw_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+template <bool EDGE>
+__device__ __forceinline__ void postpre_glds_run(const PostPreArgsT<double> &a, const Cols &k,
+                                                 double *lds)
+{
+    using T = double;
+    constexpr int R = kPPR;
+    constexpr int MODE = 0;
+    double *const SXb = lds;                                   // [slot][q][kGlRow]
+    double *const SEb = lds + kGlSlots * R * kGlRow;           // [ring][kGlCRow]
+    double *const red = SEb + kGlCRing * kGlCRow;              // block-sum scratch
+    const int N = a.N, Nc = a.Nc;
+    const long long P = a.P, Pc = a.Pc;
+    const int jcb = a.jc0 + blockIdx.y * a.rows_per_block;
+    const int jce = min(jcb + a.rows_per_block, a.jc1);
+    const int olo = max(2 * jcb, a.row_lo), ohi = min(2 * jce, a.row_hi);
+    const int clo = max(jcb, max(1, a.rc_lo)), chi = min(jce, min(N / 2, a.rc_hi));
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
+        atomicAdd(&a.stats[0], 4ull);
+    ProlongCols pc;
+    pc.ic = (k.c - 1) >> 1;
+    pc.vx = k.c >= 3 && k.c <= N - 2;
+    pc.vy = k.c + 1 >= 2 && k.c + 1 <= N - 3;
+    T *__restrict__ O = a.x4 + k.c;
+    const T hh = a.hh, ih = a.ih;
+    const V2<T> z = zero2<T>();
+
+    const int wpb = blockDim.x >> 6;
+    const int t = threadIdx.x;
+    const int L0 = kPPStride * wpb * blockIdx.x + 1 - kPPMargin;
+    // Every lane issues every DMA (a wave's count of vector-memory operations per pair must
+    // be exactly 4 for the counted waits): lanes past the grid re-read its last valid pair
+    // (N - 2 is odd: 16-byte aligned); columns >= N never matter.
+    const T *__restrict__ GX = a.phi + min(L0 + 2 * t, N - 2);
+    const int cc0 = (L0 - 1) >> 1;
+    // coarse rows: dword d = i * 256 + t (i = 0, 1) of the block window, clamped likewise
+    const int dmax = 2 * (Nc - 1 - cc0) + 1;
+    const char *__restrict__ GE = reinterpret_cast<const char *>(a.ec + cc0);
+    const int ce0 = 4 * min(t, dmax), ce1 = 4 * min(256 + t, dmax);
+    const double fxa = a.gfx[k.c], fxb = a.gfx[k.c + 1];
+    const __attribute__((address_space(4))) double *gsy4 =
+        (const __attribute__((address_space(4))) double *)a.gsy;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int xo = kPPStride * w + 2 * lane;
+    const int co = (kPPStride / 2) * w + lane;
+
+    V2<T> e0 = z, e1 = z, b0 = z, b1 = z, c0 = z, c1 = z, g0 = z, g1 = z, h0 = z, h1 = z,
+            d0 = z, d1 = z;
+    V2<T> f1 = z, f2 = z, f3 = z, f4 = z, f5 = z;
+    double acc1 = 0.0, acc2 = 0.0;
+    const int i_begin = 2 * jcb - 6;
+    const int ng = (2 * (jce - jcb) + 11 + R - 1) / R;
+    const int m0 = i_begin >> 1;
+    auto ring = [](int m) { return (m + kGlCRing * 4096) % kGlCRing; };   // m >= -3
+    auto SX = [&](int slot, int q) { return SXb + (slot * R + q) * kGlRow; };
+    auto SE = [&](int r) { return SEb + r * kGlCRow; };
+    // one coarse row into ring slot r: this wave's 2 dword DMAs
+    auto issue_coarse = [&](int m) {
+        double *dst = SE(ring(m));
+        const char *src = GE + (long long)m * Pc * 8;
+        glds4(src + ce0, dst + 32 * w);
+        glds4(src + ce1, dst + 128 + 32 * w);
+    };
+    // pair p: its R rows into slot p % kGlSlots and its second coarse row (4 DMAs per wave)
+    auto issue_pair = [&](int p) {
+        #pragma unroll
+        for (int q = 0; q < R; ++q)
+            glds16(GX + (long long)(i_begin + p * R + q) * P, SX(p % kGlSlots, q) + 128 * w);
+        issue_coarse(m0 + p + 1);
+    };
+    // prologue: coarse row m0 (2 DMAs), pairs 0 .. 2 (4 each); wait for row m0 + pair 0
+    issue_coarse(m0);
+    issue_pair(0);
+    if (ng > 1) issue_pair(1);
+    if (ng > 2) issue_pair(2);
+    vm_wait(4 * (min(ng, 3) - 1));
+    raw_barrier();
+
+    T wprev = T(0);
+    for (int gi = 0; gi < ng; ++gi) {
+        if (gi + 3 < ng) issue_pair(gi + 3);   // into the slot of pair gi - 1 (read before the barrier)
+        const int slot = gi % kGlSlots;
+        const int i = i_begin + gi * R;
+        const int m = m0 + gi;
+        const T *E0 = SE(ring(m)), *E1 = SE(ring(m + 1));
+        const T cr0 = E0[co], crn0 = E0[co + 1], cr1 = E1[co], crn1 = E1[co + 1];
+        #pragma unroll
+        for (int s = 0; s < R; ++s) {
+            const int ii = i + s;
+            const V2<T> xr = ldv(SX(slot, s) + xo);
+            const double sy = gsy4[ii];   // scalar load: a vector one would be waited for
+                                          // with vmcnt(0), draining the DMAs in flight
+            const V2<T> f0 = mk2<T>((T)(fxa * sy), (T)(fxb * sy));
+            const V2<T> e2 = add_prolong<T, EDGE>(xr, ii, cr0, crn0, cr1, crn1, pc, Nc);
+            const V2<T> b2 = jsn<MODE, T, EDGE>(e0, e1, e2, nbr<T>(e1), f1, hh, k, boundary_row(ii - 1, N));
+            const Nbr<T> nb1 = nbr<T>(b1), nc1 = nbr<T>(c1), ng1 = nbr<T>(g1);
+            {
+                const V2<T> r1 = rsn<MODE, T>(b0, b1, b2, nb1, f2, ih);
+                const int row = ii - 2;
+                if (row >= olo && row < ohi && k.own) {
+                    acc1 = sqacc(acc1, r1.x);
+                    if (!k.by) acc1 = sqacc(acc1, r1.y);
+                }
+            }
+            const V2<T> c2 = jsn<MODE, T, EDGE>(b0, b1, b2, nb1, f2, hh, k, boundary_row(ii - 2, N));
+            const V2<T> g2 = jsn<MODE, T, EDGE>(c0, c1, c2, nc1, f3, hh, k, boundary_row(ii - 3, N));
+            {
+                const V2<T> r3 = rsn<MODE, T>(g0, g1, g2, ng1, f4, ih);
+                const int row = ii - 4;
+                if (row >= olo && row < ohi && k.own) {
+                    acc2 = sqacc(acc2, r3.x);
+                    if (!k.by) acc2 = sqacc(acc2, r3.y);
+                }
+            }
+            const V2<T> h2 = jsn<MODE, T, EDGE>(g0, g1, g2, ng1, f4, hh, k, boundary_row(ii - 4, N));
+            if (ii - 4 >= olo && ii - 4 < ohi && k.own) stv(O + (ii - 4) * P, h2);
+            const V2<T> d2 = rsn<MODE, T>(h0, h1, h2, nbr<T>(h1), f5, ih);
+            if ((s & 1) == 0) {
+                const int jc = (ii - 6) >> 1;
+                const T m2 = dpp_shl(d1.x);
+                const T u2 = wprev;
+                const T w2 = dpp_shl(d2.x);
+                wprev = w2;
+                const int ic = (k.c + 1) >> 1;
+                if (jc >= clo && jc < chi && k.own && ic <= Nc - 2) {
+                    const T v = T(0.25) * d1.y + T(0.125) * (m2 + d1.x + d2.y + d0.y) +
+                                T(0.0625) * (d0.x + u2 + d2.x + w2);
+                    a.rc[(long long)jc * Pc + ic] = v;
+                }
+            }
+            e0 = e1; e1 = e2;
+            b0 = b1; b1 = b2;
+            c0 = c1; c1 = c2;
+            g0 = g1; g1 = g2;
+            h0 = h1; h1 = h2;
+            d0 = d1; d1 = d2;
+            f5 = f4; f4 = f3; f3 = f2; f2 = f1; f1 = f0;
+        }
+        // pair gi + 1 must have landed: the pairs issued after it (gi + 2, gi + 3) may fly on
+        vm_wait(4 * max(0, min(gi + 3, ng - 1) - (gi + 1)));
+        raw_barrier();
+    }
+    const int slot = blockIdx.y * gridDim.x + blockIdx.x;
+    const double s1 = fused_block_sum(acc1, red);
+    __syncthreads();
+    const double s2 = fused_block_sum(acc2, red);
+    if (threadIdx.x == 0) {
+        a.partials1[slot] = s1;
+        a.partials2[slot] = s2;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_postpre_glds(PostPreArgsT<double> a)
+{
+    __shared__ __attribute__((aligned(16))) double lds[kGlLds];
+    const Cols k = lane_cols_t<kPPStride, kPPMargin>(a.N);
+    const int jcb = a.jc0 + blockIdx.y * a.rows_per_block;
+    const int jce = min(jcb + a.rows_per_block, a.jc1);
+    const bool edge_rows = 2 * jcb - 6 <= 0 || 2 * jce + 6 >= a.N - 1;
+    if (k.edge || edge_rows)
+        postpre_glds_run<true>(a, k, lds);
+    else
+        postpre_glds_run<false>(a, k, lds);
+}
+
 // one block: both decisions, stats, flags for the conditional rare-path kernels
 // global != nullptr (row strips): the all-rank sums {post, pre} instead of the partials
 __global__ __launch_bounds__(256) void k_postpre_decide(const double *p1, const double *p2, int np,
@@ -1029,6 +1251,10 @@ void launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
         // measurement knobs for the default pass (1 GPU, regenerated f)
         const int depth = env_int("PGMG_PP_DEPTH", 2), occ = env_int("PGMG_PP_OCC", 1);
         const int mode = env_int("PGMG_PP_LDS_MODE", 0);
+        if (genf && a.partials3 == nullptr && mode == 3 && t == 256) {   // LDS-DMA rows
+            k_postpre_glds<<<g, b, 0, s>>>(a);
+            return;
+        }
         if (genf && a.partials3 == nullptr && mode == 1) {
             k_postpre_lds<T, false, true, 2, 1, 1><<<g, b, 0, s>>>(a);
             return;
