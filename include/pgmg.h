@@ -126,7 +126,7 @@ int pgmg_set_problem(pgmg_ctx *ctx, const double *phi0, const double *f);
  * pgmg_fcycle: one F-cycle = restrict phi to n_coarse, then per level up smooth(3),
  * prolongation into a zeroed finer grid, analytic RHS of that grid (h chain starting at
  * 1/(n_coarse-1)), one V-cycle; the f given to pgmg_set_problem is left untouched
- * (MultiGridTestRunner.hpp:192-205).  Single GPU only (world > 1: PGMG_ERR_STATE). */
+ * (MultiGridTestRunner.hpp:192-205).  On row strips as well (world > 1). */
 int pgmg_vcycle(pgmg_ctx *ctx, int ncycles);
 int pgmg_wcycle(pgmg_ctx *ctx, int ncycles);
 int pgmg_fcycle(pgmg_ctx *ctx, int ncycles);

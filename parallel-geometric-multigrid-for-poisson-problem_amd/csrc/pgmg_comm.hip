@@ -354,11 +354,10 @@ class StripComm : public Comm {
         return t->allreduce_min_u32(d, n, s);
     }
 
-    int run_gathered(pgmg_ctx *c, int l, int gamma, int repeats) override
+    int allgather_rows(pgmg_ctx *c, int l, const Grid &g) override
     {
         Level &L = c->lv[l];
         const size_t row = (size_t)L.P * L.es;
-        // 1. every rank's rows of the coarse right-hand side -> every rank (one group)
         int e = t->group_start();
         if (e) return e;
         for (int r = 0; r < world; ++r) {
@@ -366,13 +365,20 @@ class StripComm : public Comm {
             if (b <= a) continue;
             if (r == me) {
                 for (int q = 0; q < world && !e; ++q)
-                    if (q != me) e = t->send(row_ptr(L.F, a, L.P, L.es), (b - a) * row, q, c->s);
+                    if (q != me) e = t->send(row_ptr(g, a, L.P, L.es), (b - a) * row, q, c->s);
                 if (e) return e;
-            } else if ((e = t->recv(row_ptr(L.F, a, L.P, L.es), (b - a) * row, r, c->s))) {
+            } else if ((e = t->recv(row_ptr(g, a, L.P, L.es), (b - a) * row, r, c->s))) {
                 return e;
             }
         }
-        if ((e = t->group_end(c->s))) return e;
+        return t->group_end(c->s);
+    }
+
+    int run_gathered(pgmg_ctx *c, int l, int gamma, int repeats) override
+    {
+        // 1. every rank's rows of the coarse right-hand side -> every rank (one group)
+        int e = allgather_rows(c, l, c->lv[l].F);
+        if (e) return e;
         // 2. every rank runs the rest of the hierarchy on its full copy: identical inputs,
         //    identical (pointwise, deterministic) results, so the parent's prolongation reads
         //    the correction from its own copy and no scatter is needed

@@ -160,6 +160,9 @@ class Comm {
     // the parent produced rc of gathered level l: gather it on every rank, run `repeats`
     // cycles on every rank's full copy (identical results; no scatter needed)
     virtual int run_gathered(pgmg_ctx *c, int l, int gamma, int repeats) = 0;
+    // grid g of gathered level l: every rank's rows (the ones its parent strip restricts
+    // into) to every other rank, so every rank holds the full grid (one grouped exchange)
+    virtual int allgather_rows(pgmg_ctx *c, int l, const Grid &g) = 0;
     virtual int gather_solution(pgmg_ctx *c, double *phi_host) = 0;
     static Comm *create(pgmg_ctx *c, int *rc);
 };

@@ -1306,9 +1306,19 @@ static int enqueue_fcycle(pgmg_ctx *c)
         std::vector<double> sx, sy;
         sine_tables(c->cfg, 1, 1.0, sx, sy, factor);
     }
+    int e;
     for (int l = 0; l < nb; ++l) {
-        const Level &L = c->lv[l], &C = c->lv[l + 1];
-        launch_restrict_values(G<T>(L.A), L.N, L.P, G<T>(C.A), C.N, C.P, c->s);
+        Level &L = c->lv[l], &C = c->lv[l + 1];
+        if (!is_dist(c, l)) {
+            launch_restrict_values(G<T>(L.A), L.N, L.P, G<T>(C.A), C.N, C.P, c->s);
+            continue;
+        }
+        // row strips: the rank's coarse rows from its fine rows and one halo row each side
+        const StripRows sr = strip_rows(L, C);
+        if ((e = c->comm->halo(L.A, L, 1, c->s))) return e;
+        launch_restrict_values(G<T>(L.A), L.N, L.P, G<T>(C.A), C.N, C.P, c->s, sr.rc_lo, sr.rc_hi);
+        // first replicated level: every rank's rows to every rank
+        if (!is_dist(c, l + 1) && (e = c->comm->allgather_rows(c, l + 1, C.A))) return e;
     }
     {
         Level &Lt = c->lv[nb];
@@ -1335,17 +1345,24 @@ static int enqueue_fcycle(pgmg_ctx *c)
     }
     for (int l = nb - 1; l >= 0; --l) {
         Level &L = c->lv[l];
-        const Level &C = c->lv[l + 1];
+        Level &C = c->lv[l + 1];
         const double *sx = c->fmg_tab + c->fmg_off[l];
+        const bool dist = is_dist(c, l);
+        // rows this rank holds: all, or (row strips) its strip and the halo rows, where the
+        // analytic RHS is computed locally instead of exchanged
+        const int r0 = dist ? std::max(0, L.lo - kHalo) : 0;
+        const int r1 = dist ? std::min(L.N, L.hi + kHalo) : L.N;
         // level 0's F is the F-cycle's own analytic RHS (Ffmg): the same on every call
         if (l > 0 || !c->fmg_rhs_ready)
-            launch_rhs(G<T>(L.F), sx, sx + L.N, factor, L.N, L.P, 0, L.N, c->s);
+            launch_rhs(G<T>(L.F), sx, sx + L.N, factor, L.N, L.P, r0, r1, c->s);
         // phi_fine = 0 + P phi_coarse (MultiGrid.hpp:159-164): the prolongation assigns the
         // interior, the frame (boundary, and row/column 1 the reference never corrects) is
         // zeroed; the ping-pong buffer's frame mirrors it
-        launch_zero_frame(G<T>(L.A), L.P, L.N, c->s);
-        launch_zero_frame(G<T>(L.B), L.P, L.N, c->s);
-        if (l == 0 && c->S.base) launch_zero_frame(G<T>(c->S), L.P, L.N, c->s);   // S mirrors too
+        launch_zero_frame(G<T>(L.A), L.P, L.N, c->s, r0, r1);
+        launch_zero_frame(G<T>(L.B), L.P, L.N, c->s, r0, r1);
+        if (l == 0 && c->S.base) launch_zero_frame(G<T>(c->S), L.P, L.N, c->s, r0, r1);   // S mirrors too
+        // the prolongation of the rank's rows reads one coarse row past its strip
+        if (dist && is_dist(c, l + 1) && (e = c->comm->halo(C.A, C, 1, c->s))) return e;
         ProlongArgsT<T> p{};
         p.c = G<T>(C.A);
         p.fine = G<T>(L.A);
@@ -1353,11 +1370,11 @@ static int enqueue_fcycle(pgmg_ctx *c)
         p.Pf = L.P;
         p.Wc = C.N;
         p.Pc = C.P;
-        p.row0 = 2;
-        p.row1 = L.N - 1;
+        p.row0 = dist ? std::max(L.u0, 2) : 2;
+        p.row1 = dist ? std::min(L.u1, L.N - 1) : L.N - 1;
         p.assign = 1;
-        launch_prolong(p, c->s);
-        int e = enqueue_cycle_t<T>(c, l, 1, false);
+        if (p.row1 > p.row0) launch_prolong(p, c->s);
+        e = enqueue_cycle_t<T>(c, l, 1, false);
         if (e) return e;
         if (l > 0 && (e = enqueue_smooth<T>(c, l, 0, 3, false))) return e;
     }
@@ -1370,7 +1387,6 @@ int pgmg_fcycle(pgmg_ctx *c, int ncycles)
 {
     if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
     if (!c->have_problem) return set_err(PGMG_ERR_STATE, "pgmg_set_problem first");
-    if (c->comm) return set_err(PGMG_ERR_STATE, "F-cycle runs on one GPU (world > 1: use replicas)");
     if (ncycles <= 0) return PGMG_OK;
     int e = fmg_tables(c);
     if (e) return e;

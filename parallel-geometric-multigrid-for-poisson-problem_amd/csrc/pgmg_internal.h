@@ -136,14 +136,17 @@ template <class T> size_t tail_lds_bytes(int N_top, int n_coarse);
 template <class T>
 void launch_rhs(T *f, const double *sx, const double *sy, double factor, int W, int P, int row0,
                 int row1, hipStream_t s);
-// coarse = R fine on interior coarse points (values, not residuals): compute_coarsest_grid
+// coarse = R fine on interior coarse points (values, not residuals): compute_coarsest_grid;
+// coarse rows [jc0, jc1) (clamped to the interior; row strips: the rank's rows)
 template <class T>
 void launch_restrict_values(const T *fine, int Nf, int Pf, T *coarse, int Nc, int Pc,
-                            hipStream_t s);
+                            hipStream_t s, int jc0 = 1, int jc1 = 1 << 30);
 template <class T> void launch_fill_rows(T *o, int P, int row0, int row1, hipStream_t s);
 // zero rows 0, 1, N-1 and columns 0, N-1 of an N x N grid (what a prolongation with
-// assign = 1 over rows [2, N-2] leaves unwritten)
-template <class T> void launch_zero_frame(T *o, int P, int N, hipStream_t s);
+// assign = 1 over rows [2, N-2] leaves unwritten), within rows [r0, r1) (row strips:
+// the rank's rows and halo rows)
+template <class T>
+void launch_zero_frame(T *o, int P, int N, hipStream_t s, int r0 = 0, int r1 = 1 << 30);
 template <class T>
 void launch_resnorm_partials(const T *x, const T *f, double *partials, T inv_hh, int W, int P,
                              int row0, int row1, int nblocks, hipStream_t s);

@@ -426,12 +426,13 @@ void launch_rhs(T *f, const double *sx, const double *sy, double factor, int W, 
 
 // MultiGrid.hpp:187-205 applied to values (compute_coarsest_grid, MultiGrid.hpp:28-55)
 template <class T>
-__global__ void k_restrict_values(const T *Fn, int Nf, long long Pf, T *C, int Nc, long long Pc)
+__global__ void k_restrict_values(const T *Fn, int Nf, long long Pf, T *C, int Nc, long long Pc,
+                                  int jc0, int jc1)
 {
-    const long long n = (long long)(Nc - 2) * (Nc - 2);
+    const long long n = (long long)(jc1 - jc0) * (Nc - 2);
     for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n;
          k += (long long)gridDim.x * blockDim.x) {
-        const long long jc = 1 + k / (Nc - 2), ic = 1 + k % (Nc - 2);
+        const long long jc = jc0 + k / (Nc - 2), ic = 1 + k % (Nc - 2);
         const long long q = (2 * jc) * Pf + 2 * ic;
         C[jc * Pc + ic] = T(0.25) * Fn[q] + T(0.125) * (Fn[q + 1] + Fn[q - 1] + Fn[q + Pf] + Fn[q - Pf]) +
                           T(0.0625) * (Fn[q - Pf - 1] + Fn[q - Pf + 1] + Fn[q + Pf - 1] + Fn[q + Pf + 1]);
@@ -439,12 +440,15 @@ __global__ void k_restrict_values(const T *Fn, int Nf, long long Pf, T *C, int N
 }
 
 template <class T>
-void launch_restrict_values(const T *fine, int Nf, int Pf, T *coarse, int Nc, int Pc, hipStream_t s)
+void launch_restrict_values(const T *fine, int Nf, int Pf, T *coarse, int Nc, int Pc, hipStream_t s,
+                            int jc0, int jc1)
 {
-    long long nb = ((long long)(Nc - 2) * (Nc - 2) + 255) / 256;
+    jc0 = jc0 < 1 ? 1 : jc0;
+    jc1 = jc1 > Nc - 1 ? Nc - 1 : jc1;
+    if (jc1 <= jc0) return;
+    long long nb = ((long long)(jc1 - jc0) * (Nc - 2) + 255) / 256;
     if (nb > 4096) nb = 4096;
-    if (nb < 1) nb = 1;
-    k_restrict_values<T><<<dim3((unsigned)nb), dim3(256), 0, s>>>(fine, Nf, Pf, coarse, Nc, Pc);
+    k_restrict_values<T><<<dim3((unsigned)nb), dim3(256), 0, s>>>(fine, Nf, Pf, coarse, Nc, Pc, jc0, jc1);
 }
 
 template <class T>
@@ -467,28 +471,31 @@ void launch_fill_rows(T *o, int P, int row0, int row1, hipStream_t s)
 }
 
 template <class T>
-__global__ void k_zero_frame(T *o, long long P, int N)
+__global__ void k_zero_frame(T *o, long long P, int N, int r0, int r1)
 {
-    const int n = 3 * N + 2 * (N - 3);   // rows 0, 1, N-1; columns 0, N-1 of rows 2..N-2
+    // rows 0, 1, N-1 whole; columns 0, N-1 of rows 2..N-2; only rows in [r0, r1)
+    const int a = r0 > 2 ? r0 : 2, b = r1 < N - 1 ? r1 : N - 1;
+    const int nmid = b > a ? b - a : 0;
+    const int n = 3 * N + 2 * nmid;
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-        long long q;
-        if (k < N) q = k;
-        else if (k < 2 * N) q = P + (k - N);
-        else if (k < 3 * N) q = (long long)(N - 1) * P + (k - 2 * N);
-        else {
-            const int r = k - 3 * N;            // 0 .. 2(N-3)-1
-            const long long j = 2 + (r >> 1);
-            q = j * P + ((r & 1) ? N - 1 : 0);
+        if (k < 3 * N) {
+            const int j = k < N ? 0 : (k < 2 * N ? 1 : N - 1);
+            if (j >= r0 && j < r1) o[(long long)j * P + (k % N)] = T(0);
+        } else {
+            const int r = k - 3 * N;
+            o[(long long)(a + (r >> 1)) * P + ((r & 1) ? N - 1 : 0)] = T(0);
         }
-        o[q] = T(0);
     }
 }
 
 template <class T>
-void launch_zero_frame(T *o, int P, int N, hipStream_t s)
+void launch_zero_frame(T *o, int P, int N, hipStream_t s, int r0, int r1)
 {
-    const int n = 3 * N + 2 * (N - 3);
-    k_zero_frame<T><<<dim3((n + 255) / 256), dim3(256), 0, s>>>(o, P, N);
+    r0 = r0 < 0 ? 0 : r0;
+    r1 = r1 > N ? N : r1;
+    if (r1 <= r0) return;
+    const int n = 3 * N + 2 * (r1 - r0);
+    k_zero_frame<T><<<dim3((n + 255) / 256), dim3(256), 0, s>>>(o, P, N, r0, r1);
 }
 
 // sum r(x)^2 over rows [row0,row1), interior columns — reporting only
@@ -574,9 +581,9 @@ void launch_from_double(const double *src, int N, T *dst, int P, int row0, int r
     template void launch_copy_rows<T>(const T *, T *, int, int, int, int, hipStream_t);            \
     template void launch_rhs<T>(T *, const double *, const double *, double, int, int, int, int,   \
                                 hipStream_t);                                                      \
-    template void launch_restrict_values<T>(const T *, int, int, T *, int, int, hipStream_t);      \
+    template void launch_restrict_values<T>(const T *, int, int, T *, int, int, hipStream_t, int, int); \
     template void launch_fill_rows<T>(T *, int, int, int, hipStream_t);                            \
-    template void launch_zero_frame<T>(T *, int, int, hipStream_t);                                \
+    template void launch_zero_frame<T>(T *, int, int, hipStream_t, int, int);                      \
     template void launch_resnorm_partials<T>(const T *, const T *, double *, T, int, int, int, int, \
                                              int, hipStream_t);                                    \
     template void launch_to_double<T>(const T *, int, double *, int, int, int, hipStream_t);      \
