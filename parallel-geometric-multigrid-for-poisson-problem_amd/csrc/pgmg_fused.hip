@@ -1132,8 +1132,12 @@ static void fused_geometry(int N, int jc0, int jc1, int *threads, int *gx, int *
     if (target <= 0) {
         const long long pts = 2LL * rows * N;
         target = env_int("PGMG_FUSED_BLOCKS", (int)std::min(3072LL, std::max(256LL, pts / 21845)));
+        // latency-bound levels (N <= 2049): short bands (~8k points per workgroup); measured
+        // at N = 16385: 2049 26+20 -> 23+18 us, 1025 13+11 -> 12+10, 513..129 12+10 -> 7+7
+        if (pts <= (1LL << 23))
+            target = std::max(target, env_int("PGMG_FUSED_SMALL_BLOCKS", (int)(pts / 8192)));
     }
-    const int rmin = env_int("PGMG_FUSED_MIN_ROWS", 8);
+    const int rmin = env_int("PGMG_FUSED_MIN_ROWS", 2);
     const int rmax = env_int("PGMG_FUSED_MAX_ROWS", 512);
     int r = (int)(((long long)rows * *gx + target - 1) / target);
     r = r < rmin ? rmin : (r > rmax ? rmax : r);
