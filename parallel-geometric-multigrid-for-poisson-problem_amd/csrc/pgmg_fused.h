@@ -26,6 +26,7 @@ struct PreArgsT {
     unsigned *fired;            // non-null: the fix-up records whether the check fired
     // non-null: f is the analytic RHS, regenerated as (T)(gfx[i] * gsy[j]) (level 0 only)
     const double *gfx, *gsy;
+    int nt;                     // set by launch_pre: bit 0 x2, bit 1 rc stores non-temporal
 };
 
 // prolongation + post-smooth (2 sweeps) in one pass
@@ -49,6 +50,7 @@ struct PostArgsT {
     int fix_sweeps;             // k_post_fixup: 0/1 -> x1 (the check fired), 2 -> x2
     // non-null: f is the analytic RHS, regenerated as (T)(gfx[i] * gsy[j]) (level 0 only)
     const double *gfx, *gsy;
+    int nt;                     // set by launch_post: bit 2 x2 stores non-temporal
 };
 
 // post-smooth of cycle k + pre-smooth/residual/restriction of cycle k+1 in one pass

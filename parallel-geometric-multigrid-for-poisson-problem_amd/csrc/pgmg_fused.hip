@@ -77,9 +77,10 @@ __device__ __forceinline__ bool boundary_row(int row, int N) { return row <= 0 |
 // Wave tile: STRIDE owned columns, loaded window starts MARGIN columns to the left;
 // lanes [MARGIN/2, 63 - (64*2 - STRIDE - MARGIN)/2] own their pair.
 template <int STRIDE, int MARGIN>
-__device__ __forceinline__ Cols lane_cols_t(int N)
+__device__ __forceinline__ Cols lane_cols_t(int N, int bx = -1)
 {
-    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (bx < 0) bx = blockIdx.x;
+    const int wave = (bx * blockDim.x + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     Cols k;
     k.c = STRIDE * wave + 1 - MARGIN + 2 * lane;
@@ -187,7 +188,10 @@ __global__ __launch_bounds__(256) void k_pre(PreArgsT<T> a)
                 }
             }
             const V2<T> c2 = jstage(b0, b1, b2, f1, hh, k, boundary_row(ii - 2, N));
-            if (store && ii - 2 >= olo && ii - 2 < ohi && k.own) stv(O + (ii - 2) * P, c2);
+            if (store && ii - 2 >= olo && ii - 2 < ohi && k.own) {
+                if (a.nt & 1) stv_nt(O + (ii - 2) * P, c2);
+                else stv(O + (ii - 2) * P, c2);
+            }
             // r(x2) on row ii-3 (garbage on boundary rows; never used there)
             const V2<T> d2 = rstage(c0, c1, c2, f0, ih);
             // restriction: rows ii-5, ii-4, ii-3 = 2jc-1, 2jc, 2jc+1 when ii is even
@@ -200,7 +204,8 @@ __global__ __launch_bounds__(256) void k_pre(PreArgsT<T> a)
                 if (jc >= clo && jc < chi && k.own && ic <= a.Nc - 2) {
                     const T v = T(0.25) * d1.y + T(0.125) * (m2 + d1.x + d2.y + d0.y) +
                                      T(0.0625) * (d0.x + u2 + d2.x + e2);
-                    a.rc[(long long)jc * a.Pc + ic] = v;
+                    if (a.nt & 2) __builtin_nontemporal_store(v, &a.rc[(long long)jc * a.Pc + ic]);
+                    else a.rc[(long long)jc * a.Pc + ic] = v;
                 }
             }
             a0 = a1;
@@ -357,7 +362,10 @@ __global__ __launch_bounds__(256) void k_post(PostArgsT<T> a)
                 }
             }
             const V2<T> c2 = jstage(b0, b1, b2, f1, hh, k, boundary_row(ii - 2, N));
-            if (ii - 2 >= olo && ii - 2 < ohi && k.own) stv(O + (ii - 2) * P, c2);
+            if (ii - 2 >= olo && ii - 2 < ohi && k.own) {
+                if (a.nt & 4) stv_nt(O + (ii - 2) * P, c2);
+                else stv(O + (ii - 2) * P, c2);
+            }
             a0 = a1;
             a1 = a2;
             b0 = b1;
@@ -601,24 +609,39 @@ constexpr int kPPLdsCoarse = 2 * kPPStride + kPPMargin + 8;      // 242 doubles 
 // register allocation must allow (1 = compiler's choice).
 // MODE 1 (measurement only): stencil arithmetic replaced by one add (js/rs), to separate
 // the memory/LDS cost of the pass from its VALU cost.
+// Logical block of a 2D grid (x fastest).  XCD-aware variant: the dispatcher deals
+// workgroups round-robin over the 8 XCDs (linear id i -> XCD i % 8); remap so XCD x runs a
+// contiguous range of logical blocks (neighbouring column blocks of one band share an L2).
+struct Blk {
+    int x, y;
+};
+__device__ __forceinline__ Blk xcd_block()
+{
+    const int T = gridDim.x * gridDim.y;
+    const int i = blockIdx.y * gridDim.x + blockIdx.x;
+    const int q = T >> 3, r = T & 7, x = i & 7, pos = i >> 3;
+    const int l = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + pos;
+    return Blk{l % (int)gridDim.x, l / (int)gridDim.x};
+}
+
 constexpr int kPPR = 2;   // rows per LDS slot (a row pair)
 
 // The body of k_postpre_lds for one block.  EDGE = false: no row of the block's band and
 // no column of this wave is a boundary, so the Jacobi stages carry no passthrough selects.
-template <class T, bool R2, bool GENF, int D, int MODE, bool EDGE, bool FRECOMP>
+template <class T, bool R2, bool GENF, int D, int MODE, bool EDGE, bool FRECOMP, int OPT>
 __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const Cols &k,
                                                 double *red, T (&sx)[2][kPPR][kPPLdsRow],
                                                 T (&sf)[2][kPPR][GENF ? 1 : kPPLdsRow],
-                                                T (&se)[3][kPPLdsCoarse])
+                                                T (&se)[3][kPPLdsCoarse], const Blk bk)
 {
     constexpr int R = kPPR;
     const int N = a.N, Nc = a.Nc;
     const long long P = a.P, Pc = a.Pc;
-    const int jcb = a.jc0 + blockIdx.y * a.rows_per_block;
+    const int jcb = a.jc0 + bk.y * a.rows_per_block;
     const int jce = min(jcb + a.rows_per_block, a.jc1);
     const int olo = max(2 * jcb, a.row_lo), ohi = min(2 * jce, a.row_hi);
     const int clo = max(jcb, max(1, a.rc_lo)), chi = min(jce, min(N / 2, a.rc_hi));
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
+    if (bk.x == 0 && bk.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
         atomicAdd(&a.stats[0], 4ull);
     ProlongCols pc;
     pc.ic = (k.c - 1) >> 1;
@@ -631,7 +654,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     // loader geometry: the block window starts at column L0 (odd: 16-byte aligned pairs)
     const int wpb = blockDim.x >> 6;
     const int t = threadIdx.x;
-    const int L0 = kPPStride * wpb * blockIdx.x + 1 - kPPMargin;
+    const int L0 = kPPStride * wpb * bk.x + 1 - kPPMargin;
     const int npairs = (kPPStride * wpb + 2 * kPPMargin) / 2;
     const bool ldr = t < npairs && L0 + 2 * t <= N - 1;      // columns >= N never matter
     const int cc0 = (L0 - 1) >> 1;                               // first coarse column
@@ -763,7 +786,10 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
             }
             // pre-smooth sweep 2: x4 row ii-4 (stored)
             const V2<T> h2 = jsn<MODE, T, EDGE>(g0, g1, g2, ng1, fq4, hh, k, boundary_row(ii - 4, N));
-            if (ii - 4 >= olo && ii - 4 < ohi && k.own) stv(O + (ii - 4) * P, h2);
+            if (ii - 4 >= olo && ii - 4 < ohi && k.own) {
+                if constexpr (OPT & 2) stv_nt(O + (ii - 4) * P, h2);
+                else stv(O + (ii - 4) * P, h2);
+            }
             // r(x4) on row ii-5
             const V2<T> d2 = rsn<MODE, T>(h0, h1, h2, nbr<T>(h1), fq5, ih);
             // restriction: rows ii-7, ii-6, ii-5 = 2jc-1, 2jc, 2jc+1 when ii is even
@@ -777,7 +803,8 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                 if (jc >= clo && jc < chi && k.own && ic <= Nc - 2) {
                     const T v = T(0.25) * d1.y + T(0.125) * (m2 + d1.x + d2.y + d0.y) +
                                      T(0.0625) * (d0.x + u2 + d2.x + w2);
-                    a.rc[(long long)jc * Pc + ic] = v;
+                    if constexpr (OPT & 4) __builtin_nontemporal_store(v, &a.rc[(long long)jc * Pc + ic]);
+                    else a.rc[(long long)jc * Pc + ic] = v;
                 }
             }
             e0 = e1; e1 = e2;
@@ -806,7 +833,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
             if (gi + 2 < ng) step(gi + 2, pxA, pfA, peA);
         }
     }
-    const int slot = blockIdx.y * gridDim.x + blockIdx.x;
+    const int slot = bk.y * gridDim.x + bk.x;
     const double s1 = fused_block_sum(acc1, red);
     __syncthreads();
     const double s2 = fused_block_sum(acc2, red);
@@ -822,7 +849,8 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
 }
 
 
-template <class T, bool R2, bool GENF, int D = 2, int OCC = 1, int MODE = 0, bool FRECOMP = false>
+template <class T, bool R2, bool GENF, int D = 2, int OCC = 1, int MODE = 0, bool FRECOMP = false,
+          int OPT = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC)))
 void k_postpre_lds(PostPreArgsT<T> a)
 {
@@ -830,15 +858,16 @@ void k_postpre_lds(PostPreArgsT<T> a)
     __shared__ __attribute__((aligned(16))) T sx[2][kPPR][kPPLdsRow];
     __shared__ __attribute__((aligned(16))) T sf[2][kPPR][GENF ? 1 : kPPLdsRow];
     __shared__ __attribute__((aligned(16))) T se[3][kPPLdsCoarse];
-    const Cols k = lane_cols_t<kPPStride, kPPMargin>(a.N);
+    const Blk bk = (OPT & 1) ? xcd_block() : Blk{(int)blockIdx.x, (int)blockIdx.y};
+    const Cols k = lane_cols_t<kPPStride, kPPMargin>(a.N, bk.x);
     // the band's rows 2jcb-6 .. 2jce+5 (see postpre_lds_run): does it reach row 0 or N-1?
-    const int jcb = a.jc0 + blockIdx.y * a.rows_per_block;
+    const int jcb = a.jc0 + bk.y * a.rows_per_block;
     const int jce = min(jcb + a.rows_per_block, a.jc1);
     const bool edge_rows = 2 * jcb - 6 <= 0 || 2 * jce + 6 >= a.N - 1;
     if (k.edge || edge_rows)
-        postpre_lds_run<T, R2, GENF, D, MODE, true, FRECOMP>(a, k, red, sx, sf, se);
+        postpre_lds_run<T, R2, GENF, D, MODE, true, FRECOMP, OPT>(a, k, red, sx, sf, se, bk);
     else
-        postpre_lds_run<T, R2, GENF, D, MODE, false, FRECOMP>(a, k, red, sx, sf, se);
+        postpre_lds_run<T, R2, GENF, D, MODE, false, FRECOMP, OPT>(a, k, red, sx, sf, se, bk);
 }
 
 // ---------------------------------------------------------------------------
@@ -1165,6 +1194,10 @@ void launch_pre(const PreArgsT<T> &a0, bool x0_zero, bool fine, hipStream_t s)
     fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r);
     PreArgsT<T> a = a0;
     a.rows_per_block = r;
+    // non-temporal stores on the finest level only (its x2 is read again a level-pass later;
+    // coarse outputs are re-read while still in the caches): fine k_pre 0.99 -> 0.97 ms
+    static const int nt = env_int("PGMG_NT", -1);
+    a.nt = nt >= 0 ? nt : (fine ? 1 : 0);
     const dim3 g(gx, gy), b(t);
     // x0 = 0 (coarse levels): only f streams, so more rows in flight per lane
     // r01 sweeps: 2 as fast as 3 on 8193, faster below (4097: 52 vs 56 us), 4 slower
@@ -1197,6 +1230,9 @@ void launch_post(const PostArgsT<T> &a0, bool fine, hipStream_t s)
     fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r);
     PostArgsT<T> a = a0;
     a.rows_per_block = r;
+    // fine k_post: 1.01 -> 0.93 ms with non-temporal stores (PGMG_NT: measurement)
+    static const int nt = env_int("PGMG_NT", -1);
+    a.nt = nt >= 0 ? nt : (fine ? 4 : 0);
     const dim3 g(gx, gy), b(t);
     const bool rec = a.pre_fired != nullptr;
     static const int pr = env_int("PGMG_POSTR_PAIRS", 2);
@@ -1255,6 +1291,18 @@ void launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
         // measurement knobs for the default pass (1 GPU, regenerated f)
         const int depth = env_int("PGMG_PP_DEPTH", 2), occ = env_int("PGMG_PP_OCC", 1);
         const int mode = env_int("PGMG_PP_LDS_MODE", 0);
+        // measured (r01): 2 (NT x4) 1.18 ms vs plain 1.20; XCD remap 1.25; NT rc no gain
+        const int opt = env_int("PGMG_PP_OPT", 2);   // 1 XCD remap, 2 NT x4 stores, 4 NT rc
+        if (genf && a.partials3 == nullptr && opt != 2) {
+            switch (opt) {
+            case 0: k_postpre_lds<T, false, true><<<g, b, 0, s>>>(a); break;   // plain stores
+            case 1: k_postpre_lds<T, false, true, 2, 1, 0, false, 1><<<g, b, 0, s>>>(a); break;
+            case 3: k_postpre_lds<T, false, true, 2, 1, 0, false, 3><<<g, b, 0, s>>>(a); break;
+            case 6: k_postpre_lds<T, false, true, 2, 1, 0, false, 6><<<g, b, 0, s>>>(a); break;
+            default: k_postpre_lds<T, false, true, 2, 1, 0, false, 7><<<g, b, 0, s>>>(a); break;
+            }
+            return;
+        }
         if (genf && a.partials3 == nullptr && mode == 3 && t == 256) {   // LDS-DMA rows
             k_postpre_glds<<<g, b, 0, s>>>(a);
             return;
@@ -1274,12 +1322,13 @@ void launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
             return;
         }
     }
+    // OPT 2: non-temporal x4 stores (x4 is read again only by the next cycle's pass)
     if (a.partials3 != nullptr) {
-        if (genf) k_postpre_lds<T, true, true><<<g, b, 0, s>>>(a);
-        else k_postpre_lds<T, true, false><<<g, b, 0, s>>>(a);
+        if (genf) k_postpre_lds<T, true, true, 2, 1, 0, false, 2><<<g, b, 0, s>>>(a);
+        else k_postpre_lds<T, true, false, 2, 1, 0, false, 2><<<g, b, 0, s>>>(a);
     } else {
-        if (genf) k_postpre_lds<T, false, true><<<g, b, 0, s>>>(a);
-        else k_postpre_lds<T, false, false><<<g, b, 0, s>>>(a);
+        if (genf) k_postpre_lds<T, false, true, 2, 1, 0, false, 2><<<g, b, 0, s>>>(a);
+        else k_postpre_lds<T, false, false, 2, 1, 0, false, 2><<<g, b, 0, s>>>(a);
     }
 }
 

@@ -20,6 +20,15 @@ __device__ __forceinline__ V2<T> ldv(const T *p) { return *reinterpret_cast<cons
 template <class T>
 __device__ __forceinline__ void stv(T *p, V2<T> v) { *reinterpret_cast<V2<T> *>(p) = v; }
 template <class T>
+__device__ __forceinline__ void stv_nt(T *p, V2<T> v)
+{
+    typedef T nv2 __attribute__((ext_vector_type(2)));
+    nv2 w;
+    w.x = v.x;
+    w.y = v.y;
+    __builtin_nontemporal_store(w, reinterpret_cast<nv2 *>(p));
+}
+template <class T>
 __device__ __forceinline__ V2<T> mk2(T a, T b)
 {
     V2<T> v;
