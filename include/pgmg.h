@@ -84,6 +84,10 @@ extern "C" {
                                     fix-up launch per check; on row strips an allreduce
                                     each) instead of speculatively (validated once per
                                     call, rollback on doubt; same results)            */
+#define PGMG_FLAG_SOLO 128u     /* measurement only: world > 1 with a null transport — this
+                                    rank's share of the strip work on one GPU, no messages
+                                    (halos/gathered rows stale, allreduces local); results
+                                    are meaningless, timings are one rank's compute     */
 #define PGMG_FLAG_LOOPBACK 8u    /* world > 1 with ranks as threads of one process on
                                     one GPU: nccl_unique_id is a pgmg_loopback hub
                                     (test transport for the strip decomposition)    */

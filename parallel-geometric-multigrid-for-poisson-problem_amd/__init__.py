@@ -17,7 +17,7 @@ import subprocess
 import numpy as np
 
 from ._capi import (PGMG_FLAG_LOOPBACK, PGMG_FLAG_NO_CROSS, PGMG_FLAG_NO_GRAPH,
-                    PGMG_FLAG_STORED_RHS, PGMG_FLAG_EXACT_DIST,
+                    PGMG_FLAG_STORED_RHS, PGMG_FLAG_EXACT_DIST, PGMG_FLAG_SOLO,
                     PGMG_FLAG_TIME_FINE, PGMG_PRECISION_FP32, PGMG_PRECISION_FP64,
                     PGMG_FLAG_UNFUSED, PGMG_PROLONG_REFERENCE,
                     PGMG_PROLONG_SYMMETRIC, PgmgConfig, PgmgError, check, load)
@@ -29,7 +29,7 @@ __all__ = [
     "PGMG_FLAG_NO_GRAPH", "PGMG_FLAG_TIME_FINE", "PGMG_FLAG_UNFUSED", "PGMG_FLAG_LOOPBACK", "PGMG_FLAG_NO_CROSS",
     "PGMG_PROLONG_REFERENCE", "plan_strips", "LoopbackHub", "unique_id",
     "PGMG_PROLONG_SYMMETRIC", "PGMG_PRECISION_FP64", "PGMG_PRECISION_FP32",
-    "PGMG_FLAG_STORED_RHS", "PGMG_FLAG_EXACT_DIST",
+    "PGMG_FLAG_STORED_RHS", "PGMG_FLAG_EXACT_DIST", "PGMG_FLAG_SOLO",
 ]
 
 

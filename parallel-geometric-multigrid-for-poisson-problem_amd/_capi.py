@@ -29,6 +29,7 @@ PGMG_FLAG_LOOPBACK = 8
 PGMG_FLAG_NO_CROSS = 16
 PGMG_FLAG_STORED_RHS = 32
 PGMG_FLAG_EXACT_DIST = 64
+PGMG_FLAG_SOLO = 128
 
 PGMG_PRECISION_FP64 = 0
 PGMG_PRECISION_FP32 = 1

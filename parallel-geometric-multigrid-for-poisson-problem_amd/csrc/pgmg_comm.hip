@@ -266,6 +266,19 @@ class LoopbackTransport : public Transport {
     }
 };
 
+// Null transport (PGMG_FLAG_SOLO, measurement only): no messages, allreduces return the
+// local values.  One rank of a world-W decomposition runs alone on one GPU, so its
+// compute time per cycle can be measured without W GPUs.
+class NullTransport : public Transport {
+  public:
+    int group_start() override { return PGMG_OK; }
+    int send(const void *, size_t, int, hipStream_t) override { return PGMG_OK; }
+    int recv(void *, size_t, int, hipStream_t) override { return PGMG_OK; }
+    int group_end(hipStream_t) override { return PGMG_OK; }
+    int allreduce_sum(double *, int, hipStream_t) override { return PGMG_OK; }
+    int allreduce_min_u32(unsigned *, int, hipStream_t) override { return PGMG_OK; }
+};
+
 // ---------------------------------------------------------------------------
 // strip decomposition
 // ---------------------------------------------------------------------------
@@ -420,6 +433,13 @@ Comm *Comm::create(pgmg_ctx *c, int *rc)
 {
     *rc = PGMG_OK;
     const pgmg_config &cfg = c->cfg;
+    if (cfg.flags & PGMG_FLAG_SOLO) {
+        auto *sc = new StripComm();
+        sc->me = cfg.rank;
+        sc->world = cfg.world;
+        sc->t = new NullTransport();
+        return sc;
+    }
     if (!cfg.nccl_unique_id) {
         *rc = set_err(PGMG_ERR_ARG, "world > 1 needs nccl_unique_id (or a loopback hub)");
         return nullptr;

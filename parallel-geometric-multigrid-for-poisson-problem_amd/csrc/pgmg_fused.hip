@@ -858,7 +858,18 @@ void k_postpre_lds(PostPreArgsT<T> a)
     __shared__ __attribute__((aligned(16))) T sx[2][kPPR][kPPLdsRow];
     __shared__ __attribute__((aligned(16))) T sf[2][kPPR][GENF ? 1 : kPPLdsRow];
     __shared__ __attribute__((aligned(16))) T se[3][kPPLdsCoarse];
-    const Blk bk = (OPT & 1) ? xcd_block() : Blk{(int)blockIdx.x, (int)blockIdx.y};
+    Blk bk = (OPT & 1) ? xcd_block() : Blk{(int)blockIdx.x, (int)blockIdx.y};
+    if (a.band_stride > 0) {
+        // strided band order: the grid holds R*S bands (R = band_stride, S = ceil(nb / R));
+        // dispatch slot y runs band (y % S) * R + y / S, so the bands of one dispatch round are
+        // R apart and band b+1 is dispatched about when band b retires: its top halo rows
+        // (band b's last rows) are still in the caches
+        const int nb = (a.jc1 - a.jc0 + a.rows_per_block - 1) / a.rows_per_block;
+        const int R = a.band_stride, S = (nb + R - 1) / R;
+        const int l = (bk.y % S) * R + bk.y / S;
+        if (l >= nb) return;
+        bk.y = l;
+    }
     const Cols k = lane_cols_t<kPPStride, kPPMargin>(a.N, bk.x);
     // the band's rows 2jcb-6 .. 2jce+5 (see postpre_lds_run): does it reach row 0 or N-1?
     const int jcb = a.jc0 + bk.y * a.rows_per_block;
@@ -1257,12 +1268,20 @@ void launch_post(const PostArgsT<T> &a0, bool fine, hipStream_t s)
 // k_postpre's grid target: 3072 workgroups = 6 full rounds of the 512 that are resident
 // at once (2 per CU at its ~200 VGPRs); measured r01 against 2048 .. 8192
 // (PGMG_PP_BLOCKS): 2048 1.30 ms, 3072 1.18 ms, 4096 1.25 ms, 8192 1.28 ms at N = 16385.
-static int pp_target() { return env_int("PGMG_PP_BLOCKS", 3072); }
+// Workgroups of k_postpre: whole rounds of the 512 resident (2 per CU at 184 VGPRs), about
+// one round per ~2700 fine rows: 3072 on the full 16385 grid (r01: 2048 1.30 ms, 3072 1.18,
+// 4096 1.25), 512 on strips of 2048 / 4096 rows (scripts/strip_probe.py, per-rank time at
+// 8 ranks 0.43 -> 0.39 ms; 768 / 1024, i.e. 1.5 / 2 rounds of short bands, lose)
+static int pp_target(int jc0, int jc1)
+{
+    const int rounds = std::max(1, std::min(6, 6 * (2 * (jc1 - jc0) + 64) / 16384));
+    return env_int("PGMG_PP_BLOCKS", 512 * rounds);
+}
 
 int postpre_blocks(int N, int jc0, int jc1)
 {
     int t, gx, gy, r;
-    fused_geometry(N, jc0, jc1, &t, &gx, &gy, &r, kPPStride, pp_target());
+    fused_geometry(N, jc0, jc1, &t, &gx, &gy, &r, kPPStride, pp_target(jc0, jc1));
     return gx * gy;
 }
 
@@ -1274,9 +1293,10 @@ void launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
     int t, gx, gy, r;
     const int variant = std::is_same<T, double>::value ? env_int("PGMG_PP_VARIANT", 0) : 0;
     fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, variant == 3 ? 128 : kPPStride,
-                   pp_target());
+                   pp_target(a0.jc0, a0.jc1));
     PostPreArgsT<T> a = a0;
     a.rows_per_block = r;
+    a.band_stride = 0;
     const dim3 g(gx, gy), b(t);
     if constexpr (std::is_same<T, double>::value) {
         if ((a.partials3 != nullptr || a.gfx != nullptr) && variant != 0) return;   // 1 GPU, stored f
@@ -1323,12 +1343,14 @@ void launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
         }
     }
     // OPT 2: non-temporal x4 stores (x4 is read again only by the next cycle's pass)
+    a.band_stride = env_int("PGMG_PP_BAND_STRIDE", 0);
+    const dim3 gs(gx, a.band_stride > 0 ? (gy + a.band_stride - 1) / a.band_stride * a.band_stride : gy);
     if (a.partials3 != nullptr) {
-        if (genf) k_postpre_lds<T, true, true, 2, 1, 0, false, 2><<<g, b, 0, s>>>(a);
-        else k_postpre_lds<T, true, false, 2, 1, 0, false, 2><<<g, b, 0, s>>>(a);
+        if (genf) k_postpre_lds<T, true, true, 2, 1, 0, false, 2><<<gs, b, 0, s>>>(a);
+        else k_postpre_lds<T, true, false, 2, 1, 0, false, 2><<<gs, b, 0, s>>>(a);
     } else {
-        if (genf) k_postpre_lds<T, false, true, 2, 1, 0, false, 2><<<g, b, 0, s>>>(a);
-        else k_postpre_lds<T, false, false, 2, 1, 0, false, 2><<<g, b, 0, s>>>(a);
+        if (genf) k_postpre_lds<T, false, true, 2, 1, 0, false, 2><<<gs, b, 0, s>>>(a);
+        else k_postpre_lds<T, false, false, 2, 1, 0, false, 2><<<gs, b, 0, s>>>(a);
     }
 }
 
