@@ -1171,12 +1171,18 @@ static void fused_geometry(int N, int jc0, int jc1, int *threads, int *gx, int *
     // the finest level's first/last passes at 3072 (6 rounds of the 512 resident)
     if (target <= 0) {
         const long long pts = 2LL * rows * N;
-        target = env_int("PGMG_FUSED_BLOCKS", (int)std::min(3072LL, std::max(256LL, pts / 21845)));
-        // latency-bound levels (N <= 2049): short bands (~8k points per workgroup); measured
-        // at N = 16385: 2049 26+20 -> 23+18 us, 1025 13+11 -> 12+10, 513..129 12+10 -> 7+7
-        if (pts <= (1LL << 23))
-            target = std::max(target, env_int("PGMG_FUSED_SMALL_BLOCKS", (int)(pts / 8192)));
+        if (pts > (1LL << 23)) {
+            // ~22k points per workgroup, at least one round of the 512 resident (8193 on 8
+            // strips: 37+28 -> 34+24 us), at most 3072
+            target = env_int("PGMG_FUSED_BLOCKS", (int)std::min(3072LL, std::max(512LL, pts / 21845)));
+        } else {
+            // latency-bound levels (N <= 2049): short bands (~8k points per workgroup);
+            // measured at N = 16385: 2049 26+20 -> 23+18 us, 1025 13+11 -> 12+10, 513..129
+            // 12+10 -> 7+7
+            target = env_int("PGMG_FUSED_SMALL_BLOCKS", (int)std::max(256LL, pts / 8192));
+        }
     }
+
     const int rmin = env_int("PGMG_FUSED_MIN_ROWS", 2);
     const int rmax = env_int("PGMG_FUSED_MAX_ROWS", 512);
     int r = (int)(((long long)rows * *gx + target - 1) / target);
