@@ -1185,7 +1185,11 @@ static void fused_geometry(int N, int jc0, int jc1, int *threads, int *gx, int *
 
     const int rmin = env_int("PGMG_FUSED_MIN_ROWS", 2);
     const int rmax = env_int("PGMG_FUSED_MAX_ROWS", 512);
-    int r = (int)(((long long)rows * *gx + target - 1) / target);
+    // bands so that gx * gy does not exceed the target (a target of whole rounds of the
+    // resident workgroups must not spill a few workgroups into one more round: 3096
+    // workgroups for a 3072 target cost ~2 % in k_postpre)
+    const int gymax = std::max(1, target / *gx);
+    int r = (rows + gymax - 1) / gymax;
     r = r < rmin ? rmin : (r > rmax ? rmax : r);
     if (r > rows) r = rows;
     if (r < 1) r = 1;
@@ -1342,9 +1346,9 @@ void launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
             return;
         }
         if (genf && a.partials3 == nullptr && (depth != 2 || occ != 1)) {
-            if (depth == 3 && occ == 3) k_postpre_lds<T, false, true, 3, 3><<<g, b, 0, s>>>(a);
-            else if (depth == 3) k_postpre_lds<T, false, true, 3, 1><<<g, b, 0, s>>>(a);
-            else k_postpre_lds<T, false, true, 2, 3><<<g, b, 0, s>>>(a);
+            if (depth == 3 && occ == 3) k_postpre_lds<T, false, true, 3, 3, 0, false, 2><<<g, b, 0, s>>>(a);
+            else if (depth == 3) k_postpre_lds<T, false, true, 3, 1, 0, false, 2><<<g, b, 0, s>>>(a);
+            else k_postpre_lds<T, false, true, 2, 3, 0, false, 2><<<g, b, 0, s>>>(a);
             return;
         }
     }
