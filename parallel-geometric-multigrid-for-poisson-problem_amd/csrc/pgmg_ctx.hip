@@ -97,6 +97,22 @@ static unsigned *smooth_flags(pgmg_ctx *c, int l, int which)
 
 static int timed_begin(pgmg_ctx *c, int slot);
 static int timed_end(pgmg_ctx *c, int slot, int idx);
+// k_post row range of a fused level: the strip, or on distributed levels below the finest
+// the strip plus kPostExt rows past each edge (see enqueue_fused_level)
+struct PostRows {
+    int jc0, jc1, row_lo, row_hi;
+};
+static PostRows post_rows(const pgmg_ctx *c, int l)
+{
+    const Level &L = c->lv[l];
+    PostRows r{L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2, L.u0, L.u1};
+    if (l > 0 && is_dist(c, l)) {
+        const int r0 = std::max(L.lo - kPostExt, 0), r1 = std::min(L.hi + kPostExt, L.N - 1);
+        r = {r0 / 2, r1 / 2, std::max(r0, 1), r1};
+    }
+    return r;
+}
+
 template <class T> static int enqueue_children(pgmg_ctx *c, int l, int gamma);
 template <class T> static int enqueue_cycle_t(pgmg_ctx *c, int l, int gamma, bool x0_zero);
 
@@ -241,9 +257,15 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
     const bool recomp = x0_zero && l > 0 && c->recompute;
     unsigned *fired = smooth_flags(c, l, 0) + (kMaxSweeps - 1);
     int e;
+    // row strips, levels below the finest: k_post also computes kPostExt rows past each
+    // strip edge (from deeper halos of f and phi, exchanged with the pre-smooth's anyway),
+    // so the parent's prolongation reads this level's correction without an exchange
+    const bool ext = dist && l > 0;
     if (dist) {
         if (!x0_zero && (e = c->comm->halo(L.A, L, 4, c->s))) return e;
-        if (l > 0 && (e = c->comm->halo(L.F, L, 4, c->s))) return e;
+        // f: 4 rows for k_pre, 3 + kPostExt for the extended k_post (RECOMP reads f 3 rows
+        // past its first output row)
+        if (l > 0 && (e = c->comm->halo(L.F, L, 3 + kPostExt, c->s))) return e;
     }
     PreArgsT<T> pa{};
     pa.x0 = G<T>(L.A);
@@ -284,10 +306,9 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
         launch_pre_fixup(fa, pa, x0_zero, c->s);
     }
     if ((e = enqueue_children<T>(c, l, gamma))) return e;
-    if (dist) {
-        if (!recomp && (e = c->comm->halo(L.B, L, 2, c->s))) return e;
-        if (is_dist(c, l + 1) && (e = c->comm->halo(C.A, C, 2, c->s))) return e;
-    }
+    // the correction of level l+1 is not exchanged: a distributed child's k_post computed
+    // it kPostExt rows past its strip (a gathered child's is replicated)
+    if (dist && !recomp && (e = c->comm->halo(L.B, L, ext ? 2 + kPostExt : 2, c->s))) return e;
     PostArgsT<T> po{};
     po.phi = G<T>(L.B);
     po.pre_fired = recomp ? fired : nullptr;
@@ -306,6 +327,16 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
     po.jc1 = pa.jc1;
     po.row_lo = L.u0;
     po.row_hi = L.u1;
+    if (ext) {   // rows [lo - kPostExt, hi + kPostExt) written, the strip's rows summed
+        const PostRows pr = post_rows(c, l);
+        po.jc0 = pr.jc0;
+        po.jc1 = pr.jc1;
+        po.row_lo = pr.row_lo;
+        po.row_hi = pr.row_hi;
+        po.sum_lo = L.u0;
+        po.sum_hi = L.u1;
+        fa.np = fused_blocks(L.N, po.jc0, po.jc1);
+    }
     po.gfx = l == 0 ? c->rgfx : nullptr;
     po.gsy = l == 0 ? c->rgsy : nullptr;
     lp = chk_partials(c, fa.np, l);
@@ -419,7 +450,6 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
 {
     Level &L = c->lv[0], &C = c->lv[1];
     const bool dist = is_dist(c, 0);
-    const bool cdist = is_dist(c, 1);
     const StripRows sr = strip_rows(L, C);
     Grid gA = L.A, gB = L.B, gS = c->S;
     T *A = G<T>(gA), *B = G<T>(gB);
@@ -455,9 +485,8 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
     if ((e = enqueue_children<T>(c, 0, gamma))) return e;
     for (int k = 1; k < n; ++k) {
         T *nx = next_of(pr);
-        if (dist) {
-            const HaloReq h[2] = {{grid_of(pr), &L, 6}, {&C.A, &C, 4}};
-            if ((e = c->comm->halos(h, cdist ? 2 : 1, c->s))) return e;
+        if (dist) {   // the coarse correction's halo rows were computed locally (kPostExt)
+            if ((e = c->comm->halo(*grid_of(pr), L, 6, c->s))) return e;
         }
         PostPreArgsT<T> q{};
         q.phi = pr;
@@ -546,10 +575,7 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
     }
     // last cycle: post-smooth
     T *out = next_of(pr);
-    if (dist) {
-        const HaloReq h[2] = {{grid_of(pr), &L, 2}, {&C.A, &C, 2}};
-        if ((e = c->comm->halos(h, cdist ? 2 : 1, c->s))) return e;
-    }
+    if (dist && (e = c->comm->halo(*grid_of(pr), L, 2, c->s))) return e;
     PostArgsT<T> po = make_post<T>(c, pr, out);
     lp = chk_partials(c, np, 0);
     if (lp) po.partials = lp;
@@ -787,6 +813,9 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         int nbk = sweep_blocks(L.N, L.u0, L.u1, &rpb, &gx, &gy);
         if (nbk > maxblocks) maxblocks = nbk;
         nbk = fused_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2);
+        if (nbk > maxblocks) maxblocks = nbk;
+        const PostRows pr = post_rows(c, l);
+        nbk = fused_blocks(L.N, pr.jc0, pr.jc1);
         if (nbk > maxblocks) maxblocks = nbk;
         nbk = postpre_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2);
         if (nbk > maxblocks) maxblocks = nbk;
@@ -1037,9 +1066,11 @@ static void spec_need_level(pgmg_ctx *c, int l, int gamma, long long *dbl, long 
     if (l >= c->nb) return;
     const Level &L = c->lv[l];
     const int np = fused_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2);
+    const PostRows pr = post_rows(c, l);
+    const int npo = fused_blocks(L.N, pr.jc0, pr.jc1);
     long long d, k;
     spec_need_level(c, l + 1, gamma, &d, &k);
-    *dbl = 2LL * np + gamma * d;
+    *dbl = (long long)np + npo + gamma * d;
     *nchk = 2 + gamma * k;
 }
 

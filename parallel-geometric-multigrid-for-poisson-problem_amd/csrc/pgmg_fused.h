@@ -48,6 +48,9 @@ struct PostArgsT {
     // x0 = 0 (x1 = J(0), phi = *pre_fired ? x1 : J(x1)); PreArgs::fired of the same level
     const unsigned *pre_fired;
     int fix_sweeps;             // k_post_fixup: 0/1 -> x1 (the check fired), 2 -> x2
+    int sum_lo, sum_hi;         // sum_hi > sum_lo: the early-exit partial sums cover only
+                                // these rows (the rank's own) while [row_lo, row_hi) is
+                                // written (the strip plus kPostExt rows past each edge)
     // non-null: f is the analytic RHS, regenerated as (T)(gfx[i] * gsy[j]) (level 0 only)
     const double *gfx, *gsy;
     int nt;                     // set by launch_post: bit 2 x2 stores non-temporal

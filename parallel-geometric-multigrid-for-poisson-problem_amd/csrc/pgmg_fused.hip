@@ -266,6 +266,8 @@ __global__ __launch_bounds__(256) void k_post(PostArgsT<T> a)
     const int jcb = a.jc0 + blockIdx.y * a.rows_per_block;
     const int jce = min(jcb + a.rows_per_block, a.jc1);
     const int olo = max(2 * jcb, a.row_lo), ohi = min(2 * jce, a.row_hi);
+    const int slo = a.sum_hi > a.sum_lo ? max(olo, a.sum_lo) : olo;
+    const int shi = a.sum_hi > a.sum_lo ? min(ohi, a.sum_hi) : ohi;
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
         atomicAdd(&a.stats[0], 2ull);
     ProlongCols pc;
@@ -356,7 +358,7 @@ __global__ __launch_bounds__(256) void k_post(PostArgsT<T> a)
             {
                 const int row = ii - 2;
                 const V2<T> r1 = rstage(b0, b1, b2, f1, ih);
-                if (row >= olo && row < ohi && k.own) {
+                if (row >= slo && row < shi && k.own) {
                     acc = sqacc(acc, r1.x);
                     if (!k.by) acc = sqacc(acc, r1.y);
                 }

@@ -29,7 +29,11 @@ struct CheckRef {
 };
 
 constexpr int kOff = 15;          // doubles between allocation base and element (0,0) (fp64)
-constexpr int kHalo = 6;          // halo rows allocated above and below a level's rows
+constexpr int kHalo = 10;         // halo rows allocated above and below a level's rows
+constexpr int kPostExt = 4;       // row strips: k_post of a level below the finest also
+                                  // computes this many rows of its result past each strip
+                                  // edge (bitwise what the neighbour computes), so the
+                                  // coarse correction needs no halo exchange
 constexpr int kBlock = 256;       // threads per block for streaming kernels (4 waves)
 constexpr int kTailThreads = 1024;
 constexpr int kTailMaxN = 65;     // largest level the LDS-resident tail holds

@@ -108,3 +108,19 @@ def test_strips_random_problem(pgmg):
     outs = _run_ranks(pgmg, 4, N, 2, gather_n=65, problem={r: (phi0, f) for r in range(4)})
     for phi, _, _ in outs:
         assert_bitwise(phi, ref[0], "random strips")
+
+
+@pytest.mark.parametrize("recompute", ["1", "0"])
+@pytest.mark.parametrize("kind,eps", [("V", 1e-7), ("V", 1.0), ("W", 1e-7)])
+def test_strips_extended_post_rows(pgmg, monkeypatch, recompute, kind, eps):
+    """k_post of the levels below the finest computes kPostExt rows past its strip instead
+    of exchanging the coarse correction: thin strips (16 rows at the deepest distributed
+    level), with and without the recomputed pre-smoothed iterate, V and W cycles, forced
+    coarse early exits — bitwise equal to one GPU."""
+    monkeypatch.setenv("PGMG_RECOMPUTE", recompute)
+    N = 1025
+    ref = _single(pgmg, N, 2, kind=kind, eps=eps, tail_n=17)
+    outs = _run_ranks(pgmg, 8, N, 2, kind=kind, eps=eps, tail_n=17, gather_n=65)
+    for r, (phi, stats, _) in enumerate(outs):
+        assert_bitwise(phi, ref[0], f"rank {r} recompute={recompute} {kind} eps={eps}")
+    assert outs[0][1] == ref[1]
