@@ -246,8 +246,10 @@ static int global_sum(pgmg_ctx *c, int np, const double **out)
 }
 
 // fused level (v1 = v2 = 1): k_pre (+fixup), children, k_post (+fixup)
+// pin (F-cycle climb, x0_zero false): the level's x0 is the prolongation of level l+1's
+// grid into a zeroed grid; k_pre computes it on the fly instead of reading L.A
 template <class T>
-static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
+static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool pin = false)
 {
     Level &L = c->lv[l];
     Level &C = c->lv[l + 1];
@@ -262,7 +264,7 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
     // so the parent's prolongation reads this level's correction without an exchange
     const bool ext = dist && l > 0;
     if (dist) {
-        if (!x0_zero && (e = c->comm->halo(L.A, L, 4, c->s))) return e;
+        if (!x0_zero && !pin && (e = c->comm->halo(L.A, L, 4, c->s))) return e;
         // f: 4 rows for k_pre, 3 + kPostExt for the extended k_post (RECOMP reads f 3 rows
         // past its first output row)
         if (l > 0 && (e = c->comm->halo(L.F, L, 3 + kPostExt, c->s))) return e;
@@ -290,6 +292,7 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero)
     pa.rc_hi = pa.jc1 < C.N - 1 ? pa.jc1 : C.N - 1;
     pa.gfx = l == 0 ? c->rgfx : nullptr;   // level 0 with an analytic RHS: regenerate f
     pa.gsy = l == 0 ? c->rgsy : nullptr;
+    pa.pin_ec = pin ? G<T>(C.A) : nullptr;
     FixArgsF fa{};
     fa.partials = c->partials;
     fa.np = fused_blocks(L.N, pa.jc0, pa.jc1);
@@ -1392,6 +1395,18 @@ static int enqueue_fcycle(pgmg_ctx *c)
         launch_zero_frame(G<T>(L.A), L.P, L.N, c->s, r0, r1);
         launch_zero_frame(G<T>(L.B), L.P, L.N, c->s, r0, r1);
         if (l == 0 && c->S.base) launch_zero_frame(G<T>(c->S), L.P, L.N, c->s, r0, r1);   // S mirrors too
+        static const bool use_pin = [] {
+            const char *v = getenv("PGMG_PIN");
+            return !(v && *v == '0');
+        }();
+        if (c->fused && use_pin) {
+            // the V-cycle's k_pre computes the prolongation on the fly (PIN): no separate
+            // pass writing the zeroed fine grid; it reads 3 coarse rows past the strip
+            if (dist && is_dist(c, l + 1) && (e = c->comm->halo(C.A, C, 3, c->s))) return e;
+            if ((e = enqueue_fused_level<T>(c, l, 1, false, true))) return e;
+            if (l > 0 && (e = enqueue_smooth<T>(c, l, 0, 3, false))) return e;
+            continue;
+        }
         // the prolongation of the rank's rows reads one coarse row past its strip
         if (dist && is_dist(c, l + 1) && (e = c->comm->halo(C.A, C, 1, c->s))) return e;
         ProlongArgsT<T> p{};

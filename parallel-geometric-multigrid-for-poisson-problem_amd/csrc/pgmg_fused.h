@@ -27,6 +27,10 @@ struct PreArgsT {
     // non-null: f is the analytic RHS, regenerated as (T)(gfx[i] * gsy[j]) (level 0 only)
     const double *gfx, *gsy;
     int nt;                     // set by launch_pre: bit 0 x2, bit 1 rc stores non-temporal
+    // non-null (F-cycle): x0 is not read but is the prolongation of this coarse grid into a
+    // zeroed fine grid, x0 = (+0) + P ec on rows/columns [2, N-2], 0 on the frame
+    // (MultiGrid.hpp:159-164 followed by the V-cycle's pre-smooth)
+    const T *pin_ec;
 };
 
 // prolongation + post-smooth (2 sweeps) in one pass

@@ -107,11 +107,36 @@ __device__ __forceinline__ double fused_block_sum(double v, double *red)
     return s;
 }
 
+struct ProlongCols {
+    bool vx, vy;   // column c / c+1 receives a correction
+    int ic;        // coarse column of the odd fine column c: (c-1)/2
+};
+
+// EDGE = false: the caller guarantees row in [2, Nf-2] and both columns in [2, Nf-2]
+// (interior bands and wave tiles), so no masks
+template <class T, bool EDGE = true>
+__device__ __forceinline__ V2<T> add_prolong(V2<T> p, int row, T ca, T cb, T da, T db, const ProlongCols &pc, int Nc)
+{
+    // MultiGrid.hpp:219-223; row in [2, Nf-2] <=> its coarse row m in [1, Nc-2]
+    const int m = row >> 1;
+    if (EDGE && (m < 1 || m > Nc - 2)) return p;
+    if ((row & 1) == 0) {
+        if (!EDGE || pc.vx) p.x = p.x + T(0.5) * (ca + cb);
+        if (!EDGE || pc.vy) p.y = p.y + cb;
+    } else {
+        if (!EDGE || pc.vx) p.x = p.x + T(0.25) * (ca + cb + da + db);
+        if (!EDGE || pc.vy) p.y = p.y + T(0.5) * (cb + db);
+    }
+    return p;
+}
+
 // ---------------------------------------------------------------------------
 // k_pre
 // ---------------------------------------------------------------------------
 // GENF: f is the analytic RHS, regenerated per row from the gfx/gsy tables (see k_postpre_lds)
-template <class T, bool X0_ZERO, bool FINE, int PAIRS, bool GENF = false>
+// PIN (F-cycle): x0 = (+0) + P ec (a.pin_ec), computed per row from the coarse rows
+// (2 B/point read instead of 8, and the prolongation pass into the zeroed grid is gone)
+template <class T, bool X0_ZERO, bool FINE, int PAIRS, bool GENF = false, bool PIN = false>
 __global__ __launch_bounds__(256) void k_pre(PreArgsT<T> a)
 {
     constexpr int R = 2 * PAIRS;  // rows loaded per iteration (and prefetched ahead)
@@ -146,29 +171,66 @@ __global__ __launch_bounds__(256) void k_pre(PreArgsT<T> a)
     const int i_end = idle ? i_begin
                            : i_begin + ((2 * (jce - jcb) + 8 + R - 1) / R) * R;
     V2<T> nx[R], nf[R];
+    // PIN: coarse rows (i >> 1) .. (i >> 1) + PAIRS of an iteration starting at row i
+    ProlongCols pc;
+    pc.ic = (k.c - 1) >> 1;
+    pc.vx = k.c >= 3 && k.c <= N - 2;
+    pc.vy = k.c + 1 >= 2 && k.c + 1 <= N - 3;
+    const T *__restrict__ E = PIN ? a.pin_ec + pc.ic : nullptr;
+    const long long Pc = a.Pc;
+    // both coarse columns ic and ic+1 are loaded (no DPP for ic+1): the wave's last lane
+    // needs column ic+1 too, since k_pre's four stencil levels after x0 use the whole
+    // 4-column margin of the 128-column tile
+    T ncr[PAIRS + 1], ncrn[PAIRS + 1];
     #pragma unroll
     for (int q = 0; q < R; ++q) {
-        nx[q] = (X0_ZERO || idle) ? z : ldv(X + (i_begin + q) * P);
+        nx[q] = (X0_ZERO || PIN || idle) ? z : ldv(X + (i_begin + q) * P);
         if constexpr (!GENF) nf[q] = idle ? z : ldv(F + (i_begin + q) * P);
+    }
+    if constexpr (PIN) {
+        #pragma unroll
+        for (int q = 0; q <= PAIRS; ++q) {
+            ncr[q] = idle ? T(0) : E[(long long)((i_begin >> 1) + q) * Pc];
+            ncrn[q] = idle ? T(0) : E[(long long)((i_begin >> 1) + q) * Pc + 1];
+        }
     }
     for (int i = i_begin; i < i_end; i += R) {
         V2<T> cx[R], cf[R];
+        T cr[PAIRS + 1], crn[PAIRS + 1];
         #pragma unroll
         for (int q = 0; q < R; ++q) {
             cx[q] = nx[q];
             if constexpr (!GENF) cf[q] = nf[q];
         }
+        if constexpr (PIN) {
+            #pragma unroll
+            for (int q = 0; q <= PAIRS; ++q) {
+                cr[q] = ncr[q];
+                crn[q] = ncrn[q];
+            }
+        }
         if (i + R < i_end) {  // prefetch the next R rows
             #pragma unroll
             for (int q = 0; q < R; ++q) {
-                if (!X0_ZERO) nx[q] = ldv(X + (i + R + q) * P);
+                if (!X0_ZERO && !PIN) nx[q] = ldv(X + (i + R + q) * P);
                 if constexpr (!GENF) nf[q] = ldv(F + (i + R + q) * P);
+            }
+            if constexpr (PIN) {
+                #pragma unroll
+                for (int q = 0; q <= PAIRS; ++q) {
+                    ncr[q] = E[(long long)(((i + R) >> 1) + q) * Pc];
+                    ncrn[q] = E[(long long)(((i + R) >> 1) + q) * Pc + 1];
+                }
             }
         }
         #pragma unroll
         for (int s = 0; s < R; ++s) {
             const int ii = i + s;
-            const V2<T> a2 = cx[s];
+            V2<T> a2 = cx[s];
+            if constexpr (PIN) {
+                const int pq = s >> 1;
+                a2 = add_prolong(z, ii, cr[pq], crn[pq], cr[pq + 1], crn[pq + 1], pc, a.Nc);
+            }
             V2<T> f3;
             if constexpr (GENF) {
                 const double sy = a.gsy[ii];
@@ -228,29 +290,6 @@ __global__ __launch_bounds__(256) void k_pre(PreArgsT<T> a)
 // ---------------------------------------------------------------------------
 // k_post
 // ---------------------------------------------------------------------------
-struct ProlongCols {
-    bool vx, vy;   // column c / c+1 receives a correction
-    int ic;        // coarse column of the odd fine column c: (c-1)/2
-};
-
-// EDGE = false: the caller guarantees row in [2, Nf-2] and both columns in [2, Nf-2]
-// (interior bands and wave tiles), so no masks
-template <class T, bool EDGE = true>
-__device__ __forceinline__ V2<T> add_prolong(V2<T> p, int row, T ca, T cb, T da, T db, const ProlongCols &pc, int Nc)
-{
-    // MultiGrid.hpp:219-223; row in [2, Nf-2] <=> its coarse row m in [1, Nc-2]
-    const int m = row >> 1;
-    if (EDGE && (m < 1 || m > Nc - 2)) return p;
-    if ((row & 1) == 0) {
-        if (!EDGE || pc.vx) p.x = p.x + T(0.5) * (ca + cb);
-        if (!EDGE || pc.vy) p.y = p.y + cb;
-    } else {
-        if (!EDGE || pc.vx) p.x = p.x + T(0.25) * (ca + cb + da + db);
-        if (!EDGE || pc.vy) p.y = p.y + T(0.5) * (cb + db);
-    }
-    return p;
-}
-
 // RECOMP (levels entered with x0 = 0): phi is not read.  The loaded row is f[ii+1];
 // x1 = J(0) is pointwise, so x1 row ii+1 -> phi row ii = J(x1) (or x1 when the pre
 // check fired) -> x_eff row ii: one more row of lag than reading phi, 16 B/point less.
@@ -1222,6 +1261,12 @@ void launch_pre(const PreArgsT<T> &a0, bool x0_zero, bool fine, hipStream_t s)
     static const int nt = env_int("PGMG_NT", -1);
     a.nt = nt >= 0 ? nt : (fine ? 1 : 0);
     const dim3 g(gx, gy), b(t);
+    if (a.pin_ec != nullptr) {   // F-cycle: x0 = prolongation of the coarse grid
+        if (fine && a.gfx != nullptr) k_pre<T, false, true, 2, true, true><<<g, b, 0, s>>>(a);
+        else if (fine) k_pre<T, false, true, 2, false, true><<<g, b, 0, s>>>(a);
+        else k_pre<T, false, false, 2, false, true><<<g, b, 0, s>>>(a);
+        return;
+    }
     // x0 = 0 (coarse levels): only f streams, so more rows in flight per lane
     // r01 sweeps: 2 as fast as 3 on 8193, faster below (4097: 52 vs 56 us), 4 slower
     static const int p0 = env_int("PGMG_PRE0_PAIRS", 2);
@@ -1452,11 +1497,16 @@ struct FixCtx {
     T hh, ih;
     bool x0_zero;
     const unsigned *pre_fired;  // non-null: phi (x0 of fxeff) is recomputed from f
+    bool pin;                   // x0 = (+0) + P ec (k_pre PIN, F-cycle)
 };
+
+template <class T>
+__device__ T fxpin(const FixCtx<T> &c, int j, int i);
 
 template <class T>
 __device__ __forceinline__ T fx0(const FixCtx<T> &c, int j, int i)
 {
+    if (c.pin) return fxpin(c, j, i);
     return c.x0_zero ? T(0) : c.x0[(long long)j * c.P + i];
 }
 
@@ -1487,6 +1537,25 @@ __device__ T fxeff(const FixCtx<T> &c, int j, int i)
     T w;
     if ((j & 1) == 0) {
         w = ((i & 1) == 0) ? C0[ic] : T(0.5) * (C0[ic] + C0[ic + 1]);
+    } else {
+        const T *C1 = C0 + c.Pc;
+        w = ((i & 1) == 0) ? T(0.5) * (C0[ic] + C1[ic]) : T(0.25) * (C0[ic] + C0[ic + 1] + C1[ic] + C1[ic + 1]);
+    }
+    return v + w;
+}
+
+// x0 of a PIN pre-smooth: the prolongation of ec into a zeroed grid (frame 0)
+template <class T>
+__device__ T fxpin(const FixCtx<T> &c, int j, int i)
+{
+    const T v = T(0);
+    if (j < 2 || i < 2 || j > c.N - 2 || i > c.N - 2) return v;
+    const int jc = j >> 1, ic = i >> 1;
+    const T *C0 = c.ec + (long long)jc * c.Pc;
+    T w;
+    if ((j & 1) == 0) {
+        if ((i & 1) == 0) return v + C0[ic];
+        w = T(0.5) * (C0[ic] + C0[ic + 1]);
     } else {
         const T *C1 = C0 + c.Pc;
         w = ((i & 1) == 0) ? T(0.5) * (C0[ic] + C1[ic]) : T(0.25) * (C0[ic] + C0[ic + 1] + C1[ic] + C1[ic + 1]);
@@ -1533,7 +1602,8 @@ __global__ __launch_bounds__(256) void k_pre_fixup(FixArgsF a, PreArgsT<T> p, in
     const bool t = fix_decide(a, red, &trig);
     if (p.fired != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *p.fired = t ? 1u : 0u;
     if (!t) return;
-    FixCtx<T> c{p.x0, p.f, nullptr, p.N, p.Nc, p.P, p.Pc, p.hh, p.ih, x0_zero != 0, nullptr};
+    FixCtx<T> c{p.x0, p.f, p.pin_ec, p.N, p.Nc, p.P, p.Pc, p.hh, p.ih, x0_zero != 0, nullptr,
+                p.pin_ec != nullptr};
     const long long W = p.N - 2;
     const long long nrows = p.x2 != nullptr ? (long long)(p.row_hi - p.row_lo) : 0;
     const long long stride = (long long)gridDim.x * blockDim.x;

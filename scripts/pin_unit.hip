@@ -1,0 +1,136 @@
+// Unit check of k_pre's PIN input stage (x0 = (+0) + P ec computed in-kernel): the pass
+// with PIN and the pass reading the same x0 (the prolongation into a zeroed grid, computed
+// on the host) must write bitwise the same x2 and rc.  Generous padding around every buffer.
+//   hipcc --offload-arch=gfx950 -std=c++17 -I../include scripts/pin_unit.hip -L<pkg> -lpgmg
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+#include "../parallel-geometric-multigrid-for-poisson-problem_amd/csrc/pgmg_fused.h"
+
+namespace pgmg {
+template <class T> void launch_pre(const PreArgsT<T> &a, bool x0_zero, bool fine, hipStream_t s);
+}
+
+int main(int argc, char **argv)
+{
+    const int N = argc > 1 ? atoi(argv[1]) : 129, Nc = (N - 1) / 2 + 1;
+    const int P = (N + 15) / 16 * 16, Pc = (Nc + 15) / 16 * 16;
+    const int pad_rows = 64;
+    const size_t fine_elems = (size_t)(N + 2 * pad_rows) * P + 4096;
+    const size_t coarse_elems = (size_t)(Nc + 2 * pad_rows) * Pc + 4096;
+    double *fb, *xb, *cb, *rb, *part;
+    hipMalloc(&fb, fine_elems * 8);
+    hipMalloc(&xb, fine_elems * 8);
+    hipMalloc(&cb, coarse_elems * 8);
+    hipMalloc(&rb, coarse_elems * 8);
+    hipMalloc(&part, 1 << 20);
+    hipMemset(fb, 0, fine_elems * 8);
+    hipMemset(xb, 0, fine_elems * 8);
+    hipMemset(rb, 0, coarse_elems * 8);
+    // origins: 15 doubles + pad_rows rows in (column 1 on a 128-byte boundary like the library)
+    double *f = fb + 15 + (size_t)pad_rows * P, *x = xb + 15 + (size_t)pad_rows * P;
+    double *c = cb + 15 + (size_t)pad_rows * Pc, *r = rb + 15 + (size_t)pad_rows * Pc;
+    std::vector<double> hc(coarse_elems, 0.0);
+    for (int m = 0; m < Nc; ++m)
+        for (int i = 0; i < Nc; ++i) hc[15 + (size_t)(pad_rows + m) * Pc + i] = 1000.0 * m + i + 0.25;
+    hipMemcpy(cb, hc.data(), coarse_elems * 8, hipMemcpyHostToDevice);
+    pgmg::PreArgsT<double> a{};
+    a.x0 = x;
+    a.f = f;
+    a.x2 = x;
+    a.rc = r;
+    a.partials = part;
+    a.hh = 1.0;
+    a.ih = 1.0;
+    a.N = N;
+    a.P = P;
+    a.Nc = Nc;
+    a.Pc = Pc;
+    a.jc0 = 0;
+    a.jc1 = (N - 1) / 2;
+    a.row_lo = 1;
+    a.row_hi = N - 1;
+    a.rc_lo = 1;
+    a.rc_hi = Nc - 1;
+    const bool fine = argc > 2 && atoi(argv[2]) != 0;
+    double *gt;
+    hipMalloc(&gt, (size_t)(4 * P + 8192) * 8);
+    hipMemset(gt, 0, (size_t)(4 * P + 8192) * 8);
+    if (fine) {   // regenerated f: tables valid from index -8 (contents irrelevant here)
+        a.gfx = gt + 1024;
+        a.gsy = gt + 1024 + 2 * P + 1024;
+    }
+    a.pin_ec = c;
+    // x0 = the prolongation of c into a zeroed grid, on the host
+    auto C = [&](int m, int i) { return hc[15 + (size_t)(pad_rows + m) * Pc + i]; };
+    std::vector<double> hx(fine_elems, 0.0);
+    for (int j = 2; j <= N - 2; ++j)
+        for (int i = 2; i <= N - 2; ++i) {
+            const int jc = j >> 1, ic = i >> 1;
+            double w;
+            if ((j & 1) == 0)
+                w = (i & 1) == 0 ? C(jc, ic) : 0.5 * (C(jc, ic) + C(jc, ic + 1));
+            else
+                w = (i & 1) == 0 ? 0.5 * (C(jc, ic) + C(jc + 1, ic))
+                                 : 0.25 * (C(jc, ic) + C(jc, ic + 1) + C(jc + 1, ic) + C(jc + 1, ic + 1));
+            hx[15 + (size_t)(pad_rows + j) * P + i] = 0.0 + w;
+        }
+    hipMemcpy(xb, hx.data(), fine_elems * 8, hipMemcpyHostToDevice);
+    hipError_t e = hipSuccess;
+    int bad = 0;
+    // full pass: PIN vs non-PIN k_pre from the same x0 (written by the debug run above into
+    // x), f = 1: compare x2 and rc bitwise
+    {
+        std::vector<double> one(fine_elems, 1.0);
+        hipMemcpy(fb, one.data(), fine_elems * 8, hipMemcpyHostToDevice);
+        double *x2a, *x2b, *rca, *rcb;
+        hipMalloc(&x2a, fine_elems * 8);
+        hipMalloc(&x2b, fine_elems * 8);
+        hipMalloc(&rca, coarse_elems * 8);
+        hipMalloc(&rcb, coarse_elems * 8);
+        hipMemset(x2a, 0, fine_elems * 8);
+        hipMemset(x2b, 0, fine_elems * 8);
+        hipMemset(rca, 0, coarse_elems * 8);
+        hipMemset(rcb, 0, coarse_elems * 8);
+        pgmg::PreArgsT<double> b = a;
+        b.nt = 0;
+        b.hh = 1.0 / 4096;
+        b.ih = 4096.0;
+        b.x2 = x2a + 15 + (size_t)pad_rows * P;
+        b.rc = rca + 15 + (size_t)pad_rows * Pc;
+        pgmg::launch_pre(b, false, fine, nullptr);   // PIN
+        pgmg::PreArgsT<double> q = b;
+        q.pin_ec = nullptr;
+        q.x0 = x;
+        q.x2 = x2b + 15 + (size_t)pad_rows * P;
+        q.rc = rcb + 15 + (size_t)pad_rows * Pc;
+        pgmg::launch_pre(q, false, fine, nullptr);   // x0 read from x
+        e = hipDeviceSynchronize();
+        if (e != hipSuccess) {
+            printf("error %s\n", hipGetErrorString(e));
+            return 1;
+        }
+        std::vector<double> ha(fine_elems), hb(fine_elems), ra(coarse_elems), rbv(coarse_elems);
+        hipMemcpy(ha.data(), x2a, fine_elems * 8, hipMemcpyDeviceToHost);
+        hipMemcpy(hb.data(), x2b, fine_elems * 8, hipMemcpyDeviceToHost);
+        hipMemcpy(ra.data(), rca, coarse_elems * 8, hipMemcpyDeviceToHost);
+        hipMemcpy(rbv.data(), rcb, coarse_elems * 8, hipMemcpyDeviceToHost);
+        int bx = 0, br = 0;
+        for (size_t k = 0; k < fine_elems; ++k)
+            if (ha[k] != hb[k] && bx++ < 8) {
+                const long long o = (long long)k - 15 - (long long)pad_rows * P;
+                printf("x2 row %lld col %lld: pin %.6g ref %.6g\n", o / P, o % P, ha[k], hb[k]);
+            }
+        for (size_t k = 0; k < coarse_elems; ++k)
+            if (ra[k] != rbv[k] && br++ < 8) {
+                const long long o = (long long)k - 15 - (long long)pad_rows * Pc;
+                printf("rc row %lld col %lld: pin %.6g ref %.6g\n", o / Pc, o % Pc, ra[k], rbv[k]);
+            }
+        printf("N=%d fine=%d: x2 mismatches %d rc mismatches %d\n", N, (int)fine, bx, br);
+        bad += bx + br;
+    }
+    return bad != 0;
+}
