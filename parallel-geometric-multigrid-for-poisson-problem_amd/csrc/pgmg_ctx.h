@@ -70,6 +70,7 @@ struct pgmg_ctx {
     unsigned long long *stats = nullptr;
     double *scalar = nullptr;
     hipGraphExec_t gexec = nullptr;
+    bool fsmooth_swapped = false; // an F-cycle swapped L.A / L.B of a level (fused smooth(3))
     bool have_problem = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     struct EventPool {

@@ -823,13 +823,13 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         nbk = postpre_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2);
         if (nbk > maxblocks) maxblocks = nbk;
     }
-    if (rc == PGMG_OK && c->cross) {
-        rc = alloc_grid(c->S, c->lv[0]);
-        if (rc == PGMG_OK && (hipMalloc((void **)&c->partials2, sizeof(double) * maxblocks) != hipSuccess ||
-                              hipMalloc((void **)&c->partials3, sizeof(double) * maxblocks) != hipSuccess ||
-                              hipMalloc((void **)&c->ppflags, 4 * sizeof(unsigned)) != hipSuccess))
-            rc = set_err(PGMG_ERR_NOMEM, "cross-cycle buffers");
-    }
+    if (rc == PGMG_OK && c->cross) rc = alloc_grid(c->S, c->lv[0]);
+    // partial sums of k_postpre's second and third checks (cross-cycle fusion, and the
+    // F-cycle's fused smooth(3)), its decision flags
+    if (rc == PGMG_OK && (hipMalloc((void **)&c->partials2, sizeof(double) * maxblocks) != hipSuccess ||
+                          hipMalloc((void **)&c->partials3, sizeof(double) * maxblocks) != hipSuccess ||
+                          hipMalloc((void **)&c->ppflags, 4 * sizeof(unsigned)) != hipSuccess))
+        rc = set_err(PGMG_ERR_NOMEM, "cross-cycle buffers");
     c->partials_cap = maxblocks;
     if (rc == PGMG_OK && hipMalloc((void **)&c->partials, sizeof(double) * maxblocks) != hipSuccess)
         rc = set_err(PGMG_ERR_NOMEM, "partials");
@@ -1331,6 +1331,52 @@ static int fmg_tables(pgmg_ctx *c)
 // the V-cycle kernels with the level's F replaced by the analytic RHS of the FMG chain.
 }  // extern "C"
 
+// smooth(3) of the F-cycle climb (MultiGrid.hpp:153) on a bulk level, fused: four sweeps in
+// one pass into L.B with the three checks summed speculatively, the decision, the exact
+// rare path (x_k from the untouched x0), then L.A and L.B trade places (both frames zero)
+template <class T>
+static int enqueue_smooth3_fused(pgmg_ctx *c, int l)
+{
+    Level &L = c->lv[l];
+    const bool dist = is_dist(c, l);
+    int e;
+    // x0 is read 6 rows past the strip (the pass's pipeline), f is local (analytic)
+    if (dist && (e = c->comm->halo(L.A, L, 6, c->s))) return e;
+    PostPreArgsT<T> q{};
+    q.phi = G<T>(L.A);
+    q.f = G<T>(L.F);
+    q.x4 = G<T>(L.B);
+    q.partials1 = c->partials;
+    q.partials2 = c->partials2;
+    q.partials3 = c->partials3;
+    q.hh = (T)L.hh;
+    q.ih = (T)L.ih;
+    q.N = L.N;
+    q.P = L.P;
+    q.Nc = c->lv[l + 1].N;
+    q.Pc = c->lv[l + 1].P;
+    q.jc0 = L.lo / 2;
+    q.jc1 = (L.hi < L.N ? L.hi : L.N - 1) / 2;
+    q.row_lo = L.u0;
+    q.row_hi = L.u1;
+    q.rc_lo = 1;
+    q.rc_hi = 1;
+    launch_smooth4(q, c->s);
+    const int np = postpre_blocks(L.N, q.jc0, q.jc1);
+    const double *g3 = nullptr;
+    if (dist) {
+        launch_sum_partials(q.partials1, np, c->scalar, c->s);
+        launch_sum_partials(q.partials2, np, c->scalar + 1, c->s);
+        launch_sum_partials(q.partials3, np, c->scalar + 2, c->s);
+        if ((e = c->comm->allreduce_sum(c->scalar, 3, c->s))) return e;
+        g3 = c->scalar;
+    }
+    launch_smooth4_finish(q, np, g3, c->cfg.eps, c->ppflags, c->stats, c->s);
+    std::swap(L.A, L.B);
+    c->fsmooth_swapped = true;
+    return PGMG_OK;
+}
+
 template <class T>
 static int enqueue_fcycle(pgmg_ctx *c)
 {
@@ -1404,7 +1450,7 @@ static int enqueue_fcycle(pgmg_ctx *c)
             // pass writing the zeroed fine grid; it reads 3 coarse rows past the strip
             if (dist && is_dist(c, l + 1) && (e = c->comm->halo(C.A, C, 3, c->s))) return e;
             if ((e = enqueue_fused_level<T>(c, l, 1, false, true))) return e;
-            if (l > 0 && (e = enqueue_smooth<T>(c, l, 0, 3, false))) return e;
+            if (l > 0 && (e = enqueue_smooth3_fused<T>(c, l))) return e;
             continue;
         }
         // the prolongation of the rank's rows reads one coarse row past its strip
@@ -1459,6 +1505,12 @@ int pgmg_fcycle(pgmg_ctx *c, int ncycles)
         c->fmg_rhs_ready = true;
     }
     if (c->nb > 0) std::swap(L0.F, c->Ffmg);
+    if (c->fsmooth_swapped && c->gexec) {   // its level buffers traded places: recapture
+        HIPC(hipStreamSynchronize(c->s));
+        HIPC(hipGraphExecDestroy(c->gexec));
+        c->gexec = nullptr;
+    }
+    c->fsmooth_swapped = false;
     c->rgfx = sgx;
     c->rgsy = sgy;
     for (int l = 0; l <= c->nb; ++l) {

@@ -108,6 +108,12 @@ void launch_pre_fixup(const FixArgsF &a, const PreArgsT<T> &p, bool x0_zero, hip
 template <class T> void launch_post_fixup(const FixArgsF &a, const PostArgsT<T> &p, hipStream_t s);
 int postpre_blocks(int N, int jc0, int jc1);
 template <class T> void launch_postpre(const PostPreArgsT<T> &a, hipStream_t s);
+// fused smooth(3): x4 of a.phi into a.x4 with the three checks' partial sums
+// (partials1 r(x1), partials3 r(x2), partials2 r(x3)); then the decision + rare path
+template <class T> void launch_smooth4(const PostPreArgsT<T> &a, hipStream_t s);
+template <class T>
+void launch_smooth4_finish(const PostPreArgsT<T> &a, int np, const double *global3, double eps,
+                           unsigned *flags, unsigned long long *stats, hipStream_t s);
 // flags[0] = post check fired; flags[1] = pre check fired (and post did not).
 // global != nullptr: all-rank sums {post, pre} (row strips) instead of the partials.
 void launch_postpre_decide(const double *partials1, const double *partials2,

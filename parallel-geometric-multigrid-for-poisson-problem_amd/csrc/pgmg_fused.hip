@@ -700,7 +700,8 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     const bool ldr = t < npairs && L0 + 2 * t <= N - 1;      // columns >= N never matter
     const int cc0 = (L0 - 1) >> 1;                               // first coarse column
     const int ncc = (kPPStride / 2) * wpb + kPPMargin + 2;
-    const bool cldr = t < ncc && cc0 + t <= Nc - 1;
+    // OPT & 64 (F-cycle smooth(3)): no coarse correction, no restriction
+    const bool cldr = !(OPT & 64) && t < ncc && cc0 + t <= Nc - 1;
     const T *__restrict__ GX = a.phi + L0 + 2 * t;
     const T *__restrict__ GF = a.f + L0 + 2 * t;
     const T *__restrict__ GE = a.ec + cc0 + t;
@@ -793,7 +794,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
             };
             const V2<T> fq1 = fr(ii - 1, f1), fq2 = fr(ii - 2, f2), fq3 = fr(ii - 3, f3),
                         fq4 = fr(ii - 4, f4), fq5 = fr(ii - 5, f5);
-            const V2<T> e2 = add_prolong<T, EDGE>(xr, ii, cr0, crn0, cr1, crn1, pc, Nc);
+            const V2<T> e2 = (OPT & 64) ? xr : add_prolong<T, EDGE>(xr, ii, cr0, crn0, cr1, crn1, pc, Nc);
             // post-smooth sweep 1: x1 row ii-1
             const V2<T> b2 = jsn<MODE, T, EDGE>(e0, e1, e2, nbr<T>(e1), fq1, hh, k, boundary_row(ii - 1, N));
             const Nbr<T> nb1 = nbr<T>(b1), nc1 = nbr<T>(c1), ng1 = nbr<T>(g1);
@@ -834,7 +835,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
             // r(x4) on row ii-5
             const V2<T> d2 = rsn<MODE, T>(h0, h1, h2, nbr<T>(h1), fq5, ih);
             // restriction: rows ii-7, ii-6, ii-5 = 2jc-1, 2jc, 2jc+1 when ii is even
-            if ((s & 1) == 0) {
+            if (!(OPT & 64) && (s & 1) == 0) {
                 const int jc = (ii - 6) >> 1;
                 const T m2 = dpp_shl(d1.x);
                 const T u2 = wprev;               // = dpp_shl(d0.x): row ii-7 was d2 two rows ago
@@ -1411,6 +1412,106 @@ void launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
     }
 }
 
+// ---------------------------------------------------------------------------
+// Fused smooth(3) (JacobiSmoother::smooth with num_iter = 3, Smoother.hpp:38-116): four
+// sweeps x0 -> x4 in ONE pass of k_postpre_lds (OPT 64: no correction, no restriction)
+// with the checks ||r(x1)||, ||r(x2)||, ||r(x3)|| < eps summed speculatively; the decision
+// kernel finds the first check that fires and the rare-path kernel recomputes x_k from
+// the untouched x0.  Used by the F-cycle climb on the levels below the finest.
+// ---------------------------------------------------------------------------
+template <class T>
+void launch_smooth4(const PostPreArgsT<T> &a0, hipStream_t s)
+{
+    int t, gx, gy, r;
+    fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, kPPStride, pp_target(a0.jc0, a0.jc1));
+    PostPreArgsT<T> a = a0;
+    a.rows_per_block = r;
+    a.band_stride = 0;
+    k_postpre_lds<T, true, false, 2, 1, 0, false, 64><<<dim3(gx, gy), dim3(t), 0, s>>>(a);
+}
+
+__device__ __forceinline__ double block_sum_strided(const double *p, int n, double *red)
+{
+    double v = 0.0;
+    for (int k = threadIdx.x; k < n; k += blockDim.x) v += p[k];
+    return fused_block_sum(v, red);
+}
+
+// flags[0] = first k in 1..3 whose check ||r(x_k)|| < eps fires, 0 if none; stats
+// [sweeps, exits].  global3 (row strips): all-rank sums {r(x1), r(x3), r(x2)}.
+__global__ __launch_bounds__(256) void k_smooth4_decide(const double *p1, const double *p2,
+                                                        const double *p3, int np,
+                                                        const double *global3, double eps,
+                                                        unsigned *flags,
+                                                        unsigned long long *stats)
+{
+    __shared__ double red[4];
+    double s1 = block_sum_strided(p1, np, red);
+    __syncthreads();
+    double s3 = block_sum_strided(p3, np, red);
+    __syncthreads();
+    double s2 = block_sum_strided(p2, np, red);
+    if (threadIdx.x == 0) {
+        if (global3 != nullptr) {
+            s1 = global3[0];
+            s2 = global3[1];
+            s3 = global3[2];
+        }
+        const int k = sqrt(s1) < eps ? 1 : (sqrt(s3) < eps ? 2 : (sqrt(s2) < eps ? 3 : 0));
+        flags[0] = (unsigned)k;
+        if (stats != nullptr) {
+            atomicAdd(&stats[0], (unsigned long long)(k ? k : 4));
+            if (k) atomicAdd(&stats[1], 1ull);
+        }
+    }
+}
+
+// x_K = J^K(x0) at one point (boundary points pass through)
+template <int K, class T>
+__device__ T fxs(const T *x0, const T *f, long long P, int N, T hh, int j, int i)
+{
+    if constexpr (K == 0) {
+        return x0[(long long)j * P + i];
+    } else {
+        if (j <= 0 || i <= 0 || j >= N - 1 || i >= N - 1) return x0[(long long)j * P + i];
+        return T(0.25) * ((hh * f[(long long)j * P + i]) + fxs<K - 1>(x0, f, P, N, hh, j, i - 1) +
+                          fxs<K - 1>(x0, f, P, N, hh, j, i + 1) +
+                          fxs<K - 1>(x0, f, P, N, hh, j - 1, i) +
+                          fxs<K - 1>(x0, f, P, N, hh, j + 1, i));
+    }
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void k_smooth4_fix(const unsigned *flags, const T *x0, const T *f,
+                                                     T *out, long long P, int N, T hh, int row_lo,
+                                                     int row_hi)
+{
+    const unsigned k = flags[0];
+    if (k == 0) return;   // uniform: the normal case
+    const long long W = N - 2;
+    const long long n = (long long)(row_hi - row_lo) * W;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
+        const int j = row_lo + (int)(q / W), i = 1 + (int)(q % W);
+        T v;
+        if (k == 1) v = fxs<1>(x0, f, P, N, hh, j, i);
+        else if (k == 2) v = fxs<2>(x0, f, P, N, hh, j, i);
+        else v = fxs<3>(x0, f, P, N, hh, j, i);
+        out[(long long)j * P + i] = v;
+    }
+}
+
+template <class T>
+void launch_smooth4_finish(const PostPreArgsT<T> &a, int np, const double *global3, double eps,
+                           unsigned *flags, unsigned long long *stats, hipStream_t s)
+{
+    k_smooth4_decide<<<dim3(1), dim3(256), 0, s>>>(a.partials1, a.partials2, a.partials3, np,
+                                                    global3, eps, flags, stats);
+    const int blocks = std::max(1, std::min(1024, (int)(((long long)(a.row_hi - a.row_lo) * a.N + 255) / 256)));
+    k_smooth4_fix<T><<<dim3(blocks), dim3(256), 0, s>>>(flags, a.phi, a.f, a.x4, a.P, a.N, a.hh,
+                                                        a.row_lo, a.row_hi);
+}
+
 void launch_postpre_decide(const double *partials1, const double *partials2, unsigned long long *stats,
                            int np, const double *global, double eps, unsigned *flags, hipStream_t s)
 {
@@ -1667,6 +1768,9 @@ void launch_post_fixup(const FixArgsF &a, const PostArgsT<T> &p, hipStream_t s)
     template void launch_pre<T>(const PreArgsT<T> &, bool, bool, hipStream_t);                   \
     template void launch_post<T>(const PostArgsT<T> &, bool, hipStream_t);                       \
     template void launch_postpre<T>(const PostPreArgsT<T> &, hipStream_t);                       \
+    template void launch_smooth4<T>(const PostPreArgsT<T> &, hipStream_t);                        \
+    template void launch_smooth4_finish<T>(const PostPreArgsT<T> &, int, const double *, double, \
+                                           unsigned *, unsigned long long *, hipStream_t);       \
     template void launch_pre_fixup<T>(const FixArgsF &, const PreArgsT<T> &, bool, hipStream_t);  \
     template void launch_post_fixup<T>(const FixArgsF &, const PostArgsT<T> &, hipStream_t);
 PGMG_INSTANTIATE(double)
