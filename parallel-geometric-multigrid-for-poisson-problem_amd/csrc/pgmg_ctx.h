@@ -119,6 +119,7 @@ struct pgmg_ctx {
     // F-cycle (pgmg_fcycle): analytic level-0 RHS of the FMG h chain, and the sine
     // tables of every level (built on the first call)
     pgmg::Grid Ffmg;
+    std::vector<pgmg::Grid> Ffmg_l;   // the analytic RHS of bulk levels 1.. of the FMG climb
     bool fmg_rhs_ready = false;   // Ffmg holds the level-0 analytic RHS of the FMG h chain
     double *fmg_tab = nullptr;
     std::vector<int> fmg_off;     // per level 0..nb then tail levels below nb: sx offset

@@ -714,6 +714,7 @@ int pgmg_destroy(pgmg_ctx *c)
     if (c->ppflags) (void)hipFree(c->ppflags);
     free_grid(c->S);
     free_grid(c->Ffmg);
+    for (auto &g : c->Ffmg_l) free_grid(g);
     if (c->fmg_tab) (void)hipFree(c->fmg_tab);
     if (c->flags) (void)hipFree(c->flags);
     if (c->stats) (void)hipFree(c->stats);
@@ -1432,8 +1433,12 @@ static int enqueue_fcycle(pgmg_ctx *c)
         // analytic RHS is computed locally instead of exchanged
         const int r0 = dist ? std::max(0, L.lo - kHalo) : 0;
         const int r1 = dist ? std::min(L.N, L.hi + kHalo) : L.N;
-        // level 0's F is the F-cycle's own analytic RHS (Ffmg): the same on every call
-        if (l > 0 || !c->fmg_rhs_ready)
+        // the level's analytic RHS of the FMG h chain is the same on every call: computed
+        // once into its own grid (Ffmg for level 0, Ffmg_l[l] below), which stands in for
+        // L.F while this level runs (the V-cycle's restriction writes the coarser level's
+        // own F, not its cached RHS)
+        if (l > 0) std::swap(L.F, c->Ffmg_l[l]);
+        if (!c->fmg_rhs_ready)
             launch_rhs(G<T>(L.F), sx, sx + L.N, factor, L.N, L.P, r0, r1, c->s);
         // phi_fine = 0 + P phi_coarse (MultiGrid.hpp:159-164): the prolongation assigns the
         // interior, the frame (boundary, and row/column 1 the reference never corrects) is
@@ -1451,6 +1456,7 @@ static int enqueue_fcycle(pgmg_ctx *c)
             if (dist && is_dist(c, l + 1) && (e = c->comm->halo(C.A, C, 3, c->s))) return e;
             if ((e = enqueue_fused_level<T>(c, l, 1, false, true))) return e;
             if (l > 0 && (e = enqueue_smooth3_fused<T>(c, l))) return e;
+            if (l > 0) std::swap(L.F, c->Ffmg_l[l]);
             continue;
         }
         // the prolongation of the rank's rows reads one coarse row past its strip
@@ -1469,6 +1475,7 @@ static int enqueue_fcycle(pgmg_ctx *c)
         e = enqueue_cycle_t<T>(c, l, 1, false);
         if (e) return e;
         if (l > 0 && (e = enqueue_smooth<T>(c, l, 0, 3, false))) return e;
+        if (l > 0) std::swap(L.F, c->Ffmg_l[l]);
     }
     return PGMG_OK;
 }
@@ -1484,6 +1491,11 @@ int pgmg_fcycle(pgmg_ctx *c, int ncycles)
     if (e) return e;
     Level &L0 = c->lv[0];
     if (c->nb > 0 && !c->Ffmg.base && (e = alloc_grid(c->Ffmg, L0))) return e;
+    if ((int)c->Ffmg_l.size() < c->nb) {
+        c->Ffmg_l.resize(c->nb);
+        for (int l = 1; l < c->nb; ++l)
+            if ((e = alloc_grid(c->Ffmg_l[l], c->lv[l]))) return e;
+    }
     // the F-cycle's levels use the FMG h chain and (level 0) the analytic RHS of that chain
     // (every level including the tail's top, whose h enqueue_tail passes on)
     std::vector<Level> saved(c->lv);
