@@ -1746,9 +1746,15 @@ __global__ __launch_bounds__(256) void k_post_fixup(FixArgsF a, PostArgsT<T> p)
 // 2^20 points up (a fired recompute on the finest levels then still has the whole chip).
 static int fixup_blocks(int N, int row_lo, int row_hi)
 {
+    // the rare-path recompute is scalar pointwise recursion (tens of loads per point): one
+    // thread per point, up to 8192 blocks (was one per 16, at most 256 blocks: a fired
+    // coarse-level fix-up cost ~40 us; 200 V-cycles at N = 4097, where the levels above
+    // the tail converge and fire every cycle: 1083 -> 2435 V-cycles/s; 100 at 16385:
+    // 439 -> 523; scripts/long_run.sh)
     const long long pts = (long long)(row_hi > row_lo ? row_hi - row_lo : 0) * N;
-    long long b = pts >> 12;
-    return (int)(b < 1 ? 1 : (b > 256 ? 256 : b));
+    const long long shift = env_int("PGMG_FIX_SHIFT", 8), cap = env_int("PGMG_FIX_CAP", 8192);
+    long long b = pts >> shift;
+    return (int)(b < 1 ? 1 : (b > cap ? cap : b));
 }
 
 template <class T>
