@@ -80,6 +80,7 @@ struct pgmg_ctx {
     // finest-level kernel timing (PGMG_FLAG_TIME_FINE): 0 plain sweep, 1 k_pre, 2 k_post
     EventPool tpool[4];           // 3: k_postpre
     bool fused = false;           // v1 = v2 = 1: two fused passes per level
+    bool rare_fused = true;       // in-stream rare paths as fused one-sweep passes
     bool cross = false;           // finest level fuses post(k) with pre(k+1) across cycles
     bool recompute = true;        // levels entered with x0 = 0 recompute x2 in k_post
     pgmg::Grid S;                 // finest-level scratch for k_postpre's rare paths

@@ -306,7 +306,8 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     if ((e = timed_end(c, 1, ev))) return e;
     if (!lp) {
         if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
-        launch_pre_fixup(fa, pa, x0_zero, c->s);
+        if (c->rare_fused) launch_pre_rare(fa, pa, x0_zero, c->s);
+        else launch_pre_fixup(fa, pa, x0_zero, c->s);
     }
     if ((e = enqueue_children<T>(c, l, gamma))) return e;
     // the correction of level l+1 is not exchanged: a distributed child's k_post computed
@@ -350,7 +351,8 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     if (!lp) {
         fa.global_sum = nullptr;
         if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
-        launch_post_fixup(fa, po, c->s);
+        if (c->rare_fused) launch_post_rare(fa, po, c->s);
+        else launch_post_fixup(fa, po, c->s);
     }
     return PGMG_OK;
 }
@@ -800,6 +802,10 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         if (rc == PGMG_OK && l < c->nb) rc = alloc_grid(L.B, L);
     }
     c->fused = cfg->v1 == 1 && cfg->v2 == 1 && !(cfg->flags & PGMG_FLAG_UNFUSED);
+    {   // in-stream rare paths as fused one-sweep passes (PGMG_RARE_FUSED=0: scalar fix-ups)
+        const char *ev = getenv("PGMG_RARE_FUSED");
+        c->rare_fused = !(ev && *ev == '0');
+    }
     {
         const char *ev = getenv("PGMG_RECOMPUTE");
         c->recompute = !(ev && *ev == '0');

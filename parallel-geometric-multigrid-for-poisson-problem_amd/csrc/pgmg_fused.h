@@ -106,6 +106,10 @@ template <class T> void launch_post(const PostArgsT<T> &a, bool fine, hipStream_
 template <class T>
 void launch_pre_fixup(const FixArgsF &a, const PreArgsT<T> &p, bool x0_zero, hipStream_t s);
 template <class T> void launch_post_fixup(const FixArgsF &a, const PostArgsT<T> &p, hipStream_t s);
+// the same rare paths as fused one-sweep passes (in-stream checks of enqueue_fused_level)
+template <class T>
+void launch_pre_rare(const FixArgsF &f, const PreArgsT<T> &a, bool x0_zero, hipStream_t s);
+template <class T> void launch_post_rare(const FixArgsF &f, const PostArgsT<T> &a, hipStream_t s);
 int postpre_blocks(int N, int jc0, int jc1);
 template <class T> void launch_postpre(const PostPreArgsT<T> &a, hipStream_t s);
 // fused smooth(3): x4 of a.phi into a.x4 with the three checks' partial sums

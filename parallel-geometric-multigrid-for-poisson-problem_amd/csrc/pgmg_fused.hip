@@ -136,11 +136,13 @@ __device__ __forceinline__ V2<T> add_prolong(V2<T> p, int row, T ca, T cb, T da,
 // GENF: f is the analytic RHS, regenerated per row from the gfx/gsy tables (see k_postpre_lds)
 // PIN (F-cycle): x0 = (+0) + P ec (a.pin_ec), computed per row from the coarse rows
 // (2 B/point read instead of 8, and the prolongation pass into the zeroed grid is gone)
-template <class T, bool X0_ZERO, bool FINE, int PAIRS, bool GENF = false, bool PIN = false>
-__global__ __launch_bounds__(256) void k_pre(PreArgsT<T> a)
+// S1 (rare path of an in-stream check, k_pre_rare): the check after the first sweep fired,
+// so the pass is redone with ONE sweep — x1 stored instead of x2, rc = R r(x1) — and
+// writes no partial sums and no sweep count (the decision kernel's job)
+template <class T, bool X0_ZERO, bool FINE, int PAIRS, bool GENF, bool PIN, bool S1>
+__device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red)
 {
     constexpr int R = 2 * PAIRS;  // rows loaded per iteration (and prefetched ahead)
-    __shared__ double red[4];
     if (a.cond != nullptr && *a.cond == 0u) return;  // conditional (rare-path) launch
     const Cols k = lane_cols(a.N);
     const int N = a.N;
@@ -149,7 +151,7 @@ __global__ __launch_bounds__(256) void k_pre(PreArgsT<T> a)
     const int jce = min(jcb + a.rows_per_block, a.jc1);
     const int olo = max(2 * jcb, a.row_lo), ohi = min(2 * jce, a.row_hi);  // x2 rows written
     const int clo = max(jcb, max(1, a.rc_lo)), chi = min(jce, min(N / 2, a.rc_hi));  // rc rows
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
+    if (!S1 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
         atomicAdd(&a.stats[0], 2ull);
     const T *__restrict__ X = a.x0 + k.c;
     const T *__restrict__ F = a.f + k.c;
@@ -161,6 +163,7 @@ __global__ __launch_bounds__(256) void k_pre(PreArgsT<T> a)
     // windows: x0 rows i-2,i-1 ; x1 rows i-3,i-2 ; x2 rows i-4,i-3 ; r rows i-5,i-4 ;
     //          f rows i-3,i-2,i-1
     V2<T> a0 = z, a1 = z, b0 = z, b1 = z, c0 = z, c1 = z, d0 = z, d1 = z, f0 = z, f1 = z, f2 = z;
+    V2<T> q0 = z, q1 = z;   // S1: r(x1) rows ii-4, ii-3
     double acc = 0.0;
     // steps [i_begin, i_end): rows 2jcb-4 .. 2jce+3, rounded up to whole iterations
     // (the extra rows are computed but never stored; kHalo covers their loads)
@@ -241,9 +244,36 @@ __global__ __launch_bounds__(256) void k_pre(PreArgsT<T> a)
             // x1 row ii-1
             const V2<T> b2 = jstage(a0, a1, a2, f2, hh, k, boundary_row(ii - 1, N));
             // r(x1) and x2 on row ii-2
+            const V2<T> r1 = rstage(b0, b1, b2, f1, ih);
+            if constexpr (S1) {
+                // x1 row ii-1 is the result; restriction of r(x1): rows ii-4, ii-3, ii-2 =
+                // 2jc-1, 2jc, 2jc+1 when ii is odd
+                if (store && ii - 1 >= olo && ii - 1 < ohi && k.own) stv(O + (ii - 1) * P, b2);
+                if ((s & 1) == 1) {
+                    const int jc = (ii - 3) >> 1;
+                    const T m2 = dpp_shl(q1.x);
+                    const T u2 = dpp_shl(q0.x);
+                    const T e2 = dpp_shl(r1.x);
+                    const int ic = (k.c + 1) >> 1;
+                    if (jc >= clo && jc < chi && k.own && ic <= a.Nc - 2) {
+                        const T v = T(0.25) * q1.y + T(0.125) * (m2 + q1.x + r1.y + q0.y) +
+                                    T(0.0625) * (q0.x + u2 + r1.x + e2);
+                        a.rc[(long long)jc * a.Pc + ic] = v;
+                    }
+                }
+                q0 = q1;
+                q1 = r1;
+                a0 = a1;
+                a1 = a2;
+                b0 = b1;
+                b1 = b2;
+                f0 = f1;
+                f1 = f2;
+                f2 = f3;
+                continue;
+            }
             {
                 const int row = ii - 2;
-                const V2<T> r1 = rstage(b0, b1, b2, f1, ih);
                 if (row >= olo && row < ohi && k.own) {
                     acc = sqacc(acc, r1.x);
                     if (!k.by) acc = sqacc(acc, r1.y);
@@ -283,8 +313,53 @@ __global__ __launch_bounds__(256) void k_pre(PreArgsT<T> a)
             f2 = f3;
         }
     }
-    const double sum = fused_block_sum(acc, red);
-    if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = sum;
+    if constexpr (!S1) {
+        const double sum = fused_block_sum(acc, red);
+        if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = sum;
+    }
+}
+
+template <class T, bool X0_ZERO, bool FINE, int PAIRS, bool GENF = false, bool PIN = false>
+__global__ __launch_bounds__(256) void k_pre(PreArgsT<T> a)
+{
+    __shared__ double red[4];
+    pre_body<T, X0_ZERO, FINE, PAIRS, GENF, PIN, false>(a, red);
+}
+
+// Decision of an in-stream early-exit check from the partial sums of the pass just run
+// (every block re-reduces them in the same order; a row strip's all-rank sum comes in
+// f.global_sum); block (0,0) books the exit.  Blocks that find it did not fire return.
+__device__ __forceinline__ bool rare_decide(const FixArgsF &f, double *red, int *trig)
+{
+    double v = 0.0;
+    for (int k = threadIdx.x; k < f.np; k += blockDim.x) v += f.partials[k];
+    v = fused_block_sum(v, red);
+    if (threadIdx.x == 0) {
+        const double tot = f.global_sum != nullptr ? *f.global_sum : v;
+        *trig = (sqrt(tot) < f.eps) ? 1 : 0;
+    }
+    __syncthreads();
+    const bool t = *trig != 0;
+    if (t && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && f.stats != nullptr) {
+        atomicAdd(&f.stats[0], (unsigned long long)-1LL);
+        atomicAdd(&f.stats[1], 1ull);
+    }
+    return t;
+}
+
+// rare path of k_pre's check (replaces the scalar k_pre_fixup on in-stream levels): when it
+// fired, the same fused pass with one sweep; a.fired records the decision for k_post RECOMP
+template <class T, bool X0_ZERO, int PAIRS, bool PIN>
+__global__ __launch_bounds__(256) void k_pre_rare(PreArgsT<T> a, FixArgsF f)
+{
+    __shared__ double red[4];
+    __shared__ int trig;
+    const bool t = rare_decide(f, red, &trig);
+    if (a.fired != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+        *a.fired = t ? 1u : 0u;
+    if (!t) return;
+    __syncthreads();
+    pre_body<T, X0_ZERO, false, PAIRS, false, PIN, true>(a, red);
 }
 
 // ---------------------------------------------------------------------------
@@ -293,11 +368,10 @@ __global__ __launch_bounds__(256) void k_pre(PreArgsT<T> a)
 // RECOMP (levels entered with x0 = 0): phi is not read.  The loaded row is f[ii+1];
 // x1 = J(0) is pointwise, so x1 row ii+1 -> phi row ii = J(x1) (or x1 when the pre
 // check fired) -> x_eff row ii: one more row of lag than reading phi, 16 B/point less.
-template <class T, bool FINE, int PAIRS, bool RECOMP, bool GENF = false>
-__global__ __launch_bounds__(256) void k_post(PostArgsT<T> a)
+template <class T, bool FINE, int PAIRS, bool RECOMP, bool GENF, bool S1>
+__device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
 {
     constexpr int R = 2 * PAIRS;
-    __shared__ double red[4];
     if (a.cond != nullptr && *a.cond == 0u) return;  // conditional (rare-path) launch
     const Cols k = lane_cols(a.N);
     const int N = a.N, Nc = a.Nc;
@@ -307,7 +381,7 @@ __global__ __launch_bounds__(256) void k_post(PostArgsT<T> a)
     const int olo = max(2 * jcb, a.row_lo), ohi = min(2 * jce, a.row_hi);
     const int slo = a.sum_hi > a.sum_lo ? max(olo, a.sum_lo) : olo;
     const int shi = a.sum_hi > a.sum_lo ? min(ohi, a.sum_hi) : ohi;
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
+    if (!S1 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
         atomicAdd(&a.stats[0], 2ull);
     ProlongCols pc;
     pc.ic = (k.c - 1) >> 1;
@@ -394,6 +468,14 @@ __global__ __launch_bounds__(256) void k_post(PostArgsT<T> a)
             }
             const V2<T> a2 = add_prolong(ph, ii, cr[pq], crn[pq], cr[pq + 1], crn[pq + 1], pc, Nc);
             const V2<T> b2 = jstage(a0, a1, a2, f2, hh, k, boundary_row(ii - 1, N));
+            if constexpr (S1) {   // the post check fired: x1 row ii-1 is the result
+                if (ii - 1 >= olo && ii - 1 < ohi && k.own) stv(O + (ii - 1) * P, b2);
+                a0 = a1;
+                a1 = a2;
+                f1 = f2;
+                f2 = f3;
+                continue;
+            }
             {
                 const int row = ii - 2;
                 const V2<T> r1 = rstage(b0, b1, b2, f1, ih);
@@ -415,9 +497,30 @@ __global__ __launch_bounds__(256) void k_post(PostArgsT<T> a)
             f2 = f3;
         }
     }
-    const double sum = fused_block_sum(acc, red);
-    if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = sum;
+    if constexpr (!S1) {
+        const double sum = fused_block_sum(acc, red);
+        if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = sum;
+    }
 }
+
+template <class T, bool FINE, int PAIRS, bool RECOMP, bool GENF = false>
+__global__ __launch_bounds__(256) void k_post(PostArgsT<T> a)
+{
+    __shared__ double red[4];
+    post_body<T, FINE, PAIRS, RECOMP, GENF, false>(a, red);
+}
+
+// rare path of k_post's check (replaces the scalar k_post_fixup on in-stream levels)
+template <class T, int PAIRS, bool RECOMP>
+__global__ __launch_bounds__(256) void k_post_rare(PostArgsT<T> a, FixArgsF f)
+{
+    __shared__ double red[4];
+    __shared__ int trig;
+    if (!rare_decide(f, red, &trig)) return;
+    __syncthreads();
+    post_body<T, false, PAIRS, RECOMP, false, true>(a, red);
+}
+
 
 // ---------------------------------------------------------------------------
 // k_postpre: the finest level between two consecutive cycles of one call.
@@ -1757,6 +1860,38 @@ static int fixup_blocks(int N, int row_lo, int row_hi)
     return (int)(b < 1 ? 1 : (b > cap ? cap : b));
 }
 
+// rare paths of the in-stream checks as fused one-sweep passes (decision inside; a launch
+// that finds the check did not fire returns at once).  f is streamed (the stored f is
+// valid whenever a pass regenerates it in-kernel).
+template <class T>
+void launch_pre_rare(const FixArgsF &f, const PreArgsT<T> &a0, bool x0_zero, hipStream_t s)
+{
+    int t, gx, gy, r;
+    fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r);
+    PreArgsT<T> a = a0;
+    a.rows_per_block = r;
+    a.gfx = a.gsy = nullptr;
+    a.nt = 0;
+    const dim3 g(gx, gy), b(t);
+    if (x0_zero) k_pre_rare<T, true, 2, false><<<g, b, 0, s>>>(a, f);
+    else if (a.pin_ec != nullptr) k_pre_rare<T, false, 2, true><<<g, b, 0, s>>>(a, f);
+    else k_pre_rare<T, false, 2, false><<<g, b, 0, s>>>(a, f);
+}
+
+template <class T>
+void launch_post_rare(const FixArgsF &f, const PostArgsT<T> &a0, hipStream_t s)
+{
+    int t, gx, gy, r;
+    fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r);
+    PostArgsT<T> a = a0;
+    a.rows_per_block = r;
+    a.gfx = a.gsy = nullptr;
+    a.nt = 0;
+    const dim3 g(gx, gy), b(t);
+    if (a.pre_fired != nullptr) k_post_rare<T, 2, true><<<g, b, 0, s>>>(a, f);
+    else k_post_rare<T, 2, false><<<g, b, 0, s>>>(a, f);
+}
+
 template <class T>
 void launch_pre_fixup(const FixArgsF &a, const PreArgsT<T> &p, bool x0_zero, hipStream_t s)
 {
@@ -1778,6 +1913,8 @@ void launch_post_fixup(const FixArgsF &a, const PostArgsT<T> &p, hipStream_t s)
     template void launch_smooth4_finish<T>(const PostPreArgsT<T> &, int, const double *, double, \
                                            unsigned *, unsigned long long *, hipStream_t);       \
     template void launch_pre_fixup<T>(const FixArgsF &, const PreArgsT<T> &, bool, hipStream_t);  \
+    template void launch_pre_rare<T>(const FixArgsF &, const PreArgsT<T> &, bool, hipStream_t);   \
+    template void launch_post_rare<T>(const FixArgsF &, const PostArgsT<T> &, hipStream_t);       \
     template void launch_post_fixup<T>(const FixArgsF &, const PostArgsT<T> &, hipStream_t);
 PGMG_INSTANTIATE(double)
 PGMG_INSTANTIATE(float)
