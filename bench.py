@@ -111,16 +111,22 @@ def main():
 
     dist = None
     uid = None
+    # PGMG_BENCH_SOLO=1 (harness test on a one-GPU box only): every rank on device 0 with the
+    # null transport (PGMG_FLAG_SOLO: no messages, results meaningless); the line says so
+    solo = world > 1 and os.environ.get("PGMG_BENCH_SOLO") == "1"
+    device = 0 if (world == 1 or solo) else local_rank
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
+        torch.cuda.set_device(device)
         dist.init_process_group("gloo")
         t = torch.tensor(list(pg.unique_id()) if rank == 0 else [0] * 128, dtype=torch.uint8)
         dist.broadcast(t, 0)
         uid = bytes(t.tolist())
 
     flags = pg.PGMG_FLAG_TIME_FINE if args.timing == "events" else 0
-    kw = dict(flags=flags, device=local_rank if world > 1 else 0, dtype=args.dtype)
+    if solo:
+        flags |= pg.PGMG_FLAG_SOLO
+    kw = dict(flags=flags, device=device, dtype=args.dtype)
     if world > 1:
         kw.update(rank=rank, world=world, uid=uid)
     s = pg.Solver(args.n, **kw)
@@ -223,7 +229,9 @@ def main():
                             f"sweeps, eps=1e-7 early exit, {bulk} bulk levels + one-workgroup LDS "
                             f"tail from N={tail_top} to N=5",
                 "N": n, "bulk_levels": bulk, "tail_top": tail_top,
-                "parallelism": "single-gpu" if world == 1 else f"row-strips x{world} (RCCL halos)",
+                "parallelism": "single-gpu" if world == 1 else (
+                    f"row-strips x{world} (SOLO null transport on one GPU: harness test, "
+                    f"not a measurement)" if solo else f"row-strips x{world} (RCCL halos)"),
                 "timing": args.timing,
             },
             "roofline": roof[0],

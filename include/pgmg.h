@@ -226,6 +226,10 @@ int pgmg_device_count(int *n);
 /* RCCL bootstrap: fill a 128-byte buffer with a fresh ncclUniqueId (rank 0). */
 int pgmg_comm_unique_id(void *out128);
 
+/* Self-test of the RCCL transport on one GPU (a world-1 communicator): the strip path's
+ * grouped send/recv, allreduce(sum, double) and allreduce(min, u32) on a stream; 0 = ok. */
+int pgmg_rccl_selftest(const void *uid128, int device);
+
 /* In-process rank hub for PGMG_FLAG_LOOPBACK (tests of the strip decomposition). */
 int pgmg_loopback_create(int world, void **hub);
 int pgmg_loopback_destroy(void *hub);

@@ -481,6 +481,62 @@ int pgmg_comm_unique_id(void *out128)
     return PGMG_OK;
 }
 
+// Self-test of the RCCL transport on one GPU: a world-1 communicator (the only size a
+// one-GPU box can form) runs the exact calls of the strip path — a grouped send/recv
+// (to itself), allreduce(sum) of doubles and allreduce(min) of u32 — on a stream, and
+// checks the results.  0 on success.
+int pgmg_rccl_selftest(const void *uid128, int device)
+{
+    if (!uid128) return pgmg::set_err(PGMG_ERR_ARG, "null unique id");
+    if (hipSetDevice(device) != hipSuccess) return pgmg::set_err(PGMG_ERR_HIP, "hipSetDevice");
+    pgmg::RcclTransport t;
+    int e = t.init(uid128, 1, 0);
+    if (e) return e;
+    hipStream_t s;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
+        return pgmg::set_err(PGMG_ERR_HIP, "stream");
+    const int n = 1 << 16;
+    double *a = nullptr, *b = nullptr;
+    unsigned *u = nullptr;
+    std::vector<double> h(n), g(n);
+    for (int i = 0; i < n; ++i) h[i] = 0.5 * i - 7.0;
+    int rc = PGMG_OK;
+    if (hipMalloc(&a, n * sizeof(double)) != hipSuccess || hipMalloc(&b, n * sizeof(double)) != hipSuccess ||
+        hipMalloc(&u, 4 * sizeof(unsigned)) != hipSuccess)
+        rc = pgmg::set_err(PGMG_ERR_NOMEM, "selftest buffers");
+    const unsigned hu[4] = {3u, 1u, 4u, 1u};
+    unsigned gu[4] = {0, 0, 0, 0};
+    if (!rc && (hipMemcpy(a, h.data(), n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemset(b, 0, n * sizeof(double)) != hipSuccess ||
+                hipMemcpy(u, hu, sizeof(hu), hipMemcpyHostToDevice) != hipSuccess))
+        rc = pgmg::set_err(PGMG_ERR_HIP, "selftest upload");
+    if (!rc) rc = t.group_start();
+    if (!rc) rc = t.send(a, n * sizeof(double), 0, s);
+    if (!rc) rc = t.recv(b, n * sizeof(double), 0, s);
+    if (!rc) rc = t.group_end(s);
+    if (!rc) rc = t.allreduce_sum(a, 3, s);
+    if (!rc) rc = t.allreduce_min_u32(u, 4, s);
+    if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = pgmg::set_err(PGMG_ERR_HIP, "selftest sync");
+    if (!rc && (hipMemcpy(g.data(), b, n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(gu, u, sizeof(gu), hipMemcpyDeviceToHost) != hipSuccess))
+        rc = pgmg::set_err(PGMG_ERR_HIP, "selftest download");
+    if (!rc && std::memcmp(g.data(), h.data(), n * sizeof(double)) != 0)
+        rc = pgmg::set_err(PGMG_ERR_COMM, "selftest: received rows differ from the sent rows");
+    if (!rc && std::memcmp(gu, hu, sizeof(hu)) != 0)
+        rc = pgmg::set_err(PGMG_ERR_COMM, "selftest: allreduce(min) of one rank changed values");
+    if (!rc) {
+        double a3[3];
+        if (hipMemcpy(a3, a, sizeof(a3), hipMemcpyDeviceToHost) != hipSuccess || a3[0] != h[0] ||
+            a3[1] != h[1] || a3[2] != h[2])
+            rc = pgmg::set_err(PGMG_ERR_COMM, "selftest: allreduce(sum) of one rank changed values");
+    }
+    (void)hipFree(a);
+    (void)hipFree(b);
+    (void)hipFree(u);
+    (void)hipStreamDestroy(s);
+    return rc;
+}
+
 int pgmg_loopback_create(int world, void **hub)
 {
     if (!hub || world < 1 || world > 64) return pgmg::set_err(PGMG_ERR_ARG, "bad argument");
