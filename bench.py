@@ -49,17 +49,24 @@ def parse():
 
 
 def cpu_baseline(n, cycles=1, kind="V"):
-    """The oracle (our C restatement of mg_cpu_exec, 1 thread) on the host: a bounded
-    sample of the same workload (one cycle of the same kind at the same N)."""
-    exe = ROOT / "oracle" / "mg_cpu_exec_port"
-    if not exe.exists():
-        subprocess.run(["make", "-C", str(ROOT / "oracle"), "-s",
-                        str(exe)], check=True, capture_output=True)
+    """The reference's own CPU multigrid (MultigridSolver::v_cycle of mg_cpu_exec, compiled
+    from its sources by oracle/Makefile into oracle/_ref/ref_harness, 1 thread) on the host:
+    a bounded sample of the same workload (one cycle of the same kind at the same N).
+    Without that binary: the oracle (our C restatement, oracle/mg_cpu_exec_port)."""
+    ref = ROOT / "oracle" / "_ref" / "ref_harness"
+    port = ROOT / "oracle" / "mg_cpu_exec_port"
+    if ref.exists():
+        exe, what = ref, "reference"
+    else:
+        exe, what = port, "port"
+        if not exe.exists():
+            subprocess.run(["make", "-C", str(ROOT / "oracle"), "-s",
+                            str(exe)], check=True, capture_output=True)
     cmd = [str(exe), kind, str(n), str(cycles), "1e-7"]
     if shutil.which("taskset"):
         cmd = ["taskset", "-c", "0"] + cmd
     out = subprocess.run(cmd, check=True, capture_output=True, text=True).stdout
-    secs = [float(l.split("seconds")[1]) for l in out.splitlines() if "seconds" in l]
+    secs = [float(l.split("seconds")[1].split()[0]) for l in out.splitlines() if "seconds" in l]
     t = sum(secs) / len(secs)
     model = platform.processor() or ""
     try:
@@ -69,9 +76,11 @@ def cpu_baseline(n, cycles=1, kind="V"):
                 break
     except OSError:
         pass
-    return {"value": round(1.0 / t, 6), "unit": f"{kind}-cycles/s", "cores": 1, "kind": "port",
-            "sample": f"{cycles} {kind}-cycle(s) at N={n}, phi0=0, analytic f; oracle/mg_cpu_exec_port "
-                      f"-O2 single thread (taskset -c 0); {t:.2f} s per {kind}-cycle; host {model}"}
+    src = ("the reference's MultigridSolver (2_part_MG/MultiGrid.hpp) via oracle/_ref/ref_harness"
+           if what == "reference" else "oracle/mg_cpu_exec_port (our C restatement)")
+    return {"value": round(1.0 / t, 6), "unit": f"{kind}-cycles/s", "cores": 1, "kind": what,
+            "sample": f"{cycles} {kind}-cycle(s) at N={n}, phi0=0, analytic f; {src}, g++/gcc -O2 "
+                      f"single thread (taskset -c 0); {t:.2f} s per {kind}-cycle; host {model}"}
 
 
 def pmc_traffic(n, key):

@@ -9,11 +9,13 @@
 // Usage: ref_harness <V|W|F> <N> <cycles> <eps> [phi_out.bin]
 // Prints one line per cycle:
 //   cycle <k> relerr <e> res <r> center <phi[(N/2)*N+N/2]> hash <fnv64> sweeps <s> exits <x>
+//   seconds <wall time of the reference's cycle call alone>  (bench.py's cpu_baseline)
 // and, if given, writes phi after the last cycle as raw little-endian doubles.
 //
 // operator new[] is calloc-backed: the reference reads the never-written
 // boundary of `new double[L]` residual buffers (Smoother.hpp:75-76), which is
 // undefined; zero is what it reads in practice and what we pin.
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -137,6 +139,7 @@ int main(int argc, char **argv)
     DynamicGridUtils::compute_rhs(f0, n0, n0, h0);
 
     for (int k = 1; k <= cycles; ++k) {
+        const auto t0 = std::chrono::steady_clock::now();
         if (kind == 'V') {
             mg.v_cycle(phi, f, N, h);
         } else if (kind == 'W') {
@@ -148,6 +151,8 @@ int main(int argc, char **argv)
             std::memcpy(phi, mg.final_solution, sizeof(double) * L);
             delete[] p0;
         }
+        const double secs =
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         DynamicGridUtils::initialize_zeros(r, L);
         DynamicGridUtils::compute_residual(r, phi, f, N, N, h);
         double res = DynamicGridUtils::norm(r, L);
@@ -155,9 +160,10 @@ int main(int argc, char **argv)
         DynamicGridUtils::compute_error(e, phi, ex, L);
         double rel = DynamicGridUtils::norm(e, L) / DynamicGridUtils::norm(ex, L);
         delete[] e;
-        std::printf("cycle %d relerr %.17g res %.17g center %.17g hash %016llx sweeps %lld exits %lld\n",
+        std::printf("cycle %d relerr %.17g res %.17g center %.17g hash %016llx sweeps %lld exits %lld"
+                    " seconds %.6f\n",
                     k, rel, res, phi[(long long)(N / 2) * N + N / 2],
-                    (unsigned long long)fnv(phi, L), sm.sweeps, sm.exits);
+                    (unsigned long long)fnv(phi, L), sm.sweeps, sm.exits, secs);
         std::fflush(stdout);
     }
     if (argc > 5) {
