@@ -533,7 +533,11 @@ __global__ __launch_bounds__(256) void k_post_rare(PostArgsT<T> a, FixArgsF f)
 // Stage lags behind the loaded row i: xe i, x1 i-1, x2 i-2, x3 i-3, x4 i-4,
 // r(x4) i-5, rc when i-5 = 2jc+1.
 // ---------------------------------------------------------------------------
-constexpr int kPPStride = 114, kPPMargin = 6;
+// 128-column wave tiles owning 116: six stencil levels shrink the validity six columns
+// from the left; on the right the prolongation reads coarse column ic+1 from LDS (no DPP),
+// so six suffice there too (114 + 6/8 before: 1.13-1.14 -> 1.11-1.13 ms; 112 + 8/8 with
+// line-aligned stores: slower, 1.133 ms)
+constexpr int kPPStride = 116, kPPMargin = 6;
 
 // MODE 0: the real pass.  MODE 1 (PGMG_PP_VARIANT=1, measurement only): the same loads
 // and stores with the stencil arithmetic replaced by one add, to separate the memory
