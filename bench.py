@@ -182,7 +182,7 @@ def main():
                     + ")", f"k_postpre_lds<{T},{'true' if r2 else 'false'},"
                            f"{'true' if gen else 'false'}>"),
                 (1, "k_pre<false,true> (finest level: 2 Jacobi sweeps + residual + restriction, "
-                    "fused)", f"k_pre<{T},false,true,2,true>" if gen else f"k_pre<{T},false,true>"),
+                    "fused)", f"k_pre<{T},false,true,2,{'true' if gen else 'false'},false>"),
                 (2, "k_post<true> (finest level: prolongation + 2 Jacobi sweeps, fused)",
                  f"k_post<{T},true,2,false,true>" if gen else f"k_post<{T},true,2,false>")):
             cnt, ms = s.fine_pass_time(which)
