@@ -230,6 +230,12 @@ int pgmg_comm_unique_id(void *out128);
  * grouped send/recv, allreduce(sum, double) and allreduce(min, u32) on a stream; 0 = ok. */
 int pgmg_rccl_selftest(const void *uid128, int device);
 
+/* Measurement: with PGMG_TAIL_PROF=1 in the environment, the LDS tail accumulates shader-
+ * clock cycles per stage kind ([0] wave-team hand-offs, [1] block smooth, [2] block
+ * res+restrict, [3] block prolong, [4] whole kernel, [5] launches, [6] wave smooth, [7] wave
+ * res+restrict+prolong); read (and reset) them.  -1 when the variable is unset. */
+int pgmg_tail_prof(unsigned long long *out16, int reset);
+
 /* In-process rank hub for PGMG_FLAG_LOOPBACK (tests of the strip decomposition). */
 int pgmg_loopback_create(int world, void **hub);
 int pgmg_loopback_destroy(void *hub);

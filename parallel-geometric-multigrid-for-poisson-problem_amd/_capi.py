@@ -103,6 +103,7 @@ SIGNATURES = [
     ("pgmg_device_count", C.c_int, [C.POINTER(C.c_int)]),
     ("pgmg_comm_unique_id", C.c_int, [_P]),
     ("pgmg_rccl_selftest", C.c_int, [_P, C.c_int]),
+    ("pgmg_tail_prof", C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
     ("pgmg_loopback_create", C.c_int, [C.c_int, C.POINTER(_P)]),
     ("pgmg_loopback_destroy", C.c_int, [_P]),
     ("pgmg_plan_strips", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,

@@ -36,7 +36,13 @@ struct TailArgsDev {
     TailLevel<Real> lv[kTailMaxLevels];
     int gamma;
     int wave_n;      // levels with N <= wave_n run on wave 0 alone (no workgroup barriers)
+    // measurement (PGMG_TAIL_PROF=1, pgmg_tail_prof): thread 0 adds shader-clock cycles
+    // [0] wave-team hand-offs, [1] block smooth, [2] block res+restrict, [3] block
+    // prolong, [4] whole kernel, [5] launches, [6] wave smooth, [7] wave res+restrict+prolong
+    unsigned long long *prof;
 };
+
+__device__ __forceinline__ unsigned long long tail_clock() { return __builtin_amdgcn_s_memtime(); }
 
 // Two execution teams for the same level code.  BlockTeam: the whole 1024-thread
 // workgroup, stages separated by __syncthreads.  WaveTeam: wave 0 alone; LDS operations
@@ -213,22 +219,33 @@ __device__ void tail_gcycle(const TailArgsDev<Real> &d, int top, int reps, Real 
         if (descending) {
             if (kBlock && l != top && d.lv[l].N <= d.wave_n) {
                 // the whole gamma-recursion of level l on wave 0
+                const unsigned long long c0 = d.prof ? tail_clock() : 0;
                 if (threadIdx.x < 64)
                     tail_gcycle<WaveTeam, Real>(d, l, d.gamma, E, F, T, red, par, sweeps, exits);
                 __syncthreads();
+                if (d.prof && threadIdx.x == 0) d.prof[0] += tail_clock() - c0;
                 visits[l] = d.gamma - 1;
                 descending = false;
                 continue;
             }
+            const int pi = kBlock ? 1 : 6, pr = kBlock ? 2 : 7;
+            unsigned long long c0 = d.prof ? tail_clock() : 0;
             if (l == last) {
                 tail_smooth<Team>(E + d.lv[l].off, F + d.lv[l].off, d.lv[l], a.coarse_iter, a.eps, T,
                                   red, par, sweeps, exits);
+                if (d.prof && threadIdx.x == 0) d.prof[pi] += tail_clock() - c0;
                 descending = false;
             } else {
                 tail_smooth<Team>(E + d.lv[l].off, F + d.lv[l].off, d.lv[l], a.v1, a.eps, T, red,
                                   par, sweeps, exits);
+                if (d.prof && threadIdx.x == 0) {
+                    const unsigned long long c1 = tail_clock();
+                    d.prof[pi] += c1 - c0;
+                    c0 = c1;
+                }
                 tail_res_restrict<Team>(E + d.lv[l].off, F + d.lv[l].off, d.lv[l],
                                         F + d.lv[l + 1].off, E + d.lv[l + 1].off, d.lv[l + 1], T);
+                if (d.prof && threadIdx.x == 0) d.prof[pr] += tail_clock() - c0;
                 visits[l + 1] = 0;
                 ++l;
             }
@@ -244,9 +261,17 @@ __device__ void tail_gcycle(const TailArgsDev<Real> &d, int top, int reps, Real 
             if (++visits[l] < d.gamma) {
                 descending = true;   // call the cycle on level l again
             } else {
+                const int pi = kBlock ? 1 : 6, pr = kBlock ? 3 : 7;
+                unsigned long long c0 = d.prof ? tail_clock() : 0;
                 tail_prolong<Team>(E + d.lv[p].off, d.lv[p], E + d.lv[l].off, d.lv[l]);
+                if (d.prof && threadIdx.x == 0) {
+                    const unsigned long long c1 = tail_clock();
+                    d.prof[pr] += c1 - c0;
+                    c0 = c1;
+                }
                 tail_smooth<Team>(E + d.lv[p].off, F + d.lv[p].off, d.lv[p], a.v2, a.eps, T, red,
                                   par, sweeps, exits);
+                if (d.prof && threadIdx.x == 0) d.prof[pi] += tail_clock() - c0;
                 l = p;
             }
         }
@@ -291,6 +316,7 @@ template <class Real>
 __global__ __launch_bounds__(kTailThreads) void k_tail(TailArgsDev<Real> d)
 {
     extern __shared__ __attribute__((aligned(16))) double lds[];
+    const unsigned long long k0 = d.prof ? tail_clock() : 0;
     const TailArgsT<Real> &a = d.a;
     const int S = d.S;
     double *red = lds;                                   // kTailThreads / 64 + 1 partial sums
@@ -352,6 +378,10 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(TailArgsDev<Real> d)
         atomicAdd(&a.stats[0], (unsigned long long)sweeps);
         atomicAdd(&a.stats[1], (unsigned long long)exits);
     }
+    if (d.prof && threadIdx.x == 0) {
+        d.prof[4] += tail_clock() - k0;
+        d.prof[5] += 1;
+    }
 }
 
 template <class Real>
@@ -365,6 +395,19 @@ size_t tail_lds_bytes(int N_top, int n_coarse)
         N = (N - 1) / 2 + 1;
     }
     return kTailRed * sizeof(double) + (2 * S + (size_t)N_top * N_top) * sizeof(Real);
+}
+
+// PGMG_TAIL_PROF=1: the per-stage cycle counters of k_tail (measurement only)
+static unsigned long long *tail_prof_buffer()
+{
+    static unsigned long long *buf = [] {
+        unsigned long long *p = nullptr;
+        const char *v = getenv("PGMG_TAIL_PROF");
+        if (v && *v == '1' && hipMalloc(&p, 16 * sizeof(unsigned long long)) == hipSuccess)
+            (void)hipMemset(p, 0, 16 * sizeof(unsigned long long));
+        return p;
+    }();
+    return buf;
 }
 
 template <class Real>
@@ -400,6 +443,7 @@ hipError_t launch_tail_gamma(const TailArgsT<Real> &a, int gamma, hipStream_t s)
         }();
         d.wave_n = wave_n;
     }
+    d.prof = tail_prof_buffer();
     const size_t bytes = tail_lds_bytes<Real>(a.N_top, a.n_coarse);
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute((const void *)k_tail<Real>,
@@ -412,6 +456,21 @@ hipError_t launch_tail_gamma(const TailArgsT<Real> &a, int gamma, hipStream_t s)
 }
 
 template hipError_t launch_tail_gamma<double>(const TailArgsT<double> &, int, hipStream_t);
+
+}  // namespace pgmg
+
+// Read (and optionally reset) the k_tail cycle counters; -1 when PGMG_TAIL_PROF is unset.
+extern "C" int pgmg_tail_prof(unsigned long long *out16, int reset)
+{
+    unsigned long long *b = pgmg::tail_prof_buffer();
+    if (!b || !out16) return -1;
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    if (hipMemcpy(out16, b, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return -2;
+    if (reset) (void)hipMemset(b, 0, 16 * sizeof(unsigned long long));
+    return 0;
+}
+
+namespace pgmg {
 template hipError_t launch_tail_gamma<float>(const TailArgsT<float> &, int, hipStream_t);
 template size_t tail_lds_bytes<double>(int, int);
 template size_t tail_lds_bytes<float>(int, int);
