@@ -19,6 +19,11 @@ namespace pgmg {
 constexpr int kTailMaxLevels = 8;
 constexpr int kTailWaves = kTailThreads / 64;
 constexpr int kTailRed = 2 * kTailWaves + 2;  // doubles of reduction scratch at the LDS base
+#ifndef PGMG_TAIL_SMALL_OFF
+constexpr bool kTailSmallOff = false;          // (compile with -DPGMG_TAIL_SMALL_OFF for A/B)
+#else
+constexpr bool kTailSmallOff = true;
+#endif
 
 template <class Real>
 struct TailLevel {
@@ -112,6 +117,58 @@ __device__ __forceinline__ double tail_jacobi(const Real *cur, Real *out, const 
     return acc;
 }
 
+// The smoother of a level whose interior fits one wave ((N-2)^2 <= 64: N = 5, 9), run by
+// the wave team: one interior point per lane, its iterate and h*h*f in registers, sweeps
+// IN PLACE in LDS (a wave's LDS reads of the old neighbours precede its writes in program
+// order; the compiler fence keeps them there), the check of x_k fused into sweep k+1 and,
+// when it fires, the lane's register copy of x_k written back — no scratch grid, no
+// boundary lanes, no copy pass.  Same expressions and operand order as tail_jacobi.
+template <class Real>
+__device__ void tail_smooth_small(Real *x, const Real *f, const TailLevel<Real> &L, int num_iter,
+                                  double eps, long long &sweeps, long long &exits)
+{
+    const int N = L.N, m = N - 2;
+    const int lane = threadIdx.x & 63;
+    const bool act = lane < m * m;
+    const int mg = (65536 + m - 1) / m;                 // lane / m for lane < 64, m <= 7
+    const int jj = (lane * mg) >> 16;
+    const int k = act ? (1 + jj) * N + 1 + (lane - jj * m) : N + 1;
+    const Real hh = L.hh, ih = L.ih;
+    const Real fk = f[k];
+    const Real hf = hh * fk;
+    Real xc = x[k];
+    auto fence = [] {
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __builtin_amdgcn_wave_barrier();
+    };
+    {   // sweep 1 (no check before it)
+        const Real l = x[k - 1], r = x[k + 1], u = x[k - N], d = x[k + N];
+        const Real nx = Real(0.25) * (hf + l + r + u + d);
+        fence();
+        if (act) x[k] = nx;
+        fence();
+        xc = nx;
+        ++sweeps;
+    }
+    for (int it = 2; it <= num_iter + 1; ++it) {
+        const Real l = x[k - 1], r = x[k + 1], u = x[k - N], d = x[k + N];
+        const Real res = fk - ih * (Real(4) * xc - l - r - u - d);
+        const Real nx = Real(0.25) * (hf + l + r + u + d);
+        fence();
+        if (act) x[k] = nx;
+        fence();
+        const double s = wave_sum(act ? sq(res) : 0.0);
+        if (sqrt(s) < eps) {   // x_{it-1} is the result: the speculative sweep is undone
+            if (act) x[k] = xc;
+            fence();
+            ++exits;
+            return;
+        }
+        xc = nx;
+        ++sweeps;
+    }
+}
+
 // JacobiSmoother::smooth(x, f, N, N, h, num_iter): num_iter+1 sweeps, break as
 // soon as ||r(x_k)|| < eps.  The check of x_k is fused into sweep k+1 (which
 // reads the same neighbourhood); when it fires, sweep k+1's output is dropped.
@@ -120,6 +177,12 @@ __device__ void tail_smooth(Real *x, const Real *f, const TailLevel<Real> &L, in
                             double eps, Real *T, double *red, int &par, long long &sweeps,
                             long long &exits)
 {
+    if constexpr (Team::size == 64) {
+        if ((L.N - 2) * (L.N - 2) <= 64 && !kTailSmallOff) {
+            tail_smooth_small(x, f, L, num_iter, eps, sweeps, exits);
+            return;
+        }
+    }
     Real *cur = x, *oth = T;
     tail_jacobi<Team, Real, false>(cur, oth, f, L);
     Team::sync();
