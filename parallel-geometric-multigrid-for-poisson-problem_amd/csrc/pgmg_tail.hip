@@ -123,48 +123,75 @@ __device__ __forceinline__ double tail_jacobi(const Real *cur, Real *out, const 
 // order; the compiler fence keeps them there), the check of x_k fused into sweep k+1 and,
 // when it fires, the lane's register copy of x_k written back — no scratch grid, no
 // boundary lanes, no copy pass.  Same expressions and operand order as tail_jacobi.
-template <class Real>
+template <int PP, class Real>
 __device__ void tail_smooth_small(Real *x, const Real *f, const TailLevel<Real> &L, int num_iter,
                                   double eps, long long &sweeps, long long &exits)
 {
-    const int N = L.N, m = N - 2;
+    // PP interior points per lane: point q of lane t is interior index t + 64 q
+    const int N = L.N, m = N - 2, nin = m * m;
     const int lane = threadIdx.x & 63;
-    const bool act = lane < m * m;
-    const int mg = (65536 + m - 1) / m;                 // lane / m for lane < 64, m <= 7
-    const int jj = (lane * mg) >> 16;
-    const int k = act ? (1 + jj) * N + 1 + (lane - jj * m) : N + 1;
+    const int mg = (65536 + m - 1) / m;                 // p / m for p < 256, m <= 15
+    bool act[PP];
+    int k[PP];
+    Real fk[PP], hf[PP], xc[PP];
     const Real hh = L.hh, ih = L.ih;
-    const Real fk = f[k];
-    const Real hf = hh * fk;
-    Real xc = x[k];
+    #pragma unroll
+    for (int q = 0; q < PP; ++q) {
+        const int p = lane + 64 * q;
+        act[q] = p < nin;
+        const int jj = (p * mg) >> 16;
+        k[q] = act[q] ? (1 + jj) * N + 1 + (p - jj * m) : N + 1;
+        fk[q] = f[k[q]];
+        hf[q] = hh * fk[q];
+        xc[q] = x[k[q]];
+    }
     auto fence = [] {
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         __builtin_amdgcn_wave_barrier();
     };
     {   // sweep 1 (no check before it)
-        const Real l = x[k - 1], r = x[k + 1], u = x[k - N], d = x[k + N];
-        const Real nx = Real(0.25) * (hf + l + r + u + d);
+        Real nx[PP];
+        #pragma unroll
+        for (int q = 0; q < PP; ++q) {
+            const int kk = k[q];
+            nx[q] = Real(0.25) * (hf[q] + x[kk - 1] + x[kk + 1] + x[kk - N] + x[kk + N]);
+        }
         fence();
-        if (act) x[k] = nx;
+        #pragma unroll
+        for (int q = 0; q < PP; ++q) {
+            if (act[q]) x[k[q]] = nx[q];
+            xc[q] = nx[q];
+        }
         fence();
-        xc = nx;
         ++sweeps;
     }
     for (int it = 2; it <= num_iter + 1; ++it) {
-        const Real l = x[k - 1], r = x[k + 1], u = x[k - N], d = x[k + N];
-        const Real res = fk - ih * (Real(4) * xc - l - r - u - d);
-        const Real nx = Real(0.25) * (hf + l + r + u + d);
+        Real nx[PP];
+        double acc = 0.0;
+        #pragma unroll
+        for (int q = 0; q < PP; ++q) {
+            const int kk = k[q];
+            const Real l = x[kk - 1], r = x[kk + 1], u = x[kk - N], d = x[kk + N];
+            const Real res = fk[q] - ih * (Real(4) * xc[q] - l - r - u - d);
+            if (act[q]) acc += sq(res);
+            nx[q] = Real(0.25) * (hf[q] + l + r + u + d);
+        }
         fence();
-        if (act) x[k] = nx;
+        #pragma unroll
+        for (int q = 0; q < PP; ++q)
+            if (act[q]) x[k[q]] = nx[q];
         fence();
-        const double s = wave_sum(act ? sq(res) : 0.0);
+        const double s = wave_sum(acc);
         if (sqrt(s) < eps) {   // x_{it-1} is the result: the speculative sweep is undone
-            if (act) x[k] = xc;
+            #pragma unroll
+            for (int q = 0; q < PP; ++q)
+                if (act[q]) x[k[q]] = xc[q];
             fence();
             ++exits;
             return;
         }
-        xc = nx;
+        #pragma unroll
+        for (int q = 0; q < PP; ++q) xc[q] = nx[q];
         ++sweeps;
     }
 }
@@ -178,10 +205,13 @@ __device__ void tail_smooth(Real *x, const Real *f, const TailLevel<Real> &L, in
                             long long &exits)
 {
     if constexpr (Team::size == 64) {
-        if ((L.N - 2) * (L.N - 2) <= 64 && !kTailSmallOff) {
-            tail_smooth_small(x, f, L, num_iter, eps, sweeps, exits);
+        const int nin = (L.N - 2) * (L.N - 2);
+        if (!kTailSmallOff && nin <= 64) {
+            tail_smooth_small<1>(x, f, L, num_iter, eps, sweeps, exits);
             return;
         }
+        // (tail_smooth_small<4> for N = 17 on the wave team measured no faster than the
+        // block team there: W at 4097 5.98 vs 5.99 /s, wave_n 17 vs 9)
     }
     Real *cur = x, *oth = T;
     tail_jacobi<Team, Real, false>(cur, oth, f, L);
