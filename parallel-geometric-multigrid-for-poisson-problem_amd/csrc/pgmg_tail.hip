@@ -240,11 +240,45 @@ __device__ void tail_smooth(Real *x, const Real *f, const TailLevel<Real> &L, in
     Team::sync();
 }
 
+// interior point p of an m x m interior (lane p of the wave team): its flat index
+__device__ __forceinline__ int tail_small_index(int p, int m, int N)
+{
+    const int mg = (65536 + m - 1) / m;
+    const int jj = (p * mg) >> 16;
+    return (1 + jj) * N + 1 + (p - jj * m);
+}
+
 // T = r(x) on the interior, 0 on the boundary; then fc = R T (MultiGrid.hpp:70-78)
 template <class Team, class Real>
 __device__ void tail_res_restrict(const Real *x, const Real *f, const TailLevel<Real> &Lf, Real *fc,
                                   Real *ec, const TailLevel<Real> &Lc, Real *T)
 {
+    if constexpr (Team::size == 64) {
+        // wave team, interior <= 64 points: one residual per lane (the restriction reads
+        // only interior fine points, so T's boundary is never needed), then one coarse
+        // point per lane
+        const int N = Lf.N, m = N - 2;
+        if (!kTailSmallOff && m * m <= 64) {
+            const int lane = threadIdx.x & 63;
+            if (lane < m * m) {
+                const int k = tail_small_index(lane, m, N);
+                T[k] = f[k] - Lf.ih * (Real(4) * x[k] - x[k - 1] - x[k + 1] - x[k - N] - x[k + N]);
+            }
+            Team::sync();
+            const int Nc = Lc.N;
+            if (lane < Nc * Nc) {
+                const int jc = tail_row(lane, Lc.rN), ic = lane - jc * Nc;
+                ec[lane] = Real(0);  // MultiGrid.hpp:81-82 e_coarse = 0
+                if (ic > 0 && jc > 0 && ic < Nc - 1 && jc < Nc - 1) {
+                    const int k = (2 * jc) * N + 2 * ic;
+                    fc[lane] = Real(0.25) * T[k] + Real(0.125) * (T[k + 1] + T[k - 1] + T[k + N] + T[k - N]) +
+                               Real(0.0625) * (T[k - N - 1] + T[k - N + 1] + T[k + N - 1] + T[k + N + 1]);
+                }
+            }
+            Team::sync();
+            return;
+        }
+    }
     const int N = Lf.N, n = N * N;
     for (int k = Team::tid(); k < n; k += Team::size) {
         const int j = tail_row(k, Lf.rN);
@@ -275,10 +309,24 @@ __device__ void tail_prolong(Real *x, const TailLevel<Real> &Lf, const Real *e,
                              const TailLevel<Real> &Lc)
 {
     const int N = Lf.N, Nc = Lc.N, n = N * N;
-    for (int k = Team::tid(); k < n; k += Team::size) {
-        const int j = tail_row(k, Lf.rN);
-        const int i = k - j * N;
-        if (i < 2 || j < 2 || i > N - 2 || j > N - 2) continue;
+    // wave team, (N-3)^2 <= 64 corrected points: one per lane, no boundary tests
+    const bool small = Team::size == 64 && !kTailSmallOff && (N - 3) * (N - 3) <= 64;
+    const int m3 = N - 3;
+    for (int k0 = Team::tid(); k0 < n; k0 += Team::size) {
+        int k, j, i;
+        if (small) {
+            if (k0 >= m3 * m3) break;
+            const int mg = (65536 + m3 - 1) / m3;
+            const int jj = (k0 * mg) >> 16;
+            j = 2 + jj;
+            i = 2 + (k0 - jj * m3);
+            k = j * N + i;
+        } else {
+            k = k0;
+            j = tail_row(k, Lf.rN);
+            i = k - j * N;
+            if (i < 2 || j < 2 || i > N - 2 || j > N - 2) continue;
+        }
         const int jc = j >> 1, ic = i >> 1;
         const Real *C0 = e + jc * Nc;
         Real v;
