@@ -17,3 +17,18 @@ def test_rccl_transport_selftest(pgmg):
     lib = pgmg.load()
     rc = lib.pgmg_rccl_selftest(C.cast(uid, C.c_void_p), 0)
     assert rc == 0, lib.pgmg_last_error()
+
+
+@pytest.mark.parametrize("world,rank", [(2, 0), (2, 1), (8, 3)])
+def test_solo_rank_runs(pgmg, world, rank):
+    """PGMG_FLAG_SOLO (measurement mode of scripts/strip_probe.py): one rank of a world-W
+    strip decomposition on one GPU with the null transport runs V, W and F cycles (the
+    values are meaningless; the test pins that the mode works and plans the strips)."""
+    with pgmg.Solver(1025, rank=rank, world=world, flags=pgmg.PGMG_FLAG_SOLO, gather_n=65) as s:
+        s.set_problem()
+        s.vcycle(2)
+        s.wcycle(1)
+        s.fcycle(1)
+        s.sync()
+        lo, hi, nd = pgmg.plan_strips(1025, world, rank, 65, 65)
+        assert nd > 0 and hi > lo
