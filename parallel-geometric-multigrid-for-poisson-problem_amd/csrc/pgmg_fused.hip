@@ -742,8 +742,12 @@ __global__ __launch_bounds__(256, 4) void k_postpre_o4(PostPreArgsT<T> a)
 // are in flight in registers and pair g+1 sits in the other slot; one barrier per
 // row pair.  Coarse rows live in a ring of 3 (pair g reads coarse rows g and g+1).
 // ---------------------------------------------------------------------------
-constexpr int kPPLdsRow = 4 * kPPStride + 2 * kPPMargin + 4;     // 472 doubles per row
-constexpr int kPPLdsCoarse = 2 * kPPStride + kPPMargin + 8;      // 242 doubles per coarse row
+#ifndef PGMG_PP_WAVES   // -DPGMG_PP_WAVES=8 (A/B builds only): 8-wave blocks measured equal
+#define PGMG_PP_WAVES 4   // (1.125-1.147 vs 1.126-1.146 ms; the other k_postpre variants assume 4)
+#endif
+constexpr int kPPWaves = PGMG_PP_WAVES;                            // waves per k_postpre block
+constexpr int kPPLdsRow = kPPWaves * kPPStride + 2 * kPPMargin + 4;          // doubles per row
+constexpr int kPPLdsCoarse = kPPWaves * (kPPStride / 2) + kPPMargin + 8;     // per coarse row
 
 // R2 (row strips): also sum r(x2)^2 into partials3.  When the post check fires the
 // pre-smooth restarts from x1 and its first check is ||r(J(x1))|| = ||r(x2)||; having it
@@ -1000,10 +1004,10 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
 
 template <class T, bool R2, bool GENF, int D = 2, int OCC = 1, int MODE = 0, bool FRECOMP = false,
           int OPT = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC)))
+__global__ __launch_bounds__(64 * kPPWaves) __attribute__((amdgpu_waves_per_eu(OCC)))
 void k_postpre_lds(PostPreArgsT<T> a)
 {
-    __shared__ double red[4];
+    __shared__ double red[kPPWaves];
     __shared__ __attribute__((aligned(16))) T sx[2][kPPR][kPPLdsRow];
     __shared__ __attribute__((aligned(16))) T sf[2][kPPR][GENF ? 1 : kPPLdsRow];
     __shared__ __attribute__((aligned(16))) T se[3][kPPLdsCoarse];
@@ -1308,10 +1312,10 @@ static int env_int(const char *name, int dflt)
 }
 
 static void fused_geometry(int N, int jc0, int jc1, int *threads, int *gx, int *gy, int *rpb,
-                           int stride = 120, int target = 0)
+                           int stride = 120, int target = 0, int maxw = 4)
 {
     const int waves = (N - 2 + stride - 1) / stride;
-    const int wpb = waves < 4 ? waves : 4;
+    const int wpb = waves < maxw ? waves : maxw;
     *threads = 64 * wpb;
     *gx = (waves + wpb - 1) / wpb;
     const int rows = jc1 - jc0;   // coarse rows
@@ -1440,13 +1444,13 @@ void launch_post(const PostArgsT<T> &a0, bool fine, hipStream_t s)
 static int pp_target(int jc0, int jc1)
 {
     const int rounds = std::max(1, std::min(6, 6 * (2 * (jc1 - jc0) + 64) / 16384));
-    return env_int("PGMG_PP_BLOCKS", 512 * rounds);
+    return env_int("PGMG_PP_BLOCKS", (2048 / kPPWaves) * rounds);   // 512 resident at 4 waves
 }
 
 int postpre_blocks(int N, int jc0, int jc1)
 {
     int t, gx, gy, r;
-    fused_geometry(N, jc0, jc1, &t, &gx, &gy, &r, kPPStride, pp_target(jc0, jc1));
+    fused_geometry(N, jc0, jc1, &t, &gx, &gy, &r, kPPStride, pp_target(jc0, jc1), kPPWaves);
     return gx * gy;
 }
 
@@ -1458,7 +1462,7 @@ void launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
     int t, gx, gy, r;
     const int variant = std::is_same<T, double>::value ? env_int("PGMG_PP_VARIANT", 0) : 0;
     fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, variant == 3 ? 128 : kPPStride,
-                   pp_target(a0.jc0, a0.jc1));
+                   pp_target(a0.jc0, a0.jc1), kPPWaves);
     PostPreArgsT<T> a = a0;
     a.rows_per_block = r;
     a.band_stride = 0;
@@ -1530,7 +1534,8 @@ template <class T>
 void launch_smooth4(const PostPreArgsT<T> &a0, hipStream_t s)
 {
     int t, gx, gy, r;
-    fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, kPPStride, pp_target(a0.jc0, a0.jc1));
+    fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, kPPStride, pp_target(a0.jc0, a0.jc1),
+                   kPPWaves);
     PostPreArgsT<T> a = a0;
     a.rows_per_block = r;
     a.band_stride = 0;
