@@ -171,3 +171,26 @@ def test_fcycle_regenerated_rhs_equals_stored(pgmg, N):
             out.append((s.solution(), s.stats()))
     assert np.array_equal(out[0][0].view(np.uint64), out[1][0].view(np.uint64))
     assert out[0][1] == out[1][1]
+
+
+def test_vcycle_graph_after_fused_smooth3_swaps(pgmg, oracle_mod):
+    """The F-cycle's fused smooth(3) makes levels 1.. trade their A/B buffers; a V-cycle
+    hipGraph captured before must be dropped and recaptured (N < 2049: graph replay)."""
+    N = 513
+    rng = np.random.default_rng(5)
+    f = rng.standard_normal((N, N))
+    f[0, :] = f[-1, :] = f[:, 0] = f[:, -1] = 0.0
+    o = oracle_mod.Oracle()
+    want = np.zeros((N, N))
+    for _ in range(3):
+        o.v_cycle(want, f)
+    o.f_cycle_outer(want)
+    for _ in range(3):
+        o.v_cycle(want, f)
+    with pgmg.Solver(N) as s:
+        s.set_problem(None, f)
+        s.vcycle(3)          # eager first cycle, then a captured graph
+        s.fcycle(1)
+        s.vcycle(3)
+        got = s.solution()
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
