@@ -72,6 +72,13 @@ __device__ __forceinline__ V2<T> rstage(V2<T> up, V2<T> ce, V2<T> dn, V2<T> f, T
     return o;
 }
 
+// Row factor of the regenerated RHS through the constant address space: a scalar load
+// (the table is read-only), not a per-row vector load the row loop would wait on
+__device__ __forceinline__ double gsy_s(const double *gsy, int row)
+{
+    return ((const __attribute__((address_space(4))) double *)gsy)[row];
+}
+
 __device__ __forceinline__ bool boundary_row(int row, int N) { return row <= 0 || row >= N - 1; }
 
 // Wave tile: STRIDE owned columns, loaded window starts MARGIN columns to the left;
@@ -170,7 +177,12 @@ __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red)
     const int i_begin = 2 * jcb - 4;
     // a wave whose owned columns all lie past the grid (the last block's spare
     // waves) streams nothing; it still joins the block reduction below
-    const bool idle = (k.c - 2 * (threadIdx.x & 63) + 4) > N - 2;
+    // (c0w: the wave's first column, wave-uniform, so the row loop is scalar-controlled)
+    const int c0w = __builtin_amdgcn_readfirstlane(k.c - 2 * (int)(threadIdx.x & 63));
+    const bool idle = c0w + 4 > N - 2;
+    // wave-uniform: no lane has a boundary column and every prolongation column pair is
+    // corrected (c0 >= 3, c0 + 127 <= N - 3)
+    const bool inner = c0w >= 3 && c0w + 127 <= N - 3;
     const int i_end = idle ? i_begin
                            : i_begin + ((2 * (jce - jcb) + 8 + R - 1) / R) * R;
     V2<T> nx[R], nf[R];
@@ -226,92 +238,108 @@ __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red)
                 }
             }
         }
-        #pragma unroll
-        for (int s = 0; s < R; ++s) {
-            const int ii = i + s;
-            V2<T> a2 = cx[s];
-            if constexpr (PIN) {
-                const int pq = s >> 1;
-                a2 = add_prolong(z, ii, cr[pq], crn[pq], cr[pq + 1], crn[pq + 1], pc, a.Nc);
-            }
-            V2<T> f3;
-            if constexpr (GENF) {
-                const double sy = a.gsy[ii];
-                f3 = mk2<T>((T)(fxa * sy), (T)(fxb * sy));
-            } else {
-                f3 = cf[s];
-            }
-            // x1 row ii-1
-            const V2<T> b2 = jstage(a0, a1, a2, f2, hh, k, boundary_row(ii - 1, N));
-            // r(x1) and x2 on row ii-2
-            const V2<T> r1 = rstage(b0, b1, b2, f1, ih);
-            if constexpr (S1) {
-                // x1 row ii-1 is the result; restriction of r(x1): rows ii-4, ii-3, ii-2 =
-                // 2jc-1, 2jc, 2jc+1 when ii is odd
-                if (store && ii - 1 >= olo && ii - 1 < ohi && k.own) stv(O + (ii - 1) * P, b2);
-                if ((s & 1) == 1) {
-                    const int jc = (ii - 3) >> 1;
-                    const T m2 = dpp_shl(q1.x);
-                    const T u2 = dpp_shl(q0.x);
-                    const T e2 = dpp_shl(r1.x);
-                    const int ic = (k.c + 1) >> 1;
-                    if (jc >= clo && jc < chi && k.own && ic <= a.Nc - 2) {
-                        const T v = T(0.25) * q1.y + T(0.125) * (m2 + q1.x + r1.y + q0.y) +
-                                    T(0.0625) * (q0.x + u2 + r1.x + e2);
-                        a.rc[(long long)jc * a.Pc + ic] = v;
+        // FULL: every row of this iteration is interior to the band, the grid and the
+        // restriction range, and the wave's columns are all interior (no boundary column,
+        // every prolongation column corrected): the per-row range checks and the boundary
+        // selects drop out
+        double gy[R];   // GENF row factors of the iteration, loaded together up front
+        if constexpr (GENF) {
+            #pragma unroll
+            for (int q = 0; q < R; ++q) gy[q] = gsy_s(a.gsy, i + q);
+        }
+        auto rows = [&](auto full_t) {
+            constexpr bool FULL = decltype(full_t)::value;
+            #pragma unroll
+            for (int s = 0; s < R; ++s) {
+                const int ii = i + s;
+                V2<T> a2 = cx[s];
+                if constexpr (PIN) {
+                    const int pq = s >> 1;
+                    a2 = add_prolong<T, !FULL>(z, ii, cr[pq], crn[pq], cr[pq + 1], crn[pq + 1], pc, a.Nc);
+                }
+                V2<T> f3;
+                if constexpr (GENF) {
+                    f3 = mk2<T>((T)(fxa * gy[s]), (T)(fxb * gy[s]));
+                } else {
+                    f3 = cf[s];
+                }
+                // x1 row ii-1
+                const V2<T> b2 = jstage<T, !FULL>(a0, a1, a2, f2, hh, k, boundary_row(ii - 1, N));
+                // r(x1) and x2 on row ii-2
+                const V2<T> r1 = rstage(b0, b1, b2, f1, ih);
+                if constexpr (S1) {
+                    // x1 row ii-1 is the result; restriction of r(x1): rows ii-4, ii-3, ii-2 =
+                    // 2jc-1, 2jc, 2jc+1 when ii is odd
+                    if (store && ii - 1 >= olo && ii - 1 < ohi && k.own) stv(O + (ii - 1) * P, b2);
+                    if ((s & 1) == 1) {
+                        const int jc = (ii - 3) >> 1;
+                        const T m2 = dpp_shl(q1.x);
+                        const T u2 = dpp_shl(q0.x);
+                        const T e2 = dpp_shl(r1.x);
+                        const int ic = (k.c + 1) >> 1;
+                        if (jc >= clo && jc < chi && k.own && ic <= a.Nc - 2) {
+                            const T v = T(0.25) * q1.y + T(0.125) * (m2 + q1.x + r1.y + q0.y) +
+                                        T(0.0625) * (q0.x + u2 + r1.x + e2);
+                            a.rc[(long long)jc * a.Pc + ic] = v;
+                        }
+                    }
+                    q0 = q1;
+                    q1 = r1;
+                    a0 = a1;
+                    a1 = a2;
+                    b0 = b1;
+                    b1 = b2;
+                    f0 = f1;
+                    f1 = f2;
+                    f2 = f3;
+                    continue;
+                }
+                {
+                    const int row = ii - 2;
+                    if ((FULL || (row >= olo && row < ohi)) && k.own) {
+                        acc = sqacc(acc, r1.x);
+                        if (FULL || !k.by) acc = sqacc(acc, r1.y);
                     }
                 }
-                q0 = q1;
-                q1 = r1;
+                const V2<T> c2 = jstage<T, !FULL>(b0, b1, b2, f1, hh, k, boundary_row(ii - 2, N));
+                if (store && (FULL || (ii - 2 >= olo && ii - 2 < ohi)) && k.own) {
+                    if (a.nt & 1) stv_nt(O + (ii - 2) * P, c2);
+                    else stv(O + (ii - 2) * P, c2);
+                }
+                // r(x2) on row ii-3 (garbage on boundary rows; never used there)
+                const V2<T> d2 = rstage(c0, c1, c2, f0, ih);
+                // restriction: rows ii-5, ii-4, ii-3 = 2jc-1, 2jc, 2jc+1 when ii is even
+                if ((s & 1) == 0) {
+                    const int jc = (ii - 4) >> 1;
+                    const T m2 = dpp_shl(d1.x);
+                    const T u2 = dpp_shl(d0.x);
+                    const T e2 = dpp_shl(d2.x);
+                    const int ic = (k.c + 1) >> 1;
+                    if ((FULL || (jc >= clo && jc < chi && ic <= a.Nc - 2)) && k.own) {
+                        const T v = T(0.25) * d1.y + T(0.125) * (m2 + d1.x + d2.y + d0.y) +
+                                         T(0.0625) * (d0.x + u2 + d2.x + e2);
+                        if (a.nt & 2) __builtin_nontemporal_store(v, &a.rc[(long long)jc * a.Pc + ic]);
+                        else a.rc[(long long)jc * a.Pc + ic] = v;
+                    }
+                }
                 a0 = a1;
                 a1 = a2;
                 b0 = b1;
                 b1 = b2;
+                c0 = c1;
+                c1 = c2;
+                d0 = d1;
+                d1 = d2;
                 f0 = f1;
                 f1 = f2;
                 f2 = f3;
-                continue;
             }
-            {
-                const int row = ii - 2;
-                if (row >= olo && row < ohi && k.own) {
-                    acc = sqacc(acc, r1.x);
-                    if (!k.by) acc = sqacc(acc, r1.y);
-                }
-            }
-            const V2<T> c2 = jstage(b0, b1, b2, f1, hh, k, boundary_row(ii - 2, N));
-            if (store && ii - 2 >= olo && ii - 2 < ohi && k.own) {
-                if (a.nt & 1) stv_nt(O + (ii - 2) * P, c2);
-                else stv(O + (ii - 2) * P, c2);
-            }
-            // r(x2) on row ii-3 (garbage on boundary rows; never used there)
-            const V2<T> d2 = rstage(c0, c1, c2, f0, ih);
-            // restriction: rows ii-5, ii-4, ii-3 = 2jc-1, 2jc, 2jc+1 when ii is even
-            if ((s & 1) == 0) {
-                const int jc = (ii - 4) >> 1;
-                const T m2 = dpp_shl(d1.x);
-                const T u2 = dpp_shl(d0.x);
-                const T e2 = dpp_shl(d2.x);
-                const int ic = (k.c + 1) >> 1;
-                if (jc >= clo && jc < chi && k.own && ic <= a.Nc - 2) {
-                    const T v = T(0.25) * d1.y + T(0.125) * (m2 + d1.x + d2.y + d0.y) +
-                                     T(0.0625) * (d0.x + u2 + d2.x + e2);
-                    if (a.nt & 2) __builtin_nontemporal_store(v, &a.rc[(long long)jc * a.Pc + ic]);
-                    else a.rc[(long long)jc * a.Pc + ic] = v;
-                }
-            }
-            a0 = a1;
-            a1 = a2;
-            b0 = b1;
-            b1 = b2;
-            c0 = c1;
-            c1 = c2;
-            d0 = d1;
-            d1 = d2;
-            f0 = f1;
-            f1 = f2;
-            f2 = f3;
-        }
+        };
+        const bool full = !S1 && inner && i >= 3 && i + R <= N && i - 2 >= olo && i + R - 3 < ohi &&
+                          ((i - 4) >> 1) >= clo && ((i + R - 6) >> 1) < chi &&
+                          (!PIN || ((i >> 1) >= 1 && ((i + R - 1) >> 1) <= a.Nc - 2));
+        if (full) rows(std::true_type{});
+        else rows(std::false_type{});
     }
     if constexpr (!S1) {
         const double sum = fused_block_sum(acc, red);
@@ -444,6 +472,11 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
         T crn[PAIRS + 1];
         #pragma unroll
         for (int q = 0; q <= PAIRS; ++q) crn[q] = dpp_shl(cr[q]);
+        double gy[R];   // GENF row factors of the iteration, loaded together up front
+        if constexpr (GENF) {
+            #pragma unroll
+            for (int q = 0; q < R; ++q) gy[q] = gsy_s(a.gsy, i + q);
+        }
         #pragma unroll
         for (int s = 0; s < R; ++s) {
             const int ii = i + s;
@@ -460,8 +493,7 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
             } else {
                 ph = cp[s];
                 if constexpr (GENF) {
-                    const double sy = a.gsy[ii];
-                    f3 = mk2<T>((T)(fxa * sy), (T)(fxb * sy));
+                    f3 = mk2<T>((T)(fxa * gy[s]), (T)(fxb * gy[s]));
                 } else {
                     f3 = cf[s];
                 }
@@ -892,12 +924,12 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
             V2<T> f0 = z;
             if constexpr (!GENF) f0 = ldv(&sf[slot][s][xo]);
             if constexpr (GENF && !FRECOMP) {
-                const double sy = a.gsy[ii];
+                const double sy = gsy_s(a.gsy, ii);
                 f0 = mk2<T>((T)(fxa * sy), (T)(fxb * sy));
             }
             auto fr = [&](int row, const V2<T> &win) -> V2<T> {
                 if constexpr (GENF && FRECOMP) {
-                    const double sy = a.gsy[row];
+                    const double sy = gsy_s(a.gsy, row);
                     return mk2<T>((T)(fxa * sy), (T)(fxb * sy));
                 } else {
                     return win;
