@@ -429,7 +429,9 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
     V2<T> g0 = z, g1 = z, fc = z;
     double acc = 0.0;
     const int i_begin = 2 * jcb - 2;
-    const bool idle = (k.c - 2 * (threadIdx.x & 63) + 4) > N - 2;  // spare wave
+    const int c0w = __builtin_amdgcn_readfirstlane(k.c - 2 * (int)(threadIdx.x & 63));
+    const bool idle = c0w + 4 > N - 2;  // spare wave (wave-uniform)
+    const bool inner = c0w >= 3 && c0w + 127 <= N - 3;   // see pre_body
     const int i_end = idle ? i_begin
                            : i_begin + ((2 * (jce - jcb) + 4 + R - 1) / R) * R;
     const bool pfired = RECOMP && *a.pre_fired != 0u;
@@ -477,57 +479,66 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
             #pragma unroll
             for (int q = 0; q < R; ++q) gy[q] = gsy_s(a.gsy, i + q);
         }
-        #pragma unroll
-        for (int s = 0; s < R; ++s) {
-            const int ii = i + s;
-            const int pq = s >> 1;
-            V2<T> ph, f3;
-            if (RECOMP) {
-                const V2<T> fn = cp[s];  // f row ii+1
-                const V2<T> g2 = jstage(z, z, z, fn, hh, k, boundary_row(ii + 1, N));
-                ph = pfired ? g1 : jstage(g0, g1, g2, fc, hh, k, boundary_row(ii, N));
-                f3 = fc;
-                g0 = g1;
-                g1 = g2;
-                fc = fn;
-            } else {
-                ph = cp[s];
-                if constexpr (GENF) {
-                    f3 = mk2<T>((T)(fxa * gy[s]), (T)(fxb * gy[s]));
+        // FULL: as in pre_body (rows interior to the band, the sum range and the grid;
+        // interior wave columns)
+        auto rows = [&](auto full_t) {
+            constexpr bool FULL = decltype(full_t)::value;
+            #pragma unroll
+            for (int s = 0; s < R; ++s) {
+                const int ii = i + s;
+                const int pq = s >> 1;
+                V2<T> ph, f3;
+                if (RECOMP) {
+                    const V2<T> fn = cp[s];  // f row ii+1
+                    const V2<T> g2 = jstage<T, !FULL>(z, z, z, fn, hh, k, boundary_row(ii + 1, N));
+                    ph = pfired ? g1 : jstage<T, !FULL>(g0, g1, g2, fc, hh, k, boundary_row(ii, N));
+                    f3 = fc;
+                    g0 = g1;
+                    g1 = g2;
+                    fc = fn;
                 } else {
-                    f3 = cf[s];
+                    ph = cp[s];
+                    if constexpr (GENF) {
+                        f3 = mk2<T>((T)(fxa * gy[s]), (T)(fxb * gy[s]));
+                    } else {
+                        f3 = cf[s];
+                    }
                 }
-            }
-            const V2<T> a2 = add_prolong(ph, ii, cr[pq], crn[pq], cr[pq + 1], crn[pq + 1], pc, Nc);
-            const V2<T> b2 = jstage(a0, a1, a2, f2, hh, k, boundary_row(ii - 1, N));
-            if constexpr (S1) {   // the post check fired: x1 row ii-1 is the result
-                if (ii - 1 >= olo && ii - 1 < ohi && k.own) stv(O + (ii - 1) * P, b2);
+                const V2<T> a2 = add_prolong<T, !FULL>(ph, ii, cr[pq], crn[pq], cr[pq + 1], crn[pq + 1], pc, Nc);
+                const V2<T> b2 = jstage<T, !FULL>(a0, a1, a2, f2, hh, k, boundary_row(ii - 1, N));
+                if constexpr (S1) {   // the post check fired: x1 row ii-1 is the result
+                    if (ii - 1 >= olo && ii - 1 < ohi && k.own) stv(O + (ii - 1) * P, b2);
+                    a0 = a1;
+                    a1 = a2;
+                    f1 = f2;
+                    f2 = f3;
+                    continue;
+                }
+                {
+                    const int row = ii - 2;
+                    const V2<T> r1 = rstage(b0, b1, b2, f1, ih);
+                    if ((FULL || (row >= slo && row < shi)) && k.own) {
+                        acc = sqacc(acc, r1.x);
+                        if (FULL || !k.by) acc = sqacc(acc, r1.y);
+                    }
+                }
+                const V2<T> c2 = jstage<T, !FULL>(b0, b1, b2, f1, hh, k, boundary_row(ii - 2, N));
+                if ((FULL || (ii - 2 >= olo && ii - 2 < ohi)) && k.own) {
+                    if (a.nt & 4) stv_nt(O + (ii - 2) * P, c2);
+                    else stv(O + (ii - 2) * P, c2);
+                }
                 a0 = a1;
                 a1 = a2;
+                b0 = b1;
+                b1 = b2;
                 f1 = f2;
                 f2 = f3;
-                continue;
             }
-            {
-                const int row = ii - 2;
-                const V2<T> r1 = rstage(b0, b1, b2, f1, ih);
-                if (row >= slo && row < shi && k.own) {
-                    acc = sqacc(acc, r1.x);
-                    if (!k.by) acc = sqacc(acc, r1.y);
-                }
-            }
-            const V2<T> c2 = jstage(b0, b1, b2, f1, hh, k, boundary_row(ii - 2, N));
-            if (ii - 2 >= olo && ii - 2 < ohi && k.own) {
-                if (a.nt & 4) stv_nt(O + (ii - 2) * P, c2);
-                else stv(O + (ii - 2) * P, c2);
-            }
-            a0 = a1;
-            a1 = a2;
-            b0 = b1;
-            b1 = b2;
-            f1 = f2;
-            f2 = f3;
-        }
+        };
+        const bool full = !S1 && inner && i >= 3 && i + R <= N - 2 && i - 2 >= slo &&
+                          i + R - 3 < shi && ((i + R - 1) >> 1) <= Nc - 2;
+        if (full) rows(std::true_type{});
+        else rows(std::false_type{});
     }
     if constexpr (!S1) {
         const double sum = fused_block_sum(acc, red);
