@@ -424,18 +424,87 @@ void launch_rhs(T *f, const double *sx, const double *sy, double factor, int W, 
                                                                   row0, row1);
 }
 
-// MultiGrid.hpp:187-205 applied to values (compute_coarsest_grid, MultiGrid.hpp:28-55)
-template <class T>
-__global__ void k_restrict_values(const T *Fn, int Nf, long long Pf, T *C, int Nc, long long Pc,
-                                  int jc0, int jc1)
+// MultiGrid.hpp:187-205 applied to values (compute_coarsest_grid, MultiGrid.hpp:28-55).
+// A lane owns coarse column ic and marches down a band of coarse rows; per fine row it
+// loads the aligned pair (2ic-1, 2ic) (one 16-byte load) and takes 2ic+1 from the next
+// lane by DPP (the wave's last lane loads it), so every fine row is read once, whole.
+// Fine row 2jc+1 is kept for the next coarse row.
+// wave_shl:1 with the wave's last lane keeping `last` (bound_ctrl off: a lane without a
+// source lane is not written).  One instruction per dword and no select, so it cannot
+// be sunk into a branch that disables the source lane.
+__device__ __forceinline__ double shl_or_last(double v, double last)
 {
-    const long long n = (long long)(jc1 - jc0) * (Nc - 2);
-    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n;
-         k += (long long)gridDim.x * blockDim.x) {
-        const long long jc = jc0 + k / (Nc - 2), ic = 1 + k % (Nc - 2);
-        const long long q = (2 * jc) * Pf + 2 * ic;
-        C[jc * Pc + ic] = T(0.25) * Fn[q] + T(0.125) * (Fn[q + 1] + Fn[q - 1] + Fn[q + Pf] + Fn[q - Pf]) +
-                          T(0.0625) * (Fn[q - Pf - 1] + Fn[q - Pf + 1] + Fn[q + Pf - 1] + Fn[q + Pf + 1]);
+    const long long b = __double_as_longlong(v), o = __double_as_longlong(last);
+    const int lo = __builtin_amdgcn_update_dpp((int)o, (int)b, 0x130, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), 0x130, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ float shl_or_last(float v, float last)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(last), __float_as_int(v), 0x130,
+                                                      0xF, 0xF, false));
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void k_restrict_values(const T *Fn, long long Pf, T *C, int Nc,
+                                                         long long Pc, int jc0, int jc1, int rpb)
+{
+    const int jb = jc0 + blockIdx.y * rpb;
+    const int je = min(jb + rpb, jc1);
+    if (jb >= je) return;   // uniform over the block
+    const int lane = threadIdx.x & 63;
+    const int ic = 1 + blockIdx.x * 256 + threadIdx.x;
+    const bool own = ic <= Nc - 2;
+    // lanes past the last coarse column load the boundary pair (in range) and store nothing;
+    // lane Nc-1's pair.x is the east column of lane Nc-2
+    const T *__restrict__ q = Fn + 2 * min(ic, Nc - 1) - 1;
+    T uw, uc, ue;
+    {
+        const T *p = q + (long long)(2 * jb - 1) * Pf;
+        const V2<T> v = ldv(p);
+        const T x = lane == 63 ? p[2] : T(0);
+        uw = v.x;
+        uc = v.y;
+        ue = shl_or_last(v.x, x);
+    }
+    // coarse row jc from fine rows 2jc (m) and 2jc+1 (d) and the kept row 2jc-1
+    auto emit = [&](int jc, V2<T> vm, V2<T> vd, T xm, T xd) {
+        const T me = shl_or_last(vm.x, xm), de = shl_or_last(vd.x, xd);
+        if (own)
+            C[(long long)jc * Pc + ic] = T(0.25) * vm.y + T(0.125) * (me + vm.x + vd.y + uc) +
+                                         T(0.0625) * (uw + ue + vd.x + de);
+        uw = vd.x;
+        uc = vd.y;
+        ue = de;
+    };
+    // RB coarse rows (2 RB fine-row loads in flight per lane) per step
+    constexpr int RB = 4;
+    int jc = jb;
+    for (; jc + RB <= je; jc += RB) {
+        const T *m = q + (long long)(2 * jc) * Pf;
+        V2<T> v[2 * RB];
+        T x[2 * RB];
+        #pragma unroll
+        for (int k = 0; k < 2 * RB; ++k) {
+            v[k] = ldv(m + k * Pf);
+            x[k] = T(0);
+        }
+        if (lane == 63) {
+            #pragma unroll
+            for (int k = 0; k < 2 * RB; ++k) x[k] = m[k * Pf + 2];
+        }
+        #pragma unroll
+        for (int r = 0; r < RB; ++r) emit(jc + r, v[2 * r], v[2 * r + 1], x[2 * r], x[2 * r + 1]);
+    }
+    for (; jc < je; ++jc) {
+        const T *m = q + (long long)(2 * jc) * Pf, *d = m + Pf;
+        const V2<T> vm = ldv(m), vd = ldv(d);
+        T xm = T(0), xd = T(0);
+        if (lane == 63) {
+            xm = m[2];
+            xd = d[2];
+        }
+        emit(jc, vm, vd, xm, xd);
     }
 }
 
@@ -443,12 +512,17 @@ template <class T>
 void launch_restrict_values(const T *fine, int Nf, int Pf, T *coarse, int Nc, int Pc, hipStream_t s,
                             int jc0, int jc1)
 {
+    (void)Nf;
     jc0 = jc0 < 1 ? 1 : jc0;
     jc1 = jc1 > Nc - 1 ? Nc - 1 : jc1;
     if (jc1 <= jc0) return;
-    long long nb = ((long long)(jc1 - jc0) * (Nc - 2) + 255) / 256;
-    if (nb > 4096) nb = 4096;
-    k_restrict_values<T><<<dim3((unsigned)nb), dim3(256), 0, s>>>(fine, Nf, Pf, coarse, Nc, Pc, jc0, jc1);
+    const int gx = (Nc - 2 + 255) / 256;
+    // ~2048 workgroups (8 rounds of the resident ones), bands of at least 8 coarse rows
+    const int rows = jc1 - jc0;
+    int rpb = (rows * gx + 2047) / 2048;
+    rpb = rpb < 8 ? 8 : rpb;
+    const int gy = (rows + rpb - 1) / rpb;
+    k_restrict_values<T><<<dim3(gx, gy), dim3(256), 0, s>>>(fine, Pf, coarse, Nc, Pc, jc0, jc1, rpb);
 }
 
 template <class T>
