@@ -1394,9 +1394,21 @@ static int enqueue_fcycle(pgmg_ctx *c)
         sine_tables(c->cfg, 1, 1.0, sx, sy, factor);
     }
     int e;
+    static const bool use_r2 = [] {   // two restriction steps per pass (PGMG_R2=0: one)
+        const char *v = getenv("PGMG_R2");
+        return !(v && *v == '0');
+    }();
     for (int l = 0; l < nb; ++l) {
         Level &L = c->lv[l], &C = c->lv[l + 1];
         if (!is_dist(c, l)) {
+            // the intermediate level's restricted values are dead (the climb overwrites that
+            // level's grid before reading it), so two levels go in one pass
+            if (use_r2 && l + 2 <= nb && !is_dist(c, l + 1)) {
+                const Level &C2 = c->lv[l + 2];
+                launch_restrict2_values(G<T>(L.A), L.P, G<T>(C2.A), C2.N, C2.P, c->s);
+                ++l;
+                continue;
+            }
             launch_restrict_values(G<T>(L.A), L.N, L.P, G<T>(C.A), C.N, C.P, c->s);
             continue;
         }

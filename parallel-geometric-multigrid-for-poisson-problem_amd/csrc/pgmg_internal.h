@@ -145,6 +145,9 @@ void launch_rhs(T *f, const double *sx, const double *sy, double factor, int W, 
 template <class T>
 void launch_restrict_values(const T *fine, int Nf, int Pf, T *coarse, int Nc, int Pc,
                             hipStream_t s, int jc0 = 1, int jc1 = 1 << 30);
+// coarse = R R fine (two levels down in one pass, single grid, all interior rows)
+template <class T>
+void launch_restrict2_values(const T *fine, int Pf, T *coarse, int Nc, int Pc, hipStream_t s);
 template <class T> void launch_fill_rows(T *o, int P, int row0, int row1, hipStream_t s);
 // zero rows 0, 1, N-1 and columns 0, N-1 of an N x N grid (what a prolongation with
 // assign = 1 over rows [2, N-2] leaves unwritten), within rows [r0, r1) (row strips:

@@ -525,6 +525,85 @@ void launch_restrict_values(const T *fine, int Nf, int Pf, T *coarse, int Nc, in
     k_restrict_values<T><<<dim3(gx, gy), dim3(256), 0, s>>>(fine, Pf, coarse, Nc, Pc, jc0, jc1, rpb);
 }
 
+// Two full-weighting steps in one pass: level l+2 = R R (level l) on its interior points,
+// the intermediate level's values computed in registers, never stored (compute_coarsest_grid,
+// MultiGrid.hpp:28-55, restricts level by level; a level-(l+2) interior point reads only
+// interior points of level l+1, so the intermediate grid's frame never matters).  Lane t of
+// a wave owns level-(l+2) column i (63 per wave; lane 63 only supplies its neighbour's east
+// values); per lane and fine row: the two aligned pairs of columns 4i-3 .. 4i, the east
+// column 4i+1 from the next lane; per level-(l+2) row, four fine rows are loaded and two
+// level-(l+1) rows computed.  Every value goes through the reference's expression in the
+// reference's order, so the result is bitwise the two-step one.
+template <class T>
+__device__ __forceinline__ T rfw(T u_w, T u_c, T u_e, T m_w, T m_c, T m_e, T d_w, T d_c, T d_e)
+{
+    return T(0.25) * m_c + T(0.125) * (m_e + m_w + d_c + u_c) + T(0.0625) * (u_w + u_e + d_w + d_e);
+}
+
+template <class T> struct Row4 {   // a lane's fine columns 4i-3 .. 4i and 4i+1
+    T a, b, c, d, e;
+};
+
+template <class T>
+__global__ __launch_bounds__(256) void k_restrict2_values(const T *Fn, long long Pf, T *C, int Nc,
+                                                          long long Pc, int jc0, int jc1, int rpb)
+{
+    const int jb = jc0 + blockIdx.y * rpb;
+    const int je = min(jb + rpb, jc1);
+    if (jb >= je) return;   // uniform over the block
+    const int lane = threadIdx.x & 63;
+    const int i = 1 + blockIdx.x * 252 + (int)(threadIdx.x >> 6) * 63 + lane;
+    const bool own = lane < 63 && i <= Nc - 2;
+    const T *__restrict__ q = Fn + 4 * min(i, Nc - 1) - 3;   // in range (see k_restrict_values)
+    auto ld = [&](int r) {
+        const T *p = q + (long long)r * Pf;
+        const V2<T> v0 = ldv(p), v1 = ldv(p + 2);
+        const T x = lane == 63 ? p[4] : T(0);
+        Row4<T> o;
+        o.a = v0.x;
+        o.b = v0.y;
+        o.c = v1.x;
+        o.d = v1.y;
+        o.e = shl_or_last(v0.x, x);
+        return o;
+    };
+    // the two intermediate values of a lane (columns 2i-1 and 2i) from fine rows u, m, d
+    auto mid = [&](const Row4<T> &u, const Row4<T> &m, const Row4<T> &d, T &A, T &B) {
+        A = rfw(u.a, u.b, u.c, m.a, m.b, m.c, d.a, d.b, d.c);
+        B = rfw(u.c, u.d, u.e, m.c, m.d, m.e, d.c, d.d, d.e);
+    };
+    Row4<T> f3 = ld(4 * jb - 1);   // fine row 4j-1 of the step j
+    T pA, pB;                       // intermediate row 2j-1
+    {
+        const Row4<T> u = ld(4 * jb - 3), m = ld(4 * jb - 2);
+        mid(u, m, f3, pA, pB);
+    }
+    for (int j = jb; j < je; ++j) {
+        const Row4<T> r0 = ld(4 * j), r1 = ld(4 * j + 1), r2 = ld(4 * j + 2), r3 = ld(4 * j + 3);
+        T mA, mB, dA, dB;
+        mid(f3, r0, r1, mA, mB);   // intermediate row 2j
+        mid(r1, r2, r3, dA, dB);   // intermediate row 2j+1
+        const T pE = dpp_shl(pA), mE = dpp_shl(mA), dE = dpp_shl(dA);
+        if (own) C[(long long)j * Pc + i] = rfw(pA, pB, pE, mA, mB, mE, dA, dB, dE);
+        f3 = r3;
+        pA = dA;
+        pB = dB;
+    }
+}
+
+template <class T>
+void launch_restrict2_values(const T *fine, int Pf, T *coarse, int Nc, int Pc, hipStream_t s)
+{
+    const int jc0 = 1, jc1 = Nc - 1;
+    if (jc1 <= jc0) return;
+    const int gx = (Nc - 2 + 251) / 252;
+    const int rows = jc1 - jc0;
+    int rpb = (rows * gx + 2047) / 2048;
+    rpb = rpb < 4 ? 4 : rpb;
+    const int gy = (rows + rpb - 1) / rpb;
+    k_restrict2_values<T><<<dim3(gx, gy), dim3(256), 0, s>>>(fine, Pf, coarse, Nc, Pc, jc0, jc1, rpb);
+}
+
 template <class T>
 __global__ void k_fill_rows(T *o, long long P, int row0, int row1)
 {
@@ -656,6 +735,7 @@ void launch_from_double(const double *src, int N, T *dst, int P, int row0, int r
     template void launch_rhs<T>(T *, const double *, const double *, double, int, int, int, int,   \
                                 hipStream_t);                                                      \
     template void launch_restrict_values<T>(const T *, int, int, T *, int, int, hipStream_t, int, int); \
+    template void launch_restrict2_values<T>(const T *, int, T *, int, int, hipStream_t);            \
     template void launch_fill_rows<T>(T *, int, int, int, hipStream_t);                            \
     template void launch_zero_frame<T>(T *, int, int, hipStream_t, int, int);                      \
     template void launch_resnorm_partials<T>(const T *, const T *, double *, T, int, int, int, int, \
