@@ -120,6 +120,12 @@ struct pgmg_ctx {
     // F-cycle (pgmg_fcycle): analytic level-0 RHS of the FMG h chain, and the sine
     // tables of every level (built on the first call)
     pgmg::Grid Ffmg;
+    // F-cycle climb: regenerated-RHS tables (factor*sx, sy) of every bulk level of the FMG
+    // chain (level l at fmg_gtab + fmg_goff[l]); the level whose V-cycle and smooth(3) are
+    // being enqueued regenerates its analytic f in-kernel (gen_level, lgfx, lgsy)
+    std::vector<size_t> fmg_goff;
+    int gen_level = 0;
+    const double *lgfx = nullptr, *lgsy = nullptr;
     std::vector<pgmg::Grid> Ffmg_l;   // the analytic RHS of bulk levels 1.. of the FMG climb
     bool fmg_rhs_ready = false;   // Ffmg holds the level-0 analytic RHS of the FMG h chain
     double *fmg_tab = nullptr;

@@ -290,8 +290,9 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     // coarse rows this rank restricts into (its strip's rows; the fix-up honours them too)
     pa.rc_lo = pa.jc0 > 1 ? pa.jc0 : 1;
     pa.rc_hi = pa.jc1 < C.N - 1 ? pa.jc1 : C.N - 1;
-    pa.gfx = l == 0 ? c->rgfx : nullptr;   // level 0 with an analytic RHS: regenerate f
-    pa.gsy = l == 0 ? c->rgsy : nullptr;
+    // level 0 with an analytic RHS, or the F climb's current level: regenerate f in-kernel
+    pa.gfx = l == 0 ? c->rgfx : (l == c->gen_level ? c->lgfx : nullptr);
+    pa.gsy = l == 0 ? c->rgsy : (l == c->gen_level ? c->lgsy : nullptr);
     pa.pin_ec = pin ? G<T>(C.A) : nullptr;
     FixArgsF fa{};
     fa.partials = c->partials;
@@ -341,8 +342,8 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
         po.sum_hi = L.u1;
         fa.np = fused_blocks(L.N, po.jc0, po.jc1);
     }
-    po.gfx = l == 0 ? c->rgfx : nullptr;
-    po.gsy = l == 0 ? c->rgsy : nullptr;
+    po.gfx = pa.gfx;
+    po.gsy = pa.gsy;
     lp = chk_partials(c, fa.np, l);
     if (lp) po.partials = lp;
     ev = fine ? timed_begin(c, 2) : -1;
@@ -1314,16 +1315,22 @@ static int fmg_tables(pgmg_ctx *c)
     }
     HIPC(hipMalloc((void **)&c->fmg_tab, tab.size() * sizeof(double)));
     HIPC(hipMemcpy(c->fmg_tab, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice));
-    // the level-0 RHS of the FMG chain, regenerated in the level-0 passes like set_problem's
+    // the RHS of the FMG chain on every bulk level, regenerated in that level's passes like
+    // set_problem's level-0 RHS: per level [8 | factor*sx (N) | 1024 | 8 | sy (N) | 16]
     if (c->nb > 0) {
-        const int N = c->lv[0].N;
-        std::vector<double> sx, sy;
-        double factor;
-        sine_tables(c->cfg, N, fmg_h(c->cfg, N), sx, sy, factor);
-        const int nx = 8 + N + 1024, ny = 8 + N + 16;
-        std::vector<double> g((size_t)nx + ny, 0.0);
-        for (int i = 0; i < N; ++i) g[8 + i] = factor * sx[i];
-        for (int j = 0; j < N; ++j) g[(size_t)nx + 8 + j] = sy[j];
+        std::vector<double> g;
+        c->fmg_goff.assign(c->nb, 0);
+        for (int l = 0; l < c->nb; ++l) {
+            const int N = c->lv[l].N;
+            std::vector<double> sx, sy;
+            double factor;
+            sine_tables(c->cfg, N, fmg_h(c->cfg, N), sx, sy, factor);
+            const size_t o = g.size(), nx = 8 + N + 1024, ny = 8 + N + 16;
+            c->fmg_goff[l] = o;
+            g.resize(o + nx + ny, 0.0);
+            for (int i = 0; i < N; ++i) g[o + 8 + i] = factor * sx[i];
+            for (int j = 0; j < N; ++j) g[o + nx + 8 + j] = sy[j];
+        }
         HIPC(hipMalloc((void **)&c->fmg_gtab, g.size() * sizeof(double)));
         HIPC(hipMemcpy(c->fmg_gtab, g.data(), g.size() * sizeof(double), hipMemcpyHostToDevice));
     }
@@ -1353,6 +1360,8 @@ static int enqueue_smooth3_fused(pgmg_ctx *c, int l)
     q.phi = G<T>(L.A);
     q.f = G<T>(L.F);
     q.x4 = G<T>(L.B);
+    q.gfx = l == c->gen_level ? c->lgfx : nullptr;   // the climb's level: f regenerated
+    q.gsy = l == c->gen_level ? c->lgsy : nullptr;
     q.partials1 = c->partials;
     q.partials2 = c->partials2;
     q.partials3 = c->partials3;
@@ -1458,6 +1467,17 @@ static int enqueue_fcycle(pgmg_ctx *c)
         if (l > 0) std::swap(L.F, c->Ffmg_l[l]);
         if (!c->fmg_rhs_ready)
             launch_rhs(G<T>(L.F), sx, sx + L.N, factor, L.N, L.P, r0, r1, c->s);
+        // this level's passes regenerate its analytic f (bitwise the stored one); its
+        // rare paths and the coarser levels read theirs from memory
+        static const bool gen_l = [] {
+            const char *v = getenv("PGMG_GEN_LEVELS");
+            return !(v && *v == '0');
+        }();
+        if (l > 0 && gen_l && c->rgfx != nullptr) {
+            c->gen_level = l;
+            c->lgfx = c->fmg_gtab + c->fmg_goff[l] + 8;
+            c->lgsy = c->fmg_gtab + c->fmg_goff[l] + (8 + L.N + 1024) + 8;
+        }
         // phi_fine = 0 + P phi_coarse (MultiGrid.hpp:159-164): the prolongation assigns the
         // interior, the frame (boundary, and row/column 1 the reference never corrects) is
         // zeroed; the ping-pong buffer's frame mirrors it
@@ -1474,6 +1494,8 @@ static int enqueue_fcycle(pgmg_ctx *c)
             if (dist && is_dist(c, l + 1) && (e = c->comm->halo(C.A, C, 3, c->s))) return e;
             if ((e = enqueue_fused_level<T>(c, l, 1, false, true))) return e;
             if (l > 0 && (e = enqueue_smooth3_fused<T>(c, l))) return e;
+            c->gen_level = 0;
+            c->lgfx = c->lgsy = nullptr;
             if (l > 0) std::swap(L.F, c->Ffmg_l[l]);
             continue;
         }
@@ -1492,6 +1514,8 @@ static int enqueue_fcycle(pgmg_ctx *c)
         if (p.row1 > p.row0) launch_prolong(p, c->s);
         e = enqueue_cycle_t<T>(c, l, 1, false);
         if (e) return e;
+        c->gen_level = 0;   // the unfused climb streams f
+        c->lgfx = c->lgsy = nullptr;
         if (l > 0 && (e = enqueue_smooth<T>(c, l, 0, 3, false))) return e;
         if (l > 0) std::swap(L.F, c->Ffmg_l[l]);
     }

@@ -24,7 +24,8 @@ struct PreArgsT {
     int rows_per_block;
     const unsigned *cond;       // non-null: run only when *cond != 0
     unsigned *fired;            // non-null: the fix-up records whether the check fired
-    // non-null: f is the analytic RHS, regenerated as (T)(gfx[i] * gsy[j]) (level 0 only)
+    // non-null: f is the analytic RHS, regenerated as (T)(gfx[i] * gsy[j]) (level 0, or
+    // the level of the F climb whose V-cycle and smooth(3) run)
     const double *gfx, *gsy;
     int nt;                     // set by launch_pre: bit 0 x2, bit 1 rc stores non-temporal
     // non-null (F-cycle): x0 is not read but is the prolongation of this coarse grid into a
@@ -55,7 +56,8 @@ struct PostArgsT {
     int sum_lo, sum_hi;         // sum_hi > sum_lo: the early-exit partial sums cover only
                                 // these rows (the rank's own) while [row_lo, row_hi) is
                                 // written (the strip plus kPostExt rows past each edge)
-    // non-null: f is the analytic RHS, regenerated as (T)(gfx[i] * gsy[j]) (level 0 only)
+    // non-null: f is the analytic RHS, regenerated as (T)(gfx[i] * gsy[j]) (level 0, or
+    // the level of the F climb whose V-cycle and smooth(3) run)
     const double *gfx, *gsy;
     int nt;                     // set by launch_post: bit 2 x2 stores non-temporal
 };

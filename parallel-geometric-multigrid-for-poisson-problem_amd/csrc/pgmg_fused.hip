@@ -1419,6 +1419,7 @@ void launch_pre(const PreArgsT<T> &a0, bool x0_zero, bool fine, hipStream_t s)
     if (a.pin_ec != nullptr) {   // F-cycle: x0 = prolongation of the coarse grid
         if (fine && a.gfx != nullptr) k_pre<T, false, true, 2, true, true><<<g, b, 0, s>>>(a);
         else if (fine) k_pre<T, false, true, 2, false, true><<<g, b, 0, s>>>(a);
+        else if (a.gfx != nullptr) k_pre<T, false, false, 2, true, true><<<g, b, 0, s>>>(a);
         else k_pre<T, false, false, 2, false, true><<<g, b, 0, s>>>(a);
         return;
     }
@@ -1582,7 +1583,8 @@ void launch_smooth4(const PostPreArgsT<T> &a0, hipStream_t s)
     PostPreArgsT<T> a = a0;
     a.rows_per_block = r;
     a.band_stride = 0;
-    k_postpre_lds<T, true, false, 2, 1, 0, false, 64><<<dim3(gx, gy), dim3(t), 0, s>>>(a);
+    if (a.gfx != nullptr) k_postpre_lds<T, true, true, 2, 1, 0, false, 64><<<dim3(gx, gy), dim3(t), 0, s>>>(a);
+    else k_postpre_lds<T, true, false, 2, 1, 0, false, 64><<<dim3(gx, gy), dim3(t), 0, s>>>(a);
 }
 
 __device__ __forceinline__ double block_sum_strided(const double *p, int n, double *red)
