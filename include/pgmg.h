@@ -91,6 +91,15 @@ extern "C" {
 #define PGMG_FLAG_LOOPBACK 8u    /* world > 1 with ranks as threads of one process on
                                     one GPU: nccl_unique_id is a pgmg_loopback hub
                                     (test transport for the strip decomposition)    */
+/* Alternative execution plans with the same results (each is bitwise-tested against the
+ * default and the oracle; they exist to test the default's building blocks apart): */
+#define PGMG_FLAG_NO_RECOMPUTE 256u /* coarse levels store their pre-smoothed iterate
+                                       instead of recomputing it from f in k_post     */
+#define PGMG_FLAG_NO_PIN 512u       /* F-cycle: a separate prolongation pass into the
+                                       zeroed finer grid instead of k_pre computing it
+                                       on the fly                                      */
+#define PGMG_FLAG_NO_R2 1024u       /* F-cycle: one full-weighting level per restriction
+                                       pass instead of two                             */
 
 typedef struct pgmg_config {
     int N;             /* points per side incl. boundary; 2^k + 1, k >= 2        */
@@ -109,6 +118,15 @@ typedef struct pgmg_config {
     int gather_n;      /* levels with N <= gather_n collapse to one grid, replicated
                           on every rank (world > 1)                               */
     int precision;     /* PGMG_PRECISION_FP64 (default) or PGMG_PRECISION_FP32    */
+    int cross_min_n;   /* the finest level's post-smooth of cycle k and pre-smooth of
+                          cycle k+1 are one pass from this N up (default 2049; small
+                          values let tests exercise it on small grids)            */
+    int spec_segment;  /* speculative calls: at most this many cycles per validated
+                          segment (0 = sized by the log buffer; tests set it small) */
+    double comm_timeout_s; /* row strips over RCCL: a stream wait that sees no progress
+                          for this long aborts the communicator and returns
+                          PGMG_ERR_COMM (default 600); RCCL's asynchronous error
+                          state is polled while waiting                            */
 } pgmg_config;
 
 typedef struct pgmg_ctx pgmg_ctx;
@@ -139,6 +157,9 @@ int pgmg_sync(pgmg_ctx *ctx);
 /* Download phi (N*N, reference layout).  world > 1: every rank receives the
  * full grid (strips are gathered to all ranks). */
 int pgmg_get_solution(pgmg_ctx *ctx, double *phi_host);
+/* The same with the strips gathered to rank `root` only (collective: every rank calls it;
+ * ranks other than root may pass phi_host = NULL).  root < 0: every rank, as above. */
+int pgmg_gather_solution(pgmg_ctx *ctx, int root, double *phi_host);
 
 /* sqrt(sum over interior of r^2) for the current phi (synchronous). */
 int pgmg_residual_norm(pgmg_ctx *ctx, double *out);
@@ -230,7 +251,8 @@ int pgmg_comm_unique_id(void *out128);
  * grouped send/recv, allreduce(sum, double) and allreduce(min, u32) on a stream; 0 = ok. */
 int pgmg_rccl_selftest(const void *uid128, int device);
 
-/* Measurement: with PGMG_TAIL_PROF=1 in the environment, the LDS tail accumulates shader-
+/* Measurement (libpgmg_ab.so, built with -DPGMG_TUNING; the product library always
+ * returns -1): with PGMG_TAIL_PROF=1 in the environment, the LDS tail accumulates shader-
  * clock cycles per stage kind ([0] wave-team hand-offs, [1] block smooth, [2] block
  * res+restrict, [3] block prolong, [4] whole kernel, [5] launches, [6] wave smooth, [7] wave
  * res+restrict+prolong); read (and reset) them.  -1 when the variable is unset. */
@@ -239,6 +261,9 @@ int pgmg_tail_prof(unsigned long long *out16, int reset);
 /* In-process rank hub for PGMG_FLAG_LOOPBACK (tests of the strip decomposition). */
 int pgmg_loopback_create(int world, void **hub);
 int pgmg_loopback_destroy(void *hub);
+/* Test hook: the at_group-th transport group (halo exchange, gather) rank `rank` starts
+ * from now on fails with PGMG_ERR_COMM (0 = never). */
+int pgmg_loopback_fail(void *hub, int rank, long long at_group);
 
 /* Host-only strip plan: the finest-level rows [lo, hi) rank `rank` owns and the
  * number of strip-distributed levels (0: too small to split, replicas). */

@@ -5,7 +5,8 @@
  * restatement can be diffed against the reference and timed as bench.py's
  * cpu_baseline ("port") on the GPU box, where /root/reference does not exist.
  *
- * Usage: mg_cpu_exec_port <V|W|F> <N> <cycles> <eps> [phi_out.bin]
+ * Usage: mg_cpu_exec_port <V|W|F|G> <N> <cycles> <eps> [phi_out.bin]
+ *   G = FMG start + W-cycles (BASELINE config 5): cycle 1 is an F-cycle, later ones W
  */
 #define _POSIX_C_SOURCE 200809L
 #include <stdint.h>
@@ -39,7 +40,7 @@ static double now_s(void)
 int main(int argc, char **argv)
 {
     if (argc < 5) {
-        fprintf(stderr, "usage: %s <V|W|F> <N> <cycles> <eps> [phi_out.bin]\n", argv[0]);
+        fprintf(stderr, "usage: %s <V|W|F|G> <N> <cycles> <eps> [phi_out.bin]\n", argv[0]);
         return 2;
     }
     char kind = argv[1][0];
@@ -58,7 +59,7 @@ int main(int argc, char **argv)
         double t0 = now_s();
         if (kind == 'V')
             orc_v_cycle(&c, phi, f, N, h);
-        else if (kind == 'W')
+        else if (kind == 'W' || (kind == 'G' && k > 1))
             orc_w_cycle(&c, phi, f, N, h);
         else
             orc_f_cycle_outer(&c, phi, N);

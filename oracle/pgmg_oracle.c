@@ -134,18 +134,35 @@ void orc_exact(const orc_ctx *c, double *u, double h, int W, int H)
     }
 }
 
+/* ||r(x)|| of Smoother.hpp:75-76 without the residual buffer: the same r values
+ * (orc_residual's expression, rounded to `real`), squared and summed in the same
+ * sequential index order as orc_norm over the whole array — the boundary entries of the
+ * reference's buffer are 0 and adding +0.0 leaves the sum unchanged — so the result is
+ * bitwise orc_norm(r, L).  Saves one grid of host memory (N = 32769 goldens). */
+static double orc_residual_norm_seq(const real *x, const real *f, int W, int H, double h)
+{
+    const real ih = (real)(1.0 / (h * h));
+    double s = 0.0;
+    for (int y = 1; y < H - 1; ++y) {
+        for (int xi = 1; xi < W - 1; ++xi) {
+            long long k = (long long)y * W + xi;
+            const real r = f[k] - ih * (4 * x[k] - x[k - 1] - x[k + 1] - x[k - W] - x[k + W]);
+            s += (double)r * (double)r;
+        }
+    }
+    return sqrt(s);
+}
+
 /* ---- Jacobi smoother (Smoother.hpp:38-116) ------------------------------
- * Returns the number of sweeps performed.  `work` must hold 2*W*H elements.
+ * Returns the number of sweeps performed.  `work` must hold W*H elements.
  */
 int orc_jacobi_smooth(orc_ctx *c, real *x, const real *f, int W, int H, double h,
                       int num_iter, real *work)
 {
     long long L = (long long)W * H;
     real *out = work;       /* Smoother.hpp:46-47: seeded with x */
-    real *r = work + L;     /* Smoother.hpp:75: residual buffer, boundary 0 */
     const real hh = (real)(h * h);
     memcpy(out, x, sizeof(real) * L);
-    orc_zero(r, L);
     int done = 0;
     c->smooth_calls++;
     for (int it = 0; it <= num_iter; ++it) {
@@ -158,8 +175,7 @@ int orc_jacobi_smooth(orc_ctx *c, real *x, const real *f, int W, int H, double h
         memcpy(x, out, sizeof(real) * L);
         ++done;
         c->sweeps++;
-        orc_residual(r, x, f, W, H, h);
-        double nr = orc_norm(r, L);
+        double nr = orc_residual_norm_seq(x, f, W, H, h);
         if (nr < c->eps) {
             c->early_exits++;
             break;
@@ -202,59 +218,61 @@ void orc_prolong(real *F, const real *C, int Nf, int Nc)
 
 static real *orc_alloc(long long n) { return (real *)calloc((size_t)n, sizeof(real)); }
 
+/* one smoother call with its own scratch grid (allocated only while it runs) */
+static void orc_smooth_alloc(orc_ctx *c, real *x, const real *f, int N, double h, int num_iter)
+{
+    real *work = orc_alloc((long long)N * N);
+    orc_jacobi_smooth(c, x, f, N, N, h, num_iter, work);
+    free(work);
+}
+
 /* MultiGrid.hpp:57-94 */
 void orc_v_cycle(orc_ctx *c, real *phi, const real *f, int N, double h)
 {
     long long L = (long long)N * N;
-    real *work = orc_alloc(2 * L);
     if (N <= c->n_coarse) {
-        orc_jacobi_smooth(c, phi, f, N, N, h, c->coarse_iter, work);
-        free(work);
+        orc_smooth_alloc(c, phi, f, N, h, c->coarse_iter);
         return;
     }
-    orc_jacobi_smooth(c, phi, f, N, N, h, c->v1, work);
+    orc_smooth_alloc(c, phi, f, N, h, c->v1);
     real *res = orc_alloc(L);
     orc_residual(res, phi, f, N, N, h);
     int Nc = (N - 1) / 2 + 1;
     long long Lc = (long long)Nc * Nc;
     real *rc = orc_alloc(Lc);
     orc_restrict(res, rc, N, Nc);
+    free(res);   /* dead from here (host memory at N = 32769) */
     real *ec = orc_alloc(Lc);
     orc_v_cycle(c, ec, rc, Nc, 2 * h);
     orc_prolong(phi, ec, N, Nc);
-    orc_jacobi_smooth(c, phi, f, N, N, h, c->v2, work);
-    free(res);
+    orc_smooth_alloc(c, phi, f, N, h, c->v2);
     free(rc);
     free(ec);
-    free(work);
 }
 
 /* MultiGrid.hpp:96-136 */
 void orc_w_cycle(orc_ctx *c, real *phi, const real *f, int N, double h)
 {
     long long L = (long long)N * N;
-    real *work = orc_alloc(2 * L);
     if (N <= c->n_coarse) {
-        orc_jacobi_smooth(c, phi, f, N, N, h, c->coarse_iter, work);
-        free(work);
+        orc_smooth_alloc(c, phi, f, N, h, c->coarse_iter);
         return;
     }
-    orc_jacobi_smooth(c, phi, f, N, N, h, c->v1, work);
+    orc_smooth_alloc(c, phi, f, N, h, c->v1);
     real *res = orc_alloc(L);
     orc_residual(res, phi, f, N, N, h);
     int Nc = (N - 1) / 2 + 1;
     long long Lc = (long long)Nc * Nc;
     real *rc = orc_alloc(Lc);
     orc_restrict(res, rc, N, Nc);
+    free(res);   /* dead from here (host memory at N = 32769) */
     real *ec = orc_alloc(Lc);
     for (int i = 0; i < c->alpha; ++i)
         orc_w_cycle(c, ec, rc, Nc, 2.0 * h);
     orc_prolong(phi, ec, N, Nc);
-    orc_jacobi_smooth(c, phi, f, N, N, h, c->v2, work);
-    free(res);
+    orc_smooth_alloc(c, phi, f, N, h, c->v2);
     free(rc);
     free(ec);
-    free(work);
 }
 
 /* MultiGrid.hpp:28-55 — restrict `fine` repeatedly down to N_coarsest.
@@ -290,9 +308,7 @@ void orc_f_cycle(orc_ctx *c, const real *phi, const real *f, int N_init, double 
     memcpy(phic, phi, sizeof(real) * (size_t)L);
     memcpy(fc, f, sizeof(real) * (size_t)L);
     while (N < N_final) {
-        real *work = orc_alloc(2 * (long long)N * N);
-        orc_jacobi_smooth(c, phic, fc, N, N, h, 3, work);
-        free(work);
+        orc_smooth_alloc(c, phic, fc, N, h, 3);
         int Nf = 2 * N - 1;
         long long Lf = (long long)Nf * Nf;
         real *phif = orc_alloc(Lf);

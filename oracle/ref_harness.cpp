@@ -6,7 +6,8 @@
 // copied into this repository.  Used to generate tests/golden/ and to pin
 // oracle/pgmg_oracle.c bit for bit.
 //
-// Usage: ref_harness <V|W|F> <N> <cycles> <eps> [phi_out.bin]
+// Usage: ref_harness <V|W|F|G> <N> <cycles> <eps> [phi_out.bin]
+//   G = FMG start + W-cycles (BASELINE config 5): cycle 1 is an F-cycle, later ones W
 // Prints one line per cycle:
 //   cycle <k> relerr <e> res <r> center <phi[(N/2)*N+N/2]> hash <fnv64> sweeps <s> exits <x>
 //   seconds <wall time of the reference's cycle call alone>  (bench.py's cpu_baseline)
@@ -29,14 +30,28 @@
 #include <string>
 #include <vector>
 
+// Leak reclaimer: JacobiSmoother::smooth allocates a residual buffer per sweep and never
+// frees it (Smoother.hpp:75): 2 GB per sweep at N = 16385.  smooth() hands no
+// pointer out, so every new[] made inside one smooth() call and still live when it
+// returns is garbage; CountingJacobi frees it (this is what lets the harness run 30+
+// cycles at 16385).  Values are unaffected: the buffers are dead.
+static std::vector<void *> *g_track = nullptr;
+
 void *operator new[](std::size_t n)
 {
     void *p = std::calloc(n ? n : 1, 1);
     if (!p) throw std::bad_alloc();
+    if (g_track) g_track->push_back(p);
     return p;
 }
-void operator delete[](void *p) noexcept { std::free(p); }
-void operator delete[](void *p, std::size_t) noexcept { std::free(p); }
+static void untrack(void *p)
+{
+    if (!g_track || !p) return;
+    for (auto &q : *g_track)
+        if (q == p) { q = g_track->back(); g_track->pop_back(); return; }
+}
+void operator delete[](void *p) noexcept { untrack(p); std::free(p); }
+void operator delete[](void *p, std::size_t) noexcept { untrack(p); std::free(p); }
 
 #define private public
 #include "2_part_MG/MultiGrid.hpp"
@@ -51,7 +66,11 @@ struct CountingJacobi : public JacobiSmoother {
     {
         (void)residuals;
         std::vector<double> r;
+        std::vector<void *> live;
+        g_track = &live;
         JacobiSmoother::smooth(x, f, w, hgt, h, num_iter, x_true, &r, errors);
+        g_track = nullptr;
+        for (void *p : live) std::free(p);
         sweeps += (long long)r.size();
         if (!r.empty() && r.back() < epsilon) exits++;
     }
@@ -113,7 +132,7 @@ int main(int argc, char **argv)
 {
     if (argc > 1 && argv[1][0] == 'O') return op_mode(argc, argv);
     if (argc < 5) {
-        std::fprintf(stderr, "usage: %s <V|W|F> <N> <cycles> <eps> [phi_out.bin]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s <V|W|F|G> <N> <cycles> <eps> [phi_out.bin]\n", argv[0]);
         return 2;
     }
     const char kind = argv[1][0];
@@ -142,7 +161,7 @@ int main(int argc, char **argv)
         const auto t0 = std::chrono::steady_clock::now();
         if (kind == 'V') {
             mg.v_cycle(phi, f, N, h);
-        } else if (kind == 'W') {
+        } else if (kind == 'W' || (kind == 'G' && k > 1)) {
             mg.w_cycle(phi, f, N, h);
         } else {
             double *p0 = nullptr;

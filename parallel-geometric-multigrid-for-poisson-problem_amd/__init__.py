@@ -12,6 +12,7 @@ Import name: the directory name is not a Python identifier, so load it with
 """
 import ctypes as C
 import pathlib
+import contextlib
 import subprocess
 
 import numpy as np
@@ -19,17 +20,19 @@ import numpy as np
 from ._capi import (PGMG_FLAG_LOOPBACK, PGMG_FLAG_NO_CROSS, PGMG_FLAG_NO_GRAPH,
                     PGMG_FLAG_STORED_RHS, PGMG_FLAG_EXACT_DIST, PGMG_FLAG_SOLO,
                     PGMG_FLAG_TIME_FINE, PGMG_PRECISION_FP32, PGMG_PRECISION_FP64,
-                    PGMG_FLAG_UNFUSED, PGMG_PROLONG_REFERENCE,
+                    PGMG_FLAG_UNFUSED, PGMG_FLAG_NO_RECOMPUTE, PGMG_FLAG_NO_PIN,
+                    PGMG_FLAG_NO_R2, PGMG_PROLONG_REFERENCE,
                     PGMG_PROLONG_SYMMETRIC, PgmgConfig, PgmgError, check, load)
 
 PKG_DIR = pathlib.Path(__file__).resolve().parent
 
 __all__ = [
-    "build", "load", "Solver", "PgmgConfig", "PgmgError", "ops",
+    "build", "load", "Solver", "PgmgConfig", "PgmgError", "ops", "config_overrides",
     "PGMG_FLAG_NO_GRAPH", "PGMG_FLAG_TIME_FINE", "PGMG_FLAG_UNFUSED", "PGMG_FLAG_LOOPBACK", "PGMG_FLAG_NO_CROSS",
     "PGMG_PROLONG_REFERENCE", "plan_strips", "LoopbackHub", "unique_id",
     "PGMG_PROLONG_SYMMETRIC", "PGMG_PRECISION_FP64", "PGMG_PRECISION_FP32",
     "PGMG_FLAG_STORED_RHS", "PGMG_FLAG_EXACT_DIST", "PGMG_FLAG_SOLO",
+    "PGMG_FLAG_NO_RECOMPUTE", "PGMG_FLAG_NO_PIN", "PGMG_FLAG_NO_R2",
 ]
 
 
@@ -42,9 +45,37 @@ def build(jobs=8, verbose=False):
     return PKG_DIR / "libpgmg.so"
 
 
+# Config fields applied to every Solver created inside `with config_overrides(...)`
+# (flags are OR-ed in).  Tests use it to run the default plan's building blocks on small
+# grids (cross_min_n, spec_segment) or an alternative plan (PGMG_FLAG_NO_RECOMPUTE, ...)
+# through helpers that build their own Solvers.  Everything goes through pgmg_config.
+_overrides = {}
+
+
+@contextlib.contextmanager
+def config_overrides(**kw):
+    saved = dict(_overrides)
+    for k, v in kw.items():
+        if k == "flags":
+            _overrides["flags"] = _overrides.get("flags", 0) | int(v)
+        else:
+            _overrides[k] = v
+    try:
+        yield
+    finally:
+        _overrides.clear()
+        _overrides.update(saved)
+
+
 def default_config(N, **kw):
     cfg = PgmgConfig()
     check(load().pgmg_config_default(C.byref(cfg), int(N)), "pgmg_config_default")
+    kw = dict(kw)
+    for k, v in _overrides.items():
+        if k == "flags":
+            kw["flags"] = kw.get("flags", 0) | v
+        else:
+            kw.setdefault(k, v)
     for k, v in kw.items():
         if not hasattr(cfg, k):
             raise TypeError(f"unknown config field {k}")
@@ -77,6 +108,10 @@ class LoopbackHub:
         check(load().pgmg_loopback_create(int(world), C.byref(h)), "pgmg_loopback_create")
         self.h = h
         self.world = world
+
+    def fail(self, rank, at_group):
+        """Test hook: rank's at_group-th transport group from now on fails (0: never)."""
+        check(load().pgmg_loopback_fail(self.h, int(rank), int(at_group)), "pgmg_loopback_fail")
 
     def close(self):
         if self.h:
@@ -158,6 +193,14 @@ class Solver:
         out = np.empty((self.N, self.N), dtype=np.float64)
         check(self.lib.pgmg_get_solution(self.h, out.ctypes.data_as(C.c_void_p)),
               "pgmg_get_solution")
+        return out
+
+    def gather_solution(self, root, want):
+        """Collective: phi gathered to rank `root` only; returns it where `want`, else None
+        (row strips of a large grid without a full host copy per rank)."""
+        out = np.empty((self.N, self.N), dtype=np.float64) if want else None
+        ptr = out.ctypes.data_as(C.c_void_p) if want else None
+        check(self.lib.pgmg_gather_solution(self.h, int(root), ptr), "pgmg_gather_solution")
         return out
 
     def residual_norm(self):

@@ -30,6 +30,9 @@ PGMG_FLAG_NO_CROSS = 16
 PGMG_FLAG_STORED_RHS = 32
 PGMG_FLAG_EXACT_DIST = 64
 PGMG_FLAG_SOLO = 128
+PGMG_FLAG_NO_RECOMPUTE = 256
+PGMG_FLAG_NO_PIN = 512
+PGMG_FLAG_NO_R2 = 1024
 
 PGMG_PRECISION_FP64 = 0
 PGMG_PRECISION_FP32 = 1
@@ -55,6 +58,9 @@ class PgmgConfig(C.Structure):
         ("nccl_unique_id", C.c_void_p),
         ("gather_n", C.c_int),
         ("precision", C.c_int),
+        ("cross_min_n", C.c_int),
+        ("spec_segment", C.c_int),
+        ("comm_timeout_s", C.c_double),
     ]
 
 
@@ -71,6 +77,7 @@ SIGNATURES = [
     ("pgmg_fcycle", C.c_int, [_P, C.c_int]),
     ("pgmg_sync", C.c_int, [_P]),
     ("pgmg_get_solution", C.c_int, [_P, _P]),
+    ("pgmg_gather_solution", C.c_int, [_P, C.c_int, _P]),
     ("pgmg_residual_norm", C.c_int, [_P, _DP]),
     ("pgmg_stats", C.c_int, [_P, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]),
     ("pgmg_stats_detail", C.c_int, [_P, C.POINTER(C.c_longlong)]),
@@ -106,6 +113,7 @@ SIGNATURES = [
     ("pgmg_tail_prof", C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
     ("pgmg_loopback_create", C.c_int, [C.c_int, C.POINTER(_P)]),
     ("pgmg_loopback_destroy", C.c_int, [_P]),
+    ("pgmg_loopback_fail", C.c_int, [_P, C.c_int, C.c_longlong]),
     ("pgmg_plan_strips", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                    C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("pgmg_last_error", C.c_char_p, []),

@@ -26,10 +26,12 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -60,14 +62,47 @@ class Transport {
     virtual int group_end(hipStream_t s) = 0;
     virtual int allreduce_sum(double *d, int n, hipStream_t s) = 0;
     virtual int allreduce_min_u32(unsigned *d, int n, hipStream_t s) = 0;
+    virtual int wait(hipStream_t s)
+    {
+        PGMG_HIPC(hipStreamSynchronize(s));
+        return PGMG_OK;
+    }
 };
 
 class RcclTransport : public Transport {
   public:
     ncclComm_t comm = nullptr;
+    double timeout_s = 600.0;
     ~RcclTransport() override
     {
         if (comm) ncclCommDestroy(comm);
+    }
+    int abort_with(const std::string &why)
+    {
+        if (comm) ncclCommAbort(comm);
+        comm = nullptr;
+        return set_err(PGMG_ERR_COMM, why);
+    }
+    // Poll the stream instead of blocking in hipStreamSynchronize: a peer that died or
+    // stopped posting its sends would otherwise hang this rank forever.
+    int wait(hipStream_t s) override
+    {
+        if (!comm) return set_err(PGMG_ERR_COMM, "communicator aborted by an earlier error");
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int spin = 0;; ++spin) {
+            const hipError_t q = hipStreamQuery(s);
+            if (q == hipSuccess) return PGMG_OK;
+            if (q != hipErrorNotReady)
+                return abort_with(std::string("stream error while waiting: ") + hipGetErrorString(q));
+            ncclResult_t ae = ncclSuccess;
+            if (ncclCommGetAsyncError(comm, &ae) == ncclSuccess && ae != ncclSuccess &&
+                ae != ncclInProgress)
+                return abort_with(std::string("RCCL asynchronous error: ") + ncclGetErrorString(ae));
+            const double dt =
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            if (dt > timeout_s) return abort_with("RCCL wait timed out (pgmg_config.comm_timeout_s)");
+            if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
     }
     int init(const void *uid, int world, int rank)
     {
@@ -78,6 +113,7 @@ class RcclTransport : public Transport {
     }
     int group_start() override
     {
+        if (!comm) return set_err(PGMG_ERR_COMM, "communicator aborted by an earlier error");
         NCCLC(ncclGroupStart());
         return PGMG_OK;
     }
@@ -125,6 +161,10 @@ struct LoopbackHub {
     };
     std::map<std::tuple<int, int, long long>, Msg> box;
     std::map<std::pair<int, int>, long long> seq_send, seq_recv;
+    // test hook (pgmg_loopback_fail): group_end of rank r fails at its fail_at[r]-th call
+    // (1-based; 0 = never) with PGMG_ERR_COMM, before posting anything; every rank runs the
+    // same sequence of groups, so failing all ranks at the same count hangs none of them
+    long long groups[64] = {0}, fail_at[64] = {0};
     // allreduce rendezvous
     long long ar_round[64] = {0};
     std::map<long long, std::vector<double>> ar_vals;
@@ -162,6 +202,13 @@ class LoopbackTransport : public Transport {
     }
     int group_end(hipStream_t s) override
     {
+        {
+            std::lock_guard<std::mutex> g(hub->m);
+            if (++hub->groups[me] == hub->fail_at[me]) {
+                pend.clear();
+                return set_err(PGMG_ERR_COMM, "loopback: injected transport failure");
+            }
+        }
         std::vector<std::tuple<int, int, long long>> my_sends;
         // 1. post sends (data ready when the sender's stream reaches this point)
         for (auto &p : pend) {
@@ -342,26 +389,26 @@ class StripComm : public Comm {
     {
         int e = t->group_start();
         if (e) return e;
-        for (int k = 0; k < n; ++k) {
+        for (int k = 0; k < n && !e; ++k) {
             const Grid &g = *reqs[k].g;
             const Level &L = *reqs[k].L;
             const int depth = reqs[k].depth;
             const size_t row = (size_t)L.P * L.es;
             if (me > 0) {
-                if ((e = t->send(row_ptr(g, L.lo, L.P, L.es), depth * row, me - 1, s))) return e;
-                if ((e = t->recv(row_ptr(g, L.lo - depth, L.P, L.es), depth * row, me - 1, s)))
-                    return e;
+                e = t->send(row_ptr(g, L.lo, L.P, L.es), depth * row, me - 1, s);
+                if (!e) e = t->recv(row_ptr(g, L.lo - depth, L.P, L.es), depth * row, me - 1, s);
             }
-            if (me < world - 1) {
-                if ((e = t->send(row_ptr(g, L.hi - depth, L.P, L.es), depth * row, me + 1, s)))
-                    return e;
-                if ((e = t->recv(row_ptr(g, L.hi, L.P, L.es), depth * row, me + 1, s))) return e;
+            if (!e && me < world - 1) {
+                e = t->send(row_ptr(g, L.hi - depth, L.P, L.es), depth * row, me + 1, s);
+                if (!e) e = t->recv(row_ptr(g, L.hi, L.P, L.es), depth * row, me + 1, s);
             }
         }
-        return t->group_end(s);
+        const int e2 = t->group_end(s);   // the group is closed even after a failed call
+        return e ? e : e2;
     }
 
     int allreduce_sum(double *d, int n, hipStream_t s) override { return t->allreduce_sum(d, n, s); }
+    int wait(hipStream_t s) override { return t->wait(s); }
     int allreduce_min_u32(unsigned *d, int n, hipStream_t s) override
     {
         return t->allreduce_min_u32(d, n, s);
@@ -373,18 +420,18 @@ class StripComm : public Comm {
         const size_t row = (size_t)L.P * L.es;
         int e = t->group_start();
         if (e) return e;
-        for (int r = 0; r < world; ++r) {
+        for (int r = 0; r < world && !e; ++r) {
             const int a = std::max(strip_lo(r, l), 1), b = std::min(strip_hi(r, l, L.N), L.N - 1);
             if (b <= a) continue;
             if (r == me) {
                 for (int q = 0; q < world && !e; ++q)
                     if (q != me) e = t->send(row_ptr(g, a, L.P, L.es), (b - a) * row, q, c->s);
-                if (e) return e;
-            } else if ((e = t->recv(row_ptr(g, a, L.P, L.es), (b - a) * row, r, c->s))) {
-                return e;
+            } else {
+                e = t->recv(row_ptr(g, a, L.P, L.es), (b - a) * row, r, c->s);
             }
         }
-        return t->group_end(c->s);
+        const int e2 = t->group_end(c->s);   // the group is closed even after a failed call
+        return e ? e : e2;
     }
 
     int run_gathered(pgmg_ctx *c, int l, int gamma, int repeats) override
@@ -400,29 +447,35 @@ class StripComm : public Comm {
         return PGMG_OK;
     }
 
-    int gather_solution(pgmg_ctx *c, double *phi) override
+    int gather_solution(pgmg_ctx *c, double *phi, int root) override
     {
         Level &L = c->lv[0];
         const int N = L.N;
         const size_t row = (size_t)L.P * L.es;
+        const bool want = root < 0 || root == me;
         Grid full;
-        PGMG_HIPC(hipMalloc(&full.base, (size_t)N * row));
-        full.o = full.base;
-        PGMG_HIPC(hipMemcpyAsync(row_ptr(full, L.lo, L.P, L.es), row_ptr(L.A, L.lo, L.P, L.es),
-                                 (L.hi - L.lo) * row, hipMemcpyDeviceToDevice, c->s));
+        if (want) {
+            PGMG_HIPC(hipMalloc(&full.base, (size_t)N * row));
+            full.o = full.base;
+            PGMG_HIPC(hipMemcpyAsync(row_ptr(full, L.lo, L.P, L.es), row_ptr(L.A, L.lo, L.P, L.es),
+                                     (L.hi - L.lo) * row, hipMemcpyDeviceToDevice, c->s));
+        }
         int e = t->group_start();
         for (int r = 0; r < world && !e; ++r) {
             if (r == me) continue;
-            e = t->send(row_ptr(L.A, L.lo, L.P, L.es), (L.hi - L.lo) * row, r, c->s);
-            if (!e) {
+            if (root < 0 || root == r)
+                e = t->send(row_ptr(L.A, L.lo, L.P, L.es), (L.hi - L.lo) * row, r, c->s);
+            if (!e && want) {
                 const int a = strip_lo(r, 0), b = strip_hi(r, 0, N);
                 e = t->recv(row_ptr(full, a, L.P, L.es), (b - a) * row, r, c->s);
             }
         }
-        if (!e) e = t->group_end(c->s);
-        if (!e) e = download_grid(c, full.o, L.P, N, phi);
-        (void)hipStreamSynchronize(c->s);
-        (void)hipFree(full.base);
+        const int e2 = t->group_end(c->s);   // closed even after a failed send/recv
+        if (!e) e = e2;
+        if (!e && want) e = download_grid(c, full.o, L.P, N, phi);
+        if (!e) e = t->wait(c->s);
+        else (void)hipStreamSynchronize(c->s);
+        if (want) (void)hipFree(full.base);
         return e;
     }
 };
@@ -457,6 +510,7 @@ Comm *Comm::create(pgmg_ctx *c, int *rc)
         sc->t = new LoopbackTransport(hub, cfg.rank);
     } else {
         auto *rt = new RcclTransport();
+        if (cfg.comm_timeout_s > 0) rt->timeout_s = cfg.comm_timeout_s;
         sc->t = rt;
         *rc = rt->init(cfg.nccl_unique_id, cfg.world, cfg.rank);
         if (*rc) {
@@ -543,6 +597,15 @@ int pgmg_loopback_create(int world, void **hub)
     auto *h = new pgmg::LoopbackHub();
     h->world = world;
     *hub = h;
+    return PGMG_OK;
+}
+
+int pgmg_loopback_fail(void *hub, int rank, long long at_group)
+{
+    auto *h = (pgmg::LoopbackHub *)hub;
+    if (!h || rank < 0 || rank >= h->world) return pgmg::set_err(PGMG_ERR_ARG, "bad argument");
+    std::lock_guard<std::mutex> g(h->m);
+    h->fail_at[rank] = at_group > 0 ? h->groups[rank] + at_group : 0;
     return PGMG_OK;
 }
 

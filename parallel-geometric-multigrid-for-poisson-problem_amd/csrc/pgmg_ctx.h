@@ -80,7 +80,6 @@ struct pgmg_ctx {
     // finest-level kernel timing (PGMG_FLAG_TIME_FINE): 0 plain sweep, 1 k_pre, 2 k_post
     EventPool tpool[4];           // 3: k_postpre
     bool fused = false;           // v1 = v2 = 1: two fused passes per level
-    bool rare_fused = true;       // in-stream rare paths as fused one-sweep passes
     bool cross = false;           // finest level fuses post(k) with pre(k+1) across cycles
     bool recompute = true;        // levels entered with x0 = 0 recompute x2 in k_post
     pgmg::Grid S;                 // finest-level scratch for k_postpre's rare paths
@@ -126,6 +125,7 @@ struct pgmg_ctx {
     std::vector<size_t> fmg_goff;
     int gen_level = 0;
     const double *lgfx = nullptr, *lgsy = nullptr;
+    int fmg_f_swapped = -1;   // bulk level whose L.F is traded with Ffmg_l (climb), or -1
     std::vector<pgmg::Grid> Ffmg_l;   // the analytic RHS of bulk levels 1.. of the FMG climb
     bool fmg_rhs_ready = false;   // Ffmg holds the level-0 analytic RHS of the FMG h chain
     double *fmg_tab = nullptr;
@@ -172,7 +172,13 @@ class Comm {
     // grid g of gathered level l: every rank's rows (the ones its parent strip restricts
     // into) to every other rank, so every rank holds the full grid (one grouped exchange)
     virtual int allgather_rows(pgmg_ctx *c, int l, const Grid &g) = 0;
-    virtual int gather_solution(pgmg_ctx *c, double *phi_host) = 0;
+    // the strips of phi to every rank (root < 0) or to rank `root` only (others: phi_host
+    // may be null)
+    virtual int gather_solution(pgmg_ctx *c, double *phi_host, int root) = 0;
+    // hipStreamSynchronize that cannot hang on a dead or stuck peer: RCCL's asynchronous
+    // error state is polled while waiting, and after cfg.comm_timeout_s the communicator is
+    // aborted; PGMG_ERR_COMM then
+    virtual int wait(hipStream_t s) = 0;
     static Comm *create(pgmg_ctx *c, int *rc);
 };
 

@@ -31,6 +31,21 @@
 
 using namespace pgmg;
 
+// Wait for the context's stream.  On row strips through the transport's wait, which polls
+// RCCL's asynchronous error state and gives up after cfg.comm_timeout_s instead of hanging
+// on a dead or stuck peer.
+static int stream_wait(pgmg_ctx *c)
+{
+    if (c->comm) return c->comm->wait(c->s);
+    PGMG_HIPC(hipStreamSynchronize(c->s));
+    return PGMG_OK;
+}
+#define PGMG_TRY(expr)            \
+    do {                          \
+        const int e_ = (expr);    \
+        if (e_) return e_;        \
+    } while (0)
+
 static thread_local std::string g_err;
 
 int pgmg::set_err(int code, const std::string &msg)
@@ -307,8 +322,7 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     if ((e = timed_end(c, 1, ev))) return e;
     if (!lp) {
         if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
-        if (c->rare_fused) launch_pre_rare(fa, pa, x0_zero, c->s);
-        else launch_pre_fixup(fa, pa, x0_zero, c->s);
+        launch_pre_rare(fa, pa, x0_zero, c->s);
     }
     if ((e = enqueue_children<T>(c, l, gamma))) return e;
     // the correction of level l+1 is not exchanged: a distributed child's k_post computed
@@ -352,8 +366,7 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     if (!lp) {
         fa.global_sum = nullptr;
         if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
-        if (c->rare_fused) launch_post_rare(fa, po, c->s);
-        else launch_post_fixup(fa, po, c->s);
+        launch_post_rare(fa, po, c->s);
     }
     return PGMG_OK;
 }
@@ -682,6 +695,9 @@ int pgmg_config_default(pgmg_config *cfg, int N)
     cfg->nccl_unique_id = nullptr;
     cfg->gather_n = 1025;
     cfg->precision = PGMG_PRECISION_FP64;
+    cfg->cross_min_n = 2049;
+    cfg->spec_segment = 0;
+    cfg->comm_timeout_s = 600.0;
     return PGMG_OK;
 }
 
@@ -803,17 +819,9 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         if (rc == PGMG_OK && l < c->nb) rc = alloc_grid(L.B, L);
     }
     c->fused = cfg->v1 == 1 && cfg->v2 == 1 && !(cfg->flags & PGMG_FLAG_UNFUSED);
-    {   // in-stream rare paths as fused one-sweep passes (PGMG_RARE_FUSED=0: scalar fix-ups)
-        const char *ev = getenv("PGMG_RARE_FUSED");
-        c->rare_fused = !(ev && *ev == '0');
-    }
+    c->recompute = !(cfg->flags & PGMG_FLAG_NO_RECOMPUTE);
     {
-        const char *ev = getenv("PGMG_RECOMPUTE");
-        c->recompute = !(ev && *ev == '0');
-    }
-    {
-        const char *ev = getenv("PGMG_CROSS_MIN_N");
-        const int cross_min = (ev && *ev) ? atoi(ev) : 2049;
+        const int cross_min = cfg->cross_min_n > 0 ? cfg->cross_min_n : 2049;
         c->cross = c->fused && c->nb >= 1 && c->lv[0].N >= cross_min &&
                    !(cfg->flags & PGMG_FLAG_NO_CROSS);
     }
@@ -863,11 +871,7 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         }
     }
     if (rc == PGMG_OK && c->comm) rc = c->comm->setup(c);
-    {
-        const char *ev = getenv("PGMG_SPEC");
-        c->spec = c->fused && (c->cross || c->comm != nullptr) &&
-                  !(cfg->flags & PGMG_FLAG_EXACT_DIST) && !(ev && *ev == '0');
-    }
+    c->spec = c->fused && (c->cross || c->comm != nullptr) && !(cfg->flags & PGMG_FLAG_EXACT_DIST);
     if (rc != PGMG_OK) {
         pgmg_destroy(c);
         return rc;
@@ -909,7 +913,7 @@ static int upload_rows(pgmg_ctx *c, const Level &L, const Grid &g, const double 
     HIPC(hipMemcpy(d, host + (size_t)r0 * N, rows * N * sizeof(double), hipMemcpyHostToDevice));
     launch_from_double(d - (size_t)r0 * N, N, G<float>(g), L.P, r0, r1, c->s);
     HIPC(hipGetLastError());
-    HIPC(hipStreamSynchronize(c->s));
+    PGMG_TRY(stream_wait(c));
     HIPC(hipFree(d));
     return PGMG_OK;
 }
@@ -919,7 +923,7 @@ int pgmg::download_grid(pgmg_ctx *c, const void *o, int P, int N, double *host)
     if (!c->fp32) {
         HIPC(hipMemcpy2DAsync(host, N * sizeof(double), o, P * sizeof(double), N * sizeof(double),
                               N, hipMemcpyDeviceToHost, c->s));
-        HIPC(hipStreamSynchronize(c->s));
+        PGMG_TRY(stream_wait(c));
         return PGMG_OK;
     }
     double *d = nullptr;
@@ -927,7 +931,7 @@ int pgmg::download_grid(pgmg_ctx *c, const void *o, int P, int N, double *host)
     launch_to_double(static_cast<const float *>(o), P, d, N, 0, N, c->s);
     HIPC(hipGetLastError());
     HIPC(hipMemcpyAsync(host, d, (size_t)N * N * sizeof(double), hipMemcpyDeviceToHost, c->s));
-    HIPC(hipStreamSynchronize(c->s));
+    PGMG_TRY(stream_wait(c));
     HIPC(hipFree(d));
     return PGMG_OK;
 }
@@ -946,7 +950,7 @@ int pgmg_set_problem(pgmg_ctx *c, const double *phi0, const double *f)
     const size_t rows = (size_t)(r1 - r0);
     const size_t pitch = (size_t)L.P * L.es, width = (size_t)N * L.es;
     int e;
-    HIPC(hipStreamSynchronize(c->s));
+    PGMG_TRY(stream_wait(c));
     // phi (and its boundary copy in the ping-pong buffer B)
     if (phi0) {
         if ((e = upload_rows(c, L, L.A, phi0, r0, r1))) return e;
@@ -976,7 +980,7 @@ int pgmg_set_problem(pgmg_ctx *c, const double *phi0, const double *f)
         if (c->fp32) launch_rhs(G<float>(L.F), d, d + N, factor, N, L.P, r0, r1, c->s);
         else launch_rhs(G<double>(L.F), d, d + N, factor, N, L.P, r0, r1, c->s);
         HIPC(hipGetLastError());
-        HIPC(hipStreamSynchronize(c->s));
+        PGMG_TRY(stream_wait(c));
         HIPC(hipFree(d));
         // tables for regenerating f inside the level-0 passes: fx[i] = factor * sx[i]
         // (the first product of k_rhs's factor * sx[i] * sy[j]) and sy[j], zero-padded
@@ -1088,7 +1092,7 @@ static void spec_need_level(pgmg_ctx *c, int l, int gamma, long long *dbl, long 
 static int spec_reserve(pgmg_ctx *c, long long dbl, long long nchk)
 {
     if (dbl > c->plog_cap || nchk > c->chk_cap) {
-        HIPC(hipStreamSynchronize(c->s));
+        PGMG_TRY(stream_wait(c));
         if (dbl > c->plog_cap) {
             if (c->plog) HIPC(hipFree(c->plog));
             c->plog = nullptr;
@@ -1140,7 +1144,7 @@ static int spec_mark_levels(pgmg_ctx *c, int cycles)
             if (prev > 0.0) rho = std::min(rho, std::max(1e-3, last / prev));
         }
         if (!(last * std::pow(rho, (double)cycles) >= lim)) keep[l] = 0u;
-        if (getenv("PGMG_SPEC_TRACE"))
+        if (tuning_int("PGMG_SPEC_TRACE", 0))
             fprintf(stderr, "spec level %d N=%d norms[-4..] %.3e %.3e %.3e %.3e rho %.3f next %d -> %s\n",
                     l, c->lv[l].N, m >= 4 ? h[m - 4] : -1.0, m >= 3 ? h[m - 3] : -1.0, h[m - 2],
                     h[m - 1], rho, cycles, keep[l] ? "speculate" : "in-stream");
@@ -1152,7 +1156,7 @@ static int spec_mark_levels(pgmg_ctx *c, int cycles)
         if (e) return e;
         HIPC(hipMemcpyAsync(keep.data(), c->mark_dev, (c->nb + 1) * sizeof(unsigned),
                             hipMemcpyDeviceToHost, c->s));
-        HIPC(hipStreamSynchronize(c->s));
+        PGMG_TRY(stream_wait(c));
     }
     for (int l = 1; l < c->nb; ++l)
         if (!keep[l]) c->lvl_exact[l] = 1;
@@ -1178,10 +1182,7 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
     const long long per_dbl = 2LL * std::max(np0, npp) + d1, per_chk = 2 + k1;
     // segments of at most 2^27 logged doubles (1 GiB) / 2^22 checks
     long long seg_max = std::min(((1LL << 27) - 2LL * np0) / per_dbl, ((1LL << 22) - 2) / per_chk);
-    {
-        const char *ev = getenv("PGMG_SPEC_SEG");   // tests: cycles per validated segment
-        if (ev && *ev && atoi(ev) > 0) seg_max = std::min<long long>(seg_max, atoi(ev));
-    }
+    if (c->cfg.spec_segment > 0) seg_max = std::min<long long>(seg_max, c->cfg.spec_segment);
     if (seg_max < 1) return run_cycles_plain(c, ncycles, gamma);
     // the cross-fused cycles keep A intact (rotation through S); otherwise copy it
     const bool rotate = c->cross && c->S.base != nullptr;
@@ -1227,7 +1228,7 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
             HIPC(hipMemcpyAsync(c->hflag.data(), c->uflags, n * sizeof(unsigned),
                                 hipMemcpyDeviceToHost, c->s));
         }
-        HIPC(hipStreamSynchronize(c->s));
+        PGMG_TRY(stream_wait(c));
         if (h) {
             // some check could fire: roll back this segment, rerun the rest of the call with
             // in-stream decisions; the levels whose checks could fire stay in-stream
@@ -1403,10 +1404,7 @@ static int enqueue_fcycle(pgmg_ctx *c)
         sine_tables(c->cfg, 1, 1.0, sx, sy, factor);
     }
     int e;
-    static const bool use_r2 = [] {   // two restriction steps per pass (PGMG_R2=0: one)
-        const char *v = getenv("PGMG_R2");
-        return !(v && *v == '0');
-    }();
+    const bool use_r2 = !(c->cfg.flags & PGMG_FLAG_NO_R2);   // two restriction steps per pass
     for (int l = 0; l < nb; ++l) {
         Level &L = c->lv[l], &C = c->lv[l + 1];
         if (!is_dist(c, l)) {
@@ -1464,16 +1462,16 @@ static int enqueue_fcycle(pgmg_ctx *c)
         // once into its own grid (Ffmg for level 0, Ffmg_l[l] below), which stands in for
         // L.F while this level runs (the V-cycle's restriction writes the coarser level's
         // own F, not its cached RHS)
-        if (l > 0) std::swap(L.F, c->Ffmg_l[l]);
+        if (l > 0) {
+            std::swap(L.F, c->Ffmg_l[l]);
+            c->fmg_f_swapped = l;
+        }
         if (!c->fmg_rhs_ready)
             launch_rhs(G<T>(L.F), sx, sx + L.N, factor, L.N, L.P, r0, r1, c->s);
         // this level's passes regenerate its analytic f (bitwise the stored one); its
         // rare paths and the coarser levels read theirs from memory
-        static const bool gen_l = [] {
-            const char *v = getenv("PGMG_GEN_LEVELS");
-            return !(v && *v == '0');
-        }();
-        if (l > 0 && gen_l && c->rgfx != nullptr) {
+        // (PGMG_FLAG_STORED_RHS: rgfx is null, every level streams its RHS)
+        if (l > 0 && c->rgfx != nullptr) {
             c->gen_level = l;
             c->lgfx = c->fmg_gtab + c->fmg_goff[l] + 8;
             c->lgsy = c->fmg_gtab + c->fmg_goff[l] + (8 + L.N + 1024) + 8;
@@ -1484,10 +1482,7 @@ static int enqueue_fcycle(pgmg_ctx *c)
         launch_zero_frame(G<T>(L.A), L.P, L.N, c->s, r0, r1);
         launch_zero_frame(G<T>(L.B), L.P, L.N, c->s, r0, r1);
         if (l == 0 && c->S.base) launch_zero_frame(G<T>(c->S), L.P, L.N, c->s, r0, r1);   // S mirrors too
-        static const bool use_pin = [] {
-            const char *v = getenv("PGMG_PIN");
-            return !(v && *v == '0');
-        }();
+        const bool use_pin = !(c->cfg.flags & PGMG_FLAG_NO_PIN);
         if (c->fused && use_pin) {
             // the V-cycle's k_pre computes the prolongation on the fly (PIN): no separate
             // pass writing the zeroed fine grid; it reads 3 coarse rows past the strip
@@ -1497,6 +1492,7 @@ static int enqueue_fcycle(pgmg_ctx *c)
             c->gen_level = 0;
             c->lgfx = c->lgsy = nullptr;
             if (l > 0) std::swap(L.F, c->Ffmg_l[l]);
+            c->fmg_f_swapped = -1;
             continue;
         }
         // the prolongation of the rank's rows reads one coarse row past its strip
@@ -1514,10 +1510,13 @@ static int enqueue_fcycle(pgmg_ctx *c)
         if (p.row1 > p.row0) launch_prolong(p, c->s);
         e = enqueue_cycle_t<T>(c, l, 1, false);
         if (e) return e;
-        c->gen_level = 0;   // the unfused climb streams f
+        // the V-cycle above regenerated this level's f where its passes are fused; the
+        // general smooth(3) below streams the cached RHS
+        c->gen_level = 0;
         c->lgfx = c->lgsy = nullptr;
         if (l > 0 && (e = enqueue_smooth<T>(c, l, 0, 3, false))) return e;
         if (l > 0) std::swap(L.F, c->Ffmg_l[l]);
+        c->fmg_f_swapped = -1;
     }
     return PGMG_OK;
 }
@@ -1539,8 +1538,33 @@ int pgmg_fcycle(pgmg_ctx *c, int ncycles)
             if ((e = alloc_grid(c->Ffmg_l[l], c->lv[l]))) return e;
     }
     // the F-cycle's levels use the FMG h chain and (level 0) the analytic RHS of that chain
-    // (every level including the tail's top, whose h enqueue_tail passes on)
-    std::vector<Level> saved(c->lv);
+    // (every level including the tail's top, whose h enqueue_tail passes on).  Everything
+    // the F-cycle changes on the context is undone by the guard on EVERY exit path (an
+    // error half-way through the climb included), so later V/W-cycles see the user's f,
+    // h and no regenerated-RHS level.
+    struct Restore {
+        pgmg_ctx *c;
+        std::vector<Level> saved;
+        const double *sgx, *sgy;
+        bool f0_swapped = false;
+        ~Restore()
+        {
+            if (c->fmg_f_swapped > 0) {
+                std::swap(c->lv[c->fmg_f_swapped].F, c->Ffmg_l[c->fmg_f_swapped]);
+                c->fmg_f_swapped = -1;
+            }
+            if (f0_swapped) std::swap(c->lv[0].F, c->Ffmg);
+            c->gen_level = 0;
+            c->lgfx = c->lgsy = nullptr;
+            c->rgfx = sgx;
+            c->rgsy = sgy;
+            for (int l = 0; l <= c->nb; ++l) {
+                c->lv[l].h = saved[l].h;
+                c->lv[l].hh = saved[l].hh;
+                c->lv[l].ih = saved[l].ih;
+            }
+        }
+    } guard{c, c->lv, c->rgfx, c->rgsy};
     for (int l = 0; l <= c->nb; ++l) {
         Level &L = c->lv[l];
         const double h = fmg_h(c->cfg, L.N);
@@ -1548,30 +1572,24 @@ int pgmg_fcycle(pgmg_ctx *c, int ncycles)
         L.hh = h * h;
         L.ih = 1.0 / (h * h);
     }
-    if (c->nb > 0) std::swap(L0.F, c->Ffmg);
-    const double *sgx = c->rgfx, *sgy = c->rgsy;
+    if (c->nb > 0) {
+        std::swap(L0.F, c->Ffmg);
+        guard.f0_swapped = true;
+    }
     const bool gen = c->nb > 0 && !(c->cfg.flags & PGMG_FLAG_STORED_RHS);
     c->rgfx = gen ? c->fmg_gtab + 8 : nullptr;
     c->rgsy = gen ? c->fmg_gtab + (8 + L0.N + 1024) + 8 : nullptr;
     HIPC(hipEventRecord(c->ev0, c->s));
     for (int k = 0; k < ncycles && !e; ++k) {
         e = c->fp32 ? enqueue_fcycle<float>(c) : enqueue_fcycle<double>(c);
-        c->fmg_rhs_ready = true;
+        if (!e) c->fmg_rhs_ready = true;
     }
-    if (c->nb > 0) std::swap(L0.F, c->Ffmg);
     if (c->fsmooth_swapped && c->gexec) {   // its level buffers traded places: recapture
-        HIPC(hipStreamSynchronize(c->s));
+        PGMG_TRY(stream_wait(c));
         HIPC(hipGraphExecDestroy(c->gexec));
         c->gexec = nullptr;
     }
     c->fsmooth_swapped = false;
-    c->rgfx = sgx;
-    c->rgsy = sgy;
-    for (int l = 0; l <= c->nb; ++l) {
-        c->lv[l].h = saved[l].h;
-        c->lv[l].hh = saved[l].hh;
-        c->lv[l].ih = saved[l].ih;
-    }
     if (e) return e;
     HIPC(hipGetLastError());
     HIPC(hipEventRecord(c->ev1, c->s));
@@ -1581,7 +1599,7 @@ int pgmg_fcycle(pgmg_ctx *c, int ncycles)
 int pgmg_sync(pgmg_ctx *c)
 {
     if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
-    HIPC(hipStreamSynchronize(c->s));
+    PGMG_TRY(stream_wait(c));
     return PGMG_OK;
 }
 
@@ -1597,9 +1615,20 @@ int pgmg_last_elapsed_ms(pgmg_ctx *c, double *ms)
 
 int pgmg_get_solution(pgmg_ctx *c, double *phi)
 {
-    if (!c || !phi) return set_err(PGMG_ERR_ARG, "null argument");
-    HIPC(hipStreamSynchronize(c->s));
-    if (c->comm) return c->comm->gather_solution(c, phi);
+    return pgmg_gather_solution(c, -1, phi);
+}
+
+int pgmg_gather_solution(pgmg_ctx *c, int root, double *phi)
+{
+    if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
+    const int me = c->comm ? c->comm->rank() : 0;
+    if (!phi && (root < 0 || root == me)) return set_err(PGMG_ERR_ARG, "null phi on a receiving rank");
+    if (c->comm) {
+        int e = c->comm->wait(c->s);
+        if (e) return e;
+        return c->comm->gather_solution(c, phi, root);
+    }
+    PGMG_TRY(stream_wait(c));
     Level &L = c->lv[0];
     return download_grid(c, L.A.o, L.P, L.N, phi);
 }
@@ -1626,7 +1655,7 @@ int pgmg_residual_norm(pgmg_ctx *c, double *out)
     }
     double s = 0.0;
     HIPC(hipMemcpyAsync(&s, c->scalar, sizeof(double), hipMemcpyDeviceToHost, c->s));
-    HIPC(hipStreamSynchronize(c->s));
+    PGMG_TRY(stream_wait(c));
     *out = std::sqrt(s);
     return PGMG_OK;
 }
@@ -1635,7 +1664,7 @@ int pgmg_stats(pgmg_ctx *c, long long *sweeps, long long *exits)
 {
     if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
     unsigned long long h[4];
-    HIPC(hipStreamSynchronize(c->s));
+    PGMG_TRY(stream_wait(c));
     HIPC(hipMemcpy(h, c->stats, sizeof(h), hipMemcpyDeviceToHost));
     if (sweeps) *sweeps = (long long)h[0];
     if (exits) *exits = (long long)h[1];
@@ -1646,7 +1675,7 @@ int pgmg_stats_detail(pgmg_ctx *c, long long *out4)
 {
     if (!c || !out4) return set_err(PGMG_ERR_ARG, "null argument");
     unsigned long long h[4];
-    HIPC(hipStreamSynchronize(c->s));
+    PGMG_TRY(stream_wait(c));
     HIPC(hipMemcpy(h, c->stats, sizeof(h), hipMemcpyDeviceToHost));
     for (int i = 0; i < 4; ++i) out4[i] = (long long)h[i];
     out4[2] = c->cross ? out4[2] : -1;
@@ -1782,7 +1811,7 @@ int pgmg_bench_sweep(pgmg_ctx *c, int reps, double *ms)
 int pgmg_fine_pass_time(pgmg_ctx *c, int pass, int *count, double *mean_ms)
 {
     if (!c || pass < 0 || pass > 3) return set_err(PGMG_ERR_ARG, "bad argument");
-    HIPC(hipStreamSynchronize(c->s));
+    PGMG_TRY(stream_wait(c));
     auto &pool = c->tpool[pass];
     double tot = 0.0;
     const int n = pool.used / 2;

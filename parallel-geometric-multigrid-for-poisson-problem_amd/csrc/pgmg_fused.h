@@ -84,7 +84,6 @@ struct PostPreArgsT {
     int row_lo, row_hi;
     int rc_lo, rc_hi;
     int rows_per_block;
-    int band_stride;            // > 0: dispatch bands in a strided order (see k_postpre_lds)
 };
 
 struct FixArgsF {

@@ -582,9 +582,6 @@ __global__ __launch_bounds__(256) void k_post_rare(PostArgsT<T> a, FixArgsF f)
 // line-aligned stores: slower, 1.133 ms)
 constexpr int kPPStride = 116, kPPMargin = 6;
 
-// MODE 0: the real pass.  MODE 1 (PGMG_PP_VARIANT=1, measurement only): the same loads
-// and stores with the stencil arithmetic replaced by one add, to separate the memory
-// ceiling of this access pattern from the instruction cost.
 // Horizontal neighbours of a row's column pair (left of c, right of c+1), shared by the
 // stages that use the same centre row (a Jacobi sweep and a residual of the same iterate).
 template <class T> struct Nbr {
@@ -594,11 +591,10 @@ template <class T> __device__ __forceinline__ Nbr<T> nbr(V2<T> ce)
 {
     return Nbr<T>{dpp_shr(ce.y), dpp_shl(ce.x)};
 }
-template <int MODE, class T, bool EDGE>
+template <class T, bool EDGE>
 __device__ __forceinline__ V2<T> jsn(V2<T> up, V2<T> ce, V2<T> dn, Nbr<T> n, V2<T> f, T hh,
                                        const Cols &k, bool brow)
 {
-    if (MODE == 1) return mk2<T>(ce.x + f.x, ce.y + up.y + dn.y);
     V2<T> o;
     o.x = T(0.25) * ((hh * f.x) + n.l + ce.y + up.x + dn.x);
     o.y = T(0.25) * ((hh * f.y) + ce.x + n.r + up.y + dn.y);
@@ -608,170 +604,13 @@ __device__ __forceinline__ V2<T> jsn(V2<T> up, V2<T> ce, V2<T> dn, Nbr<T> n, V2<
     }
     return o;
 }
-template <int MODE, class T>
+template <class T>
 __device__ __forceinline__ V2<T> rsn(V2<T> up, V2<T> ce, V2<T> dn, Nbr<T> n, V2<T> f, T ih)
 {
-    if (MODE == 1) return mk2<T>(f.x + ce.x, f.y);
     V2<T> o;
     o.x = f.x - ih * (T(4) * ce.x - n.l - ce.y - up.x - dn.x);
     o.y = f.y - ih * (T(4) * ce.y - ce.x - n.r - up.y - dn.y);
     return o;
-}
-
-template <int MODE, class T, bool EDGE = true>
-__device__ __forceinline__ V2<T> js(V2<T> up, V2<T> ce, V2<T> dn, V2<T> f, T hh,
-                                      const Cols &k, bool brow)
-{
-    if (MODE == 1) return mk2<T>(ce.x + f.x, ce.y + up.y + dn.y);
-    return jstage<T, EDGE>(up, ce, dn, f, hh, k, brow);
-}
-template <int MODE, class T>
-__device__ __forceinline__ V2<T> rs(V2<T> up, V2<T> ce, V2<T> dn, V2<T> f, T ih)
-{
-    if (MODE == 1) return mk2<T>(f.x + ce.x, f.y);
-    return rstage(up, ce, dn, f, ih);
-}
-
-template <class T, int PAIRS, int MODE, int STRIDE = kPPStride, int MARGIN = kPPMargin>
-__device__ __forceinline__ void postpre_body(const PostPreArgsT<T> &a)
-{
-    constexpr int R = 2 * PAIRS;
-    __shared__ double red[4];
-    const Cols k = lane_cols_t<STRIDE, MARGIN>(a.N);
-    const int N = a.N, Nc = a.Nc;
-    const long long P = a.P, Pc = a.Pc;
-    const int jcb = a.jc0 + blockIdx.y * a.rows_per_block;
-    const int jce = min(jcb + a.rows_per_block, a.jc1);
-    const int olo = max(2 * jcb, a.row_lo), ohi = min(2 * jce, a.row_hi);
-    const int clo = max(jcb, max(1, a.rc_lo)), chi = min(jce, min(N / 2, a.rc_hi));
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
-        atomicAdd(&a.stats[0], 4ull);
-    ProlongCols pc;
-    pc.ic = (k.c - 1) >> 1;
-    pc.vx = k.c >= 3 && k.c <= N - 2;
-    pc.vy = k.c + 1 >= 2 && k.c + 1 <= N - 3;
-    const T *__restrict__ X = a.phi + k.c;
-    const T *__restrict__ F = a.f + k.c;
-    const T *__restrict__ E = a.ec + pc.ic;
-    T *__restrict__ O = a.x4 + k.c;
-    const T hh = a.hh, ih = a.ih;
-    const V2<T> z = zero2<T>();
-    // windows (two previous rows each) and f rows i-5 .. i-1
-    V2<T> e0 = z, e1 = z, b0 = z, b1 = z, c0 = z, c1 = z, g0 = z, g1 = z, h0 = z, h1 = z,
-            d0 = z, d1 = z;
-    V2<T> f1 = z, f2 = z, f3 = z, f4 = z, f5 = z;  // f[i-1], f[i-2], ..., f[i-5]
-    double acc1 = 0.0, acc2 = 0.0;
-    const int i_begin = 2 * jcb - 6;
-    const bool idle = (k.c - 2 * (threadIdx.x & 63) + MARGIN) > N - 2;  // spare wave
-    const int i_end = idle ? i_begin
-                           : i_begin + ((2 * (jce - jcb) + 11 + R - 1) / R) * R;
-    V2<T> np_[R], nf[R];
-    T ncr[PAIRS + 1];
-    #pragma unroll
-    for (int q = 0; q < R; ++q) {
-        np_[q] = idle ? z : ldv(X + (i_begin + q) * P);
-        nf[q] = idle ? z : ldv(F + (i_begin + q) * P);
-    }
-    #pragma unroll
-    for (int q = 0; q <= PAIRS; ++q) ncr[q] = idle ? T(0) : E[(long long)((i_begin >> 1) + q) * Pc];
-    for (int i = i_begin; i < i_end; i += R) {
-        V2<T> cp[R], cf[R];
-        T cr[PAIRS + 1];
-        #pragma unroll
-        for (int q = 0; q < R; ++q) {
-            cp[q] = np_[q];
-            cf[q] = nf[q];
-        }
-        #pragma unroll
-        for (int q = 0; q <= PAIRS; ++q) cr[q] = ncr[q];
-        if (i + R < i_end) {
-            #pragma unroll
-            for (int q = 0; q < R; ++q) {
-                np_[q] = ldv(X + (i + R + q) * P);
-                nf[q] = ldv(F + (i + R + q) * P);
-            }
-            #pragma unroll
-            for (int q = 0; q <= PAIRS; ++q) ncr[q] = E[(long long)(((i + R) >> 1) + q) * Pc];
-        }
-        T crn[PAIRS + 1];
-        #pragma unroll
-        for (int q = 0; q <= PAIRS; ++q) crn[q] = dpp_shl(cr[q]);
-        #pragma unroll
-        for (int s = 0; s < R; ++s) {
-            const int ii = i + s;
-            const int pq = s >> 1;
-            const V2<T> e2 = add_prolong(cp[s], ii, cr[pq], crn[pq], cr[pq + 1], crn[pq + 1], pc, Nc);
-            const V2<T> f0 = cf[s];  // f[ii]
-            // post-smooth sweep 1: x1 row ii-1
-            const V2<T> b2 = js<MODE, T>(e0, e1, e2, f1, hh, k, boundary_row(ii - 1, N));
-            {   // post check: r(x1) on row ii-2
-                const V2<T> r1 = rs<MODE, T>(b0, b1, b2, f2, ih);
-                const int row = ii - 2;
-                if (row >= olo && row < ohi && k.own) {
-                    acc1 = sqacc(acc1, r1.x);
-                    if (!k.by) acc1 = sqacc(acc1, r1.y);
-                }
-            }
-            // post-smooth sweep 2: x2 row ii-2 (= phi of cycle k+1)
-            const V2<T> c2 = js<MODE, T>(b0, b1, b2, f2, hh, k, boundary_row(ii - 2, N));
-            // pre-smooth sweep 1: x3 row ii-3
-            const V2<T> g2 = js<MODE, T>(c0, c1, c2, f3, hh, k, boundary_row(ii - 3, N));
-            {   // pre check: r(x3) on row ii-4
-                const V2<T> r3 = rs<MODE, T>(g0, g1, g2, f4, ih);
-                const int row = ii - 4;
-                if (row >= olo && row < ohi && k.own) {
-                    acc2 = sqacc(acc2, r3.x);
-                    if (!k.by) acc2 = sqacc(acc2, r3.y);
-                }
-            }
-            // pre-smooth sweep 2: x4 row ii-4 (stored)
-            const V2<T> h2 = js<MODE, T>(g0, g1, g2, f4, hh, k, boundary_row(ii - 4, N));
-            if (ii - 4 >= olo && ii - 4 < ohi && k.own) stv(O + (ii - 4) * P, h2);
-            // r(x4) on row ii-5
-            const V2<T> d2 = rs<MODE, T>(h0, h1, h2, f5, ih);
-            // restriction: rows ii-7, ii-6, ii-5 = 2jc-1, 2jc, 2jc+1 when ii is even
-            if ((s & 1) == 0) {
-                const int jc = (ii - 6) >> 1;
-                const T m2 = dpp_shl(d1.x);
-                const T u2 = dpp_shl(d0.x);
-                const T w2 = dpp_shl(d2.x);
-                const int ic = (k.c + 1) >> 1;
-                if (jc >= clo && jc < chi && k.own && ic <= Nc - 2) {
-                    const T v = T(0.25) * d1.y + T(0.125) * (m2 + d1.x + d2.y + d0.y) +
-                                     T(0.0625) * (d0.x + u2 + d2.x + w2);
-                    a.rc[(long long)jc * Pc + ic] = v;
-                }
-            }
-            e0 = e1; e1 = e2;
-            b0 = b1; b1 = b2;
-            c0 = c1; c1 = c2;
-            g0 = g1; g1 = g2;
-            h0 = h1; h1 = h2;
-            d0 = d1; d1 = d2;
-            f5 = f4; f4 = f3; f3 = f2; f2 = f1; f1 = f0;
-        }
-    }
-    const int slot = blockIdx.y * gridDim.x + blockIdx.x;
-    const double s1 = fused_block_sum(acc1, red);
-    __syncthreads();
-    const double s2 = fused_block_sum(acc2, red);
-    if (threadIdx.x == 0) {
-        a.partials1[slot] = s1;
-        a.partials2[slot] = s2;
-    }
-}
-
-template <class T, int PAIRS, int MODE, int STRIDE = kPPStride, int MARGIN = kPPMargin>
-__global__ __launch_bounds__(256) void k_postpre(PostPreArgsT<T> a)
-{
-    postpre_body<T, PAIRS, MODE, STRIDE, MARGIN>(a);
-}
-
-// PGMG_PP_VARIANT=2: at most 128 VGPRs (4 waves per SIMD)
-template <class T, int PAIRS>
-__global__ __launch_bounds__(256, 4) void k_postpre_o4(PostPreArgsT<T> a)
-{
-    postpre_body<T, PAIRS, 0>(a);
 }
 
 // ---------------------------------------------------------------------------
@@ -800,30 +639,18 @@ constexpr int kPPLdsCoarse = kPPWaves * (kPPStride / 2) + kPPMargin + 8;     // 
 // (per lane, in registers) and sy[j] = sin(q pi y_j / a) (per row, a scalar load) — the
 // same IEEE operations as k_rhs, so the values are identical to the stored f.  One
 // multiply per point replaces 8 bytes per point of the pass (28 -> 20 B/pt).
-// D: row pairs of loads in flight per lane (register sets); OCC: waves per SIMD the
-// register allocation must allow (1 = compiler's choice).
-// MODE 1 (measurement only): stencil arithmetic replaced by one add (js/rs), to separate
-// the memory/LDS cost of the pass from its VALU cost.
-// Logical block of a 2D grid (x fastest).  XCD-aware variant: the dispatcher deals
-// workgroups round-robin over the 8 XCDs (linear id i -> XCD i % 8); remap so XCD x runs a
-// contiguous range of logical blocks (neighbouring column blocks of one band share an L2).
+// OPT (compile-time, result-identical): 2 non-temporal x4 stores, 4 non-temporal rc
+// stores, 64 the F-cycle's smooth(3) (no correction, no restriction).
+// Logical block of the 2D grid (x: column block, y: band).
 struct Blk {
     int x, y;
 };
-__device__ __forceinline__ Blk xcd_block()
-{
-    const int T = gridDim.x * gridDim.y;
-    const int i = blockIdx.y * gridDim.x + blockIdx.x;
-    const int q = T >> 3, r = T & 7, x = i & 7, pos = i >> 3;
-    const int l = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + pos;
-    return Blk{l % (int)gridDim.x, l / (int)gridDim.x};
-}
 
 constexpr int kPPR = 2;   // rows per LDS slot (a row pair)
 
 // The body of k_postpre_lds for one block.  EDGE = false: no row of the block's band and
 // no column of this wave is a boundary, so the Jacobi stages carry no passthrough selects.
-template <class T, bool R2, bool GENF, int D, int MODE, bool EDGE, bool FRECOMP, int OPT>
+template <class T, bool R2, bool GENF, bool EDGE, int OPT>
 __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const Cols &k,
                                                 double *red, T (&sx)[2][kPPR][kPPLdsRow],
                                                 T (&sf)[2][kPPR][GENF ? 1 : kPPLdsRow],
@@ -880,9 +707,10 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
         sx[sl][q][j] = T(0);
         if constexpr (!GENF) sf[sl][q][j] = T(0);
     }
-    // D register sets: pair p's loads go to set p % D, issued D pairs ahead
-    V2<T> pxA[R], pfA[R], pxB[R], pfB[R], pxC[R], pfC[R];
-    T peA = T(0), peB = T(0), peC = T(0);
+    // two register sets: pair p's loads go to set p % 2, issued two pairs ahead
+    constexpr int D = 2;
+    V2<T> pxA[R], pfA[R], pxB[R], pfB[R];
+    T peA = T(0), peB = T(0);
     auto load_pair = [&](int p, V2<T> (&px)[R], V2<T> (&pf)[R], T &pe) {
         #pragma unroll
         for (int q = 0; q < R; ++q) {
@@ -906,12 +734,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     if (t < ncc) se[ring(m0)][t] = cldr ? GE[(long long)m0 * Pc] : T(0);
     store_pair(0, pxA, pfA, peA);
     if (ng > 1) load_pair(1, pxB, pfB, peB);
-    if constexpr (D == 2) {
-        if (ng > 2) load_pair(2, pxA, pfA, peA);
-    } else {
-        if (ng > 2) load_pair(2, pxC, pfC, peC);
-        if (ng > 3) load_pair(3, pxA, pfA, peA);
-    }
+    if (ng > 2) load_pair(2, pxA, pfA, peA);
     __syncthreads();
 
     // pair gi: compute from slot gi & 1; pair gi+1 (set (gi+1) & 1) -> the other slot;
@@ -927,33 +750,22 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
         for (int s = 0; s < R; ++s) {
             const int ii = i + s;
             const V2<T> xr = ldv(&sx[slot][s][xo]);
-            // f[ii]; GENF: f of the row each stage needs is regenerated where it is used
-            // (one multiply per value; no window of f rows is carried across rows)
-            // f[ii]: from LDS, or (GENF) generated once here and carried in the f window.
-            // FRECOMP (measurement): regenerate f at every use instead of carrying the
-            // window (fewer VGPRs, 8 more multiplies per row: measured slower, r01)
+            // f[ii]: from LDS, or (GENF) generated once here and carried in the f window
+            // (regenerating it at every use instead: fewer VGPRs, 8 more multiplies per
+            // row, measured slower in r01)
             V2<T> f0 = z;
             if constexpr (!GENF) f0 = ldv(&sf[slot][s][xo]);
-            if constexpr (GENF && !FRECOMP) {
+            if constexpr (GENF) {
                 const double sy = gsy_s(a.gsy, ii);
                 f0 = mk2<T>((T)(fxa * sy), (T)(fxb * sy));
             }
-            auto fr = [&](int row, const V2<T> &win) -> V2<T> {
-                if constexpr (GENF && FRECOMP) {
-                    const double sy = gsy_s(a.gsy, row);
-                    return mk2<T>((T)(fxa * sy), (T)(fxb * sy));
-                } else {
-                    return win;
-                }
-            };
-            const V2<T> fq1 = fr(ii - 1, f1), fq2 = fr(ii - 2, f2), fq3 = fr(ii - 3, f3),
-                        fq4 = fr(ii - 4, f4), fq5 = fr(ii - 5, f5);
+            const V2<T> fq1 = f1, fq2 = f2, fq3 = f3, fq4 = f4, fq5 = f5;
             const V2<T> e2 = (OPT & 64) ? xr : add_prolong<T, EDGE>(xr, ii, cr0, crn0, cr1, crn1, pc, Nc);
             // post-smooth sweep 1: x1 row ii-1
-            const V2<T> b2 = jsn<MODE, T, EDGE>(e0, e1, e2, nbr<T>(e1), fq1, hh, k, boundary_row(ii - 1, N));
+            const V2<T> b2 = jsn<T, EDGE>(e0, e1, e2, nbr<T>(e1), fq1, hh, k, boundary_row(ii - 1, N));
             const Nbr<T> nb1 = nbr<T>(b1), nc1 = nbr<T>(c1), ng1 = nbr<T>(g1);
             {   // post check: r(x1) on row ii-2
-                const V2<T> r1 = rsn<MODE, T>(b0, b1, b2, nb1, fq2, ih);
+                const V2<T> r1 = rsn<T>(b0, b1, b2, nb1, fq2, ih);
                 const int row = ii - 2;
                 if (row >= olo && row < ohi && k.own) {
                     acc1 = sqacc(acc1, r1.x);
@@ -961,9 +773,9 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                 }
             }
             // post-smooth sweep 2: x2 row ii-2 (= phi of cycle k+1)
-            const V2<T> c2 = jsn<MODE, T, EDGE>(b0, b1, b2, nb1, fq2, hh, k, boundary_row(ii - 2, N));
+            const V2<T> c2 = jsn<T, EDGE>(b0, b1, b2, nb1, fq2, hh, k, boundary_row(ii - 2, N));
             if (R2) {   // r(x2) on row ii-3
-                const V2<T> r2 = rsn<MODE, T>(c0, c1, c2, nc1, fq3, ih);
+                const V2<T> r2 = rsn<T>(c0, c1, c2, nc1, fq3, ih);
                 const int row = ii - 3;
                 if (row >= olo && row < ohi && k.own) {
                     acc3 = sqacc(acc3, r2.x);
@@ -971,9 +783,9 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                 }
             }
             // pre-smooth sweep 1: x3 row ii-3
-            const V2<T> g2 = jsn<MODE, T, EDGE>(c0, c1, c2, nc1, fq3, hh, k, boundary_row(ii - 3, N));
+            const V2<T> g2 = jsn<T, EDGE>(c0, c1, c2, nc1, fq3, hh, k, boundary_row(ii - 3, N));
             {   // pre check: r(x3) on row ii-4
-                const V2<T> r3 = rsn<MODE, T>(g0, g1, g2, ng1, fq4, ih);
+                const V2<T> r3 = rsn<T>(g0, g1, g2, ng1, fq4, ih);
                 const int row = ii - 4;
                 if (row >= olo && row < ohi && k.own) {
                     acc2 = sqacc(acc2, r3.x);
@@ -981,13 +793,13 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                 }
             }
             // pre-smooth sweep 2: x4 row ii-4 (stored)
-            const V2<T> h2 = jsn<MODE, T, EDGE>(g0, g1, g2, ng1, fq4, hh, k, boundary_row(ii - 4, N));
+            const V2<T> h2 = jsn<T, EDGE>(g0, g1, g2, ng1, fq4, hh, k, boundary_row(ii - 4, N));
             if (ii - 4 >= olo && ii - 4 < ohi && k.own) {
                 if constexpr (OPT & 2) stv_nt(O + (ii - 4) * P, h2);
                 else stv(O + (ii - 4) * P, h2);
             }
             // r(x4) on row ii-5
-            const V2<T> d2 = rsn<MODE, T>(h0, h1, h2, nbr<T>(h1), fq5, ih);
+            const V2<T> d2 = rsn<T>(h0, h1, h2, nbr<T>(h1), fq5, ih);
             // restriction: rows ii-7, ii-6, ii-5 = 2jc-1, 2jc, 2jc+1 when ii is even
             if (!(OPT & 64) && (s & 1) == 0) {
                 const int jc = (ii - 6) >> 1;
@@ -1009,25 +821,15 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
             g0 = g1; g1 = g2;
             h0 = h1; h1 = h2;
             d0 = d1; d1 = d2;
-            if constexpr (!GENF || !FRECOMP) {
-                f5 = f4; f4 = f3; f3 = f2; f2 = f1; f1 = f0;
-            }
+            f5 = f4; f4 = f3; f3 = f2; f2 = f1; f1 = f0;
         }
         if (gi + 1 < ng) store_pair(gi + 1, px, pf, pe);
         if (gi + 1 + D < ng) load_pair(gi + 1 + D, px, pf, pe);
         __syncthreads();
     };
-    if constexpr (D == 2) {
-        for (int gi = 0; gi < ng; gi += 2) {
-            step(gi, pxB, pfB, peB);
-            if (gi + 1 < ng) step(gi + 1, pxA, pfA, peA);
-        }
-    } else {
-        for (int gi = 0; gi < ng; gi += 3) {
-            step(gi, pxB, pfB, peB);
-            if (gi + 1 < ng) step(gi + 1, pxC, pfC, peC);
-            if (gi + 2 < ng) step(gi + 2, pxA, pfA, peA);
-        }
+    for (int gi = 0; gi < ng; gi += 2) {
+        step(gi, pxB, pfB, peB);
+        if (gi + 1 < ng) step(gi + 1, pxA, pfA, peA);
     }
     const int slot = bk.y * gridDim.x + bk.x;
     const double s1 = fused_block_sum(acc1, red);
@@ -1045,258 +847,23 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
 }
 
 
-template <class T, bool R2, bool GENF, int D = 2, int OCC = 1, int MODE = 0, bool FRECOMP = false,
-          int OPT = 0>
-__global__ __launch_bounds__(64 * kPPWaves) __attribute__((amdgpu_waves_per_eu(OCC)))
-void k_postpre_lds(PostPreArgsT<T> a)
+template <class T, bool R2, bool GENF, int OPT>
+__global__ __launch_bounds__(64 * kPPWaves) void k_postpre_lds(PostPreArgsT<T> a)
 {
     __shared__ double red[kPPWaves];
     __shared__ __attribute__((aligned(16))) T sx[2][kPPR][kPPLdsRow];
     __shared__ __attribute__((aligned(16))) T sf[2][kPPR][GENF ? 1 : kPPLdsRow];
     __shared__ __attribute__((aligned(16))) T se[3][kPPLdsCoarse];
-    Blk bk = (OPT & 1) ? xcd_block() : Blk{(int)blockIdx.x, (int)blockIdx.y};
-    if (a.band_stride > 0) {
-        // strided band order: the grid holds R*S bands (R = band_stride, S = ceil(nb / R));
-        // dispatch slot y runs band (y % S) * R + y / S, so the bands of one dispatch round are
-        // R apart and band b+1 is dispatched about when band b retires: its top halo rows
-        // (band b's last rows) are still in the caches
-        const int nb = (a.jc1 - a.jc0 + a.rows_per_block - 1) / a.rows_per_block;
-        const int R = a.band_stride, S = (nb + R - 1) / R;
-        const int l = (bk.y % S) * R + bk.y / S;
-        if (l >= nb) return;
-        bk.y = l;
-    }
+    const Blk bk{(int)blockIdx.x, (int)blockIdx.y};
     const Cols k = lane_cols_t<kPPStride, kPPMargin>(a.N, bk.x);
     // the band's rows 2jcb-6 .. 2jce+5 (see postpre_lds_run): does it reach row 0 or N-1?
     const int jcb = a.jc0 + bk.y * a.rows_per_block;
     const int jce = min(jcb + a.rows_per_block, a.jc1);
     const bool edge_rows = 2 * jcb - 6 <= 0 || 2 * jce + 6 >= a.N - 1;
     if (k.edge || edge_rows)
-        postpre_lds_run<T, R2, GENF, D, MODE, true, FRECOMP, OPT>(a, k, red, sx, sf, se, bk);
+        postpre_lds_run<T, R2, GENF, true, OPT>(a, k, red, sx, sf, se, bk);
     else
-        postpre_lds_run<T, R2, GENF, D, MODE, false, FRECOMP, OPT>(a, k, red, sx, sf, se, bk);
-}
-
-// ---------------------------------------------------------------------------
-// k_postpre_glds: k_postpre_lds with the rows brought into LDS by LDS-DMA
-// (global_load_lds_dwordx4 / _dword: no VGPR destination) instead of register staging.
-// One finest-level configuration (fp64, analytic f regenerated in-kernel, one GPU):
-// the register sets that held the prefetched rows (16 VGPRs) are gone, and the rows of
-// THREE pairs ahead are in flight per wave (a 4-slot LDS ring) where register staging
-// afforded two.  The DMA stays in flight across the per-pair barrier: a raw s_barrier
-// after a counted `s_waitcnt vmcnt(n)` that retires only the next pair (vector-memory
-// loads return in order, so at most n outstanding means every older load has landed;
-// stores in between only make the wait stricter).  __syncthreads() would drain it.
-// All LDS is one array (a second __shared__ object makes hipcc wait vmcnt(0) before
-// LDS reads).  Arithmetic identical to postpre_lds_run.
-// ---------------------------------------------------------------------------
-constexpr int kGlRow = 512;                   // doubles per fine LDS row (4 waves x 64 lanes x 2)
-constexpr int kGlSlots = 4;                   // row-pair slots (3 pairs in flight)
-constexpr int kGlCRow = 256;                  // doubles per coarse LDS row (2 dword DMAs per wave)
-constexpr int kGlCRing = 6;                   // coarse rows m-1 .. m+4 live
-constexpr int kGlLds = kGlSlots * kPPR * kGlRow + kGlCRing * kGlCRow + 8;   // doubles (40 KiB)
-
-// LDS-DMA in inline asm: hipcc's own bookkeeping would wait vmcnt(0) before every LDS read
-// of the staging array (it cannot tell the slots apart); the waits are counted by hand.
-// M0 = the wave-uniform LDS byte address, written in the same statement.
-__device__ __forceinline__ unsigned lds_addr(const double *p)
-{
-    return (unsigned)(unsigned long long)(const __attribute__((address_space(3))) double *)p;
-}
-
-__device__ __forceinline__ void glds16(const void *g, const double *lds_wave_base)
-{
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_wave_base)))
-                 : "memory");
-}
-
-__device__ __forceinline__ void glds4(const void *g, const double *lds_wave_base)
-{
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_wave_base)))
-                 : "memory");
-}
-
-// wait until at most n (0, 4 or 8) vector-memory operations of this wave are outstanding
-__device__ __forceinline__ void vm_wait(int n)
-{
-    if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-__device__ __forceinline__ void raw_barrier()
-{
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-}
-
-template <bool EDGE>
-__device__ __forceinline__ void postpre_glds_run(const PostPreArgsT<double> &a, const Cols &k,
-                                                 double *lds)
-{
-    using T = double;
-    constexpr int R = kPPR;
-    constexpr int MODE = 0;
-    double *const SXb = lds;                                   // [slot][q][kGlRow]
-    double *const SEb = lds + kGlSlots * R * kGlRow;           // [ring][kGlCRow]
-    double *const red = SEb + kGlCRing * kGlCRow;              // block-sum scratch
-    const int N = a.N, Nc = a.Nc;
-    const long long P = a.P, Pc = a.Pc;
-    const int jcb = a.jc0 + blockIdx.y * a.rows_per_block;
-    const int jce = min(jcb + a.rows_per_block, a.jc1);
-    const int olo = max(2 * jcb, a.row_lo), ohi = min(2 * jce, a.row_hi);
-    const int clo = max(jcb, max(1, a.rc_lo)), chi = min(jce, min(N / 2, a.rc_hi));
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
-        atomicAdd(&a.stats[0], 4ull);
-    ProlongCols pc;
-    pc.ic = (k.c - 1) >> 1;
-    pc.vx = k.c >= 3 && k.c <= N - 2;
-    pc.vy = k.c + 1 >= 2 && k.c + 1 <= N - 3;
-    T *__restrict__ O = a.x4 + k.c;
-    const T hh = a.hh, ih = a.ih;
-    const V2<T> z = zero2<T>();
-
-    const int wpb = blockDim.x >> 6;
-    const int t = threadIdx.x;
-    const int L0 = kPPStride * wpb * blockIdx.x + 1 - kPPMargin;
-    // Every lane issues every DMA (a wave's count of vector-memory operations per pair must
-    // be exactly 4 for the counted waits): lanes past the grid re-read its last valid pair
-    // (N - 2 is odd: 16-byte aligned); columns >= N never matter.
-    const T *__restrict__ GX = a.phi + min(L0 + 2 * t, N - 2);
-    const int cc0 = (L0 - 1) >> 1;
-    // coarse rows: dword d = i * 256 + t (i = 0, 1) of the block window, clamped likewise
-    const int dmax = 2 * (Nc - 1 - cc0) + 1;
-    const char *__restrict__ GE = reinterpret_cast<const char *>(a.ec + cc0);
-    const int ce0 = 4 * min(t, dmax), ce1 = 4 * min(256 + t, dmax);
-    const double fxa = a.gfx[k.c], fxb = a.gfx[k.c + 1];
-    const __attribute__((address_space(4))) double *gsy4 =
-        (const __attribute__((address_space(4))) double *)a.gsy;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int xo = kPPStride * w + 2 * lane;
-    const int co = (kPPStride / 2) * w + lane;
-
-    V2<T> e0 = z, e1 = z, b0 = z, b1 = z, c0 = z, c1 = z, g0 = z, g1 = z, h0 = z, h1 = z,
-            d0 = z, d1 = z;
-    V2<T> f1 = z, f2 = z, f3 = z, f4 = z, f5 = z;
-    double acc1 = 0.0, acc2 = 0.0;
-    const int i_begin = 2 * jcb - 6;
-    const int ng = (2 * (jce - jcb) + 11 + R - 1) / R;
-    const int m0 = i_begin >> 1;
-    auto ring = [](int m) { return (m + kGlCRing * 4096) % kGlCRing; };   // m >= -3
-    auto SX = [&](int slot, int q) { return SXb + (slot * R + q) * kGlRow; };
-    auto SE = [&](int r) { return SEb + r * kGlCRow; };
-    // one coarse row into ring slot r: this wave's 2 dword DMAs
-    auto issue_coarse = [&](int m) {
-        double *dst = SE(ring(m));
-        const char *src = GE + (long long)m * Pc * 8;
-        glds4(src + ce0, dst + 32 * w);
-        glds4(src + ce1, dst + 128 + 32 * w);
-    };
-    // pair p: its R rows into slot p % kGlSlots and its second coarse row (4 DMAs per wave)
-    auto issue_pair = [&](int p) {
-        #pragma unroll
-        for (int q = 0; q < R; ++q)
-            glds16(GX + (long long)(i_begin + p * R + q) * P, SX(p % kGlSlots, q) + 128 * w);
-        issue_coarse(m0 + p + 1);
-    };
-    // prologue: coarse row m0 (2 DMAs), pairs 0 .. 2 (4 each); wait for row m0 + pair 0
-    issue_coarse(m0);
-    issue_pair(0);
-    if (ng > 1) issue_pair(1);
-    if (ng > 2) issue_pair(2);
-    vm_wait(4 * (min(ng, 3) - 1));
-    raw_barrier();
-
-    T wprev = T(0);
-    for (int gi = 0; gi < ng; ++gi) {
-        if (gi + 3 < ng) issue_pair(gi + 3);   // into the slot of pair gi - 1 (read before the barrier)
-        const int slot = gi % kGlSlots;
-        const int i = i_begin + gi * R;
-        const int m = m0 + gi;
-        const T *E0 = SE(ring(m)), *E1 = SE(ring(m + 1));
-        const T cr0 = E0[co], crn0 = E0[co + 1], cr1 = E1[co], crn1 = E1[co + 1];
-        #pragma unroll
-        for (int s = 0; s < R; ++s) {
-            const int ii = i + s;
-            const V2<T> xr = ldv(SX(slot, s) + xo);
-            const double sy = gsy4[ii];   // scalar load: a vector one would be waited for
-                                          // with vmcnt(0), draining the DMAs in flight
-            const V2<T> f0 = mk2<T>((T)(fxa * sy), (T)(fxb * sy));
-            const V2<T> e2 = add_prolong<T, EDGE>(xr, ii, cr0, crn0, cr1, crn1, pc, Nc);
-            const V2<T> b2 = jsn<MODE, T, EDGE>(e0, e1, e2, nbr<T>(e1), f1, hh, k, boundary_row(ii - 1, N));
-            const Nbr<T> nb1 = nbr<T>(b1), nc1 = nbr<T>(c1), ng1 = nbr<T>(g1);
-            {
-                const V2<T> r1 = rsn<MODE, T>(b0, b1, b2, nb1, f2, ih);
-                const int row = ii - 2;
-                if (row >= olo && row < ohi && k.own) {
-                    acc1 = sqacc(acc1, r1.x);
-                    if (!k.by) acc1 = sqacc(acc1, r1.y);
-                }
-            }
-            const V2<T> c2 = jsn<MODE, T, EDGE>(b0, b1, b2, nb1, f2, hh, k, boundary_row(ii - 2, N));
-            const V2<T> g2 = jsn<MODE, T, EDGE>(c0, c1, c2, nc1, f3, hh, k, boundary_row(ii - 3, N));
-            {
-                const V2<T> r3 = rsn<MODE, T>(g0, g1, g2, ng1, f4, ih);
-                const int row = ii - 4;
-                if (row >= olo && row < ohi && k.own) {
-                    acc2 = sqacc(acc2, r3.x);
-                    if (!k.by) acc2 = sqacc(acc2, r3.y);
-                }
-            }
-            const V2<T> h2 = jsn<MODE, T, EDGE>(g0, g1, g2, ng1, f4, hh, k, boundary_row(ii - 4, N));
-            if (ii - 4 >= olo && ii - 4 < ohi && k.own) stv(O + (ii - 4) * P, h2);
-            const V2<T> d2 = rsn<MODE, T>(h0, h1, h2, nbr<T>(h1), f5, ih);
-            if ((s & 1) == 0) {
-                const int jc = (ii - 6) >> 1;
-                const T m2 = dpp_shl(d1.x);
-                const T u2 = wprev;
-                const T w2 = dpp_shl(d2.x);
-                wprev = w2;
-                const int ic = (k.c + 1) >> 1;
-                if (jc >= clo && jc < chi && k.own && ic <= Nc - 2) {
-                    const T v = T(0.25) * d1.y + T(0.125) * (m2 + d1.x + d2.y + d0.y) +
-                                T(0.0625) * (d0.x + u2 + d2.x + w2);
-                    a.rc[(long long)jc * Pc + ic] = v;
-                }
-            }
-            e0 = e1; e1 = e2;
-            b0 = b1; b1 = b2;
-            c0 = c1; c1 = c2;
-            g0 = g1; g1 = g2;
-            h0 = h1; h1 = h2;
-            d0 = d1; d1 = d2;
-            f5 = f4; f4 = f3; f3 = f2; f2 = f1; f1 = f0;
-        }
-        // pair gi + 1 must have landed: the pairs issued after it (gi + 2, gi + 3) may fly on
-        vm_wait(4 * max(0, min(gi + 3, ng - 1) - (gi + 1)));
-        raw_barrier();
-    }
-    const int slot = blockIdx.y * gridDim.x + blockIdx.x;
-    const double s1 = fused_block_sum(acc1, red);
-    __syncthreads();
-    const double s2 = fused_block_sum(acc2, red);
-    if (threadIdx.x == 0) {
-        a.partials1[slot] = s1;
-        a.partials2[slot] = s2;
-    }
-}
-
-__global__ __launch_bounds__(256) void k_postpre_glds(PostPreArgsT<double> a)
-{
-    __shared__ __attribute__((aligned(16))) double lds[kGlLds];
-    const Cols k = lane_cols_t<kPPStride, kPPMargin>(a.N);
-    const int jcb = a.jc0 + blockIdx.y * a.rows_per_block;
-    const int jce = min(jcb + a.rows_per_block, a.jc1);
-    const bool edge_rows = 2 * jcb - 6 <= 0 || 2 * jce + 6 >= a.N - 1;
-    if (k.edge || edge_rows)
-        postpre_glds_run<true>(a, k, lds);
-    else
-        postpre_glds_run<false>(a, k, lds);
+        postpre_lds_run<T, R2, GENF, false, OPT>(a, k, red, sx, sf, se, bk);
 }
 
 // one block: both decisions, stats, flags for the conditional rare-path kernels
@@ -1346,13 +913,15 @@ __global__ __launch_bounds__(256) void k_postpre_decide(const double *p1, const 
 // launch geometry
 // ---------------------------------------------------------------------------
 // Launch geometry.  Blocks march down long row bands: the grid is sized to about
-// the number of workgroups resident at once (tunable: PGMG_FUSED_BLOCKS), so the
-// 8 halo rows per band are a small fraction and there is no tail wave of blocks.
-static int env_int(const char *name, int dflt)
+// the number of workgroups resident at once, so the 8 halo rows per band are a small
+// fraction and there is no tail wave of blocks.
+#ifdef PGMG_TUNING
+int tuning_int(const char *name, int dflt)
 {
     const char *v = getenv(name);
     return (v && *v) ? atoi(v) : dflt;
 }
+#endif
 
 static void fused_geometry(int N, int jc0, int jc1, int *threads, int *gx, int *gy, int *rpb,
                            int stride = 120, int target = 0, int maxw = 4)
@@ -1370,17 +939,16 @@ static void fused_geometry(int N, int jc0, int jc1, int *threads, int *gx, int *
         if (pts > (1LL << 23)) {
             // ~22k points per workgroup, at least one round of the 512 resident (8193 on 8
             // strips: 37+28 -> 34+24 us), at most 3072
-            target = env_int("PGMG_FUSED_BLOCKS", (int)std::min(3072LL, std::max(512LL, pts / 21845)));
+            target = tuning_int("PGMG_FUSED_BLOCKS", (int)std::min(3072LL, std::max(512LL, pts / 21845)));
         } else {
             // latency-bound levels (N <= 2049): short bands (~8k points per workgroup);
             // measured at N = 16385: 2049 26+20 -> 23+18 us, 1025 13+11 -> 12+10, 513..129
             // 12+10 -> 7+7
-            target = env_int("PGMG_FUSED_SMALL_BLOCKS", (int)std::max(256LL, pts / 8192));
+            target = tuning_int("PGMG_FUSED_SMALL_BLOCKS", (int)std::max(256LL, pts / 8192));
         }
     }
 
-    const int rmin = env_int("PGMG_FUSED_MIN_ROWS", 2);
-    const int rmax = env_int("PGMG_FUSED_MAX_ROWS", 512);
+    const int rmin = 2, rmax = 512;
     // bands so that gx * gy does not exceed the target (a target of whole rounds of the
     // resident workgroups must not spill a few workgroups into one more round: 3096
     // workgroups for a 3072 target cost ~2 % in k_postpre)
@@ -1392,8 +960,6 @@ static void fused_geometry(int N, int jc0, int jc1, int *threads, int *gx, int *
     *rpb = r;
     *gy = (rows + r - 1) / r;
 }
-
-static int fused_pairs() { return env_int("PGMG_FUSED_PAIRS", 2) >= 2 ? 2 : 1; }
 
 int fused_blocks(int N, int jc0, int jc1)
 {
@@ -1413,37 +979,25 @@ void launch_pre(const PreArgsT<T> &a0, bool x0_zero, bool fine, hipStream_t s)
     a.rows_per_block = r;
     // non-temporal stores on the finest level only (its x2 is read again a level-pass later;
     // coarse outputs are re-read while still in the caches): fine k_pre 0.99 -> 0.97 ms
-    static const int nt = env_int("PGMG_NT", -1);
-    a.nt = nt >= 0 ? nt : (fine ? 1 : 0);
+    a.nt = fine ? 1 : 0;
     const dim3 g(gx, gy), b(t);
+    // two row pairs per iteration (r01 sweeps: on x0 = 0 levels 2 as fast as 3 at 8193 and
+    // faster below, 4 slower; one pair slower everywhere)
     if (a.pin_ec != nullptr) {   // F-cycle: x0 = prolongation of the coarse grid
         if (fine && a.gfx != nullptr) k_pre<T, false, true, 2, true, true><<<g, b, 0, s>>>(a);
         else if (fine) k_pre<T, false, true, 2, false, true><<<g, b, 0, s>>>(a);
         else if (a.gfx != nullptr) k_pre<T, false, false, 2, true, true><<<g, b, 0, s>>>(a);
         else k_pre<T, false, false, 2, false, true><<<g, b, 0, s>>>(a);
-        return;
-    }
-    // x0 = 0 (coarse levels): only f streams, so more rows in flight per lane
-    // r01 sweeps: 2 as fast as 3 on 8193, faster below (4097: 52 vs 56 us), 4 slower
-    static const int p0 = env_int("PGMG_PRE0_PAIRS", 2);
-    if (x0_zero && p0 == 4) {
-        k_pre<T, true, false, 4><<<g, b, 0, s>>>(a);
-        return;
-    }
-    if (x0_zero && p0 == 3) {
-        k_pre<T, true, false, 3><<<g, b, 0, s>>>(a);
-        return;
-    }
-    if (fused_pairs() == 2) {
-        if (x0_zero) k_pre<T, true, false, 2><<<g, b, 0, s>>>(a);
-        else if (fine && a.gfx != nullptr) k_pre<T, false, true, 2, true><<<g, b, 0, s>>>(a);
-        else if (fine) k_pre<T, false, true, 2><<<g, b, 0, s>>>(a);
-        else if (a.gfx != nullptr) k_pre<T, false, false, 2, true><<<g, b, 0, s>>>(a);
-        else k_pre<T, false, false, 2><<<g, b, 0, s>>>(a);
+    } else if (x0_zero) {
+        k_pre<T, true, false, 2><<<g, b, 0, s>>>(a);
+    } else if (fine && a.gfx != nullptr) {
+        k_pre<T, false, true, 2, true><<<g, b, 0, s>>>(a);
+    } else if (fine) {
+        k_pre<T, false, true, 2><<<g, b, 0, s>>>(a);
+    } else if (a.gfx != nullptr) {
+        k_pre<T, false, false, 2, true><<<g, b, 0, s>>>(a);
     } else {
-        if (x0_zero) k_pre<T, true, false, 1><<<g, b, 0, s>>>(a);
-        else if (fine) k_pre<T, false, true, 1><<<g, b, 0, s>>>(a);
-        else k_pre<T, false, false, 1><<<g, b, 0, s>>>(a);
+        k_pre<T, false, false, 2><<<g, b, 0, s>>>(a);
     }
 }
 
@@ -1454,28 +1008,15 @@ void launch_post(const PostArgsT<T> &a0, bool fine, hipStream_t s)
     fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r);
     PostArgsT<T> a = a0;
     a.rows_per_block = r;
-    // fine k_post: 1.01 -> 0.93 ms with non-temporal stores (PGMG_NT: measurement)
-    static const int nt = env_int("PGMG_NT", -1);
-    a.nt = nt >= 0 ? nt : (fine ? 4 : 0);
+    // fine k_post: 1.01 -> 0.93 ms with non-temporal stores
+    a.nt = fine ? 4 : 0;
     const dim3 g(gx, gy), b(t);
     const bool rec = a.pre_fired != nullptr;
-    static const int pr = env_int("PGMG_POSTR_PAIRS", 2);
-    if (!fine && rec && (pr == 3 || pr == 4)) {
-        if (pr == 4) k_post<T, false, 4, true><<<g, b, 0, s>>>(a);
-        else k_post<T, false, 3, true><<<g, b, 0, s>>>(a);
-        return;
-    }
-    if (fused_pairs() == 2) {
-        if (fine && a.gfx != nullptr) k_post<T, true, 2, false, true><<<g, b, 0, s>>>(a);
-        else if (fine) k_post<T, true, 2, false><<<g, b, 0, s>>>(a);
-        else if (rec) k_post<T, false, 2, true><<<g, b, 0, s>>>(a);
-        else if (a.gfx != nullptr) k_post<T, false, 2, false, true><<<g, b, 0, s>>>(a);
-        else k_post<T, false, 2, false><<<g, b, 0, s>>>(a);
-    } else {
-        if (fine) k_post<T, true, 1, false><<<g, b, 0, s>>>(a);
-        else if (rec) k_post<T, false, 1, true><<<g, b, 0, s>>>(a);
-        else k_post<T, false, 1, false><<<g, b, 0, s>>>(a);
-    }
+    if (fine && a.gfx != nullptr) k_post<T, true, 2, false, true><<<g, b, 0, s>>>(a);
+    else if (fine) k_post<T, true, 2, false><<<g, b, 0, s>>>(a);
+    else if (rec) k_post<T, false, 2, true><<<g, b, 0, s>>>(a);
+    else if (a.gfx != nullptr) k_post<T, false, 2, false, true><<<g, b, 0, s>>>(a);
+    else k_post<T, false, 2, false><<<g, b, 0, s>>>(a);
 }
 
 // k_postpre's grid target: 3072 workgroups = 6 full rounds of the 512 that are resident
@@ -1488,7 +1029,7 @@ void launch_post(const PostArgsT<T> &a0, bool fine, hipStream_t s)
 static int pp_target(int jc0, int jc1)
 {
     const int rounds = std::max(1, std::min(6, 6 * (2 * (jc1 - jc0) + 64) / 16384));
-    return env_int("PGMG_PP_BLOCKS", (2048 / kPPWaves) * rounds);   // 512 resident at 4 waves
+    return tuning_int("PGMG_PP_BLOCKS", (2048 / kPPWaves) * rounds);   // 512 resident at 4 waves
 }
 
 int postpre_blocks(int N, int jc0, int jc1)
@@ -1498,72 +1039,25 @@ int postpre_blocks(int N, int jc0, int jc1)
     return gx * gy;
 }
 
-// PGMG_PP_VARIANT (fp64 only, measurement): 1 trivial arithmetic, 2 <= 128 VGPRs,
-// 3 no column overlap, 4 per-wave HBM loads (no LDS staging)
+// The cross-cycle finest-level pass.  OPT 2: non-temporal x4 stores (x4 is read again
+// only by the next cycle's pass; r01: 1.18 vs 1.20 ms; non-temporal rc stores no gain).
+// Every launch path below launches: there is no configuration that returns without the pass.
 template <class T>
 void launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
 {
     int t, gx, gy, r;
-    const int variant = std::is_same<T, double>::value ? env_int("PGMG_PP_VARIANT", 0) : 0;
-    fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, variant == 3 ? 128 : kPPStride,
-                   pp_target(a0.jc0, a0.jc1), kPPWaves);
+    fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, kPPStride, pp_target(a0.jc0, a0.jc1),
+                   kPPWaves);
     PostPreArgsT<T> a = a0;
     a.rows_per_block = r;
-    a.band_stride = 0;
     const dim3 g(gx, gy), b(t);
-    if constexpr (std::is_same<T, double>::value) {
-        if ((a.partials3 != nullptr || a.gfx != nullptr) && variant != 0) return;   // 1 GPU, stored f
-        if (variant == 4) k_postpre<T, 1, 0><<<g, b, 0, s>>>(a);    // per-wave loads (r01)
-        else if (variant == 1) k_postpre<T, 1, 1><<<g, b, 0, s>>>(a);
-        else if (variant == 3) k_postpre<T, 1, 1, 128, 0><<<g, b, 0, s>>>(a);  // no column overlap
-        else if (variant == 2) k_postpre_o4<T, 1><<<g, b, 0, s>>>(a);
-        if (variant != 0) return;
-    }
     const bool genf = a.gfx != nullptr;
-    if constexpr (std::is_same<T, double>::value) {
-        // measurement knobs for the default pass (1 GPU, regenerated f)
-        const int depth = env_int("PGMG_PP_DEPTH", 2), occ = env_int("PGMG_PP_OCC", 1);
-        const int mode = env_int("PGMG_PP_LDS_MODE", 0);
-        // measured (r01): 2 (NT x4) 1.18 ms vs plain 1.20; XCD remap 1.25; NT rc no gain
-        const int opt = env_int("PGMG_PP_OPT", 2);   // 1 XCD remap, 2 NT x4 stores, 4 NT rc
-        if (genf && a.partials3 == nullptr && opt != 2) {
-            switch (opt) {
-            case 0: k_postpre_lds<T, false, true><<<g, b, 0, s>>>(a); break;   // plain stores
-            case 1: k_postpre_lds<T, false, true, 2, 1, 0, false, 1><<<g, b, 0, s>>>(a); break;
-            case 3: k_postpre_lds<T, false, true, 2, 1, 0, false, 3><<<g, b, 0, s>>>(a); break;
-            case 6: k_postpre_lds<T, false, true, 2, 1, 0, false, 6><<<g, b, 0, s>>>(a); break;
-            default: k_postpre_lds<T, false, true, 2, 1, 0, false, 7><<<g, b, 0, s>>>(a); break;
-            }
-            return;
-        }
-        if (genf && a.partials3 == nullptr && mode == 3 && t == 256) {   // LDS-DMA rows
-            k_postpre_glds<<<g, b, 0, s>>>(a);
-            return;
-        }
-        if (genf && a.partials3 == nullptr && mode == 1) {
-            k_postpre_lds<T, false, true, 2, 1, 1><<<g, b, 0, s>>>(a);
-            return;
-        }
-        if (genf && a.partials3 == nullptr && mode == 2) {   // f regenerated at every use
-            k_postpre_lds<T, false, true, 2, 1, 0, true><<<g, b, 0, s>>>(a);
-            return;
-        }
-        if (genf && a.partials3 == nullptr && (depth != 2 || occ != 1)) {
-            if (depth == 3 && occ == 3) k_postpre_lds<T, false, true, 3, 3, 0, false, 2><<<g, b, 0, s>>>(a);
-            else if (depth == 3) k_postpre_lds<T, false, true, 3, 1, 0, false, 2><<<g, b, 0, s>>>(a);
-            else k_postpre_lds<T, false, true, 2, 3, 0, false, 2><<<g, b, 0, s>>>(a);
-            return;
-        }
-    }
-    // OPT 2: non-temporal x4 stores (x4 is read again only by the next cycle's pass)
-    a.band_stride = env_int("PGMG_PP_BAND_STRIDE", 0);
-    const dim3 gs(gx, a.band_stride > 0 ? (gy + a.band_stride - 1) / a.band_stride * a.band_stride : gy);
     if (a.partials3 != nullptr) {
-        if (genf) k_postpre_lds<T, true, true, 2, 1, 0, false, 2><<<gs, b, 0, s>>>(a);
-        else k_postpre_lds<T, true, false, 2, 1, 0, false, 2><<<gs, b, 0, s>>>(a);
+        if (genf) k_postpre_lds<T, true, true, 2><<<g, b, 0, s>>>(a);
+        else k_postpre_lds<T, true, false, 2><<<g, b, 0, s>>>(a);
     } else {
-        if (genf) k_postpre_lds<T, false, true, 2, 1, 0, false, 2><<<gs, b, 0, s>>>(a);
-        else k_postpre_lds<T, false, false, 2, 1, 0, false, 2><<<gs, b, 0, s>>>(a);
+        if (genf) k_postpre_lds<T, false, true, 2><<<g, b, 0, s>>>(a);
+        else k_postpre_lds<T, false, false, 2><<<g, b, 0, s>>>(a);
     }
 }
 
@@ -1582,9 +1076,8 @@ void launch_smooth4(const PostPreArgsT<T> &a0, hipStream_t s)
                    kPPWaves);
     PostPreArgsT<T> a = a0;
     a.rows_per_block = r;
-    a.band_stride = 0;
-    if (a.gfx != nullptr) k_postpre_lds<T, true, true, 2, 1, 0, false, 64><<<dim3(gx, gy), dim3(t), 0, s>>>(a);
-    else k_postpre_lds<T, true, false, 2, 1, 0, false, 64><<<dim3(gx, gy), dim3(t), 0, s>>>(a);
+    if (a.gfx != nullptr) k_postpre_lds<T, true, true, 64><<<dim3(gx, gy), dim3(t), 0, s>>>(a);
+    else k_postpre_lds<T, true, false, 64><<<dim3(gx, gy), dim3(t), 0, s>>>(a);
 }
 
 __device__ __forceinline__ double block_sum_strided(const double *p, int n, double *red)
@@ -1909,7 +1402,7 @@ static int fixup_blocks(int N, int row_lo, int row_hi)
     // the tail converge and fire every cycle: 1083 -> 2435 V-cycles/s; 100 at 16385:
     // 439 -> 523; scripts/long_run.sh)
     const long long pts = (long long)(row_hi > row_lo ? row_hi - row_lo : 0) * N;
-    const long long shift = env_int("PGMG_FIX_SHIFT", 8), cap = env_int("PGMG_FIX_CAP", 8192);
+    const long long shift = 8, cap = 8192;
     long long b = pts >> shift;
     return (int)(b < 1 ? 1 : (b > cap ? cap : b));
 }

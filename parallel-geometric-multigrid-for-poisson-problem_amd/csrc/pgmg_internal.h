@@ -19,6 +19,17 @@
 
 namespace pgmg {
 
+// Tuning knobs.  The product library (libpgmg.so) reads nothing from the environment: every
+// launch geometry and variant is fixed at build time.  The measurement build
+// (libpgmg_ab.so, `make ab`, -DPGMG_TUNING) lets A/B scripts override the geometry knobs
+// named at the call sites (block counts, band heights, ...), none of which changes a
+// result bit.
+#ifdef PGMG_TUNING
+int tuning_int(const char *name, int dflt);
+#else
+inline int tuning_int(const char *, int dflt) { return dflt; }
+#endif
+
 // one early-exit check recorded by a speculative call: the producing pass's per-block
 // partial sums of r^2 (see pgmg_ctx.hip, "speculative calls")
 struct CheckRef {

@@ -538,13 +538,14 @@ size_t tail_lds_bytes(int N_top, int n_coarse)
     return kTailRed * sizeof(double) + (2 * S + (size_t)N_top * N_top) * sizeof(Real);
 }
 
-// PGMG_TAIL_PROF=1: the per-stage cycle counters of k_tail (measurement only)
+// PGMG_TAIL_PROF=1 (measurement build libpgmg_ab.so only): the per-stage cycle counters
+// of k_tail
 static unsigned long long *tail_prof_buffer()
 {
     static unsigned long long *buf = [] {
         unsigned long long *p = nullptr;
-        const char *v = getenv("PGMG_TAIL_PROF");
-        if (v && *v == '1' && hipMalloc(&p, 16 * sizeof(unsigned long long)) == hipSuccess)
+        if (tuning_int("PGMG_TAIL_PROF", 0) == 1 &&
+            hipMalloc(&p, 16 * sizeof(unsigned long long)) == hipSuccess)
             (void)hipMemset(p, 0, 16 * sizeof(unsigned long long));
         return p;
     }();
@@ -578,10 +579,7 @@ hipError_t launch_tail_gamma(const TailArgsT<Real> &a, int gamma, hipStream_t s)
     d.nl = nl;
     d.S = off;
     {
-        static const int wave_n = [] {
-            const char *v = getenv("PGMG_TAIL_WAVE_N");
-            return (v && *v) ? atoi(v) : 9;
-        }();
+        static const int wave_n = tuning_int("PGMG_TAIL_WAVE_N", 9);
         d.wave_n = wave_n;
     }
     d.prof = tail_prof_buffer();

@@ -1,3 +1,4 @@
+import contextlib
 import json
 import pathlib
 import sys
@@ -20,6 +21,20 @@ def pytest_configure(config):
 def pgmg():
     import _pkgload
     return _pkgload.load()
+
+
+@pytest.fixture
+def plan(pgmg):
+    """plan(**cfg): pgmg_config fields applied to every Solver built during this test
+    (pgmg.config_overrides; flags are OR-ed), e.g. plan(cross_min_n=9) to run the
+    cross-cycle fused finest level on small grids."""
+    stack = contextlib.ExitStack()
+
+    def set_(**kw):
+        stack.enter_context(pgmg.config_overrides(**kw))
+
+    yield set_
+    stack.close()
 
 
 @pytest.fixture(scope="session")

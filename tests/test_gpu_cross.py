@@ -2,9 +2,8 @@
 pre-smooth + residual + restriction of cycle k+1 in one pass) is bit-identical to the
 reference over multi-cycle calls, including both speculative early-exit rare paths.
 
-PGMG_CROSS_MIN_N lowers the grid size from which the finest level is cross-fused so
+pgmg_config.cross_min_n lowers the grid size from which the finest level is cross-fused so
 small grids exercise it (default 2049)."""
-import os
 
 import numpy as np
 import pytest
@@ -15,14 +14,9 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture
-def cross_everywhere():
-    old = os.environ.get("PGMG_CROSS_MIN_N")
-    os.environ["PGMG_CROSS_MIN_N"] = "9"
-    yield
-    if old is None:
-        os.environ.pop("PGMG_CROSS_MIN_N")
-    else:
-        os.environ["PGMG_CROSS_MIN_N"] = old
+def cross_everywhere(pgmg):
+    with pgmg.config_overrides(cross_min_n=9):
+        yield
 
 
 def _golden(golden_cycles, kind, N, eps=1e-7):

@@ -124,10 +124,10 @@ def test_fcycle_tiny_grids(pgmg, oracle_mod):
         assert np.array_equal(got.view(np.uint64), want.view(np.uint64)), N
 
 
-def test_fcycle_cross_context(pgmg, oracle_mod, golden_cycles, monkeypatch):
+def test_fcycle_cross_context(pgmg, oracle_mod, golden_cycles, plan):
     """A context that runs cross-cycle fused V-cycles (swapped ping-pong buffers) still
     runs F-cycles on its current solution."""
-    monkeypatch.setenv("PGMG_CROSS_MIN_N", "9")
+    plan(cross_min_n=9)
     N = 257
     o = oracle_mod.Oracle()
     f = o.rhs(N)

@@ -14,7 +14,6 @@ The reference is fp64-only, so the fp32 variant has two checks:
    7.5e-7 at 129, 5.8e-6 at 513, 1.7e-5 at 1025, 2.6e-4 at 2049): the fp32 round-off
    of the residual f - (1/h^2) A x grows like N^2, so the tolerance is per grid size.
 """
-import os
 import threading
 
 import numpy as np
@@ -26,22 +25,6 @@ pytestmark = pytest.mark.gpu
 
 # ||phi32 - phi64|| / ||phi64|| after 3 V-cycles (about 4x the oracle's measured value)
 FP32_TOL = {33: 2e-6, 129: 4e-6, 513: 3e-5, 1025: 1e-4, 2049: 1.2e-3}
-
-
-@pytest.fixture
-def env():
-    saved = {}
-
-    def set_(k, v):
-        saved.setdefault(k, os.environ.get(k))
-        os.environ[k] = v
-
-    yield set_
-    for k, v in saved.items():
-        if v is None:
-            os.environ.pop(k, None)
-        else:
-            os.environ[k] = v
 
 
 def _f32_oracle(oracle_mod, kind, N, cycles, phi0=None, f=None, **kw):
@@ -58,14 +41,14 @@ def _f32_oracle(oracle_mod, kind, N, cycles, phi0=None, f=None, **kw):
                                            (129, 33, "unfused"), (257, 17, "cross"),
                                            (513, 65, "cross"), (129, 17, "norecompute"),
                                            (2049, 65, "fused")])
-def test_fp32_vcycle_bitwise_vs_fp32_oracle(pgmg, oracle_mod, env, N, tail_n, mode):
+def test_fp32_vcycle_bitwise_vs_fp32_oracle(pgmg, oracle_mod, plan, N, tail_n, mode):
     cfg = dict(dtype="f32", tail_n=tail_n)
     if mode == "unfused":
         cfg["flags"] = pgmg.PGMG_FLAG_UNFUSED
     if mode == "cross":
-        env("PGMG_CROSS_MIN_N", "9")
+        plan(cross_min_n=9)
     if mode == "norecompute":
-        env("PGMG_RECOMPUTE", "0")
+        cfg["flags"] = pgmg.PGMG_FLAG_NO_RECOMPUTE
     cycles = 3
     ref, o = _f32_oracle(oracle_mod, "V", N, cycles)
     with pgmg.Solver(N, **cfg) as s:
@@ -94,10 +77,10 @@ def test_fp32_w_and_f_cycles_bitwise_vs_fp32_oracle(pgmg, oracle_mod, kind, N, c
         assert s.stats()[0] == o.sweeps
 
 
-def test_fp32_early_exit_rare_paths_bitwise(pgmg, oracle_mod, env):
+def test_fp32_early_exit_rare_paths_bitwise(pgmg, oracle_mod, plan):
     """Random problem, eps swept until early exits fire on bulk and tail levels and both
     k_postpre rare paths have run: still bitwise equal to the fp32 oracle."""
-    env("PGMG_CROSS_MIN_N", "9")
+    plan(cross_min_n=9)
     rng = np.random.default_rng(7)
     N = 129
     phi0 = rng.uniform(-1, 1, (N, N))

@@ -2,7 +2,7 @@
 recomputes it from f (x1 = J(0), x2 = J(x1), or x1 when the pre-smoothing check fired).
 Bit-identical to the reference in every early-exit combination (eps sweep on a random
 problem so the pre and post checks of the coarse levels fire in turn), V and W cycles,
-and equal to the stored-iterate path (PGMG_RECOMPUTE=0)."""
+and equal to the stored-iterate path (PGMG_FLAG_NO_RECOMPUTE)."""
 import numpy as np
 import pytest
 
@@ -32,8 +32,8 @@ def test_recompute_eps_sweep_matches_oracle(pgmg, oracle_mod, kind, monkeypatch)
             (o.v_cycle if kind == "V" else o.w_cycle)(ref, f)
         exits_seen += o.early_exits
         for rec in ("1", "0"):
-            monkeypatch.setenv("PGMG_RECOMPUTE", rec)
-            with pgmg.Solver(N, eps=eps, tail_n=9, flags=pgmg.PGMG_FLAG_NO_CROSS) as s:
+            fl = pgmg.PGMG_FLAG_NO_CROSS | (pgmg.PGMG_FLAG_NO_RECOMPUTE if rec == "0" else 0)
+            with pgmg.Solver(N, eps=eps, tail_n=9, flags=fl) as s:
                 s.set_problem(phi0, f)
                 (s.vcycle if kind == "V" else s.wcycle)(3)
                 assert_bitwise(s.solution(), ref, f"{kind} eps={eps} recompute={rec}")
@@ -46,8 +46,8 @@ def test_recompute_bytes_accounting(pgmg, monkeypatch):
     N = 1025
     b = {}
     for rec in ("1", "0"):
-        monkeypatch.setenv("PGMG_RECOMPUTE", rec)
-        with pgmg.Solver(N, flags=pgmg.PGMG_FLAG_NO_CROSS) as s:
+        fl = pgmg.PGMG_FLAG_NO_CROSS | (pgmg.PGMG_FLAG_NO_RECOMPUTE if rec == "0" else 0)
+        with pgmg.Solver(N, flags=fl) as s:
             b[rec] = s.vcycle_bytes()
     n1 = (513 - 2) ** 2
     assert b["0"] - b["1"] > 16 * n1

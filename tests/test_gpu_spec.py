@@ -5,10 +5,9 @@ check, across validated segments, after a rollback, for W-cycles, and after an F
 rewrote the boundary frame of the level-0 buffers (the speculative cycles rotate through
 the scratch grid S, which must mirror it).
 
-PGMG_FLAG_EXACT_DIST selects the in-stream decisions; PGMG_SPEC_SEG caps the cycles per
-validated segment.
+PGMG_FLAG_EXACT_DIST selects the in-stream decisions; pgmg_config.spec_segment caps the
+cycles per validated segment.
 """
-import os
 
 import numpy as np
 import pytest
@@ -16,22 +15,6 @@ import pytest
 from conftest import assert_bitwise
 
 pytestmark = pytest.mark.gpu
-
-
-@pytest.fixture
-def env():
-    saved = {}
-
-    def set_(k, v):
-        saved.setdefault(k, os.environ.get(k))
-        os.environ[k] = v
-
-    yield set_
-    for k, v in saved.items():
-        if v is None:
-            os.environ.pop(k, None)
-        else:
-            os.environ[k] = v
 
 
 def _run(pgmg, N, calls, problem=(None, None), cycle="v", **cfg):
@@ -43,8 +26,8 @@ def _run(pgmg, N, calls, problem=(None, None), cycle="v", **cfg):
 
 
 @pytest.mark.parametrize("N,calls", [(2049, [5]), (4097, [3, 1]), (513, [4, 2])])
-def test_speculative_equals_in_stream(pgmg, env, N, calls):
-    env("PGMG_CROSS_MIN_N", "9")
+def test_speculative_equals_in_stream(pgmg, plan, N, calls):
+    plan(cross_min_n=9)
     spec = _run(pgmg, N, calls)
     exact = _run(pgmg, N, calls, flags=pgmg.PGMG_FLAG_EXACT_DIST)
     assert spec[2] == (True, 0), spec[2]
@@ -53,11 +36,11 @@ def test_speculative_equals_in_stream(pgmg, env, N, calls):
     assert spec[1] == exact[1]
 
 
-def test_speculative_segments_match_golden(pgmg, oracle_mod, golden_cycles, env):
+def test_speculative_segments_match_golden(pgmg, oracle_mod, golden_cycles, plan):
     """Seven cycles in one call validated in segments of two (each segment restarts the
     cross-fused chain: k_pre, k_postpre..., k_post) equal the reference's seven."""
-    env("PGMG_CROSS_MIN_N", "9")
-    env("PGMG_SPEC_SEG", "2")
+    plan(cross_min_n=9)
+    plan(spec_segment=int("2"))
     case = next(c for c in golden_cycles if c["kind"] == "V" and c["N"] == 513 and c["eps"] == 1e-7)
     k = min(7, len(case["cycles"]))
     phi, det, info = _run(pgmg, 513, [k])
@@ -67,12 +50,12 @@ def test_speculative_segments_match_golden(pgmg, oracle_mod, golden_cycles, env)
 
 
 @pytest.mark.parametrize("seg", ["0", "1", "3"])
-def test_speculative_rollback_then_in_stream(pgmg, oracle_mod, env, seg):
+def test_speculative_rollback_then_in_stream(pgmg, oracle_mod, plan, seg):
     """eps above every norm, so every check fires: the first call is rolled back and rerun
     with in-stream decisions, later calls decide in-stream; every word is the oracle's."""
-    env("PGMG_CROSS_MIN_N", "9")
+    plan(cross_min_n=9)
     if seg != "0":
-        env("PGMG_SPEC_SEG", seg)
+        plan(spec_segment=int(seg))
     rng = np.random.default_rng(21)
     N, eps = 129, 1e9
     phi0 = rng.uniform(-1, 1, (N, N))
@@ -97,8 +80,8 @@ def test_speculative_rollback_then_in_stream(pgmg, oracle_mod, env, seg):
         assert s.dist_info()[1] == 2
 
 
-def test_speculative_wcycle(pgmg, oracle_mod, golden_cycles, env):
-    env("PGMG_CROSS_MIN_N", "9")
+def test_speculative_wcycle(pgmg, oracle_mod, golden_cycles, plan):
+    plan(cross_min_n=9)
     case = next(c for c in golden_cycles if c["kind"] == "W" and c["N"] == 129)
     # W-cycles revisit the coarse levels until their checks fire (the reference's 129 W-cycle
     # exits 147 times in its first cycle): they decide in-stream, never roll back
@@ -111,11 +94,11 @@ def test_speculative_wcycle(pgmg, oracle_mod, golden_cycles, env):
     assert spec[1] == exact[1]
 
 
-def test_speculative_after_fcycle_nonzero_boundary(pgmg, env):
+def test_speculative_after_fcycle_nonzero_boundary(pgmg, plan):
     """F-cycle zeroes the frame of the level-0 buffers (reference semantics); the scratch
     grid the speculative V-cycles rotate through must follow, or the boundary of later
     V-cycles goes wrong."""
-    env("PGMG_CROSS_MIN_N", "9")
+    plan(cross_min_n=9)
     rng = np.random.default_rng(8)
     N = 257
     phi0 = rng.uniform(-1, 1, (N, N))
@@ -132,12 +115,12 @@ def test_speculative_after_fcycle_nonzero_boundary(pgmg, env):
     assert out[0][1] == out[1][1]
 
 
-def test_speculative_30_cycles_golden(pgmg, oracle_mod, golden_cycles, env):
+def test_speculative_30_cycles_golden(pgmg, oracle_mod, golden_cycles, plan):
     """The reference's 30-cycle run at N = 513 (early exits from cycle 12 on, 112 in all)
     in segments of 5: the segments before the first firing check are kept, the one that
     contains it is rolled back and the rest of the call runs in-stream."""
-    env("PGMG_CROSS_MIN_N", "9")
-    env("PGMG_SPEC_SEG", "5")
+    plan(cross_min_n=9)
+    plan(spec_segment=int("5"))
     case = next(c for c in golden_cycles if c["kind"] == "V" and c["N"] == 513 and c["eps"] == 1e-7)
     last = case["cycles"][-1]
     phi, det, info = _run(pgmg, 513, [30])

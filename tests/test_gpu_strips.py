@@ -112,12 +112,13 @@ def test_strips_random_problem(pgmg):
 
 @pytest.mark.parametrize("recompute", ["1", "0"])
 @pytest.mark.parametrize("kind,eps", [("V", 1e-7), ("V", 1.0), ("W", 1e-7)])
-def test_strips_extended_post_rows(pgmg, monkeypatch, recompute, kind, eps):
+def test_strips_extended_post_rows(pgmg, plan, recompute, kind, eps):
     """k_post of the levels below the finest computes kPostExt rows past its strip instead
     of exchanging the coarse correction: thin strips (16 rows at the deepest distributed
     level), with and without the recomputed pre-smoothed iterate, V and W cycles, forced
     coarse early exits — bitwise equal to one GPU."""
-    monkeypatch.setenv("PGMG_RECOMPUTE", recompute)
+    if recompute == "0":
+        plan(flags=pgmg.PGMG_FLAG_NO_RECOMPUTE)
     N = 1025
     ref = _single(pgmg, N, 2, kind=kind, eps=eps, tail_n=17)
     outs = _run_ranks(pgmg, 8, N, 2, kind=kind, eps=eps, tail_n=17, gather_n=65)

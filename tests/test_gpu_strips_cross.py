@@ -8,7 +8,6 @@ PGMG_CROSS_MIN_N=9 cross-fuses every grid size so small strips exercise it; each
 Solver.vcycle(k) call is ONE multi-cycle call (k_pre, (children, k_postpre) x k-1,
 children, k_post).
 """
-import os
 import threading
 
 import numpy as np
@@ -20,14 +19,9 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True)
-def cross_everywhere():
-    old = os.environ.get("PGMG_CROSS_MIN_N")
-    os.environ["PGMG_CROSS_MIN_N"] = "9"
-    yield
-    if old is None:
-        os.environ.pop("PGMG_CROSS_MIN_N")
-    else:
-        os.environ["PGMG_CROSS_MIN_N"] = old
+def cross_everywhere(pgmg):
+    with pgmg.config_overrides(cross_min_n=9):
+        yield
 
 
 def _ranks(pgmg, world, N, cycles, problem=(None, None), **cfg):
