@@ -161,6 +161,12 @@ int pgmg_get_solution(pgmg_ctx *ctx, double *phi_host);
  * ranks other than root may pass phi_host = NULL).  root < 0: every rank, as above. */
 int pgmg_gather_solution(pgmg_ctx *ctx, int root, double *phi_host);
 
+/* FNV-64 hash of phi's IEEE words in the reference layout (h = 14695981039346656037,
+ * h = (h ^ word) * 1099511628211 per element, row-major N*N): the checksum of the golden
+ * fixtures (tests/golden/cycles.json).  Collective on row strips; the value lands on rank
+ * `root` (root < 0: every rank), the others get 0. */
+int pgmg_solution_hash(pgmg_ctx *ctx, int root, unsigned long long *hash);
+
 /* sqrt(sum over interior of r^2) for the current phi (synchronous). */
 int pgmg_residual_norm(pgmg_ctx *ctx, double *out);
 

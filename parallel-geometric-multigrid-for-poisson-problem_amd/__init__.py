@@ -195,6 +195,14 @@ class Solver:
               "pgmg_get_solution")
         return out
 
+    def solution_hash(self, root=0):
+        """FNV-64 of phi (hex string, the golden fixtures' format) on rank `root`; collective
+        on row strips (other ranks get None)."""
+        v = C.c_ulonglong()
+        check(self.lib.pgmg_solution_hash(self.h, int(root), C.byref(v)), "pgmg_solution_hash")
+        mine = self.cfg.world <= 1 or root < 0 or self.cfg.rank == root
+        return "%016x" % v.value if mine else None
+
     def gather_solution(self, root, want):
         """Collective: phi gathered to rank `root` only; returns it where `want`, else None
         (row strips of a large grid without a full host copy per rank)."""

@@ -78,6 +78,7 @@ SIGNATURES = [
     ("pgmg_sync", C.c_int, [_P]),
     ("pgmg_get_solution", C.c_int, [_P, _P]),
     ("pgmg_gather_solution", C.c_int, [_P, C.c_int, _P]),
+    ("pgmg_solution_hash", C.c_int, [_P, C.c_int, C.POINTER(C.c_ulonglong)]),
     ("pgmg_residual_norm", C.c_int, [_P, _DP]),
     ("pgmg_stats", C.c_int, [_P, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]),
     ("pgmg_stats_detail", C.c_int, [_P, C.POINTER(C.c_longlong)]),

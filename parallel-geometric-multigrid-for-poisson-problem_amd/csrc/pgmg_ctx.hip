@@ -1633,6 +1633,29 @@ int pgmg_gather_solution(pgmg_ctx *c, int root, double *phi)
     return download_grid(c, L.A.o, L.P, L.N, phi);
 }
 
+// FNV-64 over the IEEE words of phi in the reference layout: the checksum the golden
+// fixtures of the reference's runs carry (bench.py verifies the run it timed with it)
+int pgmg_solution_hash(pgmg_ctx *c, int root, unsigned long long *out)
+{
+    if (!c || !out) return set_err(PGMG_ERR_ARG, "null argument");
+    const int me = c->comm ? c->comm->rank() : 0;
+    const bool want = root < 0 || root == me || !c->comm;
+    const long long n = (long long)c->lv[0].N * c->lv[0].N;
+    std::vector<double> phi(want ? (size_t)n : 0);
+    int e = pgmg_gather_solution(c, root, want ? phi.data() : nullptr);
+    if (e) return e;
+    unsigned long long h = 1469598103934665603ULL;
+    if (want) {
+        for (long long i = 0; i < n; ++i) {
+            unsigned long long w;
+            std::memcpy(&w, &phi[(size_t)i], 8);
+            h = (h ^ w) * 1099511628211ULL;
+        }
+    }
+    *out = want ? h : 0ULL;
+    return PGMG_OK;
+}
+
 int pgmg_residual_norm(pgmg_ctx *c, double *out)
 {
     if (!c || !out) return set_err(PGMG_ERR_ARG, "null argument");
