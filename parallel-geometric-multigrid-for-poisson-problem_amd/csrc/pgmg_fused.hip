@@ -648,6 +648,59 @@ struct Blk {
 
 constexpr int kPPR = 2;   // rows per LDS slot (a row pair)
 
+#ifndef PGMG_PP_NTL
+#define PGMG_PP_NTL 0     // 1: non-temporal row loads (measurement builds)
+#endif
+
+// Lane t's 16-byte (fp32: 8-byte) column pair of a row segment starting at `base`; lanes
+// t >= n read 0 (descriptor range check).  The descriptor is built from wave-uniform values.
+template <class T, int NT>
+__device__ __forceinline__ V2<T> buf_row(const T *base, int n, int t)
+{
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<T *>(base), (short)0, n * (int)sizeof(V2<T>), 0x00020000);
+    if constexpr (sizeof(T) == 8) {
+        return __builtin_bit_cast(V2<T>, __builtin_amdgcn_raw_buffer_load_b128(
+                                             r, t * 16, 0, NT ? 2 : 0));
+    } else {
+        return __builtin_bit_cast(V2<T>, __builtin_amdgcn_raw_buffer_load_b64(
+                                             r, t * 8, 0, NT ? 2 : 0));
+    }
+}
+template <class T, int NT>
+__device__ __forceinline__ void buf_store_row(T *base, int bytes, int off, V2<T> v)
+{
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, bytes, 0x00020000);
+    if constexpr (sizeof(T) == 8) {
+        typedef unsigned u4 __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, off, 0, NT ? 2 : 0);
+    } else {
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, off, 0, NT ? 2 : 0);
+    }
+}
+template <class T>
+__device__ __forceinline__ void buf_store_one(T *base, int bytes, int off, T v)
+{
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, bytes, 0x00020000);
+    if constexpr (sizeof(T) == 8) {
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, off, 0, 0);
+    } else {
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
+    }
+}
+template <class T>
+__device__ __forceinline__ T buf_one(const T *base, int n, int t)
+{
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<T *>(base), (short)0, n * (int)sizeof(T), 0x00020000);
+    if constexpr (sizeof(T) == 8)
+        return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, t * 8, 0, 0));
+    else
+        return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, t * 4, 0, 0));
+}
+
 // The body of k_postpre_lds for one block.  EDGE = false: no row of the block's band and
 // no column of this wave is a boundary, so the Jacobi stages carry no passthrough selects.
 template <class T, bool R2, bool GENF, bool EDGE, int OPT>
@@ -669,7 +722,6 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     pc.ic = (k.c - 1) >> 1;
     pc.vx = k.c >= 3 && k.c <= N - 2;
     pc.vy = k.c + 1 >= 2 && k.c + 1 <= N - 3;
-    T *__restrict__ O = a.x4 + k.c;
     const T hh = a.hh, ih = a.ih;
     const V2<T> z = zero2<T>();
 
@@ -678,16 +730,29 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     const int t = threadIdx.x;
     const int L0 = kPPStride * wpb * bk.x + 1 - kPPMargin;
     const int npairs = (kPPStride * wpb + 2 * kPPMargin) / 2;
-    const bool ldr = t < npairs && L0 + 2 * t <= N - 1;      // columns >= N never matter
     const int cc0 = (L0 - 1) >> 1;                               // first coarse column
     const int ncc = (kPPStride / 2) * wpb + kPPMargin + 2;
     // OPT & 64 (F-cycle smooth(3)): no coarse correction, no restriction
-    const bool cldr = !(OPT & 64) && t < ncc && cc0 + t <= Nc - 1;
-    const T *__restrict__ GX = a.phi + L0 + 2 * t;
-    const T *__restrict__ GF = a.f + L0 + 2 * t;
-    const T *__restrict__ GE = a.ec + cc0 + t;
+    // Row loads through buffer descriptors (one per row, built from wave-uniform values):
+    // VMEM-only loads whose out-of-range lanes (past the window or the grid's last column)
+    // read 0 from the descriptor's range check.  A `ldr ? load : 0` select compiles to a
+    // FLAT load, which also counts on lgkmcnt, so the LDS wait before every barrier drained
+    // the row pairs prefetched for later steps.
+    // lanes that load (columns >= N never matter)
+    const int nvx = max(0, min(npairs, (N - 1 - L0) / 2 + 1));
+    const int nve = (OPT & 64) ? 0 : max(0, min(ncc, Nc - cc0));
+    // stores: x4 row segment of the block window (lanes that own their pair), rc (lanes
+    // owning a coarse column <= Nc-2); anything else gets an out-of-range offset
+    constexpr int kOOB = 1 << 30;
+    const int xbytes = (2 * npairs + 8) * (int)sizeof(T);
+    const int xoff = k.own ? (k.c - L0) * (int)sizeof(T) : kOOB;
+    const int cbytes = (ncc + 8) * (int)sizeof(T);
+    const int coff = (k.own && ((k.c + 1) >> 1) <= Nc - 2) ? (((k.c + 1) >> 1) - cc0) * (int)sizeof(T) : kOOB;
     // GENF: this lane's columns of fx (tables padded: valid for columns/rows -8 ..)
     const double fxa = GENF ? a.gfx[k.c] : 0.0, fxb = GENF ? a.gfx[k.c + 1] : 0.0;
+    // land them before the row loop: a load still in flight at the loop entry makes the
+    // loop's first use of fxa wait for every outstanding load (vmcnt(0)) in every iteration
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
     // this wave's window in the LDS rows
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int xo = kPPStride * w + 2 * lane;
@@ -714,10 +779,12 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     auto load_pair = [&](int p, V2<T> (&px)[R], V2<T> (&pf)[R], T &pe) {
         #pragma unroll
         for (int q = 0; q < R; ++q) {
-            px[q] = ldr ? ldv(GX + (i_begin + p * R + q) * P) : z;
-            if constexpr (!GENF) pf[q] = ldr ? ldv(GF + (i_begin + p * R + q) * P) : z;
+            const long long row = (long long)(i_begin + p * R + q) * P + L0;
+            px[q] = buf_row<T, PGMG_PP_NTL>(a.phi + row, nvx, t);
+            if constexpr (!GENF) pf[q] = buf_row<T, PGMG_PP_NTL>(a.f + row, nvx, t);
         }
-        pe = cldr ? GE[(long long)(m0 + p + 1) * Pc] : T(0);   // the pair's second coarse row
+        // the pair's second coarse row
+        pe = buf_one<T>(a.ec + (long long)(m0 + p + 1) * Pc + cc0, nve, t);
     };
     auto store_pair = [&](int p, const V2<T> (&px)[R], const V2<T> (&pf)[R], T pe) {
         if (t < npairs) {
@@ -731,7 +798,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     };
     // prologue: pair 0 (+ its first coarse row) into slot 0; pairs 1 .. D in flight
     load_pair(0, pxA, pfA, peA);
-    if (t < ncc) se[ring(m0)][t] = cldr ? GE[(long long)m0 * Pc] : T(0);
+    if (t < ncc) se[ring(m0)][t] = buf_one<T>(a.ec + (long long)m0 * Pc + cc0, nve, t);
     store_pair(0, pxA, pfA, peA);
     if (ng > 1) load_pair(1, pxB, pfB, peB);
     if (ng > 2) load_pair(2, pxA, pfA, peA);
@@ -742,6 +809,11 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     T wprev = T(0);   // dpp_shl(d2.x) of the previous restriction row (d0 starts as zero)
     auto step = [&](int gi, V2<T> (&px)[R], V2<T> (&pf)[R], T &pe) {
         const int slot = gi & 1;
+        // the other slot's previous readers passed the last barrier: stage pair gi+1 (loaded
+        // two steps ago) first and reissue its register set for pair gi+3, so the loads in
+        // flight are never younger than this step's stores (counted waits stay small)
+        if (gi + 1 < ng) store_pair(gi + 1, px, pf, pe);
+        if (gi + 1 + D < ng) load_pair(gi + 1 + D, px, pf, pe);
         const int i = i_begin + gi * R;
         const int m = m0 + gi;
         const T *E0 = se[ring(m)], *E1 = se[ring(m + 1)];
@@ -794,10 +866,11 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
             }
             // pre-smooth sweep 2: x4 row ii-4 (stored)
             const V2<T> h2 = jsn<T, EDGE>(g0, g1, g2, ng1, fq4, hh, k, boundary_row(ii - 4, N));
-            if (ii - 4 >= olo && ii - 4 < ohi && k.own) {
-                if constexpr (OPT & 2) stv_nt(O + (ii - 4) * P, h2);
-                else stv(O + (ii - 4) * P, h2);
-            }
+            // branch-free: rows outside the band get a zero-record descriptor, lanes that do
+            // not own their pair an out-of-range offset (every step issues the same memory
+            // instructions, so the compiler can count its waits)
+            buf_store_row<T, (OPT & 2) ? 1 : 0>(a.x4 + (long long)(ii - 4) * P + L0,
+                                               (ii - 4 >= olo && ii - 4 < ohi) ? xbytes : 0, xoff, h2);
             // r(x4) on row ii-5
             const V2<T> d2 = rsn<T>(h0, h1, h2, nbr<T>(h1), fq5, ih);
             // restriction: rows ii-7, ii-6, ii-5 = 2jc-1, 2jc, 2jc+1 when ii is even
@@ -807,13 +880,10 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                 const T u2 = wprev;               // = dpp_shl(d0.x): row ii-7 was d2 two rows ago
                 const T w2 = dpp_shl(d2.x);
                 wprev = w2;
-                const int ic = (k.c + 1) >> 1;
-                if (jc >= clo && jc < chi && k.own && ic <= Nc - 2) {
-                    const T v = T(0.25) * d1.y + T(0.125) * (m2 + d1.x + d2.y + d0.y) +
-                                     T(0.0625) * (d0.x + u2 + d2.x + w2);
-                    if constexpr (OPT & 4) __builtin_nontemporal_store(v, &a.rc[(long long)jc * Pc + ic]);
-                    else a.rc[(long long)jc * Pc + ic] = v;
-                }
+                const T v = T(0.25) * d1.y + T(0.125) * (m2 + d1.x + d2.y + d0.y) +
+                                 T(0.0625) * (d0.x + u2 + d2.x + w2);
+                buf_store_one<T>(a.rc + (long long)jc * Pc + cc0, (jc >= clo && jc < chi) ? cbytes : 0,
+                                 coff, v);
             }
             e0 = e1; e1 = e2;
             b0 = b1; b1 = b2;
@@ -823,8 +893,6 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
             d0 = d1; d1 = d2;
             f5 = f4; f4 = f3; f3 = f2; f2 = f1; f1 = f0;
         }
-        if (gi + 1 < ng) store_pair(gi + 1, px, pf, pe);
-        if (gi + 1 + D < ng) load_pair(gi + 1 + D, px, pf, pe);
         __syncthreads();
     };
     for (int gi = 0; gi < ng; gi += 2) {
@@ -847,8 +915,12 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
 }
 
 
+#ifndef PGMG_PP_OCC
+#define PGMG_PP_OCC 2     // waves per SIMD the register allocation must allow
+#endif
 template <class T, bool R2, bool GENF, int OPT>
-__global__ __launch_bounds__(64 * kPPWaves) void k_postpre_lds(PostPreArgsT<T> a)
+__global__ __launch_bounds__(64 * kPPWaves) __attribute__((amdgpu_waves_per_eu(PGMG_PP_OCC)))
+void k_postpre_lds(PostPreArgsT<T> a)
 {
     __shared__ double red[kPPWaves];
     __shared__ __attribute__((aligned(16))) T sx[2][kPPR][kPPLdsRow];
