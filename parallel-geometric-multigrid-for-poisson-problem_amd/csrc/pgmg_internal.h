@@ -30,6 +30,27 @@ int tuning_int(const char *name, int dflt);
 inline int tuning_int(const char *, int dflt) { return dflt; }
 #endif
 
+// The smoother's early exit is sqrt(s) < eps for s = sum of r^2 (Smoother.hpp:77-80).
+// sqrt is correctly rounded and monotonic, so for s >= 0 (and NaN) the test equals s < T
+// with T = the smallest double whose square root is >= eps: the latency-bound kernels test
+// that instead of computing a square root on the dependent chain of every sweep.
+inline double norm2_threshold(double eps)
+{
+    if (!(eps > 0.0)) return 0.0;                       // never fires (eps <= 0 or NaN)
+    if (__builtin_isinf(eps)) return __builtin_inf();   // fires for every finite s
+    unsigned long long lo = 0, hi = 0x7FF0000000000000ULL;  // sqrt(0) < eps <= sqrt(inf)
+    while (hi - lo > 1) {
+        const unsigned long long mid = lo + (hi - lo) / 2;
+        double m;
+        __builtin_memcpy(&m, &mid, 8);
+        if (__builtin_sqrt(m) >= eps) hi = mid;
+        else lo = mid;
+    }
+    double t;
+    __builtin_memcpy(&t, &hi, 8);
+    return t;
+}
+
 // one early-exit check recorded by a speculative call: the producing pass's per-block
 // partial sums of r^2 (see pgmg_ctx.hip, "speculative calls")
 struct CheckRef {

@@ -25,6 +25,11 @@ constexpr bool kTailSmallOff = false;          // (compile with -DPGMG_TAIL_SMAL
 constexpr bool kTailSmallOff = true;
 #endif
 
+#ifndef PGMG_TAIL_W9
+#define PGMG_TAIL_W9 1   // the 9x9 + 5x5 pair of levels by tail_w9 (0: the generic wave loop)
+#endif
+constexpr bool kTailW9 = PGMG_TAIL_W9 != 0;
+
 template <class Real>
 struct TailLevel {
     int N;
@@ -40,6 +45,7 @@ struct TailArgsDev {
     int S;           // elements per pyramid
     TailLevel<Real> lv[kTailMaxLevels];
     int gamma;
+    double eps2;     // the early-exit test sqrt(s) < eps as s < eps2 (norm2_threshold)
     int wave_n;      // levels with N <= wave_n run on wave 0 alone (no workgroup barriers)
     // measurement (PGMG_TAIL_PROF=1, pgmg_tail_prof): thread 0 adds shader-clock cycles
     // [0] wave-team hand-offs, [1] block smooth, [2] block res+restrict, [3] block
@@ -48,6 +54,18 @@ struct TailArgsDev {
 };
 
 __device__ __forceinline__ unsigned long long tail_clock() { return __builtin_amdgcn_s_memtime(); }
+
+// sweeps and early exits, returned by value up the call chain (counters passed by reference
+// ended up in scratch memory: a load + store on the dependent chain of every sweep)
+struct Cnt {
+    int sweeps = 0, exits = 0;
+    __device__ Cnt &operator+=(const Cnt &o)
+    {
+        sweeps += o.sweeps;
+        exits += o.exits;
+        return *this;
+    }
+};
 
 // Two execution teams for the same level code.  BlockTeam: the whole 1024-thread
 // workgroup, stages separated by __syncthreads.  WaveTeam: wave 0 alone; LDS operations
@@ -124,9 +142,10 @@ __device__ __forceinline__ double tail_jacobi(const Real *cur, Real *out, const 
 // when it fires, the lane's register copy of x_k written back — no scratch grid, no
 // boundary lanes, no copy pass.  Same expressions and operand order as tail_jacobi.
 template <int PP, class Real>
-__device__ void tail_smooth_small(Real *x, const Real *f, const TailLevel<Real> &L, int num_iter,
-                                  double eps, long long &sweeps, long long &exits)
+__device__ __forceinline__ Cnt tail_smooth_small(Real *x, const Real *f, const TailLevel<Real> &L,
+                                                 int num_iter, double eps)
 {
+    int sweeps = 0, exits = 0;
     // PP interior points per lane: point q of lane t is interior index t + 64 q
     const int N = L.N, m = N - 2, nin = m * m;
     const int lane = threadIdx.x & 63;
@@ -182,37 +201,36 @@ __device__ void tail_smooth_small(Real *x, const Real *f, const TailLevel<Real> 
             if (act[q]) x[k[q]] = nx[q];
         fence();
         const double s = wave_sum(acc);
-        if (sqrt(s) < eps) {   // x_{it-1} is the result: the speculative sweep is undone
+        if (s < eps) {   // x_{it-1} is the result: the speculative sweep is undone
             #pragma unroll
             for (int q = 0; q < PP; ++q)
                 if (act[q]) x[k[q]] = xc[q];
             fence();
             ++exits;
-            return;
+            return Cnt{sweeps, exits};
         }
         #pragma unroll
         for (int q = 0; q < PP; ++q) xc[q] = nx[q];
         ++sweeps;
     }
+    return Cnt{sweeps, exits};
 }
 
 // JacobiSmoother::smooth(x, f, N, N, h, num_iter): num_iter+1 sweeps, break as
-// soon as ||r(x_k)|| < eps.  The check of x_k is fused into sweep k+1 (which
+// soon as ||r(x_k)|| < eps, tested as sum r^2 < eps2 = norm2_threshold(eps) (no sqrt on
+// the dependent chain of every sweep; the same decisions, see pgmg_internal.h).  The check of x_k is fused into sweep k+1 (which
 // reads the same neighbourhood); when it fires, sweep k+1's output is dropped.
 template <class Team, class Real>
-__device__ void tail_smooth(Real *x, const Real *f, const TailLevel<Real> &L, int num_iter,
-                            double eps, Real *T, double *red, int &par, long long &sweeps,
-                            long long &exits)
+__device__ __forceinline__ Cnt tail_smooth(Real *x, const Real *f, const TailLevel<Real> &L,
+                                           int num_iter, double eps, Real *T, double *red, int &par)
 {
     if constexpr (Team::size == 64) {
         const int nin = (L.N - 2) * (L.N - 2);
-        if (!kTailSmallOff && nin <= 64) {
-            tail_smooth_small<1>(x, f, L, num_iter, eps, sweeps, exits);
-            return;
-        }
+        if (!kTailSmallOff && nin <= 64) return tail_smooth_small<1>(x, f, L, num_iter, eps);
         // (tail_smooth_small<4> for N = 17 on the wave team measured no faster than the
         // block team there: W at 4097 5.98 vs 5.99 /s, wave_n 17 vs 9)
     }
+    int sweeps = 0, exits = 0;
     Real *cur = x, *oth = T;
     tail_jacobi<Team, Real, false>(cur, oth, f, L);
     Team::sync();
@@ -224,7 +242,7 @@ __device__ void tail_smooth(Real *x, const Real *f, const TailLevel<Real> &L, in
         const double acc = tail_jacobi<Team, Real, true>(cur, oth, f, L);
         const double s = Team::sum(acc, red, par);   // also orders the writes of oth
         if (Team::size != kTailThreads) Team::sync();  // (the block sum has its barrier)
-        if (sqrt(s) < eps) {
+        if (s < eps) {
             ++exits;
             break;
         }
@@ -238,6 +256,7 @@ __device__ void tail_smooth(Real *x, const Real *f, const TailLevel<Real> &L, in
         for (int k = Team::tid(); k < n; k += Team::size) x[k] = cur[k];
     }
     Team::sync();
+    return Cnt{sweeps, exits};
 }
 
 // interior point p of an m x m interior (lane p of the wave team): its flat index
@@ -250,7 +269,7 @@ __device__ __forceinline__ int tail_small_index(int p, int m, int N)
 
 // T = r(x) on the interior, 0 on the boundary; then fc = R T (MultiGrid.hpp:70-78)
 template <class Team, class Real>
-__device__ void tail_res_restrict(const Real *x, const Real *f, const TailLevel<Real> &Lf, Real *fc,
+__device__ __forceinline__ void tail_res_restrict(const Real *x, const Real *f, const TailLevel<Real> &Lf, Real *fc,
                                   Real *ec, const TailLevel<Real> &Lc, Real *T)
 {
     if constexpr (Team::size == 64) {
@@ -305,7 +324,7 @@ __device__ void tail_res_restrict(const Real *x, const Real *f, const TailLevel<
 
 // x += P e (MultiGrid.hpp:208-226): fine points in [2, Nf-2]^2 only
 template <class Team, class Real>
-__device__ void tail_prolong(Real *x, const TailLevel<Real> &Lf, const Real *e,
+__device__ __forceinline__ void tail_prolong(Real *x, const TailLevel<Real> &Lf, const Real *e,
                              const TailLevel<Real> &Lc)
 {
     const int N = Lf.N, Nc = Lc.N, n = N * N;
@@ -342,17 +361,145 @@ __device__ void tail_prolong(Real *x, const TailLevel<Real> &Lf, const Real *e,
     Team::sync();
 }
 
+// DPP lane moves inside 16-lane rows for the 5x5 coarsest grid (row_shl:n = 0x100 + n,
+// row_shr:n = 0x110 + n; lanes without a source read 0)
+template <int CTRL> __device__ __forceinline__ double dpp_row(double v) { return dpp64<CTRL>(v); }
+template <int CTRL> __device__ __forceinline__ float dpp_row(float v)
+{
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+
+// The coarsest solve (JacobiSmoother::smooth with coarse_iter, Smoother.hpp:38-116) of a 5x5
+// level held in registers: lane q < 9 owns interior point (1 + q/3, 1 + q%3), the other
+// lanes hold 0 (the Dirichlet boundary); left/right/up/down neighbours are DPP moves by
+// 1 and 3 lanes inside DPP row 0 (no LDS round trip per sweep).  Same expressions, operand
+// order and fused speculative check as tail_smooth_small; the check's sum over lanes 0..8
+// is the same row scan wave_sum does, so the decisions are identical.
+template <class Real>
+__device__ __forceinline__ Cnt tail_coarse5_regs(Real &x, Real f, const TailLevel<Real> &L,
+                                                 int num_iter, double eps2)
+{
+    const int lane = threadIdx.x & 63;
+    const bool act = lane < 9;
+    const int ii = lane - 3 * (lane / 3);
+    const Real hh = L.hh, ih = L.ih, hf = hh * f;
+    auto nbrs = [&](Real v, Real &l, Real &r, Real &u, Real &dn) {
+        l = dpp_row<0x111>(v);   // row_shr:1: lane q-1
+        r = dpp_row<0x101>(v);   // row_shl:1: lane q+1
+        u = dpp_row<0x113>(v);   // row_shr:3: lane q-3 (lanes 0..2: 0)
+        dn = dpp_row<0x103>(v);  // row_shl:3: lane q+3 (lanes 6..8 read lanes 9..11 = 0)
+        if (ii == 0) l = Real(0);
+        if (ii == 2) r = Real(0);
+    };
+    int sweeps = 0, exits = 0;
+    {
+        Real l, r, u, dn;
+        nbrs(x, l, r, u, dn);
+        const Real nx = Real(0.25) * (hf + l + r + u + dn);
+        x = act ? nx : Real(0);
+        ++sweeps;
+    }
+    for (int it = 2; it <= num_iter + 1; ++it) {
+        Real l, r, u, dn;
+        nbrs(x, l, r, u, dn);
+        const Real res = f - ih * (Real(4) * x - l - r - u - dn);
+        double acc = act ? sq(res) : 0.0;
+        const Real nx = Real(0.25) * (hf + l + r + u + dn);
+        acc += dpp64<0x111>(acc);   // row_shr:1,2,4,8: lane 15 holds the total of row 0
+        acc += dpp64<0x112>(acc);
+        acc += dpp64<0x114>(acc);
+        acc += dpp64<0x118>(acc);
+        const double s = readlane64(acc, 15);
+        if (s < eps2) {   // x_{it-1} is the result: the speculative sweep is dropped
+            ++exits;
+            break;
+        }
+        x = act ? nx : Real(0);
+        ++sweeps;
+    }
+    return Cnt{sweeps, exits};
+}
+
+// `reps` gamma-cycles of a 9x9 level whose coarser level is the 5x5 coarsest one, on wave 0:
+// smoothing of the 9x9 level in LDS (tail_smooth_small), its residual and full-weighting
+// restriction straight into the coarse lanes' registers, the gamma coarsest solves in
+// registers (tail_coarse5_regs), the prolongation from one LDS copy of the correction.
+// Replaces, for this (most visited) pair of levels of a W-cycle, the generic loop's
+// per-stage LDS grids and index arithmetic.  MultiGrid.hpp:57-136 semantics.
+template <class Real>
+__device__ __forceinline__ Cnt tail_w9(const TailArgsDev<Real> &d, int l, int reps, Real *E,
+                                       Real *F, Real *T)
+{
+    const TailArgsT<Real> &a = d.a;
+    const TailLevel<Real> &L9 = d.lv[l], &L5 = d.lv[l + 1];
+    Real *x9 = E + L9.off;
+    const Real *f9 = F + L9.off;
+    Real *e5 = E + L5.off;
+    const int lane = threadIdx.x & 63;
+    const int jj = lane / 7, ii = lane - 7 * jj;
+    const bool in9 = lane < 49;
+    const int k9 = in9 ? (1 + jj) * 9 + 1 + ii : 10;
+    // coarse lane q < 9: (jc, ic) = (1 + q/3, 1 + q%3), fine centre (2jc, 2ic)
+    const int jc = 1 + lane / 3, ic = 1 + lane - 3 * (lane / 3);
+    const int kc = lane < 9 ? (2 * jc) * 9 + 2 * ic : 20;
+    auto fence = [] {
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __builtin_amdgcn_wave_barrier();
+    };
+    Cnt cnt;
+    for (int v = 0; v < reps; ++v) {
+        cnt += tail_smooth_small<1>(x9, f9, L9, a.v1, d.eps2);
+        // r = f - A x on the interior (DynamicGridUtils.hpp:59-69), into T
+        if (in9)
+            T[k9] = f9[k9] - L9.ih * (Real(4) * x9[k9] - x9[k9 - 1] - x9[k9 + 1] - x9[k9 - 9] - x9[k9 + 9]);
+        fence();
+        // rc = R r (MultiGrid.hpp:187-205); e_coarse = 0 (:81-82)
+        Real fc = Real(0), ec = Real(0);
+        if (lane < 9)
+            fc = Real(0.25) * T[kc] + Real(0.125) * (T[kc + 1] + T[kc - 1] + T[kc + 9] + T[kc - 9]) +
+                 Real(0.0625) * (T[kc - 9 - 1] + T[kc - 9 + 1] + T[kc + 9 - 1] + T[kc + 9 + 1]);
+        for (int g = 0; g < d.gamma; ++g)
+            cnt += tail_coarse5_regs(ec, fc, L5, a.coarse_iter, d.eps2);
+        // the correction into LDS (5x5, boundary 0), then x += P e on [2, 7]^2 (:208-226)
+        if (lane < 25) e5[lane] = Real(0);
+        fence();
+        if (lane < 9) e5[jc * 5 + ic] = ec;
+        fence();
+        const int j = 1 + jj, i = 1 + ii;
+        if (in9 && j >= 2 && i >= 2 && j <= 7 && i <= 7) {
+            const int cj = j >> 1, ci = i >> 1;
+            const Real *C0 = e5 + cj * 5;
+            Real w;
+            if ((j & 1) == 0) {
+                w = ((i & 1) == 0) ? C0[ci] : Real(0.5) * (C0[ci] + C0[ci + 1]);
+            } else {
+                const Real *C1 = C0 + 5;
+                w = ((i & 1) == 0) ? Real(0.5) * (C0[ci] + C1[ci])
+                                   : Real(0.25) * (C0[ci] + C0[ci + 1] + C1[ci] + C1[ci + 1]);
+            }
+            x9[k9] = x9[k9] + w;
+        }
+        fence();
+        cnt += tail_smooth_small<1>(x9, f9, L9, a.v2, d.eps2);
+    }
+    return cnt;
+}
+
 // `reps` gamma-cycles (MultiGrid.hpp:57-136) whose top is tail level `top`; levels
 // top .. last.  A BlockTeam hands every sub-hierarchy whose top has N <= wave_n to wave 0
 // (all gamma visits of it at once) and waits at a barrier.
 template <class Team, class Real>
-__device__ void tail_gcycle(const TailArgsDev<Real> &d, int top, int reps, Real *E, Real *F,
-                            Real *T, double *red, int &par, long long &sweeps, long long &exits)
+__device__ __forceinline__ Cnt tail_gcycle(const TailArgsDev<Real> &d, int top, int reps, Real *E,
+                                           Real *F, Real *T, double *red, int &par)
 {
+    Cnt cnt;
     constexpr bool kBlock = Team::size == kTailThreads;
     const TailArgsT<Real> &a = d.a;
-    int visits[kTailMaxLevels];
-    for (int i = 0; i < kTailMaxLevels; ++i) visits[i] = 0;
+    // visit counts per level, 4 bits each in one register (a dynamically indexed array
+    // would live in scratch memory)
+    unsigned visits = 0;
+    auto vget = [&](int i) { return (int)((visits >> (4 * i)) & 15u); };
+    auto vset = [&](int i, int v) { visits = (visits & ~(15u << (4 * i))) | ((unsigned)v << (4 * i)); };
     int l = top, done = 0;
     bool descending = true;
     const int last = d.nl - 1;
@@ -361,24 +508,28 @@ __device__ void tail_gcycle(const TailArgsDev<Real> &d, int top, int reps, Real 
             if (kBlock && l != top && d.lv[l].N <= d.wave_n) {
                 // the whole gamma-recursion of level l on wave 0
                 const unsigned long long c0 = d.prof ? tail_clock() : 0;
-                if (threadIdx.x < 64)
-                    tail_gcycle<WaveTeam, Real>(d, l, d.gamma, E, F, T, red, par, sweeps, exits);
+                if (threadIdx.x < 64) {
+                    if (kTailW9 && d.lv[l].N == 9 && l + 1 == last && d.lv[l + 1].N == 5)
+                        cnt += tail_w9<Real>(d, l, d.gamma, E, F, T);
+                    else
+                        cnt += tail_gcycle<WaveTeam, Real>(d, l, d.gamma, E, F, T, red, par);
+                }
                 __syncthreads();
                 if (d.prof && threadIdx.x == 0) d.prof[0] += tail_clock() - c0;
-                visits[l] = d.gamma - 1;
+                vset(l, d.gamma - 1);
                 descending = false;
                 continue;
             }
             const int pi = kBlock ? 1 : 6, pr = kBlock ? 2 : 7;
             unsigned long long c0 = d.prof ? tail_clock() : 0;
             if (l == last) {
-                tail_smooth<Team>(E + d.lv[l].off, F + d.lv[l].off, d.lv[l], a.coarse_iter, a.eps, T,
-                                  red, par, sweeps, exits);
+                cnt += tail_smooth<Team>(E + d.lv[l].off, F + d.lv[l].off, d.lv[l], a.coarse_iter,
+                                         d.eps2, T, red, par);
                 if (d.prof && threadIdx.x == 0) d.prof[pi] += tail_clock() - c0;
                 descending = false;
             } else {
-                tail_smooth<Team>(E + d.lv[l].off, F + d.lv[l].off, d.lv[l], a.v1, a.eps, T, red,
-                                  par, sweeps, exits);
+                cnt += tail_smooth<Team>(E + d.lv[l].off, F + d.lv[l].off, d.lv[l], a.v1, d.eps2, T,
+                                         red, par);
                 if (d.prof && threadIdx.x == 0) {
                     const unsigned long long c1 = tail_clock();
                     d.prof[pi] += c1 - c0;
@@ -387,7 +538,7 @@ __device__ void tail_gcycle(const TailArgsDev<Real> &d, int top, int reps, Real 
                 tail_res_restrict<Team>(E + d.lv[l].off, F + d.lv[l].off, d.lv[l],
                                         F + d.lv[l + 1].off, E + d.lv[l + 1].off, d.lv[l + 1], T);
                 if (d.prof && threadIdx.x == 0) d.prof[pr] += tail_clock() - c0;
-                visits[l + 1] = 0;
+                vset(l + 1, 0);
                 ++l;
             }
         } else {
@@ -399,7 +550,8 @@ __device__ void tail_gcycle(const TailArgsDev<Real> &d, int top, int reps, Real 
                 break;
             }
             const int p = l - 1;
-            if (++visits[l] < d.gamma) {
+            vset(l, vget(l) + 1);
+            if (vget(l) < d.gamma) {
                 descending = true;   // call the cycle on level l again
             } else {
                 const int pi = kBlock ? 1 : 6, pr = kBlock ? 3 : 7;
@@ -410,13 +562,14 @@ __device__ void tail_gcycle(const TailArgsDev<Real> &d, int top, int reps, Real 
                     d.prof[pr] += c1 - c0;
                     c0 = c1;
                 }
-                tail_smooth<Team>(E + d.lv[p].off, F + d.lv[p].off, d.lv[p], a.v2, a.eps, T, red,
-                                  par, sweeps, exits);
+                cnt += tail_smooth<Team>(E + d.lv[p].off, F + d.lv[p].off, d.lv[p], a.v2, d.eps2, T,
+                                         red, par);
                 if (d.prof && threadIdx.x == 0) d.prof[pi] += tail_clock() - c0;
                 l = p;
             }
         }
     }
+    return cnt;
 }
 
 // analytic right-hand side of tail level t from host sine tables (DynamicGridUtils.hpp:111-124)
@@ -479,11 +632,11 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(TailArgsDev<Real> d)
     }
     __syncthreads();
 
-    long long sweeps = 0, exits = 0;
+    Cnt cnt;   // sweeps and exits of this launch (< 2^31)
     int par = 0;
     const int last = d.nl - 1;
     if (!a.fmg) {
-        tail_gcycle<BlockTeam>(d, 0, 1, E, F, T, red, par, sweeps, exits);
+        cnt += tail_gcycle<BlockTeam>(d, 0, 1, E, F, T, red, par);
     } else {
         // compute_coarsest_grid: restrict phi down to the coarsest level
         for (int t = 0; t < last; ++t)
@@ -497,12 +650,12 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(TailArgsDev<Real> d)
                 for (int k = threadIdx.x; k < n; k += kTailThreads) Et[k] = Real(0);
                 __syncthreads();
                 tail_prolong<BlockTeam>(Et, d.lv[t], E + d.lv[t + 1].off, d.lv[t + 1]);   // :164
-                tail_gcycle<BlockTeam>(d, t, 1, E, F, T, red, par, sweeps, exits);  // :167 v_cycle
+                cnt += tail_gcycle<BlockTeam>(d, t, 1, E, F, T, red, par);  // :167 v_cycle
             } else {
                 __syncthreads();
             }
             if (t > 0 || a.fmg_smooth_top)                                   // :153 smooth(3)
-                tail_smooth<BlockTeam>(Et, Ft, d.lv[t], 3, a.eps, T, red, par, sweeps, exits);
+                cnt += tail_smooth<BlockTeam>(Et, Ft, d.lv[t], 3, d.eps2, T, red, par);
         }
     }
 
@@ -516,8 +669,8 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(TailArgsDev<Real> d)
         }
     }
     if (threadIdx.x == 0 && a.stats != nullptr) {
-        atomicAdd(&a.stats[0], (unsigned long long)sweeps);
-        atomicAdd(&a.stats[1], (unsigned long long)exits);
+        atomicAdd(&a.stats[0], (unsigned long long)cnt.sweeps);
+        atomicAdd(&a.stats[1], (unsigned long long)cnt.exits);
     }
     if (d.prof && threadIdx.x == 0) {
         d.prof[4] += tail_clock() - k0;
@@ -559,6 +712,7 @@ hipError_t launch_tail_gamma(const TailArgsT<Real> &a, int gamma, hipStream_t s)
     TailArgsDev<Real> d;
     d.a = a;
     d.gamma = gamma;
+    d.eps2 = norm2_threshold(a.eps);
     int N = a.N_top;
     double h = a.h_top;
     int off = 0, nl = 0;

@@ -26,15 +26,18 @@ import torch  # noqa
 import _pkgload
 pg = _pkgload.load()
 N = %(n)d
+K = %(steps)d
 with pg.Solver(N, flags=pg.PGMG_FLAG_TIME_FINE) as s:
     s.set_problem()
-    s.vcycle(2); s.sync()
+    run = {"V": s.vcycle, "W": s.wcycle, "F": s.fcycle}[%(kind)r]
+    run(2); s.sync()
     for w in range(4): s.fine_pass_time(w)
-    t0 = time.perf_counter(); s.vcycle(20); s.sync(); t1 = time.perf_counter()
+    t0 = time.perf_counter(); run(K); s.sync(); t1 = time.perf_counter()
     r = {w: s.fine_pass_time(w) for w in range(4)}
     h = s.solution_hash(0)
-print(json.dumps({"ms_cycle": (t1 - t0) * 1e3 / 20, "pp": r[3][1], "pre": r[1][1],
-                  "post": r[2][1], "hash": h}))
+    st = s.stats()
+print(json.dumps({"ms_cycle": (t1 - t0) * 1e3 / K, "pp": r[3][1], "pre": r[1][1],
+                  "post": r[2][1], "hash": h, "sweeps": st[0]}))
 """
 
 
@@ -42,12 +45,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=16385)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--kind", default="V")
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     want = None
     for c in json.loads((ROOT / "tests" / "golden" / "cycles.json").read_text()):
-        if c["kind"] == "V" and c["N"] == a.n and c["eps"] == 1e-7 and len(c["cycles"]) >= 22:
-            want = c["cycles"][21]["hash"]
+        if c["kind"] == a.kind and c["N"] == a.n and c["eps"] == 1e-7 and len(c["cycles"]) >= 2 + a.steps:
+            want = c["cycles"][1 + a.steps]["hash"]
     vs = []
     for v in a.variants:
         name, rest = v.split("=", 1)
@@ -60,7 +65,7 @@ def main():
             e.update(env)
             if lib:
                 e["PGMG_LIB"] = str((ROOT / lib).resolve())
-            out = subprocess.run([sys.executable, "-c", CHILD % {"root": str(ROOT), "n": a.n}],
+            out = subprocess.run([sys.executable, "-c", CHILD % {"root": str(ROOT), "n": a.n, "kind": a.kind, "steps": a.steps}],
                                  env=e, capture_output=True, text=True, timeout=300)
             line = next((l for l in out.stdout.splitlines() if l.startswith("{")), None)
             if line is None:
