@@ -382,41 +382,49 @@ __device__ __forceinline__ Cnt tail_coarse5_regs(Real &x, Real f, const TailLeve
     const int lane = threadIdx.x & 63;
     const bool act = lane < 9;
     const int ii = lane - 3 * (lane / 3);
+    const bool has_l = ii != 0, has_r = ii != 2;
     const Real hh = L.hh, ih = L.ih, hf = hh * f;
-    auto nbrs = [&](Real v, Real &l, Real &r, Real &u, Real &dn) {
-        l = dpp_row<0x111>(v);   // row_shr:1: lane q-1
-        r = dpp_row<0x101>(v);   // row_shl:1: lane q+1
-        u = dpp_row<0x113>(v);   // row_shr:3: lane q-3 (lanes 0..2: 0)
-        dn = dpp_row<0x103>(v);  // row_shl:3: lane q+3 (lanes 6..8 read lanes 9..11 = 0)
-        if (ii == 0) l = Real(0);
-        if (ii == 2) r = Real(0);
+    Real xv = x;
+    int sweeps = 1, exits = 0;
+    // the four moves with every lane active (a DPP move under an exec mask reads 0 from
+    // the disabled source lanes, so none may be sunk into the has_l / has_r selects)
+    auto nbrs = [&](Real v, Real *o) {
+        o[0] = dpp_row<0x111>(v);   // row_shr:1: lane q-1
+        o[1] = dpp_row<0x101>(v);   // row_shl:1: lane q+1
+        o[2] = dpp_row<0x113>(v);   // row_shr:3: lane q-3 (lanes 0..2: 0)
+        o[3] = dpp_row<0x103>(v);   // row_shl:3: lane q+3 (lanes 9..11 hold 0)
+        __asm__ volatile("" : "+v"(o[0]), "+v"(o[1]), "+v"(o[2]), "+v"(o[3]));
+        if (!has_l) o[0] = Real(0);
+        if (!has_r) o[1] = Real(0);
     };
-    int sweeps = 0, exits = 0;
     {
-        Real l, r, u, dn;
-        nbrs(x, l, r, u, dn);
+        Real o[4];
+        nbrs(xv, o);
+        const Real l = o[0], r = o[1], u = o[2], dn = o[3];
         const Real nx = Real(0.25) * (hf + l + r + u + dn);
-        x = act ? nx : Real(0);
-        ++sweeps;
+        xv = act ? nx : Real(0);
     }
     for (int it = 2; it <= num_iter + 1; ++it) {
-        Real l, r, u, dn;
-        nbrs(x, l, r, u, dn);
-        const Real res = f - ih * (Real(4) * x - l - r - u - dn);
+        Real o[4];
+        nbrs(xv, o);
+        const Real l = o[0], r = o[1], u = o[2], dn = o[3];
+        const Real res = f - ih * (Real(4) * xv - l - r - u - dn);
         double acc = act ? sq(res) : 0.0;
         const Real nx = Real(0.25) * (hf + l + r + u + dn);
         acc += dpp64<0x111>(acc);   // row_shr:1,2,4,8: lane 15 holds the total of row 0
         acc += dpp64<0x112>(acc);
         acc += dpp64<0x114>(acc);
         acc += dpp64<0x118>(acc);
+        // wave-uniform: the decision of every lane
         const double s = readlane64(acc, 15);
         if (s < eps2) {   // x_{it-1} is the result: the speculative sweep is dropped
-            ++exits;
+            exits = 1;
             break;
         }
-        x = act ? nx : Real(0);
+        xv = act ? nx : Real(0);
         ++sweeps;
     }
+    x = xv;
     return Cnt{sweeps, exits};
 }
 
@@ -446,12 +454,43 @@ __device__ __forceinline__ Cnt tail_w9(const TailArgsDev<Real> &d, int l, int re
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         __builtin_amdgcn_wave_barrier();
     };
+    const Real hh = L9.hh, ih = L9.ih;
+    const Real fk = f9[k9], hf = hh * fk;
+    Real x = x9[k9];   // this lane's point; LDS x9 always holds every lane's current value
+    // JacobiSmoother::smooth on the 9x9 level with the iterate in registers: sweeps in place
+    // (the wave's reads of the old neighbours precede its writes), the check of x_k fused
+    // into sweep k+1 and undone from the register copy when it fires (tail_smooth_small)
+    auto smooth = [&](int num_iter, Cnt &c) {
+        Real nx = Real(0.25) * (hf + x9[k9 - 1] + x9[k9 + 1] + x9[k9 - 9] + x9[k9 + 9]);
+        fence();
+        if (in9) x9[k9] = nx;
+        fence();
+        x = nx;
+        ++c.sweeps;
+        for (int it = 2; it <= num_iter + 1; ++it) {
+            const Real l0 = x9[k9 - 1], r0 = x9[k9 + 1], u0 = x9[k9 - 9], d0 = x9[k9 + 9];
+            const Real res = fk - ih * (Real(4) * x - l0 - r0 - u0 - d0);
+            const double acc = in9 ? sq(res) : 0.0;
+            nx = Real(0.25) * (hf + l0 + r0 + u0 + d0);
+            fence();
+            if (in9) x9[k9] = nx;
+            fence();
+            const double s = wave_sum(acc);
+            if (s < d.eps2) {   // x_{it-1} is the result
+                if (in9) x9[k9] = x;
+                fence();
+                ++c.exits;
+                return;
+            }
+            x = nx;
+            ++c.sweeps;
+        }
+    };
     Cnt cnt;
     for (int v = 0; v < reps; ++v) {
-        cnt += tail_smooth_small<1>(x9, f9, L9, a.v1, d.eps2);
+        smooth(a.v1, cnt);
         // r = f - A x on the interior (DynamicGridUtils.hpp:59-69), into T
-        if (in9)
-            T[k9] = f9[k9] - L9.ih * (Real(4) * x9[k9] - x9[k9 - 1] - x9[k9 + 1] - x9[k9 - 9] - x9[k9 + 9]);
+        if (in9) T[k9] = fk - ih * (Real(4) * x - x9[k9 - 1] - x9[k9 + 1] - x9[k9 - 9] - x9[k9 + 9]);
         fence();
         // rc = R r (MultiGrid.hpp:187-205); e_coarse = 0 (:81-82)
         Real fc = Real(0), ec = Real(0);
@@ -477,10 +516,11 @@ __device__ __forceinline__ Cnt tail_w9(const TailArgsDev<Real> &d, int l, int re
                 w = ((i & 1) == 0) ? Real(0.5) * (C0[ci] + C1[ci])
                                    : Real(0.25) * (C0[ci] + C0[ci + 1] + C1[ci] + C1[ci + 1]);
             }
-            x9[k9] = x9[k9] + w;
+            x = x + w;
+            x9[k9] = x;
         }
         fence();
-        cnt += tail_smooth_small<1>(x9, f9, L9, a.v2, d.eps2);
+        smooth(a.v2, cnt);
     }
     return cnt;
 }
@@ -517,6 +557,13 @@ __device__ __forceinline__ Cnt tail_gcycle(const TailArgsDev<Real> &d, int top, 
                 __syncthreads();
                 if (d.prof && threadIdx.x == 0) d.prof[0] += tail_clock() - c0;
                 vset(l, d.gamma - 1);
+                descending = false;
+                continue;
+            }
+            if (!kBlock && kTailW9 && l != top && d.lv[l].N == 9 && l + 1 == last &&
+                d.lv[l + 1].N == 5) {
+                // one visit of the 9x9 level (inside a sub-hierarchy handed to wave 0)
+                cnt += tail_w9<Real>(d, l, 1, E, F, T);
                 descending = false;
                 continue;
             }
