@@ -67,7 +67,7 @@ constexpr int kPostExt = 4;       // row strips: k_post of a level below the fin
                                   // edge (bitwise what the neighbour computes), so the
                                   // coarse correction needs no halo exchange
 constexpr int kBlock = 256;       // threads per block for streaming kernels (4 waves)
-constexpr int kTailThreads = 1024;
+constexpr int kTailThreads = 512;   // 8 waves: 256 VGPRs a lane for the wave-0 paths (tail_w9, tail_w17)
 constexpr int kTailMaxN = 65;     // largest level the LDS-resident tail holds
 
 inline int pitch_for(int N) { return (N + 15) / 16 * 16; }

@@ -29,6 +29,10 @@ constexpr bool kTailSmallOff = true;
 #define PGMG_TAIL_W9 1   // the 9x9 + 5x5 pair of levels by tail_w9 (0: the generic wave loop)
 #endif
 constexpr bool kTailW9 = PGMG_TAIL_W9 != 0;
+#ifndef PGMG_TAIL_W17
+#define PGMG_TAIL_W17 1  // the 17x17 level and below by tail_w17 on wave 0
+#endif
+constexpr bool kTailW17 = PGMG_TAIL_W17 != 0 && kTailW9;
 
 template <class Real>
 struct TailLevel {
@@ -376,7 +380,7 @@ template <int CTRL> __device__ __forceinline__ float dpp_row(float v)
 // order and fused speculative check as tail_smooth_small; the check's sum over lanes 0..8
 // is the same row scan wave_sum does, so the decisions are identical.
 template <class Real>
-__device__ __forceinline__ Cnt tail_coarse5_regs(Real &x, Real f, const TailLevel<Real> &L,
+__device__ __forceinline__ Cnt tail_coarse5_regs(Real &x, Real f, const TailLevel<Real> L,
                                                  int num_iter, double eps2)
 {
     const int lane = threadIdx.x & 63;
@@ -388,7 +392,7 @@ __device__ __forceinline__ Cnt tail_coarse5_regs(Real &x, Real f, const TailLeve
     int sweeps = 1, exits = 0;
     // the four moves with every lane active (a DPP move under an exec mask reads 0 from
     // the disabled source lanes, so none may be sunk into the has_l / has_r selects)
-    auto nbrs = [&](Real v, Real *o) {
+    auto nbrs = [&](Real v, Real *o) __attribute__((always_inline)) {
         o[0] = dpp_row<0x111>(v);   // row_shr:1: lane q-1
         o[1] = dpp_row<0x101>(v);   // row_shl:1: lane q+1
         o[2] = dpp_row<0x113>(v);   // row_shr:3: lane q-3 (lanes 0..2: 0)
@@ -439,7 +443,7 @@ __device__ __forceinline__ Cnt tail_w9(const TailArgsDev<Real> &d, int l, int re
                                        Real *F, Real *T)
 {
     const TailArgsT<Real> &a = d.a;
-    const TailLevel<Real> &L9 = d.lv[l], &L5 = d.lv[l + 1];
+    const TailLevel<Real> L9 = d.lv[l], L5 = d.lv[l + 1];   // by value: scalar registers
     Real *x9 = E + L9.off;
     const Real *f9 = F + L9.off;
     Real *e5 = E + L5.off;
@@ -450,6 +454,8 @@ __device__ __forceinline__ Cnt tail_w9(const TailArgsDev<Real> &d, int l, int re
     // coarse lane q < 9: (jc, ic) = (1 + q/3, 1 + q%3), fine centre (2jc, 2ic)
     const int jc = 1 + lane / 3, ic = 1 + lane - 3 * (lane / 3);
     const int kc = lane < 9 ? (2 * jc) * 9 + 2 * ic : 20;
+    const double eps2 = d.eps2;
+    const int gamma = d.gamma;
     auto fence = [] {
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         __builtin_amdgcn_wave_barrier();
@@ -460,7 +466,7 @@ __device__ __forceinline__ Cnt tail_w9(const TailArgsDev<Real> &d, int l, int re
     // JacobiSmoother::smooth on the 9x9 level with the iterate in registers: sweeps in place
     // (the wave's reads of the old neighbours precede its writes), the check of x_k fused
     // into sweep k+1 and undone from the register copy when it fires (tail_smooth_small)
-    auto smooth = [&](int num_iter, Cnt &c) {
+    auto smooth = [&](int num_iter, Cnt &c) __attribute__((always_inline)) {
         Real nx = Real(0.25) * (hf + x9[k9 - 1] + x9[k9 + 1] + x9[k9 - 9] + x9[k9 + 9]);
         fence();
         if (in9) x9[k9] = nx;
@@ -476,7 +482,7 @@ __device__ __forceinline__ Cnt tail_w9(const TailArgsDev<Real> &d, int l, int re
             if (in9) x9[k9] = nx;
             fence();
             const double s = wave_sum(acc);
-            if (s < d.eps2) {   // x_{it-1} is the result
+            if (s < eps2) {   // x_{it-1} is the result
                 if (in9) x9[k9] = x;
                 fence();
                 ++c.exits;
@@ -497,8 +503,8 @@ __device__ __forceinline__ Cnt tail_w9(const TailArgsDev<Real> &d, int l, int re
         if (lane < 9)
             fc = Real(0.25) * T[kc] + Real(0.125) * (T[kc + 1] + T[kc - 1] + T[kc + 9] + T[kc - 9]) +
                  Real(0.0625) * (T[kc - 9 - 1] + T[kc - 9 + 1] + T[kc + 9 - 1] + T[kc + 9 + 1]);
-        for (int g = 0; g < d.gamma; ++g)
-            cnt += tail_coarse5_regs(ec, fc, L5, a.coarse_iter, d.eps2);
+        for (int g = 0; g < gamma; ++g)
+            cnt += tail_coarse5_regs(ec, fc, L5, a.coarse_iter, eps2);
         // the correction into LDS (5x5, boundary 0), then x += P e on [2, 7]^2 (:208-226)
         if (lane < 25) e5[lane] = Real(0);
         fence();
@@ -518,6 +524,135 @@ __device__ __forceinline__ Cnt tail_w9(const TailArgsDev<Real> &d, int l, int re
             }
             x = x + w;
             x9[k9] = x;
+        }
+        fence();
+        smooth(a.v2, cnt);
+    }
+    return cnt;
+}
+
+// `reps` gamma-cycles of a 17x17 level whose coarser levels are 9x9 and the 5x5 coarsest,
+// on wave 0 (the block team's 16-wave barriers cost more than the work of a 17x17 stage):
+// four interior points per lane with their iterates in registers, flat indices computed
+// once, every stage's LDS reads issued together; the 9x9 sub-hierarchy by tail_w9.
+template <class Real>
+__device__ __forceinline__ Cnt tail_w17(const TailArgsDev<Real> &d, int l, int reps, Real *E,
+                                        Real *F, Real *T)
+{
+    constexpr int Q = 4;   // 225 interior points over 64 lanes
+    const TailArgsT<Real> &a = d.a;
+    const TailLevel<Real> L = d.lv[l], L9 = d.lv[l + 1];   // by value: scalar registers
+    Real *x17 = E + L.off;
+    const Real *f17 = F + L.off;
+    Real *x9 = E + L9.off;
+    Real *f9 = F + L9.off;
+    const int lane = threadIdx.x & 63;
+    const double eps2 = d.eps2;
+    const int gamma = d.gamma;
+    auto fence = [] {
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __builtin_amdgcn_wave_barrier();
+    };
+    int k[Q];
+    bool in[Q];
+    Real x[Q], fk[Q], hf[Q];
+    const Real hh = L.hh, ih = L.ih;
+    #pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int p = lane + 64 * q, jj = p / 15;
+        in[q] = p < 225;
+        k[q] = in[q] ? (1 + jj) * 17 + 1 + (p - 15 * jj) : 18;
+        fk[q] = f17[k[q]];
+        hf[q] = hh * fk[q];
+        x[q] = x17[k[q]];
+    }
+    auto smooth = [&](int num_iter, Cnt &c) __attribute__((always_inline)) {
+        Real nx[Q];
+        #pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int kk = k[q];
+            nx[q] = Real(0.25) * (hf[q] + x17[kk - 1] + x17[kk + 1] + x17[kk - 17] + x17[kk + 17]);
+        }
+        fence();
+        #pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            if (in[q]) x17[k[q]] = nx[q];
+            x[q] = nx[q];
+        }
+        fence();
+        ++c.sweeps;
+        for (int it = 2; it <= num_iter + 1; ++it) {
+            double acc = 0.0;
+            #pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const int kk = k[q];
+                const Real l0 = x17[kk - 1], r0 = x17[kk + 1], u0 = x17[kk - 17], d0 = x17[kk + 17];
+                const Real res = fk[q] - ih * (Real(4) * x[q] - l0 - r0 - u0 - d0);
+                if (in[q]) acc += sq(res);
+                nx[q] = Real(0.25) * (hf[q] + l0 + r0 + u0 + d0);
+            }
+            fence();
+            #pragma unroll
+            for (int q = 0; q < Q; ++q)
+                if (in[q]) x17[k[q]] = nx[q];
+            fence();
+            const double s = wave_sum(acc);
+            if (s < eps2) {   // x_{it-1} is the result
+                #pragma unroll
+                for (int q = 0; q < Q; ++q)
+                    if (in[q]) x17[k[q]] = x[q];
+                fence();
+                ++c.exits;
+                return;
+            }
+            #pragma unroll
+            for (int q = 0; q < Q; ++q) x[q] = nx[q];
+            ++c.sweeps;
+        }
+    };
+    // 9x9 lane p < 49: interior point (1 + p/7, 1 + p%7); fine centre (2j, 2i) of 17x17
+    const int j9 = 1 + lane / 7, i9 = 1 + lane - 7 * (lane / 7);
+    const bool in9 = lane < 49;
+    const int kf = in9 ? (2 * j9) * 17 + 2 * i9 : 36;
+    const int k9 = in9 ? j9 * 9 + i9 : 10;
+    Cnt cnt;
+    for (int v = 0; v < reps; ++v) {
+        smooth(a.v1, cnt);
+        // r = f - A x on the interior into T, then rc = R r straight into the 9x9 level's F
+        // and e_coarse = 0 (MultiGrid.hpp:70-82; its boundary is never written, so stays 0)
+        #pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int kk = k[q];
+            if (in[q])
+                T[kk] = fk[q] - ih * (Real(4) * x[q] - x17[kk - 1] - x17[kk + 1] - x17[kk - 17] - x17[kk + 17]);
+        }
+        fence();
+        if (in9) {
+            f9[k9] = Real(0.25) * T[kf] + Real(0.125) * (T[kf + 1] + T[kf - 1] + T[kf + 17] + T[kf - 17]) +
+                     Real(0.0625) * (T[kf - 17 - 1] + T[kf - 17 + 1] + T[kf + 17 - 1] + T[kf + 17 + 1]);
+            x9[k9] = Real(0);
+        }
+        fence();
+        cnt += tail_w9<Real>(d, l + 1, gamma, E, F, T);
+        // x += P e on fine points [2, 15]^2 (MultiGrid.hpp:208-226)
+        #pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int p = lane + 64 * q, jj = p / 15;
+            const int j = 1 + jj, i = 1 + (p - 15 * jj);
+            if (in[q] && j >= 2 && i >= 2 && j <= 15 && i <= 15) {
+                const int cj = j >> 1, ci = i >> 1;
+                const Real *C0 = x9 + cj * 9;
+                Real w;
+                if ((j & 1) == 0) {
+                    w = ((i & 1) == 0) ? C0[ci] : Real(0.5) * (C0[ci] + C0[ci + 1]);
+                } else {
+                    const Real *C1 = C0 + 9;
+                    w = ((i & 1) == 0) ? Real(0.5) * (C0[ci] + C1[ci])
+                                       : Real(0.25) * (C0[ci] + C0[ci + 1] + C1[ci] + C1[ci + 1]);
+                }
+                x[q] = x[q] + w;
+                x17[k[q]] = x[q];
+            }
         }
         fence();
         smooth(a.v2, cnt);
@@ -545,6 +680,17 @@ __device__ __forceinline__ Cnt tail_gcycle(const TailArgsDev<Real> &d, int top, 
     const int last = d.nl - 1;
     for (;;) {
         if (descending) {
+            if (kBlock && kTailW17 && l != top && d.lv[l].N == 17 && l + 2 == last &&
+                d.lv[l + 1].N == 9 && d.lv[l + 2].N == 5) {
+                // the whole gamma-recursion of the 17x17 level (and below) on wave 0
+                const unsigned long long c0 = d.prof ? tail_clock() : 0;
+                if (threadIdx.x < 64) cnt += tail_w17<Real>(d, l, d.gamma, E, F, T);
+                __syncthreads();
+                if (d.prof && threadIdx.x == 0) d.prof[0] += tail_clock() - c0;
+                vset(l, d.gamma - 1);
+                descending = false;
+                continue;
+            }
             if (kBlock && l != top && d.lv[l].N <= d.wave_n) {
                 // the whole gamma-recursion of level l on wave 0
                 const unsigned long long c0 = d.prof ? tail_clock() : 0;
@@ -621,7 +767,7 @@ __device__ __forceinline__ Cnt tail_gcycle(const TailArgsDev<Real> &d, int top, 
 
 // analytic right-hand side of tail level t from host sine tables (DynamicGridUtils.hpp:111-124)
 template <class Real>
-__device__ void tail_rhs(const TailArgsDev<Real> &d, int t, Real *F)
+__device__ __forceinline__ void tail_rhs(const TailArgsDev<Real> &d, int t, Real *F)
 {
     const int N = d.lv[t].N, n = N * N;
     const double *sx = d.a.fmg_tab + d.a.fmg_tab_off[t];
@@ -635,7 +781,7 @@ __device__ void tail_rhs(const TailArgsDev<Real> &d, int t, Real *F)
 
 // values restriction (compute_coarsest_grid) fine level t -> t+1, coarse boundary 0
 template <class Real>
-__device__ void tail_restrict_values(const Real *x, const TailLevel<Real> &Lf, Real *xc,
+__device__ __forceinline__ void tail_restrict_values(const Real *x, const TailLevel<Real> &Lf, Real *xc,
                                      const TailLevel<Real> &Lc)
 {
     const int N = Lf.N, Nc = Lc.N, nc = Nc * Nc;
