@@ -67,7 +67,10 @@ constexpr int kPostExt = 4;       // row strips: k_post of a level below the fin
                                   // edge (bitwise what the neighbour computes), so the
                                   // coarse correction needs no halo exchange
 constexpr int kBlock = 256;       // threads per block for streaming kernels (4 waves)
-constexpr int kTailThreads = 512;   // 8 waves: 256 VGPRs a lane for the wave-0 paths (tail_w9, tail_w17)
+#ifndef PGMG_TAIL_THREADS
+#define PGMG_TAIL_THREADS 512    // 512 and 1024 measured equal (W at 4097 82.4 vs 82.9 ms)
+#endif
+constexpr int kTailThreads = PGMG_TAIL_THREADS;   // the tail workgroup (wave-0 paths fit 128 VGPRs)
 constexpr int kTailMaxN = 65;     // largest level the LDS-resident tail holds
 
 inline int pitch_for(int N) { return (N + 15) / 16 * 16; }

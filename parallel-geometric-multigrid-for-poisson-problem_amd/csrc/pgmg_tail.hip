@@ -33,6 +33,10 @@ constexpr bool kTailW9 = PGMG_TAIL_W9 != 0;
 #define PGMG_TAIL_W17 1  // the 17x17 level and below by tail_w17 on wave 0
 #endif
 constexpr bool kTailW17 = PGMG_TAIL_W17 != 0 && kTailW9;
+#ifndef PGMG_TAIL_W33
+#define PGMG_TAIL_W33 0  // 1: the 33x33 level too (16 points a lane: 256 VGPRs + 512 B of spills; off)
+#endif
+constexpr bool kTailW33 = PGMG_TAIL_W33 != 0 && kTailW17;
 
 template <class Real>
 struct TailLevel {
@@ -531,21 +535,23 @@ __device__ __forceinline__ Cnt tail_w9(const TailArgsDev<Real> &d, int l, int re
     return cnt;
 }
 
-// `reps` gamma-cycles of a 17x17 level whose coarser levels are 9x9 and the 5x5 coarsest,
-// on wave 0 (the block team's 16-wave barriers cost more than the work of a 17x17 stage):
-// four interior points per lane with their iterates in registers, flat indices computed
-// once, every stage's LDS reads issued together; the 9x9 sub-hierarchy by tail_w9.
-template <class Real>
-__device__ __forceinline__ Cnt tail_w17(const TailArgsDev<Real> &d, int l, int reps, Real *E,
-                                        Real *F, Real *T)
+// `reps` gamma-cycles of an NN x NN level (NN = 17, 33) whose coarser levels halve down to
+// the 5x5 coarsest, on wave 0 (a workgroup barrier per stage costs more than the work of a
+// stage at these sizes): Q = ceil((NN-2)^2 / 64) interior points per lane with their
+// iterates in registers, flat indices computed once, every stage's LDS reads issued
+// together; the next coarser level by tail_wq<NC> (tail_w9 for 9x9).
+template <class Real, int NN>
+__device__ __forceinline__ Cnt tail_wq(const TailArgsDev<Real> &d, int l, int reps, Real *E,
+                                       Real *F, Real *T)
 {
-    constexpr int Q = 4;   // 225 interior points over 64 lanes
+    constexpr int M = NN - 2, NI = M * M, Q = (NI + 63) / 64;
+    constexpr int NC = (NN - 1) / 2 + 1, MC = NC - 2;
     const TailArgsT<Real> &a = d.a;
     const TailLevel<Real> L = d.lv[l], L9 = d.lv[l + 1];   // by value: scalar registers
     Real *x17 = E + L.off;
     const Real *f17 = F + L.off;
-    Real *x9 = E + L9.off;
-    Real *f9 = F + L9.off;
+    Real *xc9 = E + L9.off;
+    Real *fc9 = F + L9.off;
     const int lane = threadIdx.x & 63;
     const double eps2 = d.eps2;
     const int gamma = d.gamma;
@@ -553,25 +559,38 @@ __device__ __forceinline__ Cnt tail_w17(const TailArgsDev<Real> &d, int l, int r
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         __builtin_amdgcn_wave_barrier();
     };
+    // the right-hand side in registers only while it fits (Q <= 4); otherwise re-read from
+    // LDS with the neighbours (h*h*f recomputed: the same IEEE product)
+    constexpr bool REGF = Q <= 4;
     int k[Q];
     bool in[Q];
-    Real x[Q], fk[Q], hf[Q];
+    Real x[Q], fkr[REGF ? Q : 1], hfr[REGF ? Q : 1];
     const Real hh = L.hh, ih = L.ih;
     #pragma unroll
     for (int q = 0; q < Q; ++q) {
-        const int p = lane + 64 * q, jj = p / 15;
-        in[q] = p < 225;
-        k[q] = in[q] ? (1 + jj) * 17 + 1 + (p - 15 * jj) : 18;
-        fk[q] = f17[k[q]];
-        hf[q] = hh * fk[q];
+        const int p = lane + 64 * q, jj = p / M;
+        in[q] = p < NI;
+        k[q] = in[q] ? (1 + jj) * NN + 1 + (p - M * jj) : NN + 1;
+        if constexpr (REGF) {
+            fkr[q] = f17[k[q]];
+            hfr[q] = hh * fkr[q];
+        }
         x[q] = x17[k[q]];
     }
+    auto fk = [&](int q) __attribute__((always_inline)) {
+        if constexpr (REGF) return fkr[q];
+        else return f17[k[q]];
+    };
+    auto hf = [&](int q) __attribute__((always_inline)) {
+        if constexpr (REGF) return hfr[q];
+        else return hh * f17[k[q]];
+    };
     auto smooth = [&](int num_iter, Cnt &c) __attribute__((always_inline)) {
         Real nx[Q];
         #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const int kk = k[q];
-            nx[q] = Real(0.25) * (hf[q] + x17[kk - 1] + x17[kk + 1] + x17[kk - 17] + x17[kk + 17]);
+            nx[q] = Real(0.25) * (hf(q) + x17[kk - 1] + x17[kk + 1] + x17[kk - NN] + x17[kk + NN]);
         }
         fence();
         #pragma unroll
@@ -586,10 +605,10 @@ __device__ __forceinline__ Cnt tail_w17(const TailArgsDev<Real> &d, int l, int r
             #pragma unroll
             for (int q = 0; q < Q; ++q) {
                 const int kk = k[q];
-                const Real l0 = x17[kk - 1], r0 = x17[kk + 1], u0 = x17[kk - 17], d0 = x17[kk + 17];
-                const Real res = fk[q] - ih * (Real(4) * x[q] - l0 - r0 - u0 - d0);
+                const Real l0 = x17[kk - 1], r0 = x17[kk + 1], u0 = x17[kk - NN], d0 = x17[kk + NN];
+                const Real res = fk(q) - ih * (Real(4) * x[q] - l0 - r0 - u0 - d0);
                 if (in[q]) acc += sq(res);
-                nx[q] = Real(0.25) * (hf[q] + l0 + r0 + u0 + d0);
+                nx[q] = Real(0.25) * (hf(q) + l0 + r0 + u0 + d0);
             }
             fence();
             #pragma unroll
@@ -610,11 +629,17 @@ __device__ __forceinline__ Cnt tail_w17(const TailArgsDev<Real> &d, int l, int r
             ++c.sweeps;
         }
     };
-    // 9x9 lane p < 49: interior point (1 + p/7, 1 + p%7); fine centre (2j, 2i) of 17x17
-    const int j9 = 1 + lane / 7, i9 = 1 + lane - 7 * (lane / 7);
-    const bool in9 = lane < 49;
-    const int kf = in9 ? (2 * j9) * 17 + 2 * i9 : 36;
-    const int k9 = in9 ? j9 * 9 + i9 : 10;
+    // coarse interior point pc = lane + 64 qc: (1 + pc/MC, 1 + pc%MC), fine centre (2j, 2i)
+    constexpr int QC = (MC * MC + 63) / 64;
+    int kf[QC], kc9[QC];
+    bool inc[QC];
+    #pragma unroll
+    for (int qc = 0; qc < QC; ++qc) {
+        const int pc = lane + 64 * qc, jc = 1 + pc / MC, ic = 1 + pc - MC * (pc / MC);
+        inc[qc] = pc < MC * MC;
+        kf[qc] = inc[qc] ? (2 * jc) * NN + 2 * ic : 2 * NN + 2;
+        kc9[qc] = inc[qc] ? jc * NC + ic : NC + 1;
+    }
     Cnt cnt;
     for (int v = 0; v < reps; ++v) {
         smooth(a.v1, cnt);
@@ -624,29 +649,36 @@ __device__ __forceinline__ Cnt tail_w17(const TailArgsDev<Real> &d, int l, int r
         for (int q = 0; q < Q; ++q) {
             const int kk = k[q];
             if (in[q])
-                T[kk] = fk[q] - ih * (Real(4) * x[q] - x17[kk - 1] - x17[kk + 1] - x17[kk - 17] - x17[kk + 17]);
+                T[kk] = fk(q) - ih * (Real(4) * x[q] - x17[kk - 1] - x17[kk + 1] - x17[kk - NN] - x17[kk + NN]);
         }
         fence();
-        if (in9) {
-            f9[k9] = Real(0.25) * T[kf] + Real(0.125) * (T[kf + 1] + T[kf - 1] + T[kf + 17] + T[kf - 17]) +
-                     Real(0.0625) * (T[kf - 17 - 1] + T[kf - 17 + 1] + T[kf + 17 - 1] + T[kf + 17 + 1]);
-            x9[k9] = Real(0);
+        #pragma unroll
+        for (int qc = 0; qc < QC; ++qc) {
+            if (inc[qc]) {
+                const int c = kf[qc];
+                fc9[kc9[qc]] = Real(0.25) * T[c] + Real(0.125) * (T[c + 1] + T[c - 1] + T[c + NN] + T[c - NN]) +
+                               Real(0.0625) * (T[c - NN - 1] + T[c - NN + 1] + T[c + NN - 1] + T[c + NN + 1]);
+                xc9[kc9[qc]] = Real(0);
+            }
         }
         fence();
-        cnt += tail_w9<Real>(d, l + 1, gamma, E, F, T);
+        if constexpr (NC == 9)
+            cnt += tail_w9<Real>(d, l + 1, gamma, E, F, T);
+        else
+            cnt += tail_wq<Real, NC>(d, l + 1, gamma, E, F, T);
         // x += P e on fine points [2, 15]^2 (MultiGrid.hpp:208-226)
         #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            const int p = lane + 64 * q, jj = p / 15;
-            const int j = 1 + jj, i = 1 + (p - 15 * jj);
-            if (in[q] && j >= 2 && i >= 2 && j <= 15 && i <= 15) {
+            const int p = lane + 64 * q, jj = p / M;
+            const int j = 1 + jj, i = 1 + (p - M * jj);
+            if (in[q] && j >= 2 && i >= 2 && j <= NN - 2 && i <= NN - 2) {
                 const int cj = j >> 1, ci = i >> 1;
-                const Real *C0 = x9 + cj * 9;
+                const Real *C0 = xc9 + cj * NC;
                 Real w;
                 if ((j & 1) == 0) {
                     w = ((i & 1) == 0) ? C0[ci] : Real(0.5) * (C0[ci] + C0[ci + 1]);
                 } else {
-                    const Real *C1 = C0 + 9;
+                    const Real *C1 = C0 + NC;
                     w = ((i & 1) == 0) ? Real(0.5) * (C0[ci] + C1[ci])
                                        : Real(0.25) * (C0[ci] + C0[ci + 1] + C1[ci] + C1[ci + 1]);
                 }
@@ -680,11 +712,15 @@ __device__ __forceinline__ Cnt tail_gcycle(const TailArgsDev<Real> &d, int top, 
     const int last = d.nl - 1;
     for (;;) {
         if (descending) {
-            if (kBlock && kTailW17 && l != top && d.lv[l].N == 17 && l + 2 == last &&
-                d.lv[l + 1].N == 9 && d.lv[l + 2].N == 5) {
-                // the whole gamma-recursion of the 17x17 level (and below) on wave 0
+            const bool w33 = kTailW33 && d.lv[l].N == 33 && l + 3 == last && d.lv[l + 3].N == 5;
+            const bool w17 = kTailW17 && d.lv[l].N == 17 && l + 2 == last && d.lv[l + 2].N == 5;
+            if (kBlock && l != top && (w33 || w17)) {
+                // the whole gamma-recursion of this level (and below) on wave 0
                 const unsigned long long c0 = d.prof ? tail_clock() : 0;
-                if (threadIdx.x < 64) cnt += tail_w17<Real>(d, l, d.gamma, E, F, T);
+                if (threadIdx.x < 64) {
+                    if (w33) cnt += tail_wq<Real, 33>(d, l, d.gamma, E, F, T);
+                    else cnt += tail_wq<Real, 17>(d, l, d.gamma, E, F, T);
+                }
                 __syncthreads();
                 if (d.prof && threadIdx.x == 0) d.prof[0] += tail_clock() - c0;
                 vset(l, d.gamma - 1);
