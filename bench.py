@@ -19,7 +19,10 @@ reference's own runs): `parity` is true only when every repetition matched.
 
 Kernel durations for `roofline` come from one more repetition with hipEvents around every
 finest-level pass (PGMG_FLAG_TIME_FINE; the events cost ~2-4 % of the cycle, so the clean
-repetitions give `value`).  With N GPUs the same grid is split into row strips (strong
+repetitions give `value`).  `roofline.traffic` is the HBM traffic of the same kernel from
+two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over a short child run of this very
+build, made before this process touches the GPU (--pmc off: the committed
+profiles/pmc_fine.json, labelled with the build it measured).  With N GPUs the same grid is split into row strips (strong
 scaling, RCCL halo exchange); value = V-cycles of the whole job per second.
 
 Prints ONE JSON line on rank 0.  See DESIGN.md "Measurement" for every field.
@@ -60,6 +63,11 @@ def parse():
                     help="f64: the reference's precision (the headline); f32: the fp32 variant")
     ap.add_argument("--general-rhs", choices=["auto", "off"], default="auto",
                     help="also measure the stored-f path (a user RHS streamed, 24 B/pt)")
+    ap.add_argument("--pmc", choices=["auto", "off"], default="auto",
+                    help="auto: HBM traffic of the finest-level passes from two rocprofv3 --pmc "
+                         "passes (FETCH_SIZE, WRITE_SIZE) over a short child run of this build, "
+                         "before this process touches the GPU")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -106,17 +114,92 @@ def cpu_baseline(n, cycles=1, kind="V", skip=0):
                       f"{t:.4f} s per {kind}-cycle; host {_cpu_model()}"}
 
 
+def lib_build_id():
+    """sha256 prefix of the libpgmg.so this run loads (names the build a profile measured)."""
+    import hashlib
+    import _pkgload
+    p = pathlib.Path(_pkgload.PKG_DIR) / "libpgmg.so"
+    try:
+        return "libpgmg.so sha256:" + hashlib.sha256(p.read_bytes()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
+def kernel_key(name):
+    """rocprofv3 kernel name -> the symbol key bench.py uses: 'k_pre<double,false,...>'."""
+    name = name.split("(")[0].replace("void ", "").replace("pgmg::", "")
+    return name.replace(" ", "").strip()
+
+
+def pmc_child(args):
+    """The program the live PMC passes profile: the timed call's kernels (a 3-cycle call:
+    first k_pre, two cross-cycle k_postpre, last k_post) of both legs, then exit."""
+    import torch  # noqa: F401
+    import _pkgload
+    pg = _pkgload.load()
+    legs = [0]
+    if args.cycle == "V" and args.general_rhs == "auto":
+        legs.append(pg.PGMG_FLAG_STORED_RHS)
+    for flags in legs:
+        with pg.Solver(args.n, flags=flags, dtype=args.dtype) as s:
+            s.set_problem()
+            {"V": s.vcycle, "W": s.wcycle, "F": s.fcycle}[args.cycle](3 if args.cycle != "W" else 1)
+            s.sync()
+
+
+def live_pmc(args):
+    """HBM bytes per launch of every kernel of a short child run of THIS build on THIS box:
+    one rocprofv3 pass per counter (FETCH_SIZE, WRITE_SIZE; they do not fit one pass), bytes =
+    2 x FETCH_SIZE + WRITE_SIZE (KiB; MI355X_MICROARCH.md's gfx950 corrections: FETCH_SIZE
+    counts half of a 16 B/lane streaming read, WRITE_SIZE is exact).  Runs before this
+    process touches the GPU; returns ({key: bytes}, note) or (None, reason)."""
+    import csv
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None, "rocprofv3 not found"
+    vals = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="pgmg_pmc_")
+        cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", ctr, "--output-format", "csv",
+               "-d", d, "-o", "run", "--", sys.executable, str(ROOT / "bench.py"), "--pmc-child",
+               "--n", str(args.n), "--dtype", args.dtype, "--cycle", args.cycle,
+               "--general-rhs", args.general_rhs]
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=180)
+            files = list(pathlib.Path(d).rglob("*counter_collection.csv"))
+            if r.returncode != 0 or not files:
+                return None, f"rocprofv3 --pmc {ctr} failed (rc={r.returncode})"
+            for row in csv.DictReader(open(files[0])):
+                if row.get("Counter_Name") == ctr:
+                    vals.setdefault(kernel_key(row["Kernel_Name"]), {}).setdefault(ctr, []).append(
+                        float(row["Counter_Value"]))
+        except (subprocess.SubprocessError, OSError, KeyError, ValueError) as e:
+            return None, f"rocprofv3 --pmc {ctr} failed: {e}"
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+    out = {}
+    for k, v in vals.items():
+        if v.get("FETCH_SIZE") and v.get("WRITE_SIZE"):
+            fetch = sum(v["FETCH_SIZE"]) / len(v["FETCH_SIZE"])
+            write = sum(v["WRITE_SIZE"]) / len(v["WRITE_SIZE"])
+            out[k] = (2 * fetch + write) * 1024.0
+    return out, "live rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this build (bench.py --pmc)"
+
+
 def pmc_traffic(n, key):
-    """HBM bytes per launch of kernel `key` at grid n from the committed rocprofv3 PMC
-    summary, with the build it was measured on (FETCH_SIZE x2 + WRITE_SIZE, the gfx950
-    corrections of MI355X_MICROARCH.md)."""
+    """Fallback: HBM bytes per launch of kernel `key` at grid n from the committed rocprofv3
+    PMC summary, and the build it was measured on."""
     if not PMC_PROFILE.exists():
         return None, None
     try:
         d = json.loads(PMC_PROFILE.read_text())
         for k in d.get("kernels", []):
             if int(k.get("N", 0)) == n and k.get("kernel", "") == key:
-                return k.get("hbm_bytes_per_launch"), d.get("build", "unknown build")
+                build = d.get("build")
+                label = ("this build" if build and build == lib_build_id()
+                         else f"another build: {build or 'unrecorded'}")
+                return k.get("hbm_bytes_per_launch"), f"{PMC_PROFILE.relative_to(ROOT)} ({label})"
     except (ValueError, OSError):
         pass
     return None, None
@@ -136,6 +219,8 @@ def golden_hash(kind, n, cycles):
 
 def main():
     args = parse()
+    if args.pmc_child:
+        return pmc_child(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -152,6 +237,9 @@ def main():
         except Exception as e:
             cpu1 = {"value": None, "unit": "V-cycles/s", "cores": 1, "kind": "port",
                     "sample": f"failed: {e}"}
+    pmc, pmc_note = None, "off"
+    if world == 1 and rank == 0 and args.pmc == "auto":
+        pmc, pmc_note = live_pmc(args)
     import torch  # noqa: F401  (loads the ROCm runtime first; see _capi.load)
     import _pkgload
     pg = _pkgload.load()
@@ -257,12 +345,15 @@ def main():
             nbytes = leg["bytes"][w]
             ach = nbytes / (ms * 1e-3) / 1e9
             name, key = names[w]
-            traffic, build = pmc_traffic(args.n, key) if world == 1 else (None, None)
+            if pmc is not None:
+                traffic, source = pmc.get(key), pmc_note
+            else:
+                traffic, source = pmc_traffic(args.n, key) if world == 1 else (None, None)
             roof.append({"bound": "hbm", "kernel": name, "symbol": key, "achieved": round(ach, 2),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
                          "traffic": traffic,
-                         "traffic_source": (f"{PMC_PROFILE.relative_to(ROOT)} ({build})"
-                                            if traffic else None),
+                         "traffic_source": source if traffic else None,
+                         "traffic_ratio": round(traffic / nbytes, 4) if traffic else None,
                          "bytes_per_launch": nbytes, "launches_timed": cnt,
                          "ms_per_launch": round(ms, 5)})
         # the dominant kernel: largest total time over the timed region
@@ -330,6 +421,8 @@ def main():
                                    "in_stream_level_mask": spec_mask},
             "cpu_baseline": cpu,
             "cpu_baseline_config1": cpu1,
+            "pmc": pmc_note,
+            "build": lib_build_id(),
         }
         if gen_leg is not None:
             gmed = statistics.median(gen_leg["times"])

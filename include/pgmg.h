@@ -127,6 +127,10 @@ typedef struct pgmg_config {
                           for this long aborts the communicator and returns
                           PGMG_ERR_COMM (default 600); RCCL's asynchronous error
                           state is polled while waiting                            */
+    double h0;         /* finest-level mesh width; 0 (default): a / (N - 1).  The
+                          reference's cycle entry points take h from the caller
+                          (MultiGrid.hpp:57, Parallel_Mg.cu:21); coarse levels double
+                          it (MultiGrid.hpp:83)                                    */
 } pgmg_config;
 
 typedef struct pgmg_ctx pgmg_ctx;
@@ -161,7 +165,7 @@ int pgmg_get_solution(pgmg_ctx *ctx, double *phi_host);
  * ranks other than root may pass phi_host = NULL).  root < 0: every rank, as above. */
 int pgmg_gather_solution(pgmg_ctx *ctx, int root, double *phi_host);
 
-/* FNV-64 hash of phi's IEEE words in the reference layout (h = 14695981039346656037,
+/* FNV-64-style hash of phi's IEEE words in the reference layout (h = 1469598103934665603,
  * h = (h ^ word) * 1099511628211 per element, row-major N*N): the checksum of the golden
  * fixtures (tests/golden/cycles.json).  Collective on row strips; the value lands on rank
  * `root` (root < 0: every rank), the others get 0. */
@@ -192,6 +196,15 @@ int pgmg_vcycle_bytes(pgmg_ctx *ctx, double *bytes);
  * rank, for callers that want to read it in place.  The elements are double, or
  * float when the context was created with PGMG_PRECISION_FP32 (pgmg_precision). */
 int pgmg_phi_device(pgmg_ctx *ctx, double **ptr, int *pitch, int *row0, int *rows);
+
+/* Is rows [row0, row1] x columns [col0, col1] (inclusive, elements of elem_bytes, row pitch
+ * `pitch` elements, relative to element (0,0) at `origin`) inside ONE device allocation of
+ * this library (a level grid)?  PGMG_OK if so, PGMG_ERR_STATE otherwise.  The fused passes
+ * run this check on every array before each launch (they read halo rows past their bands
+ * and margin columns past their tiles); callers reading a grid in place through
+ * pgmg_phi_device can use it too. */
+int pgmg_check_span(const void *origin, long long pitch, int elem_bytes, long long row0,
+                    long long row1, long long col0, long long col1);
 
 /* Algorithmic HBM bytes of one launch of finest-level pass `pass` (numbering of
  * pgmg_fine_pass_time) on this rank: every input read once, every output written once

@@ -62,6 +62,7 @@ def lib(dtype="f64"):
             "orc_jacobi_smooth": (C.c_int, [P, P, P, C.c_int, C.c_int, C.c_double, C.c_int, P]),
             "orc_restrict": (None, [P, P, C.c_int, C.c_int]),
             "orc_prolong": (None, [P, P, C.c_int, C.c_int]),
+            "orc_prolong_sym": (None, [P, P] + [C.c_int] * 6),
             "orc_v_cycle": (None, [P, P, P, C.c_int, C.c_double]),
             "orc_w_cycle": (None, [P, P, P, C.c_int, C.c_double]),
             "orc_f_cycle_outer": (None, [P, P, C.c_int]),
@@ -165,6 +166,23 @@ def restrict(fine):
 def prolong(fine, coarse):
     out = np.array(fine, dtype=np.float64, copy=True)
     lib().orc_prolong(_p(out), _p(coarse), out.shape[0], coarse.shape[0])
+    return out
+
+
+def prolong_sym(fine, coarse, num_thread=None):
+    """fine += P_sym coarse as prolungator_kernel (Parallel_Method.cu:79-138) computes it.
+    num_thread=None: the thread grid covers the whole fine grid; otherwise the grid of
+    Parallel::ComputeProlungator (:188-199), max(1, Nf // num_thread) * num_thread wide."""
+    out = np.array(fine, dtype=np.float64, copy=True)
+    coarse = np.ascontiguousarray(coarse, dtype=np.float64)
+    Hf, Wf = out.shape
+    Hc, Wc = coarse.shape
+    if num_thread is None:
+        ey, ex = Hf, Wf
+    else:
+        ey = max(1, Hf // num_thread) * num_thread
+        ex = max(1, Hf // num_thread) * num_thread   # the launch is square in fine_N
+    lib().orc_prolong_sym(_p(out), _p(coarse), Hc, Wc, Hf, Wf, ey, ex)
     return out
 
 

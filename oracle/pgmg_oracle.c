@@ -21,6 +21,8 @@
  *   - v_cycle / w_cycle / f_cycle / compute_coarsest_grid
  *     (2_part_MG/MultiGrid.hpp:28-183), restriction (:187-205),
  *     prolongation incl. the skipped fine row/col 1 (:208-226)
+ *   - the GPU path's symmetric prolongation, prolungator_kernel
+ *     (3_part_parallel/Parallel_Method.cu:79-138)
  * Floating point: compiled with -ffp-contract=off so every expression rounds
  * exactly as the reference's plain C++ does (no FMA contraction).
  *
@@ -210,6 +212,43 @@ void orc_prolong(real *F, const real *C, int Nf, int Nc)
             F[(J + 1) * Nf + I] += (real)0.5 * (C[c] + C[c + Nc]);
             F[J * Nf + I + 1] += (real)0.5 * (C[c] + C[c + 1]);
             F[(J + 1) * Nf + I + 1] += (real)0.25 * (C[c] + C[c + 1] + C[c + Nc] + C[c + Nc + 1]);
+        }
+    }
+}
+
+/* fine += P_sym * coarse over the thread grid [0, ext_y) x [0, ext_x) of the reference's
+ * GPU prolongation `prolungator_kernel` (3_part_parallel/Parallel_Method.cu:79-138), launched
+ * by Parallel::ComputeProlungator (:188-199) with max(1, fine_N / num_thread) blocks of
+ * num_thread^2 threads per axis.  Unlike MultiGrid.hpp:208-226 it is symmetric: every
+ * interior fine point is corrected (row/col 1 included), and the boundary points the grid
+ * covers are set to 0 (:88-93).  Per case (:100-135): even/even injection; odd/odd the
+ * 4-corner average 0.25*(c + c_e + c_s + c_se) if cx+1 < Wc and cy+1 < Hc, else 0;
+ * odd column 0.5*(c + c_e) if cx+1 < Wc; odd row 0.5*(c + c_s) if cy+1 < Hc.  Points
+ * outside the thread grid are untouched (for fine_N = 2^k+1 > num_thread the grid is
+ * fine_N-1 wide, so the last boundary row/column keep their values). */
+void orc_prolong_sym(real *F, const real *C, int Hc, int Wc, int Hf, int Wf, int ext_y, int ext_x)
+{
+    for (int y = 0; y < ext_y && y < Hf; ++y) {
+        for (int x = 0; x < ext_x && x < Wf; ++x) {
+            long long k = (long long)y * Wf + x;
+            if (y == 0 || y == Hf - 1 || x == 0 || x == Wf - 1) {
+                F[k] = 0;
+                continue;
+            }
+            real v = 0;
+            int cx = x / 2, cy = y / 2;
+            long long c = (long long)cy * Wc + cx;
+            if (x % 2 == 0 && y % 2 == 0) {
+                v = C[c];
+            } else if (x % 2 == 1 && y % 2 == 1) {
+                if (cx + 1 < Wc && cy + 1 < Hc)
+                    v = (real)0.25 * (C[c] + C[c + 1] + C[c + Wc] + C[c + Wc + 1]);
+            } else if (x % 2 == 1 && y % 2 == 0) {
+                if (cx + 1 < Wc) v = (real)0.5 * (C[c] + C[c + 1]);
+            } else {
+                if (cy + 1 < Hc) v = (real)0.5 * (C[c] + C[c + Wc]);
+            }
+            F[k] += v;
         }
     }
 }

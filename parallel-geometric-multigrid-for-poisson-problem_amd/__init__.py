@@ -22,7 +22,8 @@ from ._capi import (PGMG_FLAG_LOOPBACK, PGMG_FLAG_NO_CROSS, PGMG_FLAG_NO_GRAPH,
                     PGMG_FLAG_TIME_FINE, PGMG_PRECISION_FP32, PGMG_PRECISION_FP64,
                     PGMG_FLAG_UNFUSED, PGMG_FLAG_NO_RECOMPUTE, PGMG_FLAG_NO_PIN,
                     PGMG_FLAG_NO_R2, PGMG_PROLONG_REFERENCE,
-                    PGMG_PROLONG_SYMMETRIC, PgmgConfig, PgmgError, check, load)
+                    PGMG_PROLONG_SYMMETRIC, PGMG_OK, PGMG_ERR_STATE, PgmgConfig, PgmgError,
+                    check, load)
 
 PKG_DIR = pathlib.Path(__file__).resolve().parent
 

@@ -61,6 +61,7 @@ class PgmgConfig(C.Structure):
         ("cross_min_n", C.c_int),
         ("spec_segment", C.c_int),
         ("comm_timeout_s", C.c_double),
+        ("h0", C.c_double),
     ]
 
 
@@ -85,6 +86,8 @@ SIGNATURES = [
     ("pgmg_last_elapsed_ms", C.c_int, [_P, _DP]),
     ("pgmg_levels", C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("pgmg_vcycle_bytes", C.c_int, [_P, _DP]),
+    ("pgmg_check_span", C.c_int, [_P, C.c_longlong, C.c_int, C.c_longlong, C.c_longlong,
+                                  C.c_longlong, C.c_longlong]),
     ("pgmg_phi_device", C.c_int, [_P, C.POINTER(_P), C.POINTER(C.c_int), C.POINTER(C.c_int),
                                   C.POINTER(C.c_int)]),
     ("pgmg_fine_sweep_time", C.c_int, [_P, C.POINTER(C.c_int), _DP]),

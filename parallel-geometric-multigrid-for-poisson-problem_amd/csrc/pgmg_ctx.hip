@@ -22,6 +22,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <utility>
 #include <vector>
@@ -59,6 +61,47 @@ int pgmg::set_err(int code, const std::string &msg)
 // ---------------------------------------------------------------------------
 // allocation
 // ---------------------------------------------------------------------------
+namespace {
+std::mutex g_alloc_mu;
+std::map<uintptr_t, size_t> g_allocs;   // base -> bytes of every registered allocation
+}  // namespace
+
+void pgmg::register_alloc(const void *base, size_t bytes)
+{
+    std::lock_guard<std::mutex> lk(g_alloc_mu);
+    g_allocs[(uintptr_t)base] = bytes;
+}
+
+void pgmg::unregister_alloc(const void *base)
+{
+    std::lock_guard<std::mutex> lk(g_alloc_mu);
+    g_allocs.erase((uintptr_t)base);
+}
+
+int pgmg::check_span(const void *o, long long P, int es, long long r0, long long r1,
+                     long long c0, long long c1, const char *what)
+{
+    if (o == nullptr || r1 < r0 || c1 < c0) return PGMG_OK;
+    const intptr_t org = (intptr_t)o;
+    const intptr_t lo = org + (intptr_t)((r0 * P + c0) * es);
+    const intptr_t hi = org + (intptr_t)((r1 * P + c1 + 1) * es);   // one past the last byte
+    {
+        std::lock_guard<std::mutex> lk(g_alloc_mu);
+        auto it = g_allocs.upper_bound((uintptr_t)lo);
+        if (it != g_allocs.begin()) {
+            --it;
+            const intptr_t b = (intptr_t)it->first, e = b + (intptr_t)it->second;
+            if (lo >= b && hi <= e) return PGMG_OK;
+        }
+    }
+    char buf[256];
+    std::snprintf(buf, sizeof(buf),
+                  "%s: rows %lld..%lld, columns %lld..%lld (pitch %lld) outside the array's "
+                  "allocation",
+                  what, r0, r1, c0, c1, P);
+    return set_err(PGMG_ERR_STATE, buf);
+}
+
 int pgmg::alloc_grid(Grid &g, const Level &L)
 {
     // owned rows + kHalo halo rows each side (the fused passes read 4 rows past a
@@ -73,13 +116,17 @@ int pgmg::alloc_grid(Grid &g, const Level &L)
     HIPC(hipMemset(p, 0, n * L.es));
     g.base = p;
     g.bytes = n * L.es;
+    register_alloc(p, g.bytes);
     g.o = static_cast<char *>(p) + (off + (ptrdiff_t)(kHalo - L.lo) * L.P) * L.es;
     return PGMG_OK;
 }
 
 void pgmg::free_grid(Grid &g)
 {
-    if (g.base) (void)hipFree(g.base);
+    if (g.base) {
+        unregister_alloc(g.base);
+        (void)hipFree(g.base);
+    }
     g.base = g.o = nullptr;
     g.bytes = 0;
 }
@@ -318,11 +365,11 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     double *lp = chk_partials(c, fa.np, l);   // speculative call: record the check, no fix-up
     if (lp) pa.partials = lp;
     int ev = fine ? timed_begin(c, 1) : -1;
-    launch_pre(pa, x0_zero, fine, c->s);
+    if ((e = launch_pre(pa, x0_zero, fine, c->s))) return e;
     if ((e = timed_end(c, 1, ev))) return e;
     if (!lp) {
         if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
-        launch_pre_rare(fa, pa, x0_zero, c->s);
+        if ((e = launch_pre_rare(fa, pa, x0_zero, c->s))) return e;
     }
     if ((e = enqueue_children<T>(c, l, gamma))) return e;
     // the correction of level l+1 is not exchanged: a distributed child's k_post computed
@@ -361,12 +408,12 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     lp = chk_partials(c, fa.np, l);
     if (lp) po.partials = lp;
     ev = fine ? timed_begin(c, 2) : -1;
-    launch_post(po, fine, c->s);
+    if ((e = launch_post(po, fine, c->s))) return e;
     if ((e = timed_end(c, 2, ev))) return e;
     if (!lp) {
         fa.global_sum = nullptr;
         if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
-        launch_post_rare(fa, po, c->s);
+        if ((e = launch_post_rare(fa, po, c->s))) return e;
     }
     return PGMG_OK;
 }
@@ -493,7 +540,7 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
     double *lp = chk_partials(c, np, 0);
     if (lp) pa.partials = lp;
     int ev = timed_begin(c, 1);
-    launch_pre(pa, false, true, c->s);
+    if ((e = launch_pre(pa, false, true, c->s))) return e;
     if ((e = timed_end(c, 1, ev))) return e;
     if (!lp) {
         if (dist && (e = global_sum(c, np, &fa.global_sum))) return e;
@@ -532,7 +579,7 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         q.rc_lo = sr.rc_lo;
         q.rc_hi = sr.rc_hi;
         ev = timed_begin(c, 3);
-        launch_postpre(q, c->s);
+        if ((e = launch_postpre(q, c->s))) return e;
         if ((e = timed_end(c, 3, ev))) return e;
         const double *g3 = nullptr;   // all-rank {post, pre, pre-from-x1} sums
         if (lean) {
@@ -561,7 +608,7 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         launch_post_fixup(f1, po, c->s);
         PreArgsT<T> p1 = make_pre<T>(c, S, nx);
         p1.cond = &c->ppflags[0];
-        launch_pre(p1, false, false, c->s);
+        if ((e = launch_pre(p1, false, false, c->s))) return e;
         FixArgsF f1b = fa;
         f1b.cond = &c->ppflags[0];
         f1b.global_sum = dist ? c->scalar + 2 : nullptr;
@@ -581,7 +628,7 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         } else {
             p2.cond = &c->ppflags[1];
             p2.stats = nullptr;
-            launch_post(p2, false, c->s);
+            if ((e = launch_post(p2, false, c->s))) return e;
         }
         PreArgsT<T> p3 = make_pre<T>(c, S, nx);
         FixArgsF f2 = fa;
@@ -599,7 +646,7 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
     lp = chk_partials(c, np, 0);
     if (lp) po.partials = lp;
     ev = timed_begin(c, 2);
-    launch_post(po, true, c->s);
+    if ((e = launch_post(po, true, c->s))) return e;
     if ((e = timed_end(c, 2, ev))) return e;
     if (!lp) {
         if (dist && (e = global_sum(c, np, &fa.global_sum))) return e;
@@ -698,6 +745,7 @@ int pgmg_config_default(pgmg_config *cfg, int N)
     cfg->cross_min_n = 2049;
     cfg->spec_segment = 0;
     cfg->comm_timeout_s = 600.0;
+    cfg->h0 = 0.0;
     return PGMG_OK;
 }
 
@@ -761,6 +809,8 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         return set_err(PGMG_ERR_ARG, "bad rank/world");
     if (cfg->precision != PGMG_PRECISION_FP64 && cfg->precision != PGMG_PRECISION_FP32)
         return set_err(PGMG_ERR_ARG, "precision must be PGMG_PRECISION_FP64 or _FP32");
+    if (!(cfg->h0 >= 0.0) || !std::isfinite(cfg->h0))
+        return set_err(PGMG_ERR_ARG, "h0 must be finite and >= 0 (0: a / (N - 1))");
     int ndev = 0;
     HIPC(hipGetDeviceCount(&ndev));
     if (cfg->device < 0 || cfg->device >= ndev) return set_err(PGMG_ERR_ARG, "bad device ordinal");
@@ -776,7 +826,8 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
 
     // level sizes: bulk while N > tail_n, then the tail's top level
     int N = cfg->N;
-    double h = cfg->a / (N - 1);  // MultiGridTestRunner.hpp:131
+    // MultiGridTestRunner.hpp:131, or the caller's h (MultiGrid.hpp:57's argument)
+    double h = cfg->h0 > 0.0 ? cfg->h0 : cfg->a / (N - 1);
     for (;;) {
         Level L;
         L.N = N;
@@ -1378,7 +1429,7 @@ static int enqueue_smooth3_fused(pgmg_ctx *c, int l)
     q.row_hi = L.u1;
     q.rc_lo = 1;
     q.rc_hi = 1;
-    launch_smooth4(q, c->s);
+    if ((e = launch_smooth4(q, c->s))) return e;
     const int np = postpre_blocks(L.N, q.jc0, q.jc1);
     const double *g3 = nullptr;
     if (dist) {
@@ -1779,6 +1830,14 @@ int pgmg_precision(pgmg_ctx *c, int *precision, int *elem_bytes)
     if (precision) *precision = c->fp32 ? PGMG_PRECISION_FP32 : PGMG_PRECISION_FP64;
     if (elem_bytes) *elem_bytes = c->lv[0].es;
     return PGMG_OK;
+}
+
+int pgmg_check_span(const void *origin, long long pitch, int elem_bytes, long long row0,
+                    long long row1, long long col0, long long col1)
+{
+    if (!origin || pitch <= 0 || elem_bytes <= 0 || row1 < row0 || col1 < col0)
+        return set_err(PGMG_ERR_ARG, "pgmg_check_span: bad arguments");
+    return check_span(origin, pitch, elem_bytes, row0, row1, col0, col1, "pgmg_check_span");
 }
 
 int pgmg_phi_device(pgmg_ctx *c, double **ptr, int *pitch, int *row0, int *rows)

@@ -102,20 +102,22 @@ using PostArgs = PostArgsT<double>;
 using PostPreArgs = PostPreArgsT<double>;
 
 int fused_blocks(int N, int jc0, int jc1);
-template <class T> void launch_pre(const PreArgsT<T> &a, bool x0_zero, bool fine, hipStream_t s);
-template <class T> void launch_post(const PostArgsT<T> &a, bool fine, hipStream_t s);
+// the fused-pass launchers return PGMG_ERR_STATE (and launch nothing) when a span the pass
+// would read or write lies outside its array's allocation (check_span)
+template <class T> int launch_pre(const PreArgsT<T> &a, bool x0_zero, bool fine, hipStream_t s);
+template <class T> int launch_post(const PostArgsT<T> &a, bool fine, hipStream_t s);
 template <class T>
 void launch_pre_fixup(const FixArgsF &a, const PreArgsT<T> &p, bool x0_zero, hipStream_t s);
 template <class T> void launch_post_fixup(const FixArgsF &a, const PostArgsT<T> &p, hipStream_t s);
 // the same rare paths as fused one-sweep passes (in-stream checks of enqueue_fused_level)
 template <class T>
-void launch_pre_rare(const FixArgsF &f, const PreArgsT<T> &a, bool x0_zero, hipStream_t s);
-template <class T> void launch_post_rare(const FixArgsF &f, const PostArgsT<T> &a, hipStream_t s);
+int launch_pre_rare(const FixArgsF &f, const PreArgsT<T> &a, bool x0_zero, hipStream_t s);
+template <class T> int launch_post_rare(const FixArgsF &f, const PostArgsT<T> &a, hipStream_t s);
 int postpre_blocks(int N, int jc0, int jc1);
-template <class T> void launch_postpre(const PostPreArgsT<T> &a, hipStream_t s);
+template <class T> int launch_postpre(const PostPreArgsT<T> &a, hipStream_t s);
 // fused smooth(3): x4 of a.phi into a.x4 with the three checks' partial sums
 // (partials1 r(x1), partials3 r(x2), partials2 r(x3)); then the decision + rare path
-template <class T> void launch_smooth4(const PostPreArgsT<T> &a, hipStream_t s);
+template <class T> int launch_smooth4(const PostPreArgsT<T> &a, hipStream_t s);
 template <class T>
 void launch_smooth4_finish(const PostPreArgsT<T> &a, int np, const double *global3, double eps,
                            unsigned *flags, unsigned long long *stats, hipStream_t s);

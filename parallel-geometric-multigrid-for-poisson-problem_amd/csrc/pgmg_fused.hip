@@ -31,6 +31,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "pgmg.h"
 #include "pgmg_fused.h"
 
 namespace pgmg {
@@ -1040,13 +1041,140 @@ int fused_blocks(int N, int jc0, int jc1)
     return gx * gy;
 }
 
+// ---------------------------------------------------------------------------
+// read/write extents of the fused passes (pgmg_internal.h, check_span)
+// ---------------------------------------------------------------------------
+// Every span below restates the kernel's own loop bounds: a band of coarse rows
+// [jcb, jce) streams fine rows 2jcb - lead .. 2jcb - lead + ceil((2(jce - jcb) + extra) / R)
+// * R - 1 (k_pre: lead 4, extra 8, R 4; k_post: 2, 4, 4; k_postpre_lds: 6, 11, 2), and wave w
+// of a 120-column tiling reads columns 120w - 3 .. 120w + 124 unless it is idle
+// (120w - 3 + 4 > N - 2).
+static inline long long fdiv2(long long v) { return v >= 0 ? v / 2 : -((1 - v) / 2); }
+
+struct Span {
+    long long r0, r1;   // fine rows (inclusive)
+    bool any;
+};
+
+static Span band_rows(int jc0, int jc1, int r, int lead, int extra, int R)
+{
+    Span sp{0, -1, false};
+    if (jc1 <= jc0 || r <= 0) return sp;
+    const int nb = (jc1 - jc0 + r - 1) / r;
+    sp.r0 = 2LL * jc0 - lead;
+    for (int b = std::max(0, nb - 2); b < nb; ++b) {   // the last (full or short) bands
+        const int jcb = jc0 + b * r, jce = std::min(jcb + r, jc1);
+        const long long n = ((2LL * (jce - jcb) + extra + R - 1) / R) * R;
+        sp.r1 = std::max(sp.r1, 2LL * jcb - lead + n - 1);
+    }
+    sp.any = true;
+    return sp;
+}
+
+// last column read by a non-idle wave of k_pre / k_post (120-column stride, 4-column
+// margin: wave w covers 120w - 3 .. 120w + 124); -1 when every wave is idle
+static long long tile_col_hi(int N, int waves)
+{
+    const int wmax = std::min(waves - 1, (N - 3) / 120);
+    return wmax < 0 ? -1 : 120LL * wmax - 3 + 127;
+}
+
+#define PGMG_SPAN(o, P, r0, r1, c0, c1, what)                                                  \
+    do {                                                                                       \
+        const int e_ = check_span((o), (P), (int)sizeof(T), (r0), (r1), (c0), (c1), (what));   \
+        if (e_) return e_;                                                                     \
+    } while (0)
+
+// k_pre / k_pre_rare: x0 and f over the band rows, the PIN coarse rows, x2 and rc stores
+template <class T>
+static int pre_spans(const PreArgsT<T> &a, int t, int gx, int r, bool x0_read, bool f_read)
+{
+    const Span sp = band_rows(a.jc0, a.jc1, r, 4, 8, 4);
+    const long long chi = tile_col_hi(a.N, gx * (t / 64));
+    if (!sp.any || chi < 0) return PGMG_OK;
+    if (x0_read) PGMG_SPAN(a.x0, a.P, sp.r0, sp.r1, -3, chi, "k_pre x0");
+    if (f_read) PGMG_SPAN(a.f, a.P, sp.r0, sp.r1, -3, chi, "k_pre f");
+    if (a.pin_ec != nullptr)   // coarse rows i/2 .. i/2 + 2 of every 4-row iteration i
+        PGMG_SPAN(a.pin_ec, a.Pc, fdiv2(sp.r0), fdiv2(sp.r1 + 1 - 4) + 2, -2,
+                  fdiv2(chi - 2) + 1, "k_pre PIN coarse grid");
+    const int olo = std::max(2 * a.jc0, a.row_lo), ohi = std::min(2 * a.jc1, a.row_hi);
+    if (a.x2 != nullptr) PGMG_SPAN(a.x2, a.P, olo, ohi - 1, 1, a.N - 1, "k_pre x2");
+    const int clo = std::max(a.jc0, std::max(1, a.rc_lo));
+    const int chi2 = std::min(a.jc1, std::min(a.N / 2, a.rc_hi));
+    if (a.rc != nullptr) PGMG_SPAN(a.rc, a.Pc, clo, chi2 - 1, 1, a.Nc - 2, "k_pre rc");
+    return PGMG_OK;
+}
+
+// k_post / k_post_rare: phi (or f one row ahead, RECOMP), f, the coarse correction, x2
+template <class T>
+static int post_spans(const PostArgsT<T> &a, int t, int gx, int r, bool f_read)
+{
+    const Span sp = band_rows(a.jc0, a.jc1, r, 2, 4, 4);
+    const long long chi = tile_col_hi(a.N, gx * (t / 64));
+    if (!sp.any || chi < 0) return PGMG_OK;
+    if (a.pre_fired != nullptr) {   // RECOMP: f rows i_begin - 1 .. last + 1, phi not read
+        PGMG_SPAN(a.f, a.P, sp.r0 - 1, sp.r1 + 1, -3, chi, "k_post f (recompute)");
+    } else {
+        PGMG_SPAN(a.phi, a.P, sp.r0, sp.r1, -3, chi, "k_post phi");
+        if (f_read) PGMG_SPAN(a.f, a.P, sp.r0, sp.r1, -3, chi, "k_post f");
+    }
+    PGMG_SPAN(a.ec, a.Pc, fdiv2(sp.r0), fdiv2(sp.r1 + 1 - 4) + 2, -2, fdiv2(chi - 2) + 1,
+              "k_post coarse correction");
+    const int olo = std::max(2 * a.jc0, a.row_lo), ohi = std::min(2 * a.jc1, a.row_hi);
+    if (a.x2 != nullptr) PGMG_SPAN(a.x2, a.P, olo, ohi - 1, 1, a.N - 1, "k_post x2");
+    return PGMG_OK;
+}
+
+// k_postpre_lds (and its smooth(3) form, coarse = false): each block loads its window of
+// row pairs through buffer descriptors (columns L0 .. L0 + 2 nvx - 1, coarse columns
+// cc0 .. cc0 + nve - 1; the descriptor range stops them at the grid's last column)
+template <class T>
+static int postpre_spans(const PostPreArgsT<T> &a, int t, int gx, int r, bool coarse)
+{
+    const Span sp = band_rows(a.jc0, a.jc1, r, 6, 11, kPPR);
+    if (!sp.any) return PGMG_OK;
+    const int wpb = t / 64;
+    const int npairs = (kPPStride * wpb + 2 * kPPMargin) / 2;
+    const int ncc = (kPPStride / 2) * wpb + kPPMargin + 2;
+    long long c1 = -1, e0 = 0, e1 = -1;
+    bool first = true;
+    for (int bx = 0; bx < gx; ++bx) {
+        const int L0 = kPPStride * wpb * bx + 1 - kPPMargin;
+        const int nvx = std::max(0, std::min(npairs, (a.N - 1 - L0) / 2 + 1));
+        if (nvx > 0) c1 = std::max(c1, (long long)L0 + 2 * nvx - 1);
+        const int cc0 = (L0 - 1) >> 1;
+        const int nve = std::max(0, std::min(ncc, a.Nc - cc0));
+        if (nve > 0) {
+            e0 = first ? cc0 : std::min(e0, (long long)cc0);
+            e1 = std::max(e1, (long long)cc0 + nve - 1);
+            first = false;
+        }
+    }
+    const long long c0 = 1 - kPPMargin;
+    if (c1 < c0) return PGMG_OK;
+    PGMG_SPAN(a.phi, a.P, sp.r0, sp.r1, c0, c1, "k_postpre phi");
+    if (a.gfx == nullptr) PGMG_SPAN(a.f, a.P, sp.r0, sp.r1, c0, c1, "k_postpre f");
+    if (coarse && e1 >= e0)   // coarse rows m0 .. m0 + ng of a band (m0 = jcb - 3)
+        PGMG_SPAN(a.ec, a.Pc, a.jc0 - 3, fdiv2(sp.r1 + 1), e0, e1, "k_postpre coarse correction");
+    const int olo = std::max(2 * a.jc0, a.row_lo), ohi = std::min(2 * a.jc1, a.row_hi);
+    PGMG_SPAN(a.x4, a.P, olo, ohi - 1, 1, a.N - 1, "k_postpre x4");
+    if (coarse && a.rc != nullptr) {
+        const int clo = std::max(a.jc0, std::max(1, a.rc_lo));
+        const int chi = std::min(a.jc1, std::min(a.N / 2, a.rc_hi));
+        PGMG_SPAN(a.rc, a.Pc, clo, chi - 1, 1, a.Nc - 2, "k_postpre rc");
+    }
+    return PGMG_OK;
+}
+
 // The finest level gets its own kernel symbols (FINE) so rocprofv3 statistics
 // isolate the roofline kernels.
 template <class T>
-void launch_pre(const PreArgsT<T> &a0, bool x0_zero, bool fine, hipStream_t s)
+int launch_pre(const PreArgsT<T> &a0, bool x0_zero, bool fine, hipStream_t s)
 {
     int t, gx, gy, r;
     fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r);
+    if (const int e = pre_spans(a0, t, gx, r, !x0_zero && a0.pin_ec == nullptr, a0.gfx == nullptr))
+        return e;
     PreArgsT<T> a = a0;
     a.rows_per_block = r;
     // non-temporal stores on the finest level only (its x2 is read again a level-pass later;
@@ -1071,13 +1199,15 @@ void launch_pre(const PreArgsT<T> &a0, bool x0_zero, bool fine, hipStream_t s)
     } else {
         k_pre<T, false, false, 2><<<g, b, 0, s>>>(a);
     }
+    return PGMG_OK;
 }
 
 template <class T>
-void launch_post(const PostArgsT<T> &a0, bool fine, hipStream_t s)
+int launch_post(const PostArgsT<T> &a0, bool fine, hipStream_t s)
 {
     int t, gx, gy, r;
     fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r);
+    if (const int e = post_spans(a0, t, gx, r, a0.gfx == nullptr)) return e;
     PostArgsT<T> a = a0;
     a.rows_per_block = r;
     // fine k_post: 1.01 -> 0.93 ms with non-temporal stores
@@ -1089,6 +1219,7 @@ void launch_post(const PostArgsT<T> &a0, bool fine, hipStream_t s)
     else if (rec) k_post<T, false, 2, true><<<g, b, 0, s>>>(a);
     else if (a.gfx != nullptr) k_post<T, false, 2, false, true><<<g, b, 0, s>>>(a);
     else k_post<T, false, 2, false><<<g, b, 0, s>>>(a);
+    return PGMG_OK;
 }
 
 // k_postpre's grid target: 3072 workgroups = 6 full rounds of the 512 that are resident
@@ -1115,11 +1246,12 @@ int postpre_blocks(int N, int jc0, int jc1)
 // only by the next cycle's pass; r01: 1.18 vs 1.20 ms; non-temporal rc stores no gain).
 // Every launch path below launches: there is no configuration that returns without the pass.
 template <class T>
-void launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
+int launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
 {
     int t, gx, gy, r;
     fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, kPPStride, pp_target(a0.jc0, a0.jc1),
                    kPPWaves);
+    if (const int e = postpre_spans(a0, t, gx, r, true)) return e;
     PostPreArgsT<T> a = a0;
     a.rows_per_block = r;
     const dim3 g(gx, gy), b(t);
@@ -1131,6 +1263,7 @@ void launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
         if (genf) k_postpre_lds<T, false, true, 2><<<g, b, 0, s>>>(a);
         else k_postpre_lds<T, false, false, 2><<<g, b, 0, s>>>(a);
     }
+    return PGMG_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -1141,15 +1274,17 @@ void launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
 // the untouched x0.  Used by the F-cycle climb on the levels below the finest.
 // ---------------------------------------------------------------------------
 template <class T>
-void launch_smooth4(const PostPreArgsT<T> &a0, hipStream_t s)
+int launch_smooth4(const PostPreArgsT<T> &a0, hipStream_t s)
 {
     int t, gx, gy, r;
     fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, kPPStride, pp_target(a0.jc0, a0.jc1),
                    kPPWaves);
+    if (const int e = postpre_spans(a0, t, gx, r, false)) return e;
     PostPreArgsT<T> a = a0;
     a.rows_per_block = r;
     if (a.gfx != nullptr) k_postpre_lds<T, true, true, 64><<<dim3(gx, gy), dim3(t), 0, s>>>(a);
     else k_postpre_lds<T, true, false, 64><<<dim3(gx, gy), dim3(t), 0, s>>>(a);
+    return PGMG_OK;
 }
 
 __device__ __forceinline__ double block_sum_strided(const double *p, int n, double *red)
@@ -1483,10 +1618,11 @@ static int fixup_blocks(int N, int row_lo, int row_hi)
 // that finds the check did not fire returns at once).  f is streamed (the stored f is
 // valid whenever a pass regenerates it in-kernel).
 template <class T>
-void launch_pre_rare(const FixArgsF &f, const PreArgsT<T> &a0, bool x0_zero, hipStream_t s)
+int launch_pre_rare(const FixArgsF &f, const PreArgsT<T> &a0, bool x0_zero, hipStream_t s)
 {
     int t, gx, gy, r;
     fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r);
+    if (const int e = pre_spans(a0, t, gx, r, !x0_zero && a0.pin_ec == nullptr, true)) return e;
     PreArgsT<T> a = a0;
     a.rows_per_block = r;
     a.gfx = a.gsy = nullptr;
@@ -1495,13 +1631,15 @@ void launch_pre_rare(const FixArgsF &f, const PreArgsT<T> &a0, bool x0_zero, hip
     if (x0_zero) k_pre_rare<T, true, 2, false><<<g, b, 0, s>>>(a, f);
     else if (a.pin_ec != nullptr) k_pre_rare<T, false, 2, true><<<g, b, 0, s>>>(a, f);
     else k_pre_rare<T, false, 2, false><<<g, b, 0, s>>>(a, f);
+    return PGMG_OK;
 }
 
 template <class T>
-void launch_post_rare(const FixArgsF &f, const PostArgsT<T> &a0, hipStream_t s)
+int launch_post_rare(const FixArgsF &f, const PostArgsT<T> &a0, hipStream_t s)
 {
     int t, gx, gy, r;
     fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r);
+    if (const int e = post_spans(a0, t, gx, r, true)) return e;
     PostArgsT<T> a = a0;
     a.rows_per_block = r;
     a.gfx = a.gsy = nullptr;
@@ -1509,6 +1647,7 @@ void launch_post_rare(const FixArgsF &f, const PostArgsT<T> &a0, hipStream_t s)
     const dim3 g(gx, gy), b(t);
     if (a.pre_fired != nullptr) k_post_rare<T, 2, true><<<g, b, 0, s>>>(a, f);
     else k_post_rare<T, 2, false><<<g, b, 0, s>>>(a, f);
+    return PGMG_OK;
 }
 
 template <class T>
@@ -1525,15 +1664,15 @@ void launch_post_fixup(const FixArgsF &a, const PostArgsT<T> &p, hipStream_t s)
 }
 
 #define PGMG_INSTANTIATE(T)                                                                       \
-    template void launch_pre<T>(const PreArgsT<T> &, bool, bool, hipStream_t);                   \
-    template void launch_post<T>(const PostArgsT<T> &, bool, hipStream_t);                       \
-    template void launch_postpre<T>(const PostPreArgsT<T> &, hipStream_t);                       \
-    template void launch_smooth4<T>(const PostPreArgsT<T> &, hipStream_t);                        \
+    template int launch_pre<T>(const PreArgsT<T> &, bool, bool, hipStream_t);                   \
+    template int launch_post<T>(const PostArgsT<T> &, bool, hipStream_t);                       \
+    template int launch_postpre<T>(const PostPreArgsT<T> &, hipStream_t);                       \
+    template int launch_smooth4<T>(const PostPreArgsT<T> &, hipStream_t);                        \
     template void launch_smooth4_finish<T>(const PostPreArgsT<T> &, int, const double *, double, \
                                            unsigned *, unsigned long long *, hipStream_t);       \
     template void launch_pre_fixup<T>(const FixArgsF &, const PreArgsT<T> &, bool, hipStream_t);  \
-    template void launch_pre_rare<T>(const FixArgsF &, const PreArgsT<T> &, bool, hipStream_t);   \
-    template void launch_post_rare<T>(const FixArgsF &, const PostArgsT<T> &, hipStream_t);       \
+    template int launch_pre_rare<T>(const FixArgsF &, const PreArgsT<T> &, bool, hipStream_t);   \
+    template int launch_post_rare<T>(const FixArgsF &, const PostArgsT<T> &, hipStream_t);       \
     template void launch_post_fixup<T>(const FixArgsF &, const PostArgsT<T> &, hipStream_t);
 PGMG_INSTANTIATE(double)
 PGMG_INSTANTIATE(float)

@@ -73,6 +73,21 @@ constexpr int kBlock = 256;       // threads per block for streaming kernels (4 
 constexpr int kTailThreads = PGMG_TAIL_THREADS;   // the tail workgroup (wave-0 paths fit 128 VGPRs)
 constexpr int kTailMaxN = 65;     // largest level the LDS-resident tail holds
 
+// Allocation registry and read/write span checks (DESIGN.md §2 "Read extents").  Every
+// level grid (alloc_grid) is registered; the launch wrappers of the fused passes compute,
+// from the band geometry the kernel itself uses, the first and last row and column they
+// read or write in each array, and check_span verifies that the span lies inside ONE
+// registered allocation before the pass is launched (PGMG_ERR_STATE, nothing launched,
+// otherwise).  The passes deliberately read rows past their band and columns past their
+// tiles (halos, tile margins); this turns a wrong halo or pitch assumption into an error
+// code on the host instead of a GPU memory fault.
+void register_alloc(const void *base, size_t bytes);
+void unregister_alloc(const void *base);
+// rows [r0, r1] x columns [c0, c1] (inclusive) of the array with virtual origin o (element
+// (0,0)), pitch P elements of es bytes; o == nullptr: nothing to check
+int check_span(const void *o, long long P, int es, long long r0, long long r1, long long c0,
+               long long c1, const char *what);
+
 inline int pitch_for(int N) { return (N + 15) / 16 * 16; }
 inline size_t alloc_elems(int rows, int N) { return (size_t)kOff + (size_t)rows * pitch_for(N) + 64; }
 

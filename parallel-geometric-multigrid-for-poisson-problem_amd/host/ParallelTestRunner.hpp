@@ -10,6 +10,8 @@
 #pragma once
 #include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstring>
 #include <filesystem>
 #include <fstream>
 #include <iostream>
@@ -19,6 +21,7 @@
 
 #include "Parallel_Method.hpp"
 #include "Parallel_Mg.hpp"
+#include "SequentialOps.hpp"
 
 namespace pgmg_host {
 
@@ -62,6 +65,36 @@ inline void save_pairs(const std::string &path, const std::vector<std::pair<int,
     for (auto &t : v) f << t.first << " " << t.second << "\n";
 }
 
+// FNV-64 of phi's IEEE words, row-major (the checksum of tests/golden/cycles.json and of
+// pgmg_solution_hash)
+inline unsigned long long fnv64(const std::vector<double> &v)
+{
+    unsigned long long h = 1469598103934665603ull;   // the fixtures' offset (oracle/ref_harness.cpp)
+    for (double d : v) {
+        unsigned long long w;
+        std::memcpy(&w, &d, sizeof(w));
+        h = (h ^ w) * 1099511628211ull;
+    }
+    return h;
+}
+
+// save_vector_err_file.hpp:63-83: the length, then one component per line (default
+// ostream precision), into OUTPUT_RESULT/ERR_VECTOR/iteration_last_gpu.txt
+inline void save_errors_vector_to_file_last_iteration_gpu(
+    const std::vector<std::vector<double>> &err_vect_iteration)
+{
+    std::filesystem::create_directories("./OUTPUT_RESULT/ERR_VECTOR");
+    for (const auto &v : err_vect_iteration) {
+        std::ofstream file("./OUTPUT_RESULT/ERR_VECTOR/iteration_last_gpu.txt");
+        if (!file.is_open()) {
+            std::cerr << "Unable to open file for writing Jacobian errors.\n";
+            continue;
+        }
+        file << v.size() << "\n";
+        for (double e : v) file << e << "\n";
+    }
+}
+
 inline void save_triples(const std::string &path, const std::vector<std::tuple<int, int, double>> &v)
 {
     std::ofstream f(path);
@@ -77,9 +110,11 @@ class ParallelTestRunner {
     int alpha;
     int mg_max_iterations;
     int num_thread = 32;    // globals.cpp:6; reported in the per-op timing files only
+    bool print_hash = false;  // gpu_exec --hash: one "phi FNV-64" line per cycle run
     std::vector<double> err_vec;
-    std::vector<std::tuple<int, int, double>> time_residual_gpu, time_jacobi_gpu,
-        time_restriction_gpu, time_prolungator_gpu;
+    std::vector<std::tuple<int, int, double>> time_residual_cpu, time_residual_gpu,
+        time_jacobi_cpu, time_jacobi_gpu, time_restriction_cpu, time_restriction_gpu,
+        time_prolungator_cpu, time_prolungator_gpu;
 
     ParallelTestRunner(int n, int mg_iterations, int alp)
         : N(n), alpha(alp), mg_max_iterations(mg_iterations) {}
@@ -102,8 +137,18 @@ class ParallelTestRunner {
     double run_v_cycle() { return run_cycle(false, false); }
     double run_w_cycle(bool err_vector) { return run_cycle(true, err_vector); }
 
-    // ParallelTestRunner.cu:98-125 (GPU side; the CPU side of the reference's
-    // comparison belongs to mg_cpu_exec and is not part of this library)
+    // ParallelTestRunner.cu:143-150: W-cycles per N, the last one's error vector
+    // phi - u saved for plot_cpu_vs_gpu_last_error.py
+    void run_w_cycles_err_vector_iteration(const std::vector<int> &N_list)
+    {
+        for (int n : N_list) {
+            N = n;
+            run_w_cycle(true);
+        }
+    }
+
+    // ParallelTestRunner.cu:98-125 with save_to_file.hpp:62-89: every op timed on the
+    // MI355X and, for N < 4096, sequentially on the host (SequentialOps.hpp)
     void plotTimeSequentialVsParallel(const std::vector<int> &N_list,
                                       const std::vector<int> &N_thread_list)
     {
@@ -116,9 +161,13 @@ class ParallelTestRunner {
             }
         }
         std::filesystem::create_directories("OUTPUT_RESULT");
+        pgmg_host::save_triples("OUTPUT_RESULT/timings_residual_cpu.txt", time_residual_cpu);
         pgmg_host::save_triples("OUTPUT_RESULT/timings_residual_gpu.txt", time_residual_gpu);
+        pgmg_host::save_triples("OUTPUT_RESULT/timings_jacobi_cpu.txt", time_jacobi_cpu);
         pgmg_host::save_triples("OUTPUT_RESULT/timings_jacobi_gpu.txt", time_jacobi_gpu);
+        pgmg_host::save_triples("OUTPUT_RESULT/timings_restriction_cpu.txt", time_restriction_cpu);
         pgmg_host::save_triples("OUTPUT_RESULT/timings_restriction_gpu.txt", time_restriction_gpu);
+        pgmg_host::save_triples("OUTPUT_RESULT/timings_prolungator_cpu.txt", time_prolungator_cpu);
         pgmg_host::save_triples("OUTPUT_RESULT/timings_prolungator_gpu.txt", time_prolungator_gpu);
     }
 
@@ -139,12 +188,18 @@ class ParallelTestRunner {
         }
         auto t1 = std::chrono::high_resolution_clock::now();
         const double secs = std::chrono::duration<double>(t1 - t0).count();
-        if (err_vector) {
+        if (err_vector) {   // ParallelTestRunner.cu:207-214
             err_vec.resize(L);
             for (size_t k = 0; k < L; ++k) err_vec[k] = phi[k] - x_true[k];
+            pgmg_host::save_errors_vector_to_file_last_iteration_gpu({err_vec});
         }
         std::cout << "  Final Relative L2 Error: " << pgmg_host::rel_l2_error(phi, x_true) << std::endl;
         std::cout << "  Elapsed Time: " << secs << " seconds\n";
+        if (print_hash) {
+            char buf[32];
+            std::snprintf(buf, sizeof(buf), "%016llx", pgmg_host::fnv64(phi));
+            std::cout << "  phi FNV-64: " << buf << "\n";
+        }
         return secs;
     }
 
@@ -157,7 +212,7 @@ class ParallelTestRunner {
         return std::chrono::duration<double>(t1 - t0).count();
     }
 
-    // ParallelTestRunner.cu:231-468 (GPU halves), with the correct coarse/fine sizes
+    // ParallelTestRunner.cu:231-468 (GPU and CPU halves), with the correct coarse/fine sizes
     // (the reference passes N/2 and 2N)
     void run_all_methods()
     {
@@ -170,11 +225,23 @@ class ParallelTestRunner {
         x.upload(zeros.data());
         fd.upload(f.data());
         r.upload(zeros.data());
+        const int Nc = (N - 1) / 2 + 1;
+        const bool cpu = N < 4096;   // the reference times the host side below 4096 only
+        if (cpu) {
+            std::vector<double> xh(zeros), rh(zeros), ch((size_t)Nc * Nc, 0.0), fine(zeros);
+            time_residual_cpu.push_back({num_thread, N, time_op([&] {
+                pgmg_seq::residual(rh.data(), xh.data(), f.data(), N, N, h); })});
+            time_jacobi_cpu.push_back({num_thread, N, time_op([&] {
+                pgmg_seq::jacobi(xh.data(), f.data(), N, N, h, 100, epsilon); })});
+            time_restriction_cpu.push_back({num_thread, N, time_op([&] {
+                pgmg_seq::restrict_full_weighting(f.data(), ch.data(), N, Nc); })});
+            time_prolungator_cpu.push_back({num_thread, N, time_op([&] {
+                pgmg_seq::prolongation(fine.data(), ch.data(), N, Nc); })});
+        }
         time_residual_gpu.push_back(
             {num_thread, N, time_op([&] { Parallel::ComputeResidual(r.get(), x.get(), fd.get(), N, N, h); })});
         time_jacobi_gpu.push_back(
             {num_thread, N, time_op([&] { Parallel::ComputeJacobi(x.get(), fd.get(), N, N, h, 100); })});
-        const int Nc = (N - 1) / 2 + 1;
         std::vector<double> zc((size_t)Nc * Nc, 0.0);
         pgmg_host::DeviceArray c((size_t)Nc * Nc);
         c.upload(zc.data());

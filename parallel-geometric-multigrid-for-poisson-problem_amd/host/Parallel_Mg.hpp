@@ -7,9 +7,11 @@
 // (2_part_MG/MultiGrid.hpp:57-136: 2+2 Jacobi sweeps with the per-sweep early exit,
 // recursion to N = 5) — bit-identical to mg_cpu_exec, unlike the reference GPU path
 // (in-place racy Jacobi, symmetric prolongation, CPU tail for N <= 17).
-// The context (level pyramid in HBM) is created on first use for a given N and kept.
+// The context (level pyramid in HBM) is created on first use for a given (N, h, epsilon)
+// and kept; h is the caller's finest mesh width, doubled per level as the reference does.
 #pragma once
 #include <memory>
+#include <stdexcept>
 
 #include "pgmg.hpp"
 
@@ -34,16 +36,17 @@ class ParallelMultiGridSolver {
   private:
     int alpha;
     int ctx_N = 0;
-    double ctx_eps = 0.0;
+    double ctx_eps = 0.0, ctx_h = 0.0;
     std::unique_ptr<pgmg_host::Context> ctx;
 
     void cycle(double *phi, double *f, int N, double h, bool w)
     {
-        (void)h;  // h = 1/(N-1) is implied by N (the context derives it exactly so)
-        if (!ctx || ctx_N != N || ctx_eps != epsilon) {
-            ctx.reset(new pgmg_host::Context(N, alpha, epsilon));
+        if (!(h > 0.0)) throw std::invalid_argument("ParallelMultiGridSolver: h must be > 0");
+        if (!ctx || ctx_N != N || ctx_eps != epsilon || ctx_h != h) {
+            ctx.reset(new pgmg_host::Context(N, alpha, epsilon, h));
             ctx_N = N;
             ctx_eps = epsilon;
+            ctx_h = h;
         }
         pgmg_ctx *c = ctx->get();
         pgmg_host::check(pgmg_set_problem(c, phi, f), "pgmg_set_problem");

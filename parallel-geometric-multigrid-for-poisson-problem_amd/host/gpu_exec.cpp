@@ -3,8 +3,11 @@
 // same stdout and OUTPUT_RESULT/timings_parallel_{v,w}_cycle.txt.
 //
 //   gpu_exec                       # the reference's default run
-//   gpu_exec --n 513,1025 --cycles 1 --alpha 3 [--ops]
-// --ops additionally runs the per-op timing study (plotTimeSequentialVsParallel).
+//   gpu_exec --n 513,1025 --cycles 1 --alpha 3 [--ops] [--hash] [--err-vector 8193]
+// --ops additionally runs the per-op timing study (plotTimeSequentialVsParallel);
+// --hash prints phi's FNV-64 after every cycle run (the golden fixtures' checksum);
+// --err-vector N,... runs main.cu:44-47's GPU block instead of the default run
+// (run_w_cycles_err_vector_iteration -> OUTPUT_RESULT/ERR_VECTOR/iteration_last_gpu.txt).
 #include <cstdlib>
 #include <cstring>
 #include <iostream>
@@ -19,7 +22,8 @@ int main(int argc, char **argv)
     std::vector<int> N_thread_list = {16, 32};                        // main.cu:4
     int mg_max_iterations = 3;                                        // main.cu:17
     int alpha = 3;                                                    // main.cu:15
-    bool ops = false;
+    bool ops = false, hash = false;
+    std::vector<int> err_list;
     for (int i = 1; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--n") && i + 1 < argc) {
             N_list.clear();
@@ -32,13 +36,26 @@ int main(int argc, char **argv)
             alpha = std::atoi(argv[++i]);
         } else if (!std::strcmp(argv[i], "--ops")) {
             ops = true;
+        } else if (!std::strcmp(argv[i], "--hash")) {
+            hash = true;
+        } else if (!std::strcmp(argv[i], "--err-vector") && i + 1 < argc) {
+            std::stringstream ss(argv[++i]);
+            std::string tok;
+            while (std::getline(ss, tok, ',')) err_list.push_back(std::atoi(tok.c_str()));
         } else {
-            std::cerr << "usage: " << argv[0] << " [--n 33,65,...] [--cycles K] [--alpha A] [--ops]\n";
+            std::cerr << "usage: " << argv[0]
+                      << " [--n 33,65,...] [--cycles K] [--alpha A] [--ops] [--hash]"
+                         " [--err-vector N,...]\n";
             return 2;
         }
     }
     try {
         ParallelTestRunner parallel_runner(0, mg_max_iterations, alpha);
+        parallel_runner.print_hash = hash;
+        if (!err_list.empty()) {
+            parallel_runner.run_w_cycles_err_vector_iteration(err_list);
+            return 0;
+        }
         if (ops) parallel_runner.plotTimeSequentialVsParallel(N_list, N_thread_list);
         parallel_runner.run_all_cycles(N_list);
     } catch (const std::exception &e) {

@@ -46,12 +46,14 @@ class DeviceArray {
 // RAII multigrid context
 class Context {
   public:
-    Context(int N, int alpha, double eps)
+    // h <= 0: the context's own a / (N - 1)
+    Context(int N, int alpha, double eps, double h = 0.0)
     {
         pgmg_config cfg;
         check(pgmg_config_default(&cfg, N), "pgmg_config_default");
         cfg.alpha = alpha;
         cfg.eps = eps;
+        if (h > 0.0) cfg.h0 = h;
         check(pgmg_create(&c_, &cfg), "pgmg_create");
     }
     ~Context()

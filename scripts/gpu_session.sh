@@ -21,10 +21,10 @@ run() {  # name, limit, command...
 for s in $STEPS; do
   case $s in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) run tests 900 python -m pytest tests -m gpu -q -rf ;;
+    tests) run tests 1000 python -u -m pytest tests -m gpu -v -rf --timeout 300 --timeout-method thread ;;
     strips) run strips 400 python -m pytest tests/test_gpu_strips.py -m gpu -q -rf -x ;;
     fcycle) run fcycle 600 python -m pytest tests/test_gpu_fcycle.py -m gpu -q -rf ;;
-    tests-fast) run tests 600 python -m pytest tests -m "gpu and not slow" -q -rf ;;
+    tests-fast) run tests 600 python -u -m pytest tests -m "gpu and not slow" -v -rf --timeout 200 --timeout-method thread ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
     fp32) run fp32 600 python -m pytest tests/test_gpu_fp32.py -m gpu -q -rf ;;
     bench32) run bench32 600 python bench.py --steps 20 --warmup 3 --dtype f32 --cpu-baseline off ;;

@@ -25,10 +25,7 @@ def norm_name(n):
     if not m:
         return n
     t = (m.group(2) or "").replace(" ", "")
-    # drop the prefetch-depth template argument (last int) for k_pre/k_post
-    t = re.sub(r",\d+>$", ">", t)
-    if m.group(1) == "k_postpre_lds":   # <T, R2, GENF, depth, occupancy, mode, frecomp>
-        t = "<" + ",".join(t.strip("<>").split(",")[:3]) + ">"
+    # the full template argument list, as bench.py's symbol keys spell it
     return m.group(1) + t
 
 
@@ -73,7 +70,11 @@ def main(tag, N=16385):
         kernels.append({"kernel": k, "N": N, "fetch_size_kib": fetch, "write_size_kib": write,
                         "hbm_bytes_per_launch": b,
                         "avg_ms_rocprof": stats.get(k)})
-    summary = {"tag": tag, "N": N,
+    import hashlib
+    lib = ROOT / "parallel-geometric-multigrid-for-poisson-problem_amd" / "libpgmg.so"
+    build = ("libpgmg.so sha256:" + hashlib.sha256(lib.read_bytes()).hexdigest()[:16]
+             if lib.exists() else None)
+    summary = {"tag": tag, "N": N, "build": build,
                "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
                          "bytes = 2*FETCH_SIZE + WRITE_SIZE (KiB), gfx950 read correction",
                "kernels": kernels}

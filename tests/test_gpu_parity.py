@@ -214,18 +214,21 @@ def test_op_rhs_bitwise(pgmg, oracle_mod):
     assert_bitwise(f.cpu().numpy(), oracle_mod.Oracle().rhs(N), "rhs")
 
 
-def test_symmetric_prolongation_mode(pgmg):
-    """gpu_exec's prolungator_kernel (Parallel_Method.cu:79-138): symmetric, boundary := 0."""
+@pytest.mark.parametrize("N", [9, 33, 129, 1025])
+def test_symmetric_prolongation_kat(pgmg, oracle_mod, N):
+    """gpu_exec's prolungator_kernel (Parallel_Method.cu:79-138; symmetric, boundary := 0):
+    pgmg_prolong(mode=PGMG_PROLONG_SYMMETRIC) on random coarse and fine grids (boundary
+    included) is bitwise the oracle's restatement (orc_prolong_sym, the whole grid covered)."""
     import torch
-    c = torch.zeros((5, 5), dtype=torch.float64, device="cuda:0")
-    c[1:4, 1:4] = 1.0
-    fine = torch.zeros((9, 9), dtype=torch.float64, device="cuda:0")
-    pgmg.ops.prolong(c, fine, mode=pgmg.PGMG_PROLONG_SYMMETRIC)
+    rng = np.random.default_rng(1000 + N)
+    Nc = (N - 1) // 2 + 1
+    c = rng.standard_normal((Nc, Nc))
+    f = rng.standard_normal((N, N))
+    ct = torch.tensor(c, device="cuda:0")
+    ft = torch.tensor(f, device="cuda:0")
+    pgmg.ops.prolong(ct, ft, mode=pgmg.PGMG_PROLONG_SYMMETRIC)
     torch.cuda.synchronize()
-    f = fine.cpu().numpy()
-    assert np.all(f[0] == 0) and np.all(f[-1] == 0) and np.all(f[:, 0] == 0)
-    assert np.all(f[2:7, 2:7] == 1.0)
-    assert f[1, 1] == 0.25 and f[1, 2] == 0.5 and f[7, 7] == 0.25
+    assert_bitwise(ft.cpu().numpy(), oracle_mod.prolong_sym(f, c), f"prolong_sym N={N}")
 
 
 @pytest.mark.slow
