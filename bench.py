@@ -54,7 +54,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--reps", type=int, default=5, help="timed repetitions (median reported)")
-    ap.add_argument("--n", type=int, default=16385, help="points per side (2^k+1)")
+    ap.add_argument("--n", "--N", dest="n", type=int, default=16385,
+                    help="points per side (2^k+1); --N under torch.distributed.run")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-n", type=int, default=0, help="grid for the CPU sample (default = --n)")
     ap.add_argument("--cycle", choices=["V", "W", "F"], default="V",
@@ -248,7 +249,11 @@ def main():
     # PGMG_BENCH_SOLO=1 (harness test on a one-GPU box only): every rank on device 0 with the
     # null transport (PGMG_FLAG_SOLO: no messages, results meaningless); the line says so
     solo = world > 1 and os.environ.get("PGMG_BENCH_SOLO") == "1"
-    device = 0 if (world == 1 or solo) else local_rank
+    # PGMG_BENCH_TRANSPORT=host (harness test on a one-GPU box): every rank on device 0, the
+    # strips' messages through the host-staged transport over the gloo group
+    # (PGMG_FLAG_HOST_TRANSPORT): a real multi-process solve, parity-checked, not a timing
+    host_tp = world > 1 and not solo and os.environ.get("PGMG_BENCH_TRANSPORT") == "host"
+    device = 0 if (world == 1 or solo or host_tp) else local_rank
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(device)
@@ -269,7 +274,9 @@ def main():
 
     def new_solver(flags):
         kw = dict(device=device, dtype=args.dtype)
-        if world > 1:   # a fresh RCCL communicator per context
+        if host_tp:
+            kw.update(transport=pg.HostTransport(), rank=rank, world=world)
+        elif world > 1:   # a fresh RCCL communicator per context
             t = torch.tensor(list(pg.unique_id()) if rank == 0 else [0] * 128, dtype=torch.uint8)
             dist.broadcast(t, 0)
             kw.update(rank=rank, world=world, uid=bytes(t.tolist()))
@@ -398,7 +405,10 @@ def main():
                 "N": n, "bulk_levels": bulk, "tail_top": tail_top,
                 "parallelism": "single-gpu" if world == 1 else (
                     f"row-strips x{world} (SOLO null transport on one GPU: harness test, "
-                    f"not a measurement)" if solo else f"row-strips x{world} (RCCL halos)"),
+                    f"not a measurement)" if solo else
+                    f"row-strips x{world} (host-staged transport over gloo, every rank on "
+                    f"GPU 0: harness test of the multi-process solve, not a measurement)"
+                    if host_tp else f"row-strips x{world} (RCCL halos)"),
             },
             "repetitions": {"count": len(main_leg["times"]),
                             "ms_per_step": [round(t * 1e3 / args.steps, 4) for t in main_leg["times"]],

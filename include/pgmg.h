@@ -100,6 +100,31 @@ extern "C" {
                                        on the fly                                      */
 #define PGMG_FLAG_NO_R2 1024u       /* F-cycle: one full-weighting level per restriction
                                        pass instead of two                             */
+#define PGMG_FLAG_HOST_TRANSPORT 2048u /* world > 1 without RCCL: nccl_unique_id points to
+                                       a pgmg_host_transport; every message and reduction
+                                       is staged through host memory and handed to the
+                                       caller's functions (MPI, torch.distributed/gloo,
+                                       ...; several ranks may share one GPU)           */
+
+/* The caller's transport for PGMG_FLAG_HOST_TRANSPORT.  Every function is called by all
+ * ranks in the same order (collective, blocking) and returns 0 on success; any other value
+ * fails the library call with PGMG_ERR_COMM.
+ *   exchange: one group of point-to-point messages: send send_bytes[i] bytes of host
+ *     buffer send_buf[i] to rank send_peer[i], receive recv_bytes[i] bytes from
+ *     recv_peer[i] into recv_buf[i]; messages between two ranks match in posting order
+ *     (the semantics of the RCCL path's grouped ncclSend/ncclRecv).
+ *   allreduce_sum_f64: v[i] = sum over ranks, in place; the sum taken in rank order
+ *     (0.0 + v_0 + v_1 + ...) keeps every rank's decisions identical and equal to the
+ *     in-process loopback transport's.
+ *   allreduce_min_u32: v[i] = min over ranks, in place. */
+typedef struct pgmg_host_transport {
+    void *user;
+    int (*exchange)(void *user, int nsend, const int *send_peer, const void *const *send_buf,
+                    const unsigned long long *send_bytes, int nrecv, const int *recv_peer,
+                    void *const *recv_buf, const unsigned long long *recv_bytes);
+    int (*allreduce_sum_f64)(void *user, double *v, int n);
+    int (*allreduce_min_u32)(void *user, unsigned *v, int n);
+} pgmg_host_transport;
 
 typedef struct pgmg_config {
     int N;             /* points per side incl. boundary; 2^k + 1, k >= 2        */

@@ -21,7 +21,7 @@ from ._capi import (PGMG_FLAG_LOOPBACK, PGMG_FLAG_NO_CROSS, PGMG_FLAG_NO_GRAPH,
                     PGMG_FLAG_STORED_RHS, PGMG_FLAG_EXACT_DIST, PGMG_FLAG_SOLO,
                     PGMG_FLAG_TIME_FINE, PGMG_PRECISION_FP32, PGMG_PRECISION_FP64,
                     PGMG_FLAG_UNFUSED, PGMG_FLAG_NO_RECOMPUTE, PGMG_FLAG_NO_PIN,
-                    PGMG_FLAG_NO_R2, PGMG_PROLONG_REFERENCE,
+                    PGMG_FLAG_NO_R2, PGMG_FLAG_HOST_TRANSPORT, PGMG_PROLONG_REFERENCE,
                     PGMG_PROLONG_SYMMETRIC, PGMG_OK, PGMG_ERR_STATE, PgmgConfig, PgmgError,
                     check, load)
 
@@ -34,6 +34,7 @@ __all__ = [
     "PGMG_PROLONG_SYMMETRIC", "PGMG_PRECISION_FP64", "PGMG_PRECISION_FP32",
     "PGMG_FLAG_STORED_RHS", "PGMG_FLAG_EXACT_DIST", "PGMG_FLAG_SOLO",
     "PGMG_FLAG_NO_RECOMPUTE", "PGMG_FLAG_NO_PIN", "PGMG_FLAG_NO_R2",
+    "PGMG_FLAG_HOST_TRANSPORT", "HostTransport",
 ]
 
 
@@ -100,6 +101,9 @@ def unique_id():
     return bytes(buf)
 
 
+from .hostcomm import HostTransport  # noqa: E402
+
+
 class LoopbackHub:
     """In-process rank hub: `world` Solvers in threads of one process share one GPU
     (test transport for the strip decomposition; RCCL refuses two ranks per device)."""
@@ -128,8 +132,10 @@ class Solver:
     numerics of MultigridSolver (2_part_MG/MultiGrid.hpp:57-136).
     """
 
-    def __init__(self, N, hub=None, uid=None, dtype="f64", **cfg):
+    def __init__(self, N, hub=None, uid=None, dtype="f64", transport=None, **cfg):
         """hub: LoopbackHub (ranks as threads on one GPU); uid: 128-byte RCCL unique id;
+        transport: a HostTransport (ranks as processes, messages through the caller's
+        torch.distributed group, staged in host memory);
         dtype: "f64" (bit-exact to mg_cpu_exec) or "f32" (PGMG_PRECISION_FP32)."""
         self.lib = load()
         if dtype not in ("f64", "f32"):
@@ -139,6 +145,12 @@ class Solver:
             cfg["flags"] = cfg.get("flags", 0) | PGMG_FLAG_LOOPBACK
             cfg["world"] = hub.world
             cfg["nccl_unique_id"] = hub.h
+        elif transport is not None:
+            self._transport = transport   # the callbacks must outlive the context
+            cfg["flags"] = cfg.get("flags", 0) | PGMG_FLAG_HOST_TRANSPORT
+            cfg.setdefault("world", transport.world)
+            cfg.setdefault("rank", transport.rank)
+            cfg["nccl_unique_id"] = C.cast(C.pointer(transport.struct), C.c_void_p)
         elif uid is not None:
             self._uid = (C.c_ubyte * 128)(*uid)
             cfg["nccl_unique_id"] = C.cast(self._uid, C.c_void_p)

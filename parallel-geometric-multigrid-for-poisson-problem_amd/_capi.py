@@ -33,9 +33,23 @@ PGMG_FLAG_SOLO = 128
 PGMG_FLAG_NO_RECOMPUTE = 256
 PGMG_FLAG_NO_PIN = 512
 PGMG_FLAG_NO_R2 = 1024
+PGMG_FLAG_HOST_TRANSPORT = 2048
 
 PGMG_PRECISION_FP64 = 0
 PGMG_PRECISION_FP32 = 1
+
+
+# pgmg_host_transport (include/pgmg.h): the caller's message functions
+HT_EXCHANGE = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_void_p),
+                          C.POINTER(C.c_ulonglong), C.c_int, C.POINTER(C.c_int),
+                          C.POINTER(C.c_void_p), C.POINTER(C.c_ulonglong))
+HT_SUM_F64 = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int)
+HT_MIN_U32 = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint), C.c_int)
+
+
+class PgmgHostTransport(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("exchange", HT_EXCHANGE),
+                ("allreduce_sum_f64", HT_SUM_F64), ("allreduce_min_u32", HT_MIN_U32)]
 
 
 class PgmgConfig(C.Structure):

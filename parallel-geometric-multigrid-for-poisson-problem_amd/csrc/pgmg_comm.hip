@@ -313,6 +313,92 @@ class LoopbackTransport : public Transport {
     }
 };
 
+// Host-staged transport (PGMG_FLAG_HOST_TRANSPORT): the caller's functions move the
+// messages (MPI, torch.distributed/gloo, ...), so ranks in separate processes can run the
+// strip decomposition without RCCL — several of them on one GPU, which RCCL refuses.  Each
+// group waits for the stream, copies the send buffers to host, calls exchange(), copies the
+// received bytes back; the reductions likewise.  A correctness path, not a fast one.
+class HostTransport : public Transport {
+  public:
+    const pgmg_host_transport *ht;
+    struct Pend {
+        bool is_send;
+        void *buf;
+        size_t bytes;
+        int peer;
+    };
+    std::vector<Pend> pend;
+    std::vector<std::vector<unsigned char>> stage;
+    explicit HostTransport(const pgmg_host_transport *h) : ht(h) {}
+    int group_start() override
+    {
+        pend.clear();
+        return PGMG_OK;
+    }
+    int send(const void *buf, size_t bytes, int peer, hipStream_t) override
+    {
+        pend.push_back({true, const_cast<void *>(buf), bytes, peer});
+        return PGMG_OK;
+    }
+    int recv(void *buf, size_t bytes, int peer, hipStream_t) override
+    {
+        pend.push_back({false, buf, bytes, peer});
+        return PGMG_OK;
+    }
+    int group_end(hipStream_t s) override
+    {
+        std::vector<Pend> p;
+        p.swap(pend);
+        PGMG_HIPC(hipStreamSynchronize(s));   // the send buffers are final on the stream
+        stage.resize(p.size());
+        std::vector<int> speer, rpeer;
+        std::vector<const void *> sbuf;
+        std::vector<void *> rbuf;
+        std::vector<unsigned long long> sbytes, rbytes;
+        for (size_t i = 0; i < p.size(); ++i) {
+            stage[i].resize(p[i].bytes);
+            if (p[i].is_send) {
+                if (p[i].bytes)
+                    PGMG_HIPC(hipMemcpy(stage[i].data(), p[i].buf, p[i].bytes, hipMemcpyDeviceToHost));
+                speer.push_back(p[i].peer);
+                sbuf.push_back(stage[i].data());
+                sbytes.push_back(p[i].bytes);
+            } else {
+                rpeer.push_back(p[i].peer);
+                rbuf.push_back(stage[i].data());
+                rbytes.push_back(p[i].bytes);
+            }
+        }
+        if (ht->exchange(ht->user, (int)speer.size(), speer.data(), sbuf.data(), sbytes.data(),
+                         (int)rpeer.size(), rpeer.data(), rbuf.data(), rbytes.data()) != 0)
+            return set_err(PGMG_ERR_COMM, "host transport: exchange failed");
+        for (size_t i = 0; i < p.size(); ++i)
+            if (!p[i].is_send && p[i].bytes)
+                PGMG_HIPC(hipMemcpy(p[i].buf, stage[i].data(), p[i].bytes, hipMemcpyHostToDevice));
+        return PGMG_OK;
+    }
+    int allreduce_sum(double *d, int n, hipStream_t s) override
+    {
+        std::vector<double> v(n);
+        PGMG_HIPC(hipMemcpyAsync(v.data(), d, n * sizeof(double), hipMemcpyDeviceToHost, s));
+        PGMG_HIPC(hipStreamSynchronize(s));
+        if (ht->allreduce_sum_f64(ht->user, v.data(), n) != 0)
+            return set_err(PGMG_ERR_COMM, "host transport: allreduce_sum_f64 failed");
+        PGMG_HIPC(hipMemcpy(d, v.data(), n * sizeof(double), hipMemcpyHostToDevice));
+        return PGMG_OK;
+    }
+    int allreduce_min_u32(unsigned *d, int n, hipStream_t s) override
+    {
+        std::vector<unsigned> v(n);
+        PGMG_HIPC(hipMemcpyAsync(v.data(), d, n * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+        PGMG_HIPC(hipStreamSynchronize(s));
+        if (ht->allreduce_min_u32(ht->user, v.data(), n) != 0)
+            return set_err(PGMG_ERR_COMM, "host transport: allreduce_min_u32 failed");
+        PGMG_HIPC(hipMemcpy(d, v.data(), n * sizeof(unsigned), hipMemcpyHostToDevice));
+        return PGMG_OK;
+    }
+};
+
 // Null transport (PGMG_FLAG_SOLO, measurement only): no messages, allreduces return the
 // local values.  One rank of a world-W decomposition runs alone on one GPU, so its
 // compute time per cycle can be measured without W GPUs.
@@ -494,13 +580,26 @@ Comm *Comm::create(pgmg_ctx *c, int *rc)
         return sc;
     }
     if (!cfg.nccl_unique_id) {
-        *rc = set_err(PGMG_ERR_ARG, "world > 1 needs nccl_unique_id (or a loopback hub)");
+        *rc = set_err(PGMG_ERR_ARG,
+                      "world > 1 needs nccl_unique_id (or a loopback hub / host transport)");
+        return nullptr;
+    }
+    if ((cfg.flags & PGMG_FLAG_LOOPBACK) && (cfg.flags & PGMG_FLAG_HOST_TRANSPORT)) {
+        *rc = set_err(PGMG_ERR_ARG, "PGMG_FLAG_LOOPBACK and PGMG_FLAG_HOST_TRANSPORT exclude each other");
         return nullptr;
     }
     auto *sc = new StripComm();
     sc->me = cfg.rank;
     sc->world = cfg.world;
-    if (cfg.flags & PGMG_FLAG_LOOPBACK) {
+    if (cfg.flags & PGMG_FLAG_HOST_TRANSPORT) {
+        auto *ht = (const pgmg_host_transport *)cfg.nccl_unique_id;
+        if (!ht->exchange || !ht->allreduce_sum_f64 || !ht->allreduce_min_u32) {
+            *rc = set_err(PGMG_ERR_ARG, "pgmg_host_transport: null function");
+            delete sc;
+            return nullptr;
+        }
+        sc->t = new HostTransport(ht);
+    } else if (cfg.flags & PGMG_FLAG_LOOPBACK) {
         auto *hub = (LoopbackHub *)cfg.nccl_unique_id;
         if (hub->world != cfg.world) {
             *rc = set_err(PGMG_ERR_ARG, "loopback hub world mismatch");

@@ -649,6 +649,9 @@ struct Blk {
 
 constexpr int kPPR = 2;   // rows per LDS slot (a row pair)
 
+#ifndef PGMG_PP_DEPTH
+#define PGMG_PP_DEPTH 2   // row pairs of loads in flight per wave (register sets)
+#endif
 #ifndef PGMG_PP_NTL
 #define PGMG_PP_NTL 0     // 1: non-temporal row loads (measurement builds)
 #endif
@@ -773,10 +776,12 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
         sx[sl][q][j] = T(0);
         if constexpr (!GENF) sf[sl][q][j] = T(0);
     }
-    // two register sets: pair p's loads go to set p % 2, issued two pairs ahead
-    constexpr int D = 2;
-    V2<T> pxA[R], pfA[R], pxB[R], pfB[R];
-    T peA = T(0), peB = T(0);
+    // D register sets: pair p's loads go to set p % D, issued D pairs ahead (D = 2: sets
+    // A, B; D = 3: A, B, C)
+    constexpr int D = PGMG_PP_DEPTH;
+    static_assert(D == 2 || D == 3, "PGMG_PP_DEPTH is 2 or 3");
+    V2<T> pxA[R], pfA[R], pxB[R], pfB[R], pxC[R], pfC[R];   // C unused (dead) when D = 2
+    T peA = T(0), peB = T(0), peC = T(0);
     auto load_pair = [&](int p, V2<T> (&px)[R], V2<T> (&pf)[R], T &pe) {
         #pragma unroll
         for (int q = 0; q < R; ++q) {
@@ -802,7 +807,12 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     if (t < ncc) se[ring(m0)][t] = buf_one<T>(a.ec + (long long)m0 * Pc + cc0, nve, t);
     store_pair(0, pxA, pfA, peA);
     if (ng > 1) load_pair(1, pxB, pfB, peB);
-    if (ng > 2) load_pair(2, pxA, pfA, peA);
+    if constexpr (D == 3) {
+        if (ng > 2) load_pair(2, pxC, pfC, peC);
+        if (ng > 3) load_pair(3, pxA, pfA, peA);
+    } else {
+        if (ng > 2) load_pair(2, pxA, pfA, peA);
+    }
     __syncthreads();
 
     // pair gi: compute from slot gi & 1; pair gi+1 (set (gi+1) & 1) -> the other slot;
@@ -896,9 +906,17 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
         }
         __syncthreads();
     };
-    for (int gi = 0; gi < ng; gi += 2) {
-        step(gi, pxB, pfB, peB);
-        if (gi + 1 < ng) step(gi + 1, pxA, pfA, peA);
+    if constexpr (D == 3) {
+        for (int gi = 0; gi < ng; gi += 3) {
+            step(gi, pxB, pfB, peB);
+            if (gi + 1 < ng) step(gi + 1, pxC, pfC, peC);
+            if (gi + 2 < ng) step(gi + 2, pxA, pfA, peA);
+        }
+    } else {
+        for (int gi = 0; gi < ng; gi += 2) {
+            step(gi, pxB, pfB, peB);
+            if (gi + 1 < ng) step(gi + 1, pxA, pfA, peA);
+        }
     }
     const int slot = bk.y * gridDim.x + bk.x;
     const double s1 = fused_block_sum(acc1, red);
