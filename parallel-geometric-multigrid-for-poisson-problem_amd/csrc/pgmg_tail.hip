@@ -10,7 +10,9 @@
 // Semantics are exactly MultigridSolver::v_cycle / w_cycle (MultiGrid.hpp:57-136)
 // with JacobiSmoother::smooth (Smoother.hpp:38-116), including the per-sweep
 // residual-norm early exit, evaluated sequentially (no speculation needed here).
+#include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "pgmg_internal.h"
 
@@ -37,6 +39,11 @@ constexpr bool kTailW17 = PGMG_TAIL_W17 != 0 && kTailW9;
 #define PGMG_TAIL_W33 0  // 1: the 33x33 level too (16 points a lane: 256 VGPRs + 512 B of spills; off)
 #endif
 constexpr bool kTailW33 = PGMG_TAIL_W33 != 0 && kTailW17;
+#ifndef PGMG_TAIL_ROWS
+#define PGMG_TAIL_ROWS 1  // block-team smoothing of the 65x65 / 33x33 levels with the iterate
+                          // in registers, one row per lane set (tail_smooth_rows); 0: tail_jacobi
+#endif
+constexpr bool kTailRows = PGMG_TAIL_ROWS != 0;
 
 template <class Real>
 struct TailLevel {
@@ -224,6 +231,136 @@ __device__ __forceinline__ Cnt tail_smooth_small(Real *x, const Real *f, const T
     return Cnt{sweeps, exits};
 }
 
+// Block-team smoother of an NN x NN level (NN = 33, 65) with the iterate in registers.
+// Wave w owns the rows j0 = 1 + RPW*w .. j0 + RPW - 1 with RPW = (NN - 1) / waves, so the
+// waves cover rows 1 .. NN-1 exactly and the last wave's last row is the boundary row NN-1
+// (passed through): every wave holds RPW rows and no register array is indexed at run time.
+// Lane l holds column l (NN = 65: column 64, a boundary column, is a per-row register of
+// every lane); left/right neighbours are DPP moves across the wave.  The rows above and
+// below the wave: for sweep 1 and sweep 2 (with the check of x_1) ghost rows the wave
+// computes itself (x_0 rows j0-2 .. j0+RPW read from the grid, x_1 on rows j0-1 and j0+RPW);
+// from sweep 3 on, the neighbouring waves' edge rows exchanged through LDS (scratch T,
+// double-buffered) in the same barrier that publishes the wave partials of the check.  A
+// smoother call with num_iter = 1 (2 sweeps) thus has one barrier for its check and one
+// after the write-back (tail_jacobi: two passes over the grid in LDS and a block sum per
+// sweep).  Expressions, operand order and the fused check are tail_smooth's.
+template <class Real, int NN>
+__device__ __forceinline__ Cnt tail_smooth_rows(Real *x, const Real *f, const TailLevel<Real> &L,
+                                                int num_iter, double eps, Real *T, double *red,
+                                                int &par)
+{
+    static_assert((NN - 1) % kTailWaves == 0, "waves must tile rows 1 .. NN-1");
+    constexpr int RPW = (NN - 1) / kTailWaves;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int j0 = 1 + RPW * w;
+    const bool act = lane < NN;                         // lane holds a column of the grid
+    const bool bcol = lane == 0 || lane == NN - 1;      // boundary column: passthrough
+    const Real hh = L.hh, ih = L.ih;
+    const bool first = w == 0, last = w == kTailWaves - 1;
+    auto ld = [&](int j) { return (act && j >= 0 && j < NN) ? x[j * NN + lane] : Real(0); };
+    // NN = 65: column 64 (right boundary, constant while smoothing) of row j
+    auto ldb = [&](int j) { return (NN == 65 && j >= 0 && j < NN) ? x[j * NN + 64] : Real(0); };
+    Real xr[RPW], hf[RPW], fr[RPW], xb[RPW];
+    bool brow[RPW];   // the grid's last row (last wave only): passed through, not checked
+    #pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        const int j = j0 + r;
+        brow[r] = j == NN - 1;
+        xr[r] = ld(j);
+        fr[r] = act ? f[j * NN + lane] : Real(0);
+        hf[r] = hh * fr[r];
+        xb[r] = ldb(j);
+    }
+    // rows j0-2, j0-1 above and j0+RPW, j0+RPW+1 below (rows past the grid are never used:
+    // the first wave's row above is the boundary row 0, the last wave's last row is one)
+    const Real gu2 = ld(j0 - 2), gu = ld(j0 - 1), gd = ld(j0 + RPW), gd2 = ld(j0 + RPW + 1);
+    const Real bu = ldb(j0 - 1), bd = ldb(j0 + RPW);
+    const Real fu = (act && !first) ? f[(j0 - 1) * NN + lane] : Real(0);
+    const Real fd = (act && !last) ? f[(j0 + RPW) * NN + lane] : Real(0);
+    // edge-row exchange buffer: [par][wave][first, last][64] (T holds 4 * kTailWaves * 64,
+    // tail_lds_bytes)
+    auto hbuf = [&](int pp, int ww, int side) { return T + ((pp * kTailWaves + ww) * 2 + side) * 64; };
+    int hp = 0;
+    auto put_edges = [&](const Real (&v)[RPW]) {
+        hbuf(hp, w, 0)[lane] = v[0];
+        hbuf(hp, w, 1)[lane] = v[RPW - 1];
+    };
+    auto get_edges = [&](Real &up, Real &dn) {
+        up = first ? gu : hbuf(hp, max(w - 1, 0), 1)[lane];
+        dn = last ? Real(0) : hbuf(hp, min(w + 1, kTailWaves - 1), 0)[lane];
+    };
+    // J of one row (boundary columns passed through)
+    auto jrow = [&](Real c, Real u, Real d, Real hfv, Real rb, Real &lf, Real &rt) {
+        lf = dpp_shr(c);
+        rt = dpp_shl(c);
+        if (NN == 65 && lane == 63) rt = rb;
+        const Real o = Real(0.25) * (hfv + lf + rt + u + d);
+        return (bcol || !act) ? c : o;
+    };
+    // one sweep out = J(in) on this wave's rows; NORM: acc = sum r(in)^2 over its interior points
+    auto sweep = [&](const Real (&in)[RPW], Real (&out)[RPW], Real up, Real dn, auto norm_t) {
+        constexpr bool NORM = decltype(norm_t)::value;
+        double acc = 0.0;
+        #pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            const Real u = r == 0 ? up : in[r - 1];
+            const Real d = r + 1 < RPW ? in[r + 1] : dn;
+            const Real c = in[r];
+            Real lf, rt;
+            const Real o = jrow(c, u, d, hf[r], xb[r], lf, rt);
+            out[r] = brow[r] ? c : o;
+            if (NORM) {
+                const Real res = fr[r] - ih * (Real(4) * c - lf - rt - u - d);
+                acc += (act && !bcol && !brow[r]) ? sq(res) : 0.0;
+            }
+        }
+        return acc;
+    };
+    Real nx[RPW];
+    sweep(xr, nx, gu, gd, std::false_type{});
+    int sweeps = 1, exits = 0;
+    // x_1 on the ghost rows j0-1 and j0+RPW (the boundary row 0 stays as it is)
+    Real up, dn;
+    {
+        Real lf, rt;
+        const Real u1 = jrow(gu, gu2, xr[0], hh * fu, bu, lf, rt);
+        const Real d1 = jrow(gd, xr[RPW - 1], gd2, hh * fd, bd, lf, rt);
+        up = first ? gu : u1;
+        dn = last ? Real(0) : d1;
+    }
+    for (int k = 2; k <= num_iter + 1; ++k) {
+        // sweep k (x_k = J(x_{k-1})) and the check of x_{k-1}; ONE barrier publishes both
+        // the wave partials of the check (BlockTeam::sum's arithmetic) and x_k's edge rows
+        Real nn[RPW];
+        const double acc = wave_sum(sweep(nx, nn, up, dn, std::true_type{}));
+        double *rp = red + par * kTailWaves;
+        if (lane == 0) rp[w] = acc;
+        hp ^= 1;
+        put_edges(nn);
+        __syncthreads();
+        double sm = 0.0;
+        #pragma unroll
+        for (int i = 0; i < kTailWaves; ++i) sm += rp[i];
+        par ^= 1;
+        if (sm < eps) {
+            ++exits;
+            break;
+        }
+        get_edges(up, dn);
+        #pragma unroll
+        for (int r = 0; r < RPW; ++r) nx[r] = nn[r];
+        ++sweeps;
+    }
+    // everyone has read the grid (ghost rows) before anyone writes it: the check's barrier
+    // above, or this one when no check ran
+    if (num_iter < 1) __syncthreads();
+    #pragma unroll
+    for (int r = 0; r < RPW; ++r)
+        if (act && !brow[r]) x[(j0 + r) * NN + lane] = nx[r];
+    __syncthreads();
+    return Cnt{sweeps, exits};
+}
+
 // JacobiSmoother::smooth(x, f, N, N, h, num_iter): num_iter+1 sweeps, break as
 // soon as ||r(x_k)|| < eps, tested as sum r^2 < eps2 = norm2_threshold(eps) (no sqrt on
 // the dependent chain of every sweep; the same decisions, see pgmg_internal.h).  The check of x_k is fused into sweep k+1 (which
@@ -232,6 +369,10 @@ template <class Team, class Real>
 __device__ __forceinline__ Cnt tail_smooth(Real *x, const Real *f, const TailLevel<Real> &L,
                                            int num_iter, double eps, Real *T, double *red, int &par)
 {
+    if constexpr (Team::size == kTailThreads && kTailRows) {
+        if (L.N == 65) return tail_smooth_rows<Real, 65>(x, f, L, num_iter, eps, T, red, par);
+        if (L.N == 33) return tail_smooth_rows<Real, 33>(x, f, L, num_iter, eps, T, red, par);
+    }
     if constexpr (Team::size == 64) {
         const int nin = (L.N - 2) * (L.N - 2);
         if (!kTailSmallOff && nin <= 64) return tail_smooth_small<1>(x, f, L, num_iter, eps);
@@ -917,7 +1058,9 @@ size_t tail_lds_bytes(int N_top, int n_coarse)
         if (N <= n_coarse) break;
         N = (N - 1) / 2 + 1;
     }
-    return kTailRed * sizeof(double) + (2 * S + (size_t)N_top * N_top) * sizeof(Real);
+    // scratch T: one grid of the top level, and at least tail_smooth_rows' edge-row buffers
+    const size_t t = std::max((size_t)N_top * N_top, (size_t)kTailRows * 4 * kTailWaves * 64);
+    return kTailRed * sizeof(double) + (2 * S + t) * sizeof(Real);
 }
 
 // PGMG_TAIL_PROF=1 (measurement build libpgmg_ab.so only): the per-stage cycle counters
