@@ -73,15 +73,34 @@ class RcclTransport : public Transport {
   public:
     ncclComm_t comm = nullptr;
     double timeout_s = 600.0;
+    // the side communicator of the early finest-level halos (split from `comm`, driven on
+    // the comm's side stream); polled and aborted together with `comm`
+    RcclTransport *side = nullptr;
     ~RcclTransport() override
     {
         if (comm) ncclCommDestroy(comm);
     }
     int abort_with(const std::string &why)
     {
+        if (side && side->comm) {
+            ncclCommAbort(side->comm);
+            side->comm = nullptr;
+        }
         if (comm) ncclCommAbort(comm);
         comm = nullptr;
         return set_err(PGMG_ERR_COMM, why);
+    }
+    // a communicator for a second stream: operations on two streams of ONE communicator may
+    // interleave differently on different ranks
+    int split_into(RcclTransport &out)
+    {
+        if (!comm) return set_err(PGMG_ERR_COMM, "communicator aborted by an earlier error");
+        int rank = 0;
+        NCCLC(ncclCommUserRank(comm, &rank));
+        NCCLC(ncclCommSplit(comm, 0, rank, &out.comm, nullptr));
+        out.timeout_s = timeout_s;
+        side = &out;
+        return PGMG_OK;
     }
     // Poll the stream instead of blocking in hipStreamSynchronize: a peer that died or
     // stopped posting its sends would otherwise hang this rank forever.
@@ -98,6 +117,10 @@ class RcclTransport : public Transport {
             if (ncclCommGetAsyncError(comm, &ae) == ncclSuccess && ae != ncclSuccess &&
                 ae != ncclInProgress)
                 return abort_with(std::string("RCCL asynchronous error: ") + ncclGetErrorString(ae));
+            if (side && side->comm && ncclCommGetAsyncError(side->comm, &ae) == ncclSuccess &&
+                ae != ncclSuccess && ae != ncclInProgress)
+                return abort_with(std::string("RCCL asynchronous error (side communicator): ") +
+                                  ncclGetErrorString(ae));
             const double dt =
                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
             if (dt > timeout_s) return abort_with("RCCL wait timed out (pgmg_config.comm_timeout_s)");
@@ -418,11 +441,24 @@ class NullTransport : public Transport {
 class StripComm : public Comm {
   public:
     Transport *t = nullptr;
+    Transport *t2 = nullptr;     // the early halos' transport (RCCL: a split communicator;
+                                 // the others: t itself, which takes the stream per call)
     int me = 0, world = 1;
     int Ld = 0;                  // levels 0..Ld-1 distributed; Ld = first gathered level
     std::vector<int> split;      // finest-level split points s_0 .. s_world
+    hipStream_t side = nullptr;  // the early halos' stream
+    hipEvent_t ev_ready = nullptr, ev_done = nullptr;
+    bool pending = false;
 
-    ~StripComm() override { delete t; }
+    ~StripComm() override
+    {
+        if (side) (void)hipStreamSynchronize(side);
+        if (ev_ready) (void)hipEventDestroy(ev_ready);
+        if (ev_done) (void)hipEventDestroy(ev_done);
+        if (side) (void)hipStreamDestroy(side);
+        if (t2 != t) delete t2;
+        delete t;
+    }
     int gathered_level() const override { return Ld; }
     int rank() const override { return me; }
 
@@ -469,9 +505,39 @@ class StripComm : public Comm {
         return PGMG_OK;
     }
 
-    int setup(pgmg_ctx *) override { return PGMG_OK; }
+    int setup(pgmg_ctx *) override
+    {
+        PGMG_HIPC(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+        PGMG_HIPC(hipEventCreateWithFlags(&ev_ready, hipEventDisableTiming));
+        PGMG_HIPC(hipEventCreateWithFlags(&ev_done, hipEventDisableTiming));
+        if (!t2) t2 = t;
+        return PGMG_OK;
+    }
 
-    int halos(const HaloReq *reqs, int n, hipStream_t s) override
+    int halo_begin(const Grid &g, const Level &L, int depth, hipStream_t s) override
+    {
+        if (!side || pending) return halo(g, L, depth, s);
+        PGMG_HIPC(hipEventRecord(ev_ready, s));
+        PGMG_HIPC(hipStreamWaitEvent(side, ev_ready, 0));
+        const HaloReq r{&g, &L, depth};
+        const int e = halos_on(t2, &r, 1, side);
+        if (e) return e;
+        PGMG_HIPC(hipEventRecord(ev_done, side));
+        pending = true;
+        return PGMG_OK;
+    }
+
+    int halo_end(hipStream_t s) override
+    {
+        if (!pending) return PGMG_OK;
+        pending = false;
+        PGMG_HIPC(hipStreamWaitEvent(s, ev_done, 0));
+        return PGMG_OK;
+    }
+
+    int halos(const HaloReq *reqs, int n, hipStream_t s) override { return halos_on(t, reqs, n, s); }
+
+    int halos_on(Transport *t, const HaloReq *reqs, int n, hipStream_t s)
     {
         int e = t->group_start();
         if (e) return e;
@@ -612,6 +678,11 @@ Comm *Comm::create(pgmg_ctx *c, int *rc)
         if (cfg.comm_timeout_s > 0) rt->timeout_s = cfg.comm_timeout_s;
         sc->t = rt;
         *rc = rt->init(cfg.nccl_unique_id, cfg.world, cfg.rank);
+        if (!*rc) {
+            auto *r2 = new RcclTransport();
+            sc->t2 = r2;
+            *rc = rt->split_into(*r2);
+        }
         if (*rc) {
             delete sc;
             return nullptr;
@@ -663,13 +734,37 @@ int pgmg_rccl_selftest(const void *uid128, int device)
                 hipMemset(b, 0, n * sizeof(double)) != hipSuccess ||
                 hipMemcpy(u, hu, sizeof(hu), hipMemcpyHostToDevice) != hipSuccess))
         rc = pgmg::set_err(PGMG_ERR_HIP, "selftest upload");
+    // the early-halo pattern of the strips: a split communicator on a second stream that
+    // waits for the main stream's event, exchanging while the main stream works on
+    pgmg::RcclTransport t2;
+    hipStream_t s2 = nullptr;
+    hipEvent_t ev = nullptr, ev2 = nullptr;
+    double *c2 = nullptr;
+    if (!rc) rc = t.split_into(t2);
+    if (!rc && (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&ev2, hipEventDisableTiming) != hipSuccess ||
+                hipMalloc(&c2, n * sizeof(double)) != hipSuccess))
+        rc = pgmg::set_err(PGMG_ERR_HIP, "selftest side stream");
     if (!rc) rc = t.group_start();
     if (!rc) rc = t.send(a, n * sizeof(double), 0, s);
     if (!rc) rc = t.recv(b, n * sizeof(double), 0, s);
     if (!rc) rc = t.group_end(s);
+    if (!rc && (hipEventRecord(ev, s) != hipSuccess || hipStreamWaitEvent(s2, ev, 0) != hipSuccess))
+        rc = pgmg::set_err(PGMG_ERR_HIP, "selftest events");
+    if (!rc) rc = t2.group_start();
+    if (!rc) rc = t2.send(b, n * sizeof(double), 0, s2);
+    if (!rc) rc = t2.recv(c2, n * sizeof(double), 0, s2);
+    if (!rc) rc = t2.group_end(s2);
     if (!rc) rc = t.allreduce_sum(a, 3, s);
     if (!rc) rc = t.allreduce_min_u32(u, 4, s);
+    if (!rc && (hipEventRecord(ev2, s2) != hipSuccess || hipStreamWaitEvent(s, ev2, 0) != hipSuccess))
+        rc = pgmg::set_err(PGMG_ERR_HIP, "selftest events");
+    if (!rc) rc = t.wait(s);   // polls both communicators
     if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = pgmg::set_err(PGMG_ERR_HIP, "selftest sync");
+    if (!rc && (hipMemcpy(g.data(), c2, n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
+                std::memcmp(g.data(), h.data(), n * sizeof(double)) != 0))
+        rc = pgmg::set_err(PGMG_ERR_COMM, "selftest: the side communicator's rows differ");
     if (!rc && (hipMemcpy(g.data(), b, n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
                 hipMemcpy(gu, u, sizeof(gu), hipMemcpyDeviceToHost) != hipSuccess))
         rc = pgmg::set_err(PGMG_ERR_HIP, "selftest download");
@@ -686,7 +781,12 @@ int pgmg_rccl_selftest(const void *uid128, int device)
     (void)hipFree(a);
     (void)hipFree(b);
     (void)hipFree(u);
+    if (c2) (void)hipFree(c2);
+    if (ev) (void)hipEventDestroy(ev);
+    if (ev2) (void)hipEventDestroy(ev2);
+    if (s2) (void)hipStreamDestroy(s2);
     (void)hipStreamDestroy(s);
+    t.side = nullptr;   // t2 is destroyed first (declared later)
     return rc;
 }
 

@@ -162,6 +162,15 @@ class Comm {
         const HaloReq r{&g, &L, depth};
         return halos(&r, 1, s);
     }
+    // The same exchange started early: as soon as stream s reaches this point (the rows to
+    // send are final), on a side stream of the comm, overlapping whatever s does next;
+    // halo_end(s) makes s wait for it.  Used for the finest level's halos, which are final
+    // a whole coarse hierarchy before they are read.  Default: exchange in place on s.
+    virtual int halo_begin(const Grid &g, const Level &L, int depth, hipStream_t s)
+    {
+        return halo(g, L, depth, s);
+    }
+    virtual int halo_end(hipStream_t) { return 0; }
     // in-place sum of n device doubles over all ranks
     virtual int allreduce_sum(double *d, int n, hipStream_t s) = 0;
     // in-place element-wise minimum of n device unsigned ints over all ranks

@@ -548,12 +548,14 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         fa.global_sum = nullptr;
     }
     T *pr = B;  // pre-smoothed solution of the current cycle
+    // its halo rows (6 for k_postpre, 2 for the last k_post) are final now and read only
+    // after the whole coarse hierarchy: the exchange runs on the comm's side stream
+    // meanwhile (the coarse correction's halo rows are computed locally, kPostExt)
+    if (dist && (e = c->comm->halo_begin(*grid_of(pr), L, 6, c->s))) return e;
     if ((e = enqueue_children<T>(c, 0, gamma))) return e;
     for (int k = 1; k < n; ++k) {
         T *nx = next_of(pr);
-        if (dist) {   // the coarse correction's halo rows were computed locally (kPostExt)
-            if ((e = c->comm->halo(*grid_of(pr), L, 6, c->s))) return e;
-        }
+        if (dist && (e = c->comm->halo_end(c->s))) return e;
         PostPreArgsT<T> q{};
         q.phi = pr;
         q.ec = G<T>(C.A);
@@ -584,6 +586,7 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         const double *g3 = nullptr;   // all-rank {post, pre, pre-from-x1} sums
         if (lean) {
             pr = nx;
+            if (dist && (e = c->comm->halo_begin(*grid_of(pr), L, 6, c->s))) return e;
             if ((e = enqueue_children<T>(c, 0, gamma))) return e;
             continue;
         }
@@ -636,12 +639,13 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         f2.force = 1;
         f2.stats = nullptr;
         launch_pre_fixup(f2, p3, false, c->s);
-        pr = nx;
+        pr = nx;   // final after the rare paths
+        if (dist && (e = c->comm->halo_begin(*grid_of(pr), L, 6, c->s))) return e;
         if ((e = enqueue_children<T>(c, 0, gamma))) return e;
     }
     // last cycle: post-smooth
     T *out = next_of(pr);
-    if (dist && (e = c->comm->halo(*grid_of(pr), L, 2, c->s))) return e;
+    if (dist && (e = c->comm->halo_end(c->s))) return e;
     PostArgsT<T> po = make_post<T>(c, pr, out);
     lp = chk_partials(c, np, 0);
     if (lp) po.partials = lp;

@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <map>
+#include <mutex>
 #include <vector>
 
 #include "pgmg_ctx.h"
@@ -29,22 +31,33 @@ struct OpScratch {
     size_t tmp_elems = 0;
 };
 
-OpScratch g_op;
+// One scratch set per stream: ops enqueued on different streams never share partial sums,
+// flags or the ping-pong buffer (the reference's ops are synchronous on the default stream;
+// these are asynchronous on the caller's).  Sets live for the process.
+std::mutex g_op_mu;
+std::map<hipStream_t, OpScratch> g_ops;
 
-int ensure_scratch(size_t tmp_elems)
+int ensure_scratch(hipStream_t s, size_t tmp_elems, OpScratch **out)
 {
-    if (!g_op.partials) {
-        HIPC(hipMalloc((void **)&g_op.partials, 4096 * sizeof(double)));
-        HIPC(hipMalloc((void **)&g_op.flags, (kMaxSweeps + 2) * 128 * sizeof(unsigned)));
-        HIPC(hipMalloc((void **)&g_op.stats, 4 * sizeof(unsigned long long)));
-        HIPC(hipMalloc((void **)&g_op.scalar, 4 * sizeof(double)));
+    std::lock_guard<std::mutex> lk(g_op_mu);
+    OpScratch &o = g_ops[s];
+    if (!o.partials) {
+        HIPC(hipMalloc((void **)&o.partials, 4096 * sizeof(double)));
+        HIPC(hipMalloc((void **)&o.flags, (kMaxSweeps + 2) * 128 * sizeof(unsigned)));
+        HIPC(hipMalloc((void **)&o.stats, 4 * sizeof(unsigned long long)));
+        HIPC(hipMalloc((void **)&o.scalar, 4 * sizeof(double)));
     }
-    if (tmp_elems > g_op.tmp_elems) {
-        if (g_op.tmp) HIPC(hipFree(g_op.tmp));
-        g_op.tmp = nullptr;
-        HIPC(hipMalloc((void **)&g_op.tmp, tmp_elems * sizeof(double)));
-        g_op.tmp_elems = tmp_elems;
+    if (tmp_elems > o.tmp_elems) {
+        if (o.tmp) {
+            HIPC(hipStreamSynchronize(s));   // the old buffer may still be in use on s
+            HIPC(hipFree(o.tmp));
+        }
+        o.tmp = nullptr;
+        o.tmp_elems = 0;
+        HIPC(hipMalloc((void **)&o.tmp, tmp_elems * sizeof(double)));
+        o.tmp_elems = tmp_elems;
     }
+    *out = &o;
     return PGMG_OK;
 }
 
@@ -59,8 +72,10 @@ int pgmg_jacobi(double *d_x, double *d_tmp, const double *d_f, int H, int W, dou
     hipStream_t s = (hipStream_t)stream;
     const size_t L = (size_t)H * W;
     const int S = v + 1;
-    int e = ensure_scratch(d_tmp ? 0 : L);
+    OpScratch *op = nullptr;
+    int e = ensure_scratch(s, d_tmp ? 0 : L, &op);
     if (e) return e;
+    OpScratch &g_op = *op;
     double *tmp = d_tmp ? d_tmp : g_op.tmp;
     const bool check = eps >= 0.0;
     // flag slots: a fresh block of S+1 words per call would need a ring; the op is
@@ -122,8 +137,10 @@ int pgmg_norm(const double *d_v, long long n, double *result, void *stream)
 {
     if (!d_v || n < 0 || !result) return set_err(PGMG_ERR_ARG, "pgmg_norm: bad argument");
     hipStream_t s = (hipStream_t)stream;
-    int e = ensure_scratch(0);
+    OpScratch *op = nullptr;
+    int e = ensure_scratch(s, 0, &op);
     if (e) return e;
+    OpScratch &g_op = *op;
     long long nb = (n + kBlock - 1) / kBlock;
     if (nb > 1024) nb = 1024;
     if (nb < 1) nb = 1;

@@ -214,6 +214,59 @@ def test_op_rhs_bitwise(pgmg, oracle_mod):
     assert_bitwise(f.cpu().numpy(), oracle_mod.Oracle().rhs(N), "rhs")
 
 
+def test_op_jacobi_concurrent_streams(pgmg, oracle_mod):
+    """The op-level API keeps one scratch set (partials, flags, ping-pong buffer) per stream:
+    smoothers of different problems enqueued on two streams at once, without syncs between
+    them, each equal to the oracle bit for bit (with one shared set, the second stream's
+    partial sums and early-exit flags overwrote the first's)."""
+    import torch
+    dev = torch.device("cuda:0")
+    probs = []
+    for seed, N, eps in ((1, 257, 1e-3), (2, 513, 1e-2)):
+        rng = np.random.default_rng(seed)
+        f = rng.uniform(-1, 1, (N, N))
+        f[0, :] = f[-1, :] = f[:, 0] = f[:, -1] = 0.0
+        h = 1.0 / (N - 1)
+        x = np.zeros((N, N))
+        n_ref = oracle_mod.Oracle(eps=eps).smooth(x, f, h, 40)
+        probs.append((N, h, eps, f, x, n_ref))
+    streams = [torch.cuda.Stream(device=dev) for _ in probs]
+    outs = []
+    for (N, h, eps, f, _, _), st in zip(probs, streams):
+        xt = torch.zeros((N, N), dtype=torch.float64, device=dev)
+        ft = torch.tensor(f, device=dev)
+        torch.cuda.synchronize()
+        outs.append((xt, ft, st))
+    # interleave: both ops enqueued before either is waited for
+    for rep in range(3):
+        for i, (xt, ft, st) in enumerate(outs):
+            N, h, eps, f, _, _ = probs[i]
+            xt.zero_()
+            torch.cuda.synchronize()
+            # sweeps_done = NULL: the op returns without waiting for its stream
+            pgmg.check(pgmg.load().pgmg_jacobi(C_ptr(xt), None, C_ptr(ft), N, N, h, 40, eps,
+                                               None, C_stream(st)), "pgmg_jacobi")
+        torch.cuda.synchronize()
+        for i, (xt, _, _) in enumerate(outs):
+            assert_bitwise(xt.cpu().numpy(), probs[i][4], f"stream {i} rep {rep}")
+    # and with the sweep count (synchronous form), per stream
+    for i, (xt, ft, st) in enumerate(outs):
+        N, h, eps, f, _, n_ref = probs[i]
+        xt.zero_()
+        torch.cuda.synchronize()
+        assert pgmg.ops.jacobi(xt, ft, h, 40, eps=eps, stream=C_stream(st)) == n_ref
+
+
+def C_stream(st):
+    import ctypes
+    return ctypes.c_void_p(st.cuda_stream)
+
+
+def C_ptr(t):
+    import ctypes
+    return ctypes.c_void_p(t.data_ptr())
+
+
 @pytest.mark.parametrize("N", [9, 33, 129, 1025])
 def test_symmetric_prolongation_kat(pgmg, oracle_mod, N):
     """gpu_exec's prolungator_kernel (Parallel_Method.cu:79-138; symmetric, boundary := 0):

@@ -1,8 +1,10 @@
 """GPU: the RCCL transport of the row-strip path, exercised for real on the one GPU of the
 test box.  RCCL refuses two ranks on one device, so the strip tests run over the loopback
 transport; this test drives the RCCL calls themselves (grouped ncclSend/ncclRecv,
-ncclAllReduce sum/double and min/u32 on a stream) through a world-1 communicator
-(pgmg_rccl_selftest, pgmg_comm.hip)."""
+ncclAllReduce sum/double and min/u32 on a stream) through a world-1 communicator, and the
+early finest-level halo's pattern: a communicator split off it (ncclCommSplit) exchanging
+on a second stream that waits for the first, while the first runs its reductions, both
+polled by one wait (pgmg_rccl_selftest, pgmg_comm.hip)."""
 import ctypes as C
 
 import pytest
