@@ -605,6 +605,21 @@ __device__ __forceinline__ V2<T> jsn(V2<T> up, V2<T> ce, V2<T> dn, Nbr<T> n, V2<
     }
     return o;
 }
+// jsn with the RHS term hh*f precomputed (hf): the same IEEE product, formed once per row
+// instead of once per sweep that reads the row
+template <class T, bool EDGE>
+__device__ __forceinline__ V2<T> jsh(V2<T> up, V2<T> ce, V2<T> dn, Nbr<T> n, V2<T> hf,
+                                       const Cols &k, bool brow)
+{
+    V2<T> o;
+    o.x = T(0.25) * (hf.x + n.l + ce.y + up.x + dn.x);
+    o.y = T(0.25) * (hf.y + ce.x + n.r + up.y + dn.y);
+    if constexpr (EDGE) {
+        if (brow || k.bx) o.x = ce.x;
+        if (brow || k.by) o.y = ce.y;
+    }
+    return o;
+}
 template <class T>
 __device__ __forceinline__ V2<T> rsn(V2<T> up, V2<T> ce, V2<T> dn, Nbr<T> n, V2<T> f, T ih)
 {
@@ -649,9 +664,19 @@ struct Blk {
 
 constexpr int kPPR = 2;   // rows per LDS slot (a row pair)
 
+// Row pairs of loads in flight per wave (register sets).  3 also makes the guard-free loop
+// body 6 rows, the period of the row windows (no window copies: 141 -> 129 VALU per row);
+// the fp64 instantiations with more live state (streamed f, the strips' third sum, the
+// F-cycle's four-sweep form) keep 2, which fits 256 VGPRs without spilling.
 #ifndef PGMG_PP_DEPTH
-#define PGMG_PP_DEPTH 2   // row pairs of loads in flight per wave (register sets)
+#define PGMG_PP_DEPTH 0   // 0: per instantiation as above; 2 or 3 forces it (A/B builds)
 #endif
+template <class T, bool R2, bool GENF, int OPT>
+constexpr int pp_depth()
+{
+    if constexpr (PGMG_PP_DEPTH != 0) return PGMG_PP_DEPTH;
+    return (sizeof(T) == 4 || (GENF && !R2 && !(OPT & 64))) ? 3 : 2;
+}
 #ifndef PGMG_PP_NTL
 #define PGMG_PP_NTL 0     // 1: non-temporal row loads (measurement builds)
 #endif
@@ -705,14 +730,74 @@ __device__ __forceinline__ T buf_one(const T *base, int n, int t)
         return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, t * 4, 0, 0));
 }
 
+// LDS-DMA ring of k_postpre_dma: 512 doubles per fine row (4 waves x 64 lanes x 16 B), 256
+// per coarse row (2 dword DMAs per wave), coarse rows m-1 .. m+K live
+constexpr int kDmaRow = 512;
+constexpr int kDmaCRow = 256;
+#ifndef PGMG_PP_DMA
+#define PGMG_PP_DMA 0     // > 0: the headline pass through k_postpre_dma with this ring depth
+#endif
+constexpr int kDmaCRing = (PGMG_PP_DMA > 0 ? PGMG_PP_DMA : 4) + 2;
+
+// LDS-DMA in inline asm: hipcc's own bookkeeping would wait vmcnt(0) before every LDS read
+// of the staging array (it cannot tell the slots apart); the waits are counted by hand.
+// M0 = the wave-uniform LDS byte address, written in the same statement.
+__device__ __forceinline__ unsigned lds_addr(const void *p)
+{
+    return (unsigned)(unsigned long long)(const __attribute__((address_space(3))) char *)p;
+}
+__device__ __forceinline__ void glds16(const void *g, const void *lds_wave_base)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_wave_base)))
+                 : "memory");
+}
+__device__ __forceinline__ void glds4(const void *g, const void *lds_wave_base)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_wave_base)))
+                 : "memory");
+}
+// wait until at most n (<= 31) vector-memory operations of this wave are outstanding.  Vector
+// memory operations complete in order on gfx9 (one counter for loads and stores), so every
+// operation older than the n youngest has completed
+#define PGMG_VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+__device__ __forceinline__ void vm_wait_n(int n)
+{
+    switch (n) {
+    PGMG_VMW(31) PGMG_VMW(30) PGMG_VMW(29) PGMG_VMW(28) PGMG_VMW(27) PGMG_VMW(26) PGMG_VMW(25)
+    PGMG_VMW(24) PGMG_VMW(23) PGMG_VMW(22) PGMG_VMW(21) PGMG_VMW(20) PGMG_VMW(19) PGMG_VMW(18)
+    PGMG_VMW(17) PGMG_VMW(16) PGMG_VMW(15) PGMG_VMW(14) PGMG_VMW(13) PGMG_VMW(12) PGMG_VMW(11)
+    PGMG_VMW(10) PGMG_VMW(9) PGMG_VMW(8) PGMG_VMW(7) PGMG_VMW(6) PGMG_VMW(5) PGMG_VMW(4)
+    PGMG_VMW(3) PGMG_VMW(2) PGMG_VMW(1)
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+}
+#undef PGMG_VMW
+// a barrier that leaves LDS-DMA in flight (__syncthreads() would wait vmcnt(0))
+__device__ __forceinline__ void raw_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 // The body of k_postpre_lds for one block.  EDGE = false: no row of the block's band and
 // no column of this wave is a boundary, so the Jacobi stages carry no passthrough selects.
-template <class T, bool R2, bool GENF, bool EDGE, int OPT>
+//
+// DMA = K > 0 (k_postpre_dma, fp64 / analytic f / one GPU): the rows come into LDS by LDS-DMA
+// (global_load_lds: no VGPR destination) into a ring of K row-pair slots, K - 1 pairs in
+// flight per wave instead of the register sets; waits counted by hand (see k_postpre_dma).
+template <class T, bool R2, bool GENF, bool EDGE, int OPT, int DMA = 0>
 __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const Cols &k,
                                                 double *red, T (&sx)[2][kPPR][kPPLdsRow],
                                                 T (&sf)[2][kPPR][GENF ? 1 : kPPLdsRow],
-                                                T (&se)[3][kPPLdsCoarse], const Blk bk)
+                                                T (&se)[3][kPPLdsCoarse], const Blk bk,
+                                                T *dl = nullptr)
 {
+    static_assert(DMA == 0 || (sizeof(T) == 8 && GENF && !R2 && OPT == 2), "DMA: the headline pass only");
     constexpr int R = kPPR;
     const int N = a.N, Nc = a.Nc;
     const long long P = a.P, Pc = a.Pc;
@@ -765,20 +850,34 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     V2<T> e0 = z, e1 = z, b0 = z, b1 = z, c0 = z, c1 = z, g0 = z, g1 = z, h0 = z, h1 = z,
             d0 = z, d1 = z;
     V2<T> f1 = z, f2 = z, f3 = z, f4 = z, f5 = z;  // f[i-1], f[i-2], ..., f[i-5]
+    V2<T> q1 = z, q2 = z, q3 = z, q4 = z;          // hh * f[i-1], ..., hh * f[i-4]
     double acc1 = 0.0, acc2 = 0.0, acc3 = 0.0;
     const int i_begin = 2 * jcb - 6;
     const int ng = (2 * (jce - jcb) + 11 + R - 1) / R;   // row pairs (uniform over the block)
     const int m0 = i_begin >> 1;                          // coarse row of the first pair
     auto ring = [](int m) { return (m + 3 * 4096) % 3; };  // m >= -3
 
-    if (t < 2 * R * 4) {   // the 4 pad doubles past the window (read by spare lanes only)
+    constexpr int KD = DMA > 0 ? DMA : 1;
+    // DMA ring: fine slot p = rows [p][q][kDmaRow], coarse ring after them (kDmaCRing rows)
+    T *const DX = dl;
+    T *const DE = dl + KD * R * kDmaRow;
+    auto xrow = [&](int slot, int q) -> const T * {
+        if constexpr (DMA > 0) return DX + (slot * R + q) * kDmaRow;
+        else return sx[slot][q];
+    };
+    auto dring = [](int m) { return (m + kDmaCRing * 4096) % kDmaCRing; };   // m >= -3
+    auto erow = [&](int m) -> const T * {
+        if constexpr (DMA > 0) return DE + dring(m) * kDmaCRow;
+        else return se[(m + 3 * 4096) % 3];
+    };
+    if (DMA == 0 && t < 2 * R * 4) {   // the 4 pad doubles past the window (spare lanes only)
         const int sl = t >> 3, q = (t >> 2) & 1, j = kPPLdsRow - 4 + (t & 3);
         sx[sl][q][j] = T(0);
         if constexpr (!GENF) sf[sl][q][j] = T(0);
     }
     // D register sets: pair p's loads go to set p % D, issued D pairs ahead (D = 2: sets
     // A, B; D = 3: A, B, C)
-    constexpr int D = PGMG_PP_DEPTH;
+    constexpr int D = pp_depth<T, R2, GENF, OPT>();
     static_assert(D == 2 || D == 3, "PGMG_PP_DEPTH is 2 or 3");
     V2<T> pxA[R], pfA[R], pxB[R], pfB[R], pxC[R], pfC[R];   // C unused (dead) when D = 2
     T peA = T(0), peB = T(0), peC = T(0);
@@ -802,6 +901,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
         }
         if (t < ncc) se[ring(m0 + p + 1)][t] = pe;
     };
+    if constexpr (DMA == 0) {
     // prologue: pair 0 (+ its first coarse row) into slot 0; pairs 1 .. D in flight
     load_pair(0, pxA, pfA, peA);
     if (t < ncc) se[ring(m0)][t] = buf_one<T>(a.ec + (long long)m0 * Pc + cc0, nve, t);
@@ -814,25 +914,63 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
         if (ng > 2) load_pair(2, pxA, pfA, peA);
     }
     __syncthreads();
+    }   // DMA == 0
+
+    // DMA: every lane issues every DMA (a wave's count of vector-memory operations per pair
+    // must be exactly 4 for the counted waits); lanes past the grid re-read its last valid
+    // pair (N - 2 is odd: 16-byte aligned) -- columns >= N never reach an owned result
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const T *const GX = a.phi + min(L0 + 2 * t, N - 2);
+    const int dmax = 2 * (Nc - 1 - cc0) + 1;   // coarse row: dword d = i * 256 + t, clamped
+    const char *const GE = reinterpret_cast<const char *>(a.ec + cc0);
+    const int ce0 = 4 * min(t, dmax), ce1 = 4 * min(256 + t, dmax);
+    auto issue_coarse = [&](int m) {
+        T *dst = DE + dring(m) * kDmaCRow;
+        const char *src = GE + (long long)m * Pc * 8;
+        glds4(src + ce0, dst + 32 * wv);
+        glds4(src + ce1, dst + 128 + 32 * wv);
+    };
+    auto issue_pair = [&](int p) {   // pair p's rows into slot p % DMA, its second coarse row
+        #pragma unroll
+        for (int q = 0; q < R; ++q)
+            glds16(GX + (long long)(i_begin + p * R + q) * P, DX + ((p % KD) * R + q) * kDmaRow + 128 * wv);
+        issue_coarse(m0 + p + 1);
+    };
+    if constexpr (DMA > 0) {
+        issue_coarse(m0);
+        for (int p = 0; p < DMA - 1; ++p)
+            if (p < ng) issue_pair(p);
+        // row m0 and pair 0 landed: the pairs issued after it may fly on
+        vm_wait_n(4 * (min(ng, DMA - 1) - 1));
+        raw_barrier();
+    }
 
     // pair gi: compute from slot gi & 1; pair gi+1 (set (gi+1) & 1) -> the other slot;
     // issue pair gi+3 into the set just freed; one barrier
     T wprev = T(0);   // dpp_shl(d2.x) of the previous restriction row (d0 starts as zero)
     auto step = [&](int gi, V2<T> (&px)[R], V2<T> (&pf)[R], T &pe) {
-        const int slot = gi & 1;
-        // the other slot's previous readers passed the last barrier: stage pair gi+1 (loaded
-        // two steps ago) first and reissue its register set for pair gi+3, so the loads in
-        // flight are never younger than this step's stores (counted waits stay small)
-        if (gi + 1 < ng) store_pair(gi + 1, px, pf, pe);
-        if (gi + 1 + D < ng) load_pair(gi + 1 + D, px, pf, pe);
+        // keep the scheduler inside one pair: interleaving the unrolled pairs only raises
+        // the register pressure (the loads of a pair are issued two pairs ahead anyway)
+        __builtin_amdgcn_sched_barrier(0);
+        const int slot = DMA > 0 ? gi % KD : (gi & 1);
+        if constexpr (DMA > 0) {
+            // into the slot of pair gi - 1, whose readers passed the last barrier
+            if (gi + DMA - 1 < ng) issue_pair(gi + DMA - 1);
+        } else {
+            // the other slot's previous readers passed the last barrier: stage pair gi+1
+            // (loaded two steps ago) first and reissue its register set for pair gi+3, so the
+            // loads in flight are never younger than this step's stores (counted waits stay small)
+            if (gi + 1 < ng) store_pair(gi + 1, px, pf, pe);
+            if (gi + 1 + D < ng) load_pair(gi + 1 + D, px, pf, pe);
+        }
         const int i = i_begin + gi * R;
         const int m = m0 + gi;
-        const T *E0 = se[ring(m)], *E1 = se[ring(m + 1)];
+        const T *E0 = erow(m), *E1 = erow(m + 1);
         const T cr0 = E0[co], crn0 = E0[co + 1], cr1 = E1[co], crn1 = E1[co + 1];
         #pragma unroll
         for (int s = 0; s < R; ++s) {
             const int ii = i + s;
-            const V2<T> xr = ldv(&sx[slot][s][xo]);
+            const V2<T> xr = ldv(xrow(slot, s) + xo);
             // f[ii]: from LDS, or (GENF) generated once here and carried in the f window
             // (regenerating it at every use instead: fewer VGPRs, 8 more multiplies per
             // row, measured slower in r01)
@@ -842,10 +980,12 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                 const double sy = gsy_s(a.gsy, ii);
                 f0 = mk2<T>((T)(fxa * sy), (T)(fxb * sy));
             }
-            const V2<T> fq1 = f1, fq2 = f2, fq3 = f3, fq4 = f4, fq5 = f5;
+            const V2<T> q0 = mk2<T>(hh * f0.x, hh * f0.y);
+            const V2<T> fq2 = f2, fq3 = f3, fq4 = f4, fq5 = f5;
+            const V2<T> hq1 = q1, hq2 = q2, hq3 = q3, hq4 = q4;
             const V2<T> e2 = (OPT & 64) ? xr : add_prolong<T, EDGE>(xr, ii, cr0, crn0, cr1, crn1, pc, Nc);
             // post-smooth sweep 1: x1 row ii-1
-            const V2<T> b2 = jsn<T, EDGE>(e0, e1, e2, nbr<T>(e1), fq1, hh, k, boundary_row(ii - 1, N));
+            const V2<T> b2 = jsh<T, EDGE>(e0, e1, e2, nbr<T>(e1), hq1, k, boundary_row(ii - 1, N));
             const Nbr<T> nb1 = nbr<T>(b1), nc1 = nbr<T>(c1), ng1 = nbr<T>(g1);
             {   // post check: r(x1) on row ii-2
                 const V2<T> r1 = rsn<T>(b0, b1, b2, nb1, fq2, ih);
@@ -856,7 +996,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                 }
             }
             // post-smooth sweep 2: x2 row ii-2 (= phi of cycle k+1)
-            const V2<T> c2 = jsn<T, EDGE>(b0, b1, b2, nb1, fq2, hh, k, boundary_row(ii - 2, N));
+            const V2<T> c2 = jsh<T, EDGE>(b0, b1, b2, nb1, hq2, k, boundary_row(ii - 2, N));
             if (R2) {   // r(x2) on row ii-3
                 const V2<T> r2 = rsn<T>(c0, c1, c2, nc1, fq3, ih);
                 const int row = ii - 3;
@@ -866,7 +1006,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                 }
             }
             // pre-smooth sweep 1: x3 row ii-3
-            const V2<T> g2 = jsn<T, EDGE>(c0, c1, c2, nc1, fq3, hh, k, boundary_row(ii - 3, N));
+            const V2<T> g2 = jsh<T, EDGE>(c0, c1, c2, nc1, hq3, k, boundary_row(ii - 3, N));
             {   // pre check: r(x3) on row ii-4
                 const V2<T> r3 = rsn<T>(g0, g1, g2, ng1, fq4, ih);
                 const int row = ii - 4;
@@ -876,7 +1016,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                 }
             }
             // pre-smooth sweep 2: x4 row ii-4 (stored)
-            const V2<T> h2 = jsn<T, EDGE>(g0, g1, g2, ng1, fq4, hh, k, boundary_row(ii - 4, N));
+            const V2<T> h2 = jsh<T, EDGE>(g0, g1, g2, ng1, hq4, k, boundary_row(ii - 4, N));
             // branch-free: rows outside the band get a zero-record descriptor, lanes that do
             // not own their pair an out-of-range offset (every step issues the same memory
             // instructions, so the compiler can count its waits)
@@ -903,15 +1043,38 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
             h0 = h1; h1 = h2;
             d0 = d1; d1 = d2;
             f5 = f4; f4 = f3; f3 = f2; f2 = f1; f1 = f0;
+            q4 = q3; q3 = q2; q2 = q1; q1 = q0;
         }
-        __syncthreads();
+        if constexpr (DMA > 0) {
+            // pair gi + 1 must have landed; the pairs issued after it (4 DMAs each) and this
+            // step's 3 stores (x4 of both rows, one rc row: issued in every step) may fly on
+            vm_wait_n(4 * max(0, min(gi + DMA - 1, ng - 1) - (gi + 1)) + 3);
+            raw_barrier();
+        } else {
+            __syncthreads();
+        }
     };
-    if constexpr (D == 3) {
-        for (int gi = 0; gi < ng; gi += 3) {
+    if constexpr (DMA > 0) {
+        int gi = 0;
+        for (; gi + 3 <= ng; gi += 3) {   // 6 rows: the period of the row windows
             step(gi, pxB, pfB, peB);
-            if (gi + 1 < ng) step(gi + 1, pxC, pfC, peC);
-            if (gi + 2 < ng) step(gi + 2, pxA, pfA, peA);
+            step(gi + 1, pxB, pfB, peB);
+            step(gi + 2, pxB, pfB, peB);
         }
+        if (gi < ng) step(gi, pxB, pfB, peB);
+        if (gi + 1 < ng) step(gi + 1, pxB, pfB, peB);
+    } else if constexpr (D == 3) {
+        // 6 rows per iteration, no guard inside: the row windows rotate with periods 3 (two
+        // carried rows and the new one) and 6 (f), so after 6 rows every carried value is
+        // back in its register (a guarded step would merge two paths and force copies)
+        int gi = 0;
+        for (; gi + 3 <= ng; gi += 3) {
+            step(gi, pxB, pfB, peB);
+            step(gi + 1, pxC, pfC, peC);
+            step(gi + 2, pxA, pfA, peA);
+        }
+        if (gi < ng) step(gi, pxB, pfB, peB);
+        if (gi + 1 < ng) step(gi + 1, pxC, pfC, peC);
     } else {
         for (int gi = 0; gi < ng; gi += 2) {
             step(gi, pxB, pfB, peB);
@@ -955,6 +1118,30 @@ void k_postpre_lds(PostPreArgsT<T> a)
         postpre_lds_run<T, R2, GENF, true, OPT>(a, k, red, sx, sf, se, bk);
     else
         postpre_lds_run<T, R2, GENF, false, OPT>(a, k, red, sx, sf, se, bk);
+}
+
+// k_postpre_dma: the headline finest-level pass (fp64, analytic f, one GPU) with its rows
+// brought in by LDS-DMA into a ring of K row-pair slots; all LDS is one array (a second
+// __shared__ object makes hipcc wait vmcnt(0) before LDS reads).  Arithmetic identical to
+// k_postpre_lds.
+template <int K>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+void k_postpre_dma(PostPreArgsT<double> a)
+{
+    __shared__ __attribute__((aligned(16))) double lds[K * kPPR * kDmaRow + kDmaCRing * kDmaCRow + 8];
+    double (&sx)[2][kPPR][kPPLdsRow] = *reinterpret_cast<double (*)[2][kPPR][kPPLdsRow]>(lds);
+    double (&sf)[2][kPPR][1] = *reinterpret_cast<double (*)[2][kPPR][1]>(lds);
+    double (&se)[3][kPPLdsCoarse] = *reinterpret_cast<double (*)[3][kPPLdsCoarse]>(lds);
+    double *red = lds + K * kPPR * kDmaRow + kDmaCRing * kDmaCRow;
+    const Blk bk{(int)blockIdx.x, (int)blockIdx.y};
+    const Cols k = lane_cols_t<kPPStride, kPPMargin>(a.N, bk.x);
+    const int jcb = a.jc0 + bk.y * a.rows_per_block;
+    const int jce = min(jcb + a.rows_per_block, a.jc1);
+    const bool edge_rows = 2 * jcb - 6 <= 0 || 2 * jce + 6 >= a.N - 1;
+    if (k.edge || edge_rows)
+        postpre_lds_run<double, false, true, true, 2, K>(a, k, red, sx, sf, se, bk, lds);
+    else
+        postpre_lds_run<double, false, true, false, 2, K>(a, k, red, sx, sf, se, bk, lds);
 }
 
 // one block: both decisions, stats, flags for the conditional rare-path kernels
@@ -1039,7 +1226,9 @@ static void fused_geometry(int N, int jc0, int jc1, int *threads, int *gx, int *
         }
     }
 
-    const int rmin = 2, rmax = 512;
+    // (no cap on the band height: a cap of 512 coarse rows once turned a one-round target of
+    // 504 workgroups at N = 16385 into 576, i.e. 1.125 rounds)
+    const int rmin = 2, rmax = 1 << 20;
     // bands so that gx * gy does not exceed the target (a target of whole rounds of the
     // resident workgroups must not spill a few workgroups into one more round: 3096
     // workgroups for a 3072 target cost ~2 % in k_postpre)
@@ -1278,6 +1467,14 @@ int launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
         if (genf) k_postpre_lds<T, true, true, 2><<<g, b, 0, s>>>(a);
         else k_postpre_lds<T, true, false, 2><<<g, b, 0, s>>>(a);
     } else {
+#if PGMG_PP_DMA > 0
+        if constexpr (sizeof(T) == 8) {
+            if (genf && t == 256) {
+                k_postpre_dma<PGMG_PP_DMA><<<g, b, 0, s>>>(a);
+                return PGMG_OK;
+            }
+        }
+#endif
         if (genf) k_postpre_lds<T, false, true, 2><<<g, b, 0, s>>>(a);
         else k_postpre_lds<T, false, false, 2><<<g, b, 0, s>>>(a);
     }
