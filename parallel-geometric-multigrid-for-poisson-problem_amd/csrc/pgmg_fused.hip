@@ -730,74 +730,14 @@ __device__ __forceinline__ T buf_one(const T *base, int n, int t)
         return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, t * 4, 0, 0));
 }
 
-// LDS-DMA ring of k_postpre_dma: 512 doubles per fine row (4 waves x 64 lanes x 16 B), 256
-// per coarse row (2 dword DMAs per wave), coarse rows m-1 .. m+K live
-constexpr int kDmaRow = 512;
-constexpr int kDmaCRow = 256;
-#ifndef PGMG_PP_DMA
-#define PGMG_PP_DMA 0     // > 0: the headline pass through k_postpre_dma with this ring depth
-#endif
-constexpr int kDmaCRing = (PGMG_PP_DMA > 0 ? PGMG_PP_DMA : 4) + 2;
-
-// LDS-DMA in inline asm: hipcc's own bookkeeping would wait vmcnt(0) before every LDS read
-// of the staging array (it cannot tell the slots apart); the waits are counted by hand.
-// M0 = the wave-uniform LDS byte address, written in the same statement.
-__device__ __forceinline__ unsigned lds_addr(const void *p)
-{
-    return (unsigned)(unsigned long long)(const __attribute__((address_space(3))) char *)p;
-}
-__device__ __forceinline__ void glds16(const void *g, const void *lds_wave_base)
-{
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_wave_base)))
-                 : "memory");
-}
-__device__ __forceinline__ void glds4(const void *g, const void *lds_wave_base)
-{
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_wave_base)))
-                 : "memory");
-}
-// wait until at most n (<= 31) vector-memory operations of this wave are outstanding.  Vector
-// memory operations complete in order on gfx9 (one counter for loads and stores), so every
-// operation older than the n youngest has completed
-#define PGMG_VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-__device__ __forceinline__ void vm_wait_n(int n)
-{
-    switch (n) {
-    PGMG_VMW(31) PGMG_VMW(30) PGMG_VMW(29) PGMG_VMW(28) PGMG_VMW(27) PGMG_VMW(26) PGMG_VMW(25)
-    PGMG_VMW(24) PGMG_VMW(23) PGMG_VMW(22) PGMG_VMW(21) PGMG_VMW(20) PGMG_VMW(19) PGMG_VMW(18)
-    PGMG_VMW(17) PGMG_VMW(16) PGMG_VMW(15) PGMG_VMW(14) PGMG_VMW(13) PGMG_VMW(12) PGMG_VMW(11)
-    PGMG_VMW(10) PGMG_VMW(9) PGMG_VMW(8) PGMG_VMW(7) PGMG_VMW(6) PGMG_VMW(5) PGMG_VMW(4)
-    PGMG_VMW(3) PGMG_VMW(2) PGMG_VMW(1)
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    }
-}
-#undef PGMG_VMW
-// a barrier that leaves LDS-DMA in flight (__syncthreads() would wait vmcnt(0))
-__device__ __forceinline__ void raw_barrier()
-{
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-}
-
 // The body of k_postpre_lds for one block.  EDGE = false: no row of the block's band and
 // no column of this wave is a boundary, so the Jacobi stages carry no passthrough selects.
-//
-// DMA = K > 0 (k_postpre_dma, fp64 / analytic f / one GPU): the rows come into LDS by LDS-DMA
-// (global_load_lds: no VGPR destination) into a ring of K row-pair slots, K - 1 pairs in
-// flight per wave instead of the register sets; waits counted by hand (see k_postpre_dma).
-template <class T, bool R2, bool GENF, bool EDGE, int OPT, int DMA = 0>
+template <class T, bool R2, bool GENF, bool EDGE, int OPT>
 __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const Cols &k,
                                                 double *red, T (&sx)[2][kPPR][kPPLdsRow],
                                                 T (&sf)[2][kPPR][GENF ? 1 : kPPLdsRow],
-                                                T (&se)[3][kPPLdsCoarse], const Blk bk,
-                                                T *dl = nullptr)
+                                                T (&se)[3][kPPLdsCoarse], const Blk bk)
 {
-    static_assert(DMA == 0 || (sizeof(T) == 8 && GENF && !R2 && OPT == 2), "DMA: the headline pass only");
     constexpr int R = kPPR;
     const int N = a.N, Nc = a.Nc;
     const long long P = a.P, Pc = a.Pc;
@@ -857,20 +797,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     const int m0 = i_begin >> 1;                          // coarse row of the first pair
     auto ring = [](int m) { return (m + 3 * 4096) % 3; };  // m >= -3
 
-    constexpr int KD = DMA > 0 ? DMA : 1;
-    // DMA ring: fine slot p = rows [p][q][kDmaRow], coarse ring after them (kDmaCRing rows)
-    T *const DX = dl;
-    T *const DE = dl + KD * R * kDmaRow;
-    auto xrow = [&](int slot, int q) -> const T * {
-        if constexpr (DMA > 0) return DX + (slot * R + q) * kDmaRow;
-        else return sx[slot][q];
-    };
-    auto dring = [](int m) { return (m + kDmaCRing * 4096) % kDmaCRing; };   // m >= -3
-    auto erow = [&](int m) -> const T * {
-        if constexpr (DMA > 0) return DE + dring(m) * kDmaCRow;
-        else return se[(m + 3 * 4096) % 3];
-    };
-    if (DMA == 0 && t < 2 * R * 4) {   // the 4 pad doubles past the window (spare lanes only)
+    if (t < 2 * R * 4) {   // the 4 pad doubles past the window (read by spare lanes only)
         const int sl = t >> 3, q = (t >> 2) & 1, j = kPPLdsRow - 4 + (t & 3);
         sx[sl][q][j] = T(0);
         if constexpr (!GENF) sf[sl][q][j] = T(0);
@@ -901,7 +828,6 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
         }
         if (t < ncc) se[ring(m0 + p + 1)][t] = pe;
     };
-    if constexpr (DMA == 0) {
     // prologue: pair 0 (+ its first coarse row) into slot 0; pairs 1 .. D in flight
     load_pair(0, pxA, pfA, peA);
     if (t < ncc) se[ring(m0)][t] = buf_one<T>(a.ec + (long long)m0 * Pc + cc0, nve, t);
@@ -914,36 +840,6 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
         if (ng > 2) load_pair(2, pxA, pfA, peA);
     }
     __syncthreads();
-    }   // DMA == 0
-
-    // DMA: every lane issues every DMA (a wave's count of vector-memory operations per pair
-    // must be exactly 4 for the counted waits); lanes past the grid re-read its last valid
-    // pair (N - 2 is odd: 16-byte aligned) -- columns >= N never reach an owned result
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const T *const GX = a.phi + min(L0 + 2 * t, N - 2);
-    const int dmax = 2 * (Nc - 1 - cc0) + 1;   // coarse row: dword d = i * 256 + t, clamped
-    const char *const GE = reinterpret_cast<const char *>(a.ec + cc0);
-    const int ce0 = 4 * min(t, dmax), ce1 = 4 * min(256 + t, dmax);
-    auto issue_coarse = [&](int m) {
-        T *dst = DE + dring(m) * kDmaCRow;
-        const char *src = GE + (long long)m * Pc * 8;
-        glds4(src + ce0, dst + 32 * wv);
-        glds4(src + ce1, dst + 128 + 32 * wv);
-    };
-    auto issue_pair = [&](int p) {   // pair p's rows into slot p % DMA, its second coarse row
-        #pragma unroll
-        for (int q = 0; q < R; ++q)
-            glds16(GX + (long long)(i_begin + p * R + q) * P, DX + ((p % KD) * R + q) * kDmaRow + 128 * wv);
-        issue_coarse(m0 + p + 1);
-    };
-    if constexpr (DMA > 0) {
-        issue_coarse(m0);
-        for (int p = 0; p < DMA - 1; ++p)
-            if (p < ng) issue_pair(p);
-        // row m0 and pair 0 landed: the pairs issued after it may fly on
-        vm_wait_n(4 * (min(ng, DMA - 1) - 1));
-        raw_barrier();
-    }
 
     // pair gi: compute from slot gi & 1; pair gi+1 (set (gi+1) & 1) -> the other slot;
     // issue pair gi+3 into the set just freed; one barrier
@@ -952,25 +848,20 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
         // keep the scheduler inside one pair: interleaving the unrolled pairs only raises
         // the register pressure (the loads of a pair are issued two pairs ahead anyway)
         __builtin_amdgcn_sched_barrier(0);
-        const int slot = DMA > 0 ? gi % KD : (gi & 1);
-        if constexpr (DMA > 0) {
-            // into the slot of pair gi - 1, whose readers passed the last barrier
-            if (gi + DMA - 1 < ng) issue_pair(gi + DMA - 1);
-        } else {
-            // the other slot's previous readers passed the last barrier: stage pair gi+1
-            // (loaded two steps ago) first and reissue its register set for pair gi+3, so the
-            // loads in flight are never younger than this step's stores (counted waits stay small)
-            if (gi + 1 < ng) store_pair(gi + 1, px, pf, pe);
-            if (gi + 1 + D < ng) load_pair(gi + 1 + D, px, pf, pe);
-        }
+        const int slot = gi & 1;
+        // the other slot's previous readers passed the last barrier: stage pair gi+1 (loaded
+        // D steps ago) first and reissue its register set for pair gi+1+D, so the loads in
+        // flight are never younger than this step's stores (counted waits stay small)
+        if (gi + 1 < ng) store_pair(gi + 1, px, pf, pe);
+        if (gi + 1 + D < ng) load_pair(gi + 1 + D, px, pf, pe);
         const int i = i_begin + gi * R;
         const int m = m0 + gi;
-        const T *E0 = erow(m), *E1 = erow(m + 1);
+        const T *E0 = se[ring(m)], *E1 = se[ring(m + 1)];
         const T cr0 = E0[co], crn0 = E0[co + 1], cr1 = E1[co], crn1 = E1[co + 1];
         #pragma unroll
         for (int s = 0; s < R; ++s) {
             const int ii = i + s;
-            const V2<T> xr = ldv(xrow(slot, s) + xo);
+            const V2<T> xr = ldv(&sx[slot][s][xo]);
             // f[ii]: from LDS, or (GENF) generated once here and carried in the f window
             // (regenerating it at every use instead: fewer VGPRs, 8 more multiplies per
             // row, measured slower in r01)
@@ -1045,25 +936,9 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
             f5 = f4; f4 = f3; f3 = f2; f2 = f1; f1 = f0;
             q4 = q3; q3 = q2; q2 = q1; q1 = q0;
         }
-        if constexpr (DMA > 0) {
-            // pair gi + 1 must have landed; the pairs issued after it (4 DMAs each) and this
-            // step's 3 stores (x4 of both rows, one rc row: issued in every step) may fly on
-            vm_wait_n(4 * max(0, min(gi + DMA - 1, ng - 1) - (gi + 1)) + 3);
-            raw_barrier();
-        } else {
-            __syncthreads();
-        }
+        __syncthreads();
     };
-    if constexpr (DMA > 0) {
-        int gi = 0;
-        for (; gi + 3 <= ng; gi += 3) {   // 6 rows: the period of the row windows
-            step(gi, pxB, pfB, peB);
-            step(gi + 1, pxB, pfB, peB);
-            step(gi + 2, pxB, pfB, peB);
-        }
-        if (gi < ng) step(gi, pxB, pfB, peB);
-        if (gi + 1 < ng) step(gi + 1, pxB, pfB, peB);
-    } else if constexpr (D == 3) {
+    if constexpr (D == 3) {
         // 6 rows per iteration, no guard inside: the row windows rotate with periods 3 (two
         // carried rows and the new one) and 6 (f), so after 6 rows every carried value is
         // back in its register (a guarded step would merge two paths and force copies)
@@ -1118,30 +993,6 @@ void k_postpre_lds(PostPreArgsT<T> a)
         postpre_lds_run<T, R2, GENF, true, OPT>(a, k, red, sx, sf, se, bk);
     else
         postpre_lds_run<T, R2, GENF, false, OPT>(a, k, red, sx, sf, se, bk);
-}
-
-// k_postpre_dma: the headline finest-level pass (fp64, analytic f, one GPU) with its rows
-// brought in by LDS-DMA into a ring of K row-pair slots; all LDS is one array (a second
-// __shared__ object makes hipcc wait vmcnt(0) before LDS reads).  Arithmetic identical to
-// k_postpre_lds.
-template <int K>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
-void k_postpre_dma(PostPreArgsT<double> a)
-{
-    __shared__ __attribute__((aligned(16))) double lds[K * kPPR * kDmaRow + kDmaCRing * kDmaCRow + 8];
-    double (&sx)[2][kPPR][kPPLdsRow] = *reinterpret_cast<double (*)[2][kPPR][kPPLdsRow]>(lds);
-    double (&sf)[2][kPPR][1] = *reinterpret_cast<double (*)[2][kPPR][1]>(lds);
-    double (&se)[3][kPPLdsCoarse] = *reinterpret_cast<double (*)[3][kPPLdsCoarse]>(lds);
-    double *red = lds + K * kPPR * kDmaRow + kDmaCRing * kDmaCRow;
-    const Blk bk{(int)blockIdx.x, (int)blockIdx.y};
-    const Cols k = lane_cols_t<kPPStride, kPPMargin>(a.N, bk.x);
-    const int jcb = a.jc0 + bk.y * a.rows_per_block;
-    const int jce = min(jcb + a.rows_per_block, a.jc1);
-    const bool edge_rows = 2 * jcb - 6 <= 0 || 2 * jce + 6 >= a.N - 1;
-    if (k.edge || edge_rows)
-        postpre_lds_run<double, false, true, true, 2, K>(a, k, red, sx, sf, se, bk, lds);
-    else
-        postpre_lds_run<double, false, true, false, 2, K>(a, k, red, sx, sf, se, bk, lds);
 }
 
 // one block: both decisions, stats, flags for the conditional rare-path kernels
@@ -1467,14 +1318,6 @@ int launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
         if (genf) k_postpre_lds<T, true, true, 2><<<g, b, 0, s>>>(a);
         else k_postpre_lds<T, true, false, 2><<<g, b, 0, s>>>(a);
     } else {
-#if PGMG_PP_DMA > 0
-        if constexpr (sizeof(T) == 8) {
-            if (genf && t == 256) {
-                k_postpre_dma<PGMG_PP_DMA><<<g, b, 0, s>>>(a);
-                return PGMG_OK;
-            }
-        }
-#endif
         if (genf) k_postpre_lds<T, false, true, 2><<<g, b, 0, s>>>(a);
         else k_postpre_lds<T, false, false, 2><<<g, b, 0, s>>>(a);
     }
