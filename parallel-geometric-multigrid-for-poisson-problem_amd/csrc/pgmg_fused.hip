@@ -61,6 +61,22 @@ __device__ __forceinline__ V2<T> jstage(V2<T> up, V2<T> ce, V2<T> dn, V2<T> f, T
     return o;
 }
 
+// J(0): the Jacobi stage of an all-zero iterate, 0.25 * ((hh*f) + 0 + 0 + 0 + 0).  The first
+// +0 turns a -0 into +0 and the other three change nothing, so ONE add of +0 gives the same
+// IEEE result (the compiler may not drop x + 0 itself: it is not an identity for x = -0)
+template <class T, bool EDGE = true>
+__device__ __forceinline__ V2<T> j0stage(V2<T> f, T hh, const Cols &k, bool brow)
+{
+    V2<T> o;
+    o.x = T(0.25) * ((hh * f.x) + T(0));
+    o.y = T(0.25) * ((hh * f.y) + T(0));
+    if constexpr (EDGE) {
+        if (brow || k.bx) o.x = T(0);
+        if (brow || k.by) o.y = T(0);
+    }
+    return o;
+}
+
 // Residual r = f - (1/h^2)(4x - xl - xr - xu - xd) on a row (DynamicGridUtils.hpp:59-69)
 template <class T>
 __device__ __forceinline__ V2<T> rstage(V2<T> up, V2<T> ce, V2<T> dn, V2<T> f, T ih)
@@ -138,6 +154,38 @@ __device__ __forceinline__ V2<T> add_prolong(V2<T> p, int row, T ca, T cb, T da,
     return p;
 }
 
+// The row loop of k_pre / k_post: iterations of R rows at i = i_begin, i_begin + R, ..,
+// < i_end; full_at(i) holds on one contiguous run of them.  The run is executed three
+// iterations (3R = 12 rows) at a time with no branch inside: the row windows (two carried
+// rows and the new one: period 3; f in k_pre: period 4) come back to their registers after
+// 12 rows, and no merge of the FULL and general paths forces copies of every window.
+template <int R, int U, class FullAt, class Iter>
+__device__ __forceinline__ void row_loop(int i_begin, int i_end, const FullAt &full_at, const Iter &iter)
+{
+    int i = i_begin;
+    if constexpr (U == 0) {   // one loop, the path chosen per iteration
+        for (; i < i_end; i += R) {
+            if (full_at(i)) iter(i, std::true_type{});
+            else iter(i, std::false_type{});
+        }
+        return;
+    }
+    for (; i < i_end && !full_at(i); i += R) iter(i, std::false_type{});
+    if constexpr (U == 3) {
+        for (; i + 3 * R <= i_end && full_at(i + 2 * R); i += 3 * R) {
+            iter(i, std::true_type{});
+            iter(i + R, std::true_type{});
+            iter(i + 2 * R, std::true_type{});
+        }
+    } else {
+        for (; i < i_end && full_at(i); i += R) iter(i, std::true_type{});
+    }
+    for (; i < i_end; i += R) {
+        if (full_at(i)) iter(i, std::true_type{});
+        else iter(i, std::false_type{});
+    }
+}
+
 // ---------------------------------------------------------------------------
 // k_pre
 // ---------------------------------------------------------------------------
@@ -210,7 +258,16 @@ __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red)
             ncrn[q] = idle ? T(0) : E[(long long)((i_begin >> 1) + q) * Pc + 1];
         }
     }
-    for (int i = i_begin; i < i_end; i += R) {
+    // FULL: every row of the iteration is interior to the band, the grid and the restriction
+    // range, and the wave's columns are all interior (no boundary column, every prolongation
+    // column corrected): the per-row range checks and the boundary selects drop out.  The
+    // condition holds on one contiguous run of iterations (each clause bounds i from one side)
+    auto full_at = [&](int i) {
+        return !S1 && inner && i >= 3 && i + R <= N && i - 2 >= olo && i + R - 3 < ohi &&
+               ((i - 4) >> 1) >= clo && ((i + R - 6) >> 1) < chi &&
+               (!PIN || ((i >> 1) >= 1 && ((i + R - 1) >> 1) <= a.Nc - 2));
+    };
+    auto iter = [&](int i, auto full_t) {
         V2<T> cx[R], cf[R];
         T cr[PAIRS + 1], crn[PAIRS + 1];
         #pragma unroll
@@ -239,16 +296,12 @@ __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red)
                 }
             }
         }
-        // FULL: every row of this iteration is interior to the band, the grid and the
-        // restriction range, and the wave's columns are all interior (no boundary column,
-        // every prolongation column corrected): the per-row range checks and the boundary
-        // selects drop out
         double gy[R];   // GENF row factors of the iteration, loaded together up front
         if constexpr (GENF) {
             #pragma unroll
             for (int q = 0; q < R; ++q) gy[q] = gsy_s(a.gsy, i + q);
         }
-        auto rows = [&](auto full_t) {
+        {
             constexpr bool FULL = decltype(full_t)::value;
             #pragma unroll
             for (int s = 0; s < R; ++s) {
@@ -265,7 +318,8 @@ __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red)
                     f3 = cf[s];
                 }
                 // x1 row ii-1
-                const V2<T> b2 = jstage<T, !FULL>(a0, a1, a2, f2, hh, k, boundary_row(ii - 1, N));
+                const V2<T> b2 = (X0_ZERO && !PIN) ? j0stage<T, !FULL>(f2, hh, k, boundary_row(ii - 1, N))
+                                                   : jstage<T, !FULL>(a0, a1, a2, f2, hh, k, boundary_row(ii - 1, N));
                 // r(x1) and x2 on row ii-2
                 const V2<T> r1 = rstage(b0, b1, b2, f1, ih);
                 if constexpr (S1) {
@@ -335,13 +389,10 @@ __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red)
                 f1 = f2;
                 f2 = f3;
             }
-        };
-        const bool full = !S1 && inner && i >= 3 && i + R <= N && i - 2 >= olo && i + R - 3 < ohi &&
-                          ((i - 4) >> 1) >= clo && ((i + R - 6) >> 1) < chi &&
-                          (!PIN || ((i >> 1) >= 1 && ((i + R - 1) >> 1) <= a.Nc - 2));
-        if (full) rows(std::true_type{});
-        else rows(std::false_type{});
-    }
+        }
+    };
+    // (PIN: the 12-row form needs 170 VGPRs, past the 168 of 3 waves per SIMD)
+    row_loop<R, PIN ? 0 : 3>(i_begin, i_end, full_at, iter);
     if constexpr (!S1) {
         const double sum = fused_block_sum(acc, red);
         if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = sum;
@@ -439,8 +490,8 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
     if (RECOMP && !idle) {
         const V2<T> fm = ldv(F + (i_begin - 1) * P);
         fc = ldv(F + i_begin * P);
-        g0 = jstage(z, z, z, fm, hh, k, boundary_row(i_begin - 1, N));
-        g1 = jstage(z, z, z, fc, hh, k, boundary_row(i_begin, N));
+        g0 = j0stage(fm, hh, k, boundary_row(i_begin - 1, N));
+        g1 = j0stage(fc, hh, k, boundary_row(i_begin, N));
     }
     // coarse row m = ii/2 of fine row ii; an iteration of R rows uses coarse rows
     // i/2 .. i/2 + PAIRS
@@ -453,7 +504,13 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
     }
     #pragma unroll
     for (int q = 0; q <= PAIRS; ++q) ncr[q] = idle ? T(0) : E[(long long)((i_begin >> 1) + q) * Pc];
-    for (int i = i_begin; i < i_end; i += R) {
+    // FULL: as in pre_body (rows interior to the band, the sum range and the grid; interior
+    // wave columns)
+    auto full_at = [&](int i) {
+        return !S1 && inner && i >= 3 && i + R <= N - 2 && i - 2 >= slo && i + R - 3 < shi &&
+               ((i + R - 1) >> 1) <= Nc - 2;
+    };
+    auto iter = [&](int i, auto full_t) {
         V2<T> cp[R], cf[R];
         T cr[PAIRS + 1];
         #pragma unroll
@@ -480,9 +537,7 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
             #pragma unroll
             for (int q = 0; q < R; ++q) gy[q] = gsy_s(a.gsy, i + q);
         }
-        // FULL: as in pre_body (rows interior to the band, the sum range and the grid;
-        // interior wave columns)
-        auto rows = [&](auto full_t) {
+        {
             constexpr bool FULL = decltype(full_t)::value;
             #pragma unroll
             for (int s = 0; s < R; ++s) {
@@ -491,7 +546,7 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
                 V2<T> ph, f3;
                 if (RECOMP) {
                     const V2<T> fn = cp[s];  // f row ii+1
-                    const V2<T> g2 = jstage<T, !FULL>(z, z, z, fn, hh, k, boundary_row(ii + 1, N));
+                    const V2<T> g2 = j0stage<T, !FULL>(fn, hh, k, boundary_row(ii + 1, N));
                     ph = pfired ? g1 : jstage<T, !FULL>(g0, g1, g2, fc, hh, k, boundary_row(ii, N));
                     f3 = fc;
                     g0 = g1;
@@ -535,12 +590,12 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
                 f1 = f2;
                 f2 = f3;
             }
-        };
-        const bool full = !S1 && inner && i >= 3 && i + R <= N - 2 && i - 2 >= slo &&
-                          i + R - 3 < shi && ((i + R - 1) >> 1) <= Nc - 2;
-        if (full) rows(std::true_type{});
-        else rows(std::false_type{});
-    }
+        }
+    };
+    // (one loop with the path chosen per iteration: the 12-row form of k_pre costs k_post
+    // 150 -> 210 VGPRs, i.e. 3 -> 2 waves per SIMD, and measured slower; hoisting the pre
+    // check's outcome out of the loop measured no gain)
+    row_loop<R, 0>(i_begin, i_end, full_at, iter);
     if constexpr (!S1) {
         const double sum = fused_block_sum(acc, red);
         if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = sum;
