@@ -42,7 +42,9 @@ __device__ __forceinline__ double2 bload(const double *base, int n, int t)
     return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, t * 16, 0, NT ? 2 : 0));
 }
 
-template <int WAVES, int LDS, int NTL>
+// ALT: odd bands march upward (their halo rows are then read at the same time as the
+// neighbouring bands read the same rows: second reads hit a cache)
+template <int WAVES, int LDS, int NTL, int ALT = 0>
 __global__ __launch_bounds__(64 * WAVES) void k_band(const double *__restrict__ in,
                                                      double *__restrict__ out, int N, long long P,
                                                      int rb, double *sink)
@@ -60,9 +62,14 @@ __global__ __launch_bounds__(64 * WAVES) void k_band(const double *__restrict__ 
     double acc = 0.0;
     if (LDS) {
         double2 pa0, pa1, pb0, pb1;
+        const bool up = ALT && (blockIdx.y & 1);
+        const int np = (r1 - r0) / 2;
+        // pair starting at logical row r (r0, r0 + 2, ..) -> physical first row of the pair
+        auto phys = [&](int r) { return up ? r0 + 2 * (np - 1 - (r - r0) / 2) : r; };
         auto ld = [&](int r, double2 &a, double2 &b) {
-            a = bload<NTL>(in + (long long)r * P + L0, nv, t);
-            b = bload<NTL>(in + (long long)(r + 1) * P + L0, nv, t);
+            const int pr = phys(r);
+            a = bload<NTL>(in + (long long)pr * P + L0, nv, t);
+            b = bload<NTL>(in + (long long)(pr + 1) * P + L0, nv, t);
         };
         ld(r0, pa0, pa1);
         if (t < npairs) {
@@ -85,7 +92,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_band(const double *__restrict__ 
                 if (rr + 6 < r1) ld(rr + 6, q0, q1);
                 for (int s = 0; s < 2; ++s) {
                     const double2 v = *reinterpret_cast<const double2 *>(&sx[slot][s][kStride * w + 2 * lane]);
-                    const int row = rr + s;
+                    const int row = phys(rr) + s;
                     if (own && row >= r0 + 6 && row < r1 - 6 && row < N - 1)
                         st_nt(out + row * P + c, v);
                     acc += v.x;
@@ -116,7 +123,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_band(const double *__restrict__ 
     if (acc == 12345.678) *sink = acc;
 }
 
-template <int WAVES, int LDS, int NTL>
+template <int WAVES, int LDS, int NTL, int ALT = 0>
 int run(const double *in, double *out, int N, long long P, int blocks, double *sink)
 {
     const int cols = (N - 2 + kStride * WAVES - 1) / (kStride * WAVES);
@@ -132,7 +139,7 @@ int run(const double *in, double *out, int N, long long P, int blocks, double *s
     float best = 1e9;
     for (int rep = 0; rep < 6; ++rep) {
         CK(hipEventRecord(e0));
-        k_band<WAVES, LDS, NTL><<<dim3(cols, bands), dim3(64 * WAVES)>>>(in + 1 * P, out + 1 * P, N, P, rb, sink);
+        k_band<WAVES, LDS, NTL, ALT><<<dim3(cols, bands), dim3(64 * WAVES)>>>(in + 1 * P, out + 1 * P, N, P, rb, sink);
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
         float ms;
@@ -140,9 +147,9 @@ int run(const double *in, double *out, int N, long long P, int blocks, double *s
         if (rep > 0 && ms < best) best = ms;
     }
     const double pts = (double)(N - 2) * (N - 2);
-    printf("{\"waves\": %d, \"lds\": %d, \"ntl\": %d, \"blocks\": %d, \"band_rows\": %d, \"ms\": %.4f, "
+    printf("{\"waves\": %d, \"lds\": %d, \"ntl\": %d, \"alt\": %d, \"blocks\": %d, \"band_rows\": %d, \"ms\": %.4f, "
            "\"alg_GBps\": %.1f}\n",
-           WAVES, LDS, NTL, cols * bands, rb, best, 16.0 * pts / (best * 1e-3) / 1e9);
+           WAVES, LDS, NTL, ALT, cols * bands, rb, best, 16.0 * pts / (best * 1e-3) / 1e9);
     fflush(stdout);
     return 0;
 }
@@ -159,6 +166,16 @@ int main(int argc, char **argv)
     CK(hipMemset(in0, 0, bytes));
     CK(hipMemset(out0, 0, bytes));
     const int bl[] = {512, 1024, 2048, 3072, 4096, 6144};
+    if (argc > 1 && argv[1][0] == 'a') {   // alternating band direction
+        const long long P = 16400;
+        double *in = in0 + 10 * P, *out = out0 + 10 * P;
+        for (int rep = 0; rep < 2; ++rep)
+            for (int b : {512, 1024, 3072, 6144}) {
+                run<4, 1, 0, 0>(in, out, N, P, b, sink);
+                run<4, 1, 0, 1>(in, out, N, P, b, sink);
+            }
+        return 0;
+    }
     if (argc > 1) {   // pitch sweep at fixed shape
         const long long pitches[] = {16400, 16384 + 16, 16384 + 32, 16384 + 64, 16384 + 128, 16384 + 256,
                                      16384 + 512, 16384 + 48, 16384 + 80, 16384 + 144};
