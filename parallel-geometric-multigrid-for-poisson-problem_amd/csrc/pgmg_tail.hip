@@ -518,6 +518,35 @@ template <int CTRL> __device__ __forceinline__ float dpp_row(float v)
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 
+// Bilinear prolongation of one fine point (j, i) of a wave-team level (MultiGrid.hpp:208-226),
+// branch-free: the four parity cases are the one expression s * (((a + b) + c) + d) with the
+// unused terms -0.0 (x + (-0) == x for every x, and 1 * x == x), so every case performs the
+// reference's operations in its order.  The geometry is computed once per call.
+struct PGeo {
+    int ob, boff;   // coarse (cj, ci) offset; offset of the second term (1 or NC)
+    bool cor;       // the point is corrected: j, i in [2, Nf - 2]
+    bool mb, mcd;   // term b is used (i or j odd); terms c, d are used (both odd)
+};
+__device__ __forceinline__ PGeo pgeo(int j, int i, int Nf, int NC, bool in)
+{
+    PGeo g;
+    const bool jo = (j & 1) != 0, io = (i & 1) != 0;
+    g.cor = in && j >= 2 && i >= 2 && j <= Nf - 2 && i <= Nf - 2;
+    g.ob = g.cor ? (j >> 1) * NC + (i >> 1) : 0;
+    g.boff = io ? 1 : NC;
+    g.mb = jo || io;
+    g.mcd = jo && io;
+    return g;
+}
+template <class Real>
+__device__ __forceinline__ Real pweight(const Real *C, const PGeo &g, int NC)
+{
+    const Real a = C[g.ob], b = C[g.ob + g.boff], c = C[g.ob + NC], d = C[g.ob + NC + 1];
+    const Real nz = -Real(0);
+    const Real s = g.mcd ? Real(0.25) : (g.mb ? Real(0.5) : Real(1));
+    return s * (((a + (g.mb ? b : nz)) + (g.mcd ? c : nz)) + (g.mcd ? d : nz));
+}
+
 // The coarsest solve (JacobiSmoother::smooth with coarse_iter, Smoother.hpp:38-116) of a 5x5
 // level held in registers: lane q < 9 owns interior point (1 + q/3, 1 + q%3), the other
 // lanes hold 0 (the Dirichlet boundary); left/right/up/down neighbours are DPP moves by
@@ -608,6 +637,7 @@ __device__ __forceinline__ Cnt tail_w9(const TailArgsDev<Real> &d, int l, int re
     const Real hh = L9.hh, ih = L9.ih;
     const Real fk = f9[k9], hf = hh * fk;
     Real x = x9[k9];   // this lane's point; LDS x9 always holds every lane's current value
+    const PGeo pg9 = pgeo(1 + jj, 1 + ii, 9, 5, in9);
     // JacobiSmoother::smooth on the 9x9 level with the iterate in registers: sweeps in place
     // (the wave's reads of the old neighbours precede its writes), the check of x_k fused
     // into sweep k+1 and undone from the register copy when it fires (tail_smooth_small)
@@ -638,8 +668,23 @@ __device__ __forceinline__ Cnt tail_w9(const TailArgsDev<Real> &d, int l, int re
         }
     };
     Cnt cnt;
+#ifdef PGMG_TUNING
+    // stage clocks of the 9x9 visits (PGMG_TAIL_PROF): prof[8..11] smooth, res+restrict,
+    // coarsest solves, prolongation; prof[15] visits
+    unsigned long long st[4] = {0, 0, 0, 0}, tc = d.prof ? tail_clock() : 0;
+    auto stamp = [&](int i) {
+        if (d.prof) {
+            const unsigned long long t1 = tail_clock();
+            st[i] += t1 - tc;
+            tc = t1;
+        }
+    };
+#else
+    auto stamp = [](int) {};
+#endif
     for (int v = 0; v < reps; ++v) {
         smooth(a.v1, cnt);
+        stamp(0);
         // r = f - A x on the interior (DynamicGridUtils.hpp:59-69), into T
         if (in9) T[k9] = fk - ih * (Real(4) * x - x9[k9 - 1] - x9[k9 + 1] - x9[k9 - 9] - x9[k9 + 9]);
         fence();
@@ -648,31 +693,33 @@ __device__ __forceinline__ Cnt tail_w9(const TailArgsDev<Real> &d, int l, int re
         if (lane < 9)
             fc = Real(0.25) * T[kc] + Real(0.125) * (T[kc + 1] + T[kc - 1] + T[kc + 9] + T[kc - 9]) +
                  Real(0.0625) * (T[kc - 9 - 1] + T[kc - 9 + 1] + T[kc + 9 - 1] + T[kc + 9 + 1]);
+        stamp(1);
         for (int g = 0; g < gamma; ++g)
             cnt += tail_coarse5_regs(ec, fc, L5, a.coarse_iter, eps2);
+        stamp(2);
         // the correction into LDS (5x5, boundary 0), then x += P e on [2, 7]^2 (:208-226)
         if (lane < 25) e5[lane] = Real(0);
         fence();
         if (lane < 9) e5[jc * 5 + ic] = ec;
         fence();
-        const int j = 1 + jj, i = 1 + ii;
-        if (in9 && j >= 2 && i >= 2 && j <= 7 && i <= 7) {
-            const int cj = j >> 1, ci = i >> 1;
-            const Real *C0 = e5 + cj * 5;
-            Real w;
-            if ((j & 1) == 0) {
-                w = ((i & 1) == 0) ? C0[ci] : Real(0.5) * (C0[ci] + C0[ci + 1]);
-            } else {
-                const Real *C1 = C0 + 5;
-                w = ((i & 1) == 0) ? Real(0.5) * (C0[ci] + C1[ci])
-                                   : Real(0.25) * (C0[ci] + C0[ci + 1] + C1[ci] + C1[ci + 1]);
+        {
+            const Real w = pweight(e5, pg9, 5);
+            if (pg9.cor) {
+                x = x + w;
+                x9[k9] = x;
             }
-            x = x + w;
-            x9[k9] = x;
         }
         fence();
+        stamp(3);
         smooth(a.v2, cnt);
+        stamp(0);
     }
+#ifdef PGMG_TUNING
+    if (d.prof && lane == 0) {
+        for (int i = 0; i < 4; ++i) atomicAdd(&d.prof[8 + i], st[i]);
+        atomicAdd(&d.prof[15], (unsigned long long)reps);
+    }
+#endif
     return cnt;
 }
 
@@ -770,6 +817,12 @@ __device__ __forceinline__ Cnt tail_wq(const TailArgsDev<Real> &d, int l, int re
             ++c.sweeps;
         }
     };
+    PGeo pg[Q];
+    #pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int p = lane + 64 * q, jj = p / M;
+        pg[q] = pgeo(1 + jj, 1 + (p - M * jj), NN, NC, in[q]);
+    }
     // coarse interior point pc = lane + 64 qc: (1 + pc/MC, 1 + pc%MC), fine centre (2j, 2i)
     constexpr int QC = (MC * MC + 63) / 64;
     int kf[QC], kc9[QC];
@@ -782,8 +835,23 @@ __device__ __forceinline__ Cnt tail_wq(const TailArgsDev<Real> &d, int l, int re
         kc9[qc] = inc[qc] ? jc * NC + ic : NC + 1;
     }
     Cnt cnt;
+#ifdef PGMG_TUNING
+    // stage clocks of this level's own stages (PGMG_TAIL_PROF): prof[12..14] smooth,
+    // res+restrict, prolongation (the coarser visits excluded)
+    unsigned long long st[3] = {0, 0, 0}, tc = d.prof ? tail_clock() : 0;
+    auto stamp = [&](int i) {
+        if (d.prof) {
+            const unsigned long long t1 = tail_clock();
+            if (i >= 0) st[i] += t1 - tc;
+            tc = t1;
+        }
+    };
+#else
+    auto stamp = [](int) {};
+#endif
     for (int v = 0; v < reps; ++v) {
         smooth(a.v1, cnt);
+        stamp(0);
         // r = f - A x on the interior into T, then rc = R r straight into the 9x9 level's F
         // and e_coarse = 0 (MultiGrid.hpp:70-82; its boundary is never written, so stays 0)
         #pragma unroll
@@ -803,33 +871,34 @@ __device__ __forceinline__ Cnt tail_wq(const TailArgsDev<Real> &d, int l, int re
             }
         }
         fence();
+        stamp(1);
         if constexpr (NC == 9)
             cnt += tail_w9<Real>(d, l + 1, gamma, E, F, T);
         else
             cnt += tail_wq<Real, NC>(d, l + 1, gamma, E, F, T);
+        stamp(-1);
         // x += P e on fine points [2, 15]^2 (MultiGrid.hpp:208-226)
-        #pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const int p = lane + 64 * q, jj = p / M;
-            const int j = 1 + jj, i = 1 + (p - M * jj);
-            if (in[q] && j >= 2 && i >= 2 && j <= NN - 2 && i <= NN - 2) {
-                const int cj = j >> 1, ci = i >> 1;
-                const Real *C0 = xc9 + cj * NC;
-                Real w;
-                if ((j & 1) == 0) {
-                    w = ((i & 1) == 0) ? C0[ci] : Real(0.5) * (C0[ci] + C0[ci + 1]);
-                } else {
-                    const Real *C1 = C0 + NC;
-                    w = ((i & 1) == 0) ? Real(0.5) * (C0[ci] + C1[ci])
-                                       : Real(0.25) * (C0[ci] + C0[ci + 1] + C1[ci] + C1[ci + 1]);
+        {
+            Real w[Q];
+            #pragma unroll
+            for (int q = 0; q < Q; ++q) w[q] = pweight(xc9, pg[q], NC);
+            #pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                if (pg[q].cor) {
+                    x[q] = x[q] + w[q];
+                    x17[k[q]] = x[q];
                 }
-                x[q] = x[q] + w;
-                x17[k[q]] = x[q];
             }
         }
         fence();
+        stamp(2);
         smooth(a.v2, cnt);
+        stamp(0);
     }
+#ifdef PGMG_TUNING
+    if (d.prof && lane == 0 && NN == 17)
+        for (int q = 0; q < 3; ++q) atomicAdd(&d.prof[12 + q], st[q]);
+#endif
     return cnt;
 }
 

@@ -31,8 +31,15 @@ def main():
             (s.wcycle if kind == "W" else s.vcycle)(1)
             s.sync()
             assert lib.pgmg_tail_prof(buf, 1) == 0
+            w9 = list(buf)[8:16]
             v = list(buf)[:8]
             k = v[4] or 1
+            if w9[7]:
+                print(json.dumps({"w9_visits": w9[7], "w9_cycles_per_visit": {
+                    n: round(w9[i] / w9[7], 1) for i, n in enumerate(
+                        ["smooth (both)", "res+restrict", "coarsest solves", "prolong"])},
+                    "w17_cycles_per_visit": {n: round(w9[4 + i] / (w9[7] / 3), 1) for i, n in enumerate(
+                        ["smooth (both)", "res+restrict", "prolong"])}}))
             print(json.dumps({"N": N, "cycle": kind, "launches": v[5],
                               "cycles_per_launch": v[4] / max(v[5], 1),
                               "share": {NAMES[i]: round(v[i] / k, 4) for i in (0, 1, 2, 3, 6, 7)}}))
