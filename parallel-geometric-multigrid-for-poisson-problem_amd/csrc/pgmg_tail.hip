@@ -606,6 +606,68 @@ __device__ __forceinline__ Cnt tail_coarse5_regs(Real &x, Real f, const TailLeve
     return Cnt{sweeps, exits};
 }
 
+// The gamma coarsest solves of one 9x9 visit, each continuing from the previous one's result.
+// The iterates x_1, x_2, .. are one Jacobi sequence whatever the call boundaries are (a call
+// ends at the first check that fires, the next continues from that iterate), and in a W-cycle
+// every call ends at its first check (the oracle's statistics: 1.0 sweeps per call from the
+// second cycle on).  So the fast path computes x_1 .. x_gamma back to back — the sweeps are
+// the only dependent chain — with their gamma checks beside them, and keeps x_gamma when all
+// of them fire (gamma sweeps, gamma exits: exactly the sequential calls' work and counters);
+// otherwise the calls run one by one from the untouched x_0.
+template <class Real>
+__device__ __forceinline__ Cnt tail_coarse5_gamma(Real &x, Real f, const TailLevel<Real> L,
+                                                  int num_iter, double eps2, int gamma)
+{
+    if (gamma <= 3 && num_iter >= 1) {
+        const int lane = threadIdx.x & 63;
+        const bool act = lane < 9;
+        const int ii = lane - 3 * (lane / 3);
+        const bool has_l = ii != 0, has_r = ii != 2;
+        const Real hh = L.hh, ih = L.ih, hf = hh * f;
+        auto nbrs = [&](Real v, Real *o) __attribute__((always_inline)) {
+            o[0] = dpp_row<0x111>(v);
+            o[1] = dpp_row<0x101>(v);
+            o[2] = dpp_row<0x113>(v);
+            o[3] = dpp_row<0x103>(v);
+            __asm__ volatile("" : "+v"(o[0]), "+v"(o[1]), "+v"(o[2]), "+v"(o[3]));
+            if (!has_l) o[0] = Real(0);
+            if (!has_r) o[1] = Real(0);
+        };
+        // one sweep x -> J(x) and the check sum of r(J(x)) (its neighbours are the next
+        // sweep's; the sum is reduced over DPP row 0 as in tail_coarse5_regs)
+        auto sweep = [&](Real v) __attribute__((always_inline)) {
+            Real o[4];
+            nbrs(v, o);
+            const Real nx = Real(0.25) * (hf + o[0] + o[1] + o[2] + o[3]);
+            return act ? nx : Real(0);
+        };
+        auto check = [&](Real v) __attribute__((always_inline)) {
+            Real o[4];
+            nbrs(v, o);
+            const Real res = f - ih * (Real(4) * v - o[0] - o[1] - o[2] - o[3]);
+            double acc = act ? sq(res) : 0.0;
+            acc += dpp64<0x111>(acc);
+            acc += dpp64<0x112>(acc);
+            acc += dpp64<0x114>(acc);
+            acc += dpp64<0x118>(acc);
+            return readlane64(acc, 15);
+        };
+        const Real x1 = sweep(x);
+        const Real x2 = gamma >= 2 ? sweep(x1) : x1;
+        const Real x3 = gamma >= 3 ? sweep(x2) : x2;
+        const double s1 = check(x1);
+        const double s2 = gamma >= 2 ? check(x2) : 0.0;
+        const double s3 = gamma >= 3 ? check(x3) : 0.0;
+        if (s1 < eps2 && s2 < eps2 && s3 < eps2) {
+            x = gamma >= 3 ? x3 : (gamma == 2 ? x2 : x1);
+            return Cnt{gamma, gamma};
+        }
+    }
+    Cnt c;
+    for (int g = 0; g < gamma; ++g) c += tail_coarse5_regs(x, f, L, num_iter, eps2);
+    return c;
+}
+
 // `reps` gamma-cycles of a 9x9 level whose coarser level is the 5x5 coarsest one, on wave 0:
 // smoothing of the 9x9 level in LDS (tail_smooth_small), its residual and full-weighting
 // restriction straight into the coarse lanes' registers, the gamma coarsest solves in
@@ -641,7 +703,10 @@ __device__ __forceinline__ Cnt tail_w9(const TailArgsDev<Real> &d, int l, int re
     // JacobiSmoother::smooth on the 9x9 level with the iterate in registers: sweeps in place
     // (the wave's reads of the old neighbours precede its writes), the check of x_k fused
     // into sweep k+1 and undone from the register copy when it fires (tail_smooth_small)
-    auto smooth = [&](int num_iter, Cnt &c) __attribute__((always_inline)) {
+    // returns true when a check fired: rlast then holds r(result), the residual the
+    // restriction needs (the check computed it with the result's neighbours)
+    Real rlast = Real(0);
+    auto smooth = [&](int num_iter, Cnt &c) __attribute__((always_inline)) -> bool {
         Real nx = Real(0.25) * (hf + x9[k9 - 1] + x9[k9 + 1] + x9[k9 - 9] + x9[k9 + 9]);
         fence();
         if (in9) x9[k9] = nx;
@@ -661,11 +726,13 @@ __device__ __forceinline__ Cnt tail_w9(const TailArgsDev<Real> &d, int l, int re
                 if (in9) x9[k9] = x;
                 fence();
                 ++c.exits;
-                return;
+                rlast = res;
+                return true;
             }
             x = nx;
             ++c.sweeps;
         }
+        return false;
     };
     Cnt cnt;
 #ifdef PGMG_TUNING
@@ -683,10 +750,15 @@ __device__ __forceinline__ Cnt tail_w9(const TailArgsDev<Real> &d, int l, int re
     auto stamp = [](int) {};
 #endif
     for (int v = 0; v < reps; ++v) {
-        smooth(a.v1, cnt);
+        const bool have_r = smooth(a.v1, cnt);
         stamp(0);
-        // r = f - A x on the interior (DynamicGridUtils.hpp:59-69), into T
-        if (in9) T[k9] = fk - ih * (Real(4) * x - x9[k9 - 1] - x9[k9 + 1] - x9[k9 - 9] - x9[k9 + 9]);
+        // r = f - A x on the interior (DynamicGridUtils.hpp:59-69), into T: the check's
+        // residual of the result when a check fired (the same expression on the same values)
+        if (have_r) {
+            if (in9) T[k9] = rlast;
+        } else {
+            if (in9) T[k9] = fk - ih * (Real(4) * x - x9[k9 - 1] - x9[k9 + 1] - x9[k9 - 9] - x9[k9 + 9]);
+        }
         fence();
         // rc = R r (MultiGrid.hpp:187-205); e_coarse = 0 (:81-82)
         Real fc = Real(0), ec = Real(0);
@@ -694,8 +766,7 @@ __device__ __forceinline__ Cnt tail_w9(const TailArgsDev<Real> &d, int l, int re
             fc = Real(0.25) * T[kc] + Real(0.125) * (T[kc + 1] + T[kc - 1] + T[kc + 9] + T[kc - 9]) +
                  Real(0.0625) * (T[kc - 9 - 1] + T[kc - 9 + 1] + T[kc + 9 - 1] + T[kc + 9 + 1]);
         stamp(1);
-        for (int g = 0; g < gamma; ++g)
-            cnt += tail_coarse5_regs(ec, fc, L5, a.coarse_iter, eps2);
+        cnt += tail_coarse5_gamma(ec, fc, L5, a.coarse_iter, eps2, gamma);
         stamp(2);
         // the correction into LDS (5x5, boundary 0), then x += P e on [2, 7]^2 (:208-226)
         if (lane < 25) e5[lane] = Real(0);
@@ -773,8 +844,10 @@ __device__ __forceinline__ Cnt tail_wq(const TailArgsDev<Real> &d, int l, int re
         if constexpr (REGF) return hfr[q];
         else return hh * f17[k[q]];
     };
-    auto smooth = [&](int num_iter, Cnt &c) __attribute__((always_inline)) {
-        Real nx[Q];
+    // returns true when a check fired: rl[] then holds r(result) (see tail_w9)
+    Real rl[Q];
+    auto smooth = [&](int num_iter, Cnt &c) __attribute__((always_inline)) -> bool {
+        Real nx[Q], rs[Q];
         #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const int kk = k[q];
@@ -796,6 +869,7 @@ __device__ __forceinline__ Cnt tail_wq(const TailArgsDev<Real> &d, int l, int re
                 const Real l0 = x17[kk - 1], r0 = x17[kk + 1], u0 = x17[kk - NN], d0 = x17[kk + NN];
                 const Real res = fk(q) - ih * (Real(4) * x[q] - l0 - r0 - u0 - d0);
                 if (in[q]) acc += sq(res);
+                rs[q] = res;
                 nx[q] = Real(0.25) * (hf(q) + l0 + r0 + u0 + d0);
             }
             fence();
@@ -806,16 +880,19 @@ __device__ __forceinline__ Cnt tail_wq(const TailArgsDev<Real> &d, int l, int re
             const double s = wave_sum(acc);
             if (s < eps2) {   // x_{it-1} is the result
                 #pragma unroll
-                for (int q = 0; q < Q; ++q)
+                for (int q = 0; q < Q; ++q) {
                     if (in[q]) x17[k[q]] = x[q];
+                    rl[q] = rs[q];
+                }
                 fence();
                 ++c.exits;
-                return;
+                return true;
             }
             #pragma unroll
             for (int q = 0; q < Q; ++q) x[q] = nx[q];
             ++c.sweeps;
         }
+        return false;
     };
     PGeo pg[Q];
     #pragma unroll
@@ -850,15 +927,22 @@ __device__ __forceinline__ Cnt tail_wq(const TailArgsDev<Real> &d, int l, int re
     auto stamp = [](int) {};
 #endif
     for (int v = 0; v < reps; ++v) {
-        smooth(a.v1, cnt);
+        const bool have_r = smooth(a.v1, cnt);
         stamp(0);
-        // r = f - A x on the interior into T, then rc = R r straight into the 9x9 level's F
-        // and e_coarse = 0 (MultiGrid.hpp:70-82; its boundary is never written, so stays 0)
-        #pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const int kk = k[q];
-            if (in[q])
-                T[kk] = fk(q) - ih * (Real(4) * x[q] - x17[kk - 1] - x17[kk + 1] - x17[kk - NN] - x17[kk + NN]);
+        // r = f - A x on the interior into T (the check's residual of the result when a check
+        // fired), then rc = R r straight into the 9x9 level's F and e_coarse = 0
+        // (MultiGrid.hpp:70-82; its boundary is never written, so stays 0)
+        if (have_r) {
+            #pragma unroll
+            for (int q = 0; q < Q; ++q)
+                if (in[q]) T[k[q]] = rl[q];
+        } else {
+            #pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const int kk = k[q];
+                if (in[q])
+                    T[kk] = fk(q) - ih * (Real(4) * x[q] - x17[kk - 1] - x17[kk + 1] - x17[kk - NN] - x17[kk + NN]);
+            }
         }
         fence();
         #pragma unroll
