@@ -633,33 +633,31 @@ __device__ __forceinline__ Cnt tail_coarse5_gamma(Real &x, Real f, const TailLev
             if (!has_l) o[0] = Real(0);
             if (!has_r) o[1] = Real(0);
         };
-        // one sweep x -> J(x) and the check sum of r(J(x)) (its neighbours are the next
-        // sweep's; the sum is reduced over DPP row 0 as in tail_coarse5_regs)
-        auto sweep = [&](Real v) __attribute__((always_inline)) {
-            Real o[4];
-            nbrs(v, o);
-            const Real nx = Real(0.25) * (hf + o[0] + o[1] + o[2] + o[3]);
-            return act ? nx : Real(0);
-        };
-        auto check = [&](Real v) __attribute__((always_inline)) {
-            Real o[4];
-            nbrs(v, o);
-            const Real res = f - ih * (Real(4) * v - o[0] - o[1] - o[2] - o[3]);
-            double acc = act ? sq(res) : 0.0;
-            acc += dpp64<0x111>(acc);
-            acc += dpp64<0x112>(acc);
-            acc += dpp64<0x114>(acc);
-            acc += dpp64<0x118>(acc);
-            return readlane64(acc, 15);
-        };
-        const Real x1 = sweep(x);
-        const Real x2 = gamma >= 2 ? sweep(x1) : x1;
-        const Real x3 = gamma >= 3 ? sweep(x2) : x2;
-        const double s1 = check(x1);
-        const double s2 = gamma >= 2 ? check(x2) : 0.0;
-        const double s3 = gamma >= 3 ? check(x3) : 0.0;
-        if (s1 < eps2 && s2 < eps2 && s3 < eps2) {
-            x = gamma >= 3 ? x3 : (gamma == 2 ? x2 : x1);
+        // x_k's neighbours serve both its check r(x_k) and the next sweep J(x_k); the gamma
+        // checks are summed per lane and reduced ONCE: every lane's sum bounds each of its
+        // terms and the DPP reduction tree is the same for both, so (fl(a + b) is monotone in
+        // a and b) the reduced total bounds every reduced check sum — a total below eps2
+        // means every check fires; otherwise the exact sequential calls decide
+        Real o[4];
+        nbrs(x, o);
+        const Real x1 = act ? Real(0.25) * (hf + o[0] + o[1] + o[2] + o[3]) : Real(0);
+        Real xk = x1, xl = x1;
+        double acc = 0.0;
+        #pragma unroll
+        for (int g = 1; g <= 3; ++g) {
+            if (g > gamma) break;
+            nbrs(xk, o);
+            const Real res = f - ih * (Real(4) * xk - o[0] - o[1] - o[2] - o[3]);
+            acc += act ? sq(res) : 0.0;
+            xl = xk;
+            if (g < gamma) xk = act ? Real(0.25) * (hf + o[0] + o[1] + o[2] + o[3]) : Real(0);
+        }
+        acc += dpp64<0x111>(acc);
+        acc += dpp64<0x112>(acc);
+        acc += dpp64<0x114>(acc);
+        acc += dpp64<0x118>(acc);
+        if (readlane64(acc, 15) < eps2) {
+            x = xl;
             return Cnt{gamma, gamma};
         }
     }
@@ -749,24 +747,16 @@ __device__ __forceinline__ Cnt tail_w9(const TailArgsDev<Real> &d, int l, int re
 #else
     auto stamp = [](int) {};
 #endif
-    for (int v = 0; v < reps; ++v) {
-        const bool have_r = smooth(a.v1, cnt);
-        stamp(0);
-        // r = f - A x on the interior (DynamicGridUtils.hpp:59-69), into T: the check's
-        // residual of the result when a check fired (the same expression on the same values)
-        if (have_r) {
-            if (in9) T[k9] = rlast;
-        } else {
-            if (in9) T[k9] = fk - ih * (Real(4) * x - x9[k9 - 1] - x9[k9 + 1] - x9[k9 - 9] - x9[k9 + 9]);
-        }
-        fence();
+    // the rest of a visit once T holds the residual of the pre-smoothed iterate: restriction,
+    // the gamma coarsest solves, prolongation, post-smooth
+    auto rest = [&](Cnt &c) __attribute__((always_inline)) {
         // rc = R r (MultiGrid.hpp:187-205); e_coarse = 0 (:81-82)
         Real fc = Real(0), ec = Real(0);
         if (lane < 9)
             fc = Real(0.25) * T[kc] + Real(0.125) * (T[kc + 1] + T[kc - 1] + T[kc + 9] + T[kc - 9]) +
                  Real(0.0625) * (T[kc - 9 - 1] + T[kc - 9 + 1] + T[kc + 9 - 1] + T[kc + 9 + 1]);
         stamp(1);
-        cnt += tail_coarse5_gamma(ec, fc, L5, a.coarse_iter, eps2, gamma);
+        c += tail_coarse5_gamma(ec, fc, L5, a.coarse_iter, eps2, gamma);
         stamp(2);
         // the correction into LDS (5x5, boundary 0), then x += P e on [2, 7]^2 (:208-226)
         if (lane < 25) e5[lane] = Real(0);
@@ -782,8 +772,54 @@ __device__ __forceinline__ Cnt tail_w9(const TailArgsDev<Real> &d, int l, int re
         }
         fence();
         stamp(3);
-        smooth(a.v2, cnt);
+        smooth(a.v2, c);
         stamp(0);
+    };
+    bool spec = gamma > 1;   // W-cycles (a V-cycle's 9x9 level needs two sweeps early on)
+    for (int v = 0; v < reps; ++v) {
+        // Fast path: the pre-smooth's first check fires (a 9x9 level of a W-cycle exits after
+        // its first sweep in ~99 % of the visits from the second cycle on).  Its decision
+        // (the norm's reduction, read-out and compare: a long dependent chain) is taken after
+        // the rest of the visit instead of before it, the speculative second sweep is not
+        // computed, and when it turns out not to fire the visit is rolled back to its start
+        // (x in registers and LDS; the coarse grid and T are rewritten anyway) and run exactly.
+        if (spec && a.v1 >= 1) {
+            const Real x0 = x;
+            Cnt cf;
+            const Real nx = Real(0.25) * (hf + x9[k9 - 1] + x9[k9 + 1] + x9[k9 - 9] + x9[k9 + 9]);
+            fence();
+            if (in9) x9[k9] = nx;
+            fence();
+            x = nx;
+            cf.sweeps = 1;
+            const Real l0 = x9[k9 - 1], r0 = x9[k9 + 1], u0 = x9[k9 - 9], d0 = x9[k9 + 9];
+            const Real res = fk - ih * (Real(4) * x - l0 - r0 - u0 - d0);
+            const double s_pre = wave_sum(in9 ? sq(res) : 0.0);
+            cf.exits = 1;
+            stamp(0);
+            if (in9) T[k9] = res;
+            fence();
+            rest(cf);
+            if (s_pre < eps2) {
+                cnt += cf;
+                continue;
+            }
+            x = x0;   // roll back, and decide in order for the rest of this call
+            if (in9) x9[k9] = x0;
+            fence();
+            spec = false;
+        }
+        const bool have_r = smooth(a.v1, cnt);
+        stamp(0);
+        // r = f - A x on the interior (DynamicGridUtils.hpp:59-69), into T: the check's
+        // residual of the result when a check fired (the same expression on the same values)
+        if (have_r) {
+            if (in9) T[k9] = rlast;
+        } else {
+            if (in9) T[k9] = fk - ih * (Real(4) * x - x9[k9 - 1] - x9[k9 + 1] - x9[k9 - 9] - x9[k9 + 9]);
+        }
+        fence();
+        rest(cnt);
     }
 #ifdef PGMG_TUNING
     if (d.prof && lane == 0) {
@@ -926,25 +962,9 @@ __device__ __forceinline__ Cnt tail_wq(const TailArgsDev<Real> &d, int l, int re
 #else
     auto stamp = [](int) {};
 #endif
-    for (int v = 0; v < reps; ++v) {
-        const bool have_r = smooth(a.v1, cnt);
-        stamp(0);
-        // r = f - A x on the interior into T (the check's residual of the result when a check
-        // fired), then rc = R r straight into the 9x9 level's F and e_coarse = 0
-        // (MultiGrid.hpp:70-82; its boundary is never written, so stays 0)
-        if (have_r) {
-            #pragma unroll
-            for (int q = 0; q < Q; ++q)
-                if (in[q]) T[k[q]] = rl[q];
-        } else {
-            #pragma unroll
-            for (int q = 0; q < Q; ++q) {
-                const int kk = k[q];
-                if (in[q])
-                    T[kk] = fk(q) - ih * (Real(4) * x[q] - x17[kk - 1] - x17[kk + 1] - x17[kk - NN] - x17[kk + NN]);
-            }
-        }
-        fence();
+    // rc = R r straight into the coarser level's F and e_coarse = 0 (MultiGrid.hpp:70-82; its
+    // boundary is never written, so stays 0), r in T
+    auto restrict_T = [&]() __attribute__((always_inline)) {
         #pragma unroll
         for (int qc = 0; qc < QC; ++qc) {
             if (inc[qc]) {
@@ -955,6 +975,77 @@ __device__ __forceinline__ Cnt tail_wq(const TailArgsDev<Real> &d, int l, int re
             }
         }
         fence();
+    };
+    bool spec = gamma > 1;   // W-cycles (see tail_w9)
+    for (int v = 0; v < reps; ++v) {
+        // Fast path (as tail_w9's, over a shorter span): assume the pre-smooth's first check
+        // fires, restrict r(x_1) while its norm is reduced, decide before the coarser visits;
+        // when it does not fire, roll x back to x_0 and smooth in order
+        bool pre_done = false;
+        if (spec && a.v1 >= 1) {
+            Real x0[Q], nx[Q];
+            #pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const int kk = k[q];
+                x0[q] = x[q];
+                nx[q] = Real(0.25) * (hf(q) + x17[kk - 1] + x17[kk + 1] + x17[kk - NN] + x17[kk + NN]);
+            }
+            fence();
+            #pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                if (in[q]) x17[k[q]] = nx[q];
+                x[q] = nx[q];
+            }
+            fence();
+            double acc = 0.0;
+            #pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const int kk = k[q];
+                const Real l0 = x17[kk - 1], r0 = x17[kk + 1], u0 = x17[kk - NN], d0 = x17[kk + NN];
+                const Real res = fk(q) - ih * (Real(4) * x[q] - l0 - r0 - u0 - d0);
+                if (in[q]) {
+                    acc += sq(res);
+                    T[kk] = res;
+                }
+            }
+            const double s_pre = wave_sum(acc);
+            fence();
+            stamp(0);
+            restrict_T();
+            if (s_pre < eps2) {
+                ++cnt.sweeps;
+                ++cnt.exits;
+                pre_done = true;
+            } else {
+                #pragma unroll
+                for (int q = 0; q < Q; ++q) {
+                    x[q] = x0[q];
+                    if (in[q]) x17[k[q]] = x0[q];
+                }
+                fence();
+                spec = false;
+            }
+        }
+        if (!pre_done) {
+            const bool have_r = smooth(a.v1, cnt);
+            stamp(0);
+            // r = f - A x on the interior into T (the check's residual of the result when a
+            // check fired)
+            if (have_r) {
+                #pragma unroll
+                for (int q = 0; q < Q; ++q)
+                    if (in[q]) T[k[q]] = rl[q];
+            } else {
+                #pragma unroll
+                for (int q = 0; q < Q; ++q) {
+                    const int kk = k[q];
+                    if (in[q])
+                        T[kk] = fk(q) - ih * (Real(4) * x[q] - x17[kk - 1] - x17[kk + 1] - x17[kk - NN] - x17[kk + NN]);
+                }
+            }
+            fence();
+            restrict_T();
+        }
         stamp(1);
         if constexpr (NC == 9)
             cnt += tail_w9<Real>(d, l + 1, gamma, E, F, T);
