@@ -1342,9 +1342,11 @@ int launch_post(const PostArgsT<T> &a0, bool fine, hipStream_t s)
 // one round per ~2700 fine rows: 3072 on the full 16385 grid (r01: 2048 1.30 ms, 3072 1.18,
 // 4096 1.25), 512 on strips of 2048 / 4096 rows (scripts/strip_probe.py, per-rank time at
 // 8 ranks 0.43 -> 0.39 ms; 768 / 1024, i.e. 1.5 / 2 rounds of short bands, lose)
+// (r02: bands of ~190 fine rows are the invariant — on the 32769 grid 12 rounds, 6144
+// workgroups, beat 6: 6.79 -> 6.70 ms per V-cycle; 9216 / 12288 the same as 6144)
 static int pp_target(int jc0, int jc1)
 {
-    const int rounds = std::max(1, std::min(6, 6 * (2 * (jc1 - jc0) + 64) / 16384));
+    const int rounds = std::max(1, std::min(12, 6 * (2 * (jc1 - jc0) + 64) / 16384));
     return tuning_int("PGMG_PP_BLOCKS", (2048 / kPPWaves) * rounds);   // 512 resident at 4 waves
 }
 
