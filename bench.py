@@ -68,6 +68,9 @@ def parse():
                     help="auto: HBM traffic of the finest-level passes from two rocprofv3 --pmc "
                          "passes (FETCH_SIZE, WRITE_SIZE) over a short child run of this build, "
                          "before this process touches the GPU")
+    ap.add_argument("--other-configs", choices=["auto", "off"], default="auto",
+                    help="auto (the default headline run only: one GPU, V, f64, N = 16385): also "
+                         "time BASELINE.json's other GPU configs on this GPU, each hash-checked")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -330,6 +333,65 @@ def main():
             and main_leg["gen"]):
         gen_leg = run_leg(pg.PGMG_FLAG_STORED_RHS, 3)
 
+    # BASELINE.json's other GPU configs on this one GPU (timed after the headline legs, each
+    # with the reference's hash of its result; the 8-GPU configs' grids as one GPU's run)
+    others = None
+    if (world == 1 and args.other_configs == "auto" and args.cycle == "V" and args.dtype == "f64"
+            and args.n == 16385):
+        others = []
+
+        def timed(s, run, warm, k, reps):
+            ts = []
+            for _ in range(reps):
+                s.set_problem()
+                run(warm)
+                s.sync()
+                t0 = time.perf_counter()
+                run(k)
+                s.sync()
+                ts.append(time.perf_counter() - t0)
+            return statistics.median(ts)
+
+        def hashed(s, runs, kind, n, cycles):
+            s.set_problem()
+            for run, k in runs:
+                run(k)
+            s.sync()
+            w = golden_hash(kind, n, cycles)
+            h = s.solution_hash(0)
+            return None if w is None or h is None else h == w
+
+        with pg.Solver(4097, device=device) as s:   # configs[1]
+            dt = timed(s, s.vcycle, 3, 40, 3)
+            others.append({"config": "BASELINE configs[1]: 1xMI355X V-cycle, N=4096^2, 2+2 Jacobi, "
+                                     "6 bulk levels, fp64",
+                           "value": round(40 / dt, 2), "unit": "V-cycles/s",
+                           "ms_per_step": round(dt * 1e3 / 40, 4), "timed": "3 + 40 cycles, median of 3",
+                           "parity": hashed(s, [(s.vcycle, 3)], "V", 4097, 3)})
+        with pg.Solver(32769, device=device) as s:  # configs[3]'s grid on one GPU
+            dt = timed(s, s.vcycle, 1, 5, 3)
+            others.append({"config": "BASELINE configs[3]'s grid (N=32768^2) on ONE MI355X: V-cycle, fp64 "
+                                     "(the 8-GPU row-strip run is the driver's scaling bench)",
+                           "value": round(5 / dt, 3), "unit": "V-cycles/s",
+                           "ms_per_step": round(dt * 1e3 / 5, 4), "timed": "1 + 5 cycles, median of 3",
+                           "parity": hashed(s, [(s.vcycle, 2)], "V", 32769, 2)})
+            # configs[4]'s cycle: the FMG start (one F-cycle) then one W-cycle, fp64
+            s.set_problem()
+            t0 = time.perf_counter()
+            s.fcycle(1)
+            s.sync()
+            t1 = time.perf_counter()
+            s.wcycle(1)
+            s.sync()
+            t2 = time.perf_counter()
+            w = golden_hash("G", 32769, 2)
+            h = s.solution_hash(0)
+            others.append({"config": "BASELINE configs[4]'s cycle (N=32768^2) on ONE MI355X: FMG start "
+                                     "(one F-cycle) + one W-cycle, fp64 (fp32-vs-fp64 sweep: "
+                                     "profiles/r02_fp32/)",
+                           "f_cycle_s": round(t1 - t0, 4), "w_cycle_s": round(t2 - t1, 4),
+                           "parity": None if w is None or h is None else h == w})
+
     T = "double" if args.dtype == "f64" else "float"
 
     def roofline(leg):
@@ -434,6 +496,8 @@ def main():
             "pmc": pmc_note,
             "build": lib_build_id(),
         }
+        if others is not None:
+            line["other_configs"] = others
         if gen_leg is not None:
             gmed = statistics.median(gen_leg["times"])
             groof = roofline(gen_leg)
