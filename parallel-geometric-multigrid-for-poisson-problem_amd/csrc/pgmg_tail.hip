@@ -416,7 +416,36 @@ __device__ __forceinline__ int tail_small_index(int p, int m, int N)
     return (1 + jj) * N + 1 + (p - jj * m);
 }
 
-// T = r(x) on the interior, 0 on the boundary; then fc = R T (MultiGrid.hpp:70-78)
+// Bilinear prolongation of one fine point (j, i) of a tail level (MultiGrid.hpp:208-226),
+// branch-free: the four parity cases are the one expression s * (((a + b) + c) + d) with the
+// unused terms -0.0 (x + (-0) == x for every x, and 1 * x == x), so every case performs the
+// reference's operations in its order.  The geometry is computed once per call.
+struct PGeo {
+    int ob, boff;   // coarse (cj, ci) offset; offset of the second term (1 or NC)
+    bool cor;       // the point is corrected: j, i in [2, Nf - 2]
+    bool mb, mcd;   // term b is used (i or j odd); terms c, d are used (both odd)
+};
+__device__ __forceinline__ PGeo pgeo(int j, int i, int Nf, int NC, bool in)
+{
+    PGeo g;
+    const bool jo = (j & 1) != 0, io = (i & 1) != 0;
+    g.cor = in && j >= 2 && i >= 2 && j <= Nf - 2 && i <= Nf - 2;
+    g.ob = g.cor ? (j >> 1) * NC + (i >> 1) : 0;
+    g.boff = io ? 1 : NC;
+    g.mb = jo || io;
+    g.mcd = jo && io;
+    return g;
+}
+template <class Real>
+__device__ __forceinline__ Real pweight(const Real *C, const PGeo &g, int NC)
+{
+    const Real a = C[g.ob], b = C[g.ob + g.boff], c = C[g.ob + NC], d = C[g.ob + NC + 1];
+    const Real nz = -Real(0);
+    const Real s = g.mcd ? Real(0.25) : (g.mb ? Real(0.5) : Real(1));
+    return s * (((a + (g.mb ? b : nz)) + (g.mcd ? c : nz)) + (g.mcd ? d : nz));
+}
+
+// T = r(x) on the interior (its boundary is never read); then fc = R T (MultiGrid.hpp:70-78)
 template <class Team, class Real>
 __device__ __forceinline__ void tail_res_restrict(const Real *x, const Real *f, const TailLevel<Real> &Lf, Real *fc,
                                   Real *ec, const TailLevel<Real> &Lc, Real *T)
@@ -447,14 +476,12 @@ __device__ __forceinline__ void tail_res_restrict(const Real *x, const Real *f, 
             return;
         }
     }
-    const int N = Lf.N, n = N * N;
-    for (int k = Team::tid(); k < n; k += Team::size) {
-        const int j = tail_row(k, Lf.rN);
-        const int i = k - j * N;
-        if (i == 0 || j == 0 || i == N - 1 || j == N - 1) {
-            T[k] = Real(0);
-            continue;
-        }
+    // the residual on the interior only: the restriction reads no boundary point of T
+    const int N = Lf.N, m = N - 2, mm = m * m;
+    const float rm = 1.0f / (float)m;
+    for (int p = Team::tid(); p < mm; p += Team::size) {
+        const int jj = tail_row(p, rm);
+        const int k = (1 + jj) * N + 1 + (p - jj * m);
         T[k] = f[k] - Lf.ih * (Real(4) * x[k] - x[k - 1] - x[k + 1] - x[k - N] - x[k + N]);
     }
     Team::sync();
@@ -495,17 +522,8 @@ __device__ __forceinline__ void tail_prolong(Real *x, const TailLevel<Real> &Lf,
             i = k - j * N;
             if (i < 2 || j < 2 || i > N - 2 || j > N - 2) continue;
         }
-        const int jc = j >> 1, ic = i >> 1;
-        const Real *C0 = e + jc * Nc;
-        Real v;
-        if ((j & 1) == 0) {
-            v = ((i & 1) == 0) ? C0[ic] : Real(0.5) * (C0[ic] + C0[ic + 1]);
-        } else {
-            const Real *C1 = C0 + Nc;
-            v = ((i & 1) == 0) ? Real(0.5) * (C0[ic] + C1[ic])
-                               : Real(0.25) * (C0[ic] + C0[ic + 1] + C1[ic] + C1[ic + 1]);
-        }
-        x[k] = x[k] + v;
+        // (branch-free, see pweight: the four parity cases in one expression)
+        x[k] = x[k] + pweight(e, pgeo(j, i, N, Nc, true), Nc);
     }
     Team::sync();
 }
@@ -516,35 +534,6 @@ template <int CTRL> __device__ __forceinline__ double dpp_row(double v) { return
 template <int CTRL> __device__ __forceinline__ float dpp_row(float v)
 {
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
-}
-
-// Bilinear prolongation of one fine point (j, i) of a wave-team level (MultiGrid.hpp:208-226),
-// branch-free: the four parity cases are the one expression s * (((a + b) + c) + d) with the
-// unused terms -0.0 (x + (-0) == x for every x, and 1 * x == x), so every case performs the
-// reference's operations in its order.  The geometry is computed once per call.
-struct PGeo {
-    int ob, boff;   // coarse (cj, ci) offset; offset of the second term (1 or NC)
-    bool cor;       // the point is corrected: j, i in [2, Nf - 2]
-    bool mb, mcd;   // term b is used (i or j odd); terms c, d are used (both odd)
-};
-__device__ __forceinline__ PGeo pgeo(int j, int i, int Nf, int NC, bool in)
-{
-    PGeo g;
-    const bool jo = (j & 1) != 0, io = (i & 1) != 0;
-    g.cor = in && j >= 2 && i >= 2 && j <= Nf - 2 && i <= Nf - 2;
-    g.ob = g.cor ? (j >> 1) * NC + (i >> 1) : 0;
-    g.boff = io ? 1 : NC;
-    g.mb = jo || io;
-    g.mcd = jo && io;
-    return g;
-}
-template <class Real>
-__device__ __forceinline__ Real pweight(const Real *C, const PGeo &g, int NC)
-{
-    const Real a = C[g.ob], b = C[g.ob + g.boff], c = C[g.ob + NC], d = C[g.ob + NC + 1];
-    const Real nz = -Real(0);
-    const Real s = g.mcd ? Real(0.25) : (g.mb ? Real(0.5) : Real(1));
-    return s * (((a + (g.mb ? b : nz)) + (g.mcd ? c : nz)) + (g.mcd ? d : nz));
 }
 
 // The coarsest solve (JacobiSmoother::smooth with coarse_iter, Smoother.hpp:38-116) of a 5x5
