@@ -1224,13 +1224,34 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(TailArgsDev<Real> d)
     for (int k = threadIdx.x; k < 2 * S; k += kTailThreads) E[k] = Real(0);
     __syncthreads();
     {
+        // the top level from global memory: every load of a thread issued before the first
+        // LDS store (a load-store loop waited one global-memory latency per point)
         const int N = d.lv[0].N, n = N * N;
         const long long P = a.P_top;
-        for (int k = threadIdx.x; k < n; k += kTailThreads) {
+        const bool ldf = !a.fmg, lde = a.x0_from_global || a.fmg;
+        constexpr int KU = (65 * 65 + kTailThreads - 1) / kTailThreads;   // N_top <= 65
+        Real fv[KU], ev[KU];
+        #pragma unroll
+        for (int q = 0; q < KU; ++q) {
+            // (clamped: a point past the grid re-reads the last one, never past the array)
+            const int k = min((int)threadIdx.x + q * kTailThreads, n - 1);
+            const int j = tail_row(k, d.lv[0].rN), i = k - j * N;
+            fv[q] = ldf ? a.f_top[j * P + i] : Real(0);
+            ev[q] = lde ? a.e_top[j * P + i] : Real(0);
+        }
+        #pragma unroll
+        for (int q = 0; q < KU; ++q) {
+            const int k = threadIdx.x + q * kTailThreads;
+            if (k < n) {
+                if (ldf) F[k] = fv[q];
+                if (lde) E[k] = ev[q];
+            }
+        }
+        for (int k = threadIdx.x + KU * kTailThreads; k < n; k += kTailThreads) {
             const int j = k / N;
             const int i = k - j * N;
-            if (!a.fmg) F[k] = a.f_top[j * P + i];
-            if (a.x0_from_global || a.fmg) E[k] = a.e_top[j * P + i];
+            if (ldf) F[k] = a.f_top[j * P + i];
+            if (lde) E[k] = a.e_top[j * P + i];
         }
     }
     __syncthreads();
