@@ -71,6 +71,10 @@ def parse():
     ap.add_argument("--other-configs", choices=["auto", "off"], default="auto",
                     help="auto (the default headline run only: one GPU, V, f64, N = 16385): also "
                          "time BASELINE.json's other GPU configs on this GPU, each hash-checked")
+    ap.add_argument("--fast-mode", choices=["auto", "off"], default="auto",
+                    help="auto (one GPU, V, f64): also time PGMG_FLAG_FAST (FMA / shared "
+                         "neighbour sums in the finest pass; not bitwise) and report its "
+                         "difference from the EXACT result")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -144,6 +148,8 @@ def pmc_child(args):
     legs = [0]
     if args.cycle == "V" and args.general_rhs == "auto":
         legs.append(pg.PGMG_FLAG_STORED_RHS)
+    if args.cycle == "V" and args.dtype == "f64" and args.fast_mode == "auto":
+        legs.append(pg.PGMG_FLAG_FAST)
     for flags in legs:
         with pg.Solver(args.n, flags=flags, dtype=args.dtype) as s:
             s.set_problem()
@@ -168,7 +174,7 @@ def live_pmc(args):
         cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", ctr, "--output-format", "csv",
                "-d", d, "-o", "run", "--", sys.executable, str(ROOT / "bench.py"), "--pmc-child",
                "--n", str(args.n), "--dtype", args.dtype, "--cycle", args.cycle,
-               "--general-rhs", args.general_rhs]
+               "--general-rhs", args.general_rhs, "--fast-mode", args.fast_mode]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=180)
             files = list(pathlib.Path(d).rglob("*counter_collection.csv"))
@@ -392,6 +398,29 @@ def main():
                            "f_cycle_s": round(t1 - t0, 4), "w_cycle_s": round(t2 - t1, 4),
                            "parity": None if w is None or h is None else h == w})
 
+    # FAST mode (PGMG_FLAG_FAST): its rate, and phi after 10 cycles (SURVEY §8(c)'s window:
+    # later, near convergence, a borderline early-exit check may decide differently) against
+    # the EXACT default's (relative L2 and max-abs; tolerance in tests/test_gpu_fast.py)
+    fast_leg = fast_cmp = None
+    if (world == 1 and args.cycle == "V" and args.dtype == "f64" and args.fast_mode == "auto"
+            and main_leg["fused"]):
+        import numpy as np
+        fast_leg = run_leg(pg.PGMG_FLAG_FAST, 3)
+        sols = []
+        for fl in (0, pg.PGMG_FLAG_FAST):
+            s = new_solver(fl)
+            s.set_problem()
+            s.vcycle(10)
+            sols.append((s.solution(), s.stats()[0]))
+            s.close()
+        (ref_phi, ref_sw), (got_phi, got_sw) = sols
+        d = got_phi - ref_phi
+        fast_cmp = {"cycles": 10, "tolerance": "tests/test_gpu_fast.py (3e-11 at N = 16385)",
+                    "rel_l2_vs_exact": float(np.linalg.norm(d) / np.linalg.norm(ref_phi)),
+                    "max_abs_vs_exact": float(np.max(np.abs(d))),
+                    "sweep_counts_equal": ref_sw == got_sw}
+        del sols, ref_phi, got_phi, d
+
     T = "double" if args.dtype == "f64" else "float"
 
     def roofline(leg):
@@ -407,6 +436,8 @@ def main():
                 f"k_post<{T},true,2,false,true>" if leg["gen"] else f"k_post<{T},true,2,false>"),
             0: ("k_sweep (finest-level Jacobi sweep, unfused path)", f"k_sweep<{T},false,false,true>"),
         }
+        if leg.get("fast"):
+            names[3] = (names[3][0] + " — FAST mode", names[3][1].replace(",2>", ",18>"))
         roof = []
         for w, cnt, ms in leg["passes"]:
             if not cnt or ms <= 0:
@@ -498,6 +529,20 @@ def main():
         }
         if others is not None:
             line["other_configs"] = others
+        if fast_leg is not None:
+            fast_leg["fast"] = True
+            fmed = statistics.median(fast_leg["times"])
+            froof = roofline(fast_leg)
+            line["fast_mode"] = {
+                "what": "PGMG_FLAG_FAST: the finest cross-cycle pass with shared neighbour sums "
+                        "and FMA residuals (not the reference's expression order: a tolerance, "
+                        "not bitwise; SURVEY §8(c) FAST mode)",
+                "value": round(args.steps / fmed, 4), "unit": "V-cycles/s",
+                "ms_per_step": round(fmed * 1e3 / args.steps, 4),
+                "repetitions": len(fast_leg["times"]),
+                "vs_exact": fast_cmp,
+                "roofline": froof[0] if froof else None,
+            }
         if gen_leg is not None:
             gmed = statistics.median(gen_leg["times"])
             groof = roofline(gen_leg)

@@ -100,6 +100,13 @@ extern "C" {
                                        on the fly                                      */
 #define PGMG_FLAG_NO_R2 1024u       /* F-cycle: one full-weighting level per restriction
                                        pass instead of two                             */
+#define PGMG_FLAG_FAST 4096u    /* FAST mode: the finest
+                                   level's cross-cycle pass shares each iterate's neighbour
+                                   sum between its Jacobi sweep and its residual and forms
+                                   the residuals with FMA — not the reference's expression
+                                   order, so phi agrees with the EXACT default within
+                                   1e-12 relative (after <= 10 cycles) instead of bitwise.
+                                   One GPU (row strips ignore it); everything else exact */
 #define PGMG_FLAG_HOST_TRANSPORT 2048u /* world > 1 without RCCL: nccl_unique_id points to
                                        a pgmg_host_transport; every message and reduction
                                        is staged through host memory and handed to the

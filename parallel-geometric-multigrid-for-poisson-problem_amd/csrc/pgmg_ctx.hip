@@ -580,6 +580,7 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         q.row_hi = sr.row_hi;
         q.rc_lo = sr.rc_lo;
         q.rc_hi = sr.rc_hi;
+        q.fast = (c->cfg.flags & PGMG_FLAG_FAST) != 0 && !dist;
         ev = timed_begin(c, 3);
         if ((e = launch_postpre(q, c->s))) return e;
         if ((e = timed_end(c, 3, ev))) return e;

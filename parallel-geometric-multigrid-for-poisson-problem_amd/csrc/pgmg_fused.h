@@ -84,6 +84,7 @@ struct PostPreArgsT {
     int row_lo, row_hi;
     int rc_lo, rc_hi;
     int rows_per_block;
+    int fast;                   // PGMG_FLAG_FAST (one GPU, f regenerated or stored)
 };
 
 struct FixArgsF {

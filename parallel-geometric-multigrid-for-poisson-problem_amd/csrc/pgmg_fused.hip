@@ -675,6 +675,36 @@ __device__ __forceinline__ V2<T> jsh(V2<T> up, V2<T> ce, V2<T> dn, Nbr<T> n, V2<
     }
     return o;
 }
+// FAST mode (OPT & 16): the neighbour sum of a centre row, S = (l + r) + (u + d), shared by
+// its Jacobi stage, 0.25 * (hh*f + S), and its residual, f - ih * (4x - S) as two FMAs
+template <class T>
+__device__ __forceinline__ V2<T> nsum(V2<T> up, V2<T> ce, V2<T> dn, Nbr<T> n)
+{
+    V2<T> sm;
+    sm.x = (n.l + ce.y) + (up.x + dn.x);
+    sm.y = (ce.x + n.r) + (up.y + dn.y);
+    return sm;
+}
+template <class T, bool EDGE>
+__device__ __forceinline__ V2<T> jsum(V2<T> sm, V2<T> ce, V2<T> hf, const Cols &k, bool brow)
+{
+    V2<T> o;
+    o.x = T(0.25) * (hf.x + sm.x);
+    o.y = T(0.25) * (hf.y + sm.y);
+    if constexpr (EDGE) {
+        if (brow || k.bx) o.x = ce.x;
+        if (brow || k.by) o.y = ce.y;
+    }
+    return o;
+}
+template <class T>
+__device__ __forceinline__ V2<T> rsum(V2<T> sm, V2<T> ce, V2<T> f, T ih)
+{
+    V2<T> o;
+    o.x = __builtin_fma(-ih, __builtin_fma(T(4), ce.x, -sm.x), f.x);
+    o.y = __builtin_fma(-ih, __builtin_fma(T(4), ce.y, -sm.y), f.y);
+    return o;
+}
 template <class T>
 __device__ __forceinline__ V2<T> rsn(V2<T> up, V2<T> ce, V2<T> dn, Nbr<T> n, V2<T> f, T ih)
 {
@@ -930,11 +960,16 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
             const V2<T> fq2 = f2, fq3 = f3, fq4 = f4, fq5 = f5;
             const V2<T> hq1 = q1, hq2 = q2, hq3 = q3, hq4 = q4;
             const V2<T> e2 = (OPT & 64) ? xr : add_prolong<T, EDGE>(xr, ii, cr0, crn0, cr1, crn1, pc, Nc);
+            constexpr bool FAST = (OPT & 16) != 0;
             // post-smooth sweep 1: x1 row ii-1
-            const V2<T> b2 = jsh<T, EDGE>(e0, e1, e2, nbr<T>(e1), hq1, k, boundary_row(ii - 1, N));
+            const V2<T> b2 = FAST ? jsum<T, EDGE>(nsum<T>(e0, e1, e2, nbr<T>(e1)), e1, hq1, k, boundary_row(ii - 1, N))
+                                  : jsh<T, EDGE>(e0, e1, e2, nbr<T>(e1), hq1, k, boundary_row(ii - 1, N));
             const Nbr<T> nb1 = nbr<T>(b1), nc1 = nbr<T>(c1), ng1 = nbr<T>(g1);
+            // FAST: the neighbour sums of x1 row ii-2 and x3 row ii-4, each shared by a sweep
+            // and a check
+            const V2<T> sb = FAST ? nsum<T>(b0, b1, b2, nb1) : z;
             {   // post check: r(x1) on row ii-2
-                const V2<T> r1 = rsn<T>(b0, b1, b2, nb1, fq2, ih);
+                const V2<T> r1 = FAST ? rsum<T>(sb, b1, fq2, ih) : rsn<T>(b0, b1, b2, nb1, fq2, ih);
                 const int row = ii - 2;
                 if (row >= olo && row < ohi && k.own) {
                     acc1 = sqacc(acc1, r1.x);
@@ -942,7 +977,8 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                 }
             }
             // post-smooth sweep 2: x2 row ii-2 (= phi of cycle k+1)
-            const V2<T> c2 = jsh<T, EDGE>(b0, b1, b2, nb1, hq2, k, boundary_row(ii - 2, N));
+            const V2<T> c2 = FAST ? jsum<T, EDGE>(sb, b1, hq2, k, boundary_row(ii - 2, N))
+                                  : jsh<T, EDGE>(b0, b1, b2, nb1, hq2, k, boundary_row(ii - 2, N));
             if (R2) {   // r(x2) on row ii-3
                 const V2<T> r2 = rsn<T>(c0, c1, c2, nc1, fq3, ih);
                 const int row = ii - 3;
@@ -952,9 +988,11 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                 }
             }
             // pre-smooth sweep 1: x3 row ii-3
-            const V2<T> g2 = jsh<T, EDGE>(c0, c1, c2, nc1, hq3, k, boundary_row(ii - 3, N));
+            const V2<T> g2 = FAST ? jsum<T, EDGE>(nsum<T>(c0, c1, c2, nc1), c1, hq3, k, boundary_row(ii - 3, N))
+                                  : jsh<T, EDGE>(c0, c1, c2, nc1, hq3, k, boundary_row(ii - 3, N));
+            const V2<T> sgg = FAST ? nsum<T>(g0, g1, g2, ng1) : z;
             {   // pre check: r(x3) on row ii-4
-                const V2<T> r3 = rsn<T>(g0, g1, g2, ng1, fq4, ih);
+                const V2<T> r3 = FAST ? rsum<T>(sgg, g1, fq4, ih) : rsn<T>(g0, g1, g2, ng1, fq4, ih);
                 const int row = ii - 4;
                 if (row >= olo && row < ohi && k.own) {
                     acc2 = sqacc(acc2, r3.x);
@@ -962,14 +1000,16 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                 }
             }
             // pre-smooth sweep 2: x4 row ii-4 (stored)
-            const V2<T> h2 = jsh<T, EDGE>(g0, g1, g2, ng1, hq4, k, boundary_row(ii - 4, N));
+            const V2<T> h2 = FAST ? jsum<T, EDGE>(sgg, g1, hq4, k, boundary_row(ii - 4, N))
+                                  : jsh<T, EDGE>(g0, g1, g2, ng1, hq4, k, boundary_row(ii - 4, N));
             // branch-free: rows outside the band get a zero-record descriptor, lanes that do
             // not own their pair an out-of-range offset (every step issues the same memory
             // instructions, so the compiler can count its waits)
             buf_store_row<T, (OPT & 2) ? 1 : 0>(a.x4 + (long long)(ii - 4) * P + L0,
                                                (ii - 4 >= olo && ii - 4 < ohi) ? xbytes : 0, xoff, h2);
             // r(x4) on row ii-5
-            const V2<T> d2 = rsn<T>(h0, h1, h2, nbr<T>(h1), fq5, ih);
+            const V2<T> d2 = FAST ? rsum<T>(nsum<T>(h0, h1, h2, nbr<T>(h1)), h1, fq5, ih)
+                                  : rsn<T>(h0, h1, h2, nbr<T>(h1), fq5, ih);
             // restriction: rows ii-7, ii-6, ii-5 = 2jc-1, 2jc, 2jc+1 when ii is even
             if (!(OPT & 64) && (s & 1) == 0) {
                 const int jc = (ii - 6) >> 1;
@@ -1375,7 +1415,10 @@ int launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
         if (genf) k_postpre_lds<T, true, true, 2><<<g, b, 0, s>>>(a);
         else k_postpre_lds<T, true, false, 2><<<g, b, 0, s>>>(a);
     } else {
-        if (genf) k_postpre_lds<T, false, true, 2><<<g, b, 0, s>>>(a);
+        if (a.fast && sizeof(T) == 8) {   // FAST mode (one GPU, fp64)
+            if (genf) k_postpre_lds<T, false, true, 2 | 16><<<g, b, 0, s>>>(a);
+            else k_postpre_lds<T, false, false, 2 | 16><<<g, b, 0, s>>>(a);
+        } else if (genf) k_postpre_lds<T, false, true, 2><<<g, b, 0, s>>>(a);
         else k_postpre_lds<T, false, false, 2><<<g, b, 0, s>>>(a);
     }
     return PGMG_OK;
