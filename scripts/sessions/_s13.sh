@@ -4,4 +4,4 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fc
 PGMG_LIB=$PWD/parallel-geometric-multigrid-for-poisson-problem_amd/libpgmg_ab.so timeout -k 10 200 python scripts/tail_prof.py 4097 > gpurun_out/tail_prof3.jsonl 2>&1 || exit 1; head -2 gpurun_out/tail_prof3.jsonl
 for L in libpgmg_base.so libpgmg.so libpgmg_base.so libpgmg.so; do PGMG_LIB=$PWD/parallel-geometric-multigrid-for-poisson-problem_amd/$L timeout -k 10 200 python bench.py --cycle W --n 4097 --steps 3 --warmup 1 --cpu-baseline off --general-rhs off --pmc off > gpurun_out/bw.log 2>&1 || exit 1; python3 -c "
 import json; d=json.loads(open('gpurun_out/bw.log').read().strip().splitlines()[-1]); print('$L', d['value'], d['ms_per_step'])"; done
-bash scripts/_s12.sh
+bash scripts/sessions/_s12.sh
