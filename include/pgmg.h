@@ -107,6 +107,11 @@ extern "C" {
                                    order, so phi agrees with the EXACT default within
                                    1e-12 relative (after <= 10 cycles) instead of bitwise.
                                    One GPU (row strips ignore it); everything else exact */
+#define PGMG_FLAG_L1POST 8192u  /* one GPU, speculative V-cycles: level 1's post-smooth of
+                                   cycle k runs inside the finest level's cross-cycle pass
+                                   (k_postpre) instead of its own pass; level 1's solution
+                                   is then never written.  Bitwise the same results;
+                                   measured slower at 16385: opt-in only */
 #define PGMG_FLAG_HOST_TRANSPORT 2048u /* world > 1 without RCCL: nccl_unique_id points to
                                        a pgmg_host_transport; every message and reduction
                                        is staged through host memory and handed to the

@@ -35,6 +35,7 @@ PGMG_FLAG_NO_PIN = 512
 PGMG_FLAG_NO_R2 = 1024
 PGMG_FLAG_HOST_TRANSPORT = 2048
 PGMG_FLAG_FAST = 4096
+PGMG_FLAG_L1POST = 8192
 
 PGMG_PRECISION_FP64 = 0
 PGMG_PRECISION_FP32 = 1

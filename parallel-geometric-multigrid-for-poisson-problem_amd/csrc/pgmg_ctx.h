@@ -83,6 +83,11 @@ struct pgmg_ctx {
     bool cross = false;           // finest level fuses post(k) with pre(k+1) across cycles
     bool recompute = true;        // levels entered with x0 = 0 recompute x2 in k_post
     pgmg::Grid S;                 // finest-level scratch for k_postpre's rare paths
+    // PGMG_FLAG_L1POST: level 1's second RHS buffer (k_postpre reads f1 of cycle k from
+    // one while it restricts cycle k+1's into the other; swapped with lv[1].F) and the
+    // mark that the level-1 visit being enqueued leaves its post-smooth to k_postpre
+    pgmg::Grid F1alt;
+    bool skip_l1_post = false;
     double *partials2 = nullptr;  // second partials buffer (k_postpre's pre check)
     double *partials3 = nullptr;  // third (row strips: k_postpre's pre check from x1)
     // analytic RHS (set_problem with f = NULL): level-0 passes may regenerate f in-kernel

@@ -372,6 +372,10 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
         if ((e = launch_pre_rare(fa, pa, x0_zero, c->s))) return e;
     }
     if ((e = enqueue_children<T>(c, l, gamma))) return e;
+    if (l == 1 && c->skip_l1_post) {   // the finest level's k_postpre runs it (L1POST)
+        c->skip_l1_post = false;
+        return PGMG_OK;
+    }
     // the correction of level l+1 is not exchanged: a distributed child's k_post computed
     // it kPostExt rows past its strip (a gathered child's is replicated)
     if (dist && !recomp && (e = c->comm->halo(L.B, L, ext ? 2 + kPostExt : 2, c->s))) return e;
@@ -534,6 +538,13 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
     fa.eps = c->cfg.eps;
     fa.stats = c->stats;
     int e;
+    // PGMG_FLAG_L1POST: level 1's post-smooth of cycle k inside k_postpre (speculative
+    // V-cycles on one GPU, level 1 a bulk level entered with x0 = 0 whose checks are not
+    // decided in-stream); its RHS alternates between lv[1].F and F1alt
+    const bool l1post = lean && (c->cfg.flags & PGMG_FLAG_L1POST) && !dist && c->comm == nullptr &&
+                        gamma == 1 && c->nb > 1 && c->recompute && !c->lvl_exact[1] &&
+                        !(c->cfg.flags & PGMG_FLAG_FAST);
+    if (l1post && !c->F1alt.base && (e = alloc_grid(c->F1alt, C))) return e;
     // cycle 1: pre-smooth (+ residual, restriction) A -> B
     if (dist && (e = c->comm->halo(gA, L, 4, c->s))) return e;
     PreArgsT<T> pa = make_pre<T>(c, A, B);
@@ -552,6 +563,7 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
     // after the whole coarse hierarchy: the exchange runs on the comm's side stream
     // meanwhile (the coarse correction's halo rows are computed locally, kPostExt)
     if (dist && (e = c->comm->halo_begin(*grid_of(pr), L, 6, c->s))) return e;
+    c->skip_l1_post = l1post && n > 1;
     if ((e = enqueue_children<T>(c, 0, gamma))) return e;
     for (int k = 1; k < n; ++k) {
         T *nx = next_of(pr);
@@ -562,6 +574,17 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         q.f = G<T>(L.F);
         q.x4 = nx;
         q.rc = G<T>(C.F);
+        if (l1post) {   // level 1's post check first: the log keeps each level's order
+            const Level &CC = c->lv[2];
+            q.f1 = G<T>(C.F);
+            q.rc = G<T>(c->F1alt);
+            q.e2 = G<T>(CC.A);
+            q.N2 = CC.N;
+            q.P2 = CC.P;
+            q.hh1 = (T)C.hh;
+            q.ih1 = (T)C.ih;
+            q.partials4 = chk_partials(c, npp, 1);
+        }
         q.partials1 = lean ? chk_partials(c, npp, 0) : c->partials;
         q.partials2 = lean ? chk_partials(c, npp, 0) : c->partials2;
         q.partials3 = (dist && !lean) ? c->partials3 : nullptr;   // lean: no rare path runs
@@ -584,10 +607,12 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         ev = timed_begin(c, 3);
         if ((e = launch_postpre(q, c->s))) return e;
         if ((e = timed_end(c, 3, ev))) return e;
+        if (l1post) std::swap(C.F, c->F1alt);   // cycle k+1's level-1 RHS
         const double *g3 = nullptr;   // all-rank {post, pre, pre-from-x1} sums
         if (lean) {
             pr = nx;
             if (dist && (e = c->comm->halo_begin(*grid_of(pr), L, 6, c->s))) return e;
+            c->skip_l1_post = l1post && k + 1 < n;
             if ((e = enqueue_children<T>(c, 0, gamma))) return e;
             continue;
         }
@@ -785,6 +810,7 @@ int pgmg_destroy(pgmg_ctx *c)
     free_grid(c->bk);
     if (c->ppflags) (void)hipFree(c->ppflags);
     free_grid(c->S);
+    free_grid(c->F1alt);
     free_grid(c->Ffmg);
     for (auto &g : c->Ffmg_l) free_grid(g);
     if (c->fmg_tab) (void)hipFree(c->fmg_tab);
@@ -1235,7 +1261,8 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
     const int npp = c->cross ? postpre_blocks(L0.N, L0.lo / 2, (L0.hi < L0.N ? L0.hi : L0.N - 1) / 2) : 0;
     long long d1, k1;
     spec_need_level(c, 1, gamma, &d1, &k1);
-    const long long per_dbl = 2LL * std::max(np0, npp) + d1, per_chk = 2 + k1;
+    // (+ npp: L1POST logs level 1's post check with k_postpre's block count)
+    const long long per_dbl = 2LL * std::max(np0, npp) + d1 + npp, per_chk = 2 + k1;
     // segments of at most 2^27 logged doubles (1 GiB) / 2^22 checks
     long long seg_max = std::min(((1LL << 27) - 2LL * np0) / per_dbl, ((1LL << 22) - 2) / per_chk);
     if (c->cfg.spec_segment > 0) seg_max = std::min<long long>(seg_max, c->cfg.spec_segment);

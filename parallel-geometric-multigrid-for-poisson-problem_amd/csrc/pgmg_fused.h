@@ -85,6 +85,15 @@ struct PostPreArgsT {
     int rc_lo, rc_hi;
     int rows_per_block;
     int fast;                   // PGMG_FLAG_FAST (one GPU, f regenerated or stored)
+    // non-null (PGMG_FLAG_L1POST, one GPU): level 1's post-smooth of cycle k runs inside
+    // this pass instead of its own k_post: ec is not read but computed per block from
+    // f1 (level 1's RHS of cycle k; rc above must then be another buffer) and e2 (level
+    // 2's corrected solution); sum r(x1)^2 of level 1 into partials4
+    const T *f1;
+    const T *e2;
+    double *partials4;
+    int N2, P2;
+    T hh1, ih1;
 };
 
 struct FixArgsF {

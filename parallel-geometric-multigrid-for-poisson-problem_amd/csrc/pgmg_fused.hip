@@ -760,7 +760,7 @@ template <class T, bool R2, bool GENF, int OPT>
 constexpr int pp_depth()
 {
     if constexpr (PGMG_PP_DEPTH != 0) return PGMG_PP_DEPTH;
-    return (sizeof(T) == 4 || (GENF && !R2 && !(OPT & 64))) ? 3 : 2;
+    return (sizeof(T) == 4 || (GENF && !R2 && !(OPT & (64 | 32)))) ? 3 : 2;
 }
 #ifndef PGMG_PP_NTL
 #define PGMG_PP_NTL 0     // 1: non-temporal row loads (measurement builds)
@@ -815,14 +815,34 @@ __device__ __forceinline__ T buf_one(const T *base, int n, int t)
         return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, t * 4, 0, 0));
 }
 
+// OPT & 32 (PGMG_FLAG_L1POST): level 1's post-smooth of cycle k inside the pass.  The
+// block's 256 lanes own one level-1 column each, c1 = cc0 - 3 + t (the coarse window plus
+// 3 columns each side: x_eff, x1, x2 each lose one), and per row pair compute one row of
+// each stage, lagging 2 rows apart (x_eff row m0+g+6, x1 m0+g+4, x2 m0+g+2), as k_post
+// RECOMP does with the pre check not fired (the speculative call's assumption, verified
+// after the call): x_pre = J(J(0)) from f1, x_eff = x_pre + P e2, x1 = J(x_eff), x2 = J(x1)
+// with r(x1) summed.  x2 goes straight into the coarse ring se the level-0 prolongation
+// reads, so level 1's solution is never written and never read back (18 B per level-1
+// point of its k_post, against 2.5 B per level-1 point here: f1 and e2).
+constexpr int kL1Row = 64 * kPPWaves + 2;    // lane t at [t + 1]
+constexpr int kL1E = 32 * kPPWaves + 8;      // level-2 column ((cc0 - 3) >> 1) + t at [t]
+template <class T> struct L1Lds {
+    T f[8][kL1Row];   // f1 rows (ring 8: rows g+2 .. g+7 read, g+8 stored per step)
+    T x[4][kL1Row];   // x_eff rows
+    T y[4][kL1Row];   // x1 rows
+    T e[8][kL1E];     // e2 rows
+};
+
 // The body of k_postpre_lds for one block.  EDGE = false: no row of the block's band and
 // no column of this wave is a boundary, so the Jacobi stages carry no passthrough selects.
 template <class T, bool R2, bool GENF, bool EDGE, int OPT>
 __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const Cols &k,
                                                 double *red, T (&sx)[2][kPPR][kPPLdsRow],
                                                 T (&sf)[2][kPPR][GENF ? 1 : kPPLdsRow],
-                                                T (&se)[3][kPPLdsCoarse], const Blk bk)
+                                                T (&se)[3][kPPLdsCoarse], L1Lds<T> *l1,
+                                                const Blk bk)
 {
+    constexpr bool L1 = (OPT & 32) != 0;
     constexpr int R = kPPR;
     const int N = a.N, Nc = a.Nc;
     const long long P = a.P, Pc = a.Pc;
@@ -831,7 +851,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     const int olo = max(2 * jcb, a.row_lo), ohi = min(2 * jce, a.row_hi);
     const int clo = max(jcb, max(1, a.rc_lo)), chi = min(jce, min(N / 2, a.rc_hi));
     if (bk.x == 0 && bk.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
-        atomicAdd(&a.stats[0], 4ull);
+        atomicAdd(&a.stats[0], L1 ? 6ull : 4ull);
     ProlongCols pc;
     pc.ic = (k.c - 1) >> 1;
     pc.vx = k.c >= 3 && k.c <= N - 2;
@@ -854,7 +874,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     // the row pairs prefetched for later steps.
     // lanes that load (columns >= N never matter)
     const int nvx = max(0, min(npairs, (N - 1 - L0) / 2 + 1));
-    const int nve = (OPT & 64) ? 0 : max(0, min(ncc, Nc - cc0));
+    const int nve = (OPT & (64 | 32)) ? 0 : max(0, min(ncc, Nc - cc0));
     // stores: x4 row segment of the block window (lanes that own their pair), rc (lanes
     // owning a coarse column <= Nc-2); anything else gets an out-of-range offset
     constexpr int kOOB = 1 << 30;
@@ -892,18 +912,44 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     constexpr int D = pp_depth<T, R2, GENF, OPT>();
     static_assert(D == 2 || D == 3, "PGMG_PP_DEPTH is 2 or 3");
     V2<T> pxA[R], pfA[R], pxB[R], pfB[R], pxC[R], pfC[R];   // C unused (dead) when D = 2
-    T peA = T(0), peB = T(0), peC = T(0);
-    auto load_pair = [&](int p, V2<T> (&px)[R], V2<T> (&pf)[R], T &pe) {
+    // L1: a register T carries two values, lane t's f1 (low) and e2 (high) of the pair --
+    // kept as V2 sets with the coarse row's slot otherwise
+    V2<T> peA = z, peB = z, peC = z;
+    // L1 geometry: lane t = level-1 column lc (see L1Lds)
+    const int N1 = Nc;
+    const int lc = cc0 - 3 + t;
+    const bool cin = lc >= 1 && lc <= N1 - 2, cinl = lc >= 2 && lc <= N1 - 1,
+               cinr = lc >= 0 && lc <= N1 - 3, ccor = lc >= 2 && lc <= N1 - 2;
+    const int n0 = (cc0 - 3) >> 1;
+    const int ne = (lc >> 1) - n0;                       // 0 .. 128
+    // the check's columns: level-1 columns (c+1)/2 of the block's owned odd fine columns c
+    const bool own1 = t >= 7 && t < 7 + (kPPStride / 2) * wpb && lc <= N1 - 2;
+    const int fcol = min(max(lc, 0), N1 - 1), ecol = min(max(n0 + t, 0), a.N2 - 1);
+    auto l1_f = [&](int r) -> T {   // f1[r][lc] (clamped; masked where it matters)
+        return buf_one<T>(a.f1 + (long long)min(max(r, 0), N1 - 1) * Pc, N1, fcol);
+    };
+    auto l1_e = [&](int m) -> T {   // e2[m][n0 + t]
+        return buf_one<T>(a.e2 + (long long)min(max(m, 0), a.N2 - 1) * a.P2, a.N2, ecol);
+    };
+    // pair p carries f1 row m0 + p + 7 and e2 row (m0 + p + 8) >> 1 (stored one step ahead)
+    auto l1_store = [&](int r, V2<T> v) {
+        l1->f[r & 7][t + 1] = v.x;
+        if (t < kL1E) l1->e[((r + 1) >> 1) & 7][t] = v.y;
+    };
+    auto load_pair = [&](int p, V2<T> (&px)[R], V2<T> (&pf)[R], V2<T> &pe) {
         #pragma unroll
         for (int q = 0; q < R; ++q) {
             const long long row = (long long)(i_begin + p * R + q) * P + L0;
             px[q] = buf_row<T, PGMG_PP_NTL>(a.phi + row, nvx, t);
             if constexpr (!GENF) pf[q] = buf_row<T, PGMG_PP_NTL>(a.f + row, nvx, t);
         }
-        // the pair's second coarse row
-        pe = buf_one<T>(a.ec + (long long)(m0 + p + 1) * Pc + cc0, nve, t);
+        if constexpr (L1) {
+            if (p >= 1) pe = mk2<T>(l1_f(m0 + p + 7), l1_e((m0 + p + 8) >> 1));
+        } else {   // the pair's second coarse row
+            pe.x = buf_one<T>(a.ec + (long long)(m0 + p + 1) * Pc + cc0, nve, t);
+        }
     };
-    auto store_pair = [&](int p, const V2<T> (&px)[R], const V2<T> (&pf)[R], T pe) {
+    auto store_pair = [&](int p, const V2<T> (&px)[R], const V2<T> (&pf)[R], V2<T> pe) {
         if (t < npairs) {
             #pragma unroll
             for (int q = 0; q < R; ++q) {
@@ -911,11 +957,83 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                 if constexpr (!GENF) *reinterpret_cast<V2<T> *>(&sf[p & 1][q][2 * t]) = pf[q];
             }
         }
-        if (t < ncc) se[ring(m0 + p + 1)][t] = pe;
+        if constexpr (L1) {
+            if (p >= 1) l1_store(m0 + p + 7, pe);
+        } else {
+            if (t < ncc) se[ring(m0 + p + 1)][t] = pe.x;
+        }
     };
+    // L1: one row of each level-1 stage per step g (virtual steps g < 0 fill the pipeline)
+    double acc4 = 0.0;
+    const T hh1 = a.hh1, ih1 = a.ih1;
+    auto l1_stage = [&](int g, bool chk) {
+        {   // x_eff row re
+            const int re = m0 + g + 6;
+            const T *Fm = l1->f[(re - 1) & 7] + 1, *F0 = l1->f[re & 7] + 1, *Fp = l1->f[(re + 1) & 7] + 1;
+            const bool bre = re <= 0 || re >= N1 - 1;
+            const bool bm = re - 1 <= 0 || re - 1 >= N1 - 1, bp = re + 1 <= 0 || re + 1 >= N1 - 1;
+            // J(0) at the four neighbours: 0.25 * ((hh*f) + 0), 0 on the frame (j0stage)
+            auto j0 = [&](T f, bool b) { return b ? T(0) : T(0.25) * ((hh1 * f) + T(0)); };
+            const T jl = j0(F0[t - 1], bre || !cinl), jr = j0(F0[t + 1], bre || !cinr);
+            const T ju = j0(Fm[t], bm || !cin), jd = j0(Fp[t], bp || !cin);
+            T v = T(0.25) * ((hh1 * F0[t]) + jl + jr + ju + jd);
+            if (bre || !cin) v = T(0);
+            if (ccor && re >= 2 && re <= N1 - 2) {   // + P e2 (add_prolong, one column)
+                const int mm = re >> 1;
+                const T *C0 = l1->e[mm & 7], *C1 = l1->e[(mm + 1) & 7];
+                const T ca = C0[ne];
+                if ((re & 1) == 0) {
+                    v = (lc & 1) == 0 ? v + ca : v + T(0.5) * (ca + C0[ne + 1]);
+                } else {
+                    const T da = C1[ne];
+                    v = (lc & 1) == 0 ? v + T(0.5) * (ca + da)
+                                      : v + T(0.25) * (ca + C0[ne + 1] + da + C1[ne + 1]);
+                }
+            }
+            l1->x[re & 3][t + 1] = v;
+        }
+        {   // x1 row r = J(x_eff)
+            const int r = m0 + g + 4;
+            const T *Xm = l1->x[(r - 1) & 3] + 1, *X0 = l1->x[r & 3] + 1, *Xp = l1->x[(r + 1) & 3] + 1;
+            const T xc = X0[t];
+            T v = T(0.25) * ((hh1 * l1->f[r & 7][t + 1]) + X0[t - 1] + X0[t + 1] + Xm[t] + Xp[t]);
+            if (r <= 0 || r >= N1 - 1 || !cin) v = xc;
+            l1->y[r & 3][t + 1] = v;
+        }
+        {   // x2 row r = J(x1) -> the coarse ring; r(x1) on row r
+            const int r = m0 + g + 2;
+            const T *Ym = l1->y[(r - 1) & 3] + 1, *Y0 = l1->y[r & 3] + 1, *Yp = l1->y[(r + 1) & 3] + 1;
+            const T fc = l1->f[r & 7][t + 1];
+            const T yc = Y0[t], yl = Y0[t - 1], yr = Y0[t + 1], yu = Ym[t], yd = Yp[t];
+            T v = T(0.25) * ((hh1 * fc) + yl + yr + yu + yd);
+            if (r <= 0 || r >= N1 - 1 || !cin) v = yc;
+            if (t >= 3 && t < 3 + ncc) se[ring(r)][t - 3] = v;
+            if (chk) {
+                const T rs = fc - ih1 * (T(4) * yc - yl - yr - yu - yd);
+                if (own1 && r >= jcb && r < jce && r >= 1) acc4 = sqacc(acc4, rs);
+            }
+        }
+    };
+    V2<T> vq[3];   // L1: the pairs of the virtual steps -3 .. -1 (f1 rows m0+5 .. m0+7)
+    if constexpr (L1) {
+        // f1 rows m0-3 .. m0+4 and e2 rows of x_eff rows m0-2 .. m0+5 straight into LDS
+        T pf[8], pg[6];
+        #pragma unroll
+        for (int q = 0; q < 8; ++q) pf[q] = l1_f(m0 - 3 + q);
+        #pragma unroll
+        for (int q = 0; q < 6; ++q) pg[q] = l1_e(((m0 - 2) >> 1) + q);
+        #pragma unroll
+        for (int q = 0; q < 3; ++q) vq[q] = mk2<T>(l1_f(m0 + 5 + q), l1_e((m0 + 6 + q) >> 1));
+        #pragma unroll
+        for (int q = 0; q < 8; ++q) l1->f[(m0 - 3 + q) & 7][t + 1] = pf[q];
+        if (t < kL1E) {
+            #pragma unroll
+            for (int q = 0; q < 6; ++q) l1->e[(((m0 - 2) >> 1) + q) & 7][t] = pg[q];
+        }
+    }
     // prologue: pair 0 (+ its first coarse row) into slot 0; pairs 1 .. D in flight
     load_pair(0, pxA, pfA, peA);
-    if (t < ncc) se[ring(m0)][t] = buf_one<T>(a.ec + (long long)m0 * Pc + cc0, nve, t);
+    if (!L1 && t < ncc) se[ring(m0)][t] = buf_one<T>(a.ec + (long long)m0 * Pc + cc0, nve, t);
     store_pair(0, pxA, pfA, peA);
     if (ng > 1) load_pair(1, pxB, pfB, peB);
     if constexpr (D == 3) {
@@ -925,11 +1043,19 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
         if (ng > 2) load_pair(2, pxA, pfA, peA);
     }
     __syncthreads();
+    if constexpr (L1) {   // virtual steps: x_eff rows m0-2 .., x1 rows m0-1 .., x2 rows m0, m0+1
+        #pragma unroll
+        for (int g = -8; g < 0; ++g) {
+            if (g >= -3) l1_store(m0 + g + 8, vq[g + 3]);   // pairs -2 .. 0
+            l1_stage(g, false);
+            __syncthreads();
+        }
+    }
 
     // pair gi: compute from slot gi & 1; pair gi+1 (set (gi+1) & 1) -> the other slot;
     // issue pair gi+3 into the set just freed; one barrier
     T wprev = T(0);   // dpp_shl(d2.x) of the previous restriction row (d0 starts as zero)
-    auto step = [&](int gi, V2<T> (&px)[R], V2<T> (&pf)[R], T &pe) {
+    auto step = [&](int gi, V2<T> (&px)[R], V2<T> (&pf)[R], V2<T> &pe) {
         // keep the scheduler inside one pair: interleaving the unrolled pairs only raises
         // the register pressure (the loads of a pair are issued two pairs ahead anyway)
         __builtin_amdgcn_sched_barrier(0);
@@ -939,6 +1065,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
         // flight are never younger than this step's stores (counted waits stay small)
         if (gi + 1 < ng) store_pair(gi + 1, px, pf, pe);
         if (gi + 1 + D < ng) load_pair(gi + 1 + D, px, pf, pe);
+        if constexpr (L1) l1_stage(gi, true);
         const int i = i_begin + gi * R;
         const int m = m0 + gi;
         const T *E0 = se[ring(m)], *E1 = se[ring(m + 1)];
@@ -1060,6 +1187,11 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
         const double s3 = fused_block_sum(acc3, red);
         if (threadIdx.x == 0) a.partials3[slot] = s3;
     }
+    if constexpr (L1) {
+        __syncthreads();
+        const double s4 = fused_block_sum(acc4, red);
+        if (threadIdx.x == 0) a.partials4[slot] = s4;
+    }
     if (threadIdx.x == 0) {
         a.partials1[slot] = s1;
         a.partials2[slot] = s2;
@@ -1078,6 +1210,9 @@ void k_postpre_lds(PostPreArgsT<T> a)
     __shared__ __attribute__((aligned(16))) T sx[2][kPPR][kPPLdsRow];
     __shared__ __attribute__((aligned(16))) T sf[2][kPPR][GENF ? 1 : kPPLdsRow];
     __shared__ __attribute__((aligned(16))) T se[3][kPPLdsCoarse];
+    __shared__ __attribute__((aligned(16))) std::conditional_t<(OPT & 32) != 0, L1Lds<T>, char> l1s;
+    L1Lds<T> *l1 = nullptr;
+    if constexpr ((OPT & 32) != 0) l1 = &l1s;
     const Blk bk{(int)blockIdx.x, (int)blockIdx.y};
     const Cols k = lane_cols_t<kPPStride, kPPMargin>(a.N, bk.x);
     // the band's rows 2jcb-6 .. 2jce+5 (see postpre_lds_run): does it reach row 0 or N-1?
@@ -1085,9 +1220,9 @@ void k_postpre_lds(PostPreArgsT<T> a)
     const int jce = min(jcb + a.rows_per_block, a.jc1);
     const bool edge_rows = 2 * jcb - 6 <= 0 || 2 * jce + 6 >= a.N - 1;
     if (k.edge || edge_rows)
-        postpre_lds_run<T, R2, GENF, true, OPT>(a, k, red, sx, sf, se, bk);
+        postpre_lds_run<T, R2, GENF, true, OPT>(a, k, red, sx, sf, se, l1, bk);
     else
-        postpre_lds_run<T, R2, GENF, false, OPT>(a, k, red, sx, sf, se, bk);
+        postpre_lds_run<T, R2, GENF, false, OPT>(a, k, red, sx, sf, se, l1, bk);
 }
 
 // one block: both decisions, stats, flags for the conditional rare-path kernels
@@ -1307,7 +1442,8 @@ static int postpre_spans(const PostPreArgsT<T> &a, int t, int gx, int r, bool co
     if (c1 < c0) return PGMG_OK;
     PGMG_SPAN(a.phi, a.P, sp.r0, sp.r1, c0, c1, "k_postpre phi");
     if (a.gfx == nullptr) PGMG_SPAN(a.f, a.P, sp.r0, sp.r1, c0, c1, "k_postpre f");
-    if (coarse && e1 >= e0)   // coarse rows m0 .. m0 + ng of a band (m0 = jcb - 3)
+    // (L1: f1 and e2 are read at clamped rows and columns, ec not at all)
+    if (coarse && e1 >= e0 && a.f1 == nullptr)   // coarse rows m0 .. m0 + ng of a band (m0 = jcb - 3)
         PGMG_SPAN(a.ec, a.Pc, a.jc0 - 3, fdiv2(sp.r1 + 1), e0, e1, "k_postpre coarse correction");
     const int olo = std::max(2 * a.jc0, a.row_lo), ohi = std::min(2 * a.jc1, a.row_hi);
     PGMG_SPAN(a.x4, a.P, olo, ohi - 1, 1, a.N - 1, "k_postpre x4");
@@ -1414,6 +1550,9 @@ int launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
     if (a.partials3 != nullptr) {
         if (genf) k_postpre_lds<T, true, true, 2><<<g, b, 0, s>>>(a);
         else k_postpre_lds<T, true, false, 2><<<g, b, 0, s>>>(a);
+    } else if (a.f1 != nullptr) {   // level 1's post-smooth inside (PGMG_FLAG_L1POST)
+        if (genf) k_postpre_lds<T, false, true, 2 | 32><<<g, b, 0, s>>>(a);
+        else k_postpre_lds<T, false, false, 2 | 32><<<g, b, 0, s>>>(a);
     } else {
         if (a.fast && sizeof(T) == 8) {   // FAST mode (one GPU, fp64)
             if (genf) k_postpre_lds<T, false, true, 2 | 16><<<g, b, 0, s>>>(a);
