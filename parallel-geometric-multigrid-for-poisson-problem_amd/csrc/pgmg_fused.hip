@@ -824,6 +824,9 @@ __device__ __forceinline__ T buf_one(const T *base, int n, int t)
 // with r(x1) summed.  x2 goes straight into the coarse ring se the level-0 prolongation
 // reads, so level 1's solution is never written and never read back (18 B per level-1
 // point of its k_post, against 2.5 B per level-1 point here: f1 and e2).
+#ifndef PGMG_L1_EXP
+#define PGMG_L1_EXP 0   // A/B builds only (wrong results): 1 no frame masks, 2 no level-1 stages
+#endif
 constexpr int kL1Row = 64 * kPPWaves + 2;    // lane t at [t + 1]
 constexpr int kL1E = 32 * kPPWaves + 8;      // level-2 column ((cc0 - 3) >> 1) + t at [t]
 template <class T> struct L1Lds {
@@ -967,18 +970,23 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     double acc4 = 0.0;
     const T hh1 = a.hh1, ih1 = a.ih1;
     auto l1_stage = [&](int g, bool chk) {
+        if constexpr (PGMG_L1_EXP == 2) {   // keep the level-1 check from firing
+            acc4 = 1.0;
+            return;
+        }
+        constexpr bool MK = PGMG_L1_EXP != 1;
         {   // x_eff row re
             const int re = m0 + g + 6;
             const T *Fm = l1->f[(re - 1) & 7] + 1, *F0 = l1->f[re & 7] + 1, *Fp = l1->f[(re + 1) & 7] + 1;
             const bool bre = re <= 0 || re >= N1 - 1;
             const bool bm = re - 1 <= 0 || re - 1 >= N1 - 1, bp = re + 1 <= 0 || re + 1 >= N1 - 1;
             // J(0) at the four neighbours: 0.25 * ((hh*f) + 0), 0 on the frame (j0stage)
-            auto j0 = [&](T f, bool b) { return b ? T(0) : T(0.25) * ((hh1 * f) + T(0)); };
+            auto j0 = [&](T f, bool b) { return (MK && b) ? T(0) : T(0.25) * ((hh1 * f) + T(0)); };
             const T jl = j0(F0[t - 1], bre || !cinl), jr = j0(F0[t + 1], bre || !cinr);
             const T ju = j0(Fm[t], bm || !cin), jd = j0(Fp[t], bp || !cin);
             T v = T(0.25) * ((hh1 * F0[t]) + jl + jr + ju + jd);
-            if (bre || !cin) v = T(0);
-            if (ccor && re >= 2 && re <= N1 - 2) {   // + P e2 (add_prolong, one column)
+            if (MK && (bre || !cin)) v = T(0);
+            if (!MK || (ccor && re >= 2 && re <= N1 - 2)) {   // + P e2 (add_prolong, one column)
                 const int mm = re >> 1;
                 const T *C0 = l1->e[mm & 7], *C1 = l1->e[(mm + 1) & 7];
                 const T ca = C0[ne];
@@ -997,7 +1005,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
             const T *Xm = l1->x[(r - 1) & 3] + 1, *X0 = l1->x[r & 3] + 1, *Xp = l1->x[(r + 1) & 3] + 1;
             const T xc = X0[t];
             T v = T(0.25) * ((hh1 * l1->f[r & 7][t + 1]) + X0[t - 1] + X0[t + 1] + Xm[t] + Xp[t]);
-            if (r <= 0 || r >= N1 - 1 || !cin) v = xc;
+            if (MK && (r <= 0 || r >= N1 - 1 || !cin)) v = xc;
             l1->y[r & 3][t + 1] = v;
         }
         {   // x2 row r = J(x1) -> the coarse ring; r(x1) on row r
@@ -1006,7 +1014,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
             const T fc = l1->f[r & 7][t + 1];
             const T yc = Y0[t], yl = Y0[t - 1], yr = Y0[t + 1], yu = Ym[t], yd = Yp[t];
             T v = T(0.25) * ((hh1 * fc) + yl + yr + yu + yd);
-            if (r <= 0 || r >= N1 - 1 || !cin) v = yc;
+            if (MK && (r <= 0 || r >= N1 - 1 || !cin)) v = yc;
             if (t >= 3 && t < 3 + ncc) se[ring(r)][t - 3] = v;
             if (chk) {
                 const T rs = fc - ih1 * (T(4) * yc - yl - yr - yu - yd);
