@@ -244,10 +244,14 @@ __device__ __forceinline__ Cnt tail_smooth_small(Real *x, const Real *f, const T
 // smoother call with num_iter = 1 (2 sweeps) thus has one barrier for its check and one
 // after the write-back (tail_jacobi: two passes over the grid in LDS and a block sum per
 // sweep).  Expressions, operand order and the fused check are tail_smooth's.
+// R != nullptr (a pre-smooth followed by the residual and restriction): also R = r(x) of the
+// result on the interior, from the registers (the final iterate and its neighbour rows are
+// at hand: tail_res_restrict's expression and operand order), written after the closing
+// barrier -- R may be T, whose edge-row buffers are free by then; the caller syncs
 template <class Real, int NN>
 __device__ __forceinline__ Cnt tail_smooth_rows(Real *x, const Real *f, const TailLevel<Real> &L,
                                                 int num_iter, double eps, Real *T, double *red,
-                                                int &par)
+                                                int &par, Real *R = nullptr)
 {
     static_assert((NN - 1) % kTailWaves == 0, "waves must tile rows 1 .. NN-1");
     constexpr int RPW = (NN - 1) / kTailWaves;
@@ -358,6 +362,19 @@ __device__ __forceinline__ Cnt tail_smooth_rows(Real *x, const Real *f, const Ta
     for (int r = 0; r < RPW; ++r)
         if (act && !brow[r]) x[(j0 + r) * NN + lane] = nx[r];
     __syncthreads();
+    if (R != nullptr) {   // up / dn: the final iterate's neighbour rows (x_1's ghost rows,
+        #pragma unroll    // the last exchange, or the rows a firing check used)
+        for (int r = 0; r < RPW; ++r) {
+            const Real u = r == 0 ? up : nx[r - 1];
+            const Real d = r + 1 < RPW ? nx[r + 1] : dn;
+            const Real c = nx[r];
+            const Real lf = dpp_shr(c);
+            Real rt = dpp_shl(c);
+            if (NN == 65 && lane == 63) rt = xb[r];
+            const Real res = fr[r] - ih * (Real(4) * c - lf - rt - u - d);
+            if (act && !bcol && !brow[r]) R[(j0 + r) * NN + lane] = res;
+        }
+    }
     return Cnt{sweeps, exits};
 }
 
@@ -365,13 +382,15 @@ __device__ __forceinline__ Cnt tail_smooth_rows(Real *x, const Real *f, const Ta
 // soon as ||r(x_k)|| < eps, tested as sum r^2 < eps2 = norm2_threshold(eps) (no sqrt on
 // the dependent chain of every sweep; the same decisions, see pgmg_internal.h).  The check of x_k is fused into sweep k+1 (which
 // reads the same neighbourhood); when it fires, sweep k+1's output is dropped.
+// R: see tail_smooth_rows (only the block team's register levels, tail_rows_level)
 template <class Team, class Real>
 __device__ __forceinline__ Cnt tail_smooth(Real *x, const Real *f, const TailLevel<Real> &L,
-                                           int num_iter, double eps, Real *T, double *red, int &par)
+                                           int num_iter, double eps, Real *T, double *red, int &par,
+                                           Real *R = nullptr)
 {
     if constexpr (Team::size == kTailThreads && kTailRows) {
-        if (L.N == 65) return tail_smooth_rows<Real, 65>(x, f, L, num_iter, eps, T, red, par);
-        if (L.N == 33) return tail_smooth_rows<Real, 33>(x, f, L, num_iter, eps, T, red, par);
+        if (L.N == 65) return tail_smooth_rows<Real, 65>(x, f, L, num_iter, eps, T, red, par, R);
+        if (L.N == 33) return tail_smooth_rows<Real, 33>(x, f, L, num_iter, eps, T, red, par, R);
     }
     if constexpr (Team::size == 64) {
         const int nin = (L.N - 2) * (L.N - 2);
@@ -445,6 +464,31 @@ __device__ __forceinline__ Real pweight(const Real *C, const PGeo &g, int NC)
     return s * (((a + (g.mb ? b : nz)) + (g.mcd ? c : nz)) + (g.mcd ? d : nz));
 }
 
+// the levels tail_smooth smooths in registers with the block team
+template <class Team>
+__device__ __forceinline__ bool tail_rows_level(int N)
+{
+    return Team::size == kTailThreads && kTailRows && (N == 65 || N == 33);
+}
+
+// fc = R T, ec = 0 from a residual T already on the interior (MultiGrid.hpp:78-82)
+template <class Team, class Real>
+__device__ __forceinline__ void tail_restrict_T(const Real *T, const TailLevel<Real> &Lf, Real *fc, Real *ec,
+                                                const TailLevel<Real> &Lc)
+{
+    const int N = Lf.N, Nc = Lc.N, nc = Nc * Nc;
+    for (int q = Team::tid(); q < nc; q += Team::size) {
+        const int jc = tail_row(q, Lc.rN);
+        const int ic = q - jc * Nc;
+        ec[q] = Real(0);  // MultiGrid.hpp:81-82 e_coarse = 0
+        if (ic == 0 || jc == 0 || ic == Nc - 1 || jc == Nc - 1) continue;
+        const int k = (2 * jc) * N + 2 * ic;
+        fc[q] = Real(0.25) * T[k] + Real(0.125) * (T[k + 1] + T[k - 1] + T[k + N] + T[k - N]) +
+                Real(0.0625) * (T[k - N - 1] + T[k - N + 1] + T[k + N - 1] + T[k + N + 1]);
+    }
+    Team::sync();
+}
+
 // T = r(x) on the interior (its boundary is never read); then fc = R T (MultiGrid.hpp:70-78)
 template <class Team, class Real>
 __device__ __forceinline__ void tail_res_restrict(const Real *x, const Real *f, const TailLevel<Real> &Lf, Real *fc,
@@ -485,17 +529,7 @@ __device__ __forceinline__ void tail_res_restrict(const Real *x, const Real *f, 
         T[k] = f[k] - Lf.ih * (Real(4) * x[k] - x[k - 1] - x[k + 1] - x[k - N] - x[k + N]);
     }
     Team::sync();
-    const int Nc = Lc.N, nc = Nc * Nc;
-    for (int q = Team::tid(); q < nc; q += Team::size) {
-        const int jc = tail_row(q, Lc.rN);
-        const int ic = q - jc * Nc;
-        ec[q] = Real(0);  // MultiGrid.hpp:81-82 e_coarse = 0
-        if (ic == 0 || jc == 0 || ic == Nc - 1 || jc == Nc - 1) continue;
-        const int k = (2 * jc) * N + 2 * ic;
-        fc[q] = Real(0.25) * T[k] + Real(0.125) * (T[k + 1] + T[k - 1] + T[k + N] + T[k - N]) +
-                Real(0.0625) * (T[k - N - 1] + T[k - N + 1] + T[k + N - 1] + T[k + N + 1]);
-    }
-    Team::sync();
+    tail_restrict_T<Team>(T, Lf, fc, ec, Lc);
 }
 
 // x += P e (MultiGrid.hpp:208-226): fine points in [2, Nf-2]^2 only
@@ -1131,15 +1165,22 @@ __device__ __forceinline__ Cnt tail_gcycle(const TailArgsDev<Real> &d, int top, 
                 if (d.prof && threadIdx.x == 0) d.prof[pi] += tail_clock() - c0;
                 descending = false;
             } else {
+                // the block team's register levels leave r(x) in T (no re-read of x)
+                const bool rr = tail_rows_level<Team>(d.lv[l].N);
                 cnt += tail_smooth<Team>(E + d.lv[l].off, F + d.lv[l].off, d.lv[l], a.v1, d.eps2, T,
-                                         red, par);
+                                         red, par, rr ? T : nullptr);
                 if (d.prof && threadIdx.x == 0) {
                     const unsigned long long c1 = tail_clock();
                     d.prof[pi] += c1 - c0;
                     c0 = c1;
                 }
-                tail_res_restrict<Team>(E + d.lv[l].off, F + d.lv[l].off, d.lv[l],
-                                        F + d.lv[l + 1].off, E + d.lv[l + 1].off, d.lv[l + 1], T);
+                if (rr) {
+                    Team::sync();
+                    tail_restrict_T<Team>(T, d.lv[l], F + d.lv[l + 1].off, E + d.lv[l + 1].off, d.lv[l + 1]);
+                } else {
+                    tail_res_restrict<Team>(E + d.lv[l].off, F + d.lv[l].off, d.lv[l],
+                                            F + d.lv[l + 1].off, E + d.lv[l + 1].off, d.lv[l + 1], T);
+                }
                 if (d.prof && threadIdx.x == 0) d.prof[pr] += tail_clock() - c0;
                 vset(l + 1, 0);
                 ++l;
