@@ -70,6 +70,8 @@ def lib(dtype="f64"):
             "orc_residual_norm": (C.c_double, [P, P, C.c_int, C.c_double]),
             "orc_hash": (C.c_uint64, [P, C.c_longlong]),
             "orc_real_size": (C.c_int, []),
+            "orc_mt64_nth": (C.c_uint64, [C.c_uint64, C.c_longlong]),
+            "orc_rhs_mt64": (None, [P, C.c_int, C.c_uint64]),
         }
         for k, (r, a) in sig.items():
             fn = getattr(L, k)
@@ -146,6 +148,15 @@ class Oracle:
     def _chk(self, *arrays):
         for a in arrays:
             assert a.dtype == self.dt and a.flags.c_contiguous, (a.dtype, self.dt)
+
+
+def rhs_mt64(N, seed=12345, dtype="f64"):
+    """SURVEY §8(d)'s robustness RHS: std::uniform_real_distribution<double>(-1, 1) over
+    std::mt19937_64(seed), one draw per point in row-major order, boundary 0
+    (orc_rhs_mt64; pinned to libstdc++ by tests/golden/mt_rhs.json)."""
+    f = np.zeros((N, N), dtype=_np_dtype(dtype))
+    lib(dtype).orc_rhs_mt64(_p(f), N, seed)
+    return f
 
 
 def residual(x, f, h):

@@ -426,3 +426,70 @@ uint64_t orc_hash(const real *v, long long n)
     }
     return hsh;
 }
+
+/* The robustness right-hand side of SURVEY §8(d): uniform values in [-1, 1) from
+ * std::mt19937_64 seeded with `seed`, drawn for every point in row-major order
+ * (boundary points included, then set to 0), each as libstdc++'s
+ * std::uniform_real_distribution<double>(-1, 1) computes it:
+ * u = generate_canonical<double, 53> = (double)x / 2^64 (k = 1 draw of 64 bits; u >= 1
+ * becomes nextafter(1, 0)), value = u * (b - a) + a.  The engine is the standard's
+ * mt19937_64 (w 64, n 312, m 156, r 31; its required 10000th output of the default
+ * seed is checked by tests/test_oracle_mt_rhs.py), and tests/golden/mt_rhs.json
+ * (tests/golden/make_mt_rhs.cpp, libstdc++ itself) pins the values. */
+typedef struct {
+    uint64_t mt[312];
+    int i;
+} orc_mt64;
+
+static void orc_mt64_seed(orc_mt64 *g, uint64_t seed)
+{
+    g->mt[0] = seed;
+    for (int i = 1; i < 312; ++i)
+        g->mt[i] = 6364136223846793005ULL * (g->mt[i - 1] ^ (g->mt[i - 1] >> 62)) + (uint64_t)i;
+    g->i = 312;
+}
+
+static uint64_t orc_mt64_next(orc_mt64 *g)
+{
+    const uint64_t up = ~((1ULL << 31) - 1), lo = (1ULL << 31) - 1;
+    if (g->i >= 312) {
+        for (int k = 0; k < 312; ++k) {
+            const uint64_t x = (g->mt[k] & up) | (g->mt[(k + 1) % 312] & lo);
+            uint64_t xa = x >> 1;
+            if (x & 1ULL) xa ^= 0xB5026F5AA96619E9ULL;
+            g->mt[k] = g->mt[(k + 156) % 312] ^ xa;
+        }
+        g->i = 0;
+    }
+    uint64_t y = g->mt[g->i++];
+    y ^= (y >> 29) & 0x5555555555555555ULL;
+    y ^= (y << 17) & 0x71D67FFFEDA60000ULL;
+    y ^= (y << 37) & 0xFFF7EEE000000000ULL;
+    y ^= y >> 43;
+    return y;
+}
+
+/* the n-th output (1-based) of mt19937_64 seeded with `seed` */
+uint64_t orc_mt64_nth(uint64_t seed, long long n)
+{
+    orc_mt64 g;
+    orc_mt64_seed(&g, seed);
+    uint64_t y = 0;
+    for (long long k = 0; k < n; ++k) y = orc_mt64_next(&g);
+    return y;
+}
+
+void orc_rhs_mt64(real *f, int N, uint64_t seed)
+{
+    orc_mt64 g;
+    orc_mt64_seed(&g, seed);
+    const double two64 = 18446744073709551616.0;
+    for (int j = 0; j < N; ++j)
+        for (int i = 0; i < N; ++i) {
+            double u = (double)orc_mt64_next(&g) / two64;
+            if (u >= 1.0) u = nextafter(1.0, 0.0);
+            const double v = u * (1.0 - -1.0) + -1.0;
+            const int b = j == 0 || i == 0 || j == N - 1 || i == N - 1;
+            f[(long long)j * N + i] = b ? (real)0 : (real)v;
+        }
+}
