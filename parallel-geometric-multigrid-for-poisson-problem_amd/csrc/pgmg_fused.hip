@@ -1311,7 +1311,9 @@ static void fused_geometry(int N, int jc0, int jc1, int *threads, int *gx, int *
             // latency-bound levels (N <= 2049): short bands (~8k points per workgroup);
             // measured at N = 16385: 2049 26+20 -> 23+18 us, 1025 13+11 -> 12+10, 513..129
             // 12+10 -> 7+7
-            target = tuning_int("PGMG_FUSED_SMALL_BLOCKS", (int)std::max(256LL, pts / 8192));
+            target = tuning_int("PGMG_FUSED_SMALL_BLOCKS",
+                                (int)std::max((long long)tuning_int("PGMG_FUSED_SMALL_MIN", 256),
+                                              pts / tuning_int("PGMG_FUSED_SMALL_PTS", 8192)));
         }
     }
 
