@@ -30,7 +30,7 @@ def _gpu(pgmg, N, f, calls, kind="V", **kw):
         return s.solution(), s.stats()[0]
 
 
-@pytest.mark.parametrize("N,calls", [(2049, [3]), (2049, [1, 2]), (513, [5, 25])])
+@pytest.mark.parametrize("N,calls", [(2049, [3]), (2049, [1, 2]), (513, [5, 25]), (4097, [3])])
 def test_robust_rhs_vcycle(pgmg, oracle_mod, N, calls):
     f, ref, sw = _oracle(oracle_mod, N, calls)
     got, gsw = _gpu(pgmg, N, f, calls)
@@ -79,3 +79,24 @@ def test_robust_rhs_strips(pgmg, oracle_mod):
             raise e
     for r in range(W):
         assert_bitwise(out[r], ref, f"mt64 RHS strips rank {r}")
+
+
+def test_robust_rhs_l1post(pgmg, oracle_mod):
+    f, ref, sw = _oracle(oracle_mod, 2049, [4])
+    got, gsw = _gpu(pgmg, 2049, f, [4], flags=pgmg.PGMG_FLAG_L1POST)
+    assert_bitwise(got, ref, "mt64 RHS L1POST")
+    assert gsw == sw
+
+
+@pytest.mark.parametrize("N", [2049, 4097])
+def test_robust_rhs_fast_tolerance(pgmg, oracle_mod, N):
+    """FAST mode on a rough RHS: the same tolerance against the exact default as on the
+    analytic one (test_gpu_fast.TOL), equal sweep counts."""
+    f = oracle_mod.rhs_mt64(N)
+    ref, sw = _gpu(pgmg, N, f, [10])
+    got, gsw = _gpu(pgmg, N, f, [10], flags=pgmg.PGMG_FLAG_FAST)
+    d = got - ref
+    rel = np.linalg.norm(d) / np.linalg.norm(ref)
+    print(f"N={N} FAST vs exact on the mt64 RHS: rel {rel:.3e} max-abs {np.max(np.abs(d)):.3e}")
+    assert rel <= 1e-12 and np.max(np.abs(d)) <= 1e-12 * max(1.0, np.max(np.abs(ref)))
+    assert gsw == sw
