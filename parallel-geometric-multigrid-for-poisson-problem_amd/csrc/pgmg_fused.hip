@@ -117,7 +117,29 @@ __device__ __forceinline__ Cols lane_cols_t(int N, int bx = -1)
     return k;
 }
 
-__device__ __forceinline__ Cols lane_cols(int N) { return lane_cols_t<120, 4>(N); }
+__device__ __forceinline__ Cols lane_cols(int N, int bx = -1) { return lane_cols_t<120, 4>(N, bx); }
+
+#ifndef PGMG_XCD_MAP
+#define PGMG_XCD_MAP 0   // A/B builds: 1 = k_pre / k_post blocks in XCD-contiguous vertical runs
+#endif
+// Logical (column block, band) of this workgroup.  PGMG_XCD_MAP: workgroups go to the 8 XCDs
+// round-robin by linear id, so XCD p % 8 takes logical blocks (p % 8) * B/8 + p / 8 in
+// column-major order: the bands a workgroup's halo rows are shared with run on the same
+// XCD (its L2) at about the same time.
+__device__ __forceinline__ void fused_block(int &bx, int &by)
+{
+    bx = blockIdx.x;
+    by = blockIdx.y;
+    if constexpr (PGMG_XCD_MAP != 0) {
+        const int gx = gridDim.x, gy = gridDim.y, B = gx * gy;
+        if ((B & 7) == 0) {
+            const int p = blockIdx.y * gx + blockIdx.x;
+            const int L = (p & 7) * (B >> 3) + (p >> 3);
+            by = L % gy;
+            bx = L / gy;
+        }
+    }
+}
 
 // deterministic sum over the block (fixed tree) -> thread 0
 __device__ __forceinline__ double fused_block_sum(double v, double *red)
@@ -200,10 +222,12 @@ __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red)
 {
     constexpr int R = 2 * PAIRS;  // rows loaded per iteration (and prefetched ahead)
     if (a.cond != nullptr && *a.cond == 0u) return;  // conditional (rare-path) launch
-    const Cols k = lane_cols(a.N);
+    int lbx, lby;
+    fused_block(lbx, lby);
+    const Cols k = lane_cols(a.N, lbx);
     const int N = a.N;
     const long long P = a.P;
-    const int jcb = a.jc0 + blockIdx.y * a.rows_per_block;
+    const int jcb = a.jc0 + lby * a.rows_per_block;
     const int jce = min(jcb + a.rows_per_block, a.jc1);
     const int olo = max(2 * jcb, a.row_lo), ohi = min(2 * jce, a.row_hi);  // x2 rows written
     const int clo = max(jcb, max(1, a.rc_lo)), chi = min(jce, min(N / 2, a.rc_hi));  // rc rows
@@ -453,10 +477,12 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
 {
     constexpr int R = 2 * PAIRS;
     if (a.cond != nullptr && *a.cond == 0u) return;  // conditional (rare-path) launch
-    const Cols k = lane_cols(a.N);
+    int lbx, lby;
+    fused_block(lbx, lby);
+    const Cols k = lane_cols(a.N, lbx);
     const int N = a.N, Nc = a.Nc;
     const long long P = a.P, Pc = a.Pc;
-    const int jcb = a.jc0 + blockIdx.y * a.rows_per_block;
+    const int jcb = a.jc0 + lby * a.rows_per_block;
     const int jce = min(jcb + a.rows_per_block, a.jc1);
     const int olo = max(2 * jcb, a.row_lo), ohi = min(2 * jce, a.row_hi);
     const int slo = a.sum_hi > a.sum_lo ? max(olo, a.sum_lo) : olo;
