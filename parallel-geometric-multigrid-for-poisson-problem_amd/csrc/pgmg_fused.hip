@@ -791,6 +791,9 @@ constexpr int pp_depth()
 #ifndef PGMG_PP_NTL
 #define PGMG_PP_NTL 0     // 1: non-temporal row loads (measurement builds)
 #endif
+#ifndef PGMG_PP_PRIO
+#define PGMG_PP_PRIO 0    // measurement builds: 1 static s_setprio 1 for odd workgroups,
+#endif                    // 2 priority 1 while a step issues its row loads
 
 // Lane t's 16-byte (fp32: 8-byte) column pair of a row segment starting at `base`; lanes
 // t >= n read 0 (descriptor range check).  The descriptor is built from wave-uniform values.
@@ -1065,6 +1068,9 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
             for (int q = 0; q < 6; ++q) l1->e[(((m0 - 2) >> 1) + q) & 7][t] = pg[q];
         }
     }
+    if constexpr (PGMG_PP_PRIO == 1) {
+        if (__builtin_amdgcn_readfirstlane(bk.x + bk.y) & 1) __builtin_amdgcn_s_setprio(1);
+    }
     // prologue: pair 0 (+ its first coarse row) into slot 0; pairs 1 .. D in flight
     load_pair(0, pxA, pfA, peA);
     if (!L1 && t < ncc) se[ring(m0)][t] = buf_one<T>(a.ec + (long long)m0 * Pc + cc0, nve, t);
@@ -1098,7 +1104,9 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
         // D steps ago) first and reissue its register set for pair gi+1+D, so the loads in
         // flight are never younger than this step's stores (counted waits stay small)
         if (gi + 1 < ng) store_pair(gi + 1, px, pf, pe);
+        if constexpr (PGMG_PP_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         if (gi + 1 + D < ng) load_pair(gi + 1 + D, px, pf, pe);
+        if constexpr (PGMG_PP_PRIO == 2) __builtin_amdgcn_s_setprio(0);
         if constexpr (L1) l1_stage(gi, true);
         const int i = i_begin + gi * R;
         const int m = m0 + gi;
