@@ -1098,7 +1098,9 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     auto step = [&](int gi, V2<T> (&px)[R], V2<T> (&pf)[R], V2<T> &pe) {
         // keep the scheduler inside one pair: interleaving the unrolled pairs only raises
         // the register pressure (the loads of a pair are issued two pairs ahead anyway)
+#ifndef PGMG_PP_NOSCHED   // measurement builds: 1 drops this fence
         __builtin_amdgcn_sched_barrier(0);
+#endif
         const int slot = gi & 1;
         // the other slot's previous readers passed the last barrier: stage pair gi+1 (loaded
         // D steps ago) first and reissue its register set for pair gi+1+D, so the loads in
