@@ -75,6 +75,11 @@ def parse():
                     help="auto (one GPU, V, f64): also time PGMG_FLAG_FAST (FMA / shared "
                          "neighbour sums in the finest pass; not bitwise) and report its "
                          "difference from the EXACT result")
+    ap.add_argument("--dropin", choices=["auto", "off"], default="auto",
+                    help="auto (one GPU, V, f64): also time the reference's own entry point -- "
+                         "ParallelMultiGridSolver::v_cycle called once per cycle through the C++ "
+                         "mirror (host/gpu_exec, device arrays in place) -- and the context API's "
+                         "one-cycle calls it is measured against")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -398,6 +403,64 @@ def main():
                            "f_cycle_s": round(t1 - t0, 4), "w_cycle_s": round(t2 - t1, 4),
                            "parity": None if w is None or h is None else h == w})
 
+    # The reference's entry point as its harness drives it (ParallelTestRunner::run_v_cycle ->
+    # ParallelMultiGridSolver::v_cycle once per cycle, ParallelTestRunner.cu:171-175): the C++
+    # mirror host/gpu_exec on device arrays (phi updated in place, f regenerated), W untimed
+    # + K timed one-cycle calls, its own wall clock ("Elapsed Time"); beside it the context
+    # API with one-cycle calls (pgmg_vcycle(ctx, 1), no cross-cycle fusion between calls)
+    dropin = None
+    if world == 1 and args.cycle == "V" and args.dtype == "f64" and args.dropin == "auto":
+        ts = []
+        s = new_solver(0)
+        for _ in range(3):
+            s.set_problem()
+            for _ in range(max(args.warmup, 0)):
+                s.vcycle(1)
+            s.sync()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                s.vcycle(1)
+            s.sync()
+            ts.append(time.perf_counter() - t0)
+        h_ctx = s.solution_hash(0)
+        s.close()
+        ctx_dt = statistics.median(ts)
+        exe = pathlib.Path(_pkgload.PKG_DIR) / "host" / "gpu_exec"
+        runs = []
+        for _ in range(3):
+            r = subprocess.run([str(exe), "--n", str(args.n), "--cycles", str(args.steps),
+                                "--warmup", str(max(args.warmup, 0)), "--v-only", "--hash"],
+                               capture_output=True, text=True, timeout=600)
+            out = r.stdout
+            secs = [float(l.split("Elapsed Time:")[1].split()[0]) for l in out.splitlines()
+                    if "Elapsed Time:" in l]
+            hsh = [l.split("FNV-64:")[1].strip() for l in out.splitlines() if "FNV-64:" in l]
+            mode = [l.split("phi arrays:")[1].strip() for l in out.splitlines() if "phi arrays:" in l]
+            runs.append((r.returncode, secs[0] if secs else None, hsh[0] if hsh else None,
+                         mode[0] if mode else None))
+        ok = [x for x in runs if x[0] == 0 and x[1]]
+        if ok:
+            d_dt = statistics.median([x[1] for x in ok])
+            dropin = {
+                "what": "the reference's entry point: ParallelMultiGridSolver::v_cycle(phi, f, N, h) "
+                        "called once per cycle by ParallelTestRunner::run_v_cycle (C++ mirror "
+                        "host/gpu_exec --v-only), phi and f device arrays (pgmg_alloc_grid), phi "
+                        "updated in place, f regenerated; timed by the harness's own wall clock",
+                "value": round(args.steps / d_dt, 4), "unit": "V-cycles/s",
+                "ms_per_step": round(d_dt * 1e3 / args.steps, 4),
+                "timed": f"{max(args.warmup, 0)} warmup + {args.steps} calls, median of {len(ok)} runs",
+                "phi_arrays": ok[0][3],
+                "parity": None if want is None else all(x[2] == want for x in ok),
+                "context_single_calls": {
+                    "what": "pgmg_vcycle(ctx, 1) called once per cycle on the context's own grids",
+                    "value": round(args.steps / ctx_dt, 4), "unit": "V-cycles/s",
+                    "ms_per_step": round(ctx_dt * 1e3 / args.steps, 4),
+                    "parity": None if want is None or h_ctx is None else h_ctx == want},
+                "dropin_over_context_time": round(d_dt / ctx_dt, 4),
+            }
+        else:
+            dropin = {"what": "gpu_exec drop-in leg", "failed": [x[0] for x in runs]}
+
     # FAST mode (PGMG_FLAG_FAST): its rate, and phi after 10 cycles (SURVEY §8(c)'s window:
     # later, near convergence, a borderline early-exit check may decide differently) against
     # the EXACT default's (relative L2 and max-abs; tolerance in tests/test_gpu_fast.py)
@@ -529,6 +592,8 @@ def main():
         }
         if others is not None:
             line["other_configs"] = others
+        if dropin is not None:
+            line["dropin"] = dropin
         if fast_leg is not None:
             fast_leg["fast"] = True
             fmed = statistics.median(fast_leg["times"])

@@ -107,11 +107,8 @@ extern "C" {
                                    order, so phi agrees with the EXACT default within
                                    1e-12 relative (after <= 10 cycles) instead of bitwise.
                                    One GPU (row strips ignore it); everything else exact */
-#define PGMG_FLAG_L1POST 8192u  /* one GPU, speculative V-cycles: level 1's post-smooth of
-                                   cycle k runs inside the finest level's cross-cycle pass
-                                   (k_postpre) instead of its own pass; level 1's solution
-                                   is then never written.  Bitwise the same results;
-                                   measured slower at 16385: opt-in only */
+/* (8192u: level 1's post-smooth inside the finest pass -- built in r02, measured slower,
+   removed; the bit stays unused) */
 #define PGMG_FLAG_HOST_TRANSPORT 2048u /* world > 1 without RCCL: nccl_unique_id points to
                                        a pgmg_host_transport; every message and reduction
                                        is staged through host memory and handed to the
@@ -183,6 +180,31 @@ int pgmg_destroy(pgmg_ctx *ctx);
  * host libm sine tables).  Host arrays in the reference layout (pitch N).  With
  * world > 1 every rank passes the full arrays (or NULLs) and keeps its strip. */
 int pgmg_set_problem(pgmg_ctx *ctx, const double *phi0, const double *f);
+
+/* Device-resident problem: the reference's memory contract.  ParallelMultiGridSolver::
+ * v_cycle(phi, f, N, h) (3_part_parallel/Parallel_Mg.cu:21-60) updates in place arrays the
+ * caller allocated in device-accessible memory (cudaMallocManaged,
+ * ParallelTestRunner.cu:162-163).  After this call every pgmg_vcycle / wcycle / fcycle works
+ * on the caller's DEVICE arrays in the reference layout (N*N doubles, pitch N): phi is read
+ * and updated in place, synchronously (the call returns when phi holds the result), with no
+ * host transfer.  f = NULL: the analytic RHS of compute_rhs (regenerated in-kernel, never
+ * read); otherwise the caller's f, copied on the device into the context at every call (the
+ * caller may change it between calls).  With phi from pgmg_alloc_grid on a cross-fused fp64
+ * context (N >= cross_min_n) the finest-level passes read and write phi where it lies (the
+ * same HBM bytes as a call on the context's own grids); any other device pointer is staged
+ * with device-to-device copies before and after each call.  One GPU (world 1).  Resets the
+ * statistics like pgmg_set_problem; pgmg_set_problem unbinds.  pgmg_get_solution /
+ * pgmg_solution_hash / pgmg_residual_norm read the bound phi. */
+int pgmg_set_problem_device(pgmg_ctx *ctx, double *phi, const double *f);
+/* bound = a device problem is bound; inplace = its calls read / write phi in place */
+int pgmg_problem_device_info(pgmg_ctx *ctx, int *bound, int *inplace);
+/* An N*N device grid in the reference layout (pitch N, zeroed) with guard rows before and
+ * after it, so the finest passes may read past its edges: what the in-place path of
+ * pgmg_set_problem_device needs (the mirror's stand-in for cudaMallocManaged). */
+int pgmg_alloc_grid(double **ptr, int N);
+int pgmg_free_grid(double *ptr);
+/* *is_device = 1 when p is device (or managed) memory of the HIP runtime. */
+int pgmg_pointer_is_device(const void *p, int *is_device);
 
 /* Enqueue `ncycles` cycles on the context's stream (asynchronous; a speculative call,
  * see pgmg_dist_info, returns after the device has finished it).

@@ -21,7 +21,7 @@ from ._capi import (PGMG_FLAG_LOOPBACK, PGMG_FLAG_NO_CROSS, PGMG_FLAG_NO_GRAPH,
                     PGMG_FLAG_STORED_RHS, PGMG_FLAG_EXACT_DIST, PGMG_FLAG_SOLO,
                     PGMG_FLAG_TIME_FINE, PGMG_PRECISION_FP32, PGMG_PRECISION_FP64,
                     PGMG_FLAG_UNFUSED, PGMG_FLAG_NO_RECOMPUTE, PGMG_FLAG_NO_PIN,
-                    PGMG_FLAG_NO_R2, PGMG_FLAG_HOST_TRANSPORT, PGMG_FLAG_FAST, PGMG_FLAG_L1POST,
+                    PGMG_FLAG_NO_R2, PGMG_FLAG_HOST_TRANSPORT, PGMG_FLAG_FAST,
                     PGMG_PROLONG_REFERENCE,
                     PGMG_PROLONG_SYMMETRIC, PGMG_OK, PGMG_ERR_STATE, PgmgConfig, PgmgError,
                     check, load)
@@ -34,8 +34,8 @@ __all__ = [
     "PGMG_PROLONG_REFERENCE", "plan_strips", "LoopbackHub", "unique_id",
     "PGMG_PROLONG_SYMMETRIC", "PGMG_PRECISION_FP64", "PGMG_PRECISION_FP32",
     "PGMG_FLAG_STORED_RHS", "PGMG_FLAG_EXACT_DIST", "PGMG_FLAG_SOLO",
-    "PGMG_FLAG_NO_RECOMPUTE", "PGMG_FLAG_NO_PIN", "PGMG_FLAG_NO_R2", "PGMG_FLAG_FAST", "PGMG_FLAG_L1POST",
-    "PGMG_FLAG_HOST_TRANSPORT", "HostTransport",
+    "PGMG_FLAG_NO_RECOMPUTE", "PGMG_FLAG_NO_PIN", "PGMG_FLAG_NO_R2", "PGMG_FLAG_FAST",
+    "PGMG_FLAG_HOST_TRANSPORT", "HostTransport", "DeviceGrid",
 ]
 
 
@@ -191,6 +191,20 @@ class Solver:
         p = [None if a is None else a.ctypes.data_as(C.c_void_p) for a in args]
         check(self.lib.pgmg_set_problem(self.h, p[0], p[1]), "pgmg_set_problem")
 
+    def set_problem_device(self, phi, f=None):
+        """Bind device arrays (DeviceGrid, torch tensors or raw device pointers; N*N float64
+        in the reference layout) as the problem: phi is updated in place by every following
+        cycle call; f None = the analytic RHS (pgmg_set_problem_device)."""
+        check(self.lib.pgmg_set_problem_device(self.h, _dptr(phi), _dptr(f)),
+              "pgmg_set_problem_device")
+
+    def device_info(self):
+        """(a device problem is bound, its calls run in place)"""
+        b, i = C.c_int(), C.c_int()
+        check(self.lib.pgmg_problem_device_info(self.h, C.byref(b), C.byref(i)),
+              "pgmg_problem_device_info")
+        return bool(b.value), bool(i.value)
+
     def vcycle(self, n=1):
         check(self.lib.pgmg_vcycle(self.h, int(n)), "pgmg_vcycle")
 
@@ -307,6 +321,60 @@ class Solver:
         m = C.c_double()
         check(self.lib.pgmg_bench_sweep(self.h, int(reps), C.byref(m)), "pgmg_bench_sweep")
         return m.value
+
+
+def _dptr(t):
+    if t is None:
+        return None
+    if isinstance(t, int):
+        return C.c_void_p(t)
+    if isinstance(t, DeviceGrid):
+        return C.c_void_p(t.ptr)
+    return C.c_void_p(t.data_ptr())
+
+
+class DeviceGrid:
+    """An N*N float64 device grid in the reference layout with guard rows
+    (pgmg_alloc_grid): what ParallelTestRunner allocates with cudaMallocManaged
+    (3_part_parallel/ParallelTestRunner.cu:162-163), here device memory."""
+
+    def __init__(self, N, host=None):
+        self.lib = load()
+        self.N = int(N)
+        p = C.c_void_p()
+        check(self.lib.pgmg_alloc_grid(C.byref(p), self.N), "pgmg_alloc_grid")
+        self.ptr = p.value
+        if host is not None:
+            self.upload(host)
+
+    def upload(self, host):
+        a = np.ascontiguousarray(host, dtype=np.float64)
+        assert a.shape == (self.N, self.N), a.shape
+        check(self.lib.pgmg_memcpy_h2d(C.c_void_p(self.ptr), a.ctypes.data_as(C.c_void_p),
+                                       a.nbytes), "pgmg_memcpy_h2d")
+
+    def download(self):
+        out = np.empty((self.N, self.N), dtype=np.float64)
+        check(self.lib.pgmg_memcpy_d2h(out.ctypes.data_as(C.c_void_p), C.c_void_p(self.ptr),
+                                       out.nbytes), "pgmg_memcpy_d2h")
+        return out
+
+    def close(self):
+        if getattr(self, "ptr", None):
+            self.lib.pgmg_free_grid(C.c_void_p(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
 
 
 class _Ops:

@@ -35,7 +35,6 @@ PGMG_FLAG_NO_PIN = 512
 PGMG_FLAG_NO_R2 = 1024
 PGMG_FLAG_HOST_TRANSPORT = 2048
 PGMG_FLAG_FAST = 4096
-PGMG_FLAG_L1POST = 8192
 
 PGMG_PRECISION_FP64 = 0
 PGMG_PRECISION_FP32 = 1
@@ -89,6 +88,11 @@ SIGNATURES = [
     ("pgmg_create", C.c_int, [C.POINTER(_P), C.POINTER(PgmgConfig)]),
     ("pgmg_destroy", C.c_int, [_P]),
     ("pgmg_set_problem", C.c_int, [_P, _P, _P]),
+    ("pgmg_set_problem_device", C.c_int, [_P, _P, _P]),
+    ("pgmg_problem_device_info", C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    ("pgmg_alloc_grid", C.c_int, [C.POINTER(_P), C.c_int]),
+    ("pgmg_free_grid", C.c_int, [_P]),
+    ("pgmg_pointer_is_device", C.c_int, [_P, C.POINTER(C.c_int)]),
     ("pgmg_vcycle", C.c_int, [_P, C.c_int]),
     ("pgmg_wcycle", C.c_int, [_P, C.c_int]),
     ("pgmg_fcycle", C.c_int, [_P, C.c_int]),

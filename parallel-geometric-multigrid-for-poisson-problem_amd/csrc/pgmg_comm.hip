@@ -73,33 +73,31 @@ class RcclTransport : public Transport {
   public:
     ncclComm_t comm = nullptr;
     double timeout_s = 600.0;
-    // the side communicator of the early finest-level halos (split from `comm`, driven on
-    // the comm's side stream); polled and aborted together with `comm`
-    RcclTransport *side = nullptr;
+    // one event recorded after every enqueued group / allreduce (a ring): wait() counts a
+    // completed one as progress, so comm_timeout_s bounds the time WITHOUT progress, not
+    // the time behind a long queue of healthy work
+    static constexpr int kRing = 64;
+    hipEvent_t ring[kRing] = {};
+    long long rec = 0, done = 0;
     ~RcclTransport() override
     {
+        for (hipEvent_t e : ring)
+            if (e) (void)hipEventDestroy(e);
         if (comm) ncclCommDestroy(comm);
     }
     int abort_with(const std::string &why)
     {
-        if (side && side->comm) {
-            ncclCommAbort(side->comm);
-            side->comm = nullptr;
-        }
         if (comm) ncclCommAbort(comm);
         comm = nullptr;
         return set_err(PGMG_ERR_COMM, why);
     }
-    // a communicator for a second stream: operations on two streams of ONE communicator may
-    // interleave differently on different ranks
-    int split_into(RcclTransport &out)
+    int mark(hipStream_t s)
     {
-        if (!comm) return set_err(PGMG_ERR_COMM, "communicator aborted by an earlier error");
-        int rank = 0;
-        NCCLC(ncclCommUserRank(comm, &rank));
-        NCCLC(ncclCommSplit(comm, 0, rank, &out.comm, nullptr));
-        out.timeout_s = timeout_s;
-        side = &out;
+        if (!ring[0])
+            for (hipEvent_t &e : ring) PGMG_HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        PGMG_HIPC(hipEventRecord(ring[rec % kRing], s));
+        ++rec;
+        if (rec - done > kRing) done = rec - kRing;   // older marks were overwritten
         return PGMG_OK;
     }
     // Poll the stream instead of blocking in hipStreamSynchronize: a peer that died or
@@ -107,23 +105,29 @@ class RcclTransport : public Transport {
     int wait(hipStream_t s) override
     {
         if (!comm) return set_err(PGMG_ERR_COMM, "communicator aborted by an earlier error");
-        const auto t0 = std::chrono::steady_clock::now();
+        auto t0 = std::chrono::steady_clock::now();
         for (int spin = 0;; ++spin) {
             const hipError_t q = hipStreamQuery(s);
-            if (q == hipSuccess) return PGMG_OK;
+            if (q == hipSuccess) {
+                done = rec;
+                return PGMG_OK;
+            }
             if (q != hipErrorNotReady)
                 return abort_with(std::string("stream error while waiting: ") + hipGetErrorString(q));
             ncclResult_t ae = ncclSuccess;
             if (ncclCommGetAsyncError(comm, &ae) == ncclSuccess && ae != ncclSuccess &&
                 ae != ncclInProgress)
                 return abort_with(std::string("RCCL asynchronous error: ") + ncclGetErrorString(ae));
-            if (side && side->comm && ncclCommGetAsyncError(side->comm, &ae) == ncclSuccess &&
-                ae != ncclSuccess && ae != ncclInProgress)
-                return abort_with(std::string("RCCL asynchronous error (side communicator): ") +
-                                  ncclGetErrorString(ae));
+            bool progressed = false;
+            while (done < rec && hipEventQuery(ring[done % kRing]) == hipSuccess) {
+                ++done;
+                progressed = true;
+            }
+            if (progressed) t0 = std::chrono::steady_clock::now();
             const double dt =
                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-            if (dt > timeout_s) return abort_with("RCCL wait timed out (pgmg_config.comm_timeout_s)");
+            if (dt > timeout_s)
+                return abort_with("RCCL wait: no progress for pgmg_config.comm_timeout_s");
             if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
         }
     }
@@ -150,20 +154,22 @@ class RcclTransport : public Transport {
         NCCLC(ncclRecv(buf, bytes, ncclChar, peer, comm, s));
         return PGMG_OK;
     }
-    int group_end(hipStream_t) override
+    int group_end(hipStream_t s) override
     {
         NCCLC(ncclGroupEnd());
-        return PGMG_OK;
+        return mark(s);
     }
     int allreduce_sum(double *d, int n, hipStream_t s) override
     {
+        if (!comm) return set_err(PGMG_ERR_COMM, "communicator aborted by an earlier error");
         NCCLC(ncclAllReduce(d, d, n, ncclDouble, ncclSum, comm, s));
-        return PGMG_OK;
+        return mark(s);
     }
     int allreduce_min_u32(unsigned *d, int n, hipStream_t s) override
     {
+        if (!comm) return set_err(PGMG_ERR_COMM, "communicator aborted by an earlier error");
         NCCLC(ncclAllReduce(d, d, n, ncclUint32, ncclMin, comm, s));
-        return PGMG_OK;
+        return mark(s);
     }
 };
 
@@ -441,24 +447,17 @@ class NullTransport : public Transport {
 class StripComm : public Comm {
   public:
     Transport *t = nullptr;
-    Transport *t2 = nullptr;     // the early halos' transport (RCCL: a split communicator;
-                                 // the others: t itself, which takes the stream per call)
     int me = 0, world = 1;
     int Ld = 0;                  // levels 0..Ld-1 distributed; Ld = first gathered level
     std::vector<int> split;      // finest-level split points s_0 .. s_world
-    hipStream_t side = nullptr;  // the early halos' stream
-    hipEvent_t ev_ready = nullptr, ev_done = nullptr;
+    // halo_begin's exchange, not yet posted: it joins the next grouped exchange of the
+    // stream (or is posted alone by halo_end / before an allreduce)
     bool pending = false;
+    Grid pend_g;
+    Level pend_L;
+    int pend_depth = 0;
 
-    ~StripComm() override
-    {
-        if (side) (void)hipStreamSynchronize(side);
-        if (ev_ready) (void)hipEventDestroy(ev_ready);
-        if (ev_done) (void)hipEventDestroy(ev_done);
-        if (side) (void)hipStreamDestroy(side);
-        if (t2 != t) delete t2;
-        delete t;
-    }
+    ~StripComm() override { delete t; }
     int gathered_level() const override { return Ld; }
     int rank() const override { return me; }
 
@@ -505,65 +504,90 @@ class StripComm : public Comm {
         return PGMG_OK;
     }
 
-    int setup(pgmg_ctx *) override
-    {
-        PGMG_HIPC(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
-        PGMG_HIPC(hipEventCreateWithFlags(&ev_ready, hipEventDisableTiming));
-        PGMG_HIPC(hipEventCreateWithFlags(&ev_done, hipEventDisableTiming));
-        if (!t2) t2 = t;
-        return PGMG_OK;
-    }
+    int setup(pgmg_ctx *) override { return PGMG_OK; }
 
+    // The finest level's halo rows are final a whole coarse hierarchy before the next
+    // finest pass reads them.  Instead of a second communicator on a side stream (two
+    // communicators' kernels running concurrently on one device can deadlock), the exchange
+    // is held back and posted INSIDE the next grouped exchange of the same stream: the
+    // coarse level's right-hand-side halos, or the all-to-all of the first gathered level.
+    // One RCCL group per cycle instead of two, on one communicator, in stream order.
     int halo_begin(const Grid &g, const Level &L, int depth, hipStream_t s) override
     {
-        if (!side || pending) return halo(g, L, depth, s);
-        PGMG_HIPC(hipEventRecord(ev_ready, s));
-        PGMG_HIPC(hipStreamWaitEvent(side, ev_ready, 0));
-        const HaloReq r{&g, &L, depth};
-        const int e = halos_on(t2, &r, 1, side);
-        if (e) return e;
-        PGMG_HIPC(hipEventRecord(ev_done, side));
+        if (pending) {
+            const int e = flush(s);
+            if (e) return e;
+        }
+        pend_g = g;
+        pend_L = L;
+        pend_depth = depth;
         pending = true;
         return PGMG_OK;
     }
 
-    int halo_end(hipStream_t s) override
+    int flush(hipStream_t s)
     {
         if (!pending) return PGMG_OK;
         pending = false;
-        PGMG_HIPC(hipStreamWaitEvent(s, ev_done, 0));
-        return PGMG_OK;
+        const HaloReq r{&pend_g, &pend_L, pend_depth};
+        return halos_on(t, &r, 1, s);
     }
 
-    int halos(const HaloReq *reqs, int n, hipStream_t s) override { return halos_on(t, reqs, n, s); }
+    int halo_end(hipStream_t s) override { return flush(s); }
 
-    int halos_on(Transport *t, const HaloReq *reqs, int n, hipStream_t s)
+    int halos(const HaloReq *reqs, int n, hipStream_t s) override
     {
-        int e = t->group_start();
-        if (e) return e;
-        for (int k = 0; k < n && !e; ++k) {
-            const Grid &g = *reqs[k].g;
-            const Level &L = *reqs[k].L;
-            const int depth = reqs[k].depth;
-            const size_t row = (size_t)L.P * L.es;
-            if (me > 0) {
-                e = t->send(row_ptr(g, L.lo, L.P, L.es), depth * row, me - 1, s);
-                if (!e) e = t->recv(row_ptr(g, L.lo - depth, L.P, L.es), depth * row, me - 1, s);
-            }
-            if (!e && me < world - 1) {
-                e = t->send(row_ptr(g, L.hi - depth, L.P, L.es), depth * row, me + 1, s);
-                if (!e) e = t->recv(row_ptr(g, L.hi, L.P, L.es), depth * row, me + 1, s);
-            }
+        if (!pending) return halos_on(t, reqs, n, s);
+        std::vector<HaloReq> all;
+        all.reserve(n + 1);
+        all.push_back(HaloReq{&pend_g, &pend_L, pend_depth});
+        all.insert(all.end(), reqs, reqs + n);
+        pending = false;
+        return halos_on(t, all.data(), n + 1, s);
+    }
+
+    // one array's halo send/recv pairs inside an open group
+    int post_halo(Transport *tp, const HaloReq &q, hipStream_t s)
+    {
+        const Grid &g = *q.g;
+        const Level &L = *q.L;
+        const int depth = q.depth;
+        const size_t row = (size_t)L.P * L.es;
+        int e = PGMG_OK;
+        if (me > 0) {
+            e = tp->send(row_ptr(g, L.lo, L.P, L.es), depth * row, me - 1, s);
+            if (!e) e = tp->recv(row_ptr(g, L.lo - depth, L.P, L.es), depth * row, me - 1, s);
         }
-        const int e2 = t->group_end(s);   // the group is closed even after a failed call
+        if (!e && me < world - 1) {
+            e = tp->send(row_ptr(g, L.hi - depth, L.P, L.es), depth * row, me + 1, s);
+            if (!e) e = tp->recv(row_ptr(g, L.hi, L.P, L.es), depth * row, me + 1, s);
+        }
+        return e;
+    }
+
+    int halos_on(Transport *tp, const HaloReq *reqs, int n, hipStream_t s)
+    {
+        int e = tp->group_start();
+        if (e) return e;
+        for (int k = 0; k < n && !e; ++k) e = post_halo(tp, reqs[k], s);
+        const int e2 = tp->group_end(s);   // the group is closed even after a failed call
         return e ? e : e2;
     }
 
-    int allreduce_sum(double *d, int n, hipStream_t s) override { return t->allreduce_sum(d, n, s); }
-    int wait(hipStream_t s) override { return t->wait(s); }
+    int allreduce_sum(double *d, int n, hipStream_t s) override
+    {
+        const int e = flush(s);
+        return e ? e : t->allreduce_sum(d, n, s);
+    }
+    int wait(hipStream_t s) override
+    {
+        const int e = flush(s);
+        return e ? e : t->wait(s);
+    }
     int allreduce_min_u32(unsigned *d, int n, hipStream_t s) override
     {
-        return t->allreduce_min_u32(d, n, s);
+        const int e = flush(s);
+        return e ? e : t->allreduce_min_u32(d, n, s);
     }
 
     int allgather_rows(pgmg_ctx *c, int l, const Grid &g) override
@@ -572,6 +596,10 @@ class StripComm : public Comm {
         const size_t row = (size_t)L.P * L.es;
         int e = t->group_start();
         if (e) return e;
+        if (pending) {   // the finest level's held-back halo rides in this group
+            pending = false;
+            e = post_halo(t, HaloReq{&pend_g, &pend_L, pend_depth}, c->s);
+        }
         for (int r = 0; r < world && !e; ++r) {
             const int a = std::max(strip_lo(r, l), 1), b = std::min(strip_hi(r, l, L.N), L.N - 1);
             if (b <= a) continue;
@@ -605,6 +633,7 @@ class StripComm : public Comm {
         const int N = L.N;
         const size_t row = (size_t)L.P * L.es;
         const bool want = root < 0 || root == me;
+        if (const int ef = flush(c->s)) return ef;
         Grid full;
         if (want) {
             PGMG_HIPC(hipMalloc(&full.base, (size_t)N * row));
@@ -678,11 +707,6 @@ Comm *Comm::create(pgmg_ctx *c, int *rc)
         if (cfg.comm_timeout_s > 0) rt->timeout_s = cfg.comm_timeout_s;
         sc->t = rt;
         *rc = rt->init(cfg.nccl_unique_id, cfg.world, cfg.rank);
-        if (!*rc) {
-            auto *r2 = new RcclTransport();
-            sc->t2 = r2;
-            *rc = rt->split_into(*r2);
-        }
         if (*rc) {
             delete sc;
             return nullptr;
@@ -734,37 +758,24 @@ int pgmg_rccl_selftest(const void *uid128, int device)
                 hipMemset(b, 0, n * sizeof(double)) != hipSuccess ||
                 hipMemcpy(u, hu, sizeof(hu), hipMemcpyHostToDevice) != hipSuccess))
         rc = pgmg::set_err(PGMG_ERR_HIP, "selftest upload");
-    // the early-halo pattern of the strips: a split communicator on a second stream that
-    // waits for the main stream's event, exchanging while the main stream works on
-    pgmg::RcclTransport t2;
-    hipStream_t s2 = nullptr;
-    hipEvent_t ev = nullptr, ev2 = nullptr;
+    // the merged pattern of the strips: one group carrying two messages to the same peer
+    // (the finest level's held-back halo, then a coarse level's rows), matched in order
     double *c2 = nullptr;
-    if (!rc) rc = t.split_into(t2);
-    if (!rc && (hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) != hipSuccess ||
-                hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&ev2, hipEventDisableTiming) != hipSuccess ||
-                hipMalloc(&c2, n * sizeof(double)) != hipSuccess))
-        rc = pgmg::set_err(PGMG_ERR_HIP, "selftest side stream");
+    if (!rc && hipMalloc(&c2, n * sizeof(double)) != hipSuccess)
+        rc = pgmg::set_err(PGMG_ERR_HIP, "selftest second buffer");
     if (!rc) rc = t.group_start();
     if (!rc) rc = t.send(a, n * sizeof(double), 0, s);
     if (!rc) rc = t.recv(b, n * sizeof(double), 0, s);
+    if (!rc) rc = t.send(a, (n / 2) * sizeof(double), 0, s);
+    if (!rc) rc = t.recv(c2, (n / 2) * sizeof(double), 0, s);
     if (!rc) rc = t.group_end(s);
-    if (!rc && (hipEventRecord(ev, s) != hipSuccess || hipStreamWaitEvent(s2, ev, 0) != hipSuccess))
-        rc = pgmg::set_err(PGMG_ERR_HIP, "selftest events");
-    if (!rc) rc = t2.group_start();
-    if (!rc) rc = t2.send(b, n * sizeof(double), 0, s2);
-    if (!rc) rc = t2.recv(c2, n * sizeof(double), 0, s2);
-    if (!rc) rc = t2.group_end(s2);
     if (!rc) rc = t.allreduce_sum(a, 3, s);
     if (!rc) rc = t.allreduce_min_u32(u, 4, s);
-    if (!rc && (hipEventRecord(ev2, s2) != hipSuccess || hipStreamWaitEvent(s, ev2, 0) != hipSuccess))
-        rc = pgmg::set_err(PGMG_ERR_HIP, "selftest events");
-    if (!rc) rc = t.wait(s);   // polls both communicators
+    if (!rc) rc = t.wait(s);   // polls the stream, the async error state and the progress marks
     if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = pgmg::set_err(PGMG_ERR_HIP, "selftest sync");
-    if (!rc && (hipMemcpy(g.data(), c2, n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
-                std::memcmp(g.data(), h.data(), n * sizeof(double)) != 0))
-        rc = pgmg::set_err(PGMG_ERR_COMM, "selftest: the side communicator's rows differ");
+    if (!rc && (hipMemcpy(g.data(), c2, (n / 2) * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
+                std::memcmp(g.data(), h.data(), (n / 2) * sizeof(double)) != 0))
+        rc = pgmg::set_err(PGMG_ERR_COMM, "selftest: the second message of the group differs");
     if (!rc && (hipMemcpy(g.data(), b, n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
                 hipMemcpy(gu, u, sizeof(gu), hipMemcpyDeviceToHost) != hipSuccess))
         rc = pgmg::set_err(PGMG_ERR_HIP, "selftest download");
@@ -782,11 +793,7 @@ int pgmg_rccl_selftest(const void *uid128, int device)
     (void)hipFree(b);
     (void)hipFree(u);
     if (c2) (void)hipFree(c2);
-    if (ev) (void)hipEventDestroy(ev);
-    if (ev2) (void)hipEventDestroy(ev2);
-    if (s2) (void)hipStreamDestroy(s2);
     (void)hipStreamDestroy(s);
-    t.side = nullptr;   // t2 is destroyed first (declared later)
     return rc;
 }
 

@@ -83,11 +83,6 @@ struct pgmg_ctx {
     bool cross = false;           // finest level fuses post(k) with pre(k+1) across cycles
     bool recompute = true;        // levels entered with x0 = 0 recompute x2 in k_post
     pgmg::Grid S;                 // finest-level scratch for k_postpre's rare paths
-    // PGMG_FLAG_L1POST: level 1's second RHS buffer (k_postpre reads f1 of cycle k from
-    // one while it restricts cycle k+1's into the other; swapped with lv[1].F) and the
-    // mark that the level-1 visit being enqueued leaves its post-smooth to k_postpre
-    pgmg::Grid F1alt;
-    bool skip_l1_post = false;
     double *partials2 = nullptr;  // second partials buffer (k_postpre's pre check)
     double *partials3 = nullptr;  // third (row strips: k_postpre's pre check from x1)
     // analytic RHS (set_problem with f = NULL): level-0 passes may regenerate f in-kernel
@@ -135,6 +130,20 @@ struct pgmg_ctx {
     bool fmg_rhs_ready = false;   // Ffmg holds the level-0 analytic RHS of the FMG h chain
     double *fmg_tab = nullptr;
     std::vector<int> fmg_off;     // per level 0..nb then tail levels below nb: sx offset
+    // pgmg_set_problem_device: the caller's arrays in the reference layout (pitch N, double),
+    // the problem of every following cycle call (phi updated in place)
+    double *ext_phi = nullptr;
+    const double *ext_f = nullptr;   // nullptr: the analytic RHS (regenerated in-kernel)
+    bool ext_inplace = false;        // the finest passes read / write ext_phi in place
+    // while a call is enqueued: the first k_pre reads x_in, the last k_post writes x_out
+    // (pitch ext_P) instead of the level-0 grids; defer_post stops before that last k_post
+    // (a speculative call validates its checks first: x_out is also x_in), pend_pr is the
+    // pre-smoothed iterate it will read
+    const void *x_in = nullptr;
+    void *x_out = nullptr;
+    long long ext_P = 0;
+    bool defer_post = false;
+    void *pend_pr = nullptr;
 };
 
 namespace pgmg {

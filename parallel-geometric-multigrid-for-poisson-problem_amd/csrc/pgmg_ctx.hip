@@ -78,6 +78,32 @@ void pgmg::unregister_alloc(const void *base)
     g_allocs.erase((uintptr_t)base);
 }
 
+// is [lo, hi) inside ONE registered allocation?
+static bool registered_span(intptr_t lo, intptr_t hi)
+{
+    std::lock_guard<std::mutex> lk(g_alloc_mu);
+    auto it = g_allocs.upper_bound((uintptr_t)lo);
+    if (it == g_allocs.begin()) return false;
+    --it;
+    const intptr_t b = (intptr_t)it->first, e = b + (intptr_t)it->second;
+    return lo >= b && hi <= e;
+}
+
+namespace {
+std::mutex g_user_mu;
+std::map<uintptr_t, void *> g_user_grids;   // pgmg_alloc_grid: element (0,0) -> allocation
+}  // namespace
+
+static bool is_device_ptr(const void *p)
+{
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();   // unregistered host memory: not an error to keep
+        return false;
+    }
+    return at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged;
+}
+
 int pgmg::check_span(const void *o, long long P, int es, long long r0, long long r1,
                      long long c0, long long c1, const char *what)
 {
@@ -85,15 +111,7 @@ int pgmg::check_span(const void *o, long long P, int es, long long r0, long long
     const intptr_t org = (intptr_t)o;
     const intptr_t lo = org + (intptr_t)((r0 * P + c0) * es);
     const intptr_t hi = org + (intptr_t)((r1 * P + c1 + 1) * es);   // one past the last byte
-    {
-        std::lock_guard<std::mutex> lk(g_alloc_mu);
-        auto it = g_allocs.upper_bound((uintptr_t)lo);
-        if (it != g_allocs.begin()) {
-            --it;
-            const intptr_t b = (intptr_t)it->first, e = b + (intptr_t)it->second;
-            if (lo >= b && hi <= e) return PGMG_OK;
-        }
-    }
+    if (registered_span(lo, hi)) return PGMG_OK;
     char buf[256];
     std::snprintf(buf, sizeof(buf),
                   "%s: rows %lld..%lld, columns %lld..%lld (pitch %lld) outside the array's "
@@ -372,10 +390,6 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
         if ((e = launch_pre_rare(fa, pa, x0_zero, c->s))) return e;
     }
     if ((e = enqueue_children<T>(c, l, gamma))) return e;
-    if (l == 1 && c->skip_l1_post) {   // the finest level's k_postpre runs it (L1POST)
-        c->skip_l1_post = false;
-        return PGMG_OK;
-    }
     // the correction of level l+1 is not exchanged: a distributed child's k_post computed
     // it kPostExt rows past its strip (a gathered child's is replicated)
     if (dist && !recomp && (e = c->comm->halo(L.B, L, ext ? 2 + kPostExt : 2, c->s))) return e;
@@ -529,7 +543,12 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
     // rollback restarts from it
     const bool lean = c->lean;
     auto grid_of = [&](const T *p) -> const Grid * { return p == A ? &gA : p == B ? &gB : &gS; };
-    auto next_of = [&](const T *p) -> T * { return lean ? (p == B ? S : B) : (p == A ? B : A); };
+    // (an external input is followed by B: the first k_pre writes B, then B <-> S (lean) or
+    // B <-> A, both free of the input)
+    auto next_of = [&](const T *p) -> T * { return lean ? (p == B ? S : B) : (p == B ? A : B); };
+    // the caller's array (pgmg_set_problem_device) as the call's input / output
+    const T *in = c->x_in != nullptr ? static_cast<const T *>(c->x_in) : A;
+    T *const xout = static_cast<T *>(c->x_out);
     const int np = fused_blocks(L.N, sr.jc0, sr.jc1);
     const int npp = postpre_blocks(L.N, sr.jc0, sr.jc1);
     FixArgsF fa{};
@@ -538,16 +557,10 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
     fa.eps = c->cfg.eps;
     fa.stats = c->stats;
     int e;
-    // PGMG_FLAG_L1POST: level 1's post-smooth of cycle k inside k_postpre (speculative
-    // V-cycles on one GPU, level 1 a bulk level entered with x0 = 0 whose checks are not
-    // decided in-stream); its RHS alternates between lv[1].F and F1alt
-    const bool l1post = lean && (c->cfg.flags & PGMG_FLAG_L1POST) && !dist && c->comm == nullptr &&
-                        gamma == 1 && c->nb > 1 && c->recompute && !c->lvl_exact[1] &&
-                        !(c->cfg.flags & PGMG_FLAG_FAST);
-    if (l1post && !c->F1alt.base && (e = alloc_grid(c->F1alt, C))) return e;
     // cycle 1: pre-smooth (+ residual, restriction) A -> B
     if (dist && (e = c->comm->halo(gA, L, 4, c->s))) return e;
-    PreArgsT<T> pa = make_pre<T>(c, A, B);
+    PreArgsT<T> pa = make_pre<T>(c, in, B);
+    if (c->x_in != nullptr) pa.Px = c->ext_P;
     double *lp = chk_partials(c, np, 0);
     if (lp) pa.partials = lp;
     int ev = timed_begin(c, 1);
@@ -563,7 +576,6 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
     // after the whole coarse hierarchy: the exchange runs on the comm's side stream
     // meanwhile (the coarse correction's halo rows are computed locally, kPostExt)
     if (dist && (e = c->comm->halo_begin(*grid_of(pr), L, 6, c->s))) return e;
-    c->skip_l1_post = l1post && n > 1;
     if ((e = enqueue_children<T>(c, 0, gamma))) return e;
     for (int k = 1; k < n; ++k) {
         T *nx = next_of(pr);
@@ -574,17 +586,6 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         q.f = G<T>(L.F);
         q.x4 = nx;
         q.rc = G<T>(C.F);
-        if (l1post) {   // level 1's post check first: the log keeps each level's order
-            const Level &CC = c->lv[2];
-            q.f1 = G<T>(C.F);
-            q.rc = G<T>(c->F1alt);
-            q.e2 = G<T>(CC.A);
-            q.N2 = CC.N;
-            q.P2 = CC.P;
-            q.hh1 = (T)C.hh;
-            q.ih1 = (T)C.ih;
-            q.partials4 = chk_partials(c, npp, 1);
-        }
         q.partials1 = lean ? chk_partials(c, npp, 0) : c->partials;
         q.partials2 = lean ? chk_partials(c, npp, 0) : c->partials2;
         q.partials3 = (dist && !lean) ? c->partials3 : nullptr;   // lean: no rare path runs
@@ -607,12 +608,10 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         ev = timed_begin(c, 3);
         if ((e = launch_postpre(q, c->s))) return e;
         if ((e = timed_end(c, 3, ev))) return e;
-        if (l1post) std::swap(C.F, c->F1alt);   // cycle k+1's level-1 RHS
         const double *g3 = nullptr;   // all-rank {post, pre, pre-from-x1} sums
         if (lean) {
             pr = nx;
             if (dist && (e = c->comm->halo_begin(*grid_of(pr), L, 6, c->s))) return e;
-            c->skip_l1_post = l1post && k + 1 < n;
             if ((e = enqueue_children<T>(c, 0, gamma))) return e;
             continue;
         }
@@ -670,9 +669,14 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         if ((e = enqueue_children<T>(c, 0, gamma))) return e;
     }
     // last cycle: post-smooth
-    T *out = next_of(pr);
+    if (c->defer_post) {   // enqueued by run_cycles_spec after the validation
+        c->pend_pr = pr;
+        return PGMG_OK;
+    }
+    T *out = xout != nullptr ? xout : next_of(pr);
     if (dist && (e = c->comm->halo_end(c->s))) return e;
     PostArgsT<T> po = make_post<T>(c, pr, out);
+    if (xout != nullptr) po.Po = c->ext_P;
     lp = chk_partials(c, np, 0);
     if (lp) po.partials = lp;
     ev = timed_begin(c, 2);
@@ -682,8 +686,10 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         if (dist && (e = global_sum(c, np, &fa.global_sum))) return e;
         launch_post_fixup(fa, po, c->s);
     }
-    // the solution's buffer becomes L.A (all three mirror the boundary)
-    if (lean) {
+    // the solution's buffer becomes L.A (all three mirror the boundary); an external output
+    // holds it instead (the level-0 grids keep their roles)
+    if (xout != nullptr) {
+    } else if (lean) {
         const Grid go = *grid_of(out), gp = *grid_of(pr);
         L.A = go;
         L.B = gA;
@@ -810,7 +816,6 @@ int pgmg_destroy(pgmg_ctx *c)
     free_grid(c->bk);
     if (c->ppflags) (void)hipFree(c->ppflags);
     free_grid(c->S);
-    free_grid(c->F1alt);
     free_grid(c->Ffmg);
     for (auto &g : c->Ffmg_l) free_grid(g);
     if (c->fmg_tab) (void)hipFree(c->fmg_tab);
@@ -1018,35 +1023,25 @@ int pgmg::download_grid(pgmg_ctx *c, const void *o, int P, int N, double *host)
     return PGMG_OK;
 }
 
-extern "C" {
-
-int pgmg_set_problem(pgmg_ctx *c, const double *phi0, const double *f)
+// statistics and speculation history of a new problem
+static int problem_reset(pgmg_ctx *c)
 {
-    if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
+    HIPC(hipMemset(c->stats, 0, 4 * sizeof(unsigned long long)));
+    HIPC(hipDeviceSynchronize());
+    c->have_problem = true;
+    c->spec_off = false;   // a new problem: speculate again, every level
+    c->lvl_exact.assign(c->nb + 1, 0);
+    c->lvl_hist.assign(c->nb + 1, std::vector<double>());
+    return PGMG_OK;
+}
+
+// level-0 right-hand side rows [r0, r1): the host array f, or (f = NULL) the analytic RHS of
+// compute_rhs, stored and, unless PGMG_FLAG_STORED_RHS, regenerated by the level-0 passes
+static int setup_rhs(pgmg_ctx *c, const double *f, int r0, int r1)
+{
     Level &L = c->lv[0];
     const int N = L.N;
-    if (!L.on_this_rank) return set_err(PGMG_ERR_STATE, "level 0 not on this rank");
-    // owned rows + the halo rows the fused passes read (every rank has the full host arrays)
-    const int r0 = L.lo - kHalo > 0 ? L.lo - kHalo : 0;
-    const int r1 = L.hi + kHalo < N ? L.hi + kHalo : N;
-    const size_t rows = (size_t)(r1 - r0);
-    const size_t pitch = (size_t)L.P * L.es, width = (size_t)N * L.es;
     int e;
-    PGMG_TRY(stream_wait(c));
-    // phi (and its boundary copy in the ping-pong buffer B)
-    if (phi0) {
-        if ((e = upload_rows(c, L, L.A, phi0, r0, r1))) return e;
-    } else {
-        HIPC(hipMemset2D(row_ptr(L.A, r0, L.P, L.es), pitch, 0, width, rows));
-    }
-    if (c->nb > 0)
-        HIPC(hipMemcpy2D(row_ptr(L.B, r0, L.P, L.es), pitch, row_ptr(L.A, r0, L.P, L.es), pitch,
-                         width, rows, hipMemcpyDeviceToDevice));
-    // the cross-cycle rare-path scratch S mirrors phi's boundary too (its passes never
-    // write boundary rows/columns, the k_pre that reads it passes them through)
-    if (c->S.base)
-        HIPC(hipMemcpy2D(row_ptr(c->S, r0, L.P, L.es), pitch, row_ptr(L.A, r0, L.P, L.es), pitch,
-                         width, rows, hipMemcpyDeviceToDevice));
     c->gen_rhs = false;
     c->rgfx = c->rgsy = nullptr;
     if (f) {
@@ -1083,14 +1078,212 @@ int pgmg_set_problem(pgmg_ctx *c, const double *phi0, const double *f)
             c->rgsy = c->gsy;
         }
     }
-    HIPC(hipMemset(c->stats, 0, 4 * sizeof(unsigned long long)));
-    HIPC(hipDeviceSynchronize());
-    c->have_problem = true;
-    c->spec_off = false;   // a new problem: speculate again, every level
-    c->lvl_exact.assign(c->nb + 1, 0);
-    c->lvl_hist.assign(c->nb + 1, std::vector<double>());
     return PGMG_OK;
 }
+
+extern "C" {
+
+int pgmg_set_problem(pgmg_ctx *c, const double *phi0, const double *f)
+{
+    if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
+    Level &L = c->lv[0];
+    const int N = L.N;
+    if (!L.on_this_rank) return set_err(PGMG_ERR_STATE, "level 0 not on this rank");
+    // owned rows + the halo rows the fused passes read (every rank has the full host arrays)
+    const int r0 = L.lo - kHalo > 0 ? L.lo - kHalo : 0;
+    const int r1 = L.hi + kHalo < N ? L.hi + kHalo : N;
+    const size_t rows = (size_t)(r1 - r0);
+    const size_t pitch = (size_t)L.P * L.es, width = (size_t)N * L.es;
+    int e;
+    PGMG_TRY(stream_wait(c));
+    c->ext_phi = nullptr;   // host arrays: the problem lives in the context again
+    c->ext_f = nullptr;
+    // phi (and its boundary copy in the ping-pong buffer B)
+    if (phi0) {
+        if ((e = upload_rows(c, L, L.A, phi0, r0, r1))) return e;
+    } else {
+        HIPC(hipMemset2D(row_ptr(L.A, r0, L.P, L.es), pitch, 0, width, rows));
+    }
+    if (c->nb > 0)
+        HIPC(hipMemcpy2D(row_ptr(L.B, r0, L.P, L.es), pitch, row_ptr(L.A, r0, L.P, L.es), pitch,
+                         width, rows, hipMemcpyDeviceToDevice));
+    // the cross-cycle rare-path scratch S mirrors phi's boundary too (its passes never
+    // write boundary rows/columns, the k_pre that reads it passes them through)
+    if (c->S.base)
+        HIPC(hipMemcpy2D(row_ptr(c->S, r0, L.P, L.es), pitch, row_ptr(L.A, r0, L.P, L.es), pitch,
+                         width, rows, hipMemcpyDeviceToDevice));
+    if ((e = setup_rhs(c, f, r0, r1))) return e;
+    return problem_reset(c);
+}
+
+int pgmg_set_problem_device(pgmg_ctx *c, double *phi, const double *f)
+{
+    if (!c || !phi) return set_err(PGMG_ERR_ARG, "null argument");
+    if (c->comm) return set_err(PGMG_ERR_STATE, "pgmg_set_problem_device: one GPU only (world 1)");
+    if (!is_device_ptr(phi) || (f && !is_device_ptr(f)))
+        return set_err(PGMG_ERR_ARG, "pgmg_set_problem_device: phi and f must be device memory");
+    Level &L = c->lv[0];
+    const int N = L.N;
+    PGMG_TRY(stream_wait(c));
+    int e;
+    if (!f) {
+        if ((e = setup_rhs(c, nullptr, 0, N))) return e;
+    } else {
+        c->gen_rhs = false;
+        c->rgfx = c->rgsy = nullptr;
+    }
+    // in place: a cross-fused fp64 context and phi inside an allocation that covers the rows
+    // and columns the finest passes read past the grid (pgmg_alloc_grid's guard)
+    const intptr_t o = (intptr_t)phi;
+    const long long lo = -(long long)kHalo * N - 8, hi = (long long)(N + kHalo) * N + 8;
+    c->ext_inplace = c->cross && !c->fp32 &&
+                     registered_span(o + (intptr_t)(lo * 8), o + (intptr_t)(hi * 8));
+    c->ext_phi = phi;
+    c->ext_f = f;
+    return problem_reset(c);
+}
+
+int pgmg_problem_device_info(pgmg_ctx *c, int *bound, int *inplace)
+{
+    if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
+    if (bound) *bound = c->ext_phi != nullptr ? 1 : 0;
+    if (inplace) *inplace = c->ext_phi != nullptr && c->ext_inplace ? 1 : 0;
+    return PGMG_OK;
+}
+
+int pgmg_alloc_grid(double **out, int N)
+{
+    if (!out || N < 3) return set_err(PGMG_ERR_ARG, "pgmg_alloc_grid: null pointer or N < 3");
+    *out = nullptr;
+    // (kHalo + 2) rows + 1024 elements before element (0,0) and after element (N-1, N-1);
+    // column 1 of row 0 on a 128-byte boundary
+    const size_t guard = (size_t)(kHalo + 2) * N + 1024 + 15;
+    const size_t n = 2 * guard + (size_t)N * N;
+    void *p = nullptr;
+    if (hipMalloc(&p, n * sizeof(double)) != hipSuccess)
+        return set_err(PGMG_ERR_NOMEM, "pgmg_alloc_grid: hipMalloc failed");
+    HIPC(hipMemset(p, 0, n * sizeof(double)));
+    register_alloc(p, n * sizeof(double));
+    double *o = static_cast<double *>(p) + guard;
+    {
+        std::lock_guard<std::mutex> lk(g_user_mu);
+        g_user_grids[(uintptr_t)o] = p;
+    }
+    *out = o;
+    return PGMG_OK;
+}
+
+int pgmg_free_grid(double *o)
+{
+    if (!o) return PGMG_OK;
+    void *p = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_user_mu);
+        auto it = g_user_grids.find((uintptr_t)o);
+        if (it == g_user_grids.end()) return set_err(PGMG_ERR_ARG, "pgmg_free_grid: not from pgmg_alloc_grid");
+        p = it->second;
+        g_user_grids.erase(it);
+    }
+    unregister_alloc(p);
+    HIPC(hipFree(p));
+    return PGMG_OK;
+}
+
+int pgmg_pointer_is_device(const void *p, int *is_device)
+{
+    if (!is_device) return set_err(PGMG_ERR_ARG, "null argument");
+    *is_device = (p != nullptr && is_device_ptr(p)) ? 1 : 0;
+    return PGMG_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Device-resident problems (pgmg_set_problem_device): the reference's contract.
+// ParallelMultiGridSolver::v_cycle(phi, f, N, h) (Parallel_Mg.cu:21-60) works on arrays the
+// caller allocated in device-accessible memory (cudaMallocManaged, ParallelTestRunner.cu:
+// 162-163) and updates phi in place; nothing crosses PCIe per call.  Here phi and f are
+// device arrays in the reference layout (pitch N, double).
+//   * in place (cross-fused fp64 contexts, phi from pgmg_alloc_grid): the call's first
+//     finest-level pass (k_pre) reads phi where it lies and its last (k_post) writes the
+//     result there (PreArgs::Px, PostArgs::Po = N); the level-0 grids only carry the
+//     iterates in between, so a call moves the same bytes as on the context's own grids.
+//     The passes read rows and columns past the grid (halos, tile margins): the guard rows
+//     of pgmg_alloc_grid keep those reads inside the allocation (span-checked per launch).
+//   * staged (any other device pointer, fp32, or contexts without cross-cycle fusion):
+//     phi is copied device-to-device into the level-0 grid before the call and back after.
+// f = NULL is the analytic RHS of compute_rhs, regenerated in-kernel (never read); a
+// caller's f is copied into the level-0 RHS grid at every call (the caller may change it).
+// ---------------------------------------------------------------------------
+// the boundary of the caller's phi into every level-0 grid the passes pass it through
+template <class T>
+static void ext_frames(pgmg_ctx *c)
+{
+    Level &L = c->lv[0];
+    const Grid *gs[3] = {&L.A, &L.B, &c->S};
+    for (const Grid *g : gs)
+        if (g->base) launch_copy_frame<T>(c->ext_phi, L.N, G<T>(*g), L.P, L.N, c->s);
+}
+
+// before a call: the caller's f into the level-0 RHS grid (unless analytic) and phi's frame
+// (in place) or all of phi (staged) into the level-0 grids
+static int ext_stage_in(pgmg_ctx *c, bool inplace)
+{
+    Level &L = c->lv[0];
+    const int N = L.N;
+    if (c->ext_f) {
+        if (c->fp32) launch_from_double(c->ext_f, N, G<float>(L.F), L.P, 0, N, c->s);
+        else HIPC(hipMemcpy2DAsync(L.F.o, L.P * sizeof(double), c->ext_f, N * sizeof(double),
+                                   N * sizeof(double), N, hipMemcpyDeviceToDevice, c->s));
+    }
+    if (!inplace) {
+        if (c->fp32) launch_from_double(c->ext_phi, N, G<float>(L.A), L.P, 0, N, c->s);
+        else HIPC(hipMemcpy2DAsync(L.A.o, L.P * sizeof(double), c->ext_phi, N * sizeof(double),
+                                   N * sizeof(double), N, hipMemcpyDeviceToDevice, c->s));
+    }
+    if (c->fp32) ext_frames<float>(c);
+    else ext_frames<double>(c);
+    HIPC(hipGetLastError());
+    return PGMG_OK;
+}
+
+static int ext_stage_out(pgmg_ctx *c)
+{
+    Level &L = c->lv[0];
+    const int N = L.N;
+    if (c->fp32) launch_to_double(G<float>(L.A), L.P, c->ext_phi, N, 0, N, c->s);
+    else HIPC(hipMemcpy2DAsync(c->ext_phi, N * sizeof(double), L.A.o, L.P * sizeof(double),
+                               N * sizeof(double), N, hipMemcpyDeviceToDevice, c->s));
+    HIPC(hipGetLastError());
+    return PGMG_OK;
+}
+
+// the last k_post of an in-place call whose speculative checks were validated first (its
+// input survives until then): from the pre-smoothed iterate into the caller's phi, its own
+// early-exit check decided in-stream
+template <class T>
+static int enqueue_last_post(pgmg_ctx *c)
+{
+    Level &L = c->lv[0];
+    const StripRows sr = strip_rows(L, c->lv[1]);
+    PostArgsT<T> po = make_post<T>(c, static_cast<const T *>(c->pend_pr), static_cast<T *>(c->x_out));
+    po.Po = c->ext_P;
+    const int ev = timed_begin(c, 2);
+    PGMG_TRY(launch_post(po, true, c->s));
+    PGMG_TRY(timed_end(c, 2, ev));
+    FixArgsF fa{};
+    fa.partials = c->partials;
+    fa.np = fused_blocks(L.N, sr.jc0, sr.jc1);
+    fa.eps = c->cfg.eps;
+    fa.stats = c->stats;
+    launch_post_fixup(fa, po, c->s);
+    HIPC(hipGetLastError());
+    HIPC(hipEventRecord(c->ev1, c->s));
+    c->pend_pr = nullptr;
+    return PGMG_OK;
+}
+
+extern "C" {
 
 static int run_cycles_plain(pgmg_ctx *c, int ncycles, int gamma, bool rec0 = true)
 {
@@ -1261,21 +1454,29 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
     const int npp = c->cross ? postpre_blocks(L0.N, L0.lo / 2, (L0.hi < L0.N ? L0.hi : L0.N - 1) / 2) : 0;
     long long d1, k1;
     spec_need_level(c, 1, gamma, &d1, &k1);
-    // (+ npp: L1POST logs level 1's post check with k_postpre's block count)
-    const long long per_dbl = 2LL * std::max(np0, npp) + d1 + npp, per_chk = 2 + k1;
+    const long long per_dbl = 2LL * std::max(np0, npp) + d1, per_chk = 2 + k1;
     // segments of at most 2^27 logged doubles (1 GiB) / 2^22 checks
     long long seg_max = std::min(((1LL << 27) - 2LL * np0) / per_dbl, ((1LL << 22) - 2) / per_chk);
     if (c->cfg.spec_segment > 0) seg_max = std::min<long long>(seg_max, c->cfg.spec_segment);
     if (seg_max < 1) return run_cycles_plain(c, ncycles, gamma);
     // the cross-fused cycles keep A intact (rotation through S); otherwise copy it
     const bool rotate = c->cross && c->S.base != nullptr;
+    // an in-place device call (run_cycles_ext): the first segment reads the caller's phi, the
+    // last writes it -- that final k_post only after the validation, since it overwrites the
+    // call's input (a rollback reruns from it)
+    const void *const ext_in = c->x_in;
+    void *const ext_out = c->x_out;
     bool first = true;
     while (ncycles > 0) {
         const int seg = (int)std::min<long long>(ncycles, seg_max);
+        c->x_in = first ? ext_in : nullptr;
+        c->x_out = ext_out;
         int e = spec_reserve(c, seg * per_dbl + 2LL * np0 + 64, seg * per_chk + 4);
         if (e) return e;
         if ((e = spec_mark_levels(c, seg))) return e;
         if (c->spec_off) return run_cycles_plain(c, ncycles, gamma, first);
+        const bool last = seg == ncycles;
+        const bool seg_first = first;
         const Grid A0 = L0.A, B0 = L0.B, S0 = c->S;
         if (!rotate) {
             if (!c->bk.base && (e = alloc_grid(c->bk, L0))) return e;
@@ -1288,7 +1489,11 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
         c->lean = true;
         c->plog_used = 0;
         c->chks.clear();
+        if (!last) c->x_out = nullptr;   // intermediate segments end in the level-0 grids
+        c->defer_post = ext_out != nullptr && last;
         e = run_cycles_plain(c, seg, gamma, first);
+        c->defer_post = false;
+        c->x_out = ext_out;
         c->lean = false;
         first = false;
         if (e) return e;
@@ -1328,11 +1533,47 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
                 HIPC(hipMemcpyAsync(L0.A.base, c->bk.base, L0.A.bytes, hipMemcpyDeviceToDevice, c->s));
             HIPC(hipMemcpyAsync(c->stats, c->stats_bk, 4 * sizeof(unsigned long long),
                                 hipMemcpyDeviceToDevice, c->s));
+            c->x_in = seg_first ? ext_in : nullptr;
+            c->pend_pr = nullptr;
             return run_cycles_plain(c, ncycles, gamma, false);
         }
         spec_record_norms(c, n);
+        if (ext_out != nullptr && last) {
+            e = c->fp32 ? enqueue_last_post<float>(c) : enqueue_last_post<double>(c);
+            if (e) return e;
+        }
         ncycles -= seg;
     }
+    return PGMG_OK;
+}
+
+static int run_cycles_core(pgmg_ctx *c, int ncycles, int gamma)
+{
+    // V-cycles only: W-cycles revisit the coarse levels until their checks fire (the
+    // reference's W-cycle at 129 exits 147 times in its first cycle), a rollback per call
+    if (c->spec && !c->spec_off && gamma == 1) return run_cycles_spec(c, ncycles, gamma);
+    return run_cycles_plain(c, ncycles, gamma);
+}
+
+// a call on a device-bound problem (pgmg_set_problem_device): synchronous, as the reference's
+// v_cycle is (the caller reads phi when it returns)
+static int run_cycles_ext(pgmg_ctx *c, int ncycles, int gamma)
+{
+    const bool inplace = c->ext_inplace;
+    PGMG_TRY(ext_stage_in(c, inplace));
+    if (inplace) {
+        c->x_in = c->ext_phi;
+        c->x_out = c->ext_phi;
+        c->ext_P = c->lv[0].N;
+    }
+    const int e = run_cycles_core(c, ncycles, gamma);
+    c->x_in = nullptr;
+    c->x_out = nullptr;
+    c->defer_post = false;
+    c->pend_pr = nullptr;
+    if (e) return e;
+    if (!inplace) PGMG_TRY(ext_stage_out(c));
+    PGMG_TRY(stream_wait(c));
     return PGMG_OK;
 }
 
@@ -1341,10 +1582,8 @@ static int run_cycles(pgmg_ctx *c, int ncycles, int gamma)
     if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
     if (!c->have_problem) return set_err(PGMG_ERR_STATE, "pgmg_set_problem first");
     if (ncycles <= 0) return PGMG_OK;
-    // V-cycles only: W-cycles revisit the coarse levels until their checks fire (the
-    // reference's W-cycle at 129 exits 147 times in its first cycle), a rollback per call
-    if (c->spec && !c->spec_off && gamma == 1) return run_cycles_spec(c, ncycles, gamma);
-    return run_cycles_plain(c, ncycles, gamma);
+    if (c->ext_phi) return run_cycles_ext(c, ncycles, gamma);
+    return run_cycles_core(c, ncycles, gamma);
 }
 
 int pgmg_dist_info(pgmg_ctx *c, int *speculative, long long *rollbacks)
@@ -1705,7 +1944,10 @@ int pgmg_gather_solution(pgmg_ctx *c, int root, double *phi)
 {
     if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
     const int me = c->comm ? c->comm->rank() : 0;
-    if (!phi && (root < 0 || root == me)) return set_err(PGMG_ERR_ARG, "null phi on a receiving rank");
+    if (root >= c->cfg.world) return set_err(PGMG_ERR_ARG, "root >= world");
+    // without strips every rank holds the whole solution: every root means this rank
+    if (!phi && (root < 0 || root == me || !c->comm))
+        return set_err(PGMG_ERR_ARG, "null phi on a receiving rank");
     if (c->comm) {
         int e = c->comm->wait(c->s);
         if (e) return e;
@@ -1713,6 +1955,10 @@ int pgmg_gather_solution(pgmg_ctx *c, int root, double *phi)
     }
     PGMG_TRY(stream_wait(c));
     Level &L = c->lv[0];
+    if (c->ext_phi) {   // a device-bound problem: the solution is the caller's array
+        HIPC(hipMemcpy(phi, c->ext_phi, (size_t)L.N * L.N * sizeof(double), hipMemcpyDeviceToHost));
+        return PGMG_OK;
+    }
     return download_grid(c, L.A.o, L.P, L.N, phi);
 }
 
@@ -1722,6 +1968,7 @@ int pgmg_solution_hash(pgmg_ctx *c, int root, unsigned long long *out)
 {
     if (!c || !out) return set_err(PGMG_ERR_ARG, "null argument");
     const int me = c->comm ? c->comm->rank() : 0;
+    if (root >= c->cfg.world) return set_err(PGMG_ERR_ARG, "root >= world");
     const bool want = root < 0 || root == me || !c->comm;
     const long long n = (long long)c->lv[0].N * c->lv[0].N;
     std::vector<double> phi(want ? (size_t)n : 0);
@@ -1744,6 +1991,9 @@ int pgmg_residual_norm(pgmg_ctx *c, double *out)
     if (!c || !out) return set_err(PGMG_ERR_ARG, "null argument");
     Level &L = c->lv[0];
     int nbk = c->partials_cap < 1024 ? c->partials_cap : 1024;
+    // a device-bound problem: its phi (and a caller's f) into the level-0 grids first (the
+    // analytic f is in L.F since pgmg_set_problem_device)
+    if (c->ext_phi) PGMG_TRY(ext_stage_in(c, false));
     if (c->comm) {
         int e = c->comm->halo(L.A, L, 1, c->s);
         if (e) return e;

@@ -32,6 +32,10 @@ struct PreArgsT {
     // zeroed fine grid, x0 = (+0) + P ec on rows/columns [2, N-2], 0 on the frame
     // (MultiGrid.hpp:159-164 followed by the V-cycle's pre-smooth)
     const T *pin_ec;
+    // row pitch of x0 in elements (0: P).  Non-zero when x0 is the caller's array in the
+    // reference layout (pitch N, pgmg_set_problem_device): the call's first pass reads it in
+    // place; its 16-byte column-pair loads are then 8-byte aligned on every other row
+    long long Px;
 };
 
 // prolongation + post-smooth (2 sweeps) in one pass
@@ -60,6 +64,9 @@ struct PostArgsT {
     // the level of the F climb whose V-cycle and smooth(3) run)
     const double *gfx, *gsy;
     int nt;                     // set by launch_post: bit 2 x2 stores non-temporal
+    // row pitch of x2 in elements (0: P): the call's last pass writes the caller's array
+    // (reference layout, pitch N) in place (pgmg_set_problem_device)
+    long long Po;
 };
 
 // post-smooth of cycle k + pre-smooth/residual/restriction of cycle k+1 in one pass
@@ -85,15 +92,6 @@ struct PostPreArgsT {
     int rc_lo, rc_hi;
     int rows_per_block;
     int fast;                   // PGMG_FLAG_FAST (one GPU, f regenerated or stored)
-    // non-null (PGMG_FLAG_L1POST, one GPU): level 1's post-smooth of cycle k runs inside
-    // this pass instead of its own k_post: ec is not read but computed per block from
-    // f1 (level 1's RHS of cycle k; rc above must then be another buffer) and e2 (level
-    // 2's corrected solution); sum r(x1)^2 of level 1 into partials4
-    const T *f1;
-    const T *e2;
-    double *partials4;
-    int N2, P2;
-    T hh1, ih1;
 };
 
 struct FixArgsF {

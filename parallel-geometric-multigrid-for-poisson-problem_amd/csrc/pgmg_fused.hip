@@ -119,26 +119,11 @@ __device__ __forceinline__ Cols lane_cols_t(int N, int bx = -1)
 
 __device__ __forceinline__ Cols lane_cols(int N, int bx = -1) { return lane_cols_t<120, 4>(N, bx); }
 
-#ifndef PGMG_XCD_MAP
-#define PGMG_XCD_MAP 0   // A/B builds: 1 = k_pre / k_post blocks in XCD-contiguous vertical runs
-#endif
-// Logical (column block, band) of this workgroup.  PGMG_XCD_MAP: workgroups go to the 8 XCDs
-// round-robin by linear id, so XCD p % 8 takes logical blocks (p % 8) * B/8 + p / 8 in
-// column-major order: the bands a workgroup's halo rows are shared with run on the same
-// XCD (its L2) at about the same time.
+// Logical (column block, band) of this workgroup
 __device__ __forceinline__ void fused_block(int &bx, int &by)
 {
     bx = blockIdx.x;
     by = blockIdx.y;
-    if constexpr (PGMG_XCD_MAP != 0) {
-        const int gx = gridDim.x, gy = gridDim.y, B = gx * gy;
-        if ((B & 7) == 0) {
-            const int p = blockIdx.y * gx + blockIdx.x;
-            const int L = (p & 7) * (B >> 3) + (p >> 3);
-            by = L % gy;
-            bx = L / gy;
-        }
-    }
 }
 
 // deterministic sum over the block (fixed tree) -> thread 0
@@ -234,6 +219,7 @@ __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red)
     if (!S1 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
         atomicAdd(&a.stats[0], 2ull);
     const T *__restrict__ X = a.x0 + k.c;
+    const long long Px = a.Px != 0 ? a.Px : P;   // x0's pitch (the caller's array: N)
     const T *__restrict__ F = a.f + k.c;
     const double fxa = GENF ? a.gfx[k.c] : 0.0, fxb = GENF ? a.gfx[k.c + 1] : 0.0;
     const bool store = a.x2 != nullptr;
@@ -272,7 +258,7 @@ __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red)
     T ncr[PAIRS + 1], ncrn[PAIRS + 1];
     #pragma unroll
     for (int q = 0; q < R; ++q) {
-        nx[q] = (X0_ZERO || PIN || idle) ? z : ldv(X + (i_begin + q) * P);
+        nx[q] = (X0_ZERO || PIN || idle) ? z : ldvu(X + (i_begin + q) * Px);
         if constexpr (!GENF) nf[q] = idle ? z : ldv(F + (i_begin + q) * P);
     }
     if constexpr (PIN) {
@@ -309,7 +295,7 @@ __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red)
         if (i + R < i_end) {  // prefetch the next R rows
             #pragma unroll
             for (int q = 0; q < R; ++q) {
-                if (!X0_ZERO && !PIN) nx[q] = ldv(X + (i + R + q) * P);
+                if (!X0_ZERO && !PIN) nx[q] = ldvu(X + (i + R + q) * Px);
                 if constexpr (!GENF) nf[q] = ldv(F + (i + R + q) * P);
             }
             if constexpr (PIN) {
@@ -499,6 +485,7 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
     const T *__restrict__ X = RECOMP ? F + P : a.phi + k.c;
     const T *__restrict__ E = a.ec + pc.ic;
     T *__restrict__ O = a.x2 + k.c;
+    const long long Po = a.Po != 0 ? a.Po : P;   // x2's pitch (the caller's array: N)
     const T hh = a.hh, ih = a.ih;
     const V2<T> z = zero2<T>();
     // windows: x_eff rows i-2,i-1 ; x1 rows i-3,i-2 ; f rows i-2,i-1
@@ -589,7 +576,7 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
                 const V2<T> a2 = add_prolong<T, !FULL>(ph, ii, cr[pq], crn[pq], cr[pq + 1], crn[pq + 1], pc, Nc);
                 const V2<T> b2 = jstage<T, !FULL>(a0, a1, a2, f2, hh, k, boundary_row(ii - 1, N));
                 if constexpr (S1) {   // the post check fired: x1 row ii-1 is the result
-                    if (ii - 1 >= olo && ii - 1 < ohi && k.own) stv(O + (ii - 1) * P, b2);
+                    if (ii - 1 >= olo && ii - 1 < ohi && k.own) stvu(O + (ii - 1) * Po, b2);
                     a0 = a1;
                     a1 = a2;
                     f1 = f2;
@@ -606,8 +593,8 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
                 }
                 const V2<T> c2 = jstage<T, !FULL>(b0, b1, b2, f1, hh, k, boundary_row(ii - 2, N));
                 if ((FULL || (ii - 2 >= olo && ii - 2 < ohi)) && k.own) {
-                    if (a.nt & 4) stv_nt(O + (ii - 2) * P, c2);
-                    else stv(O + (ii - 2) * P, c2);
+                    if (a.nt & 4) stv_nt(O + (ii - 2) * Po, c2);
+                    else stvu(O + (ii - 2) * Po, c2);
                 }
                 a0 = a1;
                 a1 = a2;
@@ -751,10 +738,7 @@ __device__ __forceinline__ V2<T> rsn(V2<T> up, V2<T> ce, V2<T> dn, Nbr<T> n, V2<
 // are in flight in registers and pair g+1 sits in the other slot; one barrier per
 // row pair.  Coarse rows live in a ring of 3 (pair g reads coarse rows g and g+1).
 // ---------------------------------------------------------------------------
-#ifndef PGMG_PP_WAVES   // -DPGMG_PP_WAVES=8 (A/B builds only): 8-wave blocks measured equal
-#define PGMG_PP_WAVES 4   // (1.125-1.147 vs 1.126-1.146 ms; the other k_postpre variants assume 4)
-#endif
-constexpr int kPPWaves = PGMG_PP_WAVES;                            // waves per k_postpre block
+constexpr int kPPWaves = 4;   // waves per k_postpre block (8-wave blocks measured equal, r02)
 constexpr int kPPLdsRow = kPPWaves * kPPStride + 2 * kPPMargin + 4;          // doubles per row
 constexpr int kPPLdsCoarse = kPPWaves * (kPPStride / 2) + kPPMargin + 8;     // per coarse row
 
@@ -779,22 +763,11 @@ constexpr int kPPR = 2;   // rows per LDS slot (a row pair)
 // body 6 rows, the period of the row windows (no window copies: 141 -> 129 VALU per row);
 // the fp64 instantiations with more live state (streamed f, the strips' third sum, the
 // F-cycle's four-sweep form) keep 2, which fits 256 VGPRs without spilling.
-#ifndef PGMG_PP_DEPTH
-#define PGMG_PP_DEPTH 0   // 0: per instantiation as above; 2 or 3 forces it (A/B builds)
-#endif
 template <class T, bool R2, bool GENF, int OPT>
 constexpr int pp_depth()
 {
-    if constexpr (PGMG_PP_DEPTH != 0) return PGMG_PP_DEPTH;
     return (sizeof(T) == 4 || (GENF && !R2 && !(OPT & (64 | 32)))) ? 3 : 2;
 }
-#ifndef PGMG_PP_NTL
-#define PGMG_PP_NTL 0     // 1: non-temporal row loads (measurement builds)
-#endif
-#ifndef PGMG_PP_PRIO
-#define PGMG_PP_PRIO 0    // measurement builds: 1 static s_setprio 1 for odd workgroups,
-#endif                    // 2 priority 1 while a step issues its row loads
-
 // Lane t's 16-byte (fp32: 8-byte) column pair of a row segment starting at `base`; lanes
 // t >= n read 0 (descriptor range check).  The descriptor is built from wave-uniform values.
 template <class T, int NT>
@@ -844,37 +817,14 @@ __device__ __forceinline__ T buf_one(const T *base, int n, int t)
         return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, t * 4, 0, 0));
 }
 
-// OPT & 32 (PGMG_FLAG_L1POST): level 1's post-smooth of cycle k inside the pass.  The
-// block's 256 lanes own one level-1 column each, c1 = cc0 - 3 + t (the coarse window plus
-// 3 columns each side: x_eff, x1, x2 each lose one), and per row pair compute one row of
-// each stage, lagging 2 rows apart (x_eff row m0+g+6, x1 m0+g+4, x2 m0+g+2), as k_post
-// RECOMP does with the pre check not fired (the speculative call's assumption, verified
-// after the call): x_pre = J(J(0)) from f1, x_eff = x_pre + P e2, x1 = J(x_eff), x2 = J(x1)
-// with r(x1) summed.  x2 goes straight into the coarse ring se the level-0 prolongation
-// reads, so level 1's solution is never written and never read back (18 B per level-1
-// point of its k_post, against 2.5 B per level-1 point here: f1 and e2).
-#ifndef PGMG_L1_EXP
-#define PGMG_L1_EXP 0   // A/B builds only (wrong results): 1 no frame masks, 2 no level-1 stages
-#endif
-constexpr int kL1Row = 64 * kPPWaves + 2;    // lane t at [t + 1]
-constexpr int kL1E = 32 * kPPWaves + 8;      // level-2 column ((cc0 - 3) >> 1) + t at [t]
-template <class T> struct L1Lds {
-    T f[8][kL1Row];   // f1 rows (ring 8: rows g+2 .. g+7 read, g+8 stored per step)
-    T x[4][kL1Row];   // x_eff rows
-    T y[4][kL1Row];   // x1 rows
-    T e[8][kL1E];     // e2 rows
-};
-
 // The body of k_postpre_lds for one block.  EDGE = false: no row of the block's band and
 // no column of this wave is a boundary, so the Jacobi stages carry no passthrough selects.
 template <class T, bool R2, bool GENF, bool EDGE, int OPT>
 __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const Cols &k,
                                                 double *red, T (&sx)[2][kPPR][kPPLdsRow],
                                                 T (&sf)[2][kPPR][GENF ? 1 : kPPLdsRow],
-                                                T (&se)[3][kPPLdsCoarse], L1Lds<T> *l1,
-                                                const Blk bk)
+                                                T (&se)[3][kPPLdsCoarse], const Blk bk)
 {
-    constexpr bool L1 = (OPT & 32) != 0;
     constexpr int R = kPPR;
     const int N = a.N, Nc = a.Nc;
     const long long P = a.P, Pc = a.Pc;
@@ -883,7 +833,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     const int olo = max(2 * jcb, a.row_lo), ohi = min(2 * jce, a.row_hi);
     const int clo = max(jcb, max(1, a.rc_lo)), chi = min(jce, min(N / 2, a.rc_hi));
     if (bk.x == 0 && bk.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
-        atomicAdd(&a.stats[0], L1 ? 6ull : 4ull);
+        atomicAdd(&a.stats[0], 4ull);
     ProlongCols pc;
     pc.ic = (k.c - 1) >> 1;
     pc.vx = k.c >= 3 && k.c <= N - 2;
@@ -906,7 +856,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     // the row pairs prefetched for later steps.
     // lanes that load (columns >= N never matter)
     const int nvx = max(0, min(npairs, (N - 1 - L0) / 2 + 1));
-    const int nve = (OPT & (64 | 32)) ? 0 : max(0, min(ncc, Nc - cc0));
+    const int nve = (OPT & 64) ? 0 : max(0, min(ncc, Nc - cc0));
     // stores: x4 row segment of the block window (lanes that own their pair), rc (lanes
     // owning a coarse column <= Nc-2); anything else gets an out-of-range offset
     constexpr int kOOB = 1 << 30;
@@ -942,44 +892,17 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     // D register sets: pair p's loads go to set p % D, issued D pairs ahead (D = 2: sets
     // A, B; D = 3: A, B, C)
     constexpr int D = pp_depth<T, R2, GENF, OPT>();
-    static_assert(D == 2 || D == 3, "PGMG_PP_DEPTH is 2 or 3");
+    static_assert(D == 2 || D == 3, "two or three register sets");
     V2<T> pxA[R], pfA[R], pxB[R], pfB[R], pxC[R], pfC[R];   // C unused (dead) when D = 2
-    // L1: a register T carries two values, lane t's f1 (low) and e2 (high) of the pair --
-    // kept as V2 sets with the coarse row's slot otherwise
-    V2<T> peA = z, peB = z, peC = z;
-    // L1 geometry: lane t = level-1 column lc (see L1Lds)
-    const int N1 = Nc;
-    const int lc = cc0 - 3 + t;
-    const bool cin = lc >= 1 && lc <= N1 - 2, cinl = lc >= 2 && lc <= N1 - 1,
-               cinr = lc >= 0 && lc <= N1 - 3, ccor = lc >= 2 && lc <= N1 - 2;
-    const int n0 = (cc0 - 3) >> 1;
-    const int ne = (lc >> 1) - n0;                       // 0 .. 128
-    // the check's columns: level-1 columns (c+1)/2 of the block's owned odd fine columns c
-    const bool own1 = t >= 7 && t < 7 + (kPPStride / 2) * wpb && lc <= N1 - 2;
-    const int fcol = min(max(lc, 0), N1 - 1), ecol = min(max(n0 + t, 0), a.N2 - 1);
-    auto l1_f = [&](int r) -> T {   // f1[r][lc] (clamped; masked where it matters)
-        return buf_one<T>(a.f1 + (long long)min(max(r, 0), N1 - 1) * Pc, N1, fcol);
-    };
-    auto l1_e = [&](int m) -> T {   // e2[m][n0 + t]
-        return buf_one<T>(a.e2 + (long long)min(max(m, 0), a.N2 - 1) * a.P2, a.N2, ecol);
-    };
-    // pair p carries f1 row m0 + p + 7 and e2 row (m0 + p + 8) >> 1 (stored one step ahead)
-    auto l1_store = [&](int r, V2<T> v) {
-        l1->f[r & 7][t + 1] = v.x;
-        if (t < kL1E) l1->e[((r + 1) >> 1) & 7][t] = v.y;
-    };
+    V2<T> peA = z, peB = z, peC = z;   // the pair's second coarse row (in .x)
     auto load_pair = [&](int p, V2<T> (&px)[R], V2<T> (&pf)[R], V2<T> &pe) {
         #pragma unroll
         for (int q = 0; q < R; ++q) {
             const long long row = (long long)(i_begin + p * R + q) * P + L0;
-            px[q] = buf_row<T, PGMG_PP_NTL>(a.phi + row, nvx, t);
-            if constexpr (!GENF) pf[q] = buf_row<T, PGMG_PP_NTL>(a.f + row, nvx, t);
+            px[q] = buf_row<T, 0>(a.phi + row, nvx, t);
+            if constexpr (!GENF) pf[q] = buf_row<T, 0>(a.f + row, nvx, t);
         }
-        if constexpr (L1) {
-            if (p >= 1) pe = mk2<T>(l1_f(m0 + p + 7), l1_e((m0 + p + 8) >> 1));
-        } else {   // the pair's second coarse row
-            pe.x = buf_one<T>(a.ec + (long long)(m0 + p + 1) * Pc + cc0, nve, t);
-        }
+        pe.x = buf_one<T>(a.ec + (long long)(m0 + p + 1) * Pc + cc0, nve, t);   // 2nd coarse row
     };
     auto store_pair = [&](int p, const V2<T> (&px)[R], const V2<T> (&pf)[R], V2<T> pe) {
         if (t < npairs) {
@@ -989,91 +912,11 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                 if constexpr (!GENF) *reinterpret_cast<V2<T> *>(&sf[p & 1][q][2 * t]) = pf[q];
             }
         }
-        if constexpr (L1) {
-            if (p >= 1) l1_store(m0 + p + 7, pe);
-        } else {
-            if (t < ncc) se[ring(m0 + p + 1)][t] = pe.x;
-        }
+        if (t < ncc) se[ring(m0 + p + 1)][t] = pe.x;
     };
-    // L1: one row of each level-1 stage per step g (virtual steps g < 0 fill the pipeline)
-    double acc4 = 0.0;
-    const T hh1 = a.hh1, ih1 = a.ih1;
-    auto l1_stage = [&](int g, bool chk) {
-        if constexpr (PGMG_L1_EXP == 2) {   // keep the level-1 check from firing
-            acc4 = 1.0;
-            return;
-        }
-        constexpr bool MK = PGMG_L1_EXP != 1;
-        {   // x_eff row re
-            const int re = m0 + g + 6;
-            const T *Fm = l1->f[(re - 1) & 7] + 1, *F0 = l1->f[re & 7] + 1, *Fp = l1->f[(re + 1) & 7] + 1;
-            const bool bre = re <= 0 || re >= N1 - 1;
-            const bool bm = re - 1 <= 0 || re - 1 >= N1 - 1, bp = re + 1 <= 0 || re + 1 >= N1 - 1;
-            // J(0) at the four neighbours: 0.25 * ((hh*f) + 0), 0 on the frame (j0stage)
-            auto j0 = [&](T f, bool b) { return (MK && b) ? T(0) : T(0.25) * ((hh1 * f) + T(0)); };
-            const T jl = j0(F0[t - 1], bre || !cinl), jr = j0(F0[t + 1], bre || !cinr);
-            const T ju = j0(Fm[t], bm || !cin), jd = j0(Fp[t], bp || !cin);
-            T v = T(0.25) * ((hh1 * F0[t]) + jl + jr + ju + jd);
-            if (MK && (bre || !cin)) v = T(0);
-            if (!MK || (ccor && re >= 2 && re <= N1 - 2)) {   // + P e2 (add_prolong, one column)
-                const int mm = re >> 1;
-                const T *C0 = l1->e[mm & 7], *C1 = l1->e[(mm + 1) & 7];
-                const T ca = C0[ne];
-                if ((re & 1) == 0) {
-                    v = (lc & 1) == 0 ? v + ca : v + T(0.5) * (ca + C0[ne + 1]);
-                } else {
-                    const T da = C1[ne];
-                    v = (lc & 1) == 0 ? v + T(0.5) * (ca + da)
-                                      : v + T(0.25) * (ca + C0[ne + 1] + da + C1[ne + 1]);
-                }
-            }
-            l1->x[re & 3][t + 1] = v;
-        }
-        {   // x1 row r = J(x_eff)
-            const int r = m0 + g + 4;
-            const T *Xm = l1->x[(r - 1) & 3] + 1, *X0 = l1->x[r & 3] + 1, *Xp = l1->x[(r + 1) & 3] + 1;
-            const T xc = X0[t];
-            T v = T(0.25) * ((hh1 * l1->f[r & 7][t + 1]) + X0[t - 1] + X0[t + 1] + Xm[t] + Xp[t]);
-            if (MK && (r <= 0 || r >= N1 - 1 || !cin)) v = xc;
-            l1->y[r & 3][t + 1] = v;
-        }
-        {   // x2 row r = J(x1) -> the coarse ring; r(x1) on row r
-            const int r = m0 + g + 2;
-            const T *Ym = l1->y[(r - 1) & 3] + 1, *Y0 = l1->y[r & 3] + 1, *Yp = l1->y[(r + 1) & 3] + 1;
-            const T fc = l1->f[r & 7][t + 1];
-            const T yc = Y0[t], yl = Y0[t - 1], yr = Y0[t + 1], yu = Ym[t], yd = Yp[t];
-            T v = T(0.25) * ((hh1 * fc) + yl + yr + yu + yd);
-            if (MK && (r <= 0 || r >= N1 - 1 || !cin)) v = yc;
-            if (t >= 3 && t < 3 + ncc) se[ring(r)][t - 3] = v;
-            if (chk) {
-                const T rs = fc - ih1 * (T(4) * yc - yl - yr - yu - yd);
-                if (own1 && r >= jcb && r < jce && r >= 1) acc4 = sqacc(acc4, rs);
-            }
-        }
-    };
-    V2<T> vq[3];   // L1: the pairs of the virtual steps -3 .. -1 (f1 rows m0+5 .. m0+7)
-    if constexpr (L1) {
-        // f1 rows m0-3 .. m0+4 and e2 rows of x_eff rows m0-2 .. m0+5 straight into LDS
-        T pf[8], pg[6];
-        #pragma unroll
-        for (int q = 0; q < 8; ++q) pf[q] = l1_f(m0 - 3 + q);
-        #pragma unroll
-        for (int q = 0; q < 6; ++q) pg[q] = l1_e(((m0 - 2) >> 1) + q);
-        #pragma unroll
-        for (int q = 0; q < 3; ++q) vq[q] = mk2<T>(l1_f(m0 + 5 + q), l1_e((m0 + 6 + q) >> 1));
-        #pragma unroll
-        for (int q = 0; q < 8; ++q) l1->f[(m0 - 3 + q) & 7][t + 1] = pf[q];
-        if (t < kL1E) {
-            #pragma unroll
-            for (int q = 0; q < 6; ++q) l1->e[(((m0 - 2) >> 1) + q) & 7][t] = pg[q];
-        }
-    }
-    if constexpr (PGMG_PP_PRIO == 1) {
-        if (__builtin_amdgcn_readfirstlane(bk.x + bk.y) & 1) __builtin_amdgcn_s_setprio(1);
-    }
     // prologue: pair 0 (+ its first coarse row) into slot 0; pairs 1 .. D in flight
     load_pair(0, pxA, pfA, peA);
-    if (!L1 && t < ncc) se[ring(m0)][t] = buf_one<T>(a.ec + (long long)m0 * Pc + cc0, nve, t);
+    if (t < ncc) se[ring(m0)][t] = buf_one<T>(a.ec + (long long)m0 * Pc + cc0, nve, t);
     store_pair(0, pxA, pfA, peA);
     if (ng > 1) load_pair(1, pxB, pfB, peB);
     if constexpr (D == 3) {
@@ -1083,14 +926,6 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
         if (ng > 2) load_pair(2, pxA, pfA, peA);
     }
     __syncthreads();
-    if constexpr (L1) {   // virtual steps: x_eff rows m0-2 .., x1 rows m0-1 .., x2 rows m0, m0+1
-        #pragma unroll
-        for (int g = -8; g < 0; ++g) {
-            if (g >= -3) l1_store(m0 + g + 8, vq[g + 3]);   // pairs -2 .. 0
-            l1_stage(g, false);
-            __syncthreads();
-        }
-    }
 
     // pair gi: compute from slot gi & 1; pair gi+1 (set (gi+1) & 1) -> the other slot;
     // issue pair gi+3 into the set just freed; one barrier
@@ -1098,18 +933,13 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     auto step = [&](int gi, V2<T> (&px)[R], V2<T> (&pf)[R], V2<T> &pe) {
         // keep the scheduler inside one pair: interleaving the unrolled pairs only raises
         // the register pressure (the loads of a pair are issued two pairs ahead anyway)
-#ifndef PGMG_PP_NOSCHED   // measurement builds: 1 drops this fence
         __builtin_amdgcn_sched_barrier(0);
-#endif
         const int slot = gi & 1;
         // the other slot's previous readers passed the last barrier: stage pair gi+1 (loaded
         // D steps ago) first and reissue its register set for pair gi+1+D, so the loads in
         // flight are never younger than this step's stores (counted waits stay small)
         if (gi + 1 < ng) store_pair(gi + 1, px, pf, pe);
-        if constexpr (PGMG_PP_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         if (gi + 1 + D < ng) load_pair(gi + 1 + D, px, pf, pe);
-        if constexpr (PGMG_PP_PRIO == 2) __builtin_amdgcn_s_setprio(0);
-        if constexpr (L1) l1_stage(gi, true);
         const int i = i_begin + gi * R;
         const int m = m0 + gi;
         const T *E0 = se[ring(m)], *E1 = se[ring(m + 1)];
@@ -1231,11 +1061,6 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
         const double s3 = fused_block_sum(acc3, red);
         if (threadIdx.x == 0) a.partials3[slot] = s3;
     }
-    if constexpr (L1) {
-        __syncthreads();
-        const double s4 = fused_block_sum(acc4, red);
-        if (threadIdx.x == 0) a.partials4[slot] = s4;
-    }
     if (threadIdx.x == 0) {
         a.partials1[slot] = s1;
         a.partials2[slot] = s2;
@@ -1243,20 +1068,15 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
 }
 
 
-#ifndef PGMG_PP_OCC
-#define PGMG_PP_OCC 2     // waves per SIMD the register allocation must allow
-#endif
+// two waves per SIMD (3 spills and measured slower, r02)
 template <class T, bool R2, bool GENF, int OPT>
-__global__ __launch_bounds__(64 * kPPWaves) __attribute__((amdgpu_waves_per_eu(PGMG_PP_OCC)))
+__global__ __launch_bounds__(64 * kPPWaves) __attribute__((amdgpu_waves_per_eu(2)))
 void k_postpre_lds(PostPreArgsT<T> a)
 {
     __shared__ double red[kPPWaves];
     __shared__ __attribute__((aligned(16))) T sx[2][kPPR][kPPLdsRow];
     __shared__ __attribute__((aligned(16))) T sf[2][kPPR][GENF ? 1 : kPPLdsRow];
     __shared__ __attribute__((aligned(16))) T se[3][kPPLdsCoarse];
-    __shared__ __attribute__((aligned(16))) std::conditional_t<(OPT & 32) != 0, L1Lds<T>, char> l1s;
-    L1Lds<T> *l1 = nullptr;
-    if constexpr ((OPT & 32) != 0) l1 = &l1s;
     const Blk bk{(int)blockIdx.x, (int)blockIdx.y};
     const Cols k = lane_cols_t<kPPStride, kPPMargin>(a.N, bk.x);
     // the band's rows 2jcb-6 .. 2jce+5 (see postpre_lds_run): does it reach row 0 or N-1?
@@ -1264,9 +1084,9 @@ void k_postpre_lds(PostPreArgsT<T> a)
     const int jce = min(jcb + a.rows_per_block, a.jc1);
     const bool edge_rows = 2 * jcb - 6 <= 0 || 2 * jce + 6 >= a.N - 1;
     if (k.edge || edge_rows)
-        postpre_lds_run<T, R2, GENF, true, OPT>(a, k, red, sx, sf, se, l1, bk);
+        postpre_lds_run<T, R2, GENF, true, OPT>(a, k, red, sx, sf, se, bk);
     else
-        postpre_lds_run<T, R2, GENF, false, OPT>(a, k, red, sx, sf, se, l1, bk);
+        postpre_lds_run<T, R2, GENF, false, OPT>(a, k, red, sx, sf, se, bk);
 }
 
 // one block: both decisions, stats, flags for the conditional rare-path kernels
@@ -1426,7 +1246,7 @@ static int pre_spans(const PreArgsT<T> &a, int t, int gx, int r, bool x0_read, b
     const Span sp = band_rows(a.jc0, a.jc1, r, 4, 8, 4);
     const long long chi = tile_col_hi(a.N, gx * (t / 64));
     if (!sp.any || chi < 0) return PGMG_OK;
-    if (x0_read) PGMG_SPAN(a.x0, a.P, sp.r0, sp.r1, -3, chi, "k_pre x0");
+    if (x0_read) PGMG_SPAN(a.x0, a.Px != 0 ? a.Px : a.P, sp.r0, sp.r1, -3, chi, "k_pre x0");
     if (f_read) PGMG_SPAN(a.f, a.P, sp.r0, sp.r1, -3, chi, "k_pre f");
     if (a.pin_ec != nullptr)   // coarse rows i/2 .. i/2 + 2 of every 4-row iteration i
         PGMG_SPAN(a.pin_ec, a.Pc, fdiv2(sp.r0), fdiv2(sp.r1 + 1 - 4) + 2, -2,
@@ -1455,7 +1275,7 @@ static int post_spans(const PostArgsT<T> &a, int t, int gx, int r, bool f_read)
     PGMG_SPAN(a.ec, a.Pc, fdiv2(sp.r0), fdiv2(sp.r1 + 1 - 4) + 2, -2, fdiv2(chi - 2) + 1,
               "k_post coarse correction");
     const int olo = std::max(2 * a.jc0, a.row_lo), ohi = std::min(2 * a.jc1, a.row_hi);
-    if (a.x2 != nullptr) PGMG_SPAN(a.x2, a.P, olo, ohi - 1, 1, a.N - 1, "k_post x2");
+    if (a.x2 != nullptr) PGMG_SPAN(a.x2, a.Po != 0 ? a.Po : a.P, olo, ohi - 1, 1, a.N - 1, "k_post x2");
     return PGMG_OK;
 }
 
@@ -1488,8 +1308,7 @@ static int postpre_spans(const PostPreArgsT<T> &a, int t, int gx, int r, bool co
     if (c1 < c0) return PGMG_OK;
     PGMG_SPAN(a.phi, a.P, sp.r0, sp.r1, c0, c1, "k_postpre phi");
     if (a.gfx == nullptr) PGMG_SPAN(a.f, a.P, sp.r0, sp.r1, c0, c1, "k_postpre f");
-    // (L1: f1 and e2 are read at clamped rows and columns, ec not at all)
-    if (coarse && e1 >= e0 && a.f1 == nullptr)   // coarse rows m0 .. m0 + ng of a band (m0 = jcb - 3)
+    if (coarse && e1 >= e0)   // coarse rows m0 .. m0 + ng of a band (m0 = jcb - 3)
         PGMG_SPAN(a.ec, a.Pc, a.jc0 - 3, fdiv2(sp.r1 + 1), e0, e1, "k_postpre coarse correction");
     const int olo = std::max(2 * a.jc0, a.row_lo), ohi = std::min(2 * a.jc1, a.row_hi);
     PGMG_SPAN(a.x4, a.P, olo, ohi - 1, 1, a.N - 1, "k_postpre x4");
@@ -1596,9 +1415,6 @@ int launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
     if (a.partials3 != nullptr) {
         if (genf) k_postpre_lds<T, true, true, 2><<<g, b, 0, s>>>(a);
         else k_postpre_lds<T, true, false, 2><<<g, b, 0, s>>>(a);
-    } else if (a.f1 != nullptr) {   // level 1's post-smooth inside (PGMG_FLAG_L1POST)
-        if (genf) k_postpre_lds<T, false, true, 2 | 32><<<g, b, 0, s>>>(a);
-        else k_postpre_lds<T, false, false, 2 | 32><<<g, b, 0, s>>>(a);
     } else {
         if (a.fast && sizeof(T) == 8) {   // FAST mode (one GPU, fp64)
             if (genf) k_postpre_lds<T, false, true, 2 | 16><<<g, b, 0, s>>>(a);
@@ -1799,6 +1615,7 @@ struct FixCtx {
     bool x0_zero;
     const unsigned *pre_fired;  // non-null: phi (x0 of fxeff) is recomputed from f
     bool pin;                   // x0 = (+0) + P ec (k_pre PIN, F-cycle)
+    long long Px;               // x0's pitch (0: P; the caller's array: N)
 };
 
 template <class T>
@@ -1808,7 +1625,7 @@ template <class T>
 __device__ __forceinline__ T fx0(const FixCtx<T> &c, int j, int i)
 {
     if (c.pin) return fxpin(c, j, i);
-    return c.x0_zero ? T(0) : c.x0[(long long)j * c.P + i];
+    return c.x0_zero ? T(0) : c.x0[(long long)j * (c.Px != 0 ? c.Px : c.P) + i];
 }
 
 template <bool POST, class T>
@@ -1904,7 +1721,7 @@ __global__ __launch_bounds__(256) void k_pre_fixup(FixArgsF a, PreArgsT<T> p, in
     if (p.fired != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *p.fired = t ? 1u : 0u;
     if (!t) return;
     FixCtx<T> c{p.x0, p.f, p.pin_ec, p.N, p.Nc, p.P, p.Pc, p.hh, p.ih, x0_zero != 0, nullptr,
-                p.pin_ec != nullptr};
+                p.pin_ec != nullptr, p.Px};
     const long long W = p.N - 2;
     const long long nrows = p.x2 != nullptr ? (long long)(p.row_hi - p.row_lo) : 0;
     const long long stride = (long long)gridDim.x * blockDim.x;
@@ -1934,9 +1751,10 @@ __global__ __launch_bounds__(256) void k_post_fixup(FixArgsF a, PostArgsT<T> p)
     const long long W = p.N - 2;
     const long long nrows = (long long)(p.row_hi - p.row_lo);
     const long long stride = (long long)gridDim.x * blockDim.x;
+    const long long Po = p.Po != 0 ? p.Po : p.P;
     for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < nrows * W; k += stride) {
         const int j = p.row_lo + (int)(k / W), i = 1 + (int)(k % W);
-        p.x2[(long long)j * p.P + i] = p.fix_sweeps == 2 ? fx2post(c, j, i) : fx1<true>(c, j, i);
+        p.x2[(long long)j * Po + i] = p.fix_sweeps == 2 ? fx2post(c, j, i) : fx1<true>(c, j, i);
     }
 }
 

@@ -204,6 +204,9 @@ template <class T> void launch_fill_rows(T *o, int P, int row0, int row1, hipStr
 // the rank's rows and halo rows)
 template <class T>
 void launch_zero_frame(T *o, int P, int N, hipStream_t s, int r0 = 0, int r1 = 1 << 30);
+// rows 0, N-1 and columns 0, N-1 of a double grid (pitch Ps) into a T grid (pitch Pd)
+template <class T>
+void launch_copy_frame(const double *src, long long Ps, T *dst, long long Pd, int N, hipStream_t s);
 template <class T>
 void launch_resnorm_partials(const T *x, const T *f, double *partials, T inv_hh, int W, int P,
                              int row0, int row1, int nblocks, hipStream_t s);

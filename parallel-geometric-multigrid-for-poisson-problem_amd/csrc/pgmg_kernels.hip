@@ -651,6 +651,25 @@ void launch_zero_frame(T *o, int P, int N, hipStream_t s, int r0, int r1)
     k_zero_frame<T><<<dim3((n + 255) / 256), dim3(256), 0, s>>>(o, P, N, r0, r1);
 }
 
+// rows 0 and N-1 and columns 0 and N-1 of a double grid (pitch Ps: the caller's array in the
+// reference layout) into a level grid (pitch Pd) — the boundary the passes pass through
+template <class T>
+__global__ void k_copy_frame(const double *src, long long Ps, T *dst, long long Pd, int N)
+{
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < 4 * N; k += gridDim.x * blockDim.x) {
+        const int q = k % N, w = k / N;
+        const int j = w == 0 ? 0 : (w == 1 ? N - 1 : q);
+        const int i = w < 2 ? q : (w == 2 ? 0 : N - 1);
+        dst[(long long)j * Pd + i] = (T)src[(long long)j * Ps + i];
+    }
+}
+
+template <class T>
+void launch_copy_frame(const double *src, long long Ps, T *dst, long long Pd, int N, hipStream_t s)
+{
+    k_copy_frame<T><<<dim3((4 * N + 255) / 256), dim3(256), 0, s>>>(src, Ps, dst, Pd, N);
+}
+
 // sum r(x)^2 over rows [row0,row1), interior columns — reporting only
 template <class T>
 __global__ __launch_bounds__(kBlock) void k_resnorm(const T *x, const T *f, double *partials,
@@ -738,6 +757,7 @@ void launch_from_double(const double *src, int N, T *dst, int P, int row0, int r
     template void launch_restrict2_values<T>(const T *, int, T *, int, int, hipStream_t);            \
     template void launch_fill_rows<T>(T *, int, int, int, hipStream_t);                            \
     template void launch_zero_frame<T>(T *, int, int, hipStream_t, int, int);                      \
+    template void launch_copy_frame<T>(const double *, long long, T *, long long, int, hipStream_t); \
     template void launch_resnorm_partials<T>(const T *, const T *, double *, T, int, int, int, int, \
                                              int, hipStream_t);                                    \
     template void launch_to_double<T>(const T *, int, double *, int, int, int, hipStream_t);      \

@@ -19,6 +19,18 @@ template <class T>
 __device__ __forceinline__ V2<T> ldv(const T *p) { return *reinterpret_cast<const V2<T> *>(p); }
 template <class T>
 __device__ __forceinline__ void stv(T *p, V2<T> v) { *reinterpret_cast<V2<T> *>(p) = v; }
+// the same with only element alignment promised (a column pair of an array with an odd
+// pitch: the caller's reference-layout grid).  gfx950 under ROCm runs in unaligned-access
+// mode, so this is still ONE global_load/store_dwordx4 (dwordx2 for float)
+template <class T>
+__device__ __forceinline__ V2<T> ldvu(const T *p)
+{
+    V2<T> v;
+    __builtin_memcpy(&v, p, sizeof(v));
+    return v;
+}
+template <class T>
+__device__ __forceinline__ void stvu(T *p, V2<T> v) { __builtin_memcpy(p, &v, sizeof(v)); }
 template <class T>
 __device__ __forceinline__ void stv_nt(T *p, V2<T> v)
 {

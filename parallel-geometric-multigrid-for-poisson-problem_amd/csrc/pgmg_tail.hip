@@ -21,29 +21,15 @@ namespace pgmg {
 constexpr int kTailMaxLevels = 8;
 constexpr int kTailWaves = kTailThreads / 64;
 constexpr int kTailRed = 2 * kTailWaves + 2;  // doubles of reduction scratch at the LDS base
-#ifndef PGMG_TAIL_SMALL_OFF
-constexpr bool kTailSmallOff = false;          // (compile with -DPGMG_TAIL_SMALL_OFF for A/B)
-#else
-constexpr bool kTailSmallOff = true;
-#endif
-
-#ifndef PGMG_TAIL_W9
-#define PGMG_TAIL_W9 1   // the 9x9 + 5x5 pair of levels by tail_w9 (0: the generic wave loop)
-#endif
-constexpr bool kTailW9 = PGMG_TAIL_W9 != 0;
-#ifndef PGMG_TAIL_W17
-#define PGMG_TAIL_W17 1  // the 17x17 level and below by tail_w17 on wave 0
-#endif
-constexpr bool kTailW17 = PGMG_TAIL_W17 != 0 && kTailW9;
-#ifndef PGMG_TAIL_W33
-#define PGMG_TAIL_W33 0  // 1: the 33x33 level too (16 points a lane: 256 VGPRs + 512 B of spills; off)
-#endif
-constexpr bool kTailW33 = PGMG_TAIL_W33 != 0 && kTailW17;
-#ifndef PGMG_TAIL_ROWS
-#define PGMG_TAIL_ROWS 1  // block-team smoothing of the 65x65 / 33x33 levels with the iterate
-                          // in registers, one row per lane set (tail_smooth_rows); 0: tail_jacobi
-#endif
-constexpr bool kTailRows = PGMG_TAIL_ROWS != 0;
+// The register-resident paths of the tail (r01/r02; each replaced a generic LDS loop and is
+// bitwise the same): 3x3-interior smoothing on one wave (tail_smooth_small), the 9x9 + 5x5
+// pair by tail_w9, the 17x17 level and below by tail_w17 on wave 0, and the block team's
+// 65x65 / 33x33 smoothing with the iterate in registers (tail_smooth_rows).  The 33x33 level
+// on wave 0 (16 points a lane) spills and was measured slower (r02): not built.
+constexpr bool kTailSmallOff = false;
+constexpr bool kTailW9 = true;
+constexpr bool kTailW17 = true;
+constexpr bool kTailRows = true;
 
 template <class Real>
 struct TailLevel {
@@ -1120,15 +1106,11 @@ __device__ __forceinline__ Cnt tail_gcycle(const TailArgsDev<Real> &d, int top, 
     const int last = d.nl - 1;
     for (;;) {
         if (descending) {
-            const bool w33 = kTailW33 && d.lv[l].N == 33 && l + 3 == last && d.lv[l + 3].N == 5;
             const bool w17 = kTailW17 && d.lv[l].N == 17 && l + 2 == last && d.lv[l + 2].N == 5;
-            if (kBlock && l != top && (w33 || w17)) {
+            if (kBlock && l != top && w17) {
                 // the whole gamma-recursion of this level (and below) on wave 0
                 const unsigned long long c0 = d.prof ? tail_clock() : 0;
-                if (threadIdx.x < 64) {
-                    if (w33) cnt += tail_wq<Real, 33>(d, l, d.gamma, E, F, T);
-                    else cnt += tail_wq<Real, 17>(d, l, d.gamma, E, F, T);
-                }
+                if (threadIdx.x < 64) cnt += tail_wq<Real, 17>(d, l, d.gamma, E, F, T);
                 __syncthreads();
                 if (d.prof && threadIdx.x == 0) d.prof[0] += tail_clock() - c0;
                 vset(l, d.gamma - 1);

@@ -111,6 +111,12 @@ class ParallelTestRunner {
     int mg_max_iterations;
     int num_thread = 32;    // globals.cpp:6; reported in the per-op timing files only
     bool print_hash = false;  // gpu_exec --hash: one "phi FNV-64" line per cycle run
+    // gpu_exec --host-arrays: phi and f in host memory, uploaded / downloaded per cycle (the
+    // reference keeps them in managed memory: ParallelTestRunner.cu:162-163; the default here
+    // is device memory, phi updated in place, f regenerated on the device)
+    bool host_arrays = false;
+    int last_device_mode = -1;   // of the last cycle run: ParallelMultiGridSolver::device_mode
+    int warmup_iterations = 0;   // gpu_exec --warmup: untimed cycles before the timed ones
     std::vector<double> err_vec;
     std::vector<std::tuple<int, int, double>> time_residual_cpu, time_residual_gpu,
         time_jacobi_cpu, time_jacobi_gpu, time_restriction_cpu, time_restriction_gpu,
@@ -172,22 +178,51 @@ class ParallelTestRunner {
     }
 
   private:
+    // ParallelTestRunner.cu:152-228: phi = 0 and f = compute_rhs in device-accessible memory
+    // (the reference: cudaMallocManaged + host initialisation; here pgmg_alloc_grid + the
+    // device's bitwise compute_rhs), mg_max_iterations cycles timed by wall clock, then the
+    // relative L2 error against the analytic solution on the host
     double run_cycle(bool w, bool err_vector)
     {
         const double h = 1.0 / (N - 1);
         const size_t L = (size_t)N * N;
         pgmg_host::Problem pr;
         std::vector<double> phi(L, 0.0), f, x_true;
-        pgmg_host::rhs(f, N, h, pr);
         pgmg_host::exact_solution(x_true, N, h, pr);
         ParallelMultiGridSolver solver(alpha);
-        auto t0 = std::chrono::high_resolution_clock::now();
-        for (int it = 0; it < mg_max_iterations; ++it) {
-            if (w) solver.w_cycle(phi.data(), f.data(), N, h);
-            else solver.v_cycle(phi.data(), f.data(), N, h);
+        double secs = 0.0;
+        if (host_arrays) {
+            pgmg_host::rhs(f, N, h, pr);
+            for (int it = 0; it < warmup_iterations; ++it) {
+                if (w) solver.w_cycle(phi.data(), f.data(), N, h);
+                else solver.v_cycle(phi.data(), f.data(), N, h);
+            }
+            auto t0 = std::chrono::high_resolution_clock::now();
+            for (int it = 0; it < mg_max_iterations; ++it) {
+                if (w) solver.w_cycle(phi.data(), f.data(), N, h);
+                else solver.v_cycle(phi.data(), f.data(), N, h);
+            }
+            auto t1 = std::chrono::high_resolution_clock::now();
+            secs = std::chrono::duration<double>(t1 - t0).count();
+        } else {
+            pgmg_host::DeviceGrid dphi(N), df(N);   // zeroed
+            pgmg_host::check(pgmg_rhs(df.get(), N, N, h, pr.a, pr.p, pr.q, nullptr), "pgmg_rhs");
+            pgmg_host::check(pgmg_device_sync(), "pgmg_device_sync");
+            solver.rhs_is_analytic(df.get());
+            for (int it = 0; it < warmup_iterations; ++it) {
+                if (w) solver.w_cycle(dphi.get(), df.get(), N, h);
+                else solver.v_cycle(dphi.get(), df.get(), N, h);
+            }
+            auto t0 = std::chrono::high_resolution_clock::now();
+            for (int it = 0; it < mg_max_iterations; ++it) {
+                if (w) solver.w_cycle(dphi.get(), df.get(), N, h);
+                else solver.v_cycle(dphi.get(), df.get(), N, h);
+            }
+            auto t1 = std::chrono::high_resolution_clock::now();
+            secs = std::chrono::duration<double>(t1 - t0).count();
+            dphi.download(phi.data());
         }
-        auto t1 = std::chrono::high_resolution_clock::now();
-        const double secs = std::chrono::duration<double>(t1 - t0).count();
+        last_device_mode = solver.device_mode();
         if (err_vector) {   // ParallelTestRunner.cu:207-214
             err_vec.resize(L);
             for (size_t k = 0; k < L; ++k) err_vec[k] = phi[k] - x_true[k];
@@ -199,6 +234,10 @@ class ParallelTestRunner {
             char buf[32];
             std::snprintf(buf, sizeof(buf), "%016llx", pgmg_host::fnv64(phi));
             std::cout << "  phi FNV-64: " << buf << "\n";
+            std::cout << "  phi arrays: "
+                      << (last_device_mode == 1 ? "device, in place"
+                                                : last_device_mode == 0 ? "device, staged" : "host")
+                      << "\n";
         }
         return secs;
     }

@@ -43,6 +43,39 @@ class DeviceArray {
     size_t n_ = 0;
 };
 
+// RAII N x N device grid in the reference layout (pitch N) with guard rows
+// (pgmg_alloc_grid): the stand-in for the reference's cudaMallocManaged phi and f
+// (ParallelTestRunner.cu:162-163).  The library's finest-level passes read and write such a
+// phi in place (pgmg_set_problem_device); the host reaches it through upload / download.
+class DeviceGrid {
+  public:
+    explicit DeviceGrid(int N) : N_(N)
+    {
+        check(pgmg_alloc_grid(&p_, N), "pgmg_alloc_grid");
+    }
+    ~DeviceGrid()
+    {
+        if (p_) pgmg_free_grid(p_);
+    }
+    DeviceGrid(const DeviceGrid &) = delete;
+    DeviceGrid &operator=(const DeviceGrid &) = delete;
+    double *get() const { return p_; }
+    size_t size() const { return (size_t)N_ * N_; }
+    void upload(const double *h) { check(pgmg_memcpy_h2d(p_, h, size() * sizeof(double)), "h2d"); }
+    void download(double *h) const { check(pgmg_memcpy_d2h(h, p_, size() * sizeof(double)), "d2h"); }
+
+  private:
+    double *p_ = nullptr;
+    int N_ = 0;
+};
+
+inline bool is_device_pointer(const void *p)
+{
+    int d = 0;
+    check(pgmg_pointer_is_device(p, &d), "pgmg_pointer_is_device");
+    return d != 0;
+}
+
 // RAII multigrid context
 class Context {
   public:

@@ -33,6 +33,8 @@ for s in $STEPS; do
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 10 --warmup 2 --cpu-baseline off ;;
     pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline off
          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline off ;;
+    bench-quick) run bench_quick 500 python bench.py --steps 20 --warmup 3 --other-configs off --fast-mode off --general-rhs off --pmc off --cpu-baseline off ;;
+    t=*) f=${s#t=}; run "t_$(echo "$f" | tr ',/.' '___')" 900 python -u -m pytest ${f//,/ } -m gpu -v -rf --timeout 300 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -36,8 +36,8 @@ def test_gpu_exec_matches_reference(tmp_path, golden_cycles):
         w = _golden_relerr(golden_cycles, kind, N, 3)
         assert float(f"{w:.6g}") == got, (got, w)   # std::cout default precision
     for got, (kind, N) in zip(hashes, cases):
-        # the whole mirror path (host arrays, per-call upload/download, the cached context,
-        # W through ParallelMultiGridSolver::w_cycle) bitwise equal to the reference
+        # the whole mirror path (device arrays bound to the cached context -- staged below
+        # N = 2049 --, W through ParallelMultiGridSolver::w_cycle) bitwise the reference
         assert got == _golden_hash(golden_cycles, kind, N, 3), (kind, N)
     for name in ("timings_parallel_v_cycle.txt", "timings_parallel_w_cycle.txt"):
         rows = (tmp_path / "OUTPUT_RESULT" / name).read_text().split("\n")
@@ -93,3 +93,46 @@ def test_mirror_honours_h(pgmg, oracle_mod):
         sweeps, _ = s.stats()
     assert_bitwise(got, ref, "V-cycles with h0")
     assert sweeps == o.sweeps
+
+
+REF_EXE = ROOT / "oracle" / "_ref" / "gpu_exec_ref"
+
+
+@pytest.mark.skipif(not REF_EXE.exists(), reason="oracle/_ref/gpu_exec_ref not built "
+                    "(make -C oracle ref, in a container with the reference tree)")
+def test_reference_main_on_mirror(tmp_path, golden_cycles):
+    """The reference's OWN gpu_exec main (3_part_parallel/main.cu with INTEGRATION.md's two
+    edits, built by oracle/ref_gpu_exec.sh against host/ and libpgmg.so): its default run
+    (N = 33 ... 2049, 3 V- then 3 W-cycles per N, alpha = 3) on the MI355X prints the
+    reference's errors (every golden there is) and writes its timing files."""
+    out = subprocess.run([str(REF_EXE)], cwd=tmp_path, capture_output=True, text=True,
+                         timeout=600, check=True).stdout
+    errs = [float(x) for x in re.findall(r"Final Relative L2 Error: (\S+)", out)]
+    Ns = [33, 65, 129, 257, 513, 1025, 2049]
+    assert len(errs) == 2 * len(Ns), out
+    checked = 0
+    for i, N in enumerate(Ns):
+        for j, kind in enumerate(("V", "W")):
+            c = next((c for c in golden_cycles if c["kind"] == kind and c["N"] == N
+                      and c["eps"] == 1e-7 and len(c["cycles"]) >= 3), None)
+            if c is None:
+                continue
+            assert float(f"{c['cycles'][2]['relerr']:.6g}") == errs[2 * i + j], (kind, N)
+            checked += 1
+    assert checked >= 7
+    for name in ("timings_parallel_v_cycle.txt", "timings_parallel_w_cycle.txt"):
+        rows = (tmp_path / "OUTPUT_RESULT" / name).read_text().split("\n")
+        assert [int(r.split()[0]) for r in rows if r] == Ns
+
+
+@pytest.mark.parametrize("args", [["--n", "2049", "--cycles", "2", "--v-only"],
+                                  ["--n", "129", "--cycles", "3", "--v-only", "--host-arrays"]])
+def test_gpu_exec_array_modes(tmp_path, golden_cycles, args):
+    """The mirror's v_cycle on device arrays in place (N = 2049: cross-fused) and on host
+    arrays (--host-arrays): both the reference's hash."""
+    out = subprocess.run([str(EXE), "--hash"] + args, cwd=tmp_path, capture_output=True,
+                         text=True, timeout=300, check=True).stdout
+    N, k = int(args[1]), int(args[3])
+    mode = re.findall(r"phi arrays: (.+)", out)[0].strip()
+    assert mode == ("host" if "--host-arrays" in args else "device, in place"), mode
+    assert re.findall(r"phi FNV-64: ([0-9a-f]{16})", out)[0] == _golden_hash(golden_cycles, "V", N, k)

@@ -81,13 +81,6 @@ def test_robust_rhs_strips(pgmg, oracle_mod):
         assert_bitwise(out[r], ref, f"mt64 RHS strips rank {r}")
 
 
-def test_robust_rhs_l1post(pgmg, oracle_mod):
-    f, ref, sw = _oracle(oracle_mod, 2049, [4])
-    got, gsw = _gpu(pgmg, 2049, f, [4], flags=pgmg.PGMG_FLAG_L1POST)
-    assert_bitwise(got, ref, "mt64 RHS L1POST")
-    assert gsw == sw
-
-
 @pytest.mark.parametrize("N", [2049, 4097])
 def test_robust_rhs_fast_tolerance(pgmg, oracle_mod, N):
     """FAST mode on a rough RHS: the same tolerance against the exact default as on the
