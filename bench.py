@@ -120,11 +120,13 @@ def cpu_baseline(n, cycles=1, kind="V", skip=0):
     t = statistics.median(secs[skip:])
     src = ("the reference's MultigridSolver (2_part_MG/MultiGrid.hpp) via oracle/_ref/ref_harness"
            if what == "reference" else "oracle/mg_cpu_exec_port (our C restatement)")
-    timed = len(secs) - skip
+    timed = secs[skip:]
     return {"value": round(1.0 / t, 6), "unit": f"{kind}-cycles/s", "cores": 1, "kind": what,
+            "N": n, "s_per_cycle": [round(x, 5) for x in timed],
+            "spread_pct": round(100 * (max(timed) - min(timed)) / t, 2) if len(timed) > 1 else None,
             "sample": f"{kind}-cycles at N={n} from phi0=0, analytic f: {skip} warmup + median of "
-                      f"{timed} timed; {src}, g++/gcc -O2 single thread (taskset -c 0); "
-                      f"{t:.4f} s per {kind}-cycle; host {_cpu_model()}"}
+                      f"{len(timed)} timed; {src}, g++/gcc -O2 single thread (taskset -c 0); "
+                      f"{t:.4f} s per {kind}-cycle; host {_cpu_model()}, {os.cpu_count()} CPUs"}
 
 
 def lib_build_id():
@@ -240,18 +242,24 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # CPU baselines first, before this process touches the GPU (child processes)
-    cpu = cpu1 = None
+    cpu = cpu1 = cpu4 = None
     if world == 1 and rank == 0 and args.cpu_baseline == "auto" and args.dtype == "f64":
         try:
             cpu = cpu_baseline(args.cpu_n or args.n, kind=args.cycle)
         except Exception as e:  # reported, not fatal
             cpu = {"value": None, "unit": f"{args.cycle}-cycles/s", "cores": 1, "kind": "port",
                    "sample": f"failed: {e}"}
-        try:   # BASELINE config 1: mg_cpu_exec's own size, N = 513 (1 warmup + median of 3)
-            cpu1 = cpu_baseline(513, cycles=4, kind="V", skip=1)
+        try:   # BASELINE config 1: mg_cpu_exec's own size, N = 513 (1 warmup + median of 5)
+            cpu1 = cpu_baseline(513, cycles=6, kind="V", skip=1)
         except Exception as e:
             cpu1 = {"value": None, "unit": "V-cycles/s", "cores": 1, "kind": "port",
                     "sample": f"failed: {e}"}
+        if args.cycle == "V" and args.n != 4097:
+            try:   # BASELINE.md §2's middle size, N = 4097 (1 warmup + median of 3, ~5 s)
+                cpu4 = cpu_baseline(4097, cycles=4, kind="V", skip=1)
+            except Exception as e:
+                cpu4 = {"value": None, "unit": "V-cycles/s", "cores": 1, "kind": "port",
+                        "sample": f"failed: {e}"}
     pmc, pmc_note = None, "off"
     if world == 1 and rank == 0 and args.pmc == "auto":
         pmc, pmc_note = live_pmc(args)
@@ -587,6 +595,11 @@ def main():
                                    "in_stream_level_mask": spec_mask},
             "cpu_baseline": cpu,
             "cpu_baseline_config1": cpu1,
+            "cpu_baseline_4097": cpu4,
+            # the host the CPU samples ran on: every sample uses ONE core (taskset -c 0); the
+            # reference CPU rate moves ~2x from host to host of the pool, so
+            # each sample carries its per-cycle times and their spread
+            "cpu_host": {"model": _cpu_model(), "nproc": os.cpu_count(), "cores_used": 1},
             "pmc": pmc_note,
             "build": lib_build_id(),
         }

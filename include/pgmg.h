@@ -311,6 +311,12 @@ int pgmg_residual(double *d_r, const double *d_x, const double *d_f, int H, int 
                   void *stream);
 int pgmg_restrict(const double *d_fine, double *d_coarse, int Nf, int Nc, void *stream);
 int pgmg_prolong(const double *d_coarse, double *d_fine, int Nc, int Nf, int mode, void *stream);
+/* The same with the reference's thread grid (Parallel::ComputeProlungator,
+ * Parallel_Method.cu:188-199): only fine rows and columns below max(1, Nf / num_thread) *
+ * num_thread are touched -- for Nf = 2^k + 1 > num_thread the last fine row and column keep
+ * their values, as in the reference.  num_thread = 0: the whole grid (pgmg_prolong). */
+int pgmg_prolong_grid(const double *d_coarse, double *d_fine, int Nc, int Nf, int mode,
+                      int num_thread, void *stream);
 int pgmg_norm(const double *d_v, long long n, double *result, void *stream);
 int pgmg_rhs(double *d_f, int W, int H, double h, double a, double p, double q, void *stream);
 

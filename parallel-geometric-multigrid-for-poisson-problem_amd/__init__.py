@@ -405,9 +405,12 @@ class _Ops:
         check(load().pgmg_restrict(self._ptr(fine), self._ptr(coarse), fine.shape[0],
                                    coarse.shape[0], stream), "pgmg_restrict")
 
-    def prolong(self, coarse, fine, mode=PGMG_PROLONG_REFERENCE, stream=None):
-        check(load().pgmg_prolong(self._ptr(coarse), self._ptr(fine), coarse.shape[0],
-                                  fine.shape[0], int(mode), stream), "pgmg_prolong")
+    def prolong(self, coarse, fine, mode=PGMG_PROLONG_REFERENCE, num_thread=0, stream=None):
+        """num_thread > 0: the reference's launch grid (max(1, Nf // num_thread) *
+        num_thread rows and columns touched, Parallel_Method.cu:191-197); 0: all of it."""
+        check(load().pgmg_prolong_grid(self._ptr(coarse), self._ptr(fine), coarse.shape[0],
+                                       fine.shape[0], int(mode), int(num_thread), stream),
+              "pgmg_prolong_grid")
 
     def norm(self, v, stream=None):
         out = C.c_double()

@@ -123,6 +123,7 @@ SIGNATURES = [
     ("pgmg_residual", C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_double, _P]),
     ("pgmg_restrict", C.c_int, [_P, _P, C.c_int, C.c_int, _P]),
     ("pgmg_prolong", C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, _P]),
+    ("pgmg_prolong_grid", C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P]),
     ("pgmg_norm", C.c_int, [_P, C.c_longlong, _DP, _P]),
     ("pgmg_rhs", C.c_int, [_P, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, C.c_double,
                            _P]),

@@ -162,16 +162,21 @@ void launch_g_restrict(const double *fine, double *coarse, int Nf, int Nc, hipSt
 }
 
 // mode 0: MultiGrid.hpp:208-226 (fine row/col 1 uncorrected);
-// mode 1: prolungator_kernel, Parallel_Method.cu:79-138 (symmetric, boundary := 0)
-__global__ void k_g_prolong(const double *C, double *Fn, int Nc, int Nf, int mode)
+// mode 1: prolungator_kernel, Parallel_Method.cu:79-138 (symmetric, boundary := 0).
+// Only fine points (y, x) with y, x < ext are touched: the reference's thread grid
+// (ComputeProlungator, Parallel_Method.cu:191-197) covers max(1, Nf / num_thread) * num_thread
+// rows and columns, so for Nf = 2^k + 1 its last fine row and column are never written.
+__global__ void k_g_prolong(const double *C, double *Fn, int Nc, int Nf, int mode, int ext)
 {
-    const long long n = (long long)Nf * Nf;
+    const int E = ext < Nf ? ext : Nf;
+    const long long n = (long long)E * E;
     for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n;
          k += (long long)gridDim.x * blockDim.x) {
-        const int y = (int)(k / Nf), x = (int)(k % Nf);
+        const int y = (int)(k / E), x = (int)(k % E);
+        const long long kk = (long long)y * Nf + x;
         if (mode == 1) {
             if (y == 0 || y == Nf - 1 || x == 0 || x == Nf - 1) {
-                Fn[k] = 0.0;
+                Fn[kk] = 0.0;
                 continue;
             }
             const int cx = x / 2, cy = y / 2;
@@ -186,7 +191,7 @@ __global__ void k_g_prolong(const double *C, double *Fn, int Nc, int Nf, int mod
             } else {
                 if (cy + 1 < Nc) v = 0.5 * (C[c] + C[c + Nc]);
             }
-            Fn[k] += v;
+            Fn[kk] += v;
         } else {
             if (x < 2 || y < 2 || x > Nf - 2 || y > Nf - 2) continue;
             const long long jc = y >> 1, ic = x >> 1;
@@ -199,16 +204,17 @@ __global__ void k_g_prolong(const double *C, double *Fn, int Nc, int Nf, int mod
                 v = ((x & 1) == 0) ? 0.5 * (C0[ic] + C1[ic])
                                    : 0.25 * (C0[ic] + C0[ic + 1] + C1[ic] + C1[ic + 1]);
             }
-            Fn[k] = Fn[k] + v;
+            Fn[kk] = Fn[kk] + v;
         }
     }
 }
 
-void launch_g_prolong(const double *coarse, double *fine, int Nc, int Nf, int mode, hipStream_t s)
+void launch_g_prolong(const double *coarse, double *fine, int Nc, int Nf, int mode, int ext,
+                      hipStream_t s)
 {
     long long nb = ((long long)Nf * Nf + 255) / 256;
     if (nb > 4096) nb = 4096;
-    k_g_prolong<<<dim3((unsigned)nb), dim3(256), 0, s>>>(coarse, fine, Nc, Nf, mode);
+    k_g_prolong<<<dim3((unsigned)nb), dim3(256), 0, s>>>(coarse, fine, Nc, Nf, mode, ext);
 }
 
 __global__ __launch_bounds__(kBlock) void k_g_sumsq(const double *v, long long n, double *partials)

@@ -229,7 +229,8 @@ void launch_g_copy(const double *src, double *dst, long long n, hipStream_t s);
 void launch_g_residual(double *r, const double *x, const double *f, double inv_hh, int H, int W,
                        hipStream_t s);
 void launch_g_restrict(const double *fine, double *coarse, int Nf, int Nc, hipStream_t s);
-void launch_g_prolong(const double *coarse, double *fine, int Nc, int Nf, int mode, hipStream_t s);
+void launch_g_prolong(const double *coarse, double *fine, int Nc, int Nf, int mode, int ext,
+                      hipStream_t s);
 void launch_g_sumsq(const double *v, long long n, double *partials, int nblocks, hipStream_t s);
 void launch_g_rhs(double *f, const double *sx, const double *sy, double factor, int W, int H,
                   hipStream_t s);

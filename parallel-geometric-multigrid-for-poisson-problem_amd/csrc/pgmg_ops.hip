@@ -9,6 +9,8 @@
 // JacobiSmoother::smooth bit for bit.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <cmath>
 #include <map>
 #include <mutex>
@@ -126,9 +128,18 @@ int pgmg_restrict(const double *d_fine, double *d_coarse, int Nf, int Nc, void *
 
 int pgmg_prolong(const double *d_coarse, double *d_fine, int Nc, int Nf, int mode, void *stream)
 {
-    if (!d_fine || !d_coarse || Nc < 3 || Nf != 2 * Nc - 1 || (mode != 0 && mode != 1))
-        return set_err(PGMG_ERR_ARG, "pgmg_prolong: need Nf == 2*Nc - 1, mode 0|1");
-    launch_g_prolong(d_coarse, d_fine, Nc, Nf, mode, (hipStream_t)stream);
+    return pgmg_prolong_grid(d_coarse, d_fine, Nc, Nf, mode, 0, stream);
+}
+
+int pgmg_prolong_grid(const double *d_coarse, double *d_fine, int Nc, int Nf, int mode,
+                      int num_thread, void *stream)
+{
+    if (!d_fine || !d_coarse || Nc < 3 || Nf != 2 * Nc - 1 || (mode != 0 && mode != 1) ||
+        num_thread < 0)
+        return set_err(PGMG_ERR_ARG, "pgmg_prolong: need Nf == 2*Nc - 1, mode 0|1, num_thread >= 0");
+    // ComputeProlungator's launch: max(1, fine_N / num_thread) blocks of num_thread per side
+    const int ext = num_thread > 0 ? std::max(1, Nf / num_thread) * num_thread : Nf;
+    launch_g_prolong(d_coarse, d_fine, Nc, Nf, mode, ext, (hipStream_t)stream);
     HIPC(hipGetLastError());
     return PGMG_OK;
 }

@@ -160,6 +160,7 @@ class ParallelTestRunner {
     {
         for (int nt : N_thread_list) {
             num_thread = nt;
+            Parallel::num_thread = nt;   // ParallelTestRunner.cu:102 rewrites the global
             for (int n : N_list) {
                 std::cout << "\t\tN: " << n << std::endl;
                 N = n;

@@ -14,6 +14,12 @@
 
 class Parallel {
   public:
+    // the CUDA block edge of the reference's launches (globals.cpp:6, rewritten by
+    // plotTimeSequentialVsParallel, ParallelTestRunner.cu:102); ComputeProlungator's thread
+    // grid depends on it (a class member here: the reference's global `num_thread` lives in
+    // its globals.cpp, which a program may link beside this header)
+    static inline int num_thread = 32;
+
     // Parallel_Method.cu:144-160: v+1 Jacobi sweeps of d_x with right-hand side d_f
     static void ComputeJacobi(double *d_x, double *d_f, int height, int weight, double h_act, int v)
     {
@@ -41,11 +47,13 @@ class Parallel {
     }
 
     // Parallel_Method.cu:188-199: fine += P coarse, the GPU reference's symmetric
-    // bilinear prolongation with the fine boundary set to 0
+    // bilinear prolongation with the fine boundary set to 0, over the reference's thread
+    // grid (max(1, fine_N / num_thread) blocks of num_thread per side: for fine_N = 2^k + 1
+    // the last row and column are left as they are)
     static void ComputeProlungator(double *coarse, double *fine, int coarse_N, int fine_N)
     {
-        pgmg_host::check(pgmg_prolong(coarse, fine, coarse_N, fine_N, PGMG_PROLONG_SYMMETRIC,
-                                      nullptr),
+        pgmg_host::check(pgmg_prolong_grid(coarse, fine, coarse_N, fine_N, PGMG_PROLONG_SYMMETRIC,
+                                           num_thread, nullptr),
                          "ComputeProlungator");
         pgmg_host::check(pgmg_device_sync(), "ComputeProlungator sync");
     }

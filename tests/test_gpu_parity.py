@@ -298,3 +298,25 @@ def test_vcycle_32769_oracle_hash(pgmg, oracle_mod):
         phi = s.solution()
         assert s.stats()[0] == 63
     assert oracle_mod.fnv_hash(phi) == "034c7979d0b231c7"
+
+
+@pytest.mark.parametrize("N,nt", [(33, 32), (33, 16), (129, 32), (1025, 32), (1025, 16), (9, 32)])
+def test_symmetric_prolongation_launch_grid(pgmg, oracle_mod, N, nt):
+    """Parallel::ComputeProlungator's thread grid (Parallel_Method.cu:191-197: max(1, N /
+    num_thread) blocks of num_thread per side): for N = 2^k + 1 > num_thread the last fine
+    row and column are never written.  pgmg_prolong_grid(..., num_thread) is bitwise the
+    oracle's orc_prolong_sym with that extent on random grids whose last row/column are
+    non-zero (N = 9 < 32: one block covers everything)."""
+    import torch
+    rng = np.random.default_rng(2000 + N + nt)
+    Nc = (N - 1) // 2 + 1
+    c = rng.standard_normal((Nc, Nc))
+    f = rng.standard_normal((N, N))
+    ct = torch.tensor(c, device="cuda:0")
+    ft = torch.tensor(f, device="cuda:0")
+    pgmg.ops.prolong(ct, ft, mode=pgmg.PGMG_PROLONG_SYMMETRIC, num_thread=nt)
+    torch.cuda.synchronize()
+    got = ft.cpu().numpy()
+    assert_bitwise(got, oracle_mod.prolong_sym(f, c, num_thread=nt), f"prolong_sym N={N} nt={nt}")
+    if N > nt:
+        assert np.array_equal(got[-1, :], f[-1, :]) and np.array_equal(got[:, -1], f[:, -1])
