@@ -193,103 +193,6 @@ __device__ __forceinline__ void row_loop(int i_begin, int i_end, const FullAt &f
     }
 }
 
-// Lane t's 16-byte (fp32: 8-byte) column pair of a row segment starting at `base`; lanes
-// t >= n read 0 (descriptor range check).  The descriptor is built from wave-uniform values.
-template <class T, int NT>
-__device__ __forceinline__ V2<T> buf_row(const T *base, int n, int t)
-{
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<T *>(base), (short)0, n * (int)sizeof(V2<T>), 0x00020000);
-    if constexpr (sizeof(T) == 8) {
-        return __builtin_bit_cast(V2<T>, __builtin_amdgcn_raw_buffer_load_b128(
-                                             r, t * 16, 0, NT ? 2 : 0));
-    } else {
-        return __builtin_bit_cast(V2<T>, __builtin_amdgcn_raw_buffer_load_b64(
-                                             r, t * 8, 0, NT ? 2 : 0));
-    }
-}
-template <class T, int NT>
-__device__ __forceinline__ void buf_store_row(T *base, int bytes, int off, V2<T> v)
-{
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, bytes, 0x00020000);
-    if constexpr (sizeof(T) == 8) {
-        typedef unsigned u4 __attribute__((ext_vector_type(4)));
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, off, 0, NT ? 2 : 0);
-    } else {
-        typedef unsigned u2 __attribute__((ext_vector_type(2)));
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, off, 0, NT ? 2 : 0);
-    }
-}
-template <class T>
-__device__ __forceinline__ void buf_store_one(T *base, int bytes, int off, T v)
-{
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, bytes, 0x00020000);
-    if constexpr (sizeof(T) == 8) {
-        typedef unsigned u2 __attribute__((ext_vector_type(2)));
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, off, 0, 0);
-    } else {
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
-    }
-}
-template <class T>
-__device__ __forceinline__ T buf_one(const T *base, int n, int t)
-{
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<T *>(base), (short)0, n * (int)sizeof(T), 0x00020000);
-    if constexpr (sizeof(T) == 8)
-        return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, t * 8, 0, 0));
-    else
-        return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, t * 4, 0, 0));
-}
-
-// ---------------------------------------------------------------------------
-// LDS-staged rows for k_pre / k_post on the bulk coarse levels (LDS = true).  The four wave
-// tiles of a block overlap by 8 columns (each loads 128 columns and owns 120), so streaming
-// every tile from HBM reads 6.7 % of the columns twice.  With LDS staging the block's 256
-// lanes load its 488-column window once per row (one 16-byte buffer load per lane: pair t of
-// the window, lanes past the grid's last column read 0 through the descriptor's range
-// check), park the iteration's rows in one of two LDS slots, and each wave reads its
-// 128-column window from there: one barrier per iteration of R rows, the next iteration's
-// rows in flight in registers meanwhile.  Every wave of the block runs every iteration (the
-// barriers must match), idle waves storing nothing.  Used where the block has four waves
-// (N >= 2049) and the streamed array is f (x0 = 0, not the F-cycle's PIN / generated f).
-// ---------------------------------------------------------------------------
-constexpr int kLdsRow = 512;   // doubles per staged row: 256 lanes x one pair (488 used)
-
-template <class T, int R>
-struct RowStage {
-    T *s;            // [2][R][kLdsRow]
-    const T *base;   // the streamed array's element (0, L0) of the block window
-    long long P;
-    int n;           // column pairs of the window inside the grid
-    int xo;          // this lane's window offset in a staged row
-    __device__ __forceinline__ V2<T> load(int row) const
-    {
-        return buf_row<T, 0>(base + (long long)row * P, n, threadIdx.x);
-    }
-    __device__ __forceinline__ void put(int slot, int q, V2<T> v) const
-    {
-        *reinterpret_cast<V2<T> *>(&s[(slot * R + q) * kLdsRow + 2 * threadIdx.x]) = v;
-    }
-    __device__ __forceinline__ V2<T> get(int slot, int q) const
-    {
-        return ldv(&s[(slot * R + q) * kLdsRow + xo]);
-    }
-};
-
-template <class T, int R>
-__device__ __forceinline__ RowStage<T, R> row_stage(T *lds, const T *arr, long long P, int N, int bx)
-{
-    RowStage<T, R> st;
-    const int L0 = 480 * bx - 3;   // lane 0 of wave 0 (lane_cols: 120 w + 1 - 4 + 2 lane)
-    st.s = lds;
-    st.base = arr + L0;
-    st.P = P;
-    st.n = max(0, min((int)blockDim.x, (N - 1 - L0) / 2 + 1));
-    st.xo = 120 * (int)(threadIdx.x >> 6) + 2 * (int)(threadIdx.x & 63);
-    return st;
-}
-
 // ---------------------------------------------------------------------------
 // k_pre
 // ---------------------------------------------------------------------------
@@ -299,11 +202,10 @@ __device__ __forceinline__ RowStage<T, R> row_stage(T *lds, const T *arr, long l
 // S1 (rare path of an in-stream check, k_pre_rare): the check after the first sweep fired,
 // so the pass is redone with ONE sweep — x1 stored instead of x2, rc = R r(x1) — and
 // writes no partial sums and no sweep count (the decision kernel's job)
-template <class T, bool X0_ZERO, bool FINE, int PAIRS, bool GENF, bool PIN, bool S1, bool LDS = false>
-__device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red, T *lds = nullptr)
+template <class T, bool X0_ZERO, bool FINE, int PAIRS, bool GENF, bool PIN, bool S1>
+__device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red)
 {
     constexpr int R = 2 * PAIRS;  // rows loaded per iteration (and prefetched ahead)
-    static_assert(!LDS || (X0_ZERO && !GENF && !PIN && !S1), "LDS staging streams f only");
     if (a.cond != nullptr && *a.cond == 0u) return;  // conditional (rare-path) launch
     int lbx, lby;
     fused_block(lbx, lby);
@@ -340,11 +242,9 @@ __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red, T *l
     // wave-uniform: no lane has a boundary column and every prolongation column pair is
     // corrected (c0 >= 3, c0 + 127 <= N - 3)
     const bool inner = c0w >= 3 && c0w + 127 <= N - 3;
-    const int i_end = (idle && !LDS) ? i_begin
-                                     : i_begin + ((2 * (jce - jcb) + 8 + R - 1) / R) * R;
+    const int i_end = idle ? i_begin
+                           : i_begin + ((2 * (jce - jcb) + 8 + R - 1) / R) * R;
     V2<T> nx[R], nf[R];
-    RowStage<T, R> st{};
-    if constexpr (LDS) st = row_stage<T, R>(lds, a.f, P, N, lbx);
     // PIN: coarse rows (i >> 1) .. (i >> 1) + PAIRS of an iteration starting at row i
     ProlongCols pc;
     pc.ic = (k.c - 1) >> 1;
@@ -359,8 +259,7 @@ __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red, T *l
     #pragma unroll
     for (int q = 0; q < R; ++q) {
         nx[q] = (X0_ZERO || PIN || idle) ? z : ldvu(X + (i_begin + q) * Px);
-        if constexpr (LDS) nf[q] = st.load(i_begin + q);
-        else if constexpr (!GENF) nf[q] = idle ? z : ldv(F + (i_begin + q) * P);
+        if constexpr (!GENF) nf[q] = idle ? z : ldv(F + (i_begin + q) * P);
     }
     if constexpr (PIN) {
         #pragma unroll
@@ -381,25 +280,10 @@ __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red, T *l
     auto iter = [&](int i, auto full_t) {
         V2<T> cx[R], cf[R];
         T cr[PAIRS + 1], crn[PAIRS + 1];
-        if constexpr (LDS) {   // stage this iteration's rows, prefetch the next, one barrier
-            const int slot = ((i - i_begin) / R) & 1;
-            #pragma unroll
-            for (int q = 0; q < R; ++q) st.put(slot, q, nf[q]);
-            if (i + R < i_end) {
-                #pragma unroll
-                for (int q = 0; q < R; ++q) nf[q] = st.load(i + R + q);
-            }
-            __syncthreads();
-            #pragma unroll
-            for (int q = 0; q < R; ++q) {
-                cf[q] = st.get(slot, q);
-                cx[q] = z;
-            }
-        }
         #pragma unroll
         for (int q = 0; q < R; ++q) {
-            if constexpr (!LDS) cx[q] = nx[q];
-            if constexpr (!GENF && !LDS) cf[q] = nf[q];
+            cx[q] = nx[q];
+            if constexpr (!GENF) cf[q] = nf[q];
         }
         if constexpr (PIN) {
             #pragma unroll
@@ -408,11 +292,11 @@ __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red, T *l
                 crn[q] = ncrn[q];
             }
         }
-        if (!LDS && i + R < i_end) {  // prefetch the next R rows
+        if (i + R < i_end) {  // prefetch the next R rows
             #pragma unroll
             for (int q = 0; q < R; ++q) {
                 if (!X0_ZERO && !PIN) nx[q] = ldvu(X + (i + R + q) * Px);
-                if constexpr (!GENF && !LDS) nf[q] = ldv(F + (i + R + q) * P);
+                if constexpr (!GENF) nf[q] = ldv(F + (i + R + q) * P);
             }
             if constexpr (PIN) {
                 #pragma unroll
@@ -532,15 +416,6 @@ __global__ __launch_bounds__(256) void k_pre(PreArgsT<T> a)
     pre_body<T, X0_ZERO, FINE, PAIRS, GENF, PIN, false>(a, red);
 }
 
-// the bulk coarse levels' k_pre (x0 = 0) with LDS-staged f rows
-template <class T, int PAIRS>
-__global__ __launch_bounds__(256) void k_pre_lds(PreArgsT<T> a)
-{
-    __shared__ double red[4];
-    __shared__ __attribute__((aligned(16))) T lds[2 * 2 * PAIRS * kLdsRow];
-    pre_body<T, true, false, PAIRS, false, false, false, true>(a, red, lds);
-}
-
 // Decision of an in-stream early-exit check from the partial sums of the pass just run
 // (every block re-reduces them in the same order; a row strip's all-rank sum comes in
 // f.global_sum); block (0,0) books the exit.  Blocks that find it did not fire return.
@@ -583,11 +458,10 @@ __global__ __launch_bounds__(256) void k_pre_rare(PreArgsT<T> a, FixArgsF f)
 // RECOMP (levels entered with x0 = 0): phi is not read.  The loaded row is f[ii+1];
 // x1 = J(0) is pointwise, so x1 row ii+1 -> phi row ii = J(x1) (or x1 when the pre
 // check fired) -> x_eff row ii: one more row of lag than reading phi, 16 B/point less.
-template <class T, bool FINE, int PAIRS, bool RECOMP, bool GENF, bool S1, bool LDS = false>
-__device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red, T *lds = nullptr)
+template <class T, bool FINE, int PAIRS, bool RECOMP, bool GENF, bool S1>
+__device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
 {
     constexpr int R = 2 * PAIRS;
-    static_assert(!LDS || (RECOMP && !GENF && !S1), "LDS staging streams f (RECOMP) only");
     if (a.cond != nullptr && *a.cond == 0u) return;  // conditional (rare-path) launch
     int lbx, lby;
     fused_block(lbx, lby);
@@ -623,11 +497,9 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red, T 
     const int c0w = __builtin_amdgcn_readfirstlane(k.c - 2 * (int)(threadIdx.x & 63));
     const bool idle = c0w + 4 > N - 2;  // spare wave (wave-uniform)
     const bool inner = c0w >= 3 && c0w + 127 <= N - 3;   // see pre_body
-    const int i_end = (idle && !LDS) ? i_begin
-                                     : i_begin + ((2 * (jce - jcb) + 4 + R - 1) / R) * R;
+    const int i_end = idle ? i_begin
+                           : i_begin + ((2 * (jce - jcb) + 4 + R - 1) / R) * R;
     const bool pfired = RECOMP && *a.pre_fired != 0u;
-    RowStage<T, R> st{};
-    if constexpr (LDS) st = row_stage<T, R>(lds, a.f + P, P, N, lbx);   // f one row ahead
     if (RECOMP && !idle) {
         const V2<T> fm = ldv(F + (i_begin - 1) * P);
         fc = ldv(F + i_begin * P);
@@ -640,8 +512,7 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red, T 
     T ncr[PAIRS + 1];
     #pragma unroll
     for (int q = 0; q < R; ++q) {
-        if constexpr (LDS) np_[q] = st.load(i_begin + q);
-        else np_[q] = idle ? z : ldv(X + (i_begin + q) * P);
+        np_[q] = idle ? z : ldv(X + (i_begin + q) * P);
         if (!RECOMP && !GENF) nf[q] = idle ? z : ldv(F + (i_begin + q) * P);
     }
     #pragma unroll
@@ -655,30 +526,17 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red, T 
     auto iter = [&](int i, auto full_t) {
         V2<T> cp[R], cf[R];
         T cr[PAIRS + 1];
-        if constexpr (LDS) {   // stage this iteration's rows, prefetch the next, one barrier
-            const int slot = ((i - i_begin) / R) & 1;
-            #pragma unroll
-            for (int q = 0; q < R; ++q) st.put(slot, q, np_[q]);
-            if (i + R < i_end) {
-                #pragma unroll
-                for (int q = 0; q < R; ++q) np_[q] = st.load(i + R + q);
-            }
-            __syncthreads();
-            #pragma unroll
-            for (int q = 0; q < R; ++q) cp[q] = st.get(slot, q);
-        } else {
-            #pragma unroll
-            for (int q = 0; q < R; ++q) {
-                cp[q] = np_[q];
-                if (!RECOMP && !GENF) cf[q] = nf[q];
-            }
+        #pragma unroll
+        for (int q = 0; q < R; ++q) {
+            cp[q] = np_[q];
+            if (!RECOMP && !GENF) cf[q] = nf[q];
         }
         #pragma unroll
         for (int q = 0; q <= PAIRS; ++q) cr[q] = ncr[q];
         if (i + R < i_end) {
             #pragma unroll
             for (int q = 0; q < R; ++q) {
-                if constexpr (!LDS) np_[q] = ldv(X + (i + R + q) * P);
+                np_[q] = ldv(X + (i + R + q) * P);
                 if (!RECOMP && !GENF) nf[q] = ldv(F + (i + R + q) * P);
             }
             #pragma unroll
@@ -762,16 +620,6 @@ __global__ __launch_bounds__(256) void k_post(PostArgsT<T> a)
 {
     __shared__ double red[4];
     post_body<T, FINE, PAIRS, RECOMP, GENF, false>(a, red);
-}
-
-// the bulk coarse levels' k_post (RECOMP: f streamed one row ahead) with LDS-staged f rows
-// (168 VGPRs, three waves per SIMD, no spills; unconstrained it takes 170 and two waves)
-template <class T, int PAIRS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_post_lds(PostArgsT<T> a)
-{
-    __shared__ double red[4];
-    __shared__ __attribute__((aligned(16))) T lds[2 * 2 * PAIRS * kLdsRow];
-    post_body<T, false, PAIRS, true, false, false, true>(a, red, lds);
 }
 
 // rare path of k_post's check (replaces the scalar k_post_fixup on in-stream levels)
@@ -920,6 +768,55 @@ constexpr int pp_depth()
 {
     return (sizeof(T) == 4 || (GENF && !R2 && !(OPT & (64 | 32)))) ? 3 : 2;
 }
+// Lane t's 16-byte (fp32: 8-byte) column pair of a row segment starting at `base`; lanes
+// t >= n read 0 (descriptor range check).  The descriptor is built from wave-uniform values.
+template <class T, int NT>
+__device__ __forceinline__ V2<T> buf_row(const T *base, int n, int t)
+{
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<T *>(base), (short)0, n * (int)sizeof(V2<T>), 0x00020000);
+    if constexpr (sizeof(T) == 8) {
+        return __builtin_bit_cast(V2<T>, __builtin_amdgcn_raw_buffer_load_b128(
+                                             r, t * 16, 0, NT ? 2 : 0));
+    } else {
+        return __builtin_bit_cast(V2<T>, __builtin_amdgcn_raw_buffer_load_b64(
+                                             r, t * 8, 0, NT ? 2 : 0));
+    }
+}
+template <class T, int NT>
+__device__ __forceinline__ void buf_store_row(T *base, int bytes, int off, V2<T> v)
+{
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, bytes, 0x00020000);
+    if constexpr (sizeof(T) == 8) {
+        typedef unsigned u4 __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, off, 0, NT ? 2 : 0);
+    } else {
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, off, 0, NT ? 2 : 0);
+    }
+}
+template <class T>
+__device__ __forceinline__ void buf_store_one(T *base, int bytes, int off, T v)
+{
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, bytes, 0x00020000);
+    if constexpr (sizeof(T) == 8) {
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, off, 0, 0);
+    } else {
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
+    }
+}
+template <class T>
+__device__ __forceinline__ T buf_one(const T *base, int n, int t)
+{
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<T *>(base), (short)0, n * (int)sizeof(T), 0x00020000);
+    if constexpr (sizeof(T) == 8)
+        return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, t * 8, 0, 0));
+    else
+        return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, t * 4, 0, 0));
+}
+
 // The body of k_postpre_lds for one block.  EDGE = false: no row of the block's band and
 // no column of this wave is a boundary, so the Jacobi stages carry no passthrough selects.
 template <class T, bool R2, bool GENF, bool EDGE, int OPT>
@@ -1423,13 +1320,6 @@ static int postpre_spans(const PostPreArgsT<T> &a, int t, int gx, int r, bool co
     return PGMG_OK;
 }
 
-// Bulk coarse levels whose k_pre / k_post stream f through LDS-staged rows (blocks of four
-// waves; on smaller levels the block's spare waves would iterate for nothing)
-static bool lds_level(int N, int threads)
-{
-    return threads == 256 && N >= tuning_int("PGMG_LDS_MIN_N", 2049);
-}
-
 // The finest level gets its own kernel symbols (FINE) so rocprofv3 statistics
 // isolate the roofline kernels.
 template <class T>
@@ -1452,8 +1342,6 @@ int launch_pre(const PreArgsT<T> &a0, bool x0_zero, bool fine, hipStream_t s)
         else if (fine) k_pre<T, false, true, 2, false, true><<<g, b, 0, s>>>(a);
         else if (a.gfx != nullptr) k_pre<T, false, false, 2, true, true><<<g, b, 0, s>>>(a);
         else k_pre<T, false, false, 2, false, true><<<g, b, 0, s>>>(a);
-    } else if (x0_zero && lds_level(a.N, t)) {
-        k_pre_lds<T, 2><<<g, b, 0, s>>>(a);
     } else if (x0_zero) {
         k_pre<T, true, false, 2><<<g, b, 0, s>>>(a);
     } else if (fine && a.gfx != nullptr) {
@@ -1482,7 +1370,6 @@ int launch_post(const PostArgsT<T> &a0, bool fine, hipStream_t s)
     const bool rec = a.pre_fired != nullptr;
     if (fine && a.gfx != nullptr) k_post<T, true, 2, false, true><<<g, b, 0, s>>>(a);
     else if (fine) k_post<T, true, 2, false><<<g, b, 0, s>>>(a);
-    else if (rec && lds_level(a.N, t)) k_post_lds<T, 2><<<g, b, 0, s>>>(a);
     else if (rec) k_post<T, false, 2, true><<<g, b, 0, s>>>(a);
     else if (a.gfx != nullptr) k_post<T, false, 2, false, true><<<g, b, 0, s>>>(a);
     else k_post<T, false, 2, false><<<g, b, 0, s>>>(a);
