@@ -456,46 +456,8 @@ class StripComm : public Comm {
     Grid pend_g;
     Level pend_L;
     int pend_depth = 0;
-    // Every message and reduction of this rank runs on ONE communication stream, in program
-    // order (identical on every rank): the compute stream hands over with an event and waits
-    // for the result with another, so a group can run while the compute stream does work that
-    // does not depend on it (halos_begin / halos_end), with one communicator and never two
-    // groups of it in flight out of order.
-    hipStream_t cs = nullptr;
-    static constexpr int kEv = 64;
-    hipEvent_t evs[kEv] = {};
-    int evn = 0;
-    hipEvent_t ev_async = nullptr;
-    bool async_pending = false;
 
-    ~StripComm() override
-    {
-        if (cs) (void)hipStreamSynchronize(cs);
-        for (hipEvent_t e : evs)
-            if (e) (void)hipEventDestroy(e);
-        if (ev_async) (void)hipEventDestroy(ev_async);
-        if (cs) (void)hipStreamDestroy(cs);
-        delete t;
-    }
-    hipStream_t comm_stream(hipStream_t s) const { return cs ? cs : s; }
-    // the communication stream starts where s is now
-    int to_cs(hipStream_t s)
-    {
-        if (!cs) return PGMG_OK;
-        hipEvent_t e = evs[evn++ % kEv];
-        PGMG_HIPC(hipEventRecord(e, s));
-        PGMG_HIPC(hipStreamWaitEvent(cs, e, 0));
-        return PGMG_OK;
-    }
-    // s continues after what the communication stream has done so far
-    int from_cs(hipStream_t s)
-    {
-        if (!cs) return PGMG_OK;
-        hipEvent_t e = evs[evn++ % kEv];
-        PGMG_HIPC(hipEventRecord(e, cs));
-        PGMG_HIPC(hipStreamWaitEvent(s, e, 0));
-        return PGMG_OK;
-    }
+    ~StripComm() override { delete t; }
     int gathered_level() const override { return Ld; }
     int rank() const override { return me; }
 
@@ -542,13 +504,7 @@ class StripComm : public Comm {
         return PGMG_OK;
     }
 
-    int setup(pgmg_ctx *) override
-    {
-        PGMG_HIPC(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
-        for (hipEvent_t &e : evs) PGMG_HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        PGMG_HIPC(hipEventCreateWithFlags(&ev_async, hipEventDisableTiming));
-        return PGMG_OK;
-    }
+    int setup(pgmg_ctx *) override { return PGMG_OK; }
 
     // The finest level's halo rows are final a whole coarse hierarchy before the next
     // finest pass reads them.  Instead of a second communicator on a side stream (two
@@ -574,54 +530,20 @@ class StripComm : public Comm {
         if (!pending) return PGMG_OK;
         pending = false;
         const HaloReq r{&pend_g, &pend_L, pend_depth};
-        int e = to_cs(s);
-        if (!e) e = halos_on(t, &r, 1, comm_stream(s));
-        return e ? e : from_cs(s);
+        return halos_on(t, &r, 1, s);
     }
 
-    int halo_end(hipStream_t s) override
-    {
-        int e = flush(s);
-        if (!e) e = halos_end(s);
-        return e;
-    }
-
-    // the held-back finest-level halo (if any) followed by reqs, as one group on the
-    // communication stream
-    int post_group(const HaloReq *reqs, int n, hipStream_t s)
-    {
-        std::vector<HaloReq> all;
-        all.reserve(n + 1);
-        if (pending) all.push_back(HaloReq{&pend_g, &pend_L, pend_depth});
-        pending = false;
-        all.insert(all.end(), reqs, reqs + n);
-        int e = to_cs(s);
-        return e ? e : halos_on(t, all.data(), (int)all.size(), comm_stream(s));
-    }
+    int halo_end(hipStream_t s) override { return flush(s); }
 
     int halos(const HaloReq *reqs, int n, hipStream_t s) override
     {
-        const int e = post_group(reqs, n, s);
-        return e ? e : from_cs(s);
-    }
-
-    int halos_begin(const HaloReq *reqs, int n, hipStream_t s) override
-    {
-        int e = halos_end(s);   // (one asynchronous group at a time)
-        if (!e) e = post_group(reqs, n, s);
-        if (e) return e;
-        if (!cs) return PGMG_OK;
-        PGMG_HIPC(hipEventRecord(ev_async, cs));
-        async_pending = true;
-        return PGMG_OK;
-    }
-
-    int halos_end(hipStream_t s) override
-    {
-        if (!async_pending) return PGMG_OK;
-        async_pending = false;
-        PGMG_HIPC(hipStreamWaitEvent(s, ev_async, 0));
-        return PGMG_OK;
+        if (!pending) return halos_on(t, reqs, n, s);
+        std::vector<HaloReq> all;
+        all.reserve(n + 1);
+        all.push_back(HaloReq{&pend_g, &pend_L, pend_depth});
+        all.insert(all.end(), reqs, reqs + n);
+        pending = false;
+        return halos_on(t, all.data(), n + 1, s);
     }
 
     // one array's halo send/recv pairs inside an open group
@@ -654,54 +576,42 @@ class StripComm : public Comm {
 
     int allreduce_sum(double *d, int n, hipStream_t s) override
     {
-        int e = flush(s);
-        if (!e) e = halos_end(s);
-        if (!e) e = to_cs(s);
-        if (!e) e = t->allreduce_sum(d, n, comm_stream(s));
-        return e ? e : from_cs(s);
+        const int e = flush(s);
+        return e ? e : t->allreduce_sum(d, n, s);
     }
     int wait(hipStream_t s) override
     {
-        int e = flush(s);
-        if (!e) e = halos_end(s);
+        const int e = flush(s);
         return e ? e : t->wait(s);
     }
     int allreduce_min_u32(unsigned *d, int n, hipStream_t s) override
     {
-        int e = flush(s);
-        if (!e) e = halos_end(s);
-        if (!e) e = to_cs(s);
-        if (!e) e = t->allreduce_min_u32(d, n, comm_stream(s));
-        return e ? e : from_cs(s);
+        const int e = flush(s);
+        return e ? e : t->allreduce_min_u32(d, n, s);
     }
 
     int allgather_rows(pgmg_ctx *c, int l, const Grid &g) override
     {
         Level &L = c->lv[l];
         const size_t row = (size_t)L.P * L.es;
-        int e = halos_end(c->s);
-        if (!e) e = to_cs(c->s);
-        if (e) return e;
-        hipStream_t q0 = comm_stream(c->s);
-        e = t->group_start();
+        int e = t->group_start();
         if (e) return e;
         if (pending) {   // the finest level's held-back halo rides in this group
             pending = false;
-            e = post_halo(t, HaloReq{&pend_g, &pend_L, pend_depth}, q0);
+            e = post_halo(t, HaloReq{&pend_g, &pend_L, pend_depth}, c->s);
         }
         for (int r = 0; r < world && !e; ++r) {
             const int a = std::max(strip_lo(r, l), 1), b = std::min(strip_hi(r, l, L.N), L.N - 1);
             if (b <= a) continue;
             if (r == me) {
                 for (int q = 0; q < world && !e; ++q)
-                    if (q != me) e = t->send(row_ptr(g, a, L.P, L.es), (b - a) * row, q, q0);
+                    if (q != me) e = t->send(row_ptr(g, a, L.P, L.es), (b - a) * row, q, c->s);
             } else {
-                e = t->recv(row_ptr(g, a, L.P, L.es), (b - a) * row, r, q0);
+                e = t->recv(row_ptr(g, a, L.P, L.es), (b - a) * row, r, c->s);
             }
         }
-        const int e2 = t->group_end(q0);   // the group is closed even after a failed call
-        if (e || e2) return e ? e : e2;
-        return from_cs(c->s);
+        const int e2 = t->group_end(c->s);   // the group is closed even after a failed call
+        return e ? e : e2;
     }
 
     int run_gathered(pgmg_ctx *c, int l, int gamma, int repeats) override
@@ -724,7 +634,6 @@ class StripComm : public Comm {
         const size_t row = (size_t)L.P * L.es;
         const bool want = root < 0 || root == me;
         if (const int ef = flush(c->s)) return ef;
-        if (const int ef = halos_end(c->s)) return ef;
         Grid full;
         if (want) {
             PGMG_HIPC(hipMalloc(&full.base, (size_t)N * row));
@@ -732,21 +641,18 @@ class StripComm : public Comm {
             PGMG_HIPC(hipMemcpyAsync(row_ptr(full, L.lo, L.P, L.es), row_ptr(L.A, L.lo, L.P, L.es),
                                      (L.hi - L.lo) * row, hipMemcpyDeviceToDevice, c->s));
         }
-        int e = to_cs(c->s);
-        hipStream_t q0 = comm_stream(c->s);
-        if (!e) e = t->group_start();
+        int e = t->group_start();
         for (int r = 0; r < world && !e; ++r) {
             if (r == me) continue;
             if (root < 0 || root == r)
-                e = t->send(row_ptr(L.A, L.lo, L.P, L.es), (L.hi - L.lo) * row, r, q0);
+                e = t->send(row_ptr(L.A, L.lo, L.P, L.es), (L.hi - L.lo) * row, r, c->s);
             if (!e && want) {
                 const int a = strip_lo(r, 0), b = strip_hi(r, 0, N);
-                e = t->recv(row_ptr(full, a, L.P, L.es), (b - a) * row, r, q0);
+                e = t->recv(row_ptr(full, a, L.P, L.es), (b - a) * row, r, c->s);
             }
         }
-        const int e2 = t->group_end(q0);   // closed even after a failed send/recv
+        const int e2 = t->group_end(c->s);   // closed even after a failed send/recv
         if (!e) e = e2;
-        if (!e) e = from_cs(c->s);
         if (!e && want) e = download_grid(c, full.o, L.P, N, phi);
         if (!e) e = t->wait(c->s);
         else (void)hipStreamSynchronize(c->s);

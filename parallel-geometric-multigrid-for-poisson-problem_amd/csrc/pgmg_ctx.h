@@ -185,11 +185,6 @@ class Comm {
         return halo(g, L, depth, s);
     }
     virtual int halo_end(hipStream_t) { return 0; }
-    // An exchange whose completion stream s joins later (halos_end): s goes on with work that
-    // does not read the halo rows meanwhile (the interior bands of a coarse level's k_pre).
-    // Default: in place.
-    virtual int halos_begin(const HaloReq *reqs, int n, hipStream_t s) { return halos(reqs, n, s); }
-    virtual int halos_end(hipStream_t) { return 0; }
     // in-place sum of n device doubles over all ranks
     virtual int allreduce_sum(double *d, int n, hipStream_t s) = 0;
     // in-place element-wise minimum of n device unsigned ints over all ranks

@@ -325,56 +325,6 @@ static int global_sum(pgmg_ctx *c, int np, const double **out)
     return e;
 }
 
-// k_pre of a distributed level whose right-hand-side halo is in flight (Comm::halos_begin):
-// first the bands whose rows all lie inside the strip, then -- once the exchange is joined
-// -- the edge bands.  Same bands, same partial-sum slots as one launch.
-template <class T>
-static int launch_pre_split(pgmg_ctx *c, const Level &L, const PreArgsT<T> &pa, bool x0_zero)
-{
-    int r = 0;
-    const int nb = fused_bands(L.N, pa.jc0, pa.jc1, &r);
-    // band b streams fine rows 2 jcb - 4 .. 2 jcb - 4 + ceil((2 (jce - jcb) + 8) / 4) * 4 - 1
-    auto inside = [&](int b) {
-        const int jcb = pa.jc0 + b * r, jce = std::min(jcb + r, pa.jc1);
-        const int first = 2 * jcb - 4;
-        const int last = first + ((2 * (jce - jcb) + 8 + 3) / 4) * 4 - 1;
-        return first >= L.lo && last < L.hi;
-    };
-    int b0 = 0, b1 = nb;   // interior bands [b0, b1)
-    while (b0 < nb && !inside(b0)) ++b0;
-    while (b1 > b0 && !inside(b1 - 1)) --b1;
-    for (int b = b0; b < b1; ++b)
-        if (!inside(b)) b1 = b0;   // not one run: no split
-    int e;
-    if (b1 <= b0) {   // nothing to overlap
-        if ((e = c->comm->halos_end(c->s))) return e;
-        return launch_pre(pa, x0_zero, false, c->s);
-    }
-    PreArgsT<T> q = pa;
-    q.band0 = b0;
-    q.band_step = 1;
-    q.band_count = b1 - b0;
-    if ((e = launch_pre(q, x0_zero, false, c->s))) return e;
-    if ((e = c->comm->halos_end(c->s))) return e;
-    if (b0 == 1 && b1 == nb - 1) {   // the usual case: one edge band each side, one launch
-        q.band0 = 0;
-        q.band_step = nb - 1;
-        q.band_count = 2;
-        return launch_pre(q, x0_zero, false, c->s);
-    }
-    if (b0 > 0) {
-        q.band0 = 0;
-        q.band_count = b0;
-        if ((e = launch_pre(q, x0_zero, false, c->s))) return e;
-    }
-    if (b1 < nb) {
-        q.band0 = b1;
-        q.band_count = nb - b1;
-        if ((e = launch_pre(q, x0_zero, false, c->s))) return e;
-    }
-    return PGMG_OK;
-}
-
 // fused level (v1 = v2 = 1): k_pre (+fixup), children, k_post (+fixup)
 // pin (F-cycle climb, x0_zero false): the level's x0 is the prolongation of level l+1's
 // grid into a zeroed grid; k_pre computes it on the fly instead of reading L.A
@@ -393,18 +343,11 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     // strip edge (from deeper halos of f and phi, exchanged with the pre-smooth's anyway),
     // so the parent's prolongation reads this level's correction without an exchange
     const bool ext = dist && l > 0;
-    // the right-hand side's halo of a distributed level entered with x0 = 0 is exchanged
-    // while k_pre runs the bands that do not read halo rows (split_pre below)
-    const bool split_pre = dist && l > 0 && x0_zero && !pin;
     if (dist) {
         if (!x0_zero && !pin && (e = c->comm->halo(L.A, L, 4, c->s))) return e;
         // f: 4 rows for k_pre, 3 + kPostExt for the extended k_post (RECOMP reads f 3 rows
         // past its first output row)
-        if (l > 0) {
-            const HaloReq hr{&L.F, &L, 3 + kPostExt};
-            e = split_pre ? c->comm->halos_begin(&hr, 1, c->s) : c->comm->halos(&hr, 1, c->s);
-            if (e) return e;
-        }
+        if (l > 0 && (e = c->comm->halo(L.F, L, 3 + kPostExt, c->s))) return e;
     }
     PreArgsT<T> pa{};
     pa.x0 = G<T>(L.A);
@@ -440,11 +383,7 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     double *lp = chk_partials(c, fa.np, l);   // speculative call: record the check, no fix-up
     if (lp) pa.partials = lp;
     int ev = fine ? timed_begin(c, 1) : -1;
-    if (split_pre) {
-        if ((e = launch_pre_split(c, L, pa, x0_zero))) return e;
-    } else if ((e = launch_pre(pa, x0_zero, fine, c->s))) {
-        return e;
-    }
+    if ((e = launch_pre(pa, x0_zero, fine, c->s))) return e;
     if ((e = timed_end(c, 1, ev))) return e;
     if (!lp) {
         if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;

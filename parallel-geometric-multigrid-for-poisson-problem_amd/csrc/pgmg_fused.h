@@ -36,10 +36,6 @@ struct PreArgsT {
     // reference layout (pitch N, pgmg_set_problem_device): the call's first pass reads it in
     // place; its 16-byte column-pair loads are then 8-byte aligned on every other row
     long long Px;
-    // band_count > 0: this launch runs only bands band0, band0 + band_step, ... (band_count of
-    // them) of the pass's band geometry -- row strips run the bands that need no halo rows
-    // while the halo exchange is in flight, the edge bands after it (launch_pre)
-    int band0, band_step, band_count;
 };
 
 // prolongation + post-smooth (2 sweeps) in one pass
@@ -114,8 +110,6 @@ using PostArgs = PostArgsT<double>;
 using PostPreArgs = PostPreArgsT<double>;
 
 int fused_blocks(int N, int jc0, int jc1);
-// bands (blocks along the rows) of k_pre's geometry and the coarse rows per band
-int fused_bands(int N, int jc0, int jc1, int *rows_per_band);
 // the fused-pass launchers return PGMG_ERR_STATE (and launch nothing) when a span the pass
 // would read or write lies outside its array's allocation (check_span)
 template <class T> int launch_pre(const PreArgsT<T> &a, bool x0_zero, bool fine, hipStream_t s);

@@ -31,14 +31,10 @@
 #include <cstdlib>
 #include <type_traits>
 
-#include <string>
-
 #include "pgmg.h"
 #include "pgmg_fused.h"
 
 namespace pgmg {
-
-int set_err(int code, const std::string &msg);   // pgmg_ctx.hip
 
 struct Cols {
     int c;          // odd column of this lane's pair (c, c+1)
@@ -213,7 +209,6 @@ __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red)
     if (a.cond != nullptr && *a.cond == 0u) return;  // conditional (rare-path) launch
     int lbx, lby;
     fused_block(lbx, lby);
-    if (a.band_count > 0) lby = a.band0 + lby * a.band_step;   // a subset of the bands
     const Cols k = lane_cols(a.N, lbx);
     const int N = a.N;
     const long long P = a.P;
@@ -221,7 +216,7 @@ __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red)
     const int jce = min(jcb + a.rows_per_block, a.jc1);
     const int olo = max(2 * jcb, a.row_lo), ohi = min(2 * jce, a.row_hi);  // x2 rows written
     const int clo = max(jcb, max(1, a.rc_lo)), chi = min(jce, min(N / 2, a.rc_hi));  // rc rows
-    if (!S1 && lbx == 0 && lby == 0 && threadIdx.x == 0 && a.stats != nullptr)
+    if (!S1 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
         atomicAdd(&a.stats[0], 2ull);
     const T *__restrict__ X = a.x0 + k.c;
     const long long Px = a.Px != 0 ? a.Px : P;   // x0's pitch (the caller's array: N)
@@ -410,7 +405,7 @@ __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red)
     row_loop<R, PIN ? 0 : 3>(i_begin, i_end, full_at, iter);
     if constexpr (!S1) {
         const double sum = fused_block_sum(acc, red);
-        if (threadIdx.x == 0) a.partials[lby * gridDim.x + lbx] = sum;
+        if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = sum;
     }
 }
 
@@ -1200,14 +1195,6 @@ int fused_blocks(int N, int jc0, int jc1)
     return gx * gy;
 }
 
-int fused_bands(int N, int jc0, int jc1, int *rows_per_band)
-{
-    int t, gx, gy, r;
-    fused_geometry(N, jc0, jc1, &t, &gx, &gy, &r);
-    *rows_per_band = r;
-    return gy;
-}
-
 // ---------------------------------------------------------------------------
 // read/write extents of the fused passes (pgmg_internal.h, check_span)
 // ---------------------------------------------------------------------------
@@ -1344,11 +1331,6 @@ int launch_pre(const PreArgsT<T> &a0, bool x0_zero, bool fine, hipStream_t s)
         return e;
     PreArgsT<T> a = a0;
     a.rows_per_block = r;
-    if (a.band_count > 0) {   // a subset of the bands (the spans above cover all of them)
-        if (a.band_step < 1 || a.band0 < 0 || a.band0 + (a.band_count - 1) * a.band_step >= gy)
-            return set_err(PGMG_ERR_STATE, "launch_pre: band subset outside the pass's bands");
-        gy = a.band_count;
-    }
     // non-temporal stores on the finest level only (its x2 is read again a level-pass later;
     // coarse outputs are re-read while still in the caches): fine k_pre 0.99 -> 0.97 ms
     a.nt = fine ? 1 : 0;
