@@ -109,6 +109,8 @@ extern "C" {
                                    One GPU (row strips ignore it); everything else exact */
 /* (8192u: level 1's post-smooth inside the finest pass -- built in r02, measured slower,
    removed; the bit stays unused) */
+/* (16384u: the 129x129 level inside the tail's launch -- built in r03, bitwise, measured
+   slower (one CU's fp64 VALU: ~1.2 us per pass over 129^2 points); removed) */
 #define PGMG_FLAG_HOST_TRANSPORT 2048u /* world > 1 without RCCL: nccl_unique_id points to
                                        a pgmg_host_transport; every message and reduction
                                        is staged through host memory and handed to the
@@ -319,6 +321,10 @@ int pgmg_prolong_grid(const double *d_coarse, double *d_fine, int Nc, int Nf, in
                       int num_thread, void *stream);
 int pgmg_norm(const double *d_v, long long n, double *result, void *stream);
 int pgmg_rhs(double *d_f, int W, int H, double h, double a, double p, double q, void *stream);
+/* The op-level entries keep one scratch set (partial sums, flags, ping-pong buffer) per
+ * stream they were called on; this waits for `stream` and frees its set (a later op on the
+ * same stream allocates a fresh one).  Call it before destroying a stream the ops used. */
+int pgmg_ops_release(void *stream);
 
 /* ---- device memory helpers (for host code built without HIP headers) ----- */
 int pgmg_device_alloc(void **ptr, size_t bytes);

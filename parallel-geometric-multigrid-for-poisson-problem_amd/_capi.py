@@ -127,6 +127,7 @@ SIGNATURES = [
     ("pgmg_norm", C.c_int, [_P, C.c_longlong, _DP, _P]),
     ("pgmg_rhs", C.c_int, [_P, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, C.c_double,
                            _P]),
+    ("pgmg_ops_release", C.c_int, [_P]),
     ("pgmg_device_alloc", C.c_int, [C.POINTER(_P), C.c_size_t]),
     ("pgmg_device_free", C.c_int, [_P]),
     ("pgmg_memcpy_h2d", C.c_int, [_P, _P, C.c_size_t]),

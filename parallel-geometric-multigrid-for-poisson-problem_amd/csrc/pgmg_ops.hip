@@ -35,7 +35,7 @@ struct OpScratch {
 
 // One scratch set per stream: ops enqueued on different streams never share partial sums,
 // flags or the ping-pong buffer (the reference's ops are synchronous on the default stream;
-// these are asynchronous on the caller's).  Sets live for the process.
+// these are asynchronous on the caller's).  A set lives until pgmg_ops_release(stream).
 std::mutex g_op_mu;
 std::map<hipStream_t, OpScratch> g_ops;
 
@@ -178,6 +178,24 @@ int pgmg_rhs(double *d_f, int W, int H, double h, double a, double p, double q, 
     launch_g_rhs(d_f, d, d + W, factor, W, H, s);
     HIPC(hipStreamSynchronize(s));
     HIPC(hipFree(d));
+    return PGMG_OK;
+}
+
+int pgmg_ops_release(void *stream)
+{
+    hipStream_t s = (hipStream_t)stream;
+    OpScratch o;
+    {
+        std::lock_guard<std::mutex> lk(g_op_mu);
+        auto it = g_ops.find(s);
+        if (it == g_ops.end()) return PGMG_OK;
+        o = it->second;
+        g_ops.erase(it);
+    }
+    HIPC(hipStreamSynchronize(s));   // ops still queued on s may use the set
+    for (void *p : {(void *)o.partials, (void *)o.flags, (void *)o.stats, (void *)o.scalar,
+                    (void *)o.tmp})
+        if (p) HIPC(hipFree(p));
     return PGMG_OK;
 }
 

@@ -28,7 +28,8 @@ def child(a):
         kind, n = spec[0], int(spec[1:])
         steps = a.steps if kind == "V" else max(1, a.steps // 10)
         ts = []
-        with pg.Solver(n) as s:
+        flags = int(os.environ.get("AB_FLAGS", "0"))   # pgmg_config.flags of the variant
+        with pg.Solver(n, **({"flags": flags} if flags else {})) as s:
             run = s.vcycle if kind == "V" else s.wcycle
             for _ in range(3):
                 s.set_problem()

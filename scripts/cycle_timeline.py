@@ -30,9 +30,10 @@ def child(args):
         kw.update(rank=args.rank, world=args.world, flags=kw.get("flags", 0) | pg.PGMG_FLAG_SOLO)
     with pg.Solver(args.n, **kw) as s:
         s.set_problem()
-        s.vcycle(3)
+        run = s.wcycle if args.kind == "W" else s.vcycle
+        run(1 if args.kind == "W" else 3)
         s.sync()
-        s.vcycle(args.cycles)
+        run(args.cycles)
         s.sync()
 
 
@@ -81,6 +82,7 @@ if __name__ == "__main__":
     ap.add_argument("--n", type=int, default=16385)
     ap.add_argument("--cycles", type=int, default=10)
     ap.add_argument("--flags", type=int, default=0)
+    ap.add_argument("--kind", default="V", choices=["V", "W"])
     ap.add_argument("--world", type=int, default=1)
     ap.add_argument("--rank", type=int, default=0)
     a = ap.parse_args()

@@ -255,6 +255,16 @@ def test_op_jacobi_concurrent_streams(pgmg, oracle_mod):
         xt.zero_()
         torch.cuda.synchronize()
         assert pgmg.ops.jacobi(xt, ft, h, 40, eps=eps, stream=C_stream(st)) == n_ref
+    # releasing a stream's scratch set: the next op on it allocates a fresh one
+    for i, (xt, ft, st) in enumerate(outs):
+        pgmg.check(pgmg.load().pgmg_ops_release(C_stream(st)), "pgmg_ops_release")
+        pgmg.check(pgmg.load().pgmg_ops_release(C_stream(st)), "pgmg_ops_release")  # no-op
+        N, h, eps, f, x_ref, n_ref = probs[i]
+        xt.zero_()
+        torch.cuda.synchronize()
+        assert pgmg.ops.jacobi(xt, ft, h, 40, eps=eps, stream=C_stream(st)) == n_ref
+        assert_bitwise(xt.cpu().numpy(), x_ref, f"stream {i} after release")
+        pgmg.check(pgmg.load().pgmg_ops_release(C_stream(st)), "pgmg_ops_release")
 
 
 def C_stream(st):
