@@ -107,8 +107,10 @@ extern "C" {
                                    order, so phi agrees with the EXACT default within
                                    1e-12 relative (after <= 10 cycles) instead of bitwise.
                                    One GPU (row strips ignore it); everything else exact */
-/* (8192u: level 1's post-smooth inside the finest pass -- built in r02, measured slower,
-   removed; the bit stays unused) */
+#define PGMG_FLAG_NO_SPEC_FIRE 8192u /* speculative calls without segment planning and
+                                       without levels predicted to fire (the r02 policy:
+                                       a level that will fire decides in-stream from the
+                                       call's start).  Results are identical either way */
 /* (16384u: the 129x129 level inside the tail's launch -- built in r03, bitwise, measured
    slower (one CU's fp64 VALU: ~1.2 us per pass over 129^2 points); removed) */
 #define PGMG_FLAG_HOST_TRANSPORT 2048u /* world > 1 without RCCL: nccl_unique_id points to
@@ -284,6 +286,10 @@ int pgmg_dist_info(pgmg_ctx *ctx, int *speculative, long long *rollbacks);
  * bit l (l >= 1) = level l's checks fired or are predicted to fire soon; bit 0 = no
  * speculation at all (disabled, or a finest-level check fires). */
 int pgmg_spec_levels(pgmg_ctx *ctx, unsigned long long *in_stream);
+/* Of those, the levels whose checks are predicted to FIRE in the next speculative call (one
+ * GPU; converged levels: each visit runs the one-sweep passes the in-stream rare paths would
+ * run, and the validation confirms every such check fired, else the call is rolled back). */
+int pgmg_spec_fire_levels(pgmg_ctx *ctx, unsigned long long *fire);
 
 /* The context's PGMG_PRECISION_* and its grid element size in bytes (8 or 4). */
 int pgmg_precision(pgmg_ctx *ctx, int *precision, int *elem_bytes);

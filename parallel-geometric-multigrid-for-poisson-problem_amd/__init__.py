@@ -22,6 +22,7 @@ from ._capi import (PGMG_FLAG_LOOPBACK, PGMG_FLAG_NO_CROSS, PGMG_FLAG_NO_GRAPH,
                     PGMG_FLAG_TIME_FINE, PGMG_PRECISION_FP32, PGMG_PRECISION_FP64,
                     PGMG_FLAG_UNFUSED, PGMG_FLAG_NO_RECOMPUTE, PGMG_FLAG_NO_PIN,
                     PGMG_FLAG_NO_R2, PGMG_FLAG_HOST_TRANSPORT, PGMG_FLAG_FAST,
+                    PGMG_FLAG_NO_SPEC_FIRE,
                     PGMG_PROLONG_REFERENCE,
                     PGMG_PROLONG_SYMMETRIC, PGMG_OK, PGMG_ERR_STATE, PgmgConfig, PgmgError,
                     check, load)
@@ -34,7 +35,7 @@ __all__ = [
     "PGMG_PROLONG_REFERENCE", "plan_strips", "LoopbackHub", "unique_id",
     "PGMG_PROLONG_SYMMETRIC", "PGMG_PRECISION_FP64", "PGMG_PRECISION_FP32",
     "PGMG_FLAG_STORED_RHS", "PGMG_FLAG_EXACT_DIST", "PGMG_FLAG_SOLO",
-    "PGMG_FLAG_NO_RECOMPUTE", "PGMG_FLAG_NO_PIN", "PGMG_FLAG_NO_R2", "PGMG_FLAG_FAST",
+    "PGMG_FLAG_NO_RECOMPUTE", "PGMG_FLAG_NO_PIN", "PGMG_FLAG_NO_R2", "PGMG_FLAG_FAST", "PGMG_FLAG_NO_SPEC_FIRE",
     "PGMG_FLAG_HOST_TRANSPORT", "HostTransport", "DeviceGrid",
 ]
 
@@ -304,10 +305,17 @@ class Solver:
         return bool(sp.value), rb.value
 
     def spec_levels(self):
-        """Bit mask: bit l = bulk level l decides its checks in-stream; bit 0 = no
-        speculation at all."""
+        """Bit mask: bit l = bulk level l's checks are not speculated "does not fire" (decided
+        in-stream, or predicted to fire); bit 0 = no speculation at all."""
         m = C.c_ulonglong()
         check(self.lib.pgmg_spec_levels(self.h, C.byref(m)), "pgmg_spec_levels")
+        return m.value
+
+    def spec_fire_levels(self):
+        """Bit mask: bit l = bulk level l's checks are predicted to fire (one-sweep passes,
+        confirmed by the validation)."""
+        m = C.c_ulonglong()
+        check(self.lib.pgmg_spec_fire_levels(self.h, C.byref(m)), "pgmg_spec_fire_levels")
         return m.value
 
     @property

@@ -35,6 +35,7 @@ PGMG_FLAG_NO_PIN = 512
 PGMG_FLAG_NO_R2 = 1024
 PGMG_FLAG_HOST_TRANSPORT = 2048
 PGMG_FLAG_FAST = 4096
+PGMG_FLAG_NO_SPEC_FIRE = 8192
 
 PGMG_PRECISION_FP64 = 0
 PGMG_PRECISION_FP32 = 1
@@ -117,6 +118,7 @@ SIGNATURES = [
     ("pgmg_fine_pass_bytes", C.c_int, [_P, C.c_int, _DP]),
     ("pgmg_dist_info", C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_longlong)]),
     ("pgmg_spec_levels", C.c_int, [_P, C.POINTER(C.c_ulonglong)]),
+    ("pgmg_spec_fire_levels", C.c_int, [_P, C.POINTER(C.c_ulonglong)]),
     ("pgmg_bench_sweep", C.c_int, [_P, C.c_int, _DP]),
     ("pgmg_jacobi", C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_double, C.c_int, C.c_double,
                               C.POINTER(C.c_int), _P]),

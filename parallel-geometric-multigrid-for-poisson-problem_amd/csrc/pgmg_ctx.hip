@@ -154,17 +154,34 @@ void pgmg::free_grid(Grid &g)
 // check in-stream).  The log is sized beforehand (spec_need); running past it would be a
 // bug: the check then writes the shared partials and the call is treated as failed
 // validation (rolled back), never read out of bounds.
-static double *chk_partials(pgmg_ctx *c, int np, int level)
+// How a speculative call enqueues level l's checks: 0 recorded as "does not fire" (no
+// fix-up), 1 recorded as "fires" (the one-sweep passes, no fix-up), 2 decided in-stream (the
+// fix-ups; outside speculative calls every check).
+static int chk_mode(const pgmg_ctx *c, int level)
 {
-    if (!c->lean || c->lvl_exact[level]) return nullptr;
+    if (!c->lean || c->lvl_exact[level]) return 2;
+    return c->lvl_fire[level] ? 1 : 0;
+}
+
+// A log slice for one check of mode `mode` (nullptr outside speculative calls; an in-stream
+// check is logged -- its norm only, for the per-level policy -- on one GPU)
+static double *chk_log(pgmg_ctx *c, int np, int level, int mode)
+{
+    if (!c->lean || (mode == 2 && c->comm != nullptr)) return nullptr;
     if (c->plog_used + np > c->plog_cap) {
-        c->chks.push_back({nullptr, -1, level, 0});
+        c->chks.push_back({nullptr, -1, level, mode});
         return c->partials;
     }
     double *p = c->plog + c->plog_used;
     c->plog_used += np;
-    c->chks.push_back({p, np, level, 0});
+    c->chks.push_back({p, np, level, mode});
     return p;
+}
+
+// the slice of a check recorded as "does not fire" (nullptr: decide it in-stream)
+static double *chk_partials(pgmg_ctx *c, int np, int level)
+{
+    return chk_mode(c, level) == 0 ? chk_log(c, np, level, 0) : nullptr;
 }
 
 // ---------------------------------------------------------------------------
@@ -380,14 +397,20 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     fa.eps = c->cfg.eps;
     fa.stats = c->stats;
     const bool fine = (l == 0);
-    double *lp = chk_partials(c, fa.np, l);   // speculative call: record the check, no fix-up
+    // speculative call: record the check (mode 0: no fix-up; 1: predicted to fire, the
+    // one-sweep passes, on levels entered with x0 = 0; 2: in-stream, logged for its norm)
+    int mode = chk_mode(c, l);
+    if (mode == 1 && !(recomp && !dist)) mode = 2;
+    double *lp = chk_log(c, fa.np, l, mode);
     if (lp) pa.partials = lp;
     int ev = fine ? timed_begin(c, 1) : -1;
-    if ((e = launch_pre(pa, x0_zero, fine, c->s))) return e;
+    if ((e = mode == 1 ? launch_pre1(pa, c->s) : launch_pre(pa, x0_zero, fine, c->s))) return e;
     if ((e = timed_end(c, 1, ev))) return e;
-    if (!lp) {
+    if (mode == 2) {
+        if (lp) fa.partials = lp;
         if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
         if ((e = launch_pre_rare(fa, pa, x0_zero, c->s))) return e;
+        fa.partials = c->partials;
     }
     if ((e = enqueue_children<T>(c, l, gamma))) return e;
     // the correction of level l+1 is not exchanged: a distributed child's k_post computed
@@ -423,12 +446,13 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     }
     po.gfx = pa.gfx;
     po.gsy = pa.gsy;
-    lp = chk_partials(c, fa.np, l);
+    lp = chk_log(c, fa.np, l, mode);
     if (lp) po.partials = lp;
     ev = fine ? timed_begin(c, 2) : -1;
-    if ((e = launch_post(po, fine, c->s))) return e;
+    if ((e = mode == 1 ? launch_post1(po, c->s) : launch_post(po, fine, c->s))) return e;
     if ((e = timed_end(c, 2, ev))) return e;
-    if (!lp) {
+    if (mode == 2) {
+        if (lp) fa.partials = lp;
         fa.global_sum = nullptr;
         if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
         if ((e = launch_post_rare(fa, po, c->s))) return e;
@@ -1031,6 +1055,8 @@ static int problem_reset(pgmg_ctx *c)
     c->have_problem = true;
     c->spec_off = false;   // a new problem: speculate again, every level
     c->lvl_exact.assign(c->nb + 1, 0);
+    c->lvl_fire.assign(c->nb + 1, 0);
+    c->lvl_fire_block.assign(c->nb + 1, 0);
     c->lvl_hist.assign(c->nb + 1, std::vector<double>());
     return PGMG_OK;
 }
@@ -1392,6 +1418,21 @@ static int spec_reserve(pgmg_ctx *c, long long dbl, long long nchk)
     return PGMG_OK;
 }
 
+// last norm and decay of level l's checks (spec_mark_levels' prediction); false without history
+static bool spec_level_trend(const pgmg_ctx *c, int l, double *last, double *rho)
+{
+    const std::vector<double> &h = c->lvl_hist[l];
+    const size_t m = h.size();
+    if (m < 2) return false;
+    *last = std::min(h[m - 1], h[m - 2]);
+    *rho = 0.4;
+    if (m >= 4) {
+        const double prev = std::min(h[m - 3], h[m - 4]);
+        if (prev > 0.0) *rho = std::min(*rho, std::max(1e-3, *last / prev));
+    }
+    return true;
+}
+
 // Per-level policy.  Residual norms of a level fall geometrically over the V-cycles (after
 // a few cycles of growth from phi = 0) until they level off, and on the reference problem
 // the levels just above the tail reach eps after ~27 cycles at every N >= 2049
@@ -1404,25 +1445,38 @@ static int spec_reserve(pgmg_ctx *c, long long dbl, long long nchk)
 // 1/h^2-scaled sums); if one of its checks does fire the context stops speculating.
 // Row strips: each rank predicts from its own partials (a lower bound of the global norm,
 // so earlier), then the ranks agree on the union of the marks (one allreduce).
+//
+// Predicted to fire (one GPU): a level whose last two visits' checks all had norms below
+// eps / 4 -- it converged and fires at every check -- is enqueued with its checks decided
+// "fires" (k_pre1 / k_post1: the one-sweep passes the in-stream rare paths would run, one
+// launch each instead of two) and recorded the other way round: the validation flags a
+// check that could NOT fire (sqrt(s) >= eps (1 - 1e-12)), the call is rolled back, and the
+// level decides in-stream for the rest of the problem.  A level in that mode whose norm
+// comes back above eps / 4 returns to in-stream decisions.
 static int spec_mark_levels(pgmg_ctx *c, int cycles)
 {
     const double lim = c->cfg.eps * 100.0;
+    if (c->comm == nullptr && !(c->cfg.flags & PGMG_FLAG_NO_SPEC_FIRE)) {
+        const double flim = c->cfg.eps * 0.25;
+        for (int l = 1; l < c->nb; ++l) {
+            const std::vector<double> &h = c->lvl_hist[l];
+            const size_t m = h.size();
+            const size_t need = c->lvl_fire[l] ? 2 : 4;
+            bool below = !c->lvl_fire_block[l] && m >= need;
+            for (size_t i = m - std::min(m, need); i < m && below; ++i) below = h[i] < flim;
+            c->lvl_fire[l] = below ? 1 : 0;
+            if (below) c->lvl_exact[l] = 0;
+            else if (m >= 2 && h[m - 1] < c->cfg.eps) c->lvl_exact[l] = 1;   // fired: in-stream
+        }
+    }
     std::vector<unsigned> keep(c->nb + 1, 1u);   // 1 = keep speculating
     for (int l = 1; l < c->nb; ++l) {
-        const std::vector<double> &h = c->lvl_hist[l];
-        const size_t m = h.size();
-        if (c->lvl_exact[l] || m < 2) continue;
-        const double last = std::min(h[m - 1], h[m - 2]);   // min over the last visit
-        double rho = 0.4;
-        if (m >= 4) {
-            const double prev = std::min(h[m - 3], h[m - 4]);
-            if (prev > 0.0) rho = std::min(rho, std::max(1e-3, last / prev));
-        }
+        double last, rho;   // min over the last visit; decay per cycle
+        if (c->lvl_exact[l] || c->lvl_fire[l] || !spec_level_trend(c, l, &last, &rho)) continue;
         if (!(last * std::pow(rho, (double)cycles) >= lim)) keep[l] = 0u;
         if (tuning_int("PGMG_SPEC_TRACE", 0))
-            fprintf(stderr, "spec level %d N=%d norms[-4..] %.3e %.3e %.3e %.3e rho %.3f next %d -> %s\n",
-                    l, c->lv[l].N, m >= 4 ? h[m - 4] : -1.0, m >= 3 ? h[m - 3] : -1.0, h[m - 2],
-                    h[m - 1], rho, cycles, keep[l] ? "speculate" : "in-stream");
+            fprintf(stderr, "spec level %d N=%d last %.3e rho %.3f next %d -> %s\n", l, c->lv[l].N,
+                    last, rho, cycles, keep[l] ? "speculate" : "in-stream");
     }
     if (c->comm) {
         HIPC(hipMemcpyAsync(c->mark_dev, keep.data(), (c->nb + 1) * sizeof(unsigned),
@@ -1436,6 +1490,72 @@ static int spec_mark_levels(pgmg_ctx *c, int cycles)
     for (int l = 1; l < c->nb; ++l)
         if (!keep[l]) c->lvl_exact[l] = 1;
     return PGMG_OK;
+}
+
+// Segment planning (one GPU).  spec_mark_levels sends a level in-stream for the whole
+// segment as soon as its norm is predicted to fall under 100 eps anywhere in it, so a long
+// call (the 3 + 40 cycles of BASELINE configs[1] at N = 4097: the coarse levels cross at
+// ~27 cycles) decided every coarse check in-stream from its first cycle -- two launches of
+// ~5 us per level and cycle.  Instead the segment ends just before the first such crossing
+// (the levels speculate until then and go in-stream at the next segment) when that pays for
+// the split: ~10 us per affected level and cycle saved against one more finest-level pass
+// (the cross-fused call restarts: k_post + k_pre instead of one k_postpre, 16 B per fine
+// point at ~5 TB/s) and one host round trip of the validation.
+static int spec_plan_segment(const pgmg_ctx *c, int seg)
+{
+    if (seg < 4 || (c->cfg.flags & PGMG_FLAG_NO_SPEC_FIRE)) return seg;
+    // a new problem: a short first segment gathers every level's trend (without one, a long
+    // first call speculated blind and rolled back at the first firing check, ~27 cycles in
+    // on the reference problem); history sizes are the same on every rank
+    if (seg > 8)
+        for (int l = 1; l < c->nb; ++l)
+            if (c->lvl_hist[l].size() < 2 && !c->lvl_exact[l]) return 3;
+    if (c->comm != nullptr) return seg;   // (strips: every rank must agree)
+    const double lim = c->cfg.eps * 100.0, flim = c->cfg.eps * 0.25;
+    // cycles until last * rho^k falls below t
+    auto cycles_to = [](double last, double rho, double t) {
+        return last > t ? (int)std::floor(std::log(t / last) / std::log(rho)) : 0;
+    };
+    // candidate split points: a speculating level's crossing of 100 eps (it speculates until
+    // then instead of deciding in-stream for the whole segment), an in-stream level's last
+    // cycle before it can be predicted to fire (its norm under eps / 4 for two visits)
+    std::vector<std::pair<int, int>> cand;   // (cycle, 0: speculating / 1: to fire)
+    for (int l = 1; l < c->nb; ++l) {
+        double last, rho;
+        if (c->lvl_fire[l] || !spec_level_trend(c, l, &last, &rho)) continue;
+        bool exact = c->lvl_exact[l] != 0;
+        if (!exact) {
+            const int k = cycles_to(last, rho, lim);
+            if (k >= seg) continue;
+            if (k >= 2) cand.push_back({k, 0});
+            else exact = true;   // in-stream from this segment on
+        }
+        if (exact && !c->lvl_fire_block[l]) {
+            // (the decay slows near eps: ~0.7 per cycle on the reference problem, where the
+            // steep phase shows ~0.33; a split that comes too early costs without paying)
+            const int k = cycles_to(last, std::max(rho, 0.7), flim) + 2;
+            if (k < seg) cand.push_back({std::max(k, 2), 1});
+        }
+    }
+    // level-cycles that avoid two in-stream launches (~10 us each) if the segment ends at
+    // k: a speculating level crossing at or after k speculates k cycles instead of deciding
+    // in-stream for the whole segment (one crossing before k is marked in-stream from the
+    // start either way); a level that can be predicted to fire by k does so for seg - k
+    int best_k = seg;
+    double best = 0.0;
+    for (const auto &q : cand) {
+        const int k = q.first;
+        double saved = 0.0;
+        for (const auto &p : cand)
+            saved += p.second == 0 ? (p.first >= k ? k : 0) : (p.first <= k ? seg - k : 0);
+        if (saved > best) {
+            best = saved;
+            best_k = k;
+        }
+    }
+    const double N0 = (double)c->lv[0].N;
+    const double cost = 16.0 * N0 * N0 / 5e12 + 60e-6;
+    return best * 10e-6 > cost ? best_k : seg;
 }
 
 static void spec_record_norms(pgmg_ctx *c, int n)
@@ -1468,7 +1588,7 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
     void *const ext_out = c->x_out;
     bool first = true;
     while (ncycles > 0) {
-        const int seg = (int)std::min<long long>(ncycles, seg_max);
+        const int seg = spec_plan_segment(c, (int)std::min<long long>(ncycles, seg_max));
         c->x_in = first ? ext_in : nullptr;
         c->x_out = ext_out;
         int e = spec_reserve(c, seg * per_dbl + 2LL * np0 + 64, seg * per_chk + 4);
@@ -1523,8 +1643,16 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
             ++c->rollbacks;
             for (int i = 0; i < n; ++i)
                 if (c->hflag[i] || overflow) {
-                    if (c->chks[i].level == 0) c->spec_off = true;
-                    else c->lvl_exact[c->chks[i].level] = 1;
+                    const int l = c->chks[i].level;
+                    if (l == 0) {
+                        c->spec_off = true;
+                    } else {
+                        c->lvl_exact[l] = 1;
+                        if (c->chks[i].expect == 1) {   // a "fires" prediction failed
+                            c->lvl_fire[l] = 0;
+                            c->lvl_fire_block[l] = 1;
+                        }
+                    }
                 }
             L0.A = A0;
             L0.B = B0;
@@ -1599,8 +1727,18 @@ int pgmg_spec_levels(pgmg_ctx *c, unsigned long long *in_stream)
     if (!c || !in_stream) return set_err(PGMG_ERR_ARG, "null argument");
     unsigned long long m = (!c->spec || c->spec_off) ? 1ull : 0ull;
     for (int l = 1; l < (int)c->lvl_exact.size() && l < 64; ++l)
-        if (c->lvl_exact[l]) m |= 1ull << l;
+        if (c->lvl_exact[l] || c->lvl_fire[l]) m |= 1ull << l;
     *in_stream = m;
+    return PGMG_OK;
+}
+
+int pgmg_spec_fire_levels(pgmg_ctx *c, unsigned long long *fire)
+{
+    if (!c || !fire) return set_err(PGMG_ERR_ARG, "null argument");
+    unsigned long long m = 0;
+    for (int l = 1; l < (int)c->lvl_fire.size() && l < 64; ++l)
+        if (c->lvl_fire[l]) m |= 1ull << l;
+    *fire = m;
     return PGMG_OK;
 }
 

@@ -202,7 +202,10 @@ __device__ __forceinline__ void row_loop(int i_begin, int i_end, const FullAt &f
 // S1 (rare path of an in-stream check, k_pre_rare): the check after the first sweep fired,
 // so the pass is redone with ONE sweep — x1 stored instead of x2, rc = R r(x1) — and
 // writes no partial sums and no sweep count (the decision kernel's job)
-template <class T, bool X0_ZERO, bool FINE, int PAIRS, bool GENF, bool PIN, bool S1>
+// S1P (a pre check predicted to fire, k_pre1): the S1 pass that also writes the per-block
+// partials of the check's r(x1)^2 (the same terms, rows and order as the full pass), so the
+// speculative call's validation can confirm the prediction
+template <class T, bool X0_ZERO, bool FINE, int PAIRS, bool GENF, bool PIN, bool S1, bool S1P = false>
 __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red)
 {
     constexpr int R = 2 * PAIRS;  // rows loaded per iteration (and prefetched ahead)
@@ -336,6 +339,13 @@ __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red)
                     // x1 row ii-1 is the result; restriction of r(x1): rows ii-4, ii-3, ii-2 =
                     // 2jc-1, 2jc, 2jc+1 when ii is odd
                     if (store && ii - 1 >= olo && ii - 1 < ohi && k.own) stv(O + (ii - 1) * P, b2);
+                    if constexpr (S1P) {   // the check's terms: r(x1) on row ii-2
+                        const int row = ii - 2;
+                        if (row >= olo && row < ohi && k.own) {
+                            acc = sqacc(acc, r1.x);
+                            if (!k.by) acc = sqacc(acc, r1.y);
+                        }
+                    }
                     if ((s & 1) == 1) {
                         const int jc = (ii - 3) >> 1;
                         const T m2 = dpp_shl(q1.x);
@@ -403,7 +413,7 @@ __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red)
     };
     // (PIN: the 12-row form needs 170 VGPRs, past the 168 of 3 waves per SIMD)
     row_loop<R, PIN ? 0 : 3>(i_begin, i_end, full_at, iter);
-    if constexpr (!S1) {
+    if constexpr (!S1 || S1P) {
         const double sum = fused_block_sum(acc, red);
         if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = sum;
     }
@@ -414,6 +424,24 @@ __global__ __launch_bounds__(256) void k_pre(PreArgsT<T> a)
 {
     __shared__ double red[4];
     pre_body<T, X0_ZERO, FINE, PAIRS, GENF, PIN, false>(a, red);
+}
+
+// A coarse level's pre-smooth whose check is predicted to fire (speculative calls, levels that
+// converged: pgmg_ctx.hip "predicted to fire"): x1 = J(0) is the result, rc = R r(x1), one
+// sweep and one exit booked, the "pre fired" flag the level's k_post reads set -- what k_pre +
+// k_pre_rare compute when the check fires, in one launch; the partials confirm it afterwards
+template <class T, int PAIRS>
+__global__ __launch_bounds__(256) void k_pre1(PreArgsT<T> a)
+{
+    __shared__ double red[4];
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+        if (a.fired != nullptr) *a.fired = 1u;
+        if (a.stats != nullptr) {
+            atomicAdd(&a.stats[0], 1ull);
+            atomicAdd(&a.stats[1], 1ull);
+        }
+    }
+    pre_body<T, true, false, PAIRS, false, false, true, true>(a, red);
 }
 
 // Decision of an in-stream early-exit check from the partial sums of the pass just run
@@ -458,7 +486,7 @@ __global__ __launch_bounds__(256) void k_pre_rare(PreArgsT<T> a, FixArgsF f)
 // RECOMP (levels entered with x0 = 0): phi is not read.  The loaded row is f[ii+1];
 // x1 = J(0) is pointwise, so x1 row ii+1 -> phi row ii = J(x1) (or x1 when the pre
 // check fired) -> x_eff row ii: one more row of lag than reading phi, 16 B/point less.
-template <class T, bool FINE, int PAIRS, bool RECOMP, bool GENF, bool S1>
+template <class T, bool FINE, int PAIRS, bool RECOMP, bool GENF, bool S1, bool S1P = false>
 __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
 {
     constexpr int R = 2 * PAIRS;
@@ -577,6 +605,16 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
                 const V2<T> b2 = jstage<T, !FULL>(a0, a1, a2, f2, hh, k, boundary_row(ii - 1, N));
                 if constexpr (S1) {   // the post check fired: x1 row ii-1 is the result
                     if (ii - 1 >= olo && ii - 1 < ohi && k.own) stvu(O + (ii - 1) * Po, b2);
+                    if constexpr (S1P) {   // the check's terms: r(x1) on row ii-2 (k_post1)
+                        const int row = ii - 2;
+                        const V2<T> r1 = rstage(b0, b1, b2, f1, ih);
+                        if (row >= slo && row < shi && k.own) {
+                            acc = sqacc(acc, r1.x);
+                            if (!k.by) acc = sqacc(acc, r1.y);
+                        }
+                        b0 = b1;
+                        b1 = b2;
+                    }
                     a0 = a1;
                     a1 = a2;
                     f1 = f2;
@@ -609,7 +647,7 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
     // 150 -> 210 VGPRs, i.e. 3 -> 2 waves per SIMD, and measured slower; hoisting the pre
     // check's outcome out of the loop measured no gain)
     row_loop<R, 0>(i_begin, i_end, full_at, iter);
-    if constexpr (!S1) {
+    if constexpr (!S1 || S1P) {
         const double sum = fused_block_sum(acc, red);
         if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = sum;
     }
@@ -620,6 +658,20 @@ __global__ __launch_bounds__(256) void k_post(PostArgsT<T> a)
 {
     __shared__ double red[4];
     post_body<T, FINE, PAIRS, RECOMP, GENF, false>(a, red);
+}
+
+// a coarse level's post-smooth whose check is predicted to fire (see k_pre1): x1 is the
+// result (RECOMP: the pre-smoothed iterate recomputed as the pre check decided), one sweep and
+// one exit booked, the check's partials written
+template <class T, int PAIRS>
+__global__ __launch_bounds__(256) void k_post1(PostArgsT<T> a)
+{
+    __shared__ double red[4];
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.stats != nullptr) {
+        atomicAdd(&a.stats[0], 1ull);
+        atomicAdd(&a.stats[1], 1ull);
+    }
+    post_body<T, false, PAIRS, true, false, true, true>(a, red);
 }
 
 // rare path of k_post's check (replaces the scalar k_post_fixup on in-stream levels)
@@ -1550,7 +1602,13 @@ __global__ __launch_bounds__(256) void k_verify_checks(const CheckRef *checks, d
     for (long long k = threadIdx.x; k < c.np; k += blockDim.x) s += c.partials[k];
     s = fused_block_sum(s, red);
     if (threadIdx.x == 0) {
-        out[blockIdx.x] = (sqrt(s) < eps * (1.0 + 1e-12)) ? 1u : 0u;
+        // flag = the prediction may be wrong: "does not fire" checks that could fire, "fires"
+        // checks that could not (same margin the other way); in-stream checks are logged
+        // for the norms only
+        const bool could_fire = sqrt(s) < eps * (1.0 + 1e-12);
+        const bool must_fire = sqrt(s) < eps * (1.0 - 1e-12);
+        out[blockIdx.x] = c.expect == 0 ? (could_fire ? 1u : 0u)
+                                        : (c.expect == 1 ? (must_fire ? 0u : 1u) : 0u);
         norm[blockIdx.x] = sqrt(s);
     }
 }
@@ -1811,6 +1869,36 @@ int launch_post_rare(const FixArgsF &f, const PostArgsT<T> &a0, hipStream_t s)
     return PGMG_OK;
 }
 
+// the predicted-to-fire passes of a coarse level entered with x0 = 0 (RECOMP): the full
+// passes' geometry and spans, f from memory
+template <class T>
+int launch_pre1(const PreArgsT<T> &a0, hipStream_t s)
+{
+    int t, gx, gy, r;
+    fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r);
+    if (const int e = pre_spans(a0, t, gx, r, false, true)) return e;
+    PreArgsT<T> a = a0;
+    a.rows_per_block = r;
+    a.gfx = a.gsy = nullptr;
+    a.nt = 0;
+    k_pre1<T, 2><<<dim3(gx, gy), dim3(t), 0, s>>>(a);
+    return PGMG_OK;
+}
+
+template <class T>
+int launch_post1(const PostArgsT<T> &a0, hipStream_t s)
+{
+    int t, gx, gy, r;
+    fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r);
+    if (const int e = post_spans(a0, t, gx, r, true)) return e;
+    PostArgsT<T> a = a0;
+    a.rows_per_block = r;
+    a.gfx = a.gsy = nullptr;
+    a.nt = 0;
+    k_post1<T, 2><<<dim3(gx, gy), dim3(t), 0, s>>>(a);
+    return PGMG_OK;
+}
+
 template <class T>
 void launch_pre_fixup(const FixArgsF &a, const PreArgsT<T> &p, bool x0_zero, hipStream_t s)
 {
@@ -1826,6 +1914,8 @@ void launch_post_fixup(const FixArgsF &a, const PostArgsT<T> &p, hipStream_t s)
 
 #define PGMG_INSTANTIATE(T)                                                                       \
     template int launch_pre<T>(const PreArgsT<T> &, bool, bool, hipStream_t);                   \
+    template int launch_pre1<T>(const PreArgsT<T> &, hipStream_t);                              \
+    template int launch_post1<T>(const PostArgsT<T> &, hipStream_t);                            \
     template int launch_post<T>(const PostArgsT<T> &, bool, hipStream_t);                       \
     template int launch_postpre<T>(const PostPreArgsT<T> &, hipStream_t);                       \
     template int launch_smooth4<T>(const PostPreArgsT<T> &, hipStream_t);                        \

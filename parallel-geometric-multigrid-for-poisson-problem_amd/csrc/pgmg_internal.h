@@ -57,7 +57,7 @@ struct CheckRef {
     const double *partials;
     long long np;
     int level;   // host bookkeeping (per-level speculation policy)
-    int pad;
+    int expect;  // 0: recorded as "does not fire", 1: as "fires", 2: decided in-stream (norm only)
 };
 
 constexpr int kOff = 15;          // doubles between allocation base and element (0,0) (fp64)

@@ -1,0 +1,85 @@
+"""Speculative calls on converged coarse levels (pgmg_ctx.hip "predicted to fire", "segment
+planning"), against the same solver with every check decided in-stream (PGMG_FLAG_EXACT_DIST).
+
+On the reference problem the bulk levels above the tail reach eps after ~27 V-cycles and from
+then on fire at every check.  A speculative call ends its segment just before a level's
+predicted crossing (the level speculates until then), decides the crossing levels in-stream,
+and once a level's last two visits were below eps / 4 it is enqueued with its checks
+predicted to FIRE (k_pre1 / k_post1, one launch each instead of a pass plus a rare path),
+confirmed by the validation; a failed prediction rolls the call back.  Tolerance: EXACT
+(bitwise phi, equal sweep and exit counts).
+"""
+import numpy as np
+import pytest
+
+from conftest import assert_bitwise
+
+pytestmark = pytest.mark.gpu
+
+
+def _calls(pgmg, N, calls, flags=0):
+    with pgmg.Solver(N, flags=flags) as s:
+        s.set_problem()
+        masks = []
+        for n in calls:
+            s.vcycle(n)
+            masks.append(s.spec_fire_levels())
+        return s.solution(), s.stats_detail(), s.dist_info(), masks
+
+
+@pytest.mark.parametrize("N,calls", [(2049, [3, 40]), (4097, [3, 40]), (2049, [60]),
+                                     (2049, [1] * 45), (2049, [7] * 8), (4097, [5, 20, 20])])
+def test_fire_prediction_bitwise(pgmg, N, calls):
+    phi, det, info, masks = _calls(pgmg, N, calls)
+    ref, rdet, _, _ = _calls(pgmg, N, calls, flags=pgmg.PGMG_FLAG_EXACT_DIST)
+    assert_bitwise(phi, ref, f"N={N} calls={calls}")
+    assert det == rdet
+    assert info[0] and info[1] == 0, info      # speculative, never rolled back
+    if N == 2049 and sum(calls) >= 43:       # (129 / 257 fire from cycles 27 / 30 there)
+        assert masks[-1] & ~1, masks            # converged coarse levels predicted to fire
+
+
+def test_fire_prediction_golden(pgmg, plan, golden_cycles):
+    """The reference's own 30-cycle hashes and sweep counts at N = 513 with the cross-fused
+    speculative path (cross_min_n = 9): one call, calls of 10 and calls of 1."""
+    plan(cross_min_n=9)
+    case = next(c for c in golden_cycles if c["kind"] == "V" and c["N"] == 513
+                and c["eps"] == 1e-7 and len(c["cycles"]) >= 30)
+    want = case["cycles"][29]
+    for calls in ([30], [10, 10, 10], [1] * 30, [3, 27]):
+        with pgmg.Solver(513) as s:
+            s.set_problem()
+            for n in calls:
+                s.vcycle(n)
+            assert s.solution_hash(0) == want["hash"], calls
+            assert s.stats()[0] == want["sweeps"], calls
+
+
+def test_failed_fire_prediction_rolls_back(pgmg, oracle_mod):
+    """A device-bound problem whose right-hand side the caller changes between calls: after
+    the coarse levels converged (predicted to fire), f gets a large random perturbation in
+    place, so the next call's "fires" predictions fail -- the call is rolled back and rerun
+    in-stream, bitwise the in-stream solver's result."""
+    import torch
+    N = 2049
+    f0 = oracle_mod.Oracle().rhs(N)
+    rng = np.random.default_rng(3)
+    bump = torch.tensor(rng.uniform(-1, 1, (N, N)), device="cuda:0")
+    out = []
+    for flags in (0, pgmg.PGMG_FLAG_EXACT_DIST):
+        phi = torch.zeros((N, N), dtype=torch.float64, device="cuda:0")
+        f = torch.tensor(f0, device="cuda:0")
+        with pgmg.Solver(N, flags=flags) as s:
+            s.set_problem_device(phi, f)
+            for _ in range(12):
+                s.vcycle(4)
+            fire = s.spec_fire_levels()
+            f.add_(bump)
+            torch.cuda.synchronize()
+            s.vcycle(4)
+            out.append((phi.cpu().numpy(), s.stats_detail(), s.dist_info(), fire))
+    (a, da, ia, fire), (b, db, _, _) = out
+    assert fire & ~1, bin(fire)
+    assert ia[1] >= 1, ia
+    assert_bitwise(a, b, "after the rollback")
+    assert da == db
