@@ -557,47 +557,49 @@ template <int CTRL> __device__ __forceinline__ float dpp_row(float v)
 }
 
 // The coarsest solve (JacobiSmoother::smooth with coarse_iter, Smoother.hpp:38-116) of a 5x5
-// level held in registers: lane q < 9 owns interior point (1 + q/3, 1 + q%3), the other
-// lanes hold 0 (the Dirichlet boundary); left/right/up/down neighbours are DPP moves by
-// 1 and 3 lanes inside DPP row 0 (no LDS round trip per sweep).  Same expressions, operand
-// order and fused speculative check as tail_smooth_small; the check's sum over lanes 0..8
-// is the same row scan wave_sum does, so the decisions are identical.
+// level held in registers: lane q = 4 (jc - 1) + (ic - 1) owns interior point (jc, ic) for
+// ic <= 3 (q & 3 < 3, q < 12: lanes 0-2, 4-6, 8-10); every other lane holds +0 -- the Dirichlet
+// boundary -- so the left/right/up/down neighbours are plain DPP moves by 1 and 4 lanes inside
+// DPP row 0 (a boundary neighbour is a padding lane, or a lane past the row, which bound_ctrl
+// reads as +0: the same +0 the reference adds), with no boundary selects and no LDS round trip
+// per sweep.  Same expressions, operand order and fused speculative check as
+// tail_smooth_small; the check's sum over the row is the same row scan wave_sum does.
+__device__ __forceinline__ int c5_lane(int jc, int ic) { return 4 * (jc - 1) + (ic - 1); }
+__device__ __forceinline__ bool c5_act(int lane) { return lane < 12 && (lane & 3) < 3; }
+
+template <class Real>
+__device__ __forceinline__ void c5_nbrs(Real v, Real *o)
+{
+    o[0] = dpp_row<0x111>(v);   // row_shr:1: left (lane q-1)
+    o[1] = dpp_row<0x101>(v);   // row_shl:1: right (lane q+1)
+    o[2] = dpp_row<0x114>(v);   // row_shr:4: up (lane q-4; lanes 0..3: +0)
+    o[3] = dpp_row<0x104>(v);   // row_shl:4: down (lane q+4)
+    // all four moves with every lane active (the padding lanes' +0 is read, not assumed)
+    __asm__ volatile("" : "+v"(o[0]), "+v"(o[1]), "+v"(o[2]), "+v"(o[3]));
+}
+
 template <class Real>
 __device__ __forceinline__ Cnt tail_coarse5_regs(Real &x, Real f, const TailLevel<Real> L,
                                                  int num_iter, double eps2)
 {
     const int lane = threadIdx.x & 63;
-    const bool act = lane < 9;
-    const int ii = lane - 3 * (lane / 3);
-    const bool has_l = ii != 0, has_r = ii != 2;
+    const bool act = c5_act(lane);
     const Real hh = L.hh, ih = L.ih, hf = hh * f;
     Real xv = x;
     int sweeps = 1, exits = 0;
-    // the four moves with every lane active (a DPP move under an exec mask reads 0 from
-    // the disabled source lanes, so none may be sunk into the has_l / has_r selects)
-    auto nbrs = [&](Real v, Real *o) __attribute__((always_inline)) {
-        o[0] = dpp_row<0x111>(v);   // row_shr:1: lane q-1
-        o[1] = dpp_row<0x101>(v);   // row_shl:1: lane q+1
-        o[2] = dpp_row<0x113>(v);   // row_shr:3: lane q-3 (lanes 0..2: 0)
-        o[3] = dpp_row<0x103>(v);   // row_shl:3: lane q+3 (lanes 9..11 hold 0)
-        __asm__ volatile("" : "+v"(o[0]), "+v"(o[1]), "+v"(o[2]), "+v"(o[3]));
-        if (!has_l) o[0] = Real(0);
-        if (!has_r) o[1] = Real(0);
-    };
     {
         Real o[4];
-        nbrs(xv, o);
-        const Real l = o[0], r = o[1], u = o[2], dn = o[3];
-        const Real nx = Real(0.25) * (hf + l + r + u + dn);
+        c5_nbrs(xv, o);
+        const Real nx = Real(0.25) * (hf + o[0] + o[1] + o[2] + o[3]);
         xv = act ? nx : Real(0);
     }
     for (int it = 2; it <= num_iter + 1; ++it) {
         Real o[4];
-        nbrs(xv, o);
-        const Real l = o[0], r = o[1], u = o[2], dn = o[3];
-        const Real res = f - ih * (Real(4) * xv - l - r - u - dn);
-        double acc = act ? sq(res) : 0.0;
-        const Real nx = Real(0.25) * (hf + l + r + u + dn);
+        c5_nbrs(xv, o);
+        const Real res = f - ih * (Real(4) * xv - o[0] - o[1] - o[2] - o[3]);
+        const double r2 = sq(res);
+        double acc = act ? r2 : 0.0;
+        const Real nx = Real(0.25) * (hf + o[0] + o[1] + o[2] + o[3]);
         acc += dpp64<0x111>(acc);   // row_shr:1,2,4,8: lane 15 holds the total of row 0
         acc += dpp64<0x112>(acc);
         acc += dpp64<0x114>(acc);
@@ -622,44 +624,39 @@ __device__ __forceinline__ Cnt tail_coarse5_regs(Real &x, Real f, const TailLeve
 // second cycle on).  So the fast path computes x_1 .. x_gamma back to back — the sweeps are
 // the only dependent chain — with their gamma checks beside them, and keeps x_gamma when all
 // of them fire (gamma sweeps, gamma exits: exactly the sequential calls' work and counters);
-// otherwise the calls run one by one from the untouched x_0.
-template <class Real>
+// otherwise the calls run one by one from the untouched x_0.  GAMMA: the W-cycle's alpha = 3
+// at compile time (no run-time trip count on the chain), 0 = any.
+template <class Real, int GAMMA>
 __device__ __forceinline__ Cnt tail_coarse5_gamma(Real &x, Real f, const TailLevel<Real> L,
                                                   int num_iter, double eps2, int gamma)
 {
-    if (gamma <= 3 && num_iter >= 1) {
+    const int G = GAMMA > 0 ? GAMMA : gamma;
+    if (G <= 3 && num_iter >= 1) {
         const int lane = threadIdx.x & 63;
-        const bool act = lane < 9;
-        const int ii = lane - 3 * (lane / 3);
-        const bool has_l = ii != 0, has_r = ii != 2;
+        const bool act = c5_act(lane);
         const Real hh = L.hh, ih = L.ih, hf = hh * f;
-        auto nbrs = [&](Real v, Real *o) __attribute__((always_inline)) {
-            o[0] = dpp_row<0x111>(v);
-            o[1] = dpp_row<0x101>(v);
-            o[2] = dpp_row<0x113>(v);
-            o[3] = dpp_row<0x103>(v);
-            __asm__ volatile("" : "+v"(o[0]), "+v"(o[1]), "+v"(o[2]), "+v"(o[3]));
-            if (!has_l) o[0] = Real(0);
-            if (!has_r) o[1] = Real(0);
-        };
         // x_k's neighbours serve both its check r(x_k) and the next sweep J(x_k); the gamma
         // checks are summed per lane and reduced ONCE: every lane's sum bounds each of its
         // terms and the DPP reduction tree is the same for both, so (fl(a + b) is monotone in
         // a and b) the reduced total bounds every reduced check sum — a total below eps2
         // means every check fires; otherwise the exact sequential calls decide
         Real o[4];
-        nbrs(x, o);
+        c5_nbrs(x, o);
         const Real x1 = act ? Real(0.25) * (hf + o[0] + o[1] + o[2] + o[3]) : Real(0);
         Real xk = x1, xl = x1;
         double acc = 0.0;
         #pragma unroll
         for (int g = 1; g <= 3; ++g) {
-            if (g > gamma) break;
-            nbrs(xk, o);
+            if (g > G) break;
+            c5_nbrs(xk, o);
             const Real res = f - ih * (Real(4) * xk - o[0] - o[1] - o[2] - o[3]);
-            acc += act ? sq(res) : 0.0;
+            const double r2 = sq(res);
+            acc += act ? r2 : 0.0;
             xl = xk;
-            if (g < gamma) xk = act ? Real(0.25) * (hf + o[0] + o[1] + o[2] + o[3]) : Real(0);
+            if (g < G) {
+                const Real nx = Real(0.25) * (hf + o[0] + o[1] + o[2] + o[3]);
+                xk = act ? nx : Real(0);
+            }
         }
         acc += dpp64<0x111>(acc);
         acc += dpp64<0x112>(acc);
@@ -667,11 +664,11 @@ __device__ __forceinline__ Cnt tail_coarse5_gamma(Real &x, Real f, const TailLev
         acc += dpp64<0x118>(acc);
         if (readlane64(acc, 15) < eps2) {
             x = xl;
-            return Cnt{gamma, gamma};
+            return Cnt{G, G};
         }
     }
     Cnt c;
-    for (int g = 0; g < gamma; ++g) c += tail_coarse5_regs(x, f, L, num_iter, eps2);
+    for (int g = 0; g < G; ++g) c += tail_coarse5_regs(x, f, L, num_iter, eps2);
     return c;
 }
 
@@ -694,9 +691,10 @@ __device__ __forceinline__ Cnt tail_w9(const TailArgsDev<Real> &d, int l, int re
     const int jj = lane / 7, ii = lane - 7 * jj;
     const bool in9 = lane < 49;
     const int k9 = in9 ? (1 + jj) * 9 + 1 + ii : 10;
-    // coarse lane q < 9: (jc, ic) = (1 + q/3, 1 + q%3), fine centre (2jc, 2ic)
-    const int jc = 1 + lane / 3, ic = 1 + lane - 3 * (lane / 3);
-    const int kc = lane < 9 ? (2 * jc) * 9 + 2 * ic : 20;
+    // coarse lane q (c5_act): (jc, ic) = (1 + q/4, 1 + q%4), fine centre (2jc, 2ic)
+    const bool cact = c5_act(lane);
+    const int jc = 1 + (lane >> 2), ic = 1 + (lane & 3);
+    const int kc = cact ? (2 * jc) * 9 + 2 * ic : 20;
     const double eps2 = d.eps2;
     const int gamma = d.gamma;
     auto fence = [] {
@@ -761,16 +759,17 @@ __device__ __forceinline__ Cnt tail_w9(const TailArgsDev<Real> &d, int l, int re
     auto rest = [&](Cnt &c) __attribute__((always_inline)) {
         // rc = R r (MultiGrid.hpp:187-205); e_coarse = 0 (:81-82)
         Real fc = Real(0), ec = Real(0);
-        if (lane < 9)
+        if (cact)
             fc = Real(0.25) * T[kc] + Real(0.125) * (T[kc + 1] + T[kc - 1] + T[kc + 9] + T[kc - 9]) +
                  Real(0.0625) * (T[kc - 9 - 1] + T[kc - 9 + 1] + T[kc + 9 - 1] + T[kc + 9 + 1]);
         stamp(1);
-        c += tail_coarse5_gamma(ec, fc, L5, a.coarse_iter, eps2, gamma);
+        c += gamma == 3 ? tail_coarse5_gamma<Real, 3>(ec, fc, L5, a.coarse_iter, eps2, gamma)
+                        : tail_coarse5_gamma<Real, 0>(ec, fc, L5, a.coarse_iter, eps2, gamma);
         stamp(2);
         // the correction into LDS (5x5, boundary 0), then x += P e on [2, 7]^2 (:208-226)
         if (lane < 25) e5[lane] = Real(0);
         fence();
-        if (lane < 9) e5[jc * 5 + ic] = ec;
+        if (cact) e5[jc * 5 + ic] = ec;
         fence();
         {
             const Real w = pweight(e5, pg9, 5);
