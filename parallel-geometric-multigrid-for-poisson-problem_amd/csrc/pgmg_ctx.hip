@@ -1057,6 +1057,7 @@ static int problem_reset(pgmg_ctx *c)
     c->lvl_exact.assign(c->nb + 1, 0);
     c->lvl_fire.assign(c->nb + 1, 0);
     c->lvl_fire_block.assign(c->nb + 1, 0);
+    c->lvl_fire_try.assign(c->nb + 1, 0.0);
     c->lvl_hist.assign(c->nb + 1, std::vector<double>());
     return PGMG_OK;
 }
@@ -1469,6 +1470,12 @@ static int spec_mark_levels(pgmg_ctx *c, int cycles)
             else if (m >= 2 && h[m - 1] < c->cfg.eps) c->lvl_exact[l] = 1;   // fired: in-stream
         }
     }
+    if (tuning_int("PGMG_SPEC_TRACE", 0))
+        for (int l = 1; l < c->nb; ++l)
+            fprintf(stderr, "spec level %d N=%d hist %zu last %.3e exact %d fire %d block %d\n", l,
+                    c->lv[l].N, c->lvl_hist[l].size(),
+                    c->lvl_hist[l].empty() ? -1.0 : c->lvl_hist[l].back(), (int)c->lvl_exact[l],
+                    (int)c->lvl_fire[l], (int)c->lvl_fire_block[l]);
     std::vector<unsigned> keep(c->nb + 1, 1u);   // 1 = keep speculating
     for (int l = 1; l < c->nb; ++l) {
         double last, rho;   // min over the last visit; decay per cycle
@@ -1501,7 +1508,7 @@ static int spec_mark_levels(pgmg_ctx *c, int cycles)
 // the split: ~10 us per affected level and cycle saved against one more finest-level pass
 // (the cross-fused call restarts: k_post + k_pre instead of one k_postpre, 16 B per fine
 // point at ~5 TB/s) and one host round trip of the validation.
-static int spec_plan_segment(const pgmg_ctx *c, int seg)
+static int spec_plan_segment(pgmg_ctx *c, int seg)
 {
     if (seg < 4 || (c->cfg.flags & PGMG_FLAG_NO_SPEC_FIRE)) return seg;
     // a new problem: a short first segment gathers every level's trend (without one, a long
@@ -1519,7 +1526,11 @@ static int spec_plan_segment(const pgmg_ctx *c, int seg)
     // candidate split points: a speculating level's crossing of 100 eps (it speculates until
     // then instead of deciding in-stream for the whole segment), an in-stream level's last
     // cycle before it can be predicted to fire (its norm under eps / 4 for two visits)
-    std::vector<std::pair<int, int>> cand;   // (cycle, 0: speculating / 1: to fire)
+    struct Cand {
+        int k, kind, level;   // kind 0: speculating until k, 1: predicted to fire from k
+        double norm;
+    };
+    std::vector<Cand> cand;
     for (int l = 1; l < c->nb; ++l) {
         double last, rho;
         if (c->lvl_fire[l] || !spec_level_trend(c, l, &last, &rho)) continue;
@@ -1527,14 +1538,23 @@ static int spec_plan_segment(const pgmg_ctx *c, int seg)
         if (!exact) {
             const int k = cycles_to(last, rho, lim);
             if (k >= seg) continue;
-            if (k >= 2) cand.push_back({k, 0});
+            if (k >= 2) cand.push_back({k, 0, l, last});
             else exact = true;   // in-stream from this segment on
         }
         if (exact && !c->lvl_fire_block[l]) {
+            // the fire test looks at the LARGER check norm of a visit: its decay; a level whose
+            // norm stagnates (the one above the finest typically hovers at 0.5-1 eps for good)
+            // or that already had a split at a similar norm gets none
+            const std::vector<double> &h = c->lvl_hist[l];
+            const size_t m = h.size();
+            const double ml = std::max(h[m - 1], h[m - 2]);
+            const double mp = m >= 4 ? std::max(h[m - 3], h[m - 4]) : 0.0;
+            const double rm = mp > 0.0 ? ml / mp : 1.0;
+            if (rm > 0.9 || (c->lvl_fire_try[l] > 0.0 && ml > 0.5 * c->lvl_fire_try[l])) continue;
             // (the decay slows near eps: ~0.7 per cycle on the reference problem, where the
             // steep phase shows ~0.33; a split that comes too early costs without paying)
-            const int k = cycles_to(last, std::max(rho, 0.7), flim) + 2;
-            if (k < seg) cand.push_back({std::max(k, 2), 1});
+            const int k = cycles_to(ml, std::max(rm, 0.7), flim) + 2;
+            if (k < seg) cand.push_back({std::max(k, 2), 1, l, ml});
         }
     }
     // level-cycles that avoid two in-stream launches (~10 us each) if the segment ends at
@@ -1544,10 +1564,10 @@ static int spec_plan_segment(const pgmg_ctx *c, int seg)
     int best_k = seg;
     double best = 0.0;
     for (const auto &q : cand) {
-        const int k = q.first;
+        const int k = q.k;
         double saved = 0.0;
         for (const auto &p : cand)
-            saved += p.second == 0 ? (p.first >= k ? k : 0) : (p.first <= k ? seg - k : 0);
+            saved += p.kind == 0 ? (p.k >= k ? k : 0) : (p.k <= k ? seg - k : 0);
         if (saved > best) {
             best = saved;
             best_k = k;
@@ -1555,7 +1575,13 @@ static int spec_plan_segment(const pgmg_ctx *c, int seg)
     }
     const double N0 = (double)c->lv[0].N;
     const double cost = 16.0 * N0 * N0 / 5e12 + 60e-6;
-    return best * 10e-6 > cost ? best_k : seg;
+    if (tuning_int("PGMG_SPEC_TRACE", 0))
+        fprintf(stderr, "spec plan: seg %d, %zu candidates, best split %d saves %.0f us vs %.0f us\n",
+                seg, cand.size(), best_k, best * 10.0, cost * 1e6);
+    if (!(best * 10e-6 > cost)) return seg;
+    for (const auto &p : cand)
+        if (p.kind == 1 && p.k <= best_k) c->lvl_fire_try[p.level] = p.norm;
+    return best_k;
 }
 
 static void spec_record_norms(pgmg_ctx *c, int n)

@@ -1,0 +1,26 @@
+"""Segment planning and predicted-to-fire trace of one long call (PGMG_SPEC_TRACE=1, needs the
+measurement build libpgmg_ab.so via PGMG_LIB): python scripts/spec_fire_trace.py N CYCLES"""
+import os
+import pathlib
+import sys
+import time
+
+os.environ["PGMG_SPEC_TRACE"] = "1"
+sys.path.insert(0, str(pathlib.Path(__file__).resolve().parents[1]))
+import torch  # noqa: F401,E402
+import _pkgload  # noqa: E402
+
+pg = _pkgload.load()
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 2049
+K = int(sys.argv[2]) if len(sys.argv) > 2 else 200
+with pg.Solver(N) as s:
+    s.set_problem()
+    s.vcycle(3)
+    s.sync()
+    print("--- long call", file=sys.stderr, flush=True)
+    t0 = time.perf_counter()
+    s.vcycle(K)
+    s.sync()
+    dt = time.perf_counter() - t0
+    print(f"N={N} K={K} {K / dt:.1f} V/s fire={bin(s.spec_fire_levels())} "
+          f"spec={bin(s.spec_levels())} dist={s.dist_info()}", file=sys.stderr, flush=True)

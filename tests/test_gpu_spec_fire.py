@@ -35,7 +35,9 @@ def test_fire_prediction_bitwise(pgmg, N, calls):
     assert_bitwise(phi, ref, f"N={N} calls={calls}")
     assert det == rdet
     assert info[0] and info[1] == 0, info      # speculative, never rolled back
-    if N == 2049 and sum(calls) >= 43:       # (129 / 257 fire from cycles 27 / 30 there)
+    # 129 / 257 fire from cycles 27 / 30 at 2049 and fall under eps/4 a few cycles later; a
+    # 3 + 40 call ends before a split for them pays (segment planning), longer runs get there
+    if N == 2049 and sum(calls) >= 45:
         assert masks[-1] & ~1, masks            # converged coarse levels predicted to fire
 
 
