@@ -110,7 +110,9 @@ extern "C" {
 #define PGMG_FLAG_NO_SPEC_FIRE 8192u /* speculative calls without segment planning and
                                        without levels predicted to fire (the r02 policy:
                                        a level that will fire decides in-stream from the
-                                       call's start).  Results are identical either way */
+                                       call's start), and W-cycles without plans (every
+                                       bulk check in-stream).  Results are identical
+                                       either way */
 /* (16384u: the 129x129 level inside the tail's launch -- built in r03, bitwise, measured
    slower (one CU's fp64 VALU: ~1.2 us per pass over 129^2 points); removed) */
 #define PGMG_FLAG_HOST_TRANSPORT 2048u /* world > 1 without RCCL: nccl_unique_id points to
@@ -290,6 +292,11 @@ int pgmg_spec_levels(pgmg_ctx *ctx, unsigned long long *in_stream);
  * GPU; converged levels: each visit runs the one-sweep passes the in-stream rare paths would
  * run, and the validation confirms every such check fired, else the call is rolled back). */
 int pgmg_spec_fire_levels(pgmg_ctx *ctx, unsigned long long *fire);
+/* W-cycle plans (one GPU): how the last speculative W call enqueued the visits of its bulk
+ * levels -- counts[0] recorded "does not fire", counts[1] predicted to fire, counts[2] decided
+ * in-stream -- each visit planned from the same visit of the previous cycle.  Zeros after a
+ * V call. */
+int pgmg_spec_visit_modes(pgmg_ctx *ctx, long long counts[3]);
 
 /* The context's PGMG_PRECISION_* and its grid element size in bytes (8 or 4). */
 int pgmg_precision(pgmg_ctx *ctx, int *precision, int *elem_bytes);

@@ -318,6 +318,13 @@ class Solver:
         check(self.lib.pgmg_spec_fire_levels(self.h, C.byref(m)), "pgmg_spec_fire_levels")
         return m.value
 
+    def spec_visit_modes(self):
+        """W-cycle plans: (does not fire, predicted to fire, in-stream) visit counts of the last
+        speculative W call's bulk levels."""
+        a = (C.c_longlong * 3)()
+        check(self.lib.pgmg_spec_visit_modes(self.h, a), "pgmg_spec_visit_modes")
+        return tuple(a)
+
     @property
     def elem_bytes(self):
         """8 (fp64) or 4 (fp32): bytes per grid element on the device."""

@@ -119,6 +119,7 @@ SIGNATURES = [
     ("pgmg_dist_info", C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_longlong)]),
     ("pgmg_spec_levels", C.c_int, [_P, C.POINTER(C.c_ulonglong)]),
     ("pgmg_spec_fire_levels", C.c_int, [_P, C.POINTER(C.c_ulonglong)]),
+    ("pgmg_spec_visit_modes", C.c_int, [_P, C.POINTER(C.c_longlong)]),
     ("pgmg_bench_sweep", C.c_int, [_P, C.c_int, _DP]),
     ("pgmg_jacobi", C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_double, C.c_int, C.c_double,
                               C.POINTER(C.c_int), _P]),

@@ -109,6 +109,17 @@ struct pgmg_ctx {
     std::vector<double> hnorm;
     std::vector<unsigned> hflag;
     bool lean = false;            // the cycles being enqueued record their checks
+    int spec_gamma = 1;           // gamma of the speculative call being enqueued
+    // W-cycle plan (pgmg_ctx.hip "W-cycle plans"): per visit of a bulk level in the cycle, the
+    // largest and smallest check norm of that visit in the last validated cycle
+    std::vector<double> wmax, wmin, wrho;   // wrho: the visit's decay over the last two cycles
+    int wplan_gamma = 0;          // gamma of the plan (0: none)
+    int wplan_seg = 0;            // cycles of the segment the plan was taken from
+    bool wplan_off = false;       // a plan's prediction failed: none for this problem
+    int wvisit = 0, wseg = 0;     // visits enqueued in this segment; its cycles
+    int cur_visit = -1;           // the visit whose checks chk_log records (-1: none)
+    long long wcount[3] = {0, 0, 0};   // the last W call's visits per mode
+    std::vector<int> chk_visit;   // per recorded check: its visit (-1: level 0)
     double *plog = nullptr;       // partials of every recorded check of the current call
     long long plog_cap = 0, plog_used = 0;
     std::vector<pgmg::CheckRef> chks;

@@ -157,10 +157,42 @@ void pgmg::free_grid(Grid &g)
 // How a speculative call enqueues level l's checks: 0 recorded as "does not fire" (no
 // fix-up), 1 recorded as "fires" (the one-sweep passes, no fix-up), 2 decided in-stream (the
 // fix-ups; outside speculative calls every check).
+// W-cycles (gamma > 1): a bulk level's visits are planned one by one (w_visit_mode)
 static int chk_mode(const pgmg_ctx *c, int level)
 {
-    if (!c->lean || c->lvl_exact[level]) return 2;
+    if (!c->lean || (c->spec_gamma > 1 && level > 0) || c->lvl_exact[level]) return 2;
     return c->lvl_fire[level] ? 1 : 0;
+}
+
+// W-cycle plans (one GPU).  A W-cycle visits level l 3^l times and every visit's checks are a
+// different story: a visit right after its parent's restriction starts from a large residual,
+// the later ones from a nearly solved one -- per level, some visits fire and some do not in
+// every cycle, so the per-level policy of the V-cycles leaves every bulk check in-stream (a
+// pass and a rare-path launch each, ~5 % of a W-cycle at 4097).  The visits of a cycle come
+// in the same order every cycle and their norms fall from cycle to cycle (by ~0.15 at 4097 in
+// the steady phase, by orders of magnitude in the first cycles), so visit v of the next cycle
+// is planned from visit v of the last validated one: predicted to fire (k_pre1 / k_post1) when
+// both of its checks were below eps / 4, recorded "does not fire" when both stay above eps
+// with the decay the visit showed since the previous plan, per cycle of the new segment, and a
+// further 100-fold margin; in-stream otherwise.  A failed prediction rolls the segment back and ends the plans for the
+// problem.
+static int w_visit_mode(pgmg_ctx *c, int l)
+{
+    if (!c->lean || c->spec_gamma <= 1 || l == 0) return -1;
+    const int v = c->wvisit++;
+    c->cur_visit = v;
+    const int vc = (int)c->wmax.size();
+    int m = 2;
+    if (!c->wplan_off && c->wplan_gamma == c->spec_gamma && vc > 0) {
+        const int pos = v % vc;
+        const double eps = c->cfg.eps;
+        if (c->wmax[pos] >= 0.0 && c->wmax[pos] < 0.25 * eps) m = 1;
+        else if (c->wrho[pos] > 0.0 &&
+                 c->wmin[pos] * std::pow(c->wrho[pos], (double)c->wseg) * 0.01 >= eps)
+            m = 0;
+    }
+    ++c->wcount[m];
+    return m;
 }
 
 // A log slice for one check of mode `mode` (nullptr outside speculative calls; an in-stream
@@ -168,6 +200,7 @@ static int chk_mode(const pgmg_ctx *c, int level)
 static double *chk_log(pgmg_ctx *c, int np, int level, int mode)
 {
     if (!c->lean || (mode == 2 && c->comm != nullptr)) return nullptr;
+    c->chk_visit.push_back(level > 0 ? c->cur_visit : -1);
     if (c->plog_used + np > c->plog_cap) {
         c->chks.push_back({nullptr, -1, level, mode});
         return c->partials;
@@ -398,13 +431,16 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     fa.stats = c->stats;
     const bool fine = (l == 0);
     // speculative call: record the check (mode 0: no fix-up; 1: predicted to fire, the
-    // one-sweep passes, on levels entered with x0 = 0; 2: in-stream, logged for its norm)
+    // one-sweep passes; 2: in-stream, logged for its norm)
     int mode = chk_mode(c, l);
-    if (mode == 1 && !(recomp && !dist)) mode = 2;
+    const int wm = w_visit_mode(c, l);
+    const int visit = c->cur_visit;   // (the children's visits move it)
+    if (wm >= 0) mode = wm;
+    if (mode == 1 && (dist || pin || (x0_zero && !recomp))) mode = 2;
     double *lp = chk_log(c, fa.np, l, mode);
     if (lp) pa.partials = lp;
     int ev = fine ? timed_begin(c, 1) : -1;
-    if ((e = mode == 1 ? launch_pre1(pa, c->s) : launch_pre(pa, x0_zero, fine, c->s))) return e;
+    if ((e = mode == 1 ? launch_pre1(pa, x0_zero, c->s) : launch_pre(pa, x0_zero, fine, c->s))) return e;
     if ((e = timed_end(c, 1, ev))) return e;
     if (mode == 2) {
         if (lp) fa.partials = lp;
@@ -446,6 +482,7 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     }
     po.gfx = pa.gfx;
     po.gsy = pa.gsy;
+    c->cur_visit = visit;
     lp = chk_log(c, fa.np, l, mode);
     if (lp) po.partials = lp;
     ev = fine ? timed_begin(c, 2) : -1;
@@ -1058,6 +1095,11 @@ static int problem_reset(pgmg_ctx *c)
     c->lvl_fire.assign(c->nb + 1, 0);
     c->lvl_fire_block.assign(c->nb + 1, 0);
     c->lvl_fire_try.assign(c->nb + 1, 0.0);
+    c->wmax.clear();
+    c->wmin.clear();
+    c->wrho.clear();
+    c->wplan_gamma = 0;
+    c->wplan_off = false;
     c->lvl_hist.assign(c->nb + 1, std::vector<double>());
     return PGMG_OK;
 }
@@ -1457,7 +1499,7 @@ static bool spec_level_trend(const pgmg_ctx *c, int l, double *last, double *rho
 static int spec_mark_levels(pgmg_ctx *c, int cycles)
 {
     const double lim = c->cfg.eps * 100.0;
-    if (c->comm == nullptr && !(c->cfg.flags & PGMG_FLAG_NO_SPEC_FIRE)) {
+    if (c->comm == nullptr && !(c->cfg.flags & PGMG_FLAG_NO_SPEC_FIRE) && c->spec_gamma == 1) {
         const double flim = c->cfg.eps * 0.25;
         for (int l = 1; l < c->nb; ++l) {
             const std::vector<double> &h = c->lvl_hist[l];
@@ -1471,13 +1513,14 @@ static int spec_mark_levels(pgmg_ctx *c, int cycles)
         }
     }
     if (tuning_int("PGMG_SPEC_TRACE", 0))
-        for (int l = 1; l < c->nb; ++l)
-            fprintf(stderr, "spec level %d N=%d hist %zu last %.3e exact %d fire %d block %d\n", l,
-                    c->lv[l].N, c->lvl_hist[l].size(),
-                    c->lvl_hist[l].empty() ? -1.0 : c->lvl_hist[l].back(), (int)c->lvl_exact[l],
-                    (int)c->lvl_fire[l], (int)c->lvl_fire_block[l]);
+        for (int l = 1; l < c->nb; ++l) {
+            fprintf(stderr, "spec level %d N=%d exact %d fire %d block %d hist/eps", l, c->lv[l].N,
+                    (int)c->lvl_exact[l], (int)c->lvl_fire[l], (int)c->lvl_fire_block[l]);
+            for (double v : c->lvl_hist[l]) fprintf(stderr, " %.3g", v / c->cfg.eps);
+            fprintf(stderr, "\n");
+        }
     std::vector<unsigned> keep(c->nb + 1, 1u);   // 1 = keep speculating
-    for (int l = 1; l < c->nb; ++l) {
+    for (int l = 1; l < c->nb && c->spec_gamma == 1; ++l) {
         double last, rho;   // min over the last visit; decay per cycle
         if (c->lvl_exact[l] || c->lvl_fire[l] || !spec_level_trend(c, l, &last, &rho)) continue;
         if (!(last * std::pow(rho, (double)cycles) >= lim)) keep[l] = 0u;
@@ -1510,7 +1553,7 @@ static int spec_mark_levels(pgmg_ctx *c, int cycles)
 // point at ~5 TB/s) and one host round trip of the validation.
 static int spec_plan_segment(pgmg_ctx *c, int seg)
 {
-    if (seg < 4 || (c->cfg.flags & PGMG_FLAG_NO_SPEC_FIRE)) return seg;
+    if (seg < 4 || (c->cfg.flags & PGMG_FLAG_NO_SPEC_FIRE) || c->spec_gamma > 1) return seg;
     // a new problem: a short first segment gathers every level's trend (without one, a long
     // first call speculated blind and rolled back at the first firing check, ~27 cycles in
     // on the reference problem); history sizes are the same on every rank
@@ -1591,6 +1634,43 @@ static void spec_record_norms(pgmg_ctx *c, int n)
         h.push_back(c->hnorm[i]);
         if (h.size() > 8) h.erase(h.begin(), h.end() - 4);
     }
+    if (c->spec_gamma <= 1) return;
+    // W-cycle plan: the norms of the segment's last cycle, per visit
+    const int nv = c->wvisit, seg = c->wseg;
+    const std::vector<double> pmin = c->wplan_gamma == c->spec_gamma ? c->wmin : std::vector<double>();
+    const int pseg = c->wplan_seg;
+    c->wmax.clear();
+    c->wmin.clear();
+    c->wrho.clear();
+    c->wplan_gamma = 0;
+    if (nv == 0 || seg <= 0 || nv % seg != 0 || (int)c->chk_visit.size() != n) return;
+    const int vc = nv / seg, v0 = nv - vc;
+    c->wmax.assign(vc, -1.0);
+    c->wmin.assign(vc, HUGE_VAL);
+    for (int i = 0; i < n; ++i) {
+        const int v = c->chk_visit[i];
+        if (v < v0) continue;
+        c->wmax[v - v0] = std::max(c->wmax[v - v0], c->hnorm[i]);
+        c->wmin[v - v0] = std::min(c->wmin[v - v0], c->hnorm[i]);
+    }
+    // per-cycle decay of each visit's smaller norm since the previous plan (0: unknown; the
+    // first cycles of a problem fall by orders of magnitude, so no "does not fire" without it)
+    c->wrho.assign(vc, 0.0);
+    if ((int)pmin.size() == vc && pseg > 0)
+        for (int i = 0; i < vc; ++i)
+            if (pmin[i] > 0.0 && pmin[i] < HUGE_VAL && c->wmin[i] < HUGE_VAL)
+                c->wrho[i] = std::min(1.0, std::pow(c->wmin[i] / pmin[i], 1.0 / seg));
+    c->wplan_gamma = c->spec_gamma;
+    c->wplan_seg = seg;
+    if (tuning_int("PGMG_SPEC_TRACE", 0)) {
+        int f = 0, q = 0;
+        for (int i = 0; i < vc; ++i) {
+            f += c->wmax[i] >= 0.0 && c->wmax[i] < 0.25 * c->cfg.eps;
+            q += c->wrho[i] > 0.0 && c->wmin[i] * c->wrho[i] * 0.01 >= c->cfg.eps;
+        }
+        fprintf(stderr, "W plan: %d visits per cycle, %d predicted to fire, %d not (1 cycle)\n",
+                vc, f, q);
+    }
 }
 
 static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
@@ -1600,7 +1680,8 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
     const int npp = c->cross ? postpre_blocks(L0.N, L0.lo / 2, (L0.hi < L0.N ? L0.hi : L0.N - 1) / 2) : 0;
     long long d1, k1;
     spec_need_level(c, 1, gamma, &d1, &k1);
-    const long long per_dbl = 2LL * std::max(np0, npp) + d1, per_chk = 2 + k1;
+    // (level 0 visits level 1 gamma times per cycle)
+    const long long per_dbl = 2LL * std::max(np0, npp) + gamma * d1, per_chk = 2 + gamma * k1;
     // segments of at most 2^27 logged doubles (1 GiB) / 2^22 checks
     long long seg_max = std::min(((1LL << 27) - 2LL * np0) / per_dbl, ((1LL << 22) - 2) / per_chk);
     if (c->cfg.spec_segment > 0) seg_max = std::min<long long>(seg_max, c->cfg.spec_segment);
@@ -1613,6 +1694,8 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
     const void *const ext_in = c->x_in;
     void *const ext_out = c->x_out;
     bool first = true;
+    c->spec_gamma = gamma;
+    c->wcount[0] = c->wcount[1] = c->wcount[2] = 0;
     while (ncycles > 0) {
         const int seg = spec_plan_segment(c, (int)std::min<long long>(ncycles, seg_max));
         c->x_in = first ? ext_in : nullptr;
@@ -1635,6 +1718,9 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
         c->lean = true;
         c->plog_used = 0;
         c->chks.clear();
+        c->chk_visit.clear();
+        c->wvisit = 0;
+        c->wseg = seg;
         if (!last) c->x_out = nullptr;   // intermediate segments end in the level-0 grids
         c->defer_post = ext_out != nullptr && last;
         e = run_cycles_plain(c, seg, gamma, first);
@@ -1667,6 +1753,12 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
             // some check could fire: roll back this segment, rerun the rest of the call with
             // in-stream decisions; the levels whose checks could fire stay in-stream
             ++c->rollbacks;
+            if (gamma > 1) {   // a W plan's prediction failed
+                c->wplan_off = true;
+                c->wmax.clear();
+                c->wmin.clear();
+                c->wrho.clear();
+            }
             for (int i = 0; i < n; ++i)
                 if (c->hflag[i] || overflow) {
                     const int l = c->chks[i].level;
@@ -1703,9 +1795,13 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
 
 static int run_cycles_core(pgmg_ctx *c, int ncycles, int gamma)
 {
-    // V-cycles only: W-cycles revisit the coarse levels until their checks fire (the
-    // reference's W-cycle at 129 exits 147 times in its first cycle), a rollback per call
-    if (c->spec && !c->spec_off && gamma == 1) return run_cycles_spec(c, ncycles, gamma);
+    // W-cycles revisit the coarse levels until their checks fire (the reference's W-cycle at
+    // 129 exits 147 times in its first cycle): their speculative calls decide those checks
+    // in-stream (chk_mode) and only predict converged levels to fire (one GPU, any N: a W-cycle
+    // is never a captured graph, so the smaller grids gain as much)
+    const bool w_spec = gamma > 1 && c->fused && c->comm == nullptr &&
+                        !(c->cfg.flags & (PGMG_FLAG_NO_SPEC_FIRE | PGMG_FLAG_EXACT_DIST));
+    if (!c->spec_off && (gamma == 1 ? c->spec : w_spec)) return run_cycles_spec(c, ncycles, gamma);
     return run_cycles_plain(c, ncycles, gamma);
 }
 
@@ -1755,6 +1851,13 @@ int pgmg_spec_levels(pgmg_ctx *c, unsigned long long *in_stream)
     for (int l = 1; l < (int)c->lvl_exact.size() && l < 64; ++l)
         if (c->lvl_exact[l] || c->lvl_fire[l]) m |= 1ull << l;
     *in_stream = m;
+    return PGMG_OK;
+}
+
+int pgmg_spec_visit_modes(pgmg_ctx *c, long long counts[3])
+{
+    if (!c || !counts) return set_err(PGMG_ERR_ARG, "null argument");
+    for (int i = 0; i < 3; ++i) counts[i] = c->wcount[i];
     return PGMG_OK;
 }
 

@@ -116,7 +116,7 @@ template <class T> int launch_pre(const PreArgsT<T> &a, bool x0_zero, bool fine,
 template <class T> int launch_post(const PostArgsT<T> &a, bool fine, hipStream_t s);
 // coarse levels (x0 = 0, RECOMP) whose checks are predicted to fire: the one-sweep passes
 // with the checks' partials (k_pre1 / k_post1)
-template <class T> int launch_pre1(const PreArgsT<T> &a, hipStream_t s);
+template <class T> int launch_pre1(const PreArgsT<T> &a, bool x0_zero, hipStream_t s);
 template <class T> int launch_post1(const PostArgsT<T> &a, hipStream_t s);
 template <class T>
 void launch_pre_fixup(const FixArgsF &a, const PreArgsT<T> &p, bool x0_zero, hipStream_t s);

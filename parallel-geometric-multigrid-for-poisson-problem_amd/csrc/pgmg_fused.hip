@@ -219,8 +219,13 @@ __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red)
     const int jce = min(jcb + a.rows_per_block, a.jc1);
     const int olo = max(2 * jcb, a.row_lo), ohi = min(2 * jce, a.row_hi);  // x2 rows written
     const int clo = max(jcb, max(1, a.rc_lo)), chi = min(jce, min(N / 2, a.rc_hi));  // rc rows
-    if (!S1 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
-        atomicAdd(&a.stats[0], 2ull);
+    if (!S1 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+        if (a.stats != nullptr) atomicAdd(&a.stats[0], 2ull);
+        // the pre check's outcome for k_post RECOMP: "did not fire" unless a rare path or the
+        // predicted-to-fire pass says otherwise (a level's visits share the flag: a W-cycle's
+        // visit recorded "does not fire" may follow one predicted to fire)
+        if (a.fired != nullptr) *a.fired = 0u;
+    }
     const T *__restrict__ X = a.x0 + k.c;
     const long long Px = a.Px != 0 ? a.Px : P;   // x0's pitch (the caller's array: N)
     const T *__restrict__ F = a.f + k.c;
@@ -427,10 +432,11 @@ __global__ __launch_bounds__(256) void k_pre(PreArgsT<T> a)
 }
 
 // A coarse level's pre-smooth whose check is predicted to fire (speculative calls, levels that
-// converged: pgmg_ctx.hip "predicted to fire"): x1 = J(0) is the result, rc = R r(x1), one
-// sweep and one exit booked, the "pre fired" flag the level's k_post reads set -- what k_pre +
-// k_pre_rare compute when the check fires, in one launch; the partials confirm it afterwards
-template <class T, int PAIRS>
+// converged: pgmg_ctx.hip "predicted to fire"): x1 = J(x0) (J(0) on a level entered with
+// x0 = 0) is the result, rc = R r(x1), one sweep and one exit booked, the "pre fired" flag the
+// level's RECOMP k_post reads set -- what k_pre + k_pre_rare compute when the check fires, in
+// one launch; the partials confirm it afterwards
+template <class T, bool X0_ZERO, int PAIRS>
 __global__ __launch_bounds__(256) void k_pre1(PreArgsT<T> a)
 {
     __shared__ double red[4];
@@ -441,7 +447,7 @@ __global__ __launch_bounds__(256) void k_pre1(PreArgsT<T> a)
             atomicAdd(&a.stats[1], 1ull);
         }
     }
-    pre_body<T, true, false, PAIRS, false, false, true, true>(a, red);
+    pre_body<T, X0_ZERO, false, PAIRS, false, false, true, true>(a, red);
 }
 
 // Decision of an in-stream early-exit check from the partial sums of the pass just run
@@ -661,9 +667,9 @@ __global__ __launch_bounds__(256) void k_post(PostArgsT<T> a)
 }
 
 // a coarse level's post-smooth whose check is predicted to fire (see k_pre1): x1 is the
-// result (RECOMP: the pre-smoothed iterate recomputed as the pre check decided), one sweep and
-// one exit booked, the check's partials written
-template <class T, int PAIRS>
+// result (RECOMP: the pre-smoothed iterate recomputed as the pre check decided; otherwise read),
+// one sweep and one exit booked, the check's partials written
+template <class T, int PAIRS, bool RECOMP>
 __global__ __launch_bounds__(256) void k_post1(PostArgsT<T> a)
 {
     __shared__ double red[4];
@@ -671,7 +677,7 @@ __global__ __launch_bounds__(256) void k_post1(PostArgsT<T> a)
         atomicAdd(&a.stats[0], 1ull);
         atomicAdd(&a.stats[1], 1ull);
     }
-    post_body<T, false, PAIRS, true, false, true, true>(a, red);
+    post_body<T, false, PAIRS, RECOMP, false, true, true>(a, red);
 }
 
 // rare path of k_post's check (replaces the scalar k_post_fixup on in-stream levels)
@@ -1869,19 +1875,20 @@ int launch_post_rare(const FixArgsF &f, const PostArgsT<T> &a0, hipStream_t s)
     return PGMG_OK;
 }
 
-// the predicted-to-fire passes of a coarse level entered with x0 = 0 (RECOMP): the full
-// passes' geometry and spans, f from memory
+// the predicted-to-fire passes of a coarse level (entered with x0 = 0 and RECOMP, or from the
+// previous gamma visit's iterate): the full passes' geometry and spans, f from memory
 template <class T>
-int launch_pre1(const PreArgsT<T> &a0, hipStream_t s)
+int launch_pre1(const PreArgsT<T> &a0, bool x0_zero, hipStream_t s)
 {
     int t, gx, gy, r;
     fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r);
-    if (const int e = pre_spans(a0, t, gx, r, false, true)) return e;
+    if (const int e = pre_spans(a0, t, gx, r, !x0_zero, true)) return e;
     PreArgsT<T> a = a0;
     a.rows_per_block = r;
     a.gfx = a.gsy = nullptr;
     a.nt = 0;
-    k_pre1<T, 2><<<dim3(gx, gy), dim3(t), 0, s>>>(a);
+    if (x0_zero) k_pre1<T, true, 2><<<dim3(gx, gy), dim3(t), 0, s>>>(a);
+    else k_pre1<T, false, 2><<<dim3(gx, gy), dim3(t), 0, s>>>(a);
     return PGMG_OK;
 }
 
@@ -1895,7 +1902,8 @@ int launch_post1(const PostArgsT<T> &a0, hipStream_t s)
     a.rows_per_block = r;
     a.gfx = a.gsy = nullptr;
     a.nt = 0;
-    k_post1<T, 2><<<dim3(gx, gy), dim3(t), 0, s>>>(a);
+    if (a.pre_fired != nullptr) k_post1<T, 2, true><<<dim3(gx, gy), dim3(t), 0, s>>>(a);
+    else k_post1<T, 2, false><<<dim3(gx, gy), dim3(t), 0, s>>>(a);
     return PGMG_OK;
 }
 
@@ -1914,7 +1922,7 @@ void launch_post_fixup(const FixArgsF &a, const PostArgsT<T> &p, hipStream_t s)
 
 #define PGMG_INSTANTIATE(T)                                                                       \
     template int launch_pre<T>(const PreArgsT<T> &, bool, bool, hipStream_t);                   \
-    template int launch_pre1<T>(const PreArgsT<T> &, hipStream_t);                              \
+    template int launch_pre1<T>(const PreArgsT<T> &, bool, hipStream_t);                            \
     template int launch_post1<T>(const PostArgsT<T> &, hipStream_t);                            \
     template int launch_post<T>(const PostArgsT<T> &, bool, hipStream_t);                       \
     template int launch_postpre<T>(const PostPreArgsT<T> &, hipStream_t);                       \

@@ -1,0 +1,15 @@
+#!/bin/bash
+# r03 session: W-cycle plans -- trace (measurement build), parity, A/B against the previous build
+set -u
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+D=$PWD/parallel-geometric-multigrid-for-poisson-problem_amd
+for n in 1025 4097; do
+  PGMG_LIB=$D/libpgmg_ab.so timeout -k 10 300 python3 scripts/spec_fire_trace.py $n 1 W 6 > gpurun_out/wtrace_$n.log 2>&1 || exit $?
+  grep -E "W plan|W x1" gpurun_out/wtrace_$n.log
+done
+timeout -k 10 900 python -u -m pytest tests/test_gpu_spec_fire.py tests/test_gpu_spec.py tests/test_gpu_wtail.py tests/test_gpu_fcycle.py -m gpu -x -v -s --timeout 300 --timeout-method thread > gpurun_out/wf_tests.log 2>&1
+rc=$?; grep -E "fire masks|passed|failed|Error" gpurun_out/wf_tests.log | tail -20; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 900 python3 scripts/ab_env.py --rounds 3 --grids W4097,W1025,V4097,V16385 --steps 30 \
+  "base:PGMG_LIB=$D/libpgmg_base.so" "new:PGMG_LIB=$D/libpgmg.so" > gpurun_out/wfire_ab.jsonl 2>&1 || { tail -5 gpurun_out/wfire_ab.jsonl; exit 1; }
+cat gpurun_out/wfire_ab.jsonl

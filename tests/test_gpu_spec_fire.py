@@ -17,13 +17,14 @@ from conftest import assert_bitwise
 pytestmark = pytest.mark.gpu
 
 
-def _calls(pgmg, N, calls, flags=0):
+def _calls(pgmg, N, calls, flags=0, kind="V"):
     with pgmg.Solver(N, flags=flags) as s:
         s.set_problem()
+        run = {"V": s.vcycle, "W": s.wcycle, "F": s.fcycle}[kind]
         masks = []
         for n in calls:
-            s.vcycle(n)
-            masks.append(s.spec_fire_levels())
+            run(n)
+            masks.append(s.spec_fire_levels() if kind == "V" else s.spec_visit_modes())
         return s.solution(), s.stats_detail(), s.dist_info(), masks
 
 
@@ -39,6 +40,26 @@ def test_fire_prediction_bitwise(pgmg, N, calls):
     # 3 + 40 call ends before a split for them pays (segment planning), longer runs get there
     if N == 2049 and sum(calls) >= 45:
         assert masks[-1] & ~1, masks            # converged coarse levels predicted to fire
+
+
+@pytest.mark.parametrize("kind,N,calls", [("W", 4097, [1] * 5), ("W", 1025, [1] * 10),
+                                          ("W", 2049, [2, 3]), ("W", 513, [3, 3]),
+                                          ("F", 2049, [2, 8]), ("F", 1025, [1] * 12)])
+def test_fire_prediction_w_f_bitwise(pgmg, kind, N, calls):
+    """W- and F-cycles: the second and third gamma visits of a level start from the previous
+    visit's iterate, not from 0; their predicted-to-fire passes read x0 and store x1 (k_pre1 /
+    k_post1 without RECOMP).  W calls speculate on one GPU at every N (pgmg_ctx.hip "W-cycle
+    plans": each visit of a bulk level planned from the same visit of the previous cycle);
+    F-cycles run in-stream."""
+    phi, det, info, masks = _calls(pgmg, N, calls, kind=kind)
+    ref, rdet, _, _ = _calls(pgmg, N, calls, flags=pgmg.PGMG_FLAG_EXACT_DIST, kind=kind)
+    assert_bitwise(phi, ref, f"{kind} N={N} calls={calls}")
+    assert det == rdet
+    print(kind, N, calls, "visit modes (no fire, fire, in-stream)", masks, "rollbacks", info[1])
+    if kind == "W":   # W plans: a failed prediction ends them for the problem (one rollback)
+        assert info[1] <= 1, info
+    if kind == "W" and N == 4097:   # from the second call on most visits are planned
+        assert info[1] == 0 and masks[-1][0] > 0 and masks[-1][1] > 0, masks
 
 
 def test_fire_prediction_golden(pgmg, plan, golden_cycles):
