@@ -101,6 +101,9 @@ struct pgmg_ctx {
     std::vector<char> lvl_exact;  // per bulk level: its checks fire (soon): decide in-stream
     std::vector<char> lvl_fire;   // per bulk level: its checks keep firing: predicted to fire
     std::vector<char> lvl_fire_block;   // a "fires" prediction failed: never again (this problem)
+    std::vector<int> lvl_kx;      // per bulk level: its first cycles of the segment recorded
+                                  // "does not fire" (then in-stream); lvl_vis counts its visits
+    std::vector<int> lvl_vis;
     std::vector<double> lvl_fire_try;   // norm at the last segment split made for the level to
                                         // become "fires" (0: none; no second split before it halves)
     std::vector<std::vector<double>> lvl_hist;   // per bulk level: its last check norms

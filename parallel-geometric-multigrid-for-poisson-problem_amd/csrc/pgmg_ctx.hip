@@ -433,6 +433,9 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     // speculative call: record the check (mode 0: no fix-up; 1: predicted to fire, the
     // one-sweep passes; 2: in-stream, logged for its norm)
     int mode = chk_mode(c, l);
+    // V-cycles: a speculating level records "does not fire" up to its predicted crossing of
+    // 100 eps (spec_mark_levels), in-stream after it
+    if (mode == 0 && l > 0 && c->spec_gamma == 1 && c->lvl_vis[l]++ >= c->lvl_kx[l]) mode = 2;
     const int wm = w_visit_mode(c, l);
     const int visit = c->cur_visit;   // (the children's visits move it)
     if (wm >= 0) mode = wm;
@@ -1095,6 +1098,8 @@ static int problem_reset(pgmg_ctx *c)
     c->lvl_fire.assign(c->nb + 1, 0);
     c->lvl_fire_block.assign(c->nb + 1, 0);
     c->lvl_fire_try.assign(c->nb + 1, 0.0);
+    c->lvl_kx.assign(c->nb + 1, 0);
+    c->lvl_vis.assign(c->nb + 1, 0);
     c->wmax.clear();
     c->wmin.clear();
     c->wrho.clear();
@@ -1519,14 +1524,17 @@ static int spec_mark_levels(pgmg_ctx *c, int cycles)
             for (double v : c->lvl_hist[l]) fprintf(stderr, " %.3g", v / c->cfg.eps);
             fprintf(stderr, "\n");
         }
-    std::vector<unsigned> keep(c->nb + 1, 1u);   // 1 = keep speculating
+    // keep[l]: the segment's first cycles in which level l records "does not fire" (its
+    // predicted norm last * rho^k stays at or above 100 eps); 0: in-stream from the start
+    std::vector<unsigned> keep(c->nb + 1, (unsigned)cycles);
     for (int l = 1; l < c->nb && c->spec_gamma == 1; ++l) {
         double last, rho;   // min over the last visit; decay per cycle
         if (c->lvl_exact[l] || c->lvl_fire[l] || !spec_level_trend(c, l, &last, &rho)) continue;
-        if (!(last * std::pow(rho, (double)cycles) >= lim)) keep[l] = 0u;
+        const double k = last >= lim ? std::floor(std::log(lim / last) / std::log(rho)) : 0.0;
+        keep[l] = (unsigned)std::max(0.0, std::min((double)cycles, k));
         if (tuning_int("PGMG_SPEC_TRACE", 0))
-            fprintf(stderr, "spec level %d N=%d last %.3e rho %.3f next %d -> %s\n", l, c->lv[l].N,
-                    last, rho, cycles, keep[l] ? "speculate" : "in-stream");
+            fprintf(stderr, "spec level %d N=%d last %.3e rho %.3f: speculates %u of %d cycles\n", l,
+                    c->lv[l].N, last, rho, keep[l], cycles);
     }
     if (c->comm) {
         HIPC(hipMemcpyAsync(c->mark_dev, keep.data(), (c->nb + 1) * sizeof(unsigned),
@@ -1537,20 +1545,22 @@ static int spec_mark_levels(pgmg_ctx *c, int cycles)
                             hipMemcpyDeviceToHost, c->s));
         PGMG_TRY(stream_wait(c));
     }
-    for (int l = 1; l < c->nb; ++l)
+    for (int l = 1; l < c->nb; ++l) {
         if (!keep[l]) c->lvl_exact[l] = 1;
+        c->lvl_kx[l] = (int)keep[l];
+    }
     return PGMG_OK;
 }
 
-// Segment planning (one GPU).  spec_mark_levels sends a level in-stream for the whole
-// segment as soon as its norm is predicted to fall under 100 eps anywhere in it, so a long
-// call (the 3 + 40 cycles of BASELINE configs[1] at N = 4097: the coarse levels cross at
-// ~27 cycles) decided every coarse check in-stream from its first cycle -- two launches of
-// ~5 us per level and cycle.  Instead the segment ends just before the first such crossing
-// (the levels speculate until then and go in-stream at the next segment) when that pays for
-// the split: ~10 us per affected level and cycle saved against one more finest-level pass
-// (the cross-fused call restarts: k_post + k_pre instead of one k_postpre, 16 B per fine
-// point at ~5 TB/s) and one host round trip of the validation.
+// Segment planning (one GPU).  A level that decides in-stream (two launches of ~5 us per
+// visit) can be predicted to fire -- one launch per visit -- only from the norms of a
+// validated segment, so a long call (the 3 + 40 cycles of BASELINE configs[1] at N = 4097:
+// the coarse levels cross eps at ~27 cycles) would keep it in-stream to its end.  The segment
+// ends where such levels can be predicted to fire when that pays for the split: ~10 us per
+// level and cycle saved against one more finest-level pass (the cross-fused call restarts:
+// k_post + k_pre instead of one k_postpre, 16 B per fine point at ~5 TB/s) and one host
+// round trip of the validation.  (A speculating level's crossing of 100 eps needs no split:
+// spec_mark_levels gives it its speculating cycles within the segment.)
 static int spec_plan_segment(pgmg_ctx *c, int seg)
 {
     if (seg < 4 || (c->cfg.flags & PGMG_FLAG_NO_SPEC_FIRE) || c->spec_gamma > 1) return seg;
@@ -1566,11 +1576,10 @@ static int spec_plan_segment(pgmg_ctx *c, int seg)
     auto cycles_to = [](double last, double rho, double t) {
         return last > t ? (int)std::floor(std::log(t / last) / std::log(rho)) : 0;
     };
-    // candidate split points: a speculating level's crossing of 100 eps (it speculates until
-    // then instead of deciding in-stream for the whole segment), an in-stream level's last
-    // cycle before it can be predicted to fire (its norm under eps / 4 for two visits)
+    // candidate split points: a level's last cycle before it can be predicted to fire (its
+    // norm under eps / 4 for two visits)
     struct Cand {
-        int k, kind, level;   // kind 0: speculating until k, 1: predicted to fire from k
+        int k, level;   // predicted to fire from cycle k
         double norm;
     };
     std::vector<Cand> cand;
@@ -1579,10 +1588,18 @@ static int spec_plan_segment(pgmg_ctx *c, int seg)
         if (c->lvl_fire[l] || !spec_level_trend(c, l, &last, &rho)) continue;
         bool exact = c->lvl_exact[l] != 0;
         if (!exact) {
+            // a speculating level records "does not fire" up to its crossing of 100 eps within
+            // the segment anyway (spec_mark_levels); what a split can give it is the firing
+            // prediction, from a segment that ends after its steep decay took it under eps / 4
             const int k = cycles_to(last, rho, lim);
             if (k >= seg) continue;
-            if (k >= 2) cand.push_back({k, 0, l, last});
-            else exact = true;   // in-stream from this segment on
+            if (k >= 2) {
+                const int kf = k + cycles_to(lim, rho, flim) + 2;
+                if (kf < seg && !c->lvl_fire_block[l])
+                    cand.push_back({kf, l, last * std::pow(rho, (double)kf)});
+                continue;
+            }
+            exact = true;   // in-stream from this segment on
         }
         if (exact && !c->lvl_fire_block[l]) {
             // the fire test looks at the LARGER check norm of a visit: its decay; a level whose
@@ -1597,20 +1614,17 @@ static int spec_plan_segment(pgmg_ctx *c, int seg)
             // (the decay slows near eps: ~0.7 per cycle on the reference problem, where the
             // steep phase shows ~0.33; a split that comes too early costs without paying)
             const int k = cycles_to(ml, std::max(rm, 0.7), flim) + 2;
-            if (k < seg) cand.push_back({std::max(k, 2), 1, l, ml});
+            if (k < seg) cand.push_back({std::max(k, 2), l, ml});
         }
     }
     // level-cycles that avoid two in-stream launches (~10 us each) if the segment ends at
-    // k: a speculating level crossing at or after k speculates k cycles instead of deciding
-    // in-stream for the whole segment (one crossing before k is marked in-stream from the
-    // start either way); a level that can be predicted to fire by k does so for seg - k
+    // k: a level that can be predicted to fire by k does so for seg - k
     int best_k = seg;
     double best = 0.0;
     for (const auto &q : cand) {
         const int k = q.k;
         double saved = 0.0;
-        for (const auto &p : cand)
-            saved += p.kind == 0 ? (p.k >= k ? k : 0) : (p.k <= k ? seg - k : 0);
+        for (const auto &p : cand) saved += p.k <= k ? seg - k : 0;
         if (saved > best) {
             best = saved;
             best_k = k;
@@ -1623,7 +1637,7 @@ static int spec_plan_segment(pgmg_ctx *c, int seg)
                 seg, cand.size(), best_k, best * 10.0, cost * 1e6);
     if (!(best * 10e-6 > cost)) return seg;
     for (const auto &p : cand)
-        if (p.kind == 1 && p.k <= best_k) c->lvl_fire_try[p.level] = p.norm;
+        if (p.k <= best_k) c->lvl_fire_try[p.level] = p.norm;
     return best_k;
 }
 
@@ -1721,6 +1735,7 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
         c->chk_visit.clear();
         c->wvisit = 0;
         c->wseg = seg;
+        std::fill(c->lvl_vis.begin(), c->lvl_vis.end(), 0);
         if (!last) c->x_out = nullptr;   // intermediate segments end in the level-0 grids
         c->defer_post = ext_out != nullptr && last;
         e = run_cycles_plain(c, seg, gamma, first);
