@@ -107,12 +107,12 @@ extern "C" {
                                    order, so phi agrees with the EXACT default within
                                    1e-12 relative (after <= 10 cycles) instead of bitwise.
                                    One GPU (row strips ignore it); everything else exact */
-#define PGMG_FLAG_NO_SPEC_FIRE 8192u /* speculative calls without segment planning and
-                                       without levels predicted to fire (the r02 policy:
-                                       a level that will fire decides in-stream from the
-                                       call's start), and W-cycles without plans (every
-                                       bulk check in-stream).  Results are identical
-                                       either way */
+#define PGMG_FLAG_NO_SPEC_FIRE 8192u /* speculative calls without segment planning,
+                                       per-cycle speculation windows and levels predicted
+                                       to fire (the r02 policy: a level that will fire
+                                       decides in-stream from the call's start), and
+                                       W-cycles without plans (every bulk check
+                                       in-stream).  Results are identical either way */
 /* (16384u: the 129x129 level inside the tail's launch -- built in r03, bitwise, measured
    slower (one CU's fp64 VALU: ~1.2 us per pass over 129^2 points); removed) */
 #define PGMG_FLAG_HOST_TRANSPORT 2048u /* world > 1 without RCCL: nccl_unique_id points to

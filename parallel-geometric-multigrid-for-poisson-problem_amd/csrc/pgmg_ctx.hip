@@ -1532,6 +1532,8 @@ static int spec_mark_levels(pgmg_ctx *c, int cycles)
         if (c->lvl_exact[l] || c->lvl_fire[l] || !spec_level_trend(c, l, &last, &rho)) continue;
         const double k = last >= lim ? std::floor(std::log(lim / last) / std::log(rho)) : 0.0;
         keep[l] = (unsigned)std::max(0.0, std::min((double)cycles, k));
+        // (PGMG_FLAG_NO_SPEC_FIRE, the r02 policy: in-stream for the whole segment instead)
+        if ((c->cfg.flags & PGMG_FLAG_NO_SPEC_FIRE) && keep[l] < (unsigned)cycles) keep[l] = 0u;
         if (tuning_int("PGMG_SPEC_TRACE", 0))
             fprintf(stderr, "spec level %d N=%d last %.3e rho %.3f: speculates %u of %d cycles\n", l,
                     c->lv[l].N, last, rho, keep[l], cycles);
