@@ -5,6 +5,13 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--reps R] [--n 16385]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
+`--gpus N` with N > 1 outside a launcher (no WORLD_SIZE in the environment) starts N rank
+processes itself -- `python -m torch.distributed.run --nnodes=1 --nproc-per-node N
+--master-addr 127.0.0.1` as a CHILD of this process, before anything touches the GPU -- and
+exits with its status.  Under a launcher, --gpus must equal WORLD_SIZE, and each rank needs its
+own device (LOCAL_RANK < the device count) unless PGMG_BENCH_SOLO=1 or
+PGMG_BENCH_TRANSPORT=host (harness tests on a one-GPU box); otherwise the run exits non-zero.
+
 A "step" is one V-cycle of the reference's mg_cpu_exec semantics (2+2 Jacobi sweeps with
 the per-sweep residual-norm early exit, full-weighting restriction, the reference
 prolongation, recursion to N=5) on the synthetic problem the reference itself solves:
@@ -80,7 +87,14 @@ def parse():
                          "ParallelMultiGridSolver::v_cycle called once per cycle through the C++ "
                          "mirror (host/gpu_exec, device arrays in place) -- and the context API's "
                          "one-cycle calls it is measured against")
+    ap.add_argument("--trace", choices=["auto", "off"], default="auto",
+                    help="auto: a rocprofv3 --kernel-trace --stats pass over a child run of the "
+                         "timed call (warmup + steps cycles), before this process touches the "
+                         "GPU: the dominant kernel's rocprof average beside the event timing")
+    ap.add_argument("--save-profiles", default="",
+                    help="directory to keep the rocprofv3 summaries of the trace and PMC passes")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--trace-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -164,6 +178,85 @@ def pmc_child(args):
             s.sync()
 
 
+def trace_child(args):
+    """The program the kernel-trace pass profiles: the timed call of the main leg (a fresh
+    problem, warmup cycles, then `steps` cycles in one call), then exit."""
+    import torch  # noqa: F401
+    import _pkgload
+    pg = _pkgload.load()
+    with pg.Solver(args.n, dtype=args.dtype) as s:
+        s.set_problem()
+        run = {"V": s.vcycle, "W": s.wcycle, "F": s.fcycle}[args.cycle]
+        run(max(args.warmup, 0))
+        s.sync()
+        run(args.steps)
+        s.sync()
+
+
+def _keep_profile(args, src, name):
+    if args.save_profiles and src:
+        d = pathlib.Path(args.save_profiles)
+        d.mkdir(parents=True, exist_ok=True)
+        shutil.copy(src, d / name)
+
+
+def live_trace(args):
+    """rocprofv3 --kernel-trace --stats over trace_child on THIS box, before this process
+    touches the GPU: {kernel key: (calls, average ms)} from its kernel_stats.csv, or
+    (None, reason)."""
+    import csv
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None, "rocprofv3 not found"
+    d = tempfile.mkdtemp(prefix="pgmg_trace_")
+    cmd = ["timeout", "-s", "KILL", "300", prof, "--kernel-trace", "--stats", "--output-format",
+           "csv", "-d", d, "-o", "run", "--", sys.executable, str(ROOT / "bench.py"),
+           "--trace-child", "--n", str(args.n), "--dtype", args.dtype, "--cycle", args.cycle,
+           "--steps", str(args.steps), "--warmup", str(args.warmup)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=330)
+        files = list(pathlib.Path(d).rglob("*kernel_stats.csv"))
+        if r.returncode != 0 or not files:
+            return None, f"rocprofv3 --kernel-trace failed (rc={r.returncode})"
+        _keep_profile(args, files[0], "trace_kernel_stats.csv")
+        out = {}
+        for row in csv.DictReader(open(files[0])):
+            out[kernel_key(row["Name"])] = (int(row["Calls"]), float(row["AverageNs"]) / 1e6)
+        return out, ("rocprofv3 --kernel-trace --stats of a child run of the timed call "
+                     f"({args.warmup} + {args.steps} cycles, one call each, main leg) on this box")
+    except (subprocess.SubprocessError, OSError, KeyError, ValueError) as e:
+        return None, f"rocprofv3 --kernel-trace failed: {e}"
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def launch_ranks(args):
+    """--gpus N > 1 without a launcher: N rank processes under torch.distributed.run, started
+    as a child process (never an exec) before this process touches the GPU; returns its exit
+    status.  The ranks' stdout is this process's: rank 0 prints the JSON line."""
+    import socket
+    harness = (os.environ.get("PGMG_BENCH_SOLO") == "1" or
+               os.environ.get("PGMG_BENCH_TRANSPORT") == "host")
+    stub = os.environ.get("PGMG_BENCH_LAUNCH_STUB") == "1"
+    if not (harness or stub):
+        import torch   # device_count does not initialise the GPU (hipGetDeviceCount only)
+        n = torch.cuda.device_count()
+        if n < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs, this box has {n} "
+                  "(PGMG_BENCH_SOLO=1 or PGMG_BENCH_TRANSPORT=host run the ranks on one GPU as a "
+                  "harness test)", file=sys.stderr)
+            return 2
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           f"--master-port={port}", str(ROOT / "bench.py")] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
+
+
 def live_pmc(args):
     """HBM bytes per launch of every kernel of a short child run of THIS build on THIS box:
     one rocprofv3 pass per counter (FETCH_SIZE, WRITE_SIZE; they do not fit one pass), bytes =
@@ -187,6 +280,7 @@ def live_pmc(args):
             files = list(pathlib.Path(d).rglob("*counter_collection.csv"))
             if r.returncode != 0 or not files:
                 return None, f"rocprofv3 --pmc {ctr} failed (rc={r.returncode})"
+            _keep_profile(args, files[0], f"pmc_{ctr}.csv")
             for row in csv.DictReader(open(files[0])):
                 if row.get("Counter_Name") == ctr:
                     vals.setdefault(kernel_key(row["Kernel_Name"]), {}).setdefault(ctr, []).append(
@@ -238,9 +332,22 @@ def main():
     args = parse()
     if args.pmc_child:
         return pmc_child(args)
+    if args.trace_child:
+        return trace_child(args)
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch N ranks for "
+                 f"--gpus N (or run plain `python bench.py --gpus N`, which launches them)")
+    if os.environ.get("PGMG_BENCH_LAUNCH_STUB") == "1":
+        # CPU test of the launcher (tests/test_bench_cpu.py): report the rank, touch no GPU
+        print(json.dumps({"stub_rank": rank, "world": world, "local_rank": local_rank}), flush=True)
+        return None
     # CPU baselines first, before this process touches the GPU (child processes)
     cpu = cpu1 = cpu4 = None
     if world == 1 and rank == 0 and args.cpu_baseline == "auto" and args.dtype == "f64":
@@ -263,6 +370,9 @@ def main():
     pmc, pmc_note = None, "off"
     if world == 1 and rank == 0 and args.pmc == "auto":
         pmc, pmc_note = live_pmc(args)
+    trace, trace_note = None, "off"
+    if world == 1 and rank == 0 and args.trace == "auto":
+        trace, trace_note = live_trace(args)
     import torch  # noqa: F401  (loads the ROCm runtime first; see _capi.load)
     import _pkgload
     pg = _pkgload.load()
@@ -276,6 +386,10 @@ def main():
     # (PGMG_FLAG_HOST_TRANSPORT): a real multi-process solve, parity-checked, not a timing
     host_tp = world > 1 and not solo and os.environ.get("PGMG_BENCH_TRANSPORT") == "host"
     device = 0 if (world == 1 or solo or host_tp) else local_rank
+    if world > 1 and device >= torch.cuda.device_count():
+        sys.exit(f"bench.py: rank {rank} needs GPU {device}, this box has "
+                 f"{torch.cuda.device_count()} (PGMG_BENCH_SOLO=1 or PGMG_BENCH_TRANSPORT=host "
+                 f"for a one-GPU harness test)")
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(device)
@@ -351,6 +465,7 @@ def main():
     if (world == 1 and args.cycle == "V" and args.general_rhs == "auto" and main_leg["fused"]
             and main_leg["gen"]):
         gen_leg = run_leg(pg.PGMG_FLAG_STORED_RHS, 3)
+        gen_leg["stored"] = True
 
     # BASELINE.json's other GPU configs on this one GPU (timed after the headline legs, each
     # with the reference's hash of its result; the 8-GPU configs' grids as one GPU's run)
@@ -527,6 +642,15 @@ def main():
                          "traffic_ratio": round(traffic / nbytes, 4) if traffic else None,
                          "bytes_per_launch": nbytes, "launches_timed": cnt,
                          "ms_per_launch": round(ms, 5)})
+            tr = trace.get(key) if trace is not None and not leg.get("fast") and not leg.get(
+                "stored") else None
+            if tr is not None:
+                ach_r = nbytes / (tr[1] * 1e-3) / 1e9
+                roof[-1].update({"ms_per_launch_rocprof": round(tr[1], 5),
+                                 "launches_rocprof": tr[0],
+                                 "frac_rocprof": round(ach_r / HBM_PEAK_GBPS, 4),
+                                 "event_vs_rocprof": round(ms / tr[1], 4),
+                                 "rocprof_source": trace_note})
         # the dominant kernel: largest total time over the timed region
         roof.sort(key=lambda r: -r["ms_per_launch"] * r["launches_timed"])
         return roof
@@ -601,6 +725,7 @@ def main():
             # each sample carries its per-cycle times and their spread
             "cpu_host": {"model": _cpu_model(), "nproc": os.cpu_count(), "cores_used": 1},
             "pmc": pmc_note,
+            "trace": trace_note,
             "build": lib_build_id(),
         }
         if others is not None:

@@ -107,14 +107,20 @@ extern "C" {
                                    order, so phi agrees with the EXACT default within
                                    1e-12 relative (after <= 10 cycles) instead of bitwise.
                                    One GPU (row strips ignore it); everything else exact */
-#define PGMG_FLAG_NO_SPEC_FIRE 8192u /* speculative calls without segment planning,
+#define PGMG_FLAG_NO_SPEC_FIRE 32768u /* speculative calls without segment planning,
                                        per-cycle speculation windows and levels predicted
                                        to fire (the r02 policy: a level that will fire
                                        decides in-stream from the call's start), and
                                        W-cycles without plans (every bulk check
-                                       in-stream).  Results are identical either way */
-/* (16384u: the 129x129 level inside the tail's launch -- built in r03, bitwise, measured
-   slower (one CU's fp64 VALU: ~1.2 us per pass over 129^2 points); removed) */
+                                       in-stream).  Results are identical either way.
+                                       (8192u until r03.)                              */
+/* Retired bits, rejected by pgmg_create with PGMG_ERR_ARG so that a caller built against an
+   older header fails loudly instead of silently getting another option:
+   8192u  -- PGMG_FLAG_L1POST until r02 (level 1's post-smooth inside the finest pass; removed
+             in r03), then PGMG_FLAG_NO_SPEC_FIRE in r03;
+   16384u -- the 129x129 level inside the tail's launch (built in r03, bitwise, measured
+             slower: one CU's fp64 VALU needs ~1.2 us per pass over 129^2 points; removed) */
+#define PGMG_FLAGS_RETIRED (8192u | 16384u)
 #define PGMG_FLAG_HOST_TRANSPORT 2048u /* world > 1 without RCCL: nccl_unique_id points to
                                        a pgmg_host_transport; every message and reduction
                                        is staged through host memory and handed to the
@@ -209,6 +215,10 @@ int pgmg_problem_device_info(pgmg_ctx *ctx, int *bound, int *inplace);
  * pgmg_set_problem_device needs (the mirror's stand-in for cudaMallocManaged). */
 int pgmg_alloc_grid(double **ptr, int N);
 int pgmg_free_grid(double *ptr);
+/* *serial = a number unique to this pgmg_alloc_grid allocation (never reused), 0 when ptr is
+ * not a live pgmg_alloc_grid grid: lets a caller that caches a binding by pointer (the mirror's
+ * ParallelMultiGridSolver) notice a grid freed and re-allocated at the same address. */
+int pgmg_grid_serial(const double *ptr, unsigned long long *serial);
 /* *is_device = 1 when p is device (or managed) memory of the HIP runtime. */
 int pgmg_pointer_is_device(const void *p, int *is_device);
 

@@ -35,7 +35,8 @@ PGMG_FLAG_NO_PIN = 512
 PGMG_FLAG_NO_R2 = 1024
 PGMG_FLAG_HOST_TRANSPORT = 2048
 PGMG_FLAG_FAST = 4096
-PGMG_FLAG_NO_SPEC_FIRE = 8192
+PGMG_FLAG_NO_SPEC_FIRE = 32768
+PGMG_FLAGS_RETIRED = 8192 | 16384
 
 PGMG_PRECISION_FP64 = 0
 PGMG_PRECISION_FP32 = 1
@@ -93,6 +94,7 @@ SIGNATURES = [
     ("pgmg_problem_device_info", C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("pgmg_alloc_grid", C.c_int, [C.POINTER(_P), C.c_int]),
     ("pgmg_free_grid", C.c_int, [_P]),
+    ("pgmg_grid_serial", C.c_int, [_P, C.POINTER(C.c_ulonglong)]),
     ("pgmg_pointer_is_device", C.c_int, [_P, C.POINTER(C.c_int)]),
     ("pgmg_vcycle", C.c_int, [_P, C.c_int]),
     ("pgmg_wcycle", C.c_int, [_P, C.c_int]),

@@ -73,6 +73,9 @@ struct pgmg_ctx {
     bool fsmooth_swapped = false; // an F-cycle swapped L.A / L.B of a level (fused smooth(3))
     bool have_problem = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // device-bound calls: recorded on the null stream at entry, so c->s (non-blocking) starts
+    // after the caller's outstanding default-stream work (order_after_caller)
+    hipEvent_t ev_caller = nullptr;
     struct EventPool {
         std::vector<hipEvent_t> ev;
         int used = 0;

@@ -91,7 +91,12 @@ static bool registered_span(intptr_t lo, intptr_t hi)
 
 namespace {
 std::mutex g_user_mu;
-std::map<uintptr_t, void *> g_user_grids;   // pgmg_alloc_grid: element (0,0) -> allocation
+struct UserGrid {
+    void *alloc;
+    unsigned long long serial;   // distinct for every pgmg_alloc_grid call (pgmg_grid_serial)
+};
+std::map<uintptr_t, UserGrid> g_user_grids;   // pgmg_alloc_grid: element (0,0) -> allocation
+unsigned long long g_user_serial = 0;
 }  // namespace
 
 static bool is_device_ptr(const void *p)
@@ -890,6 +895,7 @@ int pgmg_destroy(pgmg_ctx *c)
         for (auto e : pool.ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->ev_caller) (void)hipEventDestroy(c->ev_caller);
     delete c->comm;
     if (c->s) (void)hipStreamDestroy(c->s);
     delete c;
@@ -911,6 +917,9 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         return set_err(PGMG_ERR_ARG, "precision must be PGMG_PRECISION_FP64 or _FP32");
     if (!(cfg->h0 >= 0.0) || !std::isfinite(cfg->h0))
         return set_err(PGMG_ERR_ARG, "h0 must be finite and >= 0 (0: a / (N - 1))");
+    if (cfg->flags & PGMG_FLAGS_RETIRED)
+        return set_err(PGMG_ERR_ARG, "retired PGMG_FLAG_* bit (8192 / 16384; include/pgmg.h): "
+                                     "PGMG_FLAG_NO_SPEC_FIRE is 32768 since r04");
     int ndev = 0;
     HIPC(hipGetDeviceCount(&ndev));
     if (cfg->device < 0 || cfg->device >= ndev) return set_err(PGMG_ERR_ARG, "bad device ordinal");
@@ -1011,7 +1020,8 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         if (hipMemset(c->flags, 0, sizeof(unsigned) * nflags) != hipSuccess ||
             hipMemset(c->stats, 0, 4 * sizeof(unsigned long long)) != hipSuccess ||
             hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess)
+            hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_caller, hipEventDisableTiming) != hipSuccess)
             rc = set_err(PGMG_ERR_HIP, "stream/event setup failed");
     }
     if (rc == PGMG_OK && (cfg->flags & PGMG_FLAG_TIME_FINE)) {
@@ -1241,7 +1251,7 @@ int pgmg_alloc_grid(double **out, int N)
     double *o = static_cast<double *>(p) + guard;
     {
         std::lock_guard<std::mutex> lk(g_user_mu);
-        g_user_grids[(uintptr_t)o] = p;
+        g_user_grids[(uintptr_t)o] = UserGrid{p, ++g_user_serial};
     }
     *out = o;
     return PGMG_OK;
@@ -1255,11 +1265,20 @@ int pgmg_free_grid(double *o)
         std::lock_guard<std::mutex> lk(g_user_mu);
         auto it = g_user_grids.find((uintptr_t)o);
         if (it == g_user_grids.end()) return set_err(PGMG_ERR_ARG, "pgmg_free_grid: not from pgmg_alloc_grid");
-        p = it->second;
+        p = it->second.alloc;
         g_user_grids.erase(it);
     }
     unregister_alloc(p);
     HIPC(hipFree(p));
+    return PGMG_OK;
+}
+
+int pgmg_grid_serial(const double *o, unsigned long long *serial)
+{
+    if (!serial) return set_err(PGMG_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(g_user_mu);
+    auto it = g_user_grids.find((uintptr_t)o);
+    *serial = it == g_user_grids.end() ? 0ull : it->second.serial;
     return PGMG_OK;
 }
 
@@ -1299,10 +1318,26 @@ static void ext_frames(pgmg_ctx *c)
         if (g->base) launch_copy_frame<T>(c->ext_phi, L.N, G<T>(*g), L.P, L.N, c->s);
 }
 
+// The reference's v_cycle is synchronous on the default stream; the context's stream is
+// non-blocking, so a device-bound call first orders it after whatever the caller queued on
+// the null stream (an async copy into phi, a kernel writing f).  Work on the caller's own
+// non-blocking streams is the caller's to synchronise (include/pgmg.h).  The wait is skipped
+// when the null stream is already idle (the usual case: the previous call synchronised).
+static int order_after_caller(pgmg_ctx *c)
+{
+    HIPC(hipEventRecord(c->ev_caller, nullptr));
+    const hipError_t q = hipEventQuery(c->ev_caller);
+    if (q == hipSuccess) return PGMG_OK;
+    if (q != hipErrorNotReady) return set_err(PGMG_ERR_HIP, hipGetErrorString(q));
+    HIPC(hipStreamWaitEvent(c->s, c->ev_caller, 0));
+    return PGMG_OK;
+}
+
 // before a call: the caller's f into the level-0 RHS grid (unless analytic) and phi's frame
 // (in place) or all of phi (staged) into the level-0 grids
 static int ext_stage_in(pgmg_ctx *c, bool inplace)
 {
+    PGMG_TRY(order_after_caller(c));
     Level &L = c->lv[0];
     const int N = L.N;
     if (c->ext_f) {
@@ -2185,6 +2220,12 @@ int pgmg_fcycle(pgmg_ctx *c, int ncycles)
     const bool gen = c->nb > 0 && !(c->cfg.flags & PGMG_FLAG_STORED_RHS);
     c->rgfx = gen ? c->fmg_gtab + 8 : nullptr;
     c->rgsy = gen ? c->fmg_gtab + (8 + L0.N + 1024) + 8 : nullptr;
+    // a device-bound problem (pgmg_set_problem_device): the F-cycle restricts and climbs on
+    // the level-0 grids, so the caller's phi is staged into L.A first (after in-place V/W
+    // calls L.A is stale: those calls read and write the caller's array) and the result is
+    // copied back; synchronous, like the V/W calls on a bound problem
+    const bool ext = c->ext_phi != nullptr;
+    if (ext) PGMG_TRY(ext_stage_in(c, false));
     HIPC(hipEventRecord(c->ev0, c->s));
     for (int k = 0; k < ncycles && !e; ++k) {
         e = c->fp32 ? enqueue_fcycle<float>(c) : enqueue_fcycle<double>(c);
@@ -2199,6 +2240,10 @@ int pgmg_fcycle(pgmg_ctx *c, int ncycles)
     if (e) return e;
     HIPC(hipGetLastError());
     HIPC(hipEventRecord(c->ev1, c->s));
+    if (ext) {
+        PGMG_TRY(ext_stage_out(c));
+        PGMG_TRY(stream_wait(c));
+    }
     return PGMG_OK;
 }
 

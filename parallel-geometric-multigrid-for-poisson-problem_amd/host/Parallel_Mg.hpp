@@ -17,11 +17,14 @@
 //     early-exit speculation history) lasts while the caller passes the same pointers.
 //   * phi and f HOST arrays: uploaded and downloaded around every call (the general
 //     fallback for callers whose arrays are not on the device).
+//   * mixed: a device phi with a host f binds phi and a device copy of f (uploaded at every
+//     call); a host phi with a device f reads f back and takes the host path.
 // The context (level pyramid in HBM) is created on first use for a given (N, h, epsilon)
 // and kept; h is the caller's finest mesh width, doubled per level as the reference does.
 #pragma once
 #include <memory>
 #include <stdexcept>
+#include <vector>
 
 #include "pgmg.hpp"
 
@@ -56,6 +59,11 @@ class ParallelMultiGridSolver {
         return inplace;
     }
 
+    // forget the device binding: the next call binds (phi, f) afresh (statistics and the
+    // early-exit speculation history restart).  Calls rebind by themselves when the pointers
+    // change or a pgmg_alloc_grid phi / f was freed and re-allocated at the same address.
+    void rebind() { bound_phi = bound_f = nullptr; }
+
   private:
     int alpha;
     int ctx_N = 0;
@@ -63,6 +71,16 @@ class ParallelMultiGridSolver {
     std::unique_ptr<pgmg_host::Context> ctx;
     const double *analytic_f = nullptr;
     const double *bound_phi = nullptr, *bound_f = nullptr;
+    unsigned long long bound_phi_serial = 0, bound_f_serial = 0;
+    // f staged on the device when phi is a device array and f a host one
+    std::unique_ptr<pgmg_host::DeviceArray> f_dev;
+
+    static unsigned long long serial_of(const double *p)
+    {
+        unsigned long long s = 0;
+        pgmg_host::check(pgmg_grid_serial(p, &s), "pgmg_grid_serial");
+        return s;
+    }
 
     void cycle(double *phi, double *f, int N, double h, bool w)
     {
@@ -72,22 +90,43 @@ class ParallelMultiGridSolver {
             ctx_N = N;
             ctx_eps = epsilon;
             ctx_h = h;
-            bound_phi = bound_f = nullptr;
+            rebind();
         }
         pgmg_ctx *c = ctx->get();
         const char *what = w ? "pgmg_wcycle" : "pgmg_vcycle";
-        if (pgmg_host::is_device_pointer(phi)) {
-            if (bound_phi != phi || bound_f != f) {
-                pgmg_host::check(pgmg_set_problem_device(c, phi, f == analytic_f ? nullptr : f),
-                                 "pgmg_set_problem_device");
+        const bool phi_dev = pgmg_host::is_device_pointer(phi);
+        const bool f_dev_ptr = f != nullptr && pgmg_host::is_device_pointer(f);
+        if (phi_dev) {
+            // f for the device binding: the analytic RHS (regenerated), the caller's device f,
+            // or a host f copied into a device array of our own at every call
+            const double *fb = f == analytic_f ? nullptr : f;
+            if (fb && !f_dev_ptr) {
+                const size_t n = (size_t)N * N;
+                if (!f_dev || f_dev->size() != n) f_dev.reset(new pgmg_host::DeviceArray(n));
+                f_dev->upload(f);
+                fb = f_dev->get();
+            }
+            const unsigned long long ps = serial_of(phi), fs = fb ? serial_of(fb) : 0;
+            if (bound_phi != phi || bound_f != fb || bound_phi_serial != ps || bound_f_serial != fs) {
+                pgmg_host::check(pgmg_set_problem_device(c, phi, fb), "pgmg_set_problem_device");
                 bound_phi = phi;
-                bound_f = f;
+                bound_f = fb;
+                bound_phi_serial = ps;
+                bound_f_serial = fs;
             }
             pgmg_host::check(w ? pgmg_wcycle(c, 1) : pgmg_vcycle(c, 1), what);
             return;
         }
-        bound_phi = bound_f = nullptr;
-        pgmg_host::check(pgmg_set_problem(c, phi, f), "pgmg_set_problem");
+        rebind();
+        // host phi: upload / download around the call (a device f is read back first)
+        std::vector<double> fh;
+        const double *fp = f;
+        if (f_dev_ptr) {
+            fh.resize((size_t)N * N);
+            pgmg_host::check(pgmg_memcpy_d2h(fh.data(), f, fh.size() * sizeof(double)), "f to host");
+            fp = fh.data();
+        }
+        pgmg_host::check(pgmg_set_problem(c, phi, fp), "pgmg_set_problem");
         pgmg_host::check(w ? pgmg_wcycle(c, 1) : pgmg_vcycle(c, 1), what);
         pgmg_host::check(pgmg_get_solution(c, phi), "pgmg_get_solution");
     }

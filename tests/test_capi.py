@@ -75,3 +75,29 @@ def test_create_fails_loudly_without_gpu(pgmg):
 def test_bad_grid_size_rejected(pgmg):
     with pytest.raises(pgmg.PgmgError):
         pgmg.Solver(100)
+
+
+def test_flag_constants_match_header(pgmg):
+    """Every PGMG_FLAG_* the Python plumbing names has the header's value."""
+    from importlib import import_module
+    capi = import_module("pgmg_amd._capi")
+    txt = HEADER.read_text()
+    vals = {m.group(1): int(m.group(2)) for m in
+            re.finditer(r"#define (PGMG_FLAG_[A-Z0-9_]+) (\d+)u", txt)}
+    assert vals["PGMG_FLAG_NO_SPEC_FIRE"] == 32768
+    for name, v in vals.items():
+        if hasattr(capi, name):
+            assert getattr(capi, name) == v, name
+
+
+@pytest.mark.parametrize("bit", [8192, 16384])
+def test_retired_flag_bits_rejected(pgmg, bit):
+    """A flag bit that meant something else in an older header (8192: PGMG_FLAG_L1POST, then
+    r03's PGMG_FLAG_NO_SPEC_FIRE; 16384) fails pgmg_create with PGMG_ERR_ARG before any device
+    call, instead of silently selecting another option."""
+    lib = pgmg.load()
+    cfg = pgmg.default_config(129)
+    cfg.flags = bit
+    h = C.c_void_p()
+    assert lib.pgmg_create(C.byref(h), C.byref(cfg)) == -1   # PGMG_ERR_ARG
+    assert not h.value

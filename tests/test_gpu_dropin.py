@@ -183,3 +183,61 @@ def test_inplace_full_size_single_calls(pgmg, golden_cycles):
     want = next(c for c in golden_cycles if c["kind"] == "V" and c["N"] == 16385)
     from oracle import fnv_hash
     assert fnv_hash(got) == want["cycles"][19]["hash"]
+
+
+@pytest.mark.parametrize("foreign", [False, True])
+def test_fcycle_on_bound_problem(pgmg, foreign):
+    """pgmg_fcycle on a device-bound problem: the F-cycle restricts and climbs
+    on the level-0 grids, so the caller's phi -- updated in place by the V-cycles before it -- is
+    staged in and the result written back.  V, F, V, F on the bound phi is bitwise the same
+    sequence on a host problem, and pgmg_get_solution / the hash read the bound result."""
+    import torch
+    N = 513
+    seq = [("V", 1), ("F", 1), ("V", 2), ("F", 1)]
+    with pgmg.Solver(N, cross_min_n=33) as s:
+        s.set_problem()
+        for k, n in seq:
+            (s.vcycle if k == "V" else s.fcycle)(n)
+        want, want_sw = s.solution(), s.stats()[0]
+    if foreign:
+        phi = torch.zeros((N, N), dtype=torch.float64, device="cuda")
+    else:
+        phi = pgmg.DeviceGrid(N)
+    torch.cuda.synchronize()
+    with pgmg.Solver(N, cross_min_n=33) as s:
+        s.set_problem_device(phi)
+        assert s.device_info() == (True, not foreign)
+        for k, n in seq:
+            (s.vcycle if k == "V" else s.fcycle)(n)
+            got = phi.cpu().numpy() if foreign else phi.download()
+            assert_bitwise(s.solution(), got, f"bound phi after {k}")
+        assert s.stats()[0] == want_sw
+    assert_bitwise(got, want, f"V/F sequence on a bound phi (foreign={foreign})")
+    if not foreign:
+        phi.close()
+
+
+def test_bound_call_waits_for_default_stream_work(pgmg, oracle_mod):
+    """A bound call orders the context's (non-blocking) stream after the caller's outstanding
+    null-stream work: phi is written by a copy queued on torch's default
+    stream behind a long kernel chain, and the cycle is called without any synchronisation."""
+    import torch
+    N = 513
+    rng = np.random.default_rng(11)
+    phi0 = np.zeros((N, N))
+    phi0[1:-1, 1:-1] = rng.uniform(-1, 1, (N - 2, N - 2))
+    want, sw = _oracle_phi(oracle_mod, N, 1, phi0=phi0)
+    src = torch.tensor(phi0, device="cuda")
+    phi = torch.zeros((N, N), dtype=torch.float64, device="cuda")
+    big = torch.randn((4096, 4096), dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    with pgmg.Solver(N, cross_min_n=33) as s:
+        s.set_problem_device(phi)
+        assert torch.cuda.current_stream().cuda_stream == 0   # the null stream
+        for _ in range(4):              # ~tens of ms of fp64 GEMMs on the null stream
+            big = big @ big
+            big = big / big.abs().max()
+        phi.copy_(src)                  # queued behind them, not yet done
+        s.vcycle(1)                     # no torch.cuda.synchronize() before the call
+        assert s.stats()[0] == sw
+    assert_bitwise(phi.cpu().numpy(), want, "phi written on the null stream before the call")
