@@ -87,6 +87,10 @@ def parse():
                          "ParallelMultiGridSolver::v_cycle called once per cycle through the C++ "
                          "mirror (host/gpu_exec, device arrays in place) -- and the context API's "
                          "one-cycle calls it is measured against")
+    ap.add_argument("--ops", choices=["auto", "off"], default="auto",
+                    help="auto (one GPU, V, f64): the per-op study at --n -- pgmg_jacobi / "
+                         "residual / restrict / prolong on reference-layout arrays (the "
+                         "Parallel::Compute* entries), GB/s and roofline fraction per op")
     ap.add_argument("--trace", choices=["auto", "off"], default="auto",
                     help="auto: a rocprofv3 --kernel-trace --stats pass over a child run of the "
                          "timed call (warmup + steps cycles), before this process touches the "
@@ -178,6 +182,92 @@ def pmc_child(args):
             s.sync()
 
 
+# algorithmic bytes per interior point of each op (fine grid n = (N-2)^2,
+# coarse nc = (Nc-2)^2): Jacobi sweep 24 (read x, f; write x_new), residual 24, restriction
+# 8 per fine + 8 per coarse point, prolongation 16 per fine (RMW) + 8 per coarse point
+def op_cases(pg, n):
+    """The per-op study (ParallelTestRunner.cu:231-468 times ComputeJacobi(v = 100),
+    ComputeResidual, ComputeRestriction, ComputeProlungator) on reference-layout device arrays
+    at grid n: [(name, call, bytes per call, kernel keys, sweeps)], and the arrays."""
+    import torch
+    dev = torch.device("cuda:0")
+    h = 1.0 / (n - 1)
+    nc = (n - 1) // 2 + 1
+    fine, coarse = float((n - 2) ** 2), float((nc - 2) ** 2)
+    x = torch.zeros((n, n), dtype=torch.float64, device=dev)
+    f = torch.empty_like(x)
+    pg.ops.rhs(f, h)
+    tmp = torch.empty_like(x)
+    r = torch.zeros_like(x)
+    c = torch.zeros((nc, nc), dtype=torch.float64, device=dev)
+    e = torch.ones((nc, nc), dtype=torch.float64, device=dev)
+    sweep = ["k_op_sweep<4,false,true,false>", "k_op_sweep<4,false,false,false>"]
+    cases = [
+        ("jacobi v=1 (2 sweeps, no early exit: Parallel::ComputeJacobi's call in the V-cycle)",
+         lambda: pg.ops.jacobi(x, f, h, 1, eps=-1.0, tmp=tmp), 2 * 24 * fine, sweep, 2),
+        ("jacobi v=100 (101 sweeps, no early exit: the per-op study's ComputeJacobi call)",
+         lambda: pg.ops.jacobi(x, f, h, 100, eps=-1.0, tmp=tmp), 101 * 24 * fine, sweep, 101),
+        ("jacobi v=1 with the smoother's early-exit checks (JacobiSmoother::smooth)",
+         lambda: pg.ops.jacobi(x, f, h, 1, eps=1e-7, tmp=tmp), 2 * 24 * fine,
+         ["k_op_sweep<4,true,false,false>"], 2),
+        ("residual (ComputeResidual)", lambda: pg.ops.residual(r, x, f, h), 24 * fine,
+         ["k_op_residual<4>"], 0),
+        ("restriction (ComputeRestriction)", lambda: pg.ops.restrict(r, c), 8 * fine + 8 * coarse,
+         ["k_op_restrict<4>"], 0),
+        ("prolongation, symmetric over the reference's launch grid (ComputeProlungator, "
+         "num_thread 32)",
+         lambda: pg.ops.prolong(e, r, mode=pg.PGMG_PROLONG_SYMMETRIC, num_thread=32),
+         16 * fine + 8 * coarse, ["k_op_prolong<1>"], 0),
+        ("prolongation, the CPU path's (MultiGrid.hpp:208-226)",
+         lambda: pg.ops.prolong(e, r, mode=pg.PGMG_PROLONG_REFERENCE), 16 * fine + 8 * coarse,
+         ["k_op_prolong<0>"], 0),
+    ]
+    return cases, (x, f, tmp, r, c, e)
+
+
+def op_study(pg, n, trace, reps=5):
+    """Each op of op_cases called `reps` times after one warmup call on the null stream,
+    timed with events around each call (median); beside it the op's kernels' rocprof average
+    from the trace pass (same box, same build)."""
+    import torch
+    cases, keep = op_cases(pg, n)
+    out = []
+    for name, call, nbytes, keys, sweeps in cases:
+        call()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            call()
+            b.record()
+            b.synchronize()
+            ts.append(a.elapsed_time(b))
+        ms = statistics.median(ts)
+        row = {"op": name, "ms_per_call": round(ms, 5), "bytes_per_call": nbytes,
+               "achieved_gbps": round(nbytes / (ms * 1e-3) / 1e9, 1),
+               "frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
+        if sweeps:
+            per = nbytes / sweeps
+            row["ms_per_sweep"] = round(ms / sweeps, 5)
+            if trace is not None:
+                tk = [(k, trace[k]) for k in keys if k in trace]
+                if tk:
+                    calls = sum(v[0] for _, v in tk)
+                    avg = sum(v[0] * v[1] for _, v in tk) / calls
+                    row.update({"kernel_rocprof": [k for k, _ in tk],
+                                "ms_per_sweep_rocprof": round(avg, 5),
+                                "frac_sweep_rocprof": round(per / (avg * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)})
+        elif trace is not None and keys[0] in trace:
+            avg = trace[keys[0]][1]
+            row.update({"kernel_rocprof": keys[0], "ms_per_launch_rocprof": round(avg, 5),
+                        "frac_rocprof": round(nbytes / (avg * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)})
+        out.append(row)
+    del keep
+    torch.cuda.empty_cache()
+    return out
+
+
 def trace_child(args):
     """The program the kernel-trace pass profiles: the timed call of the main leg (a fresh
     problem, warmup cycles, then `steps` cycles in one call), then exit."""
@@ -191,6 +281,14 @@ def trace_child(args):
         s.sync()
         run(args.steps)
         s.sync()
+    if args.ops == "auto" and args.cycle == "V" and args.dtype == "f64":
+        import torch
+        cases, keep = op_cases(pg, args.n)
+        for _, call, _, _, _ in cases:
+            for _ in range(3):
+                call()
+        torch.cuda.synchronize()
+        del keep
 
 
 def _keep_profile(args, src, name):
@@ -213,7 +311,7 @@ def live_trace(args):
     cmd = ["timeout", "-s", "KILL", "300", prof, "--kernel-trace", "--stats", "--output-format",
            "csv", "-d", d, "-o", "run", "--", sys.executable, str(ROOT / "bench.py"),
            "--trace-child", "--n", str(args.n), "--dtype", args.dtype, "--cycle", args.cycle,
-           "--steps", str(args.steps), "--warmup", str(args.warmup)]
+           "--steps", str(args.steps), "--warmup", str(args.warmup), "--ops", args.ops]
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=330)
         files = list(pathlib.Path(d).rglob("*kernel_stats.csv"))
@@ -250,9 +348,13 @@ def launch_ranks(args):
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
+    # torch.distributed.run's parser rejects a script argument that abbreviates one of its own
+    # options ("--n" could be --nnodes / --nproc-per-node ...): pass the grid as --N
+    fwd = ["--N" if a == "--n" else ("--N=" + a[4:] if a.startswith("--n=") else a)
+           for a in sys.argv[1:]]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
-           f"--master-port={port}", str(ROOT / "bench.py")] + sys.argv[1:]
+           f"--master-port={port}", str(ROOT / "bench.py")] + fwd
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
     return subprocess.run(cmd, env=env).returncode
 
@@ -346,13 +448,15 @@ def main():
                  f"--gpus N (or run plain `python bench.py --gpus N`, which launches them)")
     if os.environ.get("PGMG_BENCH_LAUNCH_STUB") == "1":
         # CPU test of the launcher (tests/test_bench_cpu.py): report the rank, touch no GPU
-        print(json.dumps({"stub_rank": rank, "world": world, "local_rank": local_rank}), flush=True)
+        print(json.dumps({"stub_rank": rank, "world": world, "local_rank": local_rank,
+                          "n": args.n}), flush=True)
         return None
     # CPU baselines first, before this process touches the GPU (child processes)
     cpu = cpu1 = cpu4 = None
     if world == 1 and rank == 0 and args.cpu_baseline == "auto" and args.dtype == "f64":
         try:
-            cpu = cpu_baseline(args.cpu_n or args.n, kind=args.cycle)
+            # two timed cycles (~2 x 8-10 s at N = 16385 for the reference): a spread
+            cpu = cpu_baseline(args.cpu_n or args.n, cycles=2, kind=args.cycle)
         except Exception as e:  # reported, not fatal
             cpu = {"value": None, "unit": f"{args.cycle}-cycles/s", "cores": 1, "kind": "port",
                    "sample": f"failed: {e}"}
@@ -607,6 +711,15 @@ def main():
                     "sweep_counts_equal": ref_sw == got_sw}
         del sols, ref_phi, got_phi, d
 
+    # the per-op study (Parallel::Compute* on reference-layout arrays), VERDICT r03 #3
+    op_rows = None
+    if world == 1 and args.cycle == "V" and args.dtype == "f64" and args.ops == "auto":
+        op_rows = op_study(pg, args.n, trace)
+        if args.save_profiles:
+            pathlib.Path(args.save_profiles).mkdir(parents=True, exist_ok=True)
+            (pathlib.Path(args.save_profiles) / "ops_table.json").write_text(
+                json.dumps({"N": args.n, "build": lib_build_id(), "ops": op_rows}, indent=1))
+
     T = "double" if args.dtype == "f64" else "float"
 
     def roofline(leg):
@@ -732,6 +845,13 @@ def main():
             line["other_configs"] = others
         if dropin is not None:
             line["dropin"] = dropin
+        if op_rows is not None:
+            line["ops"] = {"what": "the per-op study at N = %d: the reference's op-level GPU "
+                                   "entries (Parallel::Compute*, Parallel_Method.cu:144-199) on "
+                                   "reference-layout device arrays; bytes per SURVEY §8(d) over "
+                                   "the interior points; event time per call (median of 5) and "
+                                   "the kernels' rocprofv3 average from the trace pass" % args.n,
+                           "table": op_rows}
         if fast_leg is not None:
             fast_leg["fast"] = True
             fmed = statistics.median(fast_leg["times"])

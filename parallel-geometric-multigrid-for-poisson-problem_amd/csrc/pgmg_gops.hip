@@ -1,9 +1,28 @@
 // pgmg_gops.hip — op-level kernels on caller-owned arrays in the reference layout
-// (row-major, pitch = W, no alignment guarantee).  These back the C-ABI entries
-// that mirror Parallel::Compute* (3_part_parallel/Parallel_Method.cu:144-199);
-// the V-cycle itself uses the aligned, row-marching kernels of pgmg_kernels.hip.
-// One thread per point, grid-stride with a fixed grid so the per-block partial
-// sums (and thus any early-exit decision) are deterministic run to run.
+// (row-major, pitch = W, no padding, no alignment guarantee).  These back the C-ABI entries
+// that mirror Parallel::ComputeJacobi / ComputeResidual / ComputeRestriction /
+// ComputeProlungator (3_part_parallel/Parallel_Method.cu:144-199) and the per-op study that
+// times them (ParallelTestRunner.cu:231-468); the V-cycle itself uses the aligned, fused
+// passes of pgmg_fused.hip.
+//
+// Same streaming scheme as the level kernels (pgmg_kernels.hip), adapted to the caller's
+// layout:
+//   * lane t of a wave owns the column pair (c, c+1), c = 1 + 2t: one 16-byte load per row
+//     and array.  With an odd pitch (every reference grid: W = 2^k + 1) every other row's
+//     pairs are only 8-byte aligned; gfx950 runs in unaligned-access mode, so they are still
+//     one global_load/store_dwordx4 each (ldvu / stvu, pgmg_real.h), a wave's 1 KiB row
+//     segment spanning 9 cache lines instead of 8;
+//   * workgroups march down bands of rows keeping the rows above and below in registers, U
+//     rows of loads issued before any is used, so each input element crosses HBM once per
+//     op (plus one halo row per band);
+//   * horizontal neighbours come from the adjacent lane by DPP (wave_shr / wave_shl); only
+//     a wave's edge lanes load a halo column;
+//   * no 64-bit division in the index path (the r03 kernels were one thread per point with a
+//     k / (W - 2), k % (W - 2) per point).
+// Expressions and their order are the reference's, file:line at each kernel; the build uses
+// -ffp-contract=off, so every value is bit-identical to the CPU reference (the KATs in
+// tests/test_gpu_parity.py).  Per-block partial sums use a fixed grid, so early-exit
+// decisions are deterministic run to run.
 #include "pgmg_internal.h"
 
 namespace pgmg {
@@ -22,54 +41,180 @@ __device__ __forceinline__ double gblock_sum(double v, double *red)
     return s;
 }
 
-int g_blocks(int H, int W)
+__device__ __forceinline__ void st_nt1(double *p, double v) { __builtin_nontemporal_store(v, p); }
+template <bool NT>
+__device__ __forceinline__ void st2(double *p, double2 v)
 {
-    const long long n = (long long)(H - 2) * (W - 2);
-    long long nb = (n + kBlock - 1) / kBlock;
-    if (nb > 2048) nb = 2048;
-    if (nb < 1) nb = 1;
-    return (int)nb;
+    if (NT) {
+        __builtin_nontemporal_store(v.x, p);
+        __builtin_nontemporal_store(v.y, p + 1);
+    } else {
+        stvu<double>(p, v);
+    }
 }
 
-// Smoother.hpp:63-70 (sweep) and :75-76 (residual of the input, for the check)
-__global__ __launch_bounds__(kBlock) void k_g_sweep(const double *x, const double *f, double *out,
-                                                    double *partials, const unsigned *skip,
-                                                    unsigned *reset, unsigned long long *stats,
-                                                    double hh, double ih, int H, int W)
+// Geometry of a row-marching op over `rows` rows of `pairs` lane pairs: gx column blocks of
+// kBlock lanes, gy bands of rpb rows (a multiple of U), about `target` workgroups in all.
+struct OpGeom {
+    int gx, gy, rpb;
+};
+static OpGeom op_geom(int pairs, int rows, int U, int target)
+{
+    OpGeom g;
+    g.gx = (pairs + kBlock - 1) / kBlock;
+    long long rpb = ((long long)rows * g.gx + target - 1) / target;
+    if (rpb < U) rpb = U;
+    rpb = (rpb + U - 1) / U * U;
+    if (rows < 1) rows = 1;
+    g.rpb = (int)rpb;
+    g.gy = (int)((rows + rpb - 1) / rpb);
+    if (g.gy < 1) g.gy = 1;
+    return g;
+}
+
+// ---------------------------------------------------------------------------
+// One Jacobi sweep, out-of-place.  Smoother.hpp:63-70 (JacobiSmoother::smooth):
+//   out[i] = 0.25 * ((h*h*f[i]) + x[i-1] + x[i+1] + x[i-W] + x[i+W])
+// CHECK: per-block partial sums of r(x)^2 of the INPUT x (the early-exit check of the
+// previous sweep's result, DynamicGridUtils.hpp:59-69 + norm; decided by k_g_fixup):
+//   r[i] = f[i] - (1.0/(h*h)) * (4*x[i] - x[i-1] - x[i+1] - x[i-W] - x[i+W])
+// SEED: also copy x's boundary (rows 0, H-1; columns 0, W-1) into out, so a ping-pong buffer
+// needs no full seed copy (the next sweep reads the boundary as neighbours).
+// ---------------------------------------------------------------------------
+template <int U, bool CHECK, bool SEED, bool NT>
+__global__ __launch_bounds__(kBlock) void k_op_sweep(const double *__restrict__ X,
+                                                     const double *__restrict__ F,
+                                                     double *__restrict__ O, double *partials,
+                                                     const unsigned *skip, unsigned *reset,
+                                                     unsigned long long *stats, double hh,
+                                                     double ih, int H, int W, int rpb)
 {
     __shared__ double red[kBlock / 64];
-    if (skip != nullptr && *skip != 0u) return;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (skip != nullptr && *skip != 0u) return;  // the smoother already exited (uniform)
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
         if (reset != nullptr) *reset = 0u;
         if (stats != nullptr) atomicAdd(&stats[0], 1ull);
     }
-    const long long n = (long long)(H - 2) * (W - 2);
+    const int lane = threadIdx.x & 63;
+    const int npairs = (W - 1) >> 1;
+    const int t_raw = blockIdx.x * kBlock + threadIdx.x;
+    const bool act = t_raw < npairs;
+    const int t = act ? t_raw : npairs - 1;  // idle lanes shadow the last pair
+    const int c = 1 + 2 * t;
+    const bool second = c + 1 <= W - 2;      // else column c+1 is the right boundary
+    const bool lastp = t == npairs - 1;
+    const bool ld_l = lane == 0;
+    // the right neighbour of column c+1: the next lane's column, loaded by a wave's last lane
+    // and by the last pair (W even: its next lane shadows it)
+    const bool ld_r = (lane == 63 || lastp) && second;
+    const int jb = 1 + blockIdx.y * rpb;
+    const int je = min(jb + rpb, H - 1);
+    const long long Wl = W;
     double acc = 0.0;
-    for (long long k = (long long)blockIdx.x * kBlock + threadIdx.x; k < n;
-         k += (long long)gridDim.x * kBlock) {
-        const long long j = 1 + k / (W - 2);
-        const long long i = 1 + k % (W - 2);
-        const long long q = j * W + i;
-        out[q] = 0.25 * ((hh * f[q]) + x[q - 1] + x[q + 1] + x[q - W] + x[q + W]);
-        if (partials != nullptr) {
-            const double r = f[q] - ih * (4 * x[q] - x[q - 1] - x[q + 1] - x[q - W] - x[q + W]);
-            acc += r * r;
+
+    double2 w0 = ldvu<double>(X + (long long)(jb - 1) * Wl + c);
+    double2 w1 = ldvu<double>(X + (long long)jb * Wl + c);
+    if (SEED && jb == 1 && act) st2<false>(O + c, w0);
+    for (int j = jb; j < je; j += U) {
+        double2 xn[U], fv[U];
+        double el[U], er[U];
+        #pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long long r = min(j + u, je - 1);
+            fv[u] = ldvu<double>(F + r * Wl + c);
+            xn[u] = ldvu<double>(X + (r + 1) * Wl + c);
+            el[u] = ld_l ? X[r * Wl + c - 1] : 0.0;
+            er[u] = ld_r ? X[r * Wl + c + 2] : 0.0;
         }
+        #pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = j + u;
+            const double2 up = (u == 0) ? w0 : (u == 1 ? w1 : xn[u - 2]);
+            const double2 ce = (u == 0) ? w1 : xn[u - 1];
+            const double2 dn = xn[u];
+            double left = dpp_shr(ce.y);
+            double right = dpp_shl(ce.x);
+            if (ld_l) left = el[u];
+            if (ld_r) right = er[u];
+            double2 o;
+            o.x = 0.25 * ((hh * fv[u].x) + left + ce.y + up.x + dn.x);
+            o.y = second ? 0.25 * ((hh * fv[u].y) + ce.x + right + up.y + dn.y) : ce.y;
+            const bool live = act && r < je;
+            if (CHECK) {
+                const double r0 = fv[u].x - ih * (4 * ce.x - left - ce.y - up.x - dn.x);
+                const double r1 = fv[u].y - ih * (4 * ce.y - ce.x - right - up.y - dn.y);
+                if (live) {
+                    acc += r0 * r0;
+                    if (second) acc += r1 * r1;
+                }
+            }
+            if (live) {
+                double *q = O + (long long)r * Wl + c;
+                st2<NT>(q, o);
+                if (SEED) {
+                    if (t == 0) q[-1] = el[u];
+                    if (lastp && second) q[2] = er[u];
+                }
+            }
+        }
+        w0 = xn[U - 2];
+        w1 = xn[U - 1];
     }
-    if (partials != nullptr) {
+    if (SEED && je == H - 1 && act) st2<false>(O + (long long)(H - 1) * Wl + c, w1);
+    if (CHECK) {
         const double s = gblock_sum<kBlock>(acc, red);
-        if (threadIdx.x == 0) partials[blockIdx.x] = s;
+        if (threadIdx.x == 0) partials[blockIdx.y * gridDim.x + blockIdx.x] = s;
     }
+}
+
+constexpr int kOpTarget = 4096;   // workgroups per op launch (16 per CU)
+
+int g_blocks(int H, int W)
+{
+    const int U = tuning_int("PGMG_OP_U", 4) == 8 ? 8 : 4;
+    const OpGeom g = op_geom((W - 1) / 2, H - 2, U, tuning_int("PGMG_OP_BLOCKS", kOpTarget));
+    return g.gx * g.gy;
+}
+
+template <int U, bool CHECK, bool SEED>
+static void sweep_u(const OpGeom &g, bool nt, const double *xin, const double *f, double *xout,
+                    double *partials, const unsigned *skip, unsigned *reset,
+                    unsigned long long *stats, double hh, double ih, int H, int W, hipStream_t s)
+{
+    const dim3 grid(g.gx, g.gy);
+    if (nt)
+        k_op_sweep<U, CHECK, SEED, true><<<grid, kBlock, 0, s>>>(xin, f, xout, partials, skip, reset,
+                                                                stats, hh, ih, H, W, g.rpb);
+    else
+        k_op_sweep<U, CHECK, SEED, false><<<grid, kBlock, 0, s>>>(xin, f, xout, partials, skip,
+                                                                 reset, stats, hh, ih, H, W, g.rpb);
 }
 
 void launch_g_sweep(const double *xin, const double *f, double *xout, double *partials,
                     const unsigned *skip, unsigned *reset, unsigned long long *stats, double hh,
-                    double inv_hh, int H, int W, int nblocks, hipStream_t s)
+                    double inv_hh, int H, int W, bool seed, hipStream_t s)
 {
-    k_g_sweep<<<dim3(nblocks), dim3(kBlock), 0, s>>>(xin, f, xout, partials, skip, reset, stats,
-                                                      hh, inv_hh, H, W);
+    const int U = tuning_int("PGMG_OP_U", 4) == 8 ? 8 : 4;
+    const OpGeom g = op_geom((W - 1) / 2, H - 2, U, tuning_int("PGMG_OP_BLOCKS", kOpTarget));
+    const bool nt = tuning_int("PGMG_OP_NT", 0) != 0;
+    const bool chk = partials != nullptr;
+#define PGMG_SW(UU)                                                                                \
+    do {                                                                                           \
+        if (chk && seed) sweep_u<UU, true, true>(g, nt, xin, f, xout, partials, skip, reset, stats, hh, inv_hh, H, W, s); \
+        else if (chk) sweep_u<UU, true, false>(g, nt, xin, f, xout, partials, skip, reset, stats, hh, inv_hh, H, W, s); \
+        else if (seed) sweep_u<UU, false, true>(g, nt, xin, f, xout, partials, skip, reset, stats, hh, inv_hh, H, W, s); \
+        else sweep_u<UU, false, false>(g, nt, xin, f, xout, partials, skip, reset, stats, hh, inv_hh, H, W, s); \
+    } while (0)
+    if (U == 8) PGMG_SW(8);
+    else PGMG_SW(4);
+#undef PGMG_SW
 }
 
+// ---------------------------------------------------------------------------
+// Early-exit decision after a checked sweep (Smoother.hpp:75-80): re-reduce the partials in a
+// fixed order; when sqrt(sum) < eps the sweep that followed the check is undone (out := in on
+// the interior) and every later sweep of the call skips.  Rare path: only when a check fires.
+// ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_g_fixup(const double *partials, int np, double eps,
                                                     const unsigned *done_prev, unsigned *done_next,
                                                     const double *src, double *dst,
@@ -95,12 +240,10 @@ __global__ __launch_bounds__(kBlock) void k_g_fixup(const double *partials, int 
         }
     }
     if (!trig) return;
-    const long long n = (long long)(H - 2) * (W - 2);
-    for (long long k = (long long)blockIdx.x * kBlock + threadIdx.x; k < n;
-         k += (long long)gridDim.x * kBlock) {
-        const long long q = (1 + k / (W - 2)) * W + 1 + k % (W - 2);
-        dst[q] = src[q];
-    }
+    // rows of the interior over the blocks, columns over the threads
+    const long long Wl = W;
+    for (int r = 1 + blockIdx.x; r < H - 1; r += gridDim.x)
+        for (int i = 1 + threadIdx.x; i < W - 1; i += kBlock) dst[r * Wl + i] = src[r * Wl + i];
 }
 
 void launch_g_fixup(const double *partials, int np, double eps, const unsigned *done_prev,
@@ -111,112 +254,287 @@ void launch_g_fixup(const double *partials, int np, double eps, const unsigned *
                                                   dst, stats, H, W);
 }
 
-__global__ void k_g_copy(const double *src, double *dst, long long n)
+// interior copy dst := src (rows 1 .. H-2, columns 1 .. W-2): the result of an odd number of
+// sweeps from the ping-pong buffer back into the caller's x (its boundary is already x's)
+template <int U>
+__global__ __launch_bounds__(kBlock) void k_op_copy_interior(const double *__restrict__ src,
+                                                             double *__restrict__ dst, int H,
+                                                             int W, int rpb)
 {
-    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n;
-         k += (long long)gridDim.x * blockDim.x)
-        dst[k] = src[k];
+    const int npairs = (W - 1) >> 1;
+    const int t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= npairs) return;
+    const int c = 1 + 2 * t;
+    const bool second = c + 1 <= W - 2;
+    const int jb = 1 + blockIdx.y * rpb;
+    const int je = min(jb + rpb, H - 1);
+    const long long Wl = W;
+    for (int j = jb; j < je; j += U) {
+        double2 v[U];
+        #pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = ldvu<double>(src + (long long)min(j + u, je - 1) * Wl + c);
+        #pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (j + u >= je) break;
+            double *q = dst + (long long)(j + u) * Wl + c;
+            if (second) stvu<double>(q, v[u]);
+            else q[0] = v[u].x;
+        }
+    }
 }
 
-void launch_g_copy(const double *src, double *dst, long long n, hipStream_t s)
+void launch_g_copy_interior(const double *src, double *dst, int H, int W, hipStream_t s)
 {
-    long long nb = (n + 255) / 256;
-    if (nb > 4096) nb = 4096;
-    if (nb < 1) nb = 1;
-    k_g_copy<<<dim3((unsigned)nb), dim3(256), 0, s>>>(src, dst, n);
+    const OpGeom g = op_geom((W - 1) / 2, H - 2, 4, kOpTarget);
+    k_op_copy_interior<4><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(src, dst, H, W, g.rpb);
 }
 
-// DynamicGridUtils.hpp:59-69; boundary of r untouched
-__global__ void k_g_residual(double *r, const double *x, const double *f, double ih, int H, int W)
+// ---------------------------------------------------------------------------
+// Residual on the interior, DynamicGridUtils.hpp:59-69 (= Parallel_Method.cu:29-49's
+// device_compute_residual); the boundary of r is untouched:
+//   r[i] = f[i] - (1.0/(h*h)) * (4*x[i] - x[i-1] - x[i+1] - x[i-W] - x[i+W])
+// ---------------------------------------------------------------------------
+template <int U>
+__global__ __launch_bounds__(kBlock) void k_op_residual(double *__restrict__ R,
+                                                        const double *__restrict__ X,
+                                                        const double *__restrict__ F, double ih,
+                                                        int H, int W, int rpb)
 {
-    const long long n = (long long)(H - 2) * (W - 2);
-    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n;
-         k += (long long)gridDim.x * blockDim.x) {
-        const long long q = (1 + k / (W - 2)) * W + 1 + k % (W - 2);
-        r[q] = f[q] - ih * (4 * x[q] - x[q - 1] - x[q + 1] - x[q - W] - x[q + W]);
+    const int lane = threadIdx.x & 63;
+    const int npairs = (W - 1) >> 1;
+    const int t_raw = blockIdx.x * kBlock + threadIdx.x;
+    const bool act = t_raw < npairs;
+    const int t = act ? t_raw : npairs - 1;
+    const int c = 1 + 2 * t;
+    const bool second = c + 1 <= W - 2;
+    const bool ld_l = lane == 0;
+    const bool ld_r = (lane == 63 || t == npairs - 1) && second;
+    const int jb = 1 + blockIdx.y * rpb;
+    const int je = min(jb + rpb, H - 1);
+    const long long Wl = W;
+    double2 w0 = ldvu<double>(X + (long long)(jb - 1) * Wl + c);
+    double2 w1 = ldvu<double>(X + (long long)jb * Wl + c);
+    for (int j = jb; j < je; j += U) {
+        double2 xn[U], fv[U];
+        double el[U], er[U];
+        #pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long long r = min(j + u, je - 1);
+            fv[u] = ldvu<double>(F + r * Wl + c);
+            xn[u] = ldvu<double>(X + (r + 1) * Wl + c);
+            el[u] = ld_l ? X[r * Wl + c - 1] : 0.0;
+            er[u] = ld_r ? X[r * Wl + c + 2] : 0.0;
+        }
+        #pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const double2 up = (u == 0) ? w0 : (u == 1 ? w1 : xn[u - 2]);
+            const double2 ce = (u == 0) ? w1 : xn[u - 1];
+            const double2 dn = xn[u];
+            double left = dpp_shr(ce.y);
+            double right = dpp_shl(ce.x);
+            if (ld_l) left = el[u];
+            if (ld_r) right = er[u];
+            double2 o;
+            o.x = fv[u].x - ih * (4 * ce.x - left - ce.y - up.x - dn.x);
+            o.y = fv[u].y - ih * (4 * ce.y - ce.x - right - up.y - dn.y);
+            if (act && j + u < je) {
+                double *q = R + (long long)(j + u) * Wl + c;
+                if (second) stvu<double>(q, o);
+                else q[0] = o.x;
+            }
+        }
+        w0 = xn[U - 2];
+        w1 = xn[U - 1];
     }
 }
 
 void launch_g_residual(double *r, const double *x, const double *f, double inv_hh, int H, int W,
                        hipStream_t s)
 {
-    k_g_residual<<<dim3(g_blocks(H, W)), dim3(kBlock), 0, s>>>(r, x, f, inv_hh, H, W);
+    const OpGeom g = op_geom((W - 1) / 2, H - 2, 4, tuning_int("PGMG_OP_BLOCKS", kOpTarget));
+    k_op_residual<4><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(r, x, f, inv_hh, H, W, g.rpb);
 }
 
-// MultiGrid.hpp:187-205; coarse boundary untouched
-__global__ void k_g_restrict(const double *Fn, double *C, int Nf, int Nc)
+// ---------------------------------------------------------------------------
+// Full-weighting restriction, MultiGrid.hpp:187-205 (= Parallel_Method.cu:51-77's
+// restriction_kernel_full_weighting); the coarse boundary is untouched:
+//   C[jc][ic] = 0.25*F[k] + 0.125*(F[k+1] + F[k-1] + F[k+Nf] + F[k-Nf])
+//             + 0.0625*(F[k-Nf-1] + F[k-Nf+1] + F[k+Nf-1] + F[k+Nf+1]),  k = 2jc*Nf + 2ic
+// Lane t owns coarse column ic = 1 + t and loads the fine pair (2ic, 2ic+1) of each fine row;
+// column 2ic-1 is the previous lane's second element (DPP), a wave's lane 0 loads it.  A band
+// of coarse rows marches down the fine rows 2jc-1 .. 2jc+1, carrying the shared row 2jc+1.
+// ---------------------------------------------------------------------------
+template <int U>
+__global__ __launch_bounds__(kBlock) void k_op_restrict(const double *__restrict__ Fn,
+                                                        double *__restrict__ C, int Nf, int Nc,
+                                                        int rpb)
 {
-    const long long n = (long long)(Nc - 2) * (Nc - 2);
-    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n;
-         k += (long long)gridDim.x * blockDim.x) {
-        const long long jc = 1 + k / (Nc - 2), ic = 1 + k % (Nc - 2);
-        const long long q = (2 * jc) * Nf + 2 * ic;
-        C[jc * Nc + ic] = 0.25 * Fn[q] + 0.125 * (Fn[q + 1] + Fn[q - 1] + Fn[q + Nf] + Fn[q - Nf]) +
-                          0.0625 * (Fn[q - Nf - 1] + Fn[q - Nf + 1] + Fn[q + Nf - 1] + Fn[q + Nf + 1]);
+    const int lane = threadIdx.x & 63;
+    const int nic = Nc - 2;
+    const int t_raw = blockIdx.x * kBlock + threadIdx.x;
+    const bool act = t_raw < nic;
+    const int ic = 1 + (act ? t_raw : nic - 1);
+    const int jb = 1 + blockIdx.y * rpb;
+    const int je = min(jb + rpb, Nc - 1);
+    const long long Wf = Nf;
+    const int col = 2 * ic;
+    // fine row 2jb - 1, carried
+    double2 top = ldvu<double>(Fn + (long long)(2 * jb - 1) * Wf + col);
+    double tl = lane == 0 ? Fn[(long long)(2 * jb - 1) * Wf + col - 1] : 0.0;
+    for (int jc = jb; jc < je; jc += U) {
+        double2 mid[U], bot[U];
+        double ml[U], bl[U];
+        #pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long long j = min(jc + u, je - 1);
+            const double *m = Fn + (2 * j) * Wf + col;
+            mid[u] = ldvu<double>(m);
+            bot[u] = ldvu<double>(m + Wf);
+            ml[u] = lane == 0 ? m[-1] : 0.0;
+            bl[u] = lane == 0 ? m[Wf - 1] : 0.0;
+        }
+        #pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const double2 tp = u == 0 ? top : bot[u - 1];
+            const double tlu = u == 0 ? tl : bl[u - 1];
+            // column 2ic - 1 of each row: the previous lane's .y
+            double tL = dpp_shr(tp.y), mL = dpp_shr(mid[u].y), bL = dpp_shr(bot[u].y);
+            if (lane == 0) {
+                tL = tlu;
+                mL = ml[u];
+                bL = bl[u];
+            }
+            // F[k] = mid.x; F[k+1] = mid.y; F[k-1] = mL; F[k+Nf] = bot.x; F[k-Nf] = tp.x;
+            // F[k-Nf-1] = tL; F[k-Nf+1] = tp.y; F[k+Nf-1] = bL; F[k+Nf+1] = bot.y
+            const double v = 0.25 * mid[u].x + 0.125 * (mid[u].y + mL + bot[u].x + tp.x) +
+                             0.0625 * (tL + tp.y + bL + bot[u].y);
+            if (act && jc + u < je) C[(long long)(jc + u) * Nc + ic] = v;
+        }
+        top = bot[U - 1];
+        tl = bl[U - 1];
     }
 }
 
 void launch_g_restrict(const double *fine, double *coarse, int Nf, int Nc, hipStream_t s)
 {
-    k_g_restrict<<<dim3(g_blocks(Nc, Nc)), dim3(kBlock), 0, s>>>(fine, coarse, Nf, Nc);
+    const OpGeom g = op_geom(Nc - 2, Nc - 2, 4, tuning_int("PGMG_OP_BLOCKS", kOpTarget));
+    k_op_restrict<4><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(fine, coarse, Nf, Nc, g.rpb);
 }
 
-// mode 0: MultiGrid.hpp:208-226 (fine row/col 1 uncorrected);
-// mode 1: prolungator_kernel, Parallel_Method.cu:79-138 (symmetric, boundary := 0).
-// Only fine points (y, x) with y, x < ext are touched: the reference's thread grid
-// (ComputeProlungator, Parallel_Method.cu:191-197) covers max(1, Nf / num_thread) * num_thread
-// rows and columns, so for Nf = 2^k + 1 its last fine row and column are never written.
-__global__ void k_g_prolong(const double *C, double *Fn, int Nc, int Nf, int mode, int ext)
+// ---------------------------------------------------------------------------
+// Prolongation, fine += P coarse, over the fine points (y, x) with y, x < ext only: the
+// reference's thread grid (ComputeProlungator, Parallel_Method.cu:191-197) covers
+// max(1, Nf / num_thread) * num_thread rows and columns, so for Nf = 2^k + 1 its last fine
+// row and column are never written (ext = Nf: everything).
+// Lane t owns coarse column ic = t and the fine pair (2ic, 2ic+1); C[ic+1] is the next lane's
+// coarse value (DPP), a wave's last lane loads it.  Fine rows march in pairs (2jc, 2jc+1)
+// reading coarse rows jc and jc+1 (carried).
+//  MODE 0: MultiGrid.hpp:208-226 (the CPU path): rows and columns 2 .. Nf-2 only (fine row /
+//          column 1 never corrected), Fn = Fn + v with
+//          v = C0[ic] | 0.5*(C0[ic] + C0[ic+1]) | 0.5*(C0[ic] + C1[ic])
+//            | 0.25*(C0[ic] + C0[ic+1] + C1[ic] + C1[ic+1])   (even/even, even/odd, odd/even,
+//                                                              odd/odd row/column)
+//  MODE 1: prolungator_kernel, Parallel_Method.cu:79-138 (the GPU reference's symmetric
+//          form): the fine boundary := 0, every interior point (rows / columns 1 .. Nf-2)
+//          Fn += v with the same four cases.
+// ---------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_op_prolong(const double *__restrict__ C,
+                                                       double *__restrict__ Fn, int Nc, int Nf,
+                                                       int ext, int rpb)
 {
+    const int lane = threadIdx.x & 63;
+    const int t_raw = blockIdx.x * kBlock + threadIdx.x;
+    const bool act = t_raw < Nc;
+    const int ic = act ? t_raw : Nc - 1;
     const int E = ext < Nf ? ext : Nf;
-    const long long n = (long long)E * E;
-    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n;
-         k += (long long)gridDim.x * blockDim.x) {
-        const int y = (int)(k / E), x = (int)(k % E);
-        const long long kk = (long long)y * Nf + x;
-        if (mode == 1) {
-            if (y == 0 || y == Nf - 1 || x == 0 || x == Nf - 1) {
-                Fn[kk] = 0.0;
-                continue;
-            }
-            const int cx = x / 2, cy = y / 2;
-            const long long c = (long long)cy * Nc + cx;
-            double v = 0.0;
-            if (x % 2 == 0 && y % 2 == 0) {
-                v = C[c];
-            } else if (x % 2 == 1 && y % 2 == 1) {
-                if (cx + 1 < Nc && cy + 1 < Nc) v = 0.25 * (C[c] + C[c + 1] + C[c + Nc] + C[c + Nc + 1]);
-            } else if (x % 2 == 1 && y % 2 == 0) {
-                if (cx + 1 < Nc) v = 0.5 * (C[c] + C[c + 1]);
-            } else {
-                if (cy + 1 < Nc) v = 0.5 * (C[c] + C[c + Nc]);
-            }
-            Fn[kk] += v;
+    const int x0 = 2 * ic, x1 = 2 * ic + 1;
+    const bool has1 = x1 < Nf;                        // the last coarse column has no odd fine
+    const bool ld_n = (lane == 63 || ic == Nc - 1) ? false : false;
+    (void)ld_n;
+    const long long Wf = Nf, Wc = Nc;
+    // fine rows [yb, ye) of this band, in whole pairs starting at an even row
+    const int yb = 2 * (blockIdx.y * rpb);
+    const int ye = min(yb + 2 * rpb, Nf);
+    // coarse row jc = yb / 2 and its right neighbour column
+    const bool nxt_ok = ic + 1 < Nc;
+    double c0 = C[(long long)(yb >> 1) * Wc + ic];
+    double c0n = (lane == 63 && nxt_ok) ? C[(long long)(yb >> 1) * Wc + ic + 1] : 0.0;
+    for (int y = yb; y < ye; y += 2) {
+        const int jc = y >> 1;
+        const bool has_c1 = jc + 1 < Nc;
+        const double c1 = has_c1 ? C[(long long)(jc + 1) * Wc + ic] : 0.0;
+        const double c1n = (lane == 63 && nxt_ok && has_c1) ? C[(long long)(jc + 1) * Wc + ic + 1] : 0.0;
+        double *p0 = Fn + (long long)y * Wf + x0;
+        double *p1 = p0 + Wf;
+        const bool row1 = y + 1 < ye;
+        double2 f0, f1;
+        if (has1) {
+            f0 = ldvu<double>(p0);
+            f1 = row1 ? ldvu<double>(p1) : f0;
         } else {
-            if (x < 2 || y < 2 || x > Nf - 2 || y > Nf - 2) continue;
-            const long long jc = y >> 1, ic = x >> 1;
-            const double *C0 = C + jc * Nc;
-            double v;
-            if ((y & 1) == 0) {
-                v = ((x & 1) == 0) ? C0[ic] : 0.5 * (C0[ic] + C0[ic + 1]);
-            } else {
-                const double *C1 = C0 + Nc;
-                v = ((x & 1) == 0) ? 0.5 * (C0[ic] + C1[ic])
-                                   : 0.25 * (C0[ic] + C0[ic + 1] + C1[ic] + C1[ic + 1]);
-            }
-            Fn[kk] = Fn[kk] + v;
+            f0.x = p0[0];
+            f0.y = 0.0;
+            f1.x = row1 ? p1[0] : 0.0;
+            f1.y = 0.0;
         }
+        // next coarse column by DPP (lane 63: its own load)
+        double a_n = dpp_shl(c0), b_n = dpp_shl(c1);
+        if (lane == 63) {
+            a_n = c0n;
+            b_n = c1n;
+        }
+        // even fine row y: (y, x0) = c0; (y, x1) = 0.5*(c0 + a_n)
+        // odd fine row y+1: (y+1, x0) = 0.5*(c0 + c1); (y+1, x1) = 0.25*(c0 + a_n + c1 + b_n)
+        const double v00 = c0;
+        const double v01 = 0.5 * (c0 + a_n);
+        const double v10 = 0.5 * (c0 + c1);
+        const double v11 = 0.25 * (c0 + a_n + c1 + b_n);
+        double2 o0 = f0, o1 = f1;
+        if (MODE == 0) {
+            // rows / columns 2 .. Nf-2
+            const bool cx0 = x0 >= 2 && x0 <= Nf - 2, cx1 = x1 >= 2 && x1 <= Nf - 2;
+            const bool ry0 = y >= 2 && y <= Nf - 2, ry1 = y + 1 >= 2 && y + 1 <= Nf - 2;
+            if (ry0 && cx0) o0.x = f0.x + v00;
+            if (ry0 && cx1) o0.y = f0.y + v01;
+            if (ry1 && cx0) o1.x = f1.x + v10;
+            if (ry1 && cx1) o1.y = f1.y + v11;
+        } else {
+            const bool b0 = x0 == 0 || x0 == Nf - 1, b1 = x1 == Nf - 1;
+            const bool yb0 = y == 0 || y == Nf - 1, yb1 = y + 1 == Nf - 1;
+            o0.x = (yb0 || b0) ? 0.0 : f0.x + v00;
+            o0.y = (yb0 || b1) ? 0.0 : f0.y + v01;
+            o1.x = (yb1 || b0) ? 0.0 : f1.x + v10;
+            o1.y = (yb1 || b1) ? 0.0 : f1.y + v11;
+        }
+        // write only the points inside the reference's launch extent
+        if (act && y < E) {
+            if (has1 && x1 < E) stvu<double>(p0, o0);
+            else if (x0 < E) p0[0] = o0.x;
+        }
+        if (act && row1 && y + 1 < E) {
+            if (has1 && x1 < E) stvu<double>(p1, o1);
+            else if (x0 < E) p1[0] = o1.x;
+        }
+        c0 = c1;
+        c0n = c1n;
     }
 }
 
 void launch_g_prolong(const double *coarse, double *fine, int Nc, int Nf, int mode, int ext,
                       hipStream_t s)
 {
-    long long nb = ((long long)Nf * Nf + 255) / 256;
-    if (nb > 4096) nb = 4096;
-    k_g_prolong<<<dim3((unsigned)nb), dim3(256), 0, s>>>(coarse, fine, Nc, Nf, mode, ext);
+    // one band = rpb coarse rows = 2 rpb fine rows
+    const OpGeom g = op_geom(Nc, (Nf + 1) / 2, 1, tuning_int("PGMG_OP_BLOCKS", kOpTarget));
+    const dim3 grid(g.gx, g.gy);
+    if (mode == 1) k_op_prolong<1><<<grid, kBlock, 0, s>>>(coarse, fine, Nc, Nf, ext, g.rpb);
+    else k_op_prolong<0><<<grid, kBlock, 0, s>>>(coarse, fine, Nc, Nf, ext, g.rpb);
 }
 
+// ---------------------------------------------------------------------------
+// sum of squares (DynamicGridUtils::norm's sum, DynamicGridUtils.hpp:71-80): per-block
+// partials over a flat array, 16-byte loads where the array allows
+// ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_g_sumsq(const double *v, long long n, double *partials)
 {
     __shared__ double red[kBlock / 64];
@@ -233,22 +551,26 @@ void launch_g_sumsq(const double *v, long long n, double *partials, int nblocks,
     k_g_sumsq<<<dim3(nblocks), dim3(kBlock), 0, s>>>(v, n, partials);
 }
 
+// compute_rhs, DynamicGridUtils.hpp:111-124: f[j][i] = factor * sx[i] * sy[j] (the host's
+// sine tables, so bitwise the CPU's values); a block per row band, a thread per column
 __global__ void k_g_rhs(double *f, const double *sx, const double *sy, double factor, int W, int H)
 {
-    const long long n = (long long)W * H;
-    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n;
-         k += (long long)gridDim.x * blockDim.x) {
-        const int j = (int)(k / W), i = (int)(k % W);
-        f[k] = factor * sx[i] * sy[j];
+    const long long Wl = W;
+    for (int j = blockIdx.y; j < H; j += gridDim.y) {
+        const double syj = sy[j];
+        for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < W; i += gridDim.x * blockDim.x)
+            f[j * Wl + i] = factor * sx[i] * syj;
     }
 }
 
 void launch_g_rhs(double *f, const double *sx, const double *sy, double factor, int W, int H,
                   hipStream_t s)
 {
-    long long nb = ((long long)W * H + 255) / 256;
-    if (nb > 4096) nb = 4096;
-    k_g_rhs<<<dim3((unsigned)nb), dim3(256), 0, s>>>(f, sx, sy, factor, W, H);
+    const int gx = (W + 255) / 256;
+    int gy = 4096 / gx;
+    if (gy < 1) gy = 1;
+    if (gy > H) gy = H;
+    k_g_rhs<<<dim3(gx, gy), dim3(256), 0, s>>>(f, sx, sy, factor, W, H);
 }
 
 }  // namespace pgmg

@@ -218,14 +218,17 @@ template <class T>
 void launch_from_double(const double *src, int N, T *dst, int P, int row0, int row1, hipStream_t s);
 
 // reference-layout (pitch = W, any alignment) op kernels
+// one Jacobi sweep; partials != nullptr: per-block sums of r(xin)^2 (g_blocks of them); seed:
+// also copy xin's boundary into xout
 void launch_g_sweep(const double *xin, const double *f, double *xout, double *partials,
                     const unsigned *skip, unsigned *reset, unsigned long long *stats, double hh,
-                    double inv_hh, int H, int W, int nblocks, hipStream_t s);
+                    double inv_hh, int H, int W, bool seed, hipStream_t s);
 int g_blocks(int H, int W);
+constexpr int kOpPartialsCap = 65536;   // partial sums per op scratch set (>= g_blocks)
+void launch_g_copy_interior(const double *src, double *dst, int H, int W, hipStream_t s);
 void launch_g_fixup(const double *partials, int np, double eps, const unsigned *done_prev,
                     unsigned *done_next, const double *src, double *dst,
                     unsigned long long *stats, int H, int W, hipStream_t s);
-void launch_g_copy(const double *src, double *dst, long long n, hipStream_t s);
 void launch_g_residual(double *r, const double *x, const double *f, double inv_hh, int H, int W,
                        hipStream_t s);
 void launch_g_restrict(const double *fine, double *coarse, int Nf, int Nc, hipStream_t s);

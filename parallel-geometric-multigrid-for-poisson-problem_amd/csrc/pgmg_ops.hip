@@ -44,7 +44,7 @@ int ensure_scratch(hipStream_t s, size_t tmp_elems, OpScratch **out)
     std::lock_guard<std::mutex> lk(g_op_mu);
     OpScratch &o = g_ops[s];
     if (!o.partials) {
-        HIPC(hipMalloc((void **)&o.partials, 4096 * sizeof(double)));
+        HIPC(hipMalloc((void **)&o.partials, kOpPartialsCap * sizeof(double)));
         HIPC(hipMalloc((void **)&o.flags, (kMaxSweeps + 2) * 128 * sizeof(unsigned)));
         HIPC(hipMalloc((void **)&o.stats, 4 * sizeof(unsigned long long)));
         HIPC(hipMalloc((void **)&o.scalar, 4 * sizeof(double)));
@@ -84,20 +84,26 @@ int pgmg_jacobi(double *d_x, double *d_tmp, const double *d_f, int H, int W, dou
     // synchronous w.r.t. its own flags because every launch is stream-ordered.
     unsigned *D = g_op.flags;
     HIPC(hipMemsetAsync(g_op.stats, 0, 4 * sizeof(unsigned long long), s));
-    launch_g_copy(d_x, tmp, (long long)L, s);  // Smoother.hpp:47 out seeded with x
     const double hh = h * h, ih = 1.0 / (h * h);
     const int nb = g_blocks(H, W);
+    if (nb > kOpPartialsCap) return set_err(PGMG_ERR_STATE, "pgmg_jacobi: too many blocks");
+    if (check && S >= (kMaxSweeps + 2) * 128)
+        return set_err(PGMG_ERR_ARG, "pgmg_jacobi: v too large for the early-exit flags");
+    // Sweeps alternate x -> tmp -> x ...  No seed copy of tmp (Smoother.hpp:47 copies the whole
+    // grid into its output buffer): the first sweep writes x's boundary into tmp besides the
+    // interior, which is all a later sweep reads of it.  An odd sweep count ends in tmp and
+    // copies its interior back (x's boundary is never written).
     for (int k = 1; k <= S; ++k) {
         const double *in = (k & 1) ? d_x : tmp;
         double *out = (k & 1) ? tmp : d_x;
         const bool with_check = check && k >= 2;
         launch_g_sweep(in, d_f, out, with_check ? g_op.partials : nullptr,
                        with_check ? &D[k - 1] : nullptr, k == 1 ? &D[1] : nullptr, g_op.stats, hh,
-                       ih, H, W, nb, s);
+                       ih, H, W, k == 1, s);
         if (with_check)
             launch_g_fixup(g_op.partials, nb, eps, &D[k - 1], &D[k], in, out, g_op.stats, H, W, s);
     }
-    if (S & 1) launch_g_copy(tmp, d_x, (long long)L, s);
+    if (S & 1) launch_g_copy_interior(tmp, d_x, H, W, s);
     HIPC(hipGetLastError());
     if (sweeps_done) {
         unsigned long long st[4];
@@ -153,7 +159,7 @@ int pgmg_norm(const double *d_v, long long n, double *result, void *stream)
     if (e) return e;
     OpScratch &g_op = *op;
     long long nb = (n + kBlock - 1) / kBlock;
-    if (nb > 1024) nb = 1024;
+    if (nb > 1024) nb = 1024;   // <= kOpPartialsCap
     if (nb < 1) nb = 1;
     launch_g_sumsq(d_v, n, g_op.partials, (int)nb, s);
     launch_sum_partials(g_op.partials, (int)nb, g_op.scalar, s);

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""A/B of the op-level Jacobi sweep's launch geometry (PGMG_OP_BLOCKS, PGMG_OP_U, PGMG_OP_NT)
+on the measurement build (PGMG_LIB=.../libpgmg_ab.so, `make ab`): ms per sweep of
+pgmg_jacobi(v = 100, no early exit) at N = 16385 on reference-layout arrays, variants
+interleaved over rounds, one JSON line per measurement.
+
+    PGMG_LIB=$PWD/parallel-geometric-multigrid-for-poisson-problem_amd/libpgmg_ab.so \\
+        python scripts/op_ab.py [--n 16385] [--rounds 2]
+"""
+import argparse
+import json
+import os
+import pathlib
+import statistics
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=16385)
+ap.add_argument("--rounds", type=int, default=2)
+ap.add_argument("--v", type=int, default=20)
+args = ap.parse_args()
+
+import torch  # noqa: E402
+import _pkgload  # noqa: E402
+
+pg = _pkgload.load()
+n = args.n
+h = 1.0 / (n - 1)
+x = torch.zeros((n, n), dtype=torch.float64, device="cuda:0")
+f = torch.empty_like(x)
+pg.ops.rhs(f, h)
+tmp = torch.empty_like(x)
+byt = 24.0 * (n - 2) ** 2
+variants = []
+for blocks in (2048, 4096, 8192, 16384):
+    for u in (4, 8):
+        for nt in (0, 1):
+            variants.append({"PGMG_OP_BLOCKS": blocks, "PGMG_OP_U": u, "PGMG_OP_NT": nt})
+for rnd in range(args.rounds):
+    for var in variants:
+        for k, v in var.items():
+            os.environ[k] = str(v)
+        pg.ops.jacobi(x, f, h, 1, eps=-1.0, tmp=tmp)
+        ts = []
+        for _ in range(3):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            pg.ops.jacobi(x, f, h, args.v, eps=-1.0, tmp=tmp)
+            b.record()
+            b.synchronize()
+            ts.append(a.elapsed_time(b) / (args.v + 1))
+        ms = statistics.median(ts)
+        print(json.dumps(dict(var, round=rnd, ms_per_sweep=round(ms, 5),
+                              tbps=round(byt / ms / 1e9, 3), frac=round(byt / ms / 1e9 / 8.0, 4))),
+              flush=True)

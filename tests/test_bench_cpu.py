@@ -22,13 +22,16 @@ def _env(**kw):
 
 
 def test_gpus_n_launches_n_ranks():
-    r = subprocess.run([sys.executable, BENCH, "--gpus", "2"] + OFF, capture_output=True,
-                       text=True, timeout=300, env=_env(PGMG_BENCH_LAUNCH_STUB="1"))
+    # --n: an abbreviation of the launcher's own options (--nnodes, ...), forwarded as --N
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--n", "4097"] + OFF,
+                       capture_output=True, text=True, timeout=300,
+                       env=_env(PGMG_BENCH_LAUNCH_STUB="1"))
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     assert sorted(x["stub_rank"] for x in lines) == [0, 1]
     assert all(x["world"] == 2 for x in lines)
     assert sorted(x["local_rank"] for x in lines) == [0, 1]
+    assert all(x["n"] == 4097 for x in lines)
 
 
 def test_gpus_mismatch_with_world_size_fails():
