@@ -37,6 +37,7 @@ PGMG_FLAG_HOST_TRANSPORT = 2048
 PGMG_FLAG_FAST = 4096
 PGMG_FLAG_NO_SPEC_FIRE = 32768
 PGMG_FLAGS_RETIRED = 8192 | 16384
+PGMG_FLAG_NO_CTILE = 65536
 
 PGMG_PRECISION_FP64 = 0
 PGMG_PRECISION_FP32 = 1

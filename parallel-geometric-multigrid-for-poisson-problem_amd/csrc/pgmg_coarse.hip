@@ -1,0 +1,251 @@
+// pgmg_coarse.hip — the latency-bound coarse levels' two passes as 2D LDS tiles.
+//
+// A level entered with x0 = 0 (every level below the finest in a V/W-cycle, RECOMP) costs
+// two fused passes: k_pre (x1 = J(0), the check ||r(x1)||, x2 = J(x1), rc = R r(x2)) and
+// k_post (the pre-smoothed iterate recomputed from f, + P ec, two sweeps with the check
+// ||r(x1)||).  pgmg_fused.hip runs them as row-marching bands: right for the bulk levels,
+// where HBM streaming is what counts, but on the small levels (N <= 1025: 0.02-1 M points)
+// the launch spends its ~6 µs in ONE wave's serial chain -- a band of 2 coarse rows marches
+// 12 fine rows (3x redundant) with four stencil stages per row, ~1000 VALU + 700 SALU
+// instructions per wave, one wave per SIMD, nothing to hide the latency behind
+// (profiles/r03_final/levels: k_pre at 129 7.4 µs, 64 waves, wait 47 % / issue 51 %).
+//
+// Here a workgroup owns a TC x TC tile of coarse points and the fine points around it:
+// it loads its f window (+ halo) once, then every stencil stage is one point per thread over
+// the window in LDS, a barrier between stages -- ~5 short stages instead of a 12-row chain.
+// The halo is recomputed by neighbouring tiles (~1.7x redundant points at TC = 8), spread
+// over 256 threads instead of serialised in one wave.
+//
+// Semantics are exactly k_pre / k_post's (pgmg_fused.hip pre_body / post_body with
+// X0_ZERO, RECOMP, no strips, no regenerated f), every value through the reference's
+// expression in its order (MultiGrid.hpp:57-94, Smoother.hpp:59-88, DynamicGridUtils.hpp:
+// 59-69, MultiGrid.hpp:187-226), so the results are bitwise those of the row-marching
+// passes; only the check's per-block partial sums are grouped differently (their order is
+// not part of the contract; the count goes with them into the check's record).
+#include "pgmg.h"
+#include "pgmg_coarse.h"
+
+namespace pgmg {
+
+constexpr int kCT = 256;   // threads per tile workgroup
+
+template <class T> __device__ __forceinline__ double csq(double acc, T r)
+{
+    return __builtin_fma((double)r, (double)r, acc);
+}
+
+__device__ __forceinline__ double ctile_block_sum(double v, double *red)
+{
+    v = wave_sum(v);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double s = 0.0;
+    if (threadIdx.x == 0)
+        for (int i = 0; i < kCT / 64; ++i) s += red[i];
+    return s;
+}
+
+// ---------------------------------------------------------------------------
+// pre: coarse tile rows [jca, jcb) x columns [ica, icb) of rc; window of fine points
+// (2 jca - 3 + i, 2 ica - 3 + j), i, j in [0, W): rc at (jc, ic) needs r(x2) at fine points
+// 2jc-1 .. 2jc+1, r(x2) needs x2 one further, x2 needs x1 one further (x1 = J(0) pointwise)
+// ---------------------------------------------------------------------------
+template <class T, int TC>
+__global__ __launch_bounds__(kCT) void k_pre_tile(CoarseArgsT<T> a)
+{
+    constexpr int W = 2 * TC + 5;
+    constexpr int W2 = W - 2, W4 = W - 4;
+    __shared__ T sF[W * W], sX1[W * W], sX2[W2 * W2], sR[W4 * W4];
+    __shared__ double red[kCT / 64];
+    const int N = a.N, Nc = a.Nc;
+    const long long P = a.P, Pc = a.Pc;
+    const T hh = a.hh, ih = a.ih;
+    const int jca = 1 + blockIdx.y * TC, jcb = min(jca + TC, Nc - 1);
+    const int ica = 1 + blockIdx.x * TC, icb = min(ica + TC, Nc - 1);
+    const int y0 = 2 * jca - 3, x0 = 2 * ica - 3;
+    // the check's fine points owned by this tile: a partition of the interior
+    const int oy0 = 2 * jca - 1, oy1 = jcb == Nc - 1 ? N - 1 : 2 * jcb - 1;
+    const int ox0 = 2 * ica - 1, ox1 = icb == Nc - 1 ? N - 1 : 2 * icb - 1;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+        if (a.stats != nullptr) atomicAdd(&a.stats[0], 2ull);
+        if (a.fired != nullptr) *a.fired = 0u;   // the pre check's outcome for k_post RECOMP
+    }
+    // x1 = J(0) = 0.25 * ((hh*f) + 0) on the interior, 0 on and outside the boundary
+    for (int q = threadIdx.x; q < W * W; q += kCT) {
+        const int i = q / W, j = q - (q / W) * W;
+        const int y = y0 + i, x = x0 + j;
+        const bool in = y >= 1 && y <= N - 2 && x >= 1 && x <= N - 2;
+        const T fv = in ? a.f[y * P + x] : T(0);
+        sF[q] = fv;
+        sX1[q] = in ? T(0.25) * ((hh * fv) + T(0)) : T(0);
+    }
+    __syncthreads();
+    // x2 = J(x1); the check's r(x1) on the owned points
+    double acc = 0.0;
+    for (int q = threadIdx.x; q < W2 * W2; q += kCT) {
+        const int i = 1 + q / W2, j = 1 + (q - (q / W2) * W2);
+        const int y = y0 + i, x = x0 + j;
+        const bool in = y >= 1 && y <= N - 2 && x >= 1 && x <= N - 2;
+        const int k = i * W + j;
+        const T c = sX1[k], l = sX1[k - 1], r = sX1[k + 1], u = sX1[k - W], d = sX1[k + W];
+        const T fv = sF[k];
+        sX2[q] = in ? T(0.25) * ((hh * fv) + l + r + u + d) : c;
+        if (in && y >= oy0 && y < oy1 && x >= ox0 && x < ox1) {
+            const T r1 = fv - ih * (T(4) * c - l - r - u - d);
+            acc = csq(acc, r1);
+        }
+    }
+    __syncthreads();
+    // r(x2) on the window's inner points (garbage-free: only interior points feed rc)
+    for (int q = threadIdx.x; q < W4 * W4; q += kCT) {
+        const int i = 2 + q / W4, j = 2 + (q - (q / W4) * W4);
+        const int k = (i - 1) * W2 + (j - 1);
+        const T c = sX2[k], l = sX2[k - 1], r = sX2[k + 1], u = sX2[k - W2], d = sX2[k + W2];
+        sR[q] = sF[i * W + j] - ih * (T(4) * c - l - r - u - d);
+    }
+    __syncthreads();
+    // full-weighting restriction, MultiGrid.hpp:199-202: centre fine point (2jc, 2ic) is window
+    // point (2 (jc - jca) + 3, 2 (ic - ica) + 3), sR point (2 (jc - jca) + 1, 2 (ic - ica) + 1)
+    for (int q = threadIdx.x; q < TC * TC; q += kCT) {
+        const int jc = jca + q / TC, ic = ica + (q - (q / TC) * TC);
+        if (jc < jcb && ic < icb) {
+            const int k = (2 * (jc - jca) + 1) * W4 + 2 * (ic - ica) + 1;
+            const T v = T(0.25) * sR[k] + T(0.125) * (sR[k + 1] + sR[k - 1] + sR[k + W4] + sR[k - W4]) +
+                        T(0.0625) * (sR[k - W4 - 1] + sR[k - W4 + 1] + sR[k + W4 - 1] + sR[k + W4 + 1]);
+            a.rc[jc * Pc + ic] = v;
+        }
+    }
+    const double s = ctile_block_sum(acc, red);
+    if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = s;
+}
+
+// ---------------------------------------------------------------------------
+// post: the fine points of rows [ya, yb) x columns [xa, xb) -- the tile's coarse rows'
+// fine rows 2jc-1, 2jc (the last tile down to N-2; the first / last tile column also writes
+// boundary column 0 / N-1, as k_post does); window (2 jca - 4 + i, 2 ica - 4 + j)
+//   g1 = J(0) -> ph = J(g1) (or g1 if the pre check fired) -> xe = ph + P ec -> x1 = J(xe)
+//   -> x2 = J(x1), the check r(x1) on the owned interior points
+// ---------------------------------------------------------------------------
+template <class T, int TC>
+__global__ __launch_bounds__(kCT) void k_post_tile(CoarseArgsT<T> a)
+{
+    constexpr int W = 2 * TC + 8;
+    constexpr int W2 = W - 2, W4 = W - 4;
+    constexpr int CW = TC + 6;   // coarse rows jca-2 .. jca+TC+3 (xe's prolongation reads)
+    __shared__ T sF[W * W], sG[W * W], sXE[W2 * W2], sX1[W4 * W4], sC[CW * CW];
+    __shared__ double red[kCT / 64];
+    const int N = a.N, Nc = a.Nc;
+    const long long P = a.P, Pc = a.Pc;
+    const T hh = a.hh, ih = a.ih;
+    const int jca = 1 + blockIdx.y * TC, jcb = min(jca + TC, Nc - 1);
+    const int ica = 1 + blockIdx.x * TC, icb = min(ica + TC, Nc - 1);
+    const int y0 = 2 * jca - 4, x0 = 2 * ica - 4;
+    const int cy0 = jca - 2, cx0 = ica - 2;
+    const int ya = 2 * jca - 1, yb = jcb == Nc - 1 ? N - 1 : 2 * jcb - 1;
+    const int xa = ica == 1 ? 0 : 2 * ica - 1, xb = icb == Nc - 1 ? N : 2 * icb - 1;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
+        atomicAdd(&a.stats[0], 2ull);
+    const bool pfired = *a.pre_fired != 0u;
+    for (int q = threadIdx.x; q < W * W; q += kCT) {
+        const int i = q / W, j = q - (q / W) * W;
+        const int y = y0 + i, x = x0 + j;
+        const bool in = y >= 1 && y <= N - 2 && x >= 1 && x <= N - 2;
+        const T fv = in ? a.f[y * P + x] : T(0);
+        sF[q] = fv;
+        sG[q] = in ? T(0.25) * ((hh * fv) + T(0)) : T(0);
+    }
+    for (int q = threadIdx.x; q < CW * CW; q += kCT) {
+        const int m = cy0 + q / CW, n = cx0 + (q - (q / CW) * CW);
+        sC[q] = (m >= 0 && m <= Nc - 1 && n >= 0 && n <= Nc - 1) ? a.ec[m * Pc + n] : T(0);
+    }
+    __syncthreads();
+    // ph = J(g1) (or g1), then + P ec on rows / columns 2 .. N-2 (MultiGrid.hpp:208-226)
+    for (int q = threadIdx.x; q < W2 * W2; q += kCT) {
+        const int i = 1 + q / W2, j = 1 + (q - (q / W2) * W2);
+        const int y = y0 + i, x = x0 + j;
+        const bool in = y >= 1 && y <= N - 2 && x >= 1 && x <= N - 2;
+        const int k = i * W + j;
+        const T c = sG[k];
+        T ph = c;
+        if (in && !pfired) ph = T(0.25) * ((hh * sF[k]) + sG[k - 1] + sG[k + 1] + sG[k - W] + sG[k + W]);
+        if (y >= 2 && y <= N - 2 && x >= 2 && x <= N - 2) {
+            const int m = (y >> 1) - cy0, n = (x >> 1) - cx0;
+            const int kc = m * CW + n;
+            const T c00 = sC[kc], c01 = sC[kc + 1], c10 = sC[kc + CW], c11 = sC[kc + CW + 1];
+            T v;
+            if ((y & 1) == 0) v = (x & 1) == 0 ? c00 : T(0.5) * (c00 + c01);
+            else v = (x & 1) == 0 ? T(0.5) * (c00 + c10) : T(0.25) * (c00 + c01 + c10 + c11);
+            ph = ph + v;
+        }
+        sXE[q] = ph;
+    }
+    __syncthreads();
+    // x1 = J(xe)
+    for (int q = threadIdx.x; q < W4 * W4; q += kCT) {
+        const int i = 2 + q / W4, j = 2 + (q - (q / W4) * W4);
+        const int y = y0 + i, x = x0 + j;
+        const bool in = y >= 1 && y <= N - 2 && x >= 1 && x <= N - 2;
+        const int k = (i - 1) * W2 + (j - 1);
+        const T c = sXE[k];
+        sX1[q] = in ? T(0.25) * ((hh * sF[i * W + j]) + sXE[k - 1] + sXE[k + 1] + sXE[k - W2] + sXE[k + W2]) : c;
+    }
+    __syncthreads();
+    // x2 = J(x1) on the owned points, written; the check's r(x1) on the owned interior
+    double acc = 0.0;
+    const int wc = xb - xa, npts = (yb - ya) * wc;
+    for (int q = threadIdx.x; q < npts; q += kCT) {
+        const int y = ya + q / wc, x = xa + (q - (q / wc) * wc);
+        T out = T(0);   // boundary columns: the passthrough of x1's boundary, 0
+        if (x >= 1 && x <= N - 2) {
+            const int k = (y - y0 - 2) * W4 + (x - x0 - 2);
+            const T c = sX1[k], l = sX1[k - 1], r = sX1[k + 1], u = sX1[k - W4], d = sX1[k + W4];
+            const T fv = sF[(y - y0) * W + (x - x0)];
+            const T r1 = fv - ih * (T(4) * c - l - r - u - d);
+            acc = csq(acc, r1);
+            out = T(0.25) * ((hh * fv) + l + r + u + d);
+        }
+        a.x2[y * P + x] = out;
+    }
+    const double s = ctile_block_sum(acc, red);
+    if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = s;
+}
+
+static int ctile_tc(int N) { return tuning_int("PGMG_CTILE_TC", N >= 1025 ? 16 : 8) == 16 ? 16 : 8; }
+
+bool coarse_tile_ok(int N)
+{
+    return N >= 9 && N <= tuning_int("PGMG_CTILE_MAXN", 1025);
+}
+
+int coarse_tile_blocks(int N)
+{
+    if (!coarse_tile_ok(N)) return 0;
+    const int tc = ctile_tc(N);
+    const int nt = (N / 2 - 1 + tc - 1) / tc;   // interior coarse points (Nc - 2) per side
+    return nt * nt;
+}
+
+template <class T>
+void launch_pre_tile(const CoarseArgsT<T> &a, hipStream_t s)
+{
+    const int tc = ctile_tc(a.N);
+    const int nt = (a.Nc - 2 + tc - 1) / tc;
+    if (tc == 16) k_pre_tile<T, 16><<<dim3(nt, nt), kCT, 0, s>>>(a);
+    else k_pre_tile<T, 8><<<dim3(nt, nt), kCT, 0, s>>>(a);
+}
+
+template <class T>
+void launch_post_tile(const CoarseArgsT<T> &a, hipStream_t s)
+{
+    const int tc = ctile_tc(a.N);
+    const int nt = (a.Nc - 2 + tc - 1) / tc;
+    if (tc == 16) k_post_tile<T, 16><<<dim3(nt, nt), kCT, 0, s>>>(a);
+    else k_post_tile<T, 8><<<dim3(nt, nt), kCT, 0, s>>>(a);
+}
+
+template void launch_pre_tile<double>(const CoarseArgsT<double> &, hipStream_t);
+template void launch_pre_tile<float>(const CoarseArgsT<float> &, hipStream_t);
+template void launch_post_tile<double>(const CoarseArgsT<double> &, hipStream_t);
+template void launch_post_tile<float>(const CoarseArgsT<float> &, hipStream_t);
+
+}  // namespace pgmg

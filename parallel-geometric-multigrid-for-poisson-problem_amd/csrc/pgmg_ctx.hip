@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "pgmg_ctx.h"
+#include "pgmg_coarse.h"
 #include "pgmg_fused.h"
 
 using namespace pgmg;
@@ -445,10 +446,38 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     const int visit = c->cur_visit;   // (the children's visits move it)
     if (wm >= 0) mode = wm;
     if (mode == 1 && (dist || pin || (x0_zero && !recomp))) mode = 2;
+    // the small coarse levels (pgmg_coarse.hip): both passes as 2D LDS tiles, unless the
+    // checks are predicted to fire (the one-sweep passes k_pre1 / k_post1 stay row-marching);
+    // the checks' partial count is the tile count
+    const bool tile = recomp && !dist && !pin && mode != 1 && pa.gfx == nullptr &&
+                      !(c->cfg.flags & PGMG_FLAG_NO_CTILE) && coarse_tile_ok(L.N);
+    CoarseArgsT<T> ca{};
+    if (tile) {
+        fa.np = coarse_tile_blocks(L.N);
+        ca.f = pa.f;
+        ca.ec = G<T>(C.A);
+        ca.rc = pa.rc;
+        ca.x2 = G<T>(L.A);
+        ca.stats = c->stats;
+        ca.fired = fired;
+        ca.pre_fired = fired;
+        ca.hh = pa.hh;
+        ca.ih = pa.ih;
+        ca.N = L.N;
+        ca.P = L.P;
+        ca.Nc = C.N;
+        ca.Pc = C.P;
+    }
     double *lp = chk_log(c, fa.np, l, mode);
     if (lp) pa.partials = lp;
     int ev = fine ? timed_begin(c, 1) : -1;
-    if ((e = mode == 1 ? launch_pre1(pa, x0_zero, c->s) : launch_pre(pa, x0_zero, fine, c->s))) return e;
+    if (tile) {
+        ca.partials = pa.partials;
+        launch_pre_tile(ca, c->s);
+        HIPC(hipGetLastError());
+    } else if ((e = mode == 1 ? launch_pre1(pa, x0_zero, c->s) : launch_pre(pa, x0_zero, fine, c->s))) {
+        return e;
+    }
     if ((e = timed_end(c, 1, ev))) return e;
     if (mode == 2) {
         if (lp) fa.partials = lp;
@@ -494,7 +523,13 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     lp = chk_log(c, fa.np, l, mode);
     if (lp) po.partials = lp;
     ev = fine ? timed_begin(c, 2) : -1;
-    if ((e = mode == 1 ? launch_post1(po, c->s) : launch_post(po, fine, c->s))) return e;
+    if (tile) {
+        ca.partials = po.partials;
+        launch_post_tile(ca, c->s);
+        HIPC(hipGetLastError());
+    } else if ((e = mode == 1 ? launch_post1(po, c->s) : launch_post(po, fine, c->s))) {
+        return e;
+    }
     if ((e = timed_end(c, 2, ev))) return e;
     if (mode == 2) {
         if (lp) fa.partials = lp;
@@ -997,6 +1032,8 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         nbk = fused_blocks(L.N, pr.jc0, pr.jc1);
         if (nbk > maxblocks) maxblocks = nbk;
         nbk = postpre_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2);
+        if (nbk > maxblocks) maxblocks = nbk;
+        nbk = coarse_tile_blocks(L.N);
         if (nbk > maxblocks) maxblocks = nbk;
     }
     if (rc == PGMG_OK && c->cross) rc = alloc_grid(c->S, c->lv[0]);
