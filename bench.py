@@ -201,26 +201,33 @@ def op_cases(pg, n):
     r = torch.zeros_like(x)
     c = torch.zeros((nc, nc), dtype=torch.float64, device=dev)
     e = torch.ones((nc, nc), dtype=torch.float64, device=dev)
-    sweep = ["k_op_sweep<4,false,true,false>", "k_op_sweep<4,false,false,false>"]
+    def sweep(check):   # the sweep kernels' trace keys: k_op_sweep[_ov]<U,CHECK,SEED,NT>
+        return lambda k: k.startswith("k_op_sweep") and k.split("<")[1].split(",")[1] == (
+            "true" if check else "false")
+
+    def named(prefix):
+        return lambda k: k.startswith(prefix)
+
     cases = [
         ("jacobi v=1 (2 sweeps, no early exit: Parallel::ComputeJacobi's call in the V-cycle)",
-         lambda: pg.ops.jacobi(x, f, h, 1, eps=-1.0, tmp=tmp), 2 * 24 * fine, sweep, 2),
+         lambda: pg.ops.jacobi(x, f, h, 1, eps=-1.0, tmp=tmp), 2 * 24 * fine, sweep(False), 2),
         ("jacobi v=100 (101 sweeps, no early exit: the per-op study's ComputeJacobi call)",
-         lambda: pg.ops.jacobi(x, f, h, 100, eps=-1.0, tmp=tmp), 101 * 24 * fine, sweep, 101),
+         lambda: pg.ops.jacobi(x, f, h, 100, eps=-1.0, tmp=tmp), 101 * 24 * fine, sweep(False),
+         101),
         ("jacobi v=1 with the smoother's early-exit checks (JacobiSmoother::smooth)",
          lambda: pg.ops.jacobi(x, f, h, 1, eps=1e-7, tmp=tmp), 2 * 24 * fine,
-         ["k_op_sweep<4,true,false,false>"], 2),
+         sweep(True), 2),
         ("residual (ComputeResidual)", lambda: pg.ops.residual(r, x, f, h), 24 * fine,
-         ["k_op_residual<4>"], 0),
+         named("k_op_residual"), 0),
         ("restriction (ComputeRestriction)", lambda: pg.ops.restrict(r, c), 8 * fine + 8 * coarse,
-         ["k_op_restrict<4>"], 0),
+         named("k_op_restrict"), 0),
         ("prolongation, symmetric over the reference's launch grid (ComputeProlungator, "
          "num_thread 32)",
          lambda: pg.ops.prolong(e, r, mode=pg.PGMG_PROLONG_SYMMETRIC, num_thread=32),
-         16 * fine + 8 * coarse, ["k_op_prolong<1>"], 0),
+         16 * fine + 8 * coarse, named("k_op_prolong<1>"), 0),
         ("prolongation, the CPU path's (MultiGrid.hpp:208-226)",
          lambda: pg.ops.prolong(e, r, mode=pg.PGMG_PROLONG_REFERENCE), 16 * fine + 8 * coarse,
-         ["k_op_prolong<0>"], 0),
+         named("k_op_prolong<0>"), 0),
     ]
     return cases, (x, f, tmp, r, c, e)
 
@@ -251,16 +258,17 @@ def op_study(pg, n, trace, reps=5):
             per = nbytes / sweeps
             row["ms_per_sweep"] = round(ms / sweeps, 5)
             if trace is not None:
-                tk = [(k, trace[k]) for k in keys if k in trace]
+                tk = [(k, v) for k, v in trace.items() if keys(k)]
                 if tk:
                     calls = sum(v[0] for _, v in tk)
                     avg = sum(v[0] * v[1] for _, v in tk) / calls
                     row.update({"kernel_rocprof": [k for k, _ in tk],
                                 "ms_per_sweep_rocprof": round(avg, 5),
                                 "frac_sweep_rocprof": round(per / (avg * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)})
-        elif trace is not None and keys[0] in trace:
-            avg = trace[keys[0]][1]
-            row.update({"kernel_rocprof": keys[0], "ms_per_launch_rocprof": round(avg, 5),
+        elif trace is not None and [k for k in trace if keys(k)]:
+            kk = [k for k in trace if keys(k)][0]
+            avg = trace[kk][1]
+            row.update({"kernel_rocprof": kk, "ms_per_launch_rocprof": round(avg, 5),
                         "frac_rocprof": round(nbytes / (avg * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)})
         out.append(row)
     del keep

@@ -167,45 +167,162 @@ __global__ __launch_bounds__(kBlock) void k_op_sweep(const double *__restrict__ 
     }
 }
 
+// The same sweep with overlapping wave tiles: a wave loads 128 columns (lane t: the pair
+// (124 w - 1 + 2t, +1)) and owns the 124 of lanes 1..62, so every neighbour column comes from
+// an adjacent lane by DPP and no lane issues a halo load of its own (the edge-lane halo loads
+// above double the wave's load instructions; the 4 overlapping columns per wave are L2 hits).
+// Lanes whose pair leaves the row (the grid's first and last columns) load element-wise.
+constexpr int kOvStride = 124;
+
+__device__ __forceinline__ double2 ld_pair(const double *row, int c, int W)
+{
+    if (c >= 0 && c + 1 <= W - 1) return ldvu<double>(row + c);
+    double2 v;
+    v.x = (c >= 0 && c <= W - 1) ? row[c] : 0.0;
+    v.y = (c + 1 >= 0 && c + 1 <= W - 1) ? row[c + 1] : 0.0;
+    return v;
+}
+
+template <bool NT>
+__device__ __forceinline__ void st_owned(double *q, double2 o, bool ox, bool oy)
+{
+    if (ox && oy) st2<NT>(q, o);
+    else if (ox) q[0] = o.x;
+    else if (oy) q[1] = o.y;
+}
+
+template <int U, bool CHECK, bool SEED, bool NT>
+__global__ __launch_bounds__(kBlock) void k_op_sweep_ov(const double *__restrict__ X,
+                                                        const double *__restrict__ F,
+                                                        double *__restrict__ O, double *partials,
+                                                        const unsigned *skip, unsigned *reset,
+                                                        unsigned long long *stats, double hh,
+                                                        double ih, int H, int W, int rpb)
+{
+    __shared__ double red[kBlock / 64];
+    if (skip != nullptr && *skip != 0u) return;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+        if (reset != nullptr) *reset = 0u;
+        if (stats != nullptr) atomicAdd(&stats[0], 1ull);
+    }
+    const int lane = threadIdx.x & 63;
+    const int wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int c = kOvStride * wave - 1 + 2 * lane;
+    const bool mid = lane >= 1 && lane <= 62;
+    const bool ox = mid && c >= 1 && c <= W - 2;
+    const bool oy = mid && c + 1 >= 1 && c + 1 <= W - 2;
+    // SEED: the lanes holding a boundary column copy it (rows jb .. je-1)
+    const bool bx = c == 0 || c == W - 1, by = c + 1 == 0 || c + 1 == W - 1;
+    const int jb = 1 + blockIdx.y * rpb;
+    const int je = min(jb + rpb, H - 1);
+    const long long Wl = W;
+    double acc = 0.0;
+    double2 w0 = ld_pair(X + (long long)(jb - 1) * Wl, c, W);
+    double2 w1 = ld_pair(X + (long long)jb * Wl, c, W);
+    if (SEED && jb == 1) st_owned<false>(O + c, w0, ox, oy);
+    for (int j = jb; j < je; j += U) {
+        double2 xn[U], fv[U];
+        #pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long long r = min(j + u, je - 1);
+            fv[u] = ld_pair(F + r * Wl, c, W);
+            xn[u] = ld_pair(X + (r + 1) * Wl, c, W);
+        }
+        #pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = j + u;
+            const double2 up = (u == 0) ? w0 : (u == 1 ? w1 : xn[u - 2]);
+            const double2 ce = (u == 0) ? w1 : xn[u - 1];
+            const double2 dn = xn[u];
+            const double left = dpp_shr(ce.y);
+            const double right = dpp_shl(ce.x);
+            double2 o;
+            o.x = 0.25 * ((hh * fv[u].x) + left + ce.y + up.x + dn.x);
+            o.y = 0.25 * ((hh * fv[u].y) + ce.x + right + up.y + dn.y);
+            const bool live = r < je;
+            if (CHECK && live) {
+                const double r0 = fv[u].x - ih * (4 * ce.x - left - ce.y - up.x - dn.x);
+                const double r1 = fv[u].y - ih * (4 * ce.y - ce.x - right - up.y - dn.y);
+                if (ox) acc += r0 * r0;
+                if (oy) acc += r1 * r1;
+            }
+            if (live) {
+                double *q = O + (long long)r * Wl + c;
+                st_owned<NT>(q, o, ox, oy);
+                if (SEED) {
+                    if (bx) q[0] = ce.x;
+                    if (by) q[1] = ce.y;
+                }
+            }
+        }
+        w0 = xn[U - 2];
+        w1 = xn[U - 1];
+    }
+    if (SEED && je == H - 1) st_owned<false>(O + (long long)(H - 1) * Wl + c, w1, ox, oy);
+    if (CHECK) {
+        const double s = gblock_sum<kBlock>(acc, red);
+        if (threadIdx.x == 0) partials[blockIdx.y * gridDim.x + blockIdx.x] = s;
+    }
+}
+
+static OpGeom op_geom_ov(int W, int rows, int U, int target)
+{
+    // columns 1 .. W-2 over waves of 124, kBlock / 64 waves per workgroup
+    const int waves = (W - 2 + kOvStride - 1) / kOvStride;
+    return op_geom(waves * 64, rows, U, target);
+}
+
 constexpr int kOpTarget = 4096;   // workgroups per op launch (16 per CU)
+
+static bool op_ov() { return tuning_int("PGMG_OP_OV", 1) != 0; }
+static int op_u() { return tuning_int("PGMG_OP_U", 8) == 4 ? 4 : 8; }
+static int op_target() { return tuning_int("PGMG_OP_BLOCKS", kOpTarget); }
+
+static OpGeom sweep_geom(int H, int W)
+{
+    return op_ov() ? op_geom_ov(W, H - 2, op_u(), op_target())
+                   : op_geom((W - 1) / 2, H - 2, op_u(), op_target());
+}
 
 int g_blocks(int H, int W)
 {
-    const int U = tuning_int("PGMG_OP_U", 4) == 8 ? 8 : 4;
-    const OpGeom g = op_geom((W - 1) / 2, H - 2, U, tuning_int("PGMG_OP_BLOCKS", kOpTarget));
+    const OpGeom g = sweep_geom(H, W);
     return g.gx * g.gy;
 }
 
 template <int U, bool CHECK, bool SEED>
-static void sweep_u(const OpGeom &g, bool nt, const double *xin, const double *f, double *xout,
-                    double *partials, const unsigned *skip, unsigned *reset,
+static void sweep_u(const OpGeom &g, bool ov, bool nt, const double *xin, const double *f,
+                    double *xout, double *partials, const unsigned *skip, unsigned *reset,
                     unsigned long long *stats, double hh, double ih, int H, int W, hipStream_t s)
 {
     const dim3 grid(g.gx, g.gy);
-    if (nt)
-        k_op_sweep<U, CHECK, SEED, true><<<grid, kBlock, 0, s>>>(xin, f, xout, partials, skip, reset,
-                                                                stats, hh, ih, H, W, g.rpb);
-    else
-        k_op_sweep<U, CHECK, SEED, false><<<grid, kBlock, 0, s>>>(xin, f, xout, partials, skip,
-                                                                 reset, stats, hh, ih, H, W, g.rpb);
+#define PGMG_K(KN, NTV) KN<U, CHECK, SEED, NTV><<<grid, kBlock, 0, s>>>(xin, f, xout, partials, skip, reset, stats, hh, ih, H, W, g.rpb)
+    if (ov) {
+        if (nt) PGMG_K(k_op_sweep_ov, true);
+        else PGMG_K(k_op_sweep_ov, false);
+    } else {
+        if (nt) PGMG_K(k_op_sweep, true);
+        else PGMG_K(k_op_sweep, false);
+    }
+#undef PGMG_K
 }
 
 void launch_g_sweep(const double *xin, const double *f, double *xout, double *partials,
                     const unsigned *skip, unsigned *reset, unsigned long long *stats, double hh,
                     double inv_hh, int H, int W, bool seed, hipStream_t s)
 {
-    const int U = tuning_int("PGMG_OP_U", 4) == 8 ? 8 : 4;
-    const OpGeom g = op_geom((W - 1) / 2, H - 2, U, tuning_int("PGMG_OP_BLOCKS", kOpTarget));
-    const bool nt = tuning_int("PGMG_OP_NT", 0) != 0;
+    const OpGeom g = sweep_geom(H, W);
+    const bool ov = op_ov();
+    const bool nt = tuning_int("PGMG_OP_NT", 1) != 0;
     const bool chk = partials != nullptr;
 #define PGMG_SW(UU)                                                                                \
     do {                                                                                           \
-        if (chk && seed) sweep_u<UU, true, true>(g, nt, xin, f, xout, partials, skip, reset, stats, hh, inv_hh, H, W, s); \
-        else if (chk) sweep_u<UU, true, false>(g, nt, xin, f, xout, partials, skip, reset, stats, hh, inv_hh, H, W, s); \
-        else if (seed) sweep_u<UU, false, true>(g, nt, xin, f, xout, partials, skip, reset, stats, hh, inv_hh, H, W, s); \
-        else sweep_u<UU, false, false>(g, nt, xin, f, xout, partials, skip, reset, stats, hh, inv_hh, H, W, s); \
+        if (chk && seed) sweep_u<UU, true, true>(g, ov, nt, xin, f, xout, partials, skip, reset, stats, hh, inv_hh, H, W, s); \
+        else if (chk) sweep_u<UU, true, false>(g, ov, nt, xin, f, xout, partials, skip, reset, stats, hh, inv_hh, H, W, s); \
+        else if (seed) sweep_u<UU, false, true>(g, ov, nt, xin, f, xout, partials, skip, reset, stats, hh, inv_hh, H, W, s); \
+        else sweep_u<UU, false, false>(g, ov, nt, xin, f, xout, partials, skip, reset, stats, hh, inv_hh, H, W, s); \
     } while (0)
-    if (U == 8) PGMG_SW(8);
+    if (op_u() == 8) PGMG_SW(8);
     else PGMG_SW(4);
 #undef PGMG_SW
 }

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""A/B of the op-level Jacobi sweep's launch geometry (PGMG_OP_BLOCKS, PGMG_OP_U, PGMG_OP_NT)
+"""A/B of the op-level Jacobi sweep's launch geometry (PGMG_OP_OV, PGMG_OP_BLOCKS, PGMG_OP_U, PGMG_OP_NT)
 on the measurement build (PGMG_LIB=.../libpgmg_ab.so, `make ab`): ms per sweep of
 pgmg_jacobi(v = 100, no early exit) at N = 16385 on reference-layout arrays, variants
 interleaved over rounds, one JSON line per measurement.
@@ -35,10 +35,12 @@ pg.ops.rhs(f, h)
 tmp = torch.empty_like(x)
 byt = 24.0 * (n - 2) ** 2
 variants = []
-for blocks in (2048, 4096, 8192, 16384):
-    for u in (4, 8):
-        for nt in (0, 1):
-            variants.append({"PGMG_OP_BLOCKS": blocks, "PGMG_OP_U": u, "PGMG_OP_NT": nt})
+for ov in (0, 1):
+    for blocks in (1024, 2048, 4096, 8192):
+        for u in (4, 8):
+            for nt in (0, 1):
+                variants.append({"PGMG_OP_OV": ov, "PGMG_OP_BLOCKS": blocks, "PGMG_OP_U": u,
+                                 "PGMG_OP_NT": nt})
 for rnd in range(args.rounds):
     for var in variants:
         for k, v in var.items():
