@@ -1501,9 +1501,12 @@ static void spec_need_level(pgmg_ctx *c, int l, int gamma, long long *dbl, long 
     *nchk = 0;
     if (l >= c->nb) return;
     const Level &L = c->lv[l];
-    const int np = fused_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2);
+    // the small levels' tile passes (pgmg_coarse.hip) may write more partials than the
+    // row-marching passes: reserve for the larger
+    const int nt = coarse_tile_blocks(L.N);
+    const int np = std::max(fused_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2), nt);
     const PostRows pr = post_rows(c, l);
-    const int npo = fused_blocks(L.N, pr.jc0, pr.jc1);
+    const int npo = std::max(fused_blocks(L.N, pr.jc0, pr.jc1), nt);
     long long d, k;
     spec_need_level(c, l + 1, gamma, &d, &k);
     *dbl = (long long)np + npo + gamma * d;

@@ -35,12 +35,13 @@ pg.ops.rhs(f, h)
 tmp = torch.empty_like(x)
 byt = 24.0 * (n - 2) ** 2
 variants = []
-for ov in (0, 1):
-    for blocks in (1024, 2048, 4096, 8192):
-        for u in (4, 8):
-            for nt in (0, 1):
-                variants.append({"PGMG_OP_OV": ov, "PGMG_OP_BLOCKS": blocks, "PGMG_OP_U": u,
-                                 "PGMG_OP_NT": nt})
+# one round of resident workgroups: k_op_sweep U=8 4 waves/SIMD (1024 WGs), U=4 7 (1792);
+# k_op_sweep_ov U=8 5 (1280), U=4 8 (2048)
+for ov, u, blocks in ((0, 8, 1024), (0, 8, 2048), (0, 4, 1792), (1, 8, 1280), (1, 8, 2560),
+                      (1, 4, 2048), (1, 4, 4096), (1, 8, 8192)):
+    for nt in (0, 1):
+        variants.append({"PGMG_OP_OV": ov, "PGMG_OP_BLOCKS": blocks, "PGMG_OP_U": u,
+                         "PGMG_OP_NT": nt})
 for rnd in range(args.rounds):
     for var in variants:
         for k, v in var.items():

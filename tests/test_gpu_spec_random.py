@@ -13,7 +13,10 @@ the dimensions where a rollback or a prediction bug would hide:
     boundary;
   * 1 .. 6 calls of V, W or F cycles summing to 1 .. 40 cycles, spec_segment in {0, 2, 3, 5};
 and every case is compared with the oracle (oracle/pgmg_oracle.c, pinned to the compiled
-reference): phi bitwise, sweep and early-exit counts equal.  A failure names its case index;
+reference) -- phi bitwise, sweep counts equal -- and with the same calls decided in-stream
+(PGMG_FLAG_EXACT_DIST: no speculation) -- phi, sweep and early-exit counts equal.  (The
+oracle's exit count also books a check after a smoother's LAST sweep, which decides nothing;
+the library books the exits that stop a smoother early.)  A failure names its case index;
 re-run that index alone (-k) to reproduce it."""
 import numpy as np
 import pytest
@@ -88,17 +91,21 @@ def test_speculative_calls_random(pgmg, oracle_mod, c):
                 o.w_cycle(want, f)
             else:
                 o.f_cycle_outer(want)
-    with pgmg.Solver(c["N"], eps=c["eps"], cross_min_n=33, tail_n=c["tail_n"],
-                     spec_segment=c["spec_segment"]) as s:
-        s.set_problem(phi0, f)
-        for kind, n in c["calls"]:
-            {"V": s.vcycle, "W": s.wcycle, "F": s.fcycle}[kind](n)
-        got = s.solution()
-        sweeps, exits = s.stats()
-        spec, rollbacks = s.dist_info()
+    runs = []
+    for flags in (0, pgmg.PGMG_FLAG_EXACT_DIST):
+        with pgmg.Solver(c["N"], eps=c["eps"], cross_min_n=33, tail_n=c["tail_n"],
+                         spec_segment=c["spec_segment"], flags=flags) as s:
+            s.set_problem(phi0, f)
+            for kind, n in c["calls"]:
+                {"V": s.vcycle, "W": s.wcycle, "F": s.fcycle}[kind](n)
+            runs.append((s.solution(), s.stats(), s.dist_info()))
+    (got, (sweeps, exits), (spec, _)), (exact, st_exact, (spec_x, _)) = runs
+    # the first context speculated (when it has a bulk level above the tail), the second not
+    assert spec == (c["N"] > c["tail_n"]) and not spec_x
     assert_bitwise(got, want, f"case {c['idx']}: {c}")
-    assert (sweeps, exits) == (o.sweeps, o.early_exits), (c, (sweeps, exits), (o.sweeps, o.early_exits))
-    assert spec   # the context speculated (cross-cycle fused finest level)
+    assert_bitwise(exact, want, f"case {c['idx']} in-stream")
+    assert sweeps == o.sweeps, (c, sweeps, o.sweeps)
+    assert (sweeps, exits) == st_exact, (c, (sweeps, exits), st_exact)
 
 
 def test_random_cases_cover_the_space():
