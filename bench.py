@@ -201,15 +201,22 @@ def op_cases(pg, n):
     r = torch.zeros_like(x)
     c = torch.zeros((nc, nc), dtype=torch.float64, device=dev)
     e = torch.ones((nc, nc), dtype=torch.float64, device=dev)
-    def sweep(check):   # the sweep kernels' trace keys: k_op_sweep[_ov]<U,CHECK,SEED,NT>
-        return lambda k: k.startswith("k_op_sweep") and k.split("<")[1].split(",")[1] == (
-            "true" if check else "false")
+    def sweep(check, pair=None):   # trace keys: k_op_sweep[_ov]<U,CHECK,SEED,NT>, k_op_sweep2<U,SEED,NT>
+        def m(k):
+            if k.startswith("k_op_sweep2<"):
+                return not check and pair is not False
+            return (k.startswith("k_op_sweep") and pair is not True and
+                    k.split("<")[1].split(",")[1] == ("true" if check else "false"))
+        return m
 
     def named(prefix):
         return lambda k: k.startswith(prefix)
 
     cases = [
-        ("jacobi v=1 (2 sweeps, no early exit: Parallel::ComputeJacobi's call in the V-cycle)",
+        ("jacobi v=0 (one sweep: the single-sweep kernel k_op_sweep_ov, + the interior copy back)",
+         lambda: pg.ops.jacobi(x, f, h, 0, eps=-1.0, tmp=tmp), 24 * fine, sweep(False, False), 1),
+        ("jacobi v=1 (2 sweeps, no early exit: Parallel::ComputeJacobi's call in the V-cycle; "
+         "one paired pass k_op_sweep2 + the interior copy back)",
          lambda: pg.ops.jacobi(x, f, h, 1, eps=-1.0, tmp=tmp), 2 * 24 * fine, sweep(False), 2),
         ("jacobi v=100 (101 sweeps, no early exit: the per-op study's ComputeJacobi call)",
          lambda: pg.ops.jacobi(x, f, h, 100, eps=-1.0, tmp=tmp), 101 * 24 * fine, sweep(False),
@@ -258,11 +265,14 @@ def op_study(pg, n, trace, reps=5):
             per = nbytes / sweeps
             row["ms_per_sweep"] = round(ms / sweeps, 5)
             if trace is not None:
+                # the trace pass ran each case 3 times; a k_op_sweep2 launch is two sweeps
                 tk = [(k, v) for k, v in trace.items() if keys(k)]
                 if tk:
-                    calls = sum(v[0] for _, v in tk)
-                    avg = sum(v[0] * v[1] for _, v in tk) / calls
-                    row.update({"kernel_rocprof": [k for k, _ in tk],
+                    tot = sum(v[0] * v[1] for _, v in tk)
+                    nsw = sum(v[0] * (2 if k.startswith("k_op_sweep2") else 1) for k, v in tk)
+                    avg = tot / nsw
+                    row.update({"kernel_rocprof": {k: {"launches": v[0], "ms_per_launch": round(v[1], 5)}
+                                                   for k, v in tk},
                                 "ms_per_sweep_rocprof": round(avg, 5),
                                 "frac_sweep_rocprof": round(per / (avg * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)})
         elif trace is not None and [k for k in trace if keys(k)]:

@@ -272,11 +272,132 @@ static OpGeom op_geom_ov(int W, int rows, int U, int target)
     return op_geom(waves * 64, rows, U, target);
 }
 
+// ---------------------------------------------------------------------------
+// Two Jacobi sweeps in one pass, for a smoother call without early-exit checks (the
+// reference GPU op ComputeJacobi decides nothing between its v+1 sweeps,
+// Parallel_Method.cu:144-160): x and f are read once for two sweeps -- 24 B per point per
+// pass instead of 48 (temporal blocking; SURVEY §8(d) counts 24 B per sweep).  Rows march
+// down the band with the first sweep one row behind the loads and the second two rows
+// behind, in registers; wave tiles load 128 columns and own the 120 of lanes 2..61 (two
+// stencil levels shrink the valid columns by one per side each).  Every value is the
+// single sweep's: J(x) on interior points, x's boundary passed through (the reference never
+// writes it).
+// ---------------------------------------------------------------------------
+constexpr int kOv2Stride = 120;
+
+template <int U, bool SEED, bool NT>
+__global__ __launch_bounds__(kBlock) void k_op_sweep2(const double *__restrict__ X,
+                                                      const double *__restrict__ F,
+                                                      double *__restrict__ O,
+                                                      unsigned long long *stats, double hh, int H,
+                                                      int W, int rpb)
+{
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && stats != nullptr)
+        atomicAdd(&stats[0], 2ull);
+    const int lane = threadIdx.x & 63;
+    const int wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int c = kOv2Stride * wave - 3 + 2 * lane;
+    const bool inx = c >= 1 && c <= W - 2, iny = c + 1 >= 1 && c + 1 <= W - 2;
+    const bool mid = lane >= 2 && lane <= 61;
+    const bool ox = mid && inx, oy = mid && iny;
+    // SEED: lanes holding a boundary column write it (the passthrough value)
+    const bool bx = SEED && (c == 0 || c == W - 1), by = SEED && (c + 1 == 0 || c + 1 == W - 1);
+    const int jb = 1 + blockIdx.y * rpb;
+    const int je = min(jb + rpb, H - 1);   // x2 rows [jb, je)
+    const long long Wl = W;
+    auto ldrow = [&](const double *A, int r) {
+        return (r >= 0 && r <= H - 1) ? ld_pair(A + (long long)r * Wl, c, W) : make_double2(0.0, 0.0);
+    };
+    // one sweep of a row with x's boundary columns passed through
+    auto jrow = [&](double2 up, double2 ce, double2 dn, double2 f) {
+        const double l = dpp_shr(ce.y);
+        const double r = dpp_shl(ce.x);
+        double2 o;
+        o.x = inx ? 0.25 * ((hh * f.x) + l + ce.y + up.x + dn.x) : ce.x;
+        o.y = iny ? 0.25 * ((hh * f.y) + ce.x + r + up.y + dn.y) : ce.y;
+        return o;
+    };
+    // windows at "new row i": x rows i-2, i-1; f rows i-2, i-1; x1 rows i-3, i-2
+    double2 xa = ldrow(X, jb - 2), xb = ldrow(X, jb - 1);
+    double2 fa = make_double2(0.0, 0.0), fb = ldrow(F, jb - 1);
+    double2 ya = make_double2(0.0, 0.0), yb = make_double2(0.0, 0.0);
+    if (SEED && jb == 1) st_owned<false>(O + c, xb, ox || bx, oy || by);   // row 0
+    const int iend = je + 2;   // new rows i = jb .. je+1
+    for (int i = jb; i < iend; i += U) {
+        double2 xn[U], fn[U];
+        #pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = min(i + u, iend - 1);
+            xn[u] = ldrow(X, r);
+            fn[u] = ldrow(F, r);
+        }
+        #pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int ii = i + u;
+            if (ii >= iend) break;
+            // x1 on row ii-1 (a boundary row passes x through)
+            const int r1 = ii - 1;
+            double2 y1 = jrow(xa, xb, xn[u], fb);
+            if (r1 < 1 || r1 > H - 2) y1 = xb;
+            // x2 on row ii-2
+            const int r2 = ii - 2;
+            if (r2 >= jb) {
+                const double2 z = jrow(ya, yb, y1, fa);
+                double *q = O + (long long)r2 * Wl + c;
+                st_owned<NT>(q, z, ox, oy);
+                if (SEED) {
+                    if (bx) q[0] = z.x;
+                    if (by) q[1] = z.y;
+                }
+            }
+            xa = xb;
+            xb = xn[u];
+            fa = fb;
+            fb = fn[u];
+            ya = yb;
+            yb = y1;
+        }
+    }
+    // row H-1: after the last step xa holds x row je
+    if (SEED && je == H - 1) st_owned<false>(O + (long long)(H - 1) * Wl + c, xa, ox || bx, oy || by);
+}
+
+static OpGeom sweep2_geom(int H, int W, int U, int target)
+{
+    const int waves = (W - 2 + kOv2Stride - 1) / kOv2Stride;
+    return op_geom(waves * 64, H - 2, U, target);
+}
+
+void launch_g_sweep2(const double *xin, const double *f, double *xout, unsigned long long *stats,
+                     double hh, int H, int W, bool seed, hipStream_t s)
+{
+    const int U = tuning_int("PGMG_OP2_U", 4) == 8 ? 8 : 4;
+    const OpGeom g = sweep2_geom(H, W, U, tuning_int("PGMG_OP2_BLOCKS", 2048));
+    const bool nt = tuning_int("PGMG_OP_NT", 1) != 0;
+    const dim3 grid(g.gx, g.gy);
+#define PGMG_K2(UU, SD, NTV) k_op_sweep2<UU, SD, NTV><<<grid, kBlock, 0, s>>>(xin, f, xout, stats, hh, H, W, g.rpb)
+    if (U == 8) {
+        if (seed) { if (nt) PGMG_K2(8, true, true); else PGMG_K2(8, true, false); }
+        else { if (nt) PGMG_K2(8, false, true); else PGMG_K2(8, false, false); }
+    } else {
+        if (seed) { if (nt) PGMG_K2(4, true, true); else PGMG_K2(4, true, false); }
+        else { if (nt) PGMG_K2(4, false, true); else PGMG_K2(4, false, false); }
+    }
+#undef PGMG_K2
+}
+
+bool g_fuse2() { return tuning_int("PGMG_OP_FUSE2", 1) != 0; }
+
 constexpr int kOpTarget = 4096;   // workgroups per op launch (16 per CU)
 
-static bool op_ov() { return tuning_int("PGMG_OP_OV", 1) != 0; }
+// Measured at N = 16385 (scripts/op_ab.py, profiles/r04_ops/): one round of resident
+// workgroups (k_op_sweep<8>: 120 VGPRs, 4 waves per SIMD = 1024 workgroups of 4 waves on 256
+// CUs), 8 rows of loads in flight and non-temporal stores: 1.339 ms per sweep (0.60 of 8 TB/s)
+// against 1.35-1.47 for 2048-8192 workgroups, 4 rows, default stores or the overlapping
+// tiles (k_op_sweep_ov, kept as PGMG_OP_OV=1 of the measurement build)
+static bool op_ov() { return tuning_int("PGMG_OP_OV", 0) != 0; }
 static int op_u() { return tuning_int("PGMG_OP_U", 8) == 4 ? 4 : 8; }
-static int op_target() { return tuning_int("PGMG_OP_BLOCKS", kOpTarget); }
+static int op_target() { return tuning_int("PGMG_OP_BLOCKS", 1024); }
 
 static OpGeom sweep_geom(int H, int W)
 {
@@ -456,8 +577,8 @@ __global__ __launch_bounds__(kBlock) void k_op_residual(double *__restrict__ R,
             o.y = fv[u].y - ih * (4 * ce.y - ce.x - right - up.y - dn.y);
             if (act && j + u < je) {
                 double *q = R + (long long)(j + u) * Wl + c;
-                if (second) stvu<double>(q, o);
-                else q[0] = o.x;
+                if (second) st2<true>(q, o);
+                else st_nt1(q, o.x);
             }
         }
         w0 = xn[U - 2];
@@ -468,8 +589,9 @@ __global__ __launch_bounds__(kBlock) void k_op_residual(double *__restrict__ R,
 void launch_g_residual(double *r, const double *x, const double *f, double inv_hh, int H, int W,
                        hipStream_t s)
 {
-    const OpGeom g = op_geom((W - 1) / 2, H - 2, 4, tuning_int("PGMG_OP_BLOCKS", kOpTarget));
-    k_op_residual<4><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(r, x, f, inv_hh, H, W, g.rpb);
+    // the sweep's pattern (2 reads, 1 write): its geometry (one round, 8 rows in flight)
+    const OpGeom g = op_geom((W - 1) / 2, H - 2, 8, tuning_int("PGMG_OPR_BLOCKS", 1024));
+    k_op_residual<8><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(r, x, f, inv_hh, H, W, g.rpb);
 }
 
 // ---------------------------------------------------------------------------
@@ -534,7 +656,7 @@ __global__ __launch_bounds__(kBlock) void k_op_restrict(const double *__restrict
 
 void launch_g_restrict(const double *fine, double *coarse, int Nf, int Nc, hipStream_t s)
 {
-    const OpGeom g = op_geom(Nc - 2, Nc - 2, 4, tuning_int("PGMG_OP_BLOCKS", kOpTarget));
+    const OpGeom g = op_geom(Nc - 2, Nc - 2, 4, tuning_int("PGMG_OPRS_BLOCKS", kOpTarget));
     k_op_restrict<4><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(fine, coarse, Nf, Nc, g.rpb);
 }
 
@@ -642,7 +764,7 @@ void launch_g_prolong(const double *coarse, double *fine, int Nc, int Nf, int mo
                       hipStream_t s)
 {
     // one band = rpb coarse rows = 2 rpb fine rows
-    const OpGeom g = op_geom(Nc, (Nf + 1) / 2, 1, tuning_int("PGMG_OP_BLOCKS", kOpTarget));
+    const OpGeom g = op_geom(Nc, (Nf + 1) / 2, 1, tuning_int("PGMG_OPP_BLOCKS", kOpTarget));
     const dim3 grid(g.gx, g.gy);
     if (mode == 1) k_op_prolong<1><<<grid, kBlock, 0, s>>>(coarse, fine, Nc, Nf, ext, g.rpb);
     else k_op_prolong<0><<<grid, kBlock, 0, s>>>(coarse, fine, Nc, Nf, ext, g.rpb);

@@ -226,6 +226,10 @@ void launch_g_sweep(const double *xin, const double *f, double *xout, double *pa
 int g_blocks(int H, int W);
 constexpr int kOpPartialsCap = 65536;   // partial sums per op scratch set (>= g_blocks)
 void launch_g_copy_interior(const double *src, double *dst, int H, int W, hipStream_t s);
+// two sweeps without a check in one pass (stats[0] += 2); seed as launch_g_sweep
+void launch_g_sweep2(const double *xin, const double *f, double *xout, unsigned long long *stats,
+                     double hh, int H, int W, bool seed, hipStream_t s);
+bool g_fuse2();   // pgmg_jacobi without checks runs its sweeps in pairs (default)
 void launch_g_fixup(const double *partials, int np, double eps, const unsigned *done_prev,
                     unsigned *done_next, const double *src, double *dst,
                     unsigned long long *stats, int H, int W, hipStream_t s);

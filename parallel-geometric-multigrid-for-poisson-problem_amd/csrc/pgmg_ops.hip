@@ -93,6 +93,37 @@ int pgmg_jacobi(double *d_x, double *d_tmp, const double *d_f, int H, int W, dou
     // grid into its output buffer): the first sweep writes x's boundary into tmp besides the
     // interior, which is all a later sweep reads of it.  An odd sweep count ends in tmp and
     // copies its interior back (x's boundary is never written).
+    if (!check && g_fuse2()) {
+        // no checks (the reference GPU op's ComputeJacobi): sweeps in pairs, one pass each
+        // (k_op_sweep2), an odd count's single sweep first; passes alternate x -> tmp -> x
+        const double *cur = d_x;
+        double *other = tmp;
+        int left = S;
+        bool first = true;
+        while (left > 0) {
+            if (left & 1) {
+                launch_g_sweep(cur, d_f, other, nullptr, nullptr, first ? &D[1] : nullptr,
+                               g_op.stats, hh, ih, H, W, first, s);
+                left -= 1;
+            } else {
+                launch_g_sweep2(cur, d_f, other, g_op.stats, hh, H, W, first, s);
+                left -= 2;
+            }
+            first = false;
+            double *nc = const_cast<double *>(cur);
+            cur = other;
+            other = nc;
+        }
+        if (cur == tmp) launch_g_copy_interior(tmp, d_x, H, W, s);
+        HIPC(hipGetLastError());
+        if (sweeps_done) {
+            unsigned long long st[4];
+            HIPC(hipMemcpyAsync(st, g_op.stats, sizeof(st), hipMemcpyDeviceToHost, s));
+            HIPC(hipStreamSynchronize(s));
+            *sweeps_done = (int)st[0];
+        }
+        return PGMG_OK;
+    }
     for (int k = 1; k <= S; ++k) {
         const double *in = (k & 1) ? d_x : tmp;
         double *out = (k & 1) ? tmp : d_x;
