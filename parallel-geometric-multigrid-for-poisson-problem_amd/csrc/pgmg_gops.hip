@@ -42,12 +42,17 @@ __device__ __forceinline__ double gblock_sum(double v, double *red)
 }
 
 __device__ __forceinline__ void st_nt1(double *p, double v) { __builtin_nontemporal_store(v, p); }
+// a column pair's 16-byte store (8-byte alignment promised: one global_store_dwordx4 either
+// way; NT: non-temporal, the output is read again only a whole pass later)
+typedef double dpair_u __attribute__((ext_vector_type(2), aligned(8)));
 template <bool NT>
 __device__ __forceinline__ void st2(double *p, double2 v)
 {
     if (NT) {
-        __builtin_nontemporal_store(v.x, p);
-        __builtin_nontemporal_store(v.y, p + 1);
+        dpair_u w;
+        w.x = v.x;
+        w.y = v.y;
+        __builtin_nontemporal_store(w, reinterpret_cast<dpair_u *>(p));
     } else {
         stvu<double>(p, v);
     }
@@ -515,16 +520,16 @@ __global__ __launch_bounds__(kBlock) void k_op_copy_interior(const double *__res
         for (int u = 0; u < U; ++u) {
             if (j + u >= je) break;
             double *q = dst + (long long)(j + u) * Wl + c;
-            if (second) stvu<double>(q, v[u]);
-            else q[0] = v[u].x;
+            if (second) st2<true>(q, v[u]);
+            else st_nt1(q, v[u].x);
         }
     }
 }
 
 void launch_g_copy_interior(const double *src, double *dst, int H, int W, hipStream_t s)
 {
-    const OpGeom g = op_geom((W - 1) / 2, H - 2, 4, kOpTarget);
-    k_op_copy_interior<4><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(src, dst, H, W, g.rpb);
+    const OpGeom g = op_geom((W - 1) / 2, H - 2, 8, tuning_int("PGMG_OPC_BLOCKS", 2048));
+    k_op_copy_interior<8><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(src, dst, H, W, g.rpb);
 }
 
 // ---------------------------------------------------------------------------
