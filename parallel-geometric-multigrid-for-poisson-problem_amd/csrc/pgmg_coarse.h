@@ -17,13 +17,20 @@ struct CoarseArgsT {
     const unsigned *pre_fired;   // k_post: the pre check fired -> the iterate is x1, not x2
     T hh, ih;
     int N, P, Nc, Pc;
+    // mode 2 (the in-stream rare path): the check to decide -- the mode-0 pass's partials
+    const double *dec_partials;
+    int dec_np;
+    double eps;
 };
 
 // the tile passes apply to this level size (small, latency-bound levels)
 bool coarse_tile_ok(int N);
 // per-tile partial sums one tile pass writes (0 when !coarse_tile_ok)
 int coarse_tile_blocks(int N);
-template <class T> void launch_pre_tile(const CoarseArgsT<T> &a, hipStream_t s);
-template <class T> void launch_post_tile(const CoarseArgsT<T> &a, hipStream_t s);
+// mode 0: the pass (two sweeps + the check's partials); 1: the check predicted to fire (one
+// sweep, partials, the exit booked); 2: the in-stream rare path (decide the mode-0 pass's
+// check; if it fired, the one-sweep pass)
+template <class T> void launch_pre_tile(const CoarseArgsT<T> &a, int mode, hipStream_t s);
+template <class T> void launch_post_tile(const CoarseArgsT<T> &a, int mode, hipStream_t s);
 
 }  // namespace pgmg

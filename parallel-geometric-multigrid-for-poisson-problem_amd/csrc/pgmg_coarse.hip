@@ -45,18 +45,48 @@ __device__ __forceinline__ double ctile_block_sum(double v, double *red)
     return s;
 }
 
+// Early-exit decision of an in-stream check (MODE 2): every workgroup re-reduces the
+// check's partials in the same order (pgmg_fused.hip rare_decide's semantics); workgroup
+// (0,0) books the exit (one sweep less, one exit more) when it fired.
+__device__ __forceinline__ bool ctile_decide(const double *partials, int np, double eps,
+                                             unsigned long long *stats, double *red, int *trig)
+{
+    double v = 0.0;
+    for (int k = threadIdx.x; k < np; k += kCT) v += partials[k];
+    v = ctile_block_sum(v, red);
+    if (threadIdx.x == 0) *trig = (sqrt(v) < eps) ? 1 : 0;
+    __syncthreads();
+    const bool t = *trig != 0;
+    if (t && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && stats != nullptr) {
+        atomicAdd(&stats[0], (unsigned long long)-1LL);
+        atomicAdd(&stats[1], 1ull);
+    }
+    return t;
+}
+
+// MODE 0: the pass (two sweeps, the check's partials).  MODE 1: the check predicted to fire
+// (k_pre1 / k_post1): one sweep is the result, the check's partials written, one sweep and one
+// exit booked.  MODE 2: the in-stream rare path (k_pre_rare / k_post_rare): decide the check
+// from the MODE 0 pass's partials; when it fired, redo the pass with one sweep.
 // ---------------------------------------------------------------------------
 // pre: coarse tile rows [jca, jcb) x columns [ica, icb) of rc; window of fine points
-// (2 jca - 3 + i, 2 ica - 3 + j), i, j in [0, W): rc at (jc, ic) needs r(x2) at fine points
+// (2 jca - 3 + i, 2 ica - 3 + j), i, j in [0, W): rc at (jc, ic) needs r at fine points
 // 2jc-1 .. 2jc+1, r(x2) needs x2 one further, x2 needs x1 one further (x1 = J(0) pointwise)
 // ---------------------------------------------------------------------------
-template <class T, int TC>
+template <class T, int TC, int MODE>
 __global__ __launch_bounds__(kCT) void k_pre_tile(CoarseArgsT<T> a)
 {
     constexpr int W = 2 * TC + 5;
     constexpr int W2 = W - 2, W4 = W - 4;
     __shared__ T sF[W * W], sX1[W * W], sX2[W2 * W2], sR[W4 * W4];
     __shared__ double red[kCT / 64];
+    __shared__ int trig;
+    const bool lead = blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
+    if constexpr (MODE == 2) {
+        const bool t = ctile_decide(a.dec_partials, a.dec_np, a.eps, a.stats, red, &trig);
+        if (lead && a.fired != nullptr) *a.fired = t ? 1u : 0u;
+        if (!t) return;
+    }
     const int N = a.N, Nc = a.Nc;
     const long long P = a.P, Pc = a.Pc;
     const T hh = a.hh, ih = a.ih;
@@ -66,9 +96,17 @@ __global__ __launch_bounds__(kCT) void k_pre_tile(CoarseArgsT<T> a)
     // the check's fine points owned by this tile: a partition of the interior
     const int oy0 = 2 * jca - 1, oy1 = jcb == Nc - 1 ? N - 1 : 2 * jcb - 1;
     const int ox0 = 2 * ica - 1, ox1 = icb == Nc - 1 ? N - 1 : 2 * icb - 1;
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
-        if (a.stats != nullptr) atomicAdd(&a.stats[0], 2ull);
-        if (a.fired != nullptr) *a.fired = 0u;   // the pre check's outcome for k_post RECOMP
+    if (lead) {
+        if (MODE == 0) {
+            if (a.stats != nullptr) atomicAdd(&a.stats[0], 2ull);
+            if (a.fired != nullptr) *a.fired = 0u;   // the pre check's outcome for k_post RECOMP
+        } else if (MODE == 1) {
+            if (a.fired != nullptr) *a.fired = 1u;
+            if (a.stats != nullptr) {
+                atomicAdd(&a.stats[0], 1ull);
+                atomicAdd(&a.stats[1], 1ull);
+            }
+        }
     }
     // x1 = J(0) = 0.25 * ((hh*f) + 0) on the interior, 0 on and outside the boundary
     for (int q = threadIdx.x; q < W * W; q += kCT) {
@@ -80,7 +118,8 @@ __global__ __launch_bounds__(kCT) void k_pre_tile(CoarseArgsT<T> a)
         sX1[q] = in ? T(0.25) * ((hh * fv) + T(0)) : T(0);
     }
     __syncthreads();
-    // x2 = J(x1); the check's r(x1) on the owned points
+    // x2 = J(x1) (MODE 0) or r(x1) (one sweep: the residual the restriction reads); the
+    // check's r(x1) on the owned points
     double acc = 0.0;
     for (int q = threadIdx.x; q < W2 * W2; q += kCT) {
         const int i = 1 + q / W2, j = 1 + (q - (q / W2) * W2);
@@ -89,34 +128,41 @@ __global__ __launch_bounds__(kCT) void k_pre_tile(CoarseArgsT<T> a)
         const int k = i * W + j;
         const T c = sX1[k], l = sX1[k - 1], r = sX1[k + 1], u = sX1[k - W], d = sX1[k + W];
         const T fv = sF[k];
-        sX2[q] = in ? T(0.25) * ((hh * fv) + l + r + u + d) : c;
-        if (in && y >= oy0 && y < oy1 && x >= ox0 && x < ox1) {
-            const T r1 = fv - ih * (T(4) * c - l - r - u - d);
-            acc = csq(acc, r1);
+        const T r1 = fv - ih * (T(4) * c - l - r - u - d);
+        if (MODE == 0) sX2[q] = in ? T(0.25) * ((hh * fv) + l + r + u + d) : c;
+        else sX2[q] = r1;
+        if (MODE != 2 && in && y >= oy0 && y < oy1 && x >= ox0 && x < ox1) acc = csq(acc, r1);
+    }
+    __syncthreads();
+    if (MODE == 0) {
+        // r(x2) on the window's inner points (only interior points feed rc)
+        for (int q = threadIdx.x; q < W4 * W4; q += kCT) {
+            const int i = 2 + q / W4, j = 2 + (q - (q / W4) * W4);
+            const int k = (i - 1) * W2 + (j - 1);
+            const T c = sX2[k], l = sX2[k - 1], r = sX2[k + 1], u = sX2[k - W2], d = sX2[k + W2];
+            sR[q] = sF[i * W + j] - ih * (T(4) * c - l - r - u - d);
         }
+        __syncthreads();
     }
-    __syncthreads();
-    // r(x2) on the window's inner points (garbage-free: only interior points feed rc)
-    for (int q = threadIdx.x; q < W4 * W4; q += kCT) {
-        const int i = 2 + q / W4, j = 2 + (q - (q / W4) * W4);
-        const int k = (i - 1) * W2 + (j - 1);
-        const T c = sX2[k], l = sX2[k - 1], r = sX2[k + 1], u = sX2[k - W2], d = sX2[k + W2];
-        sR[q] = sF[i * W + j] - ih * (T(4) * c - l - r - u - d);
-    }
-    __syncthreads();
     // full-weighting restriction, MultiGrid.hpp:199-202: centre fine point (2jc, 2ic) is window
-    // point (2 (jc - jca) + 3, 2 (ic - ica) + 3), sR point (2 (jc - jca) + 1, 2 (ic - ica) + 1)
+    // point (2 (jc - jca) + 3, 2 (ic - ica) + 3): sR point (2 (jc - jca) + 1, ..), sX2 point
+    // (2 (jc - jca) + 2, ..)
+    const T *R = MODE == 0 ? sR : sX2;
+    constexpr int RW = MODE == 0 ? W4 : W2;
+    constexpr int RO = MODE == 0 ? 1 : 2;
     for (int q = threadIdx.x; q < TC * TC; q += kCT) {
         const int jc = jca + q / TC, ic = ica + (q - (q / TC) * TC);
         if (jc < jcb && ic < icb) {
-            const int k = (2 * (jc - jca) + 1) * W4 + 2 * (ic - ica) + 1;
-            const T v = T(0.25) * sR[k] + T(0.125) * (sR[k + 1] + sR[k - 1] + sR[k + W4] + sR[k - W4]) +
-                        T(0.0625) * (sR[k - W4 - 1] + sR[k - W4 + 1] + sR[k + W4 - 1] + sR[k + W4 + 1]);
+            const int k = (2 * (jc - jca) + RO) * RW + 2 * (ic - ica) + RO;
+            const T v = T(0.25) * R[k] + T(0.125) * (R[k + 1] + R[k - 1] + R[k + RW] + R[k - RW]) +
+                        T(0.0625) * (R[k - RW - 1] + R[k - RW + 1] + R[k + RW - 1] + R[k + RW + 1]);
             a.rc[jc * Pc + ic] = v;
         }
     }
-    const double s = ctile_block_sum(acc, red);
-    if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = s;
+    if (MODE != 2) {
+        const double s = ctile_block_sum(acc, red);
+        if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = s;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -124,9 +170,9 @@ __global__ __launch_bounds__(kCT) void k_pre_tile(CoarseArgsT<T> a)
 // fine rows 2jc-1, 2jc (the last tile down to N-2; the first / last tile column also writes
 // boundary column 0 / N-1, as k_post does); window (2 jca - 4 + i, 2 ica - 4 + j)
 //   g1 = J(0) -> ph = J(g1) (or g1 if the pre check fired) -> xe = ph + P ec -> x1 = J(xe)
-//   -> x2 = J(x1), the check r(x1) on the owned interior points
+//   -> x2 = J(x1) (one sweep: x1 is the result), the check r(x1) on the owned interior points
 // ---------------------------------------------------------------------------
-template <class T, int TC>
+template <class T, int TC, int MODE>
 __global__ __launch_bounds__(kCT) void k_post_tile(CoarseArgsT<T> a)
 {
     constexpr int W = 2 * TC + 8;
@@ -134,6 +180,11 @@ __global__ __launch_bounds__(kCT) void k_post_tile(CoarseArgsT<T> a)
     constexpr int CW = TC + 6;   // coarse rows jca-2 .. jca+TC+3 (xe's prolongation reads)
     __shared__ T sF[W * W], sG[W * W], sXE[W2 * W2], sX1[W4 * W4], sC[CW * CW];
     __shared__ double red[kCT / 64];
+    __shared__ int trig;
+    const bool lead = blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
+    if constexpr (MODE == 2) {
+        if (!ctile_decide(a.dec_partials, a.dec_np, a.eps, a.stats, red, &trig)) return;
+    }
     const int N = a.N, Nc = a.Nc;
     const long long P = a.P, Pc = a.Pc;
     const T hh = a.hh, ih = a.ih;
@@ -143,8 +194,13 @@ __global__ __launch_bounds__(kCT) void k_post_tile(CoarseArgsT<T> a)
     const int cy0 = jca - 2, cx0 = ica - 2;
     const int ya = 2 * jca - 1, yb = jcb == Nc - 1 ? N - 1 : 2 * jcb - 1;
     const int xa = ica == 1 ? 0 : 2 * ica - 1, xb = icb == Nc - 1 ? N : 2 * icb - 1;
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
-        atomicAdd(&a.stats[0], 2ull);
+    if (lead && a.stats != nullptr) {
+        if (MODE == 0) atomicAdd(&a.stats[0], 2ull);
+        if (MODE == 1) {
+            atomicAdd(&a.stats[0], 1ull);
+            atomicAdd(&a.stats[1], 1ull);
+        }
+    }
     const bool pfired = *a.pre_fired != 0u;
     for (int q = threadIdx.x; q < W * W; q += kCT) {
         const int i = q / W, j = q - (q / W) * W;
@@ -190,7 +246,8 @@ __global__ __launch_bounds__(kCT) void k_post_tile(CoarseArgsT<T> a)
         sX1[q] = in ? T(0.25) * ((hh * sF[i * W + j]) + sXE[k - 1] + sXE[k + 1] + sXE[k - W2] + sXE[k + W2]) : c;
     }
     __syncthreads();
-    // x2 = J(x1) on the owned points, written; the check's r(x1) on the owned interior
+    // x2 = J(x1) (x1 itself with one sweep) on the owned points, written; the check's r(x1)
+    // on the owned interior
     double acc = 0.0;
     const int wc = xb - xa, npts = (yb - ya) * wc;
     for (int q = threadIdx.x; q < npts; q += kCT) {
@@ -200,14 +257,18 @@ __global__ __launch_bounds__(kCT) void k_post_tile(CoarseArgsT<T> a)
             const int k = (y - y0 - 2) * W4 + (x - x0 - 2);
             const T c = sX1[k], l = sX1[k - 1], r = sX1[k + 1], u = sX1[k - W4], d = sX1[k + W4];
             const T fv = sF[(y - y0) * W + (x - x0)];
-            const T r1 = fv - ih * (T(4) * c - l - r - u - d);
-            acc = csq(acc, r1);
-            out = T(0.25) * ((hh * fv) + l + r + u + d);
+            if (MODE != 2) {
+                const T r1 = fv - ih * (T(4) * c - l - r - u - d);
+                acc = csq(acc, r1);
+            }
+            out = MODE == 0 ? T(0.25) * ((hh * fv) + l + r + u + d) : c;
         }
         a.x2[y * P + x] = out;
     }
-    const double s = ctile_block_sum(acc, red);
-    if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = s;
+    if (MODE != 2) {
+        const double s = ctile_block_sum(acc, red);
+        if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = s;
+    }
 }
 
 static int ctile_tc(int N) { return tuning_int("PGMG_CTILE_TC", N >= 1025 ? 16 : 8) == 16 ? 16 : 8; }
@@ -226,26 +287,42 @@ int coarse_tile_blocks(int N)
 }
 
 template <class T>
-void launch_pre_tile(const CoarseArgsT<T> &a, hipStream_t s)
+void launch_pre_tile(const CoarseArgsT<T> &a, int mode, hipStream_t s)
 {
     const int tc = ctile_tc(a.N);
     const int nt = (a.Nc - 2 + tc - 1) / tc;
-    if (tc == 16) k_pre_tile<T, 16><<<dim3(nt, nt), kCT, 0, s>>>(a);
-    else k_pre_tile<T, 8><<<dim3(nt, nt), kCT, 0, s>>>(a);
+    const dim3 g(nt, nt);
+#define PGMG_PT(TCV)                                                                  \
+    do {                                                                              \
+        if (mode == 1) k_pre_tile<T, TCV, 1><<<g, kCT, 0, s>>>(a);                   \
+        else if (mode == 2) k_pre_tile<T, TCV, 2><<<g, kCT, 0, s>>>(a);              \
+        else k_pre_tile<T, TCV, 0><<<g, kCT, 0, s>>>(a);                             \
+    } while (0)
+    if (tc == 16) PGMG_PT(16);
+    else PGMG_PT(8);
+#undef PGMG_PT
 }
 
 template <class T>
-void launch_post_tile(const CoarseArgsT<T> &a, hipStream_t s)
+void launch_post_tile(const CoarseArgsT<T> &a, int mode, hipStream_t s)
 {
     const int tc = ctile_tc(a.N);
     const int nt = (a.Nc - 2 + tc - 1) / tc;
-    if (tc == 16) k_post_tile<T, 16><<<dim3(nt, nt), kCT, 0, s>>>(a);
-    else k_post_tile<T, 8><<<dim3(nt, nt), kCT, 0, s>>>(a);
+    const dim3 g(nt, nt);
+#define PGMG_PT(TCV)                                                                  \
+    do {                                                                              \
+        if (mode == 1) k_post_tile<T, TCV, 1><<<g, kCT, 0, s>>>(a);                  \
+        else if (mode == 2) k_post_tile<T, TCV, 2><<<g, kCT, 0, s>>>(a);             \
+        else k_post_tile<T, TCV, 0><<<g, kCT, 0, s>>>(a);                            \
+    } while (0)
+    if (tc == 16) PGMG_PT(16);
+    else PGMG_PT(8);
+#undef PGMG_PT
 }
 
-template void launch_pre_tile<double>(const CoarseArgsT<double> &, hipStream_t);
-template void launch_pre_tile<float>(const CoarseArgsT<float> &, hipStream_t);
-template void launch_post_tile<double>(const CoarseArgsT<double> &, hipStream_t);
-template void launch_post_tile<float>(const CoarseArgsT<float> &, hipStream_t);
+template void launch_pre_tile<double>(const CoarseArgsT<double> &, int, hipStream_t);
+template void launch_pre_tile<float>(const CoarseArgsT<float> &, int, hipStream_t);
+template void launch_post_tile<double>(const CoarseArgsT<double> &, int, hipStream_t);
+template void launch_post_tile<float>(const CoarseArgsT<float> &, int, hipStream_t);
 
 }  // namespace pgmg

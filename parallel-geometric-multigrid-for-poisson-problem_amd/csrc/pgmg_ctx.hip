@@ -446,10 +446,10 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     const int visit = c->cur_visit;   // (the children's visits move it)
     if (wm >= 0) mode = wm;
     if (mode == 1 && (dist || pin || (x0_zero && !recomp))) mode = 2;
-    // the small coarse levels (pgmg_coarse.hip): both passes as 2D LDS tiles, unless the
-    // checks are predicted to fire (the one-sweep passes k_pre1 / k_post1 stay row-marching);
-    // the checks' partial count is the tile count
-    const bool tile = recomp && !dist && !pin && mode != 1 && pa.gfx == nullptr &&
+    // the small coarse levels (pgmg_coarse.hip): both passes, their predicted-to-fire
+    // one-sweep forms and their in-stream rare paths as 2D LDS tiles; the checks' partial
+    // count is the tile count
+    const bool tile = recomp && !dist && !pin && pa.gfx == nullptr &&
                       !(c->cfg.flags & PGMG_FLAG_NO_CTILE) && coarse_tile_ok(L.N);
     CoarseArgsT<T> ca{};
     if (tile) {
@@ -473,7 +473,7 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     int ev = fine ? timed_begin(c, 1) : -1;
     if (tile) {
         ca.partials = pa.partials;
-        launch_pre_tile(ca, c->s);
+        launch_pre_tile(ca, mode == 1 ? 1 : 0, c->s);
         HIPC(hipGetLastError());
     } else if ((e = mode == 1 ? launch_pre1(pa, x0_zero, c->s) : launch_pre(pa, x0_zero, fine, c->s))) {
         return e;
@@ -481,8 +481,16 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     if ((e = timed_end(c, 1, ev))) return e;
     if (mode == 2) {
         if (lp) fa.partials = lp;
-        if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
-        if ((e = launch_pre_rare(fa, pa, x0_zero, c->s))) return e;
+        if (tile) {
+            ca.dec_partials = fa.partials;
+            ca.dec_np = fa.np;
+            ca.eps = fa.eps;
+            launch_pre_tile(ca, 2, c->s);
+            HIPC(hipGetLastError());
+        } else {
+            if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
+            if ((e = launch_pre_rare(fa, pa, x0_zero, c->s))) return e;
+        }
         fa.partials = c->partials;
     }
     if ((e = enqueue_children<T>(c, l, gamma))) return e;
@@ -525,7 +533,7 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     ev = fine ? timed_begin(c, 2) : -1;
     if (tile) {
         ca.partials = po.partials;
-        launch_post_tile(ca, c->s);
+        launch_post_tile(ca, mode == 1 ? 1 : 0, c->s);
         HIPC(hipGetLastError());
     } else if ((e = mode == 1 ? launch_post1(po, c->s) : launch_post(po, fine, c->s))) {
         return e;
@@ -533,9 +541,17 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     if ((e = timed_end(c, 2, ev))) return e;
     if (mode == 2) {
         if (lp) fa.partials = lp;
-        fa.global_sum = nullptr;
-        if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
-        if ((e = launch_post_rare(fa, po, c->s))) return e;
+        if (tile) {
+            ca.dec_partials = fa.partials;
+            ca.dec_np = fa.np;
+            ca.eps = fa.eps;
+            launch_post_tile(ca, 2, c->s);
+            HIPC(hipGetLastError());
+        } else {
+            fa.global_sum = nullptr;
+            if (dist && (e = global_sum(c, fa.np, &fa.global_sum))) return e;
+            if ((e = launch_post_rare(fa, po, c->s))) return e;
+        }
     }
     return PGMG_OK;
 }
