@@ -29,7 +29,10 @@ def child(a):
         steps = a.steps if kind == "V" else max(1, a.steps // 10)
         ts = []
         flags = int(os.environ.get("AB_FLAGS", "0"))   # pgmg_config.flags of the variant
-        with pg.Solver(n, **({"flags": flags} if flags else {})) as s:
+        kw = {"flags": flags} if flags else {}
+        if os.environ.get("AB_TAIL_N"):                # pgmg_config.tail_n of the variant
+            kw["tail_n"] = int(os.environ["AB_TAIL_N"])
+        with pg.Solver(n, **kw) as s:
             run = s.vcycle if kind == "V" else s.wcycle
             for _ in range(3):
                 s.set_problem()
