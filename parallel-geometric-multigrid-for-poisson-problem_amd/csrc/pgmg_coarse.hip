@@ -271,7 +271,10 @@ __global__ __launch_bounds__(kCT) void k_post_tile(CoarseArgsT<T> a)
     }
 }
 
-static int ctile_tc(int N) { return tuning_int("PGMG_CTILE_TC", N >= 1025 ? 16 : 8) == 16 ? 16 : 8; }
+// TC = 8 on every level (profiles/r04_ctile/ab_tc_maxn_tail.jsonl, 3 interleaved rounds): TC = 16
+// at 1025 (1024 workgroups of 51 KiB LDS, 3 resident per CU) ran its k_post_tile in 20 us
+// against 15 us row-marching; TC = 8 there is on par with the row-marching passes
+static int ctile_tc(int N) { return tuning_int("PGMG_CTILE_TC", 8) == 16 ? 16 : 8; }
 
 bool coarse_tile_ok(int N)
 {
