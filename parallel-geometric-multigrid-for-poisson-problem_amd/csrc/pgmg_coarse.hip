@@ -49,12 +49,13 @@ __device__ __forceinline__ double ctile_block_sum(double v, double *red)
 // check's partials in the same order (pgmg_fused.hip rare_decide's semantics); workgroup
 // (0,0) books the exit (one sweep less, one exit more) when it fired.
 __device__ __forceinline__ bool ctile_decide(const double *partials, int np, double eps,
+                                             const double *global_sum,
                                              unsigned long long *stats, double *red, int *trig)
 {
     double v = 0.0;
     for (int k = threadIdx.x; k < np; k += kCT) v += partials[k];
     v = ctile_block_sum(v, red);
-    if (threadIdx.x == 0) *trig = (sqrt(v) < eps) ? 1 : 0;
+    if (threadIdx.x == 0) *trig = (sqrt(global_sum != nullptr ? *global_sum : v) < eps) ? 1 : 0;
     __syncthreads();
     const bool t = *trig != 0;
     if (t && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && stats != nullptr) {
@@ -83,19 +84,24 @@ __global__ __launch_bounds__(kCT) void k_pre_tile(CoarseArgsT<T> a)
     __shared__ int trig;
     const bool lead = blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
     if constexpr (MODE == 2) {
-        const bool t = ctile_decide(a.dec_partials, a.dec_np, a.eps, a.stats, red, &trig);
+        const bool t = ctile_decide(a.dec_partials, a.dec_np, a.eps, a.global_sum, a.stats, red, &trig);
         if (lead && a.fired != nullptr) *a.fired = t ? 1u : 0u;
         if (!t) return;
     }
     const int N = a.N, Nc = a.Nc;
     const long long P = a.P, Pc = a.Pc;
     const T hh = a.hh, ih = a.ih;
-    const int jca = 1 + blockIdx.y * TC, jcb = min(jca + TC, Nc - 1);
+    const int jca = a.jt0 + blockIdx.y * TC, jcb = min(jca + TC, a.jt1);
     const int ica = 1 + blockIdx.x * TC, icb = min(ica + TC, Nc - 1);
     const int y0 = 2 * jca - 3, x0 = 2 * ica - 3;
-    // the check's fine points owned by this tile: a partition of the interior
-    const int oy0 = 2 * jca - 1, oy1 = jcb == Nc - 1 ? N - 1 : 2 * jcb - 1;
-    const int ox0 = 2 * ica - 1, ox1 = icb == Nc - 1 ? N - 1 : 2 * icb - 1;
+    // the check's fine points owned by this tile (a partition of the rank's interior rows):
+    // rows [2 jca, 2 jcb), the first tile from own_lo, the last up to own_hi; columns likewise
+    const int oy0 = blockIdx.y == 0 ? a.own_lo : 2 * jca;
+    const int oy1 = jcb == a.jt1 ? a.own_hi : 2 * jcb;
+    const int ox0 = ica == 1 ? 1 : 2 * ica, ox1 = icb == Nc - 1 ? N - 1 : 2 * icb;
+    // f rows read: x1 on [2 jca - 3, 2 jcb + 1] (a strip holds them: its halo; the window's
+    // rows past them are not loaded)
+    const int fy0 = max(1, 2 * jca - 3), fy1 = min(N - 2, 2 * jcb + 1);
     if (lead) {
         if (MODE == 0) {
             if (a.stats != nullptr) atomicAdd(&a.stats[0], 2ull);
@@ -113,7 +119,7 @@ __global__ __launch_bounds__(kCT) void k_pre_tile(CoarseArgsT<T> a)
         const int i = q / W, j = q - (q / W) * W;
         const int y = y0 + i, x = x0 + j;
         const bool in = y >= 1 && y <= N - 2 && x >= 1 && x <= N - 2;
-        const T fv = in ? a.f[y * P + x] : T(0);
+        const T fv = (in && y >= fy0 && y <= fy1) ? a.f[y * P + x] : T(0);
         sF[q] = fv;
         sX1[q] = in ? T(0.25) * ((hh * fv) + T(0)) : T(0);
     }
@@ -183,17 +189,24 @@ __global__ __launch_bounds__(kCT) void k_post_tile(CoarseArgsT<T> a)
     __shared__ int trig;
     const bool lead = blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
     if constexpr (MODE == 2) {
-        if (!ctile_decide(a.dec_partials, a.dec_np, a.eps, a.stats, red, &trig)) return;
+        if (!ctile_decide(a.dec_partials, a.dec_np, a.eps, a.global_sum, a.stats, red, &trig)) return;
     }
     const int N = a.N, Nc = a.Nc;
     const long long P = a.P, Pc = a.Pc;
     const T hh = a.hh, ih = a.ih;
-    const int jca = 1 + blockIdx.y * TC, jcb = min(jca + TC, Nc - 1);
+    const int jca = a.jt0 + blockIdx.y * TC, jcb = min(jca + TC, a.jt1);
     const int ica = 1 + blockIdx.x * TC, icb = min(ica + TC, Nc - 1);
     const int y0 = 2 * jca - 4, x0 = 2 * ica - 4;
     const int cy0 = jca - 2, cx0 = ica - 2;
-    const int ya = 2 * jca - 1, yb = jcb == Nc - 1 ? N - 1 : 2 * jcb - 1;
-    const int xa = ica == 1 ? 0 : 2 * ica - 1, xb = icb == Nc - 1 ? N : 2 * icb - 1;
+    // the fine points written by this tile: rows [2 jca, 2 jcb) (the first tile from own_lo, the
+    // last up to own_hi), columns [2 ica, 2 icb) (the first from the boundary column 0, the last
+    // up to N - 1)
+    const int ya = blockIdx.y == 0 ? a.own_lo : 2 * jca;
+    const int yb = jcb == a.jt1 ? a.own_hi : 2 * jcb;
+    const int xa = ica == 1 ? 0 : 2 * ica, xb = icb == Nc - 1 ? N : 2 * icb;
+    // rows read: f on [ya - 3, yb + 2], the correction's coarse rows of xe on [ya - 2, yb + 1]
+    const int fy0 = max(1, ya - 3), fy1 = min(N - 2, yb + 2);
+    const int cm0 = max(0, (ya - 2) >> 1), cm1 = min(Nc - 1, ((yb + 1) >> 1) + 1);
     if (lead && a.stats != nullptr) {
         if (MODE == 0) atomicAdd(&a.stats[0], 2ull);
         if (MODE == 1) {
@@ -206,13 +219,13 @@ __global__ __launch_bounds__(kCT) void k_post_tile(CoarseArgsT<T> a)
         const int i = q / W, j = q - (q / W) * W;
         const int y = y0 + i, x = x0 + j;
         const bool in = y >= 1 && y <= N - 2 && x >= 1 && x <= N - 2;
-        const T fv = in ? a.f[y * P + x] : T(0);
+        const T fv = (in && y >= fy0 && y <= fy1) ? a.f[y * P + x] : T(0);
         sF[q] = fv;
         sG[q] = in ? T(0.25) * ((hh * fv) + T(0)) : T(0);
     }
     for (int q = threadIdx.x; q < CW * CW; q += kCT) {
         const int m = cy0 + q / CW, n = cx0 + (q - (q / CW) * CW);
-        sC[q] = (m >= 0 && m <= Nc - 1 && n >= 0 && n <= Nc - 1) ? a.ec[m * Pc + n] : T(0);
+        sC[q] = (m >= cm0 && m <= cm1 && n >= 0 && n <= Nc - 1) ? a.ec[m * Pc + n] : T(0);
     }
     __syncthreads();
     // ph = J(g1) (or g1), then + P ec on rows / columns 2 .. N-2 (MultiGrid.hpp:208-226)
@@ -257,7 +270,7 @@ __global__ __launch_bounds__(kCT) void k_post_tile(CoarseArgsT<T> a)
             const int k = (y - y0 - 2) * W4 + (x - x0 - 2);
             const T c = sX1[k], l = sX1[k - 1], r = sX1[k + 1], u = sX1[k - W4], d = sX1[k + W4];
             const T fv = sF[(y - y0) * W + (x - x0)];
-            if (MODE != 2) {
+            if (MODE != 2 && y >= a.sum_lo && y < a.sum_hi) {
                 const T r1 = fv - ih * (T(4) * c - l - r - u - d);
                 acc = csq(acc, r1);
             }
@@ -276,25 +289,27 @@ __global__ __launch_bounds__(kCT) void k_post_tile(CoarseArgsT<T> a)
 // against 15 us row-marching; TC = 8 there is on par with the row-marching passes
 static int ctile_tc(int N) { return tuning_int("PGMG_CTILE_TC", 8) == 16 ? 16 : 8; }
 
-bool coarse_tile_ok(int N)
+bool coarse_tile_ok(int N, bool dist)
 {
-    return N >= 9 && N <= tuning_int("PGMG_CTILE_MAXN", 1025);
+    return N >= 9 && N <= (dist ? tuning_int("PGMG_CTILE_DIST_MAXN", 1025)
+                                : tuning_int("PGMG_CTILE_MAXN", 1025));
 }
 
-int coarse_tile_blocks(int N)
+int coarse_tile_blocks_rows(int N, int jt0, int jt1)
 {
-    if (!coarse_tile_ok(N)) return 0;
+    if (N < 9 || jt1 <= jt0) return 0;
     const int tc = ctile_tc(N);
-    const int nt = (N / 2 - 1 + tc - 1) / tc;   // interior coarse points (Nc - 2) per side
-    return nt * nt;
+    const int nx = (N / 2 - 1 + tc - 1) / tc;   // interior coarse columns (Nc - 2)
+    return nx * ((jt1 - jt0 + tc - 1) / tc);
 }
+
+int coarse_tile_blocks(int N) { return coarse_tile_blocks_rows(N, 1, N / 2); }
 
 template <class T>
 void launch_pre_tile(const CoarseArgsT<T> &a, int mode, hipStream_t s)
 {
     const int tc = ctile_tc(a.N);
-    const int nt = (a.Nc - 2 + tc - 1) / tc;
-    const dim3 g(nt, nt);
+    const dim3 g((a.Nc - 2 + tc - 1) / tc, (a.jt1 - a.jt0 + tc - 1) / tc);
 #define PGMG_PT(TCV)                                                                  \
     do {                                                                              \
         if (mode == 1) k_pre_tile<T, TCV, 1><<<g, kCT, 0, s>>>(a);                   \
@@ -310,8 +325,7 @@ template <class T>
 void launch_post_tile(const CoarseArgsT<T> &a, int mode, hipStream_t s)
 {
     const int tc = ctile_tc(a.N);
-    const int nt = (a.Nc - 2 + tc - 1) / tc;
-    const dim3 g(nt, nt);
+    const dim3 g((a.Nc - 2 + tc - 1) / tc, (a.jt1 - a.jt0 + tc - 1) / tc);
 #define PGMG_PT(TCV)                                                                  \
     do {                                                                              \
         if (mode == 1) k_post_tile<T, TCV, 1><<<g, kCT, 0, s>>>(a);                  \

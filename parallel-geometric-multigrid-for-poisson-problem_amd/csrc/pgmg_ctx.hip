@@ -249,6 +249,23 @@ static PostRows post_rows(const pgmg_ctx *c, int l)
     return r;
 }
 
+// partial sums a tile pass of bulk level l writes on this rank (0: no tile pass there);
+// pre: the rank's coarse rows, post: its k_post rows (post_rows)
+static int tile_np(const pgmg_ctx *c, int l, bool post)
+{
+    if (l < 1 || l >= c->nb) return 0;
+    const Level &L = c->lv[l];
+    if (!coarse_tile_ok(L.N, is_dist(c, l))) return 0;
+    const int Nc = c->lv[l + 1].N;
+    int jc0 = L.lo / 2, jc1 = (L.hi < L.N ? L.hi : L.N - 1) / 2;
+    if (post) {
+        const PostRows pr = post_rows(c, l);
+        jc0 = pr.jc0;
+        jc1 = pr.jc1;
+    }
+    return coarse_tile_blocks_rows(L.N, std::max(jc0, 1), std::min(jc1, Nc - 1));
+}
+
 template <class T> static int enqueue_children(pgmg_ctx *c, int l, int gamma);
 template <class T> static int enqueue_cycle_t(pgmg_ctx *c, int l, int gamma, bool x0_zero);
 
@@ -449,11 +466,17 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     // the small coarse levels (pgmg_coarse.hip): both passes, their predicted-to-fire
     // one-sweep forms and their in-stream rare paths as 2D LDS tiles; the checks' partial
     // count is the tile count
-    const bool tile = recomp && !dist && !pin && pa.gfx == nullptr &&
-                      !(c->cfg.flags & PGMG_FLAG_NO_CTILE) && coarse_tile_ok(L.N);
+    // (row strips too: the tiles cover the rank's coarse rows, its interior rows own the check)
+    const bool tile = recomp && !pin && pa.gfx == nullptr &&
+                      !(c->cfg.flags & PGMG_FLAG_NO_CTILE) && coarse_tile_ok(L.N, dist) &&
+                      pa.rc_hi > pa.rc_lo;
     CoarseArgsT<T> ca{};
     if (tile) {
-        fa.np = coarse_tile_blocks(L.N);
+        ca.jt0 = pa.rc_lo;
+        ca.jt1 = pa.rc_hi;
+        ca.own_lo = L.u0;
+        ca.own_hi = L.u1;
+        fa.np = coarse_tile_blocks_rows(L.N, ca.jt0, ca.jt1);
         ca.f = pa.f;
         ca.ec = G<T>(C.A);
         ca.rc = pa.rc;
@@ -482,6 +505,8 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     if (mode == 2) {
         if (lp) fa.partials = lp;
         if (tile) {
+            ca.global_sum = nullptr;
+            if (dist && (e = global_sum(c, fa.np, &ca.global_sum))) return e;
             ca.dec_partials = fa.partials;
             ca.dec_np = fa.np;
             ca.eps = fa.eps;
@@ -527,6 +552,15 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     }
     po.gfx = pa.gfx;
     po.gsy = pa.gsy;
+    if (tile) {   // k_post's rows: the strip plus kPostExt rows (dist), its own rows summed
+        ca.jt0 = std::max(po.jc0, 1);
+        ca.jt1 = std::min(po.jc1, C.N - 1);
+        ca.own_lo = po.row_lo;
+        ca.own_hi = po.row_hi;
+        ca.sum_lo = po.sum_hi > po.sum_lo ? po.sum_lo : po.row_lo;
+        ca.sum_hi = po.sum_hi > po.sum_lo ? po.sum_hi : po.row_hi;
+        fa.np = coarse_tile_blocks_rows(L.N, ca.jt0, ca.jt1);
+    }
     c->cur_visit = visit;
     lp = chk_log(c, fa.np, l, mode);
     if (lp) po.partials = lp;
@@ -542,6 +576,8 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     if (mode == 2) {
         if (lp) fa.partials = lp;
         if (tile) {
+            ca.global_sum = nullptr;
+            if (dist && (e = global_sum(c, fa.np, &ca.global_sum))) return e;
             ca.dec_partials = fa.partials;
             ca.dec_np = fa.np;
             ca.eps = fa.eps;
@@ -1049,7 +1085,7 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         if (nbk > maxblocks) maxblocks = nbk;
         nbk = postpre_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2);
         if (nbk > maxblocks) maxblocks = nbk;
-        nbk = coarse_tile_blocks(L.N);
+        nbk = std::max(tile_np(c, l, false), tile_np(c, l, true));
         if (nbk > maxblocks) maxblocks = nbk;
     }
     if (rc == PGMG_OK && c->cross) rc = alloc_grid(c->S, c->lv[0]);
@@ -1519,10 +1555,10 @@ static void spec_need_level(pgmg_ctx *c, int l, int gamma, long long *dbl, long 
     const Level &L = c->lv[l];
     // the small levels' tile passes (pgmg_coarse.hip) may write more partials than the
     // row-marching passes: reserve for the larger
-    const int nt = coarse_tile_blocks(L.N);
-    const int np = std::max(fused_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2), nt);
+    const int np = std::max(fused_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2),
+                            tile_np(c, l, false));
     const PostRows pr = post_rows(c, l);
-    const int npo = std::max(fused_blocks(L.N, pr.jc0, pr.jc1), nt);
+    const int npo = std::max(fused_blocks(L.N, pr.jc0, pr.jc1), tile_np(c, l, true));
     long long d, k;
     spec_need_level(c, l + 1, gamma, &d, &k);
     *dbl = (long long)np + npo + gamma * d;
