@@ -115,6 +115,9 @@ class ParallelTestRunner {
     // reference keeps them in managed memory: ParallelTestRunner.cu:162-163; the default here
     // is device memory, phi updated in place, f regenerated on the device)
     bool host_arrays = false;
+    // gpu_exec --mixed-dphi-hf / --mixed-hphi-df: phi on the device and f on the host, or the
+    // other way round (ParallelMultiGridSolver's mixed bindings; not the reference's layout)
+    int mixed = 0;
     int last_device_mode = -1;   // of the last cycle run: ParallelMultiGridSolver::device_mode
     int warmup_iterations = 0;   // gpu_exec --warmup: untimed cycles before the timed ones
     std::vector<double> err_vec;
@@ -192,7 +195,26 @@ class ParallelTestRunner {
         pgmg_host::exact_solution(x_true, N, h, pr);
         ParallelMultiGridSolver solver(alpha);
         double secs = 0.0;
-        if (host_arrays) {
+        if (mixed == 1 || mixed == 2) {
+            // 1: device phi (pgmg_alloc_grid), host f; 2: host phi, device f
+            pgmg_host::DeviceGrid dphi(N), df(N);
+            pgmg_host::rhs(f, N, h, pr);
+            if (mixed == 2) df.upload(f.data());
+            double *pp = mixed == 1 ? dphi.get() : phi.data();
+            double *fp = mixed == 1 ? f.data() : df.get();
+            for (int it = 0; it < warmup_iterations; ++it) {
+                if (w) solver.w_cycle(pp, fp, N, h);
+                else solver.v_cycle(pp, fp, N, h);
+            }
+            auto t0 = std::chrono::high_resolution_clock::now();
+            for (int it = 0; it < mg_max_iterations; ++it) {
+                if (w) solver.w_cycle(pp, fp, N, h);
+                else solver.v_cycle(pp, fp, N, h);
+            }
+            auto t1 = std::chrono::high_resolution_clock::now();
+            secs = std::chrono::duration<double>(t1 - t0).count();
+            if (mixed == 1) dphi.download(phi.data());
+        } else if (host_arrays) {
             pgmg_host::rhs(f, N, h, pr);
             for (int it = 0; it < warmup_iterations; ++it) {
                 if (w) solver.w_cycle(phi.data(), f.data(), N, h);

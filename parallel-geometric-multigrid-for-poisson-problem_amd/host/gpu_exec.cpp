@@ -27,6 +27,7 @@ int main(int argc, char **argv)
     int mg_max_iterations = 3;                                        // main.cu:17
     int alpha = 3;                                                    // main.cu:15
     bool ops = false, hash = false, host_arrays = false, v_only = false;
+    int mixed = 0;
     int warmup = 0;
     std::vector<int> err_list;
     for (int i = 1; i < argc; ++i) {
@@ -45,6 +46,10 @@ int main(int argc, char **argv)
             hash = true;
         } else if (!std::strcmp(argv[i], "--host-arrays")) {
             host_arrays = true;
+        } else if (!std::strcmp(argv[i], "--mixed-dphi-hf")) {
+            mixed = 1;
+        } else if (!std::strcmp(argv[i], "--mixed-hphi-df")) {
+            mixed = 2;
         } else if (!std::strcmp(argv[i], "--v-only")) {
             v_only = true;
         } else if (!std::strcmp(argv[i], "--warmup") && i + 1 < argc) {
@@ -56,7 +61,8 @@ int main(int argc, char **argv)
         } else {
             std::cerr << "usage: " << argv[0]
                       << " [--n 33,65,...] [--cycles K] [--alpha A] [--ops] [--hash]"
-                         " [--host-arrays] [--v-only] [--warmup W] [--err-vector N,...]\n";
+                         " [--host-arrays | --mixed-dphi-hf | --mixed-hphi-df] [--v-only]"
+                         " [--warmup W] [--err-vector N,...]\n";
             return 2;
         }
     }
@@ -64,6 +70,7 @@ int main(int argc, char **argv)
         ParallelTestRunner parallel_runner(0, mg_max_iterations, alpha);
         parallel_runner.print_hash = hash;
         parallel_runner.host_arrays = host_arrays;
+        parallel_runner.mixed = mixed;
         parallel_runner.warmup_iterations = warmup;
         if (v_only) {
             for (int n : N_list) {

@@ -126,13 +126,18 @@ def test_reference_main_on_mirror(tmp_path, golden_cycles):
 
 
 @pytest.mark.parametrize("args", [["--n", "2049", "--cycles", "2", "--v-only"],
-                                  ["--n", "129", "--cycles", "3", "--v-only", "--host-arrays"]])
+                                  ["--n", "129", "--cycles", "3", "--v-only", "--host-arrays"],
+                                  ["--n", "2049", "--cycles", "2", "--v-only", "--mixed-dphi-hf"],
+                                  ["--n", "129", "--cycles", "3", "--v-only", "--mixed-hphi-df"]])
 def test_gpu_exec_array_modes(tmp_path, golden_cycles, args):
-    """The mirror's v_cycle on device arrays in place (N = 2049: cross-fused) and on host
-    arrays (--host-arrays): both the reference's hash."""
+    """The mirror's v_cycle on device arrays in place (N = 2049: cross-fused), on host arrays
+    (--host-arrays), and mixed: a device phi with a host f binds phi and a device
+    copy of f; a host phi with a device f reads f back and takes the host path.  Every mode
+    gives the reference's hash."""
     out = subprocess.run([str(EXE), "--hash"] + args, cwd=tmp_path, capture_output=True,
                          text=True, timeout=300, check=True).stdout
     N, k = int(args[1]), int(args[3])
     mode = re.findall(r"phi arrays: (.+)", out)[0].strip()
-    assert mode == ("host" if "--host-arrays" in args else "device, in place"), mode
+    host = "--host-arrays" in args or "--mixed-hphi-df" in args
+    assert mode == ("host" if host else "device, in place"), mode
     assert re.findall(r"phi FNV-64: ([0-9a-f]{16})", out)[0] == _golden_hash(golden_cycles, "V", N, k)
