@@ -121,7 +121,7 @@ extern "C" {
    16384u -- the 129x129 level inside the tail's launch (built in r03, bitwise, measured
              slower: one CU's fp64 VALU needs ~1.2 us per pass over 129^2 points; removed) */
 #define PGMG_FLAGS_RETIRED (8192u | 16384u)
-#define PGMG_FLAG_NO_CTILE 65536u /* the small coarse levels (N <= 1025, entered with x0 = 0)
+#define PGMG_FLAG_NO_CTILE 65536u /* the small coarse levels (N <= 513, entered with x0 = 0)
                                      run the row-marching fused passes instead of the 2D LDS
                                      tile passes (r04).  Results are identical either way */
 #define PGMG_FLAG_HOST_TRANSPORT 2048u /* world > 1 without RCCL: nccl_unique_id points to

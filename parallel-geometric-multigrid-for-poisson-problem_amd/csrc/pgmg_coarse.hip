@@ -4,7 +4,7 @@
 // two fused passes: k_pre (x1 = J(0), the check ||r(x1)||, x2 = J(x1), rc = R r(x2)) and
 // k_post (the pre-smoothed iterate recomputed from f, + P ec, two sweeps with the check
 // ||r(x1)||).  pgmg_fused.hip runs them as row-marching bands: right for the bulk levels,
-// where HBM streaming is what counts, but on the small levels (N <= 1025: 0.02-1 M points)
+// where HBM streaming is what counts, but on the small levels (N <= 513: 0.02-0.26 M points)
 // the launch spends its ~6 µs in ONE wave's serial chain -- a band of 2 coarse rows marches
 // 12 fine rows (3x redundant) with four stencil stages per row, ~1000 VALU + 700 SALU
 // instructions per wave, one wave per SIMD, nothing to hide the latency behind
@@ -289,10 +289,14 @@ __global__ __launch_bounds__(kCT) void k_post_tile(CoarseArgsT<T> a)
 // against 15 us row-marching; TC = 8 there is on par with the row-marching passes
 static int ctile_tc(int N) { return tuning_int("PGMG_CTILE_TC", 8) == 16 ? 16 : 8; }
 
+// N <= 513 (profiles/r04_ctile/, profiles/r04_final/coarse/): at 1025 the row-marching passes
+// are as fast or faster (26 vs 29 us per V-cycle at TC = 8, 20 us for k_post_tile alone at
+// TC = 16); on row strips the 2049 / 4097 levels' thin strips ran 0-5 % slower per rank with
+// tiles (profiles/r04_strips/)
 bool coarse_tile_ok(int N, bool dist)
 {
-    return N >= 9 && N <= (dist ? tuning_int("PGMG_CTILE_DIST_MAXN", 1025)
-                                : tuning_int("PGMG_CTILE_MAXN", 1025));
+    return N >= 9 && N <= (dist ? tuning_int("PGMG_CTILE_DIST_MAXN", 513)
+                                : tuning_int("PGMG_CTILE_MAXN", 513));
 }
 
 int coarse_tile_blocks_rows(int N, int jt0, int jt1)
