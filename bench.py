@@ -213,7 +213,7 @@ def op_cases(pg, n):
         return lambda k: k.startswith(prefix)
 
     cases = [
-        ("jacobi v=0 (one sweep: the single-sweep kernel k_op_sweep_ov, + the interior copy back)",
+        ("jacobi v=0 (one sweep: the single-sweep kernel k_op_sweep, + the interior copy back)",
          lambda: pg.ops.jacobi(x, f, h, 0, eps=-1.0, tmp=tmp), 24 * fine, sweep(False, False), 1),
         ("jacobi v=1 (2 sweeps, no early exit: Parallel::ComputeJacobi's call in the V-cycle; "
          "one paired pass k_op_sweep2 + the interior copy back)",
