@@ -37,7 +37,7 @@ CASES = [
     ("V", 513, 30, 1e-7, []),
     ("V", 1025, 3, 1e-7, []),
     ("V", 2049, 2, 1e-7, []),
-    ("V", 4097, 3, 1e-7, []),
+    ("V", 4097, 43, 1e-7, []),    # BASELINE configs[1]: the bench times 3 + 40 cycles
     ("V", 129, 8, 1e3, [8]),     # every smoother exits after its first sweep
     ("V", 257, 5, 1.0, []),      # mixed early exits
     ("V", 65, 4, 0.0, [4]),      # never exits

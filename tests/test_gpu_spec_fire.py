@@ -30,11 +30,18 @@ def _calls(pgmg, N, calls, flags=0, kind="V"):
 
 @pytest.mark.parametrize("N,calls", [(2049, [3, 40]), (4097, [3, 40]), (2049, [60]),
                                      (2049, [1] * 45), (2049, [7] * 8), (4097, [5, 20, 20])])
-def test_fire_prediction_bitwise(pgmg, N, calls):
+def test_fire_prediction_bitwise(pgmg, oracle_mod, golden_cycles, N, calls):
     phi, det, info, masks = _calls(pgmg, N, calls)
     ref, rdet, _, _ = _calls(pgmg, N, calls, flags=pgmg.PGMG_FLAG_EXACT_DIST)
     assert_bitwise(phi, ref, f"N={N} calls={calls}")
     assert det == rdet
+    # BASELINE configs[1]'s call shapes at 4097 against the reference's own 43 cycles
+    case = next((c for c in golden_cycles if c["kind"] == "V" and c["N"] == N
+                 and c["eps"] == 1e-7 and len(c["cycles"]) >= sum(calls)), None)
+    if case is not None:
+        want = case["cycles"][sum(calls) - 1]
+        assert oracle_mod.fnv_hash(phi) == want["hash"], (N, calls)
+        assert det[0] == want["sweeps"], (N, calls, det, want)
     assert info[0] and info[1] == 0, info      # speculative, never rolled back
     # 129 / 257 fire from cycles 27 / 30 at 2049 and fall under eps/4 a few cycles later; a
     # 3 + 40 call ends before a split for them pays (segment planning), longer runs get there

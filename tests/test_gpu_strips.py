@@ -66,7 +66,7 @@ def test_strips_vcycle_bitwise_equal_single_gpu(pgmg, world, N, gather_n):
 def test_strips_match_reference_golden(pgmg, oracle_mod, golden_cycles):
     case = next(c for c in golden_cycles if c["kind"] == "V" and c["N"] == 4097)
     outs = _run_ranks(pgmg, 4, 4097, 3, gather_n=257)
-    assert oracle_mod.fnv_hash(outs[0][0]) == case["cycles"][-1]["hash"]
+    assert oracle_mod.fnv_hash(outs[0][0]) == case["cycles"][2]["hash"]
 
 
 @pytest.mark.parametrize("eps", [1e3, 1.0])
