@@ -133,6 +133,12 @@ struct pgmg_ctx {
     unsigned *uflags = nullptr;   // per-check verdicts (+ one spare word: any)
     long long chk_cap = 0;
     pgmg::Grid bk;                // level-0 solution at the start of the call (rollback)
+    // speculative F-cycles (pgmg_ctx.hip "speculative F-cycles"): every bulk check of the
+    // climb recorded "does not fire"; a rollback restarts the call's first climb from the
+    // tail top's restricted grid, saved here (the only input of the climb)
+    bool fspec = false;           // the F-cycles being enqueued are speculative
+    bool fspec_off = false;       // a speculative F call was rolled back: in-stream (problem)
+    pgmg::Grid ftop;
     unsigned long long *stats_bk = nullptr;
     long long rollbacks = 0;
     unsigned *ppflags = nullptr;  // k_postpre_decide flags

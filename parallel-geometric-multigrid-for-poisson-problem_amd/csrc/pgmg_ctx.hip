@@ -166,6 +166,7 @@ void pgmg::free_grid(Grid &g)
 // W-cycles (gamma > 1): a bulk level's visits are planned one by one (w_visit_mode)
 static int chk_mode(const pgmg_ctx *c, int level)
 {
+    if (c->lean && c->fspec) return 0;   // speculative F-cycles: every bulk check
     if (!c->lean || (c->spec_gamma > 1 && level > 0) || c->lvl_exact[level]) return 2;
     return c->lvl_fire[level] ? 1 : 0;
 }
@@ -458,7 +459,8 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     int mode = chk_mode(c, l);
     // V-cycles: a speculating level records "does not fire" up to its predicted crossing of
     // 100 eps (spec_mark_levels), in-stream after it
-    if (mode == 0 && l > 0 && c->spec_gamma == 1 && c->lvl_vis[l]++ >= c->lvl_kx[l]) mode = 2;
+    if (mode == 0 && l > 0 && c->spec_gamma == 1 && !c->fspec && c->lvl_vis[l]++ >= c->lvl_kx[l])
+        mode = 2;
     const int wm = w_visit_mode(c, l);
     const int visit = c->cur_visit;   // (the children's visits move it)
     if (wm >= 0) mode = wm;
@@ -970,6 +972,7 @@ int pgmg_destroy(pgmg_ctx *c)
     if (c->mark_dev) (void)hipFree(c->mark_dev);
     if (c->stats_bk) (void)hipFree(c->stats_bk);
     free_grid(c->bk);
+    free_grid(c->ftop);
     if (c->ppflags) (void)hipFree(c->ppflags);
     free_grid(c->S);
     free_grid(c->Ffmg);
@@ -1193,6 +1196,7 @@ static int problem_reset(pgmg_ctx *c)
     HIPC(hipDeviceSynchronize());
     c->have_problem = true;
     c->spec_off = false;   // a new problem: speculate again, every level
+    c->fspec_off = false;
     c->lvl_exact.assign(c->nb + 1, 0);
     c->lvl_fire.assign(c->nb + 1, 0);
     c->lvl_fire_block.assign(c->nb + 1, 0);
@@ -1816,6 +1820,38 @@ static void spec_record_norms(pgmg_ctx *c, int n)
     }
 }
 
+// Validation of a speculative call's check log (one host round trip): every recorded check
+// re-reduced and compared with its recorded decision (k_verify_checks; row strips: the ranks
+// agree by allreduce(min)).  *h = 1 when some check could not be confirmed -- the call must
+// be rolled back -- or the log overflowed; per-check norms and verdicts land in hnorm / hflag.
+static int spec_validate(pgmg_ctx *c, unsigned *h_out, bool *overflow_out)
+{
+    const int n = (int)c->chks.size();
+    bool overflow = false;
+    for (const CheckRef &k : c->chks) overflow |= k.np < 0;
+    unsigned h = overflow ? 1u : 0u;
+    c->hnorm.assign(n, 0.0);
+    c->hflag.assign(n, 1u);
+    if (n > 0 && !overflow) {
+        unsigned *any = c->uflags + c->chk_cap;   // the spare word past the verdicts
+        HIPC(hipMemcpyAsync(c->chk_dev, c->chks.data(), n * sizeof(CheckRef),
+                            hipMemcpyHostToDevice, c->s));
+        launch_verify_checks(c->chk_dev, n, c->cfg.eps, c->uflags, c->chk_norm, c->s);
+        int e;
+        if (c->comm && (e = c->comm->allreduce_min_u32(c->uflags, n, c->s))) return e;
+        launch_any_flag(c->uflags, n, any, c->s);
+        HIPC(hipMemcpyAsync(&h, any, sizeof(unsigned), hipMemcpyDeviceToHost, c->s));
+        HIPC(hipMemcpyAsync(c->hnorm.data(), c->chk_norm, n * sizeof(double),
+                            hipMemcpyDeviceToHost, c->s));
+        HIPC(hipMemcpyAsync(c->hflag.data(), c->uflags, n * sizeof(unsigned),
+                            hipMemcpyDeviceToHost, c->s));
+    }
+    PGMG_TRY(stream_wait(c));
+    *h_out = h;
+    *overflow_out = overflow;
+    return PGMG_OK;
+}
+
 static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
 {
     Level &L0 = c->lv[0];
@@ -1874,25 +1910,9 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
         first = false;
         if (e) return e;
         const int n = (int)c->chks.size();
+        unsigned h = 0;
         bool overflow = false;
-        for (const CheckRef &k : c->chks) overflow |= k.np < 0;
-        unsigned h = overflow ? 1u : 0u;
-        c->hnorm.assign(n, 0.0);
-        c->hflag.assign(n, 1u);
-        if (n > 0 && !overflow) {
-            unsigned *any = c->uflags + c->chk_cap;   // the spare word past the verdicts
-            HIPC(hipMemcpyAsync(c->chk_dev, c->chks.data(), n * sizeof(CheckRef),
-                                hipMemcpyHostToDevice, c->s));
-            launch_verify_checks(c->chk_dev, n, c->cfg.eps, c->uflags, c->chk_norm, c->s);
-            if (c->comm && (e = c->comm->allreduce_min_u32(c->uflags, n, c->s))) return e;
-            launch_any_flag(c->uflags, n, any, c->s);
-            HIPC(hipMemcpyAsync(&h, any, sizeof(unsigned), hipMemcpyDeviceToHost, c->s));
-            HIPC(hipMemcpyAsync(c->hnorm.data(), c->chk_norm, n * sizeof(double),
-                                hipMemcpyDeviceToHost, c->s));
-            HIPC(hipMemcpyAsync(c->hflag.data(), c->uflags, n * sizeof(unsigned),
-                                hipMemcpyDeviceToHost, c->s));
-        }
-        PGMG_TRY(stream_wait(c));
+        if ((e = spec_validate(c, &h, &overflow))) return e;
         if (h) {
             // some check could fire: roll back this segment, rerun the rest of the call with
             // in-stream decisions; the levels whose checks could fire stay in-stream
@@ -2111,8 +2131,20 @@ static int enqueue_smooth3_fused(pgmg_ctx *c, int l)
     q.row_hi = L.u1;
     q.rc_lo = 1;
     q.rc_hi = 1;
-    if ((e = launch_smooth4(q, c->s))) return e;
     const int np = postpre_blocks(L.N, q.jc0, q.jc1);
+    if (c->lean && c->fspec) {
+        // speculative F-cycles: the three checks recorded "does not fire" (the pass books its
+        // four sweeps), no decision or rare-path launch
+        q.partials1 = chk_log(c, np, l, 0);
+        q.partials2 = chk_log(c, np, l, 0);
+        q.partials3 = chk_log(c, np, l, 0);
+        q.stats = c->stats;
+        if ((e = launch_smooth4(q, c->s))) return e;
+        std::swap(L.A, L.B);
+        c->fsmooth_swapped = true;
+        return PGMG_OK;
+    }
+    if ((e = launch_smooth4(q, c->s))) return e;
     const double *g3 = nullptr;
     if (dist) {
         launch_sum_partials(q.partials1, np, c->scalar, c->s);
@@ -2127,8 +2159,12 @@ static int enqueue_smooth3_fused(pgmg_ctx *c, int l)
     return PGMG_OK;
 }
 
+// opt: kFSaveTop -- keep a copy of the tail top's restricted grid (a speculative call's first
+// F-cycle); kFFromTop -- skip the restriction, start the climb from that copy (its rerun)
+constexpr int kFSaveTop = 1, kFFromTop = 2;
+
 template <class T>
-static int enqueue_fcycle(pgmg_ctx *c)
+static int enqueue_fcycle(pgmg_ctx *c, int opt = 0)
 {
     const int nb = c->nb;
     double factor;
@@ -2138,7 +2174,9 @@ static int enqueue_fcycle(pgmg_ctx *c)
     }
     int e;
     const bool use_r2 = !(c->cfg.flags & PGMG_FLAG_NO_R2);   // two restriction steps per pass
-    for (int l = 0; l < nb; ++l) {
+    if (opt & kFFromTop)
+        HIPC(hipMemcpyAsync(c->lv[nb].A.base, c->ftop.base, c->ftop.bytes, hipMemcpyDeviceToDevice, c->s));
+    for (int l = (opt & kFFromTop) ? nb : 0; l < nb; ++l) {
         Level &L = c->lv[l], &C = c->lv[l + 1];
         if (!is_dist(c, l)) {
             // the intermediate level's restricted values are dead (the climb overwrites that
@@ -2159,6 +2197,8 @@ static int enqueue_fcycle(pgmg_ctx *c)
         // first replicated level: every rank's rows to every rank
         if (!is_dist(c, l + 1) && (e = c->comm->allgather_rows(c, l + 1, C.A))) return e;
     }
+    if (opt & kFSaveTop)
+        HIPC(hipMemcpyAsync(c->ftop.base, c->lv[nb].A.base, c->ftop.bytes, hipMemcpyDeviceToDevice, c->s));
     {
         Level &Lt = c->lv[nb];
         TailArgsT<T> t{};
@@ -2254,6 +2294,80 @@ static int enqueue_fcycle(pgmg_ctx *c)
     return PGMG_OK;
 }
 
+// Speculative F-cycles (one GPU).  The climb's V-cycles and smooth(3) passes decide their
+// early-exit checks in-stream by default: a decision launch after every bulk pass and every
+// fused smooth(3), ~86 launches of ~5 us per F-cycle at N = 16385 (9 % of it), while on the
+// reference problem no bulk check of an F-cycle fires (the F goldens: 0 exits).  A call of F
+// cycles is therefore enqueued with every bulk check recorded "does not fire" (the V-cycles'
+// mode 0; smooth(3)'s three checks too, its pass booking the four sweeps) and validated once
+// after the call, like the V-cycles' speculative calls.  A rollback needs no copy of the
+// level-0 solution: an F-cycle reads phi only through the restriction chain, whose one live
+// result is the tail top's grid (the intermediate levels' values are dead, the climb
+// overwrites them), so the first F-cycle's tail-top grid is kept (kFSaveTop) and the rerun --
+// every F-cycle of the call decided in-stream, bitwise the in-stream call -- starts its first
+// climb from it (kFFromTop).  The level buffers the smooth(3) passes swap and the statistics
+// are restored first.  A rolled-back problem keeps its F-cycles in-stream (fspec_off).
+template <class T>
+static int run_fcycles_spec(pgmg_ctx *c, int ncycles)
+{
+    const int nb = c->nb;
+    // log: per F-cycle, every climb level's V-cycle (the level and all below it) and the three
+    // smooth(3) checks of the levels below the finest
+    long long dbl = 64, nchk = 4;
+    for (int l = 0; l < nb; ++l) {
+        long long d, k;
+        spec_need_level(c, l, 1, &d, &k);
+        dbl += (long long)ncycles * d;
+        nchk += (long long)ncycles * k;
+        if (l > 0) {
+            const Level &L = c->lv[l];
+            dbl += 3LL * ncycles * postpre_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2);
+            nchk += 3LL * ncycles;
+        }
+    }
+    int e = spec_reserve(c, dbl, nchk);
+    if (e) return e;
+    if (!c->ftop.base && (e = alloc_grid(c->ftop, c->lv[nb]))) return e;
+    std::vector<Grid> A0(nb + 1), B0(nb + 1);
+    for (int l = 0; l <= nb; ++l) {
+        A0[l] = c->lv[l].A;
+        B0[l] = c->lv[l].B;
+    }
+    HIPC(hipMemcpyAsync(c->stats_bk, c->stats, 4 * sizeof(unsigned long long),
+                        hipMemcpyDeviceToDevice, c->s));
+    // the coarse levels' "pre-smooth fired" flags (written by the skipped rare paths) = 0
+    HIPC(hipMemsetAsync(c->flags, 0, sizeof(unsigned) * (c->lv.size() + 1) * 2 * kMaxSweeps, c->s));
+    c->lean = true;
+    c->fspec = true;
+    c->spec_gamma = 1;
+    c->plog_used = 0;
+    c->chks.clear();
+    c->chk_visit.clear();
+    c->wvisit = 0;
+    c->cur_visit = -1;
+    for (int k = 0; k < ncycles && !e; ++k) {
+        e = enqueue_fcycle<T>(c, k == 0 ? kFSaveTop : 0);
+        if (!e) c->fmg_rhs_ready = true;
+    }
+    c->lean = false;
+    c->fspec = false;
+    if (e) return e;
+    unsigned h = 0;
+    bool overflow = false;
+    if ((e = spec_validate(c, &h, &overflow))) return e;
+    if (!h) return PGMG_OK;
+    ++c->rollbacks;
+    c->fspec_off = true;
+    for (int l = 0; l <= nb; ++l) {
+        c->lv[l].A = A0[l];
+        c->lv[l].B = B0[l];
+    }
+    HIPC(hipMemcpyAsync(c->stats, c->stats_bk, 4 * sizeof(unsigned long long),
+                        hipMemcpyDeviceToDevice, c->s));
+    for (int k = 0; k < ncycles && !e; ++k) e = enqueue_fcycle<T>(c, k == 0 ? kFFromTop : 0);
+    return e;
+}
+
 extern "C" {
 
 int pgmg_fcycle(pgmg_ctx *c, int ncycles)
@@ -2319,9 +2433,16 @@ int pgmg_fcycle(pgmg_ctx *c, int ncycles)
     const bool ext = c->ext_phi != nullptr;
     if (ext) PGMG_TRY(ext_stage_in(c, false));
     HIPC(hipEventRecord(c->ev0, c->s));
-    for (int k = 0; k < ncycles && !e; ++k) {
-        e = c->fp32 ? enqueue_fcycle<float>(c) : enqueue_fcycle<double>(c);
-        if (!e) c->fmg_rhs_ready = true;
+    // speculative F-cycles: one GPU, the fused climb (PIN), not EXACT_DIST, not after a rollback
+    const bool fspec = c->nb > 0 && c->fused && c->comm == nullptr && !c->fspec_off &&
+                       !(c->cfg.flags & (PGMG_FLAG_EXACT_DIST | PGMG_FLAG_NO_PIN));
+    if (fspec) {
+        e = c->fp32 ? run_fcycles_spec<float>(c, ncycles) : run_fcycles_spec<double>(c, ncycles);
+    } else {
+        for (int k = 0; k < ncycles && !e; ++k) {
+            e = c->fp32 ? enqueue_fcycle<float>(c) : enqueue_fcycle<double>(c);
+            if (!e) c->fmg_rhs_ready = true;
+        }
     }
     if (c->fsmooth_swapped && c->gexec) {   // its level buffers traded places: recapture
         PGMG_TRY(stream_wait(c));

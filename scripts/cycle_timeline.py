@@ -30,9 +30,12 @@ def child(args):
         kw.update(rank=args.rank, world=args.world, flags=kw.get("flags", 0) | pg.PGMG_FLAG_SOLO)
     with pg.Solver(args.n, **kw) as s:
         s.set_problem()
-        run = s.wcycle if args.kind == "W" else s.vcycle
-        run(1 if args.kind == "W" else 3)
+        run = {"W": s.wcycle, "F": s.fcycle}.get(args.kind, s.vcycle)
+        run(3 if args.kind == "V" else 1)
         s.sync()
+        if args.kind == "F":   # a marker kernel before the timed call (F calls start variously)
+            torch.full((64,), 1.0, device=f"cuda:{torch.cuda.current_device()}")
+            torch.cuda.synchronize()
         run(args.cycles)
         s.sync()
 
@@ -46,13 +49,18 @@ def parse(args):
         gx, gy = int(r.get("Grid_Size_X", 0) or 0), int(r.get("Grid_Size_Y", 0) or 0)
         ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name, gx, gy))
     ks.sort()
-    # the timed call starts at the first finest-level k_pre after the warmup call
-    starts = [i for i, k in enumerate(ks) if k[2].startswith("k_pre<double, false, true")]
-    i0 = starts[-1]
-    seg = ks[i0:]
-    # cut at the last finest-level k_post
-    ends = [i for i, k in enumerate(seg) if k[2].startswith("k_post<double, true")]
-    seg = seg[:ends[-1] + 1] if ends else seg
+    marks = [i for i, k in enumerate(ks) if "FillFunctor" in k[2]]
+    if args.kind == "F" and marks:
+        # F: the timed call is everything after the child's marker kernel
+        seg = ks[marks[-1] + 1:]
+    else:
+        # the timed call starts at the first finest-level k_pre after the warmup call
+        starts = [i for i, k in enumerate(ks) if k[2].startswith("k_pre<double, false, true")]
+        i0 = starts[-1]
+        seg = ks[i0:]
+        # cut at the last finest-level k_post
+        ends = [i for i, k in enumerate(seg) if k[2].startswith("k_post<double, true")]
+        seg = seg[:ends[-1] + 1] if ends else seg
     total = seg[-1][1] - seg[0][0]
     agg = {}
     prev_end = seg[0][0]
@@ -82,7 +90,7 @@ if __name__ == "__main__":
     ap.add_argument("--n", type=int, default=16385)
     ap.add_argument("--cycles", type=int, default=10)
     ap.add_argument("--flags", type=int, default=0)
-    ap.add_argument("--kind", default="V", choices=["V", "W"])
+    ap.add_argument("--kind", default="V", choices=["V", "W", "F"])
     ap.add_argument("--world", type=int, default=1)
     ap.add_argument("--rank", type=int, default=0)
     a = ap.parse_args()
