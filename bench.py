@@ -78,6 +78,9 @@ def parse():
     ap.add_argument("--other-configs", choices=["auto", "off"], default="auto",
                     help="auto (the default headline run only: one GPU, V, f64, N = 16385): also "
                          "time BASELINE.json's other GPU configs on this GPU, each hash-checked")
+    ap.add_argument("--big-grid", choices=["auto", "off"], default="auto",
+                    help="auto (N > 1 GPUs, V, f64, N = 16385): also time BASELINE configs[3]'s "
+                         "N = 32769 on the same ranks (1 + 5 cycles, median of 3, hash-checked)")
     ap.add_argument("--fast-mode", choices=["auto", "off"], default="auto",
                     help="auto (one GPU, V, f64): also time PGMG_FLAG_FAST (FMA / shared "
                          "neighbour sums in the finest pass; not bitwise) and report its "
@@ -554,7 +557,7 @@ def main():
 
     want = golden_hash(args.cycle, args.n, args.warmup + args.steps) if args.dtype == "f64" else None
 
-    def new_solver(flags):
+    def new_solver(flags, n=None):
         kw = dict(device=device, dtype=args.dtype)
         if host_tp:
             kw.update(transport=pg.HostTransport(), rank=rank, world=world)
@@ -562,7 +565,8 @@ def main():
             t = torch.tensor(list(pg.unique_id()) if rank == 0 else [0] * 128, dtype=torch.uint8)
             dist.broadcast(t, 0)
             kw.update(rank=rank, world=world, uid=bytes(t.tolist()))
-        return pg.Solver(args.n, flags=flags | (pg.PGMG_FLAG_SOLO if solo else 0), **kw)
+        return pg.Solver(args.n if n is None else n,
+                         flags=flags | (pg.PGMG_FLAG_SOLO if solo else 0), **kw)
 
     def run_leg(extra_flags, reps):
         """`reps` clean repetitions on one context (set_problem restarts each from phi0 = 0)
@@ -607,6 +611,34 @@ def main():
         return out
 
     main_leg = run_leg(0, max(1, args.reps))
+    # BASELINE configs[3]'s grid (N = 32769) on the same N ranks: SURVEY §8(e) asks for
+    # V-cycles/s at 1, 2, 4 and 8 GPUs at 16385 AND 32769; the N = 1 number is other_configs'
+    # "configs[3]'s grid on ONE MI355X" (1 + 5 cycles, median of 3, the same shape)
+    big_leg = None
+    # (the host-staged transport runs it too: the harness test of this leg on a one-GPU box)
+    if (world > 1 and not solo and args.cycle == "V" and args.dtype == "f64"
+            and args.n == 16385 and args.big_grid == "auto"):
+        s = new_solver(0, n=32769)
+        ts = []
+        for _ in range(3):
+            s.set_problem()
+            s.vcycle(1)
+            s.sync()
+            barrier()
+            t0 = time.perf_counter()
+            s.vcycle(5)
+            s.sync()
+            barrier()
+            ts.append(max_over_ranks(time.perf_counter() - t0))
+        w6, h6 = golden_hash("V", 32769, 6), s.solution_hash(0)
+        s.close()
+        dt = statistics.median(ts)
+        big_leg = {"config": "BASELINE configs[3]: V-cycle N=32768^2 on the same row strips "
+                             f"x{world} ({'host-staged transport, every rank on GPU 0: harness test, not a measurement' if host_tp else 'RCCL halos'}); "
+                             "its one-GPU number: other_configs of the N = 1 line",
+                   "value": round(5 / dt, 3), "unit": "V-cycles/s", "n_gpus": world,
+                   "ms_per_step": round(dt * 1e3 / 5, 4), "timed": "1 + 5 cycles, median of 3",
+                   "parity": None if w6 is None or h6 is None else h6 == w6}
     gen_leg = None
     if (world == 1 and args.cycle == "V" and args.general_rhs == "auto" and main_leg["fused"]
             and main_leg["gen"]):
@@ -632,15 +664,6 @@ def main():
                 ts.append(time.perf_counter() - t0)
             return statistics.median(ts)
 
-        def hashed(s, runs, kind, n, cycles):
-            s.set_problem()
-            for run, k in runs:
-                run(k)
-            s.sync()
-            w = golden_hash(kind, n, cycles)
-            h = s.solution_hash(0)
-            return None if w is None or h is None else h == w
-
         with pg.Solver(4097, device=device) as s:   # configs[1]
             dt = timed(s, s.vcycle, 3, 40, 3)
             # the timed call's own result: phi after the last repetition's 3 + 40 cycles
@@ -654,11 +677,14 @@ def main():
                                             "against the reference's (tests/golden/cycles.json)"})
         with pg.Solver(32769, device=device) as s:  # configs[3]'s grid on one GPU
             dt = timed(s, s.vcycle, 1, 5, 3)
+            w6, h6 = golden_hash("V", 32769, 6), s.solution_hash(0)
             others.append({"config": "BASELINE configs[3]'s grid (N=32768^2) on ONE MI355X: V-cycle, fp64 "
-                                     "(the 8-GPU row-strip run is the driver's scaling bench)",
+                                     "(the row-strip runs on N GPUs report it as big_grid)",
                            "value": round(5 / dt, 3), "unit": "V-cycles/s",
                            "ms_per_step": round(dt * 1e3 / 5, 4), "timed": "1 + 5 cycles, median of 3",
-                           "parity": hashed(s, [(s.vcycle, 2)], "V", 32769, 2)})
+                           "parity": None if w6 is None or h6 is None else h6 == w6,
+                           "parity_detail": "FNV-64 of phi after the timed repetitions' 1 + 5 cycles "
+                                            "against oracle/mg_cpu_exec_port's (tests/golden/cycles.json)"})
             # configs[4]'s cycle: the FMG start (one F-cycle) then one W-cycle, fp64
             s.set_problem()
             t0 = time.perf_counter()
@@ -891,6 +917,8 @@ def main():
         }
         if others is not None:
             line["other_configs"] = others
+        if big_leg is not None:
+            line["big_grid"] = big_leg
         if dropin is not None:
             line["dropin"] = dropin
         if op_rows is not None:

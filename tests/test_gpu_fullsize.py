@@ -114,6 +114,17 @@ def _ranks(pgmg, world, N, work, **cfg):
     return out
 
 
+def test_vcycle_32769_bench_shape(pgmg, oracle_mod, golden_cycles):
+    """BASELINE config 4's grid on one GPU in bench.py's shape (1 + 5 cycles, two calls):
+    phi after 6 cycles bitwise oracle/mg_cpu_exec_port's (tests/golden/big_logs/V32769.txt)."""
+    rows = _case(golden_cycles, "V", 32769)
+    with pgmg.Solver(32769) as s:
+        s.set_problem()
+        s.vcycle(1)
+        s.vcycle(5)
+        _check(oracle_mod, s.solution(), s.stats(), rows, 6, "V32769 1 + 5")
+
+
 def test_strips8_vcycle_32769(pgmg, oracle_mod, golden_cycles):
     """BASELINE config 4: N = 32769 on 8 row strips, one pgmg_vcycle(2) call per rank
     (cross-fused finest level per strip, speculative decisions, RCCL-shaped halos)."""
