@@ -230,7 +230,10 @@ int pgmg_pointer_is_device(const void *p, int *is_device);
  * pgmg_fcycle: one F-cycle = restrict phi to n_coarse, then per level up smooth(3),
  * prolongation into a zeroed finer grid, analytic RHS of that grid (h chain starting at
  * 1/(n_coarse-1)), one V-cycle; the f given to pgmg_set_problem is left untouched
- * (MultiGridTestRunner.hpp:192-205).  On row strips as well (world > 1). */
+ * (MultiGridTestRunner.hpp:192-205).  On row strips as well (world > 1).  On one GPU an
+ * F-cycle call is speculative too (its bulk checks recorded "does not fire" and validated once
+ * after the call; a rollback reruns the call in-stream from the saved restricted grid and the
+ * problem's later F calls decide in-stream); PGMG_FLAG_EXACT_DIST turns that off. */
 int pgmg_vcycle(pgmg_ctx *ctx, int ncycles);
 int pgmg_wcycle(pgmg_ctx *ctx, int ncycles);
 int pgmg_fcycle(pgmg_ctx *ctx, int ncycles);
@@ -293,8 +296,8 @@ int pgmg_fine_pass_bytes(pgmg_ctx *ctx, int pass, double *bytes);
 /* Whether V/W-cycle calls decide the smoother early-exit checks speculatively (1: the
  * checks are recorded, validated once after the call, and the call is rolled back and
  * rerun with in-stream decisions when one could fire; cross-fused or row-strip contexts
- * without PGMG_FLAG_EXACT_DIST) or in-stream (0), and how many calls were rolled back.
- * After a rollback the context decides in-stream until the next pgmg_set_problem. */
+ * without PGMG_FLAG_EXACT_DIST) or in-stream (0), and how many calls (V, W or F) were rolled
+ * back.  After a rollback the context decides in-stream until the next pgmg_set_problem. */
 int pgmg_dist_info(pgmg_ctx *ctx, int *speculative, long long *rollbacks);
 
 /* Which bulk levels decide their early-exit checks in-stream in the next speculative call:
