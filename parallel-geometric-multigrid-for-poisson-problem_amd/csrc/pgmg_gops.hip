@@ -399,9 +399,16 @@ constexpr int kOpTarget = 4096;   // workgroups per op launch (16 per CU)
 // workgroups (k_op_sweep<8>: 120 VGPRs, 4 waves per SIMD = 1024 workgroups of 4 waves on 256
 // CUs), 8 rows of loads in flight and non-temporal stores: 1.339 ms per sweep (0.60 of 8 TB/s)
 // against 1.35-1.47 for 2048-8192 workgroups, 4 rows, default stores or the overlapping
-// tiles (k_op_sweep_ov, kept as PGMG_OP_OV=1 of the measurement build)
+// tiles (k_op_sweep_ov, kept as PGMG_OP_OV=1 of the measurement build).  r04 (op_ab.py --rows,
+// profiles/r04_ops/op_rows.jsonl): 16 rows in flight (214 VGPRs: 2 waves per SIMD, the 1024
+// workgroups in two rounds) 1.390-1.393 ms against 1.403-1.405 for 8 rows on the same box,
+// 16 rows at one round of 512 workgroups 1.45, 4 rows at 1792 1.46 -- 16 is the default
 static bool op_ov() { return tuning_int("PGMG_OP_OV", 0) != 0; }
-static int op_u() { return tuning_int("PGMG_OP_U", 8) == 4 ? 4 : 8; }
+static int op_u()
+{
+    const int u = tuning_int("PGMG_OP_U", 16);
+    return u == 4 ? 4 : (u == 8 ? 8 : 16);
+}
 static int op_target() { return tuning_int("PGMG_OP_BLOCKS", 1024); }
 
 static OpGeom sweep_geom(int H, int W)
@@ -449,6 +456,7 @@ void launch_g_sweep(const double *xin, const double *f, double *xout, double *pa
         else sweep_u<UU, false, false>(g, ov, nt, xin, f, xout, partials, skip, reset, stats, hh, inv_hh, H, W, s); \
     } while (0)
     if (op_u() == 8) PGMG_SW(8);
+    else if (op_u() == 16) PGMG_SW(16);
     else PGMG_SW(4);
 #undef PGMG_SW
 }

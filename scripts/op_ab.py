@@ -21,6 +21,9 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=16385)
 ap.add_argument("--rounds", type=int, default=2)
 ap.add_argument("--v", type=int, default=20)
+ap.add_argument("--rows", action="store_true",
+                help="single sweeps only (PGMG_OP_FUSE2=0): rows of loads in flight U = 4 / 8 / 16 "
+                     "at one round of resident workgroups each")
 args = ap.parse_args()
 
 import torch  # noqa: E402
@@ -42,6 +45,10 @@ for ov, u, blocks in ((0, 8, 1024), (0, 8, 2048), (0, 4, 1792), (1, 8, 1280), (1
     for nt in (0, 1):
         variants.append({"PGMG_OP_OV": ov, "PGMG_OP_BLOCKS": blocks, "PGMG_OP_U": u,
                          "PGMG_OP_NT": nt})
+if args.rows:
+    # U = 8: 120 VGPRs, 4 waves per SIMD (1024 resident); U = 16: 214, 2 (512); U = 4: 70, 7 (1792)
+    variants = [{"PGMG_OP_FUSE2": 0, "PGMG_OP_OV": 0, "PGMG_OP_BLOCKS": b, "PGMG_OP_U": u,
+                 "PGMG_OP_NT": 1} for u, b in ((8, 1024), (16, 512), (16, 1024), (4, 1792))]
 for rnd in range(args.rounds):
     for var in variants:
         for k, v in var.items():
