@@ -536,6 +536,13 @@ __global__ __launch_bounds__(kBlock) void k_op_copy_interior(const double *__res
 
 void launch_g_copy_interior(const double *src, double *dst, int H, int W, hipStream_t s)
 {
+    // rows of loads in flight: 8 (PGMG_OPC_U = 16 in the measurement build: the same within
+    // noise, profiles/r04_ops/op_ru.jsonl)
+    if (tuning_int("PGMG_OPC_U", 8) == 16) {
+        const OpGeom g = op_geom((W - 1) / 2, H - 2, 16, tuning_int("PGMG_OPC_BLOCKS", 2048));
+        k_op_copy_interior<16><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(src, dst, H, W, g.rpb);
+        return;
+    }
     const OpGeom g = op_geom((W - 1) / 2, H - 2, 8, tuning_int("PGMG_OPC_BLOCKS", 2048));
     k_op_copy_interior<8><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(src, dst, H, W, g.rpb);
 }
@@ -602,7 +609,15 @@ __global__ __launch_bounds__(kBlock) void k_op_residual(double *__restrict__ R,
 void launch_g_residual(double *r, const double *x, const double *f, double inv_hh, int H, int W,
                        hipStream_t s)
 {
-    // the sweep's pattern (2 reads, 1 write): its geometry (one round, 8 rows in flight)
+    // the sweep's pattern (2 reads, 1 write): its geometry (1024 workgroups)
+    // 16 rows in flight, as the sweep (r04, scripts/op_ru_ab.py, profiles/r04_ops/op_ru.jsonl:
+    // 1.344-1.351 ms against 1.360-1.362 for 8 rows, 3 interleaved rounds; 2048 workgroups
+    // 1.362-1.382); PGMG_OPR_U = 8 in the measurement build for the old form
+    if (tuning_int("PGMG_OPR_U", 16) == 16) {
+        const OpGeom g = op_geom((W - 1) / 2, H - 2, 16, tuning_int("PGMG_OPR_BLOCKS", 1024));
+        k_op_residual<16><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(r, x, f, inv_hh, H, W, g.rpb);
+        return;
+    }
     const OpGeom g = op_geom((W - 1) / 2, H - 2, 8, tuning_int("PGMG_OPR_BLOCKS", 1024));
     k_op_residual<8><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(r, x, f, inv_hh, H, W, g.rpb);
 }
