@@ -139,6 +139,9 @@ struct pgmg_ctx {
     bool fspec = false;           // the F-cycles being enqueued are speculative
     bool fspec_off = false;       // a speculative F call was rolled back: in-stream (problem)
     pgmg::Grid ftop;
+    // speculative F-cycle followed by another in the call: its finest k_post also forms level
+    // 2's restriction (k_post_r2; fr2_want while it is enqueued, fr2_made once it was)
+    bool fr2_want = false, fr2_made = false;
     unsigned long long *stats_bk = nullptr;
     long long rollbacks = 0;
     unsigned *ppflags = nullptr;  // k_postpre_decide flags

@@ -564,10 +564,22 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
         fa.np = coarse_tile_blocks_rows(L.N, ca.jt0, ca.jt1);
     }
     c->cur_visit = visit;
+    // speculative F-cycle followed by another: the finest k_post also restricts its result to
+    // level 2 (the next F-cycle's first restriction step; only when its check is recorded
+    // "does not fire", so x2 is the result); its 116-column tiles write more partials
+    const bool r2 = fine && mode == 0 && c->fr2_want && !dist && !recomp && po.Po == 0 &&
+                    c->nb >= 2 && !is_dist(c, 1);
+    if (r2) fa.np = post_r2_blocks(L.N, po.jc0, po.jc1);
     lp = chk_log(c, fa.np, l, mode);
     if (lp) po.partials = lp;
     ev = fine ? timed_begin(c, 2) : -1;
-    if (tile) {
+    if (r2) {
+        po.r2out = G<T>(c->lv[2].A);
+        po.Pr2 = c->lv[2].P;
+        po.Nr2 = c->lv[2].N;
+        if ((e = launch_post_r2(po, c->s))) return e;
+        c->fr2_made = true;
+    } else if (tile) {
         ca.partials = po.partials;
         launch_post_tile(ca, mode == 1 ? 1 : 0, c->s);
         HIPC(hipGetLastError());
@@ -2160,8 +2172,10 @@ static int enqueue_smooth3_fused(pgmg_ctx *c, int l)
 }
 
 // opt: kFSaveTop -- keep a copy of the tail top's restricted grid (a speculative call's first
-// F-cycle); kFFromTop -- skip the restriction, start the climb from that copy (its rerun)
-constexpr int kFSaveTop = 1, kFFromTop = 2;
+// F-cycle); kFFromTop -- skip the restriction, start the climb from that copy (its rerun);
+// kFR2Next -- another F-cycle follows: the finest k_post forms level 2's restriction
+// (k_post_r2); kFR2Done -- the previous F-cycle did: start the restriction at level 2
+constexpr int kFSaveTop = 1, kFFromTop = 2, kFR2Next = 4, kFR2Done = 8;
 
 template <class T>
 static int enqueue_fcycle(pgmg_ctx *c, int opt = 0)
@@ -2176,7 +2190,12 @@ static int enqueue_fcycle(pgmg_ctx *c, int opt = 0)
     const bool use_r2 = !(c->cfg.flags & PGMG_FLAG_NO_R2);   // two restriction steps per pass
     if (opt & kFFromTop)
         HIPC(hipMemcpyAsync(c->lv[nb].A.base, c->ftop.base, c->ftop.bytes, hipMemcpyDeviceToDevice, c->s));
-    for (int l = (opt & kFFromTop) ? nb : 0; l < nb; ++l) {
+    // level 2's values already formed by the previous F-cycle's finest k_post (k_post_r2:
+    // the pair 0 -> 2 below, bitwise)
+    const bool from2 = (opt & kFR2Done) && c->fr2_made && use_r2 && nb >= 2 && !is_dist(c, 0) &&
+                       !is_dist(c, 1);
+    c->fr2_made = false;
+    for (int l = (opt & kFFromTop) ? nb : (from2 ? 2 : 0); l < nb; ++l) {
         Level &L = c->lv[l], &C = c->lv[l + 1];
         if (!is_dist(c, l)) {
             // the intermediate level's restricted values are dead (the climb overwrites that
@@ -2260,7 +2279,10 @@ static int enqueue_fcycle(pgmg_ctx *c, int opt = 0)
             // the V-cycle's k_pre computes the prolongation on the fly (PIN): no separate
             // pass writing the zeroed fine grid; it reads 3 coarse rows past the strip
             if (dist && is_dist(c, l + 1) && (e = c->comm->halo(C.A, C, 3, c->s))) return e;
-            if ((e = enqueue_fused_level<T>(c, l, 1, false, true))) return e;
+            c->fr2_want = l == 0 && (opt & kFR2Next) && use_r2;
+            e = enqueue_fused_level<T>(c, l, 1, false, true);
+            c->fr2_want = false;
+            if (e) return e;
             if (l > 0 && (e = enqueue_smooth3_fused<T>(c, l))) return e;
             c->gen_level = 0;
             c->lgfx = c->lgsy = nullptr;
@@ -2319,6 +2341,10 @@ static int run_fcycles_spec(pgmg_ctx *c, int ncycles)
         spec_need_level(c, l, 1, &d, &k);
         dbl += (long long)ncycles * d;
         nchk += (long long)ncycles * k;
+        if (l == 0) {   // the finest k_post as k_post_r2 (more workgroups than k_post)
+            const Level &L = c->lv[0];
+            dbl += (long long)ncycles * post_r2_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2);
+        }
         if (l > 0) {
             const Level &L = c->lv[l];
             dbl += 3LL * ncycles * postpre_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2);
@@ -2345,12 +2371,16 @@ static int run_fcycles_spec(pgmg_ctx *c, int ncycles)
     c->chk_visit.clear();
     c->wvisit = 0;
     c->cur_visit = -1;
+    c->fr2_made = false;
     for (int k = 0; k < ncycles && !e; ++k) {
-        e = enqueue_fcycle<T>(c, k == 0 ? kFSaveTop : 0);
+        // consecutive F-cycles: the finest k_post of one forms the next one's level 2
+        const int opt = (k == 0 ? kFSaveTop : kFR2Done) | (k + 1 < ncycles ? kFR2Next : 0);
+        e = enqueue_fcycle<T>(c, opt);
         if (!e) c->fmg_rhs_ready = true;
     }
     c->lean = false;
     c->fspec = false;
+    c->fr2_made = false;
     if (e) return e;
     unsigned h = 0;
     bool overflow = false;
@@ -2364,6 +2394,7 @@ static int run_fcycles_spec(pgmg_ctx *c, int ncycles)
     }
     HIPC(hipMemcpyAsync(c->stats, c->stats_bk, 4 * sizeof(unsigned long long),
                         hipMemcpyDeviceToDevice, c->s));
+    // (in-stream: no k_post_r2, every F-cycle restricts from level 0)
     for (int k = 0; k < ncycles && !e; ++k) e = enqueue_fcycle<T>(c, k == 0 ? kFFromTop : 0);
     return e;
 }

@@ -489,17 +489,44 @@ __global__ __launch_bounds__(256) void k_pre_rare(PreArgsT<T> a, FixArgsF f)
 // ---------------------------------------------------------------------------
 // k_post
 // ---------------------------------------------------------------------------
+// full weighting of one point from its 3x3 neighbourhood (rows u / m / d = above / centre /
+// below, columns w / c / e): MultiGrid.hpp:187-205's expression and operand order (the same as
+// pgmg_kernels.hip's rfw for k_restrict2_values)
+constexpr int kR2Stride = 116;   // k_post_r2's wave-tile stride (6-column margin)
+
+template <class T>
+__device__ __forceinline__ T rfw_post(T u_w, T u_c, T u_e, T m_w, T m_c, T m_e, T d_w, T d_c, T d_e)
+{
+    return T(0.25) * m_c + T(0.125) * (m_e + m_w + d_c + u_c) + T(0.0625) * (u_w + u_e + d_w + d_e);
+}
+
+// R2 (k_post_r2, the finest level's last pass of an F-cycle that another one follows): the next
+// F-cycle starts by restricting this pass's result twice (compute_coarsest_grid, MultiGrid.hpp:
+// 28-55; the level-1 values are dead), so the pass forms level 2 itself from the x2 rows it
+// holds.  The band starts 4 rows earlier and ends 6 rows later (x2 valid on fine rows 2jcb-4 ..
+// 2jce+1 instead of its own 2jcb .. 2jce-1; only its own rows are stored), the last two x2 rows
+// and level-1 rows stay in registers, lane t forms the level-1 value at fine column c+1 (its
+// east column from lane t+1 by DPP) and the level-2 centre lanes (level-1 column even) the
+// level-2 value from lanes t-1 .. t+1.  A band owns the level-2 rows r2 with 4 r2 in its own
+// fine rows; a wave the level-2 columns whose centre fine column it owns.  A level-2 point
+// reads x2 three columns past its centre each side, so the wave tiles are 116 columns apart
+// with a 6-column margin (lanes 3 .. 60 own, instead of 120 / 4 and lanes 2 .. 61) and lane 63
+// loads its own east coarse column (x_eff, x1, x2 then valid on tile columns 0 .. 127, 1 .. 126,
+// 2 .. 125): every owned centre's window (at most columns 2t-2 .. 2t+4 of lane t <= 60) is in
+// the tile.
 // RECOMP (levels entered with x0 = 0): phi is not read.  The loaded row is f[ii+1];
 // x1 = J(0) is pointwise, so x1 row ii+1 -> phi row ii = J(x1) (or x1 when the pre
 // check fired) -> x_eff row ii: one more row of lag than reading phi, 16 B/point less.
-template <class T, bool FINE, int PAIRS, bool RECOMP, bool GENF, bool S1, bool S1P = false>
+template <class T, bool FINE, int PAIRS, bool RECOMP, bool GENF, bool S1, bool S1P = false,
+          bool R2 = false>
 __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
 {
     constexpr int R = 2 * PAIRS;
     if (a.cond != nullptr && *a.cond == 0u) return;  // conditional (rare-path) launch
     int lbx, lby;
     fused_block(lbx, lby);
-    const Cols k = lane_cols(a.N, lbx);
+    // R2: 116-column stride, 6-column margin (kR2Stride): see k_post_r2
+    const Cols k = R2 ? lane_cols_t<kR2Stride, 6>(a.N, lbx) : lane_cols(a.N, lbx);
     const int N = a.N, Nc = a.Nc;
     const long long P = a.P, Pc = a.Pc;
     const int jcb = a.jc0 + lby * a.rows_per_block;
@@ -527,13 +554,19 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
     // RECOMP: pre-smooth x1 rows ii-1, ii ; f row ii
     V2<T> g0 = z, g1 = z, fc = z;
     double acc = 0.0;
-    const int i_begin = 2 * jcb - 2;
+    const int i_begin = 2 * jcb - 2 - (R2 ? 4 : 0);
     const int c0w = __builtin_amdgcn_readfirstlane(k.c - 2 * (int)(threadIdx.x & 63));
     const bool idle = c0w + 4 > N - 2;  // spare wave (wave-uniform)
     const bool inner = c0w >= 3 && c0w + 127 <= N - 3;   // see pre_body
     const int i_end = idle ? i_begin
-                           : i_begin + ((2 * (jce - jcb) + 4 + R - 1) / R) * R;
+                           : i_begin + ((2 * (jce - jcb) + (R2 ? 10 : 4) + R - 1) / R) * R;
     const bool pfired = RECOMP && *a.pre_fired != 0u;
+    // R2: x2 rows q-2, q-1 and level-1 rows r1-2, r1-1 of this lane's level-1 column i1
+    V2<T> q0 = z, q1 = z;
+    T w0 = T(0), w1 = T(0);
+    const int i1 = (k.c + 1) >> 1, i2 = i1 >> 1;
+    const bool lane63 = (threadIdx.x & 63) == 63;
+    const bool r2col = R2 && (i1 & 1) == 0 && k.own && i2 >= 1 && i2 <= a.Nr2 - 2;
     if (RECOMP && !idle) {
         const V2<T> fm = ldv(F + (i_begin - 1) * P);
         fc = ldv(F + i_begin * P);
@@ -543,14 +576,17 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
     // coarse row m = ii/2 of fine row ii; an iteration of R rows uses coarse rows
     // i/2 .. i/2 + PAIRS
     V2<T> np_[R], nf[R];
-    T ncr[PAIRS + 1];
+    T ncr[PAIRS + 1], ncre[PAIRS + 1];   // ncre (R2): lane 63's east coarse column
     #pragma unroll
     for (int q = 0; q < R; ++q) {
         np_[q] = idle ? z : ldv(X + (i_begin + q) * P);
         if (!RECOMP && !GENF) nf[q] = idle ? z : ldv(F + (i_begin + q) * P);
     }
     #pragma unroll
-    for (int q = 0; q <= PAIRS; ++q) ncr[q] = idle ? T(0) : E[(long long)((i_begin >> 1) + q) * Pc];
+    for (int q = 0; q <= PAIRS; ++q) {
+        ncr[q] = idle ? T(0) : E[(long long)((i_begin >> 1) + q) * Pc];
+        if (R2) ncre[q] = idle || !lane63 ? T(0) : E[(long long)((i_begin >> 1) + q) * Pc + 1];
+    }
     // FULL: as in pre_body (rows interior to the band, the sum range and the grid; interior
     // wave columns)
     auto full_at = [&](int i) {
@@ -559,14 +595,17 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
     };
     auto iter = [&](int i, auto full_t) {
         V2<T> cp[R], cf[R];
-        T cr[PAIRS + 1];
+        T cr[PAIRS + 1], cre[PAIRS + 1];
         #pragma unroll
         for (int q = 0; q < R; ++q) {
             cp[q] = np_[q];
             if (!RECOMP && !GENF) cf[q] = nf[q];
         }
         #pragma unroll
-        for (int q = 0; q <= PAIRS; ++q) cr[q] = ncr[q];
+        for (int q = 0; q <= PAIRS; ++q) {
+            cr[q] = ncr[q];
+            if (R2) cre[q] = ncre[q];
+        }
         if (i + R < i_end) {
             #pragma unroll
             for (int q = 0; q < R; ++q) {
@@ -574,11 +613,18 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
                 if (!RECOMP && !GENF) nf[q] = ldv(F + (i + R + q) * P);
             }
             #pragma unroll
-            for (int q = 0; q <= PAIRS; ++q) ncr[q] = E[(long long)(((i + R) >> 1) + q) * Pc];
+            for (int q = 0; q <= PAIRS; ++q) {
+                ncr[q] = E[(long long)(((i + R) >> 1) + q) * Pc];
+                if (R2 && lane63) ncre[q] = E[(long long)(((i + R) >> 1) + q) * Pc + 1];
+            }
         }
         T crn[PAIRS + 1];
         #pragma unroll
-        for (int q = 0; q <= PAIRS; ++q) crn[q] = dpp_shl(cr[q]);
+        for (int q = 0; q <= PAIRS; ++q) {
+            crn[q] = dpp_shl(cr[q]);
+            // R2: lane 63's own east column, so x_eff is valid on all 128 columns of the tile
+            if (R2 && lane63) crn[q] = cre[q];
+        }
         double gy[R];   // GENF row factors of the iteration, loaded together up front
         if constexpr (GENF) {
             #pragma unroll
@@ -640,6 +686,25 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
                     if (a.nt & 4) stv_nt(O + (ii - 2) * Po, c2);
                     else stvu(O + (ii - 2) * Po, c2);
                 }
+                if constexpr (R2) {
+                    // x2 row q = ii - 2 (i is even: q is odd exactly for odd s)
+                    if (s & 1) {   // q = 2 r1 + 1: level-1 row r1 from x2 rows q-2, q-1, q
+                        const T v1 = rfw_post<T>(q0.x, q0.y, dpp_shl(q0.x), q1.x, q1.y, dpp_shl(q1.x),
+                                                 c2.x, c2.y, dpp_shl(c2.x));
+                        const int r1 = (ii - 3) >> 1;
+                        if (r1 & 1) {   // r1 = 2 r2 + 1 (wave-uniform): level-2 row r2
+                            const T v2 = rfw_post<T>(dpp_shr(w0), w0, dpp_shl(w0), dpp_shr(w1), w1,
+                                                     dpp_shl(w1), dpp_shr(v1), v1, dpp_shl(v1));
+                            const int r2 = r1 >> 1;
+                            if (r2col && 4 * r2 >= olo && 4 * r2 < ohi && r2 >= 1 && r2 <= a.Nr2 - 2)
+                                a.r2out[(long long)r2 * a.Pr2 + i2] = v2;
+                        }
+                        w0 = w1;
+                        w1 = v1;
+                    }
+                    q0 = q1;
+                    q1 = c2;
+                }
                 a0 = a1;
                 a1 = a2;
                 b0 = b1;
@@ -664,6 +729,14 @@ __global__ __launch_bounds__(256) void k_post(PostArgsT<T> a)
 {
     __shared__ double red[4];
     post_body<T, FINE, PAIRS, RECOMP, GENF, false>(a, red);
+}
+
+// the finest level's last pass of an F-cycle with the next F-cycle's level-2 restriction
+template <class T, bool GENF>
+__global__ __launch_bounds__(256) void k_post_r2(PostArgsT<T> a)
+{
+    __shared__ double red[4];
+    post_body<T, true, 2, false, GENF, false, false, true>(a, red);
 }
 
 // a coarse level's post-smooth whose check is predicted to fire (see k_pre1): x1 is the
@@ -1253,6 +1326,14 @@ int fused_blocks(int N, int jc0, int jc1)
     return gx * gy;
 }
 
+// k_post_r2's workgroups (its 116-column tiles): the partial sums its check writes
+int post_r2_blocks(int N, int jc0, int jc1)
+{
+    int t, gx, gy, r;
+    fused_geometry(N, jc0, jc1, &t, &gx, &gy, &r, kR2Stride);
+    return gx * gy;
+}
+
 // ---------------------------------------------------------------------------
 // read/write extents of the fused passes (pgmg_internal.h, check_span)
 // ---------------------------------------------------------------------------
@@ -1285,10 +1366,11 @@ static Span band_rows(int jc0, int jc1, int r, int lead, int extra, int R)
 
 // last column read by a non-idle wave of k_pre / k_post (120-column stride, 4-column
 // margin: wave w covers 120w - 3 .. 120w + 124); -1 when every wave is idle
-static long long tile_col_hi(int N, int waves)
+static long long tile_col_hi(int N, int waves, int stride = 120, int margin = 4)
 {
-    const int wmax = std::min(waves - 1, (N - 3) / 120);
-    return wmax < 0 ? -1 : 120LL * wmax - 3 + 127;
+    // wave w's tile starts at column stride*w + 1 - margin; idle once that + 4 > N - 2
+    const int wmax = std::min(waves - 1, (N - 7 + margin) / stride);
+    return wmax < 0 ? -1 : (long long)stride * wmax + 1 - margin + 127;
 }
 
 #define PGMG_SPAN(o, P, r0, r1, c0, c1, what)                                                  \
@@ -1318,19 +1400,22 @@ static int pre_spans(const PreArgsT<T> &a, int t, int gx, int r, bool x0_read, b
 }
 
 // k_post / k_post_rare: phi (or f one row ahead, RECOMP), f, the coarse correction, x2
+// (r2: k_post_r2's bands start 4 rows earlier and stream 6 rows more)
 template <class T>
-static int post_spans(const PostArgsT<T> &a, int t, int gx, int r, bool f_read)
+static int post_spans(const PostArgsT<T> &a, int t, int gx, int r, bool f_read, bool r2 = false)
 {
-    const Span sp = band_rows(a.jc0, a.jc1, r, 2, 4, 4);
-    const long long chi = tile_col_hi(a.N, gx * (t / 64));
+    const Span sp = band_rows(a.jc0, a.jc1, r, r2 ? 6 : 2, r2 ? 10 : 4, 4);
+    const int margin = r2 ? 6 : 4;   // k_post_r2: 116-column stride, 6-column margin
+    const long long chi = tile_col_hi(a.N, gx * (t / 64), r2 ? kR2Stride : 120, margin);
+    const long long clo = 1 - margin;
     if (!sp.any || chi < 0) return PGMG_OK;
     if (a.pre_fired != nullptr) {   // RECOMP: f rows i_begin - 1 .. last + 1, phi not read
-        PGMG_SPAN(a.f, a.P, sp.r0 - 1, sp.r1 + 1, -3, chi, "k_post f (recompute)");
+        PGMG_SPAN(a.f, a.P, sp.r0 - 1, sp.r1 + 1, clo, chi, "k_post f (recompute)");
     } else {
-        PGMG_SPAN(a.phi, a.P, sp.r0, sp.r1, -3, chi, "k_post phi");
-        if (f_read) PGMG_SPAN(a.f, a.P, sp.r0, sp.r1, -3, chi, "k_post f");
+        PGMG_SPAN(a.phi, a.P, sp.r0, sp.r1, clo, chi, "k_post phi");
+        if (f_read) PGMG_SPAN(a.f, a.P, sp.r0, sp.r1, clo, chi, "k_post f");
     }
-    PGMG_SPAN(a.ec, a.Pc, fdiv2(sp.r0), fdiv2(sp.r1 + 1 - 4) + 2, -2, fdiv2(chi - 2) + 1,
+    PGMG_SPAN(a.ec, a.Pc, fdiv2(sp.r0), fdiv2(sp.r1 + 1 - 4) + 2, fdiv2(clo - 1), fdiv2(chi - 2) + 1,
               "k_post coarse correction");
     const int olo = std::max(2 * a.jc0, a.row_lo), ohi = std::min(2 * a.jc1, a.row_hi);
     if (a.x2 != nullptr) PGMG_SPAN(a.x2, a.Po != 0 ? a.Po : a.P, olo, ohi - 1, 1, a.N - 1, "k_post x2");
@@ -1431,6 +1516,25 @@ int launch_post(const PostArgsT<T> &a0, bool fine, hipStream_t s)
     else if (rec) k_post<T, false, 2, true><<<g, b, 0, s>>>(a);
     else if (a.gfx != nullptr) k_post<T, false, 2, false, true><<<g, b, 0, s>>>(a);
     else k_post<T, false, 2, false><<<g, b, 0, s>>>(a);
+    return PGMG_OK;
+}
+
+template <class T>
+int launch_post_r2(const PostArgsT<T> &a0, hipStream_t s)
+{
+    int t, gx, gy, r;
+    fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, kR2Stride);
+    if (a0.r2out == nullptr || a0.pre_fired != nullptr || a0.Po != 0 || a0.Nr2 < 3 ||
+        4 * (a0.Nr2 - 1) != a0.N - 1)
+        return PGMG_ERR_ARG;
+    if (const int e = post_spans(a0, t, gx, r, a0.gfx == nullptr, true)) return e;
+    PGMG_SPAN(a0.r2out, a0.Pr2, 1, a0.Nr2 - 2, 1, a0.Nr2 - 2, "k_post_r2 level-2 restriction");
+    PostArgsT<T> a = a0;
+    a.rows_per_block = r;
+    a.nt = 4;
+    const dim3 g(gx, gy), b(t);
+    if (a.gfx != nullptr) k_post_r2<T, true><<<g, b, 0, s>>>(a);
+    else k_post_r2<T, false><<<g, b, 0, s>>>(a);
     return PGMG_OK;
 }
 
@@ -1925,6 +2029,7 @@ void launch_post_fixup(const FixArgsF &a, const PostArgsT<T> &p, hipStream_t s)
     template int launch_pre1<T>(const PreArgsT<T> &, bool, hipStream_t);                            \
     template int launch_post1<T>(const PostArgsT<T> &, hipStream_t);                            \
     template int launch_post<T>(const PostArgsT<T> &, bool, hipStream_t);                       \
+    template int launch_post_r2<T>(const PostArgsT<T> &, hipStream_t);                          \
     template int launch_postpre<T>(const PostPreArgsT<T> &, hipStream_t);                       \
     template int launch_smooth4<T>(const PostPreArgsT<T> &, hipStream_t);                        \
     template void launch_smooth4_finish<T>(const PostPreArgsT<T> &, int, const double *, double, \

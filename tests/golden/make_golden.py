@@ -55,7 +55,7 @@ CASES = [
 # used at N = 32769, where the reference needs more host memory than the build container
 # has.  Kind G = FMG start + W-cycles (BASELINE config 5): cycle 1 an F-cycle, then W.
 BIG = [("V", 16385, 30, "ref"),     # every cycle count the bench can time (warmup + steps)
-       ("F", 16385, 2, "ref"),
+       ("F", 16385, 22, "ref"),     # bench.py --cycle F: warmup 2 + steps 20
        ("G", 16385, 2, "ref"),
        ("V", 32769, 6, "port"),     # BASELINE config 4's grid (the bench times 1 + 5 cycles)
        ("G", 32769, 2, "port")]     # BASELINE config 5's grid

@@ -26,8 +26,11 @@ def _run(pgmg, N, calls, flags=0, phi0=None, f=None, **cfg):
 
 @pytest.mark.parametrize("N,calls", [(129, [("F", 1)]), (129, [("F", 3)]), (1025, [("F", 2)]),
                                      (4097, [("F", 1), ("F", 2)]), (2049, [("V", 3), ("F", 2), ("V", 2)]),
-                                     (513, [("F", 1), ("W", 1), ("F", 1)])])
+                                     (513, [("F", 1), ("W", 1), ("F", 1)]), (257, [("F", 3)]),
+                                     (2049, [("F", 4)]), (16385, [("F", 3)])])
 def test_fspec_equals_in_stream(pgmg, N, calls):
+    """Consecutive F-cycles of one call also exercise k_post_r2 (the finest k_post forming the
+    next F-cycle's level-2 restriction, N >= 257) and its fix-up columns (i2 = 30, 60, ...)."""
     got, st, info = _run(pgmg, N, calls)
     want, st_x, _ = _run(pgmg, N, calls, flags=pgmg.PGMG_FLAG_EXACT_DIST)
     assert_bitwise(got, want, f"N={N} calls={calls}")
@@ -43,6 +46,20 @@ def test_fspec_golden_16385(pgmg, oracle_mod, golden_cycles):
         s.fcycle(2)
         assert oracle_mod.fnv_hash(s.solution()) == case["cycles"][1]["hash"]
         assert s.stats()[0] == case["cycles"][1]["sweeps"]
+        assert s.dist_info()[1] == 0
+
+
+def test_fspec_bench_shape_16385(pgmg, oracle_mod, golden_cycles):
+    """bench.py --cycle F's shape (2 + 20 F-cycles in two calls, k_post_r2 between consecutive
+    F-cycles) against the reference's 22 F-cycles (tests/golden/big_logs/F16385.txt)."""
+    case = next(c for c in golden_cycles if c["kind"] == "F" and c["N"] == 16385)
+    assert len(case["cycles"]) >= 22
+    with pgmg.Solver(16385) as s:
+        s.set_problem()
+        s.fcycle(2)
+        s.fcycle(20)
+        assert oracle_mod.fnv_hash(s.solution()) == case["cycles"][21]["hash"]
+        assert s.stats()[0] == case["cycles"][21]["sweeps"]
         assert s.dist_info()[1] == 0
 
 
