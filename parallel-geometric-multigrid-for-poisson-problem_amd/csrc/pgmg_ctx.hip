@@ -568,7 +568,7 @@ static int enqueue_fused_level(pgmg_ctx *c, int l, int gamma, bool x0_zero, bool
     // level 2 (the next F-cycle's first restriction step; only when its check is recorded
     // "does not fire", so x2 is the result); its 116-column tiles write more partials
     const bool r2 = fine && mode == 0 && c->fr2_want && !dist && !recomp && po.Po == 0 &&
-                    c->nb >= 2 && !is_dist(c, 1);
+                    c->nb >= 2 && !is_dist(c, 1) && tuning_int("PGMG_F_R2", 1) != 0;
     if (r2) fa.np = post_r2_blocks(L.N, po.jc0, po.jc1);
     lp = chk_log(c, fa.np, l, mode);
     if (lp) po.partials = lp;

@@ -566,6 +566,7 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
     T w0 = T(0), w1 = T(0);
     const int i1 = (k.c + 1) >> 1, i2 = i1 >> 1;
     const bool lane63 = (threadIdx.x & 63) == 63;
+    const bool eall = R2 && (a.nt & 8) != 0;   // every lane loads its east coarse column
     const bool r2col = R2 && (i1 & 1) == 0 && k.own && i2 >= 1 && i2 <= a.Nr2 - 2;
     if (RECOMP && !idle) {
         const V2<T> fm = ldv(F + (i_begin - 1) * P);
@@ -585,7 +586,7 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
     #pragma unroll
     for (int q = 0; q <= PAIRS; ++q) {
         ncr[q] = idle ? T(0) : E[(long long)((i_begin >> 1) + q) * Pc];
-        if (R2) ncre[q] = idle || !lane63 ? T(0) : E[(long long)((i_begin >> 1) + q) * Pc + 1];
+        if (R2) ncre[q] = idle || !(lane63 || eall) ? T(0) : E[(long long)((i_begin >> 1) + q) * Pc + 1];
     }
     // FULL: as in pre_body (rows interior to the band, the sum range and the grid; interior
     // wave columns)
@@ -615,7 +616,7 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
             #pragma unroll
             for (int q = 0; q <= PAIRS; ++q) {
                 ncr[q] = E[(long long)(((i + R) >> 1) + q) * Pc];
-                if (R2 && lane63) ncre[q] = E[(long long)(((i + R) >> 1) + q) * Pc + 1];
+                if (R2 && (lane63 || eall)) ncre[q] = E[(long long)(((i + R) >> 1) + q) * Pc + 1];
             }
         }
         T crn[PAIRS + 1];
@@ -623,7 +624,7 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
         for (int q = 0; q <= PAIRS; ++q) {
             crn[q] = dpp_shl(cr[q]);
             // R2: lane 63's own east column, so x_eff is valid on all 128 columns of the tile
-            if (R2 && lane63) crn[q] = cre[q];
+            if (R2 && (lane63 || eall)) crn[q] = cre[q];
         }
         double gy[R];   // GENF row factors of the iteration, loaded together up front
         if constexpr (GENF) {
@@ -1531,7 +1532,7 @@ int launch_post_r2(const PostArgsT<T> &a0, hipStream_t s)
     PGMG_SPAN(a0.r2out, a0.Pr2, 1, a0.Nr2 - 2, 1, a0.Nr2 - 2, "k_post_r2 level-2 restriction");
     PostArgsT<T> a = a0;
     a.rows_per_block = r;
-    a.nt = 4;
+    a.nt = 4 | (tuning_int("PGMG_R2_EALL", 0) ? 8 : 0);
     const dim3 g(gx, gy), b(t);
     if (a.gfx != nullptr) k_post_r2<T, true><<<g, b, 0, s>>>(a);
     else k_post_r2<T, false><<<g, b, 0, s>>>(a);

@@ -26,17 +26,17 @@ def child(a):
     out = {}
     for spec in a.grids.split(","):
         kind, n = spec[0], int(spec[1:])
-        steps = a.steps if kind == "V" else max(1, a.steps // 10)
+        steps = a.steps if kind in ("V", "F") else max(1, a.steps // 10)
         ts = []
         flags = int(os.environ.get("AB_FLAGS", "0"))   # pgmg_config.flags of the variant
         kw = {"flags": flags} if flags else {}
         if os.environ.get("AB_TAIL_N"):                # pgmg_config.tail_n of the variant
             kw["tail_n"] = int(os.environ["AB_TAIL_N"])
         with pg.Solver(n, **kw) as s:
-            run = s.vcycle if kind == "V" else s.wcycle
+            run = {"V": s.vcycle, "W": s.wcycle, "F": s.fcycle}[kind]
             for _ in range(3):
                 s.set_problem()
-                run(3 if kind == "V" else 1)
+                run({"V": 3, "W": 1, "F": 2}[kind])
                 s.sync()
                 t0 = time.perf_counter()
                 run(steps)
