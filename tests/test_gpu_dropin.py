@@ -193,7 +193,7 @@ def test_fcycle_on_bound_problem(pgmg, foreign):
     sequence on a host problem, and pgmg_get_solution / the hash read the bound result."""
     import torch
     N = 513
-    seq = [("V", 1), ("F", 1), ("V", 2), ("F", 1)]
+    seq = [("V", 1), ("F", 1), ("V", 2), ("F", 1), ("F", 3)]   # F x 3: k_post_r2 between them
     with pgmg.Solver(N, cross_min_n=33) as s:
         s.set_problem()
         for k, n in seq:
