@@ -18,6 +18,8 @@ sys.path.insert(0, str(ROOT))
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=16385)
 ap.add_argument("--rounds", type=int, default=3)
+ap.add_argument("--restrict-prolong", action="store_true",
+                help="time restriction and prolongation instead (PGMG_OPRS_U, PGMG_OPP_U)")
 args = ap.parse_args()
 
 import torch  # noqa: E402
@@ -32,8 +34,15 @@ pg.ops.rhs(f, h)
 r = torch.empty_like(x)
 tmp = torch.empty_like(x)
 fine = float(n - 2) ** 2
-variants = [{}, {"PGMG_OPR_U": 16}, {"PGMG_OPR_U": 16, "PGMG_OPR_BLOCKS": 2048},
+nc = (n - 1) // 2 + 1
+coarse = float(nc - 2) ** 2
+c = torch.zeros((nc, nc), dtype=torch.float64, device="cuda:0")
+e = torch.zeros((nc, nc), dtype=torch.float64, device="cuda:0")
+variants = [{}, {"PGMG_OPR_U": 8}, {"PGMG_OPR_U": 16, "PGMG_OPR_BLOCKS": 2048},
             {"PGMG_OPC_U": 16}, {"PGMG_OPC_U": 16, "PGMG_OPC_BLOCKS": 1024}]
+if args.restrict_prolong:
+    variants = [{}, {"PGMG_OPP_U": 4}, {"PGMG_OPP_U": 4, "PGMG_OPP_BLOCKS": 2048},
+                {"PGMG_OPRS_U": 8}, {"PGMG_OPRS_U": 8, "PGMG_OPRS_BLOCKS": 2048}]
 keys = sorted({k for v in variants for k in v})
 
 
@@ -56,6 +65,15 @@ for rnd in range(args.rounds):
             os.environ.pop(k, None)
         for k, v in var.items():
             os.environ[k] = str(v)
+        if args.restrict_prolong:
+            ms_rs = timed(lambda: pg.ops.restrict(r, c))
+            ms_p = timed(lambda: pg.ops.prolong(e, r, mode=pg.PGMG_PROLONG_SYMMETRIC, num_thread=32))
+            print(json.dumps({"variant": var or "base", "round": rnd, "restrict_ms": round(ms_rs, 4),
+                              "restrict_frac": round((8 * fine + 8 * coarse) / ms_rs / 1e9 / 8.0, 4),
+                              "prolong_ms": round(ms_p, 4),
+                              "prolong_frac": round((16 * fine + 8 * coarse) / ms_p / 1e9 / 8.0, 4)}),
+                  flush=True)
+            continue
         ms_r = timed(lambda: pg.ops.residual(r, x, f, h))
         ms_j = timed(lambda: pg.ops.jacobi(x, f, h, 0, eps=-1.0, tmp=tmp))
         print(json.dumps({"variant": var or "base", "round": rnd, "residual_ms": round(ms_r, 4),
