@@ -50,3 +50,14 @@ def test_gpus_more_than_devices_fails():
     assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
     assert "needs 2 GPUs" in r.stderr
     assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_bench_options_listed():
+    """The options the driver's runs and DESIGN.md name exist (a rename would silently fall
+    back to argparse's prefix matching or fail only on the GPU box)."""
+    r = subprocess.run([sys.executable, BENCH, "--help"], capture_output=True, text=True,
+                       timeout=120, env=_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    for opt in ("--gpus", "--steps", "--warmup", "--big-grid", "--other-configs", "--cycle",
+                "--save-profiles", "--trace", "--pmc", "--cpu-baseline", "--ops"):
+        assert opt in r.stdout, opt
