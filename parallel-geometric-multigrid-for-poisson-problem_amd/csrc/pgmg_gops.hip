@@ -684,12 +684,13 @@ __global__ __launch_bounds__(kBlock) void k_op_restrict(const double *__restrict
 
 void launch_g_restrict(const double *fine, double *coarse, int Nf, int Nc, hipStream_t s)
 {
-    // coarse rows of loads in flight: 4 (PGMG_OPRS_U = 8 in the measurement build)
-    if (tuning_int("PGMG_OPRS_U", 4) == 8) {
-        const OpGeom g = op_geom(Nc - 2, Nc - 2, 8, tuning_int("PGMG_OPRS_BLOCKS", kOpTarget));
-        k_op_restrict<8><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(fine, coarse, Nf, Nc, g.rpb);
+#ifdef PGMG_TUNING
+    if (tuning_int("PGMG_OPRS_U", 4) == 8) {   // measurement build: 8 coarse rows in flight
+        const OpGeom g8 = op_geom(Nc - 2, Nc - 2, 8, tuning_int("PGMG_OPRS_BLOCKS", kOpTarget));
+        k_op_restrict<8><<<dim3(g8.gx, g8.gy), kBlock, 0, s>>>(fine, coarse, Nf, Nc, g8.rpb);
         return;
     }
+#endif
     const OpGeom g = op_geom(Nc - 2, Nc - 2, 4, tuning_int("PGMG_OPRS_BLOCKS", kOpTarget));
     k_op_restrict<4><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(fine, coarse, Nf, Nc, g.rpb);
 }
@@ -711,8 +712,95 @@ void launch_g_restrict(const double *fine, double *coarse, int Nf, int Nc, hipSt
 //          form): the fine boundary := 0, every interior point (rows / columns 1 .. Nf-2)
 //          Fn += v with the same four cases.
 // ---------------------------------------------------------------------------
-template <int MODE, int U>
+template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_op_prolong(const double *__restrict__ C,
+                                                       double *__restrict__ Fn, int Nc, int Nf,
+                                                       int ext, int rpb)
+{
+    const int lane = threadIdx.x & 63;
+    const int t_raw = blockIdx.x * kBlock + threadIdx.x;
+    const bool act = t_raw < Nc;
+    const int ic = act ? t_raw : Nc - 1;
+    const int E = ext < Nf ? ext : Nf;
+    const int x0 = 2 * ic, x1 = 2 * ic + 1;
+    const bool has1 = x1 < Nf;                        // the last coarse column has no odd fine
+    const bool ld_n = (lane == 63 || ic == Nc - 1) ? false : false;
+    (void)ld_n;
+    const long long Wf = Nf, Wc = Nc;
+    // fine rows [yb, ye) of this band, in whole pairs starting at an even row
+    const int yb = 2 * (blockIdx.y * rpb);
+    const int ye = min(yb + 2 * rpb, Nf);
+    // coarse row jc = yb / 2 and its right neighbour column
+    const bool nxt_ok = ic + 1 < Nc;
+    double c0 = C[(long long)(yb >> 1) * Wc + ic];
+    double c0n = (lane == 63 && nxt_ok) ? C[(long long)(yb >> 1) * Wc + ic + 1] : 0.0;
+    for (int y = yb; y < ye; y += 2) {
+        const int jc = y >> 1;
+        const bool has_c1 = jc + 1 < Nc;
+        const double c1 = has_c1 ? C[(long long)(jc + 1) * Wc + ic] : 0.0;
+        const double c1n = (lane == 63 && nxt_ok && has_c1) ? C[(long long)(jc + 1) * Wc + ic + 1] : 0.0;
+        double *p0 = Fn + (long long)y * Wf + x0;
+        double *p1 = p0 + Wf;
+        const bool row1 = y + 1 < ye;
+        double2 f0, f1;
+        if (has1) {
+            f0 = ldvu<double>(p0);
+            f1 = row1 ? ldvu<double>(p1) : f0;
+        } else {
+            f0.x = p0[0];
+            f0.y = 0.0;
+            f1.x = row1 ? p1[0] : 0.0;
+            f1.y = 0.0;
+        }
+        // next coarse column by DPP (lane 63: its own load)
+        double a_n = dpp_shl(c0), b_n = dpp_shl(c1);
+        if (lane == 63) {
+            a_n = c0n;
+            b_n = c1n;
+        }
+        // even fine row y: (y, x0) = c0; (y, x1) = 0.5*(c0 + a_n)
+        // odd fine row y+1: (y+1, x0) = 0.5*(c0 + c1); (y+1, x1) = 0.25*(c0 + a_n + c1 + b_n)
+        const double v00 = c0;
+        const double v01 = 0.5 * (c0 + a_n);
+        const double v10 = 0.5 * (c0 + c1);
+        const double v11 = 0.25 * (c0 + a_n + c1 + b_n);
+        double2 o0 = f0, o1 = f1;
+        if (MODE == 0) {
+            // rows / columns 2 .. Nf-2
+            const bool cx0 = x0 >= 2 && x0 <= Nf - 2, cx1 = x1 >= 2 && x1 <= Nf - 2;
+            const bool ry0 = y >= 2 && y <= Nf - 2, ry1 = y + 1 >= 2 && y + 1 <= Nf - 2;
+            if (ry0 && cx0) o0.x = f0.x + v00;
+            if (ry0 && cx1) o0.y = f0.y + v01;
+            if (ry1 && cx0) o1.x = f1.x + v10;
+            if (ry1 && cx1) o1.y = f1.y + v11;
+        } else {
+            const bool b0 = x0 == 0 || x0 == Nf - 1, b1 = x1 == Nf - 1;
+            const bool yb0 = y == 0 || y == Nf - 1, yb1 = y + 1 == Nf - 1;
+            o0.x = (yb0 || b0) ? 0.0 : f0.x + v00;
+            o0.y = (yb0 || b1) ? 0.0 : f0.y + v01;
+            o1.x = (yb1 || b0) ? 0.0 : f1.x + v10;
+            o1.y = (yb1 || b1) ? 0.0 : f1.y + v11;
+        }
+        // write only the points inside the reference's launch extent
+        if (act && y < E) {
+            if (has1 && x1 < E) stvu<double>(p0, o0);
+            else if (x0 < E) p0[0] = o0.x;
+        }
+        if (act && row1 && y + 1 < E) {
+            if (has1 && x1 < E) stvu<double>(p1, o1);
+            else if (x0 < E) p1[0] = o1.x;
+        }
+        c0 = c1;
+        c0n = c1n;
+    }
+}
+
+#ifdef PGMG_TUNING
+// Measurement build only (PGMG_OPP_U = 4): the prolongation with U fine row pairs of loads in
+// flight per step (every load of a step issued before the first is used); the same expressions
+// as k_op_prolong, one row pair per step there
+template <int MODE, int U>
+__global__ __launch_bounds__(kBlock) void k_op_prolong_u(const double *__restrict__ C,
                                                        double *__restrict__ Fn, int Nc, int Nf,
                                                        int ext, int rpb)
 {
@@ -807,22 +895,25 @@ __global__ __launch_bounds__(kBlock) void k_op_prolong(const double *__restrict_
         }
     }
 }
+#endif
 
 void launch_g_prolong(const double *coarse, double *fine, int Nc, int Nf, int mode, int ext,
                       hipStream_t s)
 {
-    // one band = rpb coarse rows = 2 rpb fine rows; U row pairs of loads in flight
-    // (PGMG_OPP_U: 1 or 4 in the measurement build)
-    const int u = tuning_int("PGMG_OPP_U", 1) == 4 ? 4 : 1;
-    const OpGeom g = op_geom(Nc, (Nf + 1) / 2, u, tuning_int("PGMG_OPP_BLOCKS", kOpTarget));
-    const dim3 grid(g.gx, g.gy);
-    if (u == 4) {
-        if (mode == 1) k_op_prolong<1, 4><<<grid, kBlock, 0, s>>>(coarse, fine, Nc, Nf, ext, g.rpb);
-        else k_op_prolong<0, 4><<<grid, kBlock, 0, s>>>(coarse, fine, Nc, Nf, ext, g.rpb);
-    } else {
-        if (mode == 1) k_op_prolong<1, 1><<<grid, kBlock, 0, s>>>(coarse, fine, Nc, Nf, ext, g.rpb);
-        else k_op_prolong<0, 1><<<grid, kBlock, 0, s>>>(coarse, fine, Nc, Nf, ext, g.rpb);
+    // one band = rpb coarse rows = 2 rpb fine rows
+#ifdef PGMG_TUNING
+    if (tuning_int("PGMG_OPP_U", 1) == 4) {
+        const OpGeom g4 = op_geom(Nc, (Nf + 1) / 2, 4, tuning_int("PGMG_OPP_BLOCKS", kOpTarget));
+        const dim3 grid4(g4.gx, g4.gy);
+        if (mode == 1) k_op_prolong_u<1, 4><<<grid4, kBlock, 0, s>>>(coarse, fine, Nc, Nf, ext, g4.rpb);
+        else k_op_prolong_u<0, 4><<<grid4, kBlock, 0, s>>>(coarse, fine, Nc, Nf, ext, g4.rpb);
+        return;
     }
+#endif
+    const OpGeom g = op_geom(Nc, (Nf + 1) / 2, 1, tuning_int("PGMG_OPP_BLOCKS", kOpTarget));
+    const dim3 grid(g.gx, g.gy);
+    if (mode == 1) k_op_prolong<1><<<grid, kBlock, 0, s>>>(coarse, fine, Nc, Nf, ext, g.rpb);
+    else k_op_prolong<0><<<grid, kBlock, 0, s>>>(coarse, fine, Nc, Nf, ext, g.rpb);
 }
 
 // ---------------------------------------------------------------------------
