@@ -684,15 +684,16 @@ __global__ __launch_bounds__(kBlock) void k_op_restrict(const double *__restrict
 
 void launch_g_restrict(const double *fine, double *coarse, int Nf, int Nc, hipStream_t s)
 {
-#ifdef PGMG_TUNING
-    if (tuning_int("PGMG_OPRS_U", 4) == 8) {   // measurement build: 8 coarse rows in flight
-        const OpGeom g8 = op_geom(Nc - 2, Nc - 2, 8, tuning_int("PGMG_OPRS_BLOCKS", kOpTarget));
-        k_op_restrict<8><<<dim3(g8.gx, g8.gy), kBlock, 0, s>>>(fine, coarse, Nf, Nc, g8.rpb);
+    // 8 coarse rows of loads in flight (r04, scripts/op_ru_ab.py --restrict-prolong,
+    // profiles/r04_ops/op_rp.jsonl: 0.561-0.566 ms against 0.573-0.577 for 4, 3 interleaved
+    // rounds; PGMG_OPRS_U = 4 in the measurement build for the old form)
+    if (tuning_int("PGMG_OPRS_U", 8) == 4) {
+        const OpGeom g4 = op_geom(Nc - 2, Nc - 2, 4, tuning_int("PGMG_OPRS_BLOCKS", kOpTarget));
+        k_op_restrict<4><<<dim3(g4.gx, g4.gy), kBlock, 0, s>>>(fine, coarse, Nf, Nc, g4.rpb);
         return;
     }
-#endif
-    const OpGeom g = op_geom(Nc - 2, Nc - 2, 4, tuning_int("PGMG_OPRS_BLOCKS", kOpTarget));
-    k_op_restrict<4><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(fine, coarse, Nf, Nc, g.rpb);
+    const OpGeom g = op_geom(Nc - 2, Nc - 2, 8, tuning_int("PGMG_OPRS_BLOCKS", kOpTarget));
+    k_op_restrict<8><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(fine, coarse, Nf, Nc, g.rpb);
 }
 
 // ---------------------------------------------------------------------------
@@ -795,121 +796,12 @@ __global__ __launch_bounds__(kBlock) void k_op_prolong(const double *__restrict_
     }
 }
 
-#ifdef PGMG_TUNING
-// Measurement build only (PGMG_OPP_U = 4): the prolongation with U fine row pairs of loads in
-// flight per step (every load of a step issued before the first is used); the same expressions
-// as k_op_prolong, one row pair per step there
-template <int MODE, int U>
-__global__ __launch_bounds__(kBlock) void k_op_prolong_u(const double *__restrict__ C,
-                                                       double *__restrict__ Fn, int Nc, int Nf,
-                                                       int ext, int rpb)
-{
-    const int lane = threadIdx.x & 63;
-    const int t_raw = blockIdx.x * kBlock + threadIdx.x;
-    const bool act = t_raw < Nc;
-    const int ic = act ? t_raw : Nc - 1;
-    const int E = ext < Nf ? ext : Nf;
-    const int x0 = 2 * ic, x1 = 2 * ic + 1;
-    const bool has1 = x1 < Nf;                        // the last coarse column has no odd fine
-    const long long Wf = Nf, Wc = Nc;
-    // fine rows [yb, ye) of this band, in whole pairs starting at an even row
-    const int yb = 2 * (blockIdx.y * rpb);
-    const int ye = min(yb + 2 * rpb, Nf);
-    // coarse row jc = yb / 2 and its right neighbour column
-    const bool nxt_ok = ic + 1 < Nc;
-    double c0 = C[(long long)(yb >> 1) * Wc + ic];
-    double c0n = (lane == 63 && nxt_ok) ? C[(long long)(yb >> 1) * Wc + ic + 1] : 0.0;
-    // U fine row pairs per step, every load of the step issued before the first is used
-    for (int y = yb; y < ye; y += 2 * U) {
-        double cn[U], cnn[U];
-        double2 fa[U], fb[U];
-        #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int yy = min(y + 2 * u, ye - 1);     // (past the band: a row re-read, unused)
-            const int jc = yy >> 1;
-            const bool has_c1 = jc + 1 < Nc;
-            const int yr = min(yy + 1, ye - 1);
-            cn[u] = has_c1 ? C[(long long)(jc + 1) * Wc + ic] : 0.0;
-            cnn[u] = (lane == 63 && nxt_ok && has_c1) ? C[(long long)(jc + 1) * Wc + ic + 1] : 0.0;
-            const double *p0 = Fn + (long long)yy * Wf + x0;
-            const double *p1 = Fn + (long long)yr * Wf + x0;
-            if (has1) {
-                fa[u] = ldvu<double>(p0);
-                fb[u] = ldvu<double>(p1);
-            } else {
-                fa[u].x = p0[0];
-                fa[u].y = 0.0;
-                fb[u].x = p1[0];
-                fb[u].y = 0.0;
-            }
-        }
-        #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int yy = y + 2 * u;
-            if (yy >= ye) break;   // wave-uniform
-            const double c1 = cn[u], c1n = cnn[u];
-            const bool row1 = yy + 1 < ye;
-            const double2 f0 = fa[u], f1 = row1 ? fb[u] : fa[u];
-            double *p0 = Fn + (long long)yy * Wf + x0;
-            double *p1 = p0 + Wf;
-            // next coarse column by DPP (lane 63: its own load)
-            double a_n = dpp_shl(c0), b_n = dpp_shl(c1);
-            if (lane == 63) {
-                a_n = c0n;
-                b_n = c1n;
-            }
-            // even fine row y: (y, x0) = c0; (y, x1) = 0.5*(c0 + a_n)
-            // odd fine row y+1: (y+1, x0) = 0.5*(c0 + c1); (y+1, x1) = 0.25*(c0 + a_n + c1 + b_n)
-            const double v00 = c0;
-            const double v01 = 0.5 * (c0 + a_n);
-            const double v10 = 0.5 * (c0 + c1);
-            const double v11 = 0.25 * (c0 + a_n + c1 + b_n);
-            double2 o0 = f0, o1 = f1;
-            if (MODE == 0) {
-                // rows / columns 2 .. Nf-2
-                const bool cx0 = x0 >= 2 && x0 <= Nf - 2, cx1 = x1 >= 2 && x1 <= Nf - 2;
-                const bool ry0 = yy >= 2 && yy <= Nf - 2, ry1 = yy + 1 >= 2 && yy + 1 <= Nf - 2;
-                if (ry0 && cx0) o0.x = f0.x + v00;
-                if (ry0 && cx1) o0.y = f0.y + v01;
-                if (ry1 && cx0) o1.x = f1.x + v10;
-                if (ry1 && cx1) o1.y = f1.y + v11;
-            } else {
-                const bool b0 = x0 == 0 || x0 == Nf - 1, b1 = x1 == Nf - 1;
-                const bool yb0 = yy == 0 || yy == Nf - 1, yb1 = yy + 1 == Nf - 1;
-                o0.x = (yb0 || b0) ? 0.0 : f0.x + v00;
-                o0.y = (yb0 || b1) ? 0.0 : f0.y + v01;
-                o1.x = (yb1 || b0) ? 0.0 : f1.x + v10;
-                o1.y = (yb1 || b1) ? 0.0 : f1.y + v11;
-            }
-            // write only the points inside the reference's launch extent
-            if (act && yy < E) {
-                if (has1 && x1 < E) stvu<double>(p0, o0);
-                else if (x0 < E) p0[0] = o0.x;
-            }
-            if (act && row1 && yy + 1 < E) {
-                if (has1 && x1 < E) stvu<double>(p1, o1);
-                else if (x0 < E) p1[0] = o1.x;
-            }
-            c0 = c1;
-            c0n = c1n;
-        }
-    }
-}
-#endif
-
 void launch_g_prolong(const double *coarse, double *fine, int Nc, int Nf, int mode, int ext,
                       hipStream_t s)
 {
     // one band = rpb coarse rows = 2 rpb fine rows
-#ifdef PGMG_TUNING
-    if (tuning_int("PGMG_OPP_U", 1) == 4) {
-        const OpGeom g4 = op_geom(Nc, (Nf + 1) / 2, 4, tuning_int("PGMG_OPP_BLOCKS", kOpTarget));
-        const dim3 grid4(g4.gx, g4.gy);
-        if (mode == 1) k_op_prolong_u<1, 4><<<grid4, kBlock, 0, s>>>(coarse, fine, Nc, Nf, ext, g4.rpb);
-        else k_op_prolong_u<0, 4><<<grid4, kBlock, 0, s>>>(coarse, fine, Nc, Nf, ext, g4.rpb);
-        return;
-    }
-#endif
+    // (r04: 4 row pairs of loads in flight per step measured slower, 1.07-1.09 ms against
+    // 1.006-1.016, profiles/r04_ops/op_rp.jsonl)
     const OpGeom g = op_geom(Nc, (Nf + 1) / 2, 1, tuning_int("PGMG_OPP_BLOCKS", kOpTarget));
     const dim3 grid(g.gx, g.gy);
     if (mode == 1) k_op_prolong<1><<<grid, kBlock, 0, s>>>(coarse, fine, Nc, Nf, ext, g.rpb);
