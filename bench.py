@@ -49,6 +49,7 @@ ROOT = pathlib.Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
+TRACE_PREWARM = 4         # pre-warm calls before the kernel-trace child's timed call
 METRIC = "V-cycles/sec + fine-grid stencil HBM GB/s, 2D Poisson N=16384², fp64"
 # rocprofv3 FETCH_SIZE/WRITE_SIZE of the finest-level passes (scripts/pmc_summary.py); the
 # profile names the build it was measured on
@@ -297,11 +298,13 @@ def trace_child(args):
     pg = _pkgload.load()
     with pg.Solver(args.n, dtype=args.dtype) as s:
         run = {"V": s.vcycle, "W": s.wcycle, "F": s.fcycle}[args.cycle]
-        # a pre-warm call (clocks ramp up on a GPU that sat idle during the CPU baselines),
-        # then the timed call's shape: a fresh problem, warmup cycles, `steps` cycles
-        s.set_problem()
-        run(args.steps)
-        s.sync()
+        # TRACE_PREWARM pre-warm calls (clocks ramp up on a GPU that sat idle during the CPU
+        # baselines; one call of ~35 ms left the r04 final3 box's trace 5% slower than the
+        # event-timed run), then the timed call's shape: a fresh problem, warmup cycles, `steps`
+        for _ in range(TRACE_PREWARM):
+            s.set_problem()
+            run(args.steps)
+            s.sync()
         s.set_problem()
         run(max(args.warmup, 0))
         s.sync()
@@ -348,7 +351,7 @@ def live_trace(args):
         for row in csv.DictReader(open(files[0])):
             out[kernel_key(row["Name"])] = (int(row["Calls"]), float(row["AverageNs"]) / 1e6, None)
         # the timed call's own launches of the finest-level cross-cycle pass (steps - 1 of them,
-        # after the pre-warm call's steps - 1 and the warmup call's warmup - 1): the same
+        # after each pre-warm call's steps - 1 and the warmup call's warmup - 1): the same
         # launches the event timing averages
         traces = list(pathlib.Path(d).rglob("*kernel_trace.csv"))
         if traces and args.cycle == "V":
@@ -356,16 +359,16 @@ def live_trace(args):
             for row in csv.DictReader(open(traces[0])):
                 per.setdefault(kernel_key(row["Kernel_Name"]), []).append(
                     (int(row["Start_Timestamp"]), int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
-            skip = (args.steps - 1) + max(args.warmup - 1, 0)
+            skip = TRACE_PREWARM * (args.steps - 1) + max(args.warmup - 1, 0)
             for k, v in per.items():
                 if k.startswith("k_postpre_lds") and len(v) >= skip + args.steps - 1 > skip:
                     v.sort()
                     t = [x[1] for x in v[skip:skip + args.steps - 1]]
                     out[k] = out[k][:2] + (sum(t) / len(t) / 1e6,)
         return out, ("rocprofv3 --kernel-trace --stats of a child run of the timed call "
-                     f"({args.warmup} + {args.steps} cycles, one call each, main leg, after a "
-                     f"pre-warm call of {args.steps}) on this box; the dominant kernel's time "
-                     f"is the mean over the timed call's own launches")
+                     f"({args.warmup} + {args.steps} cycles, one call each, main leg, after "
+                     f"{TRACE_PREWARM} pre-warm calls of {args.steps}) on this box; the dominant "
+                     f"kernel's time is the mean over the timed call's own launches")
     except (subprocess.SubprocessError, OSError, KeyError, ValueError) as e:
         return None, f"rocprofv3 --kernel-trace failed: {e}"
     finally:
