@@ -349,22 +349,23 @@ def live_trace(args):
         _keep_profile(args, files[0], "trace_kernel_stats.csv")
         out = {}
         for row in csv.DictReader(open(files[0])):
-            out[kernel_key(row["Name"])] = (int(row["Calls"]), float(row["AverageNs"]) / 1e6, None)
-        # the timed call's own launches of the finest-level cross-cycle pass (steps - 1 of them,
-        # after each pre-warm call's steps - 1 and the warmup call's warmup - 1): the same
-        # launches the event timing averages
+            out[kernel_key(row["Name"])] = (int(row["Calls"]), float(row["AverageNs"]) / 1e6, None, None)
+        # the timed call's own launches of the finest-level cross-cycle pass: the last steps - 1
+        # in start order (the timed call is the child's last; the fresh-problem calls before it
+        # launch fewer, their early check cycles being unfused): the launches the event timing
+        # averages
         traces = list(pathlib.Path(d).rglob("*kernel_trace.csv"))
         if traces and args.cycle == "V":
             per = {}
             for row in csv.DictReader(open(traces[0])):
                 per.setdefault(kernel_key(row["Kernel_Name"]), []).append(
                     (int(row["Start_Timestamp"]), int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
-            skip = TRACE_PREWARM * (args.steps - 1) + max(args.warmup - 1, 0)
+            last = args.steps - 1
             for k, v in per.items():
-                if k.startswith("k_postpre_lds") and len(v) >= skip + args.steps - 1 > skip:
+                if k.startswith("k_postpre_lds") and last > 0 and len(v) > last:
                     v.sort()
-                    t = [x[1] for x in v[skip:skip + args.steps - 1]]
-                    out[k] = out[k][:2] + (sum(t) / len(t) / 1e6,)
+                    t = [x[1] for x in v[-last:]]
+                    out[k] = out[k][:2] + (sum(t) / len(t) / 1e6, len(t))
         return out, ("rocprofv3 --kernel-trace --stats of a child run of the timed call "
                      f"({args.warmup} + {args.steps} cycles, one call each, main leg, after "
                      f"{TRACE_PREWARM} pre-warm calls of {args.steps}) on this box; the dominant "
@@ -838,6 +839,7 @@ def main():
                 roof[-1].update({"ms_per_launch_rocprof": round(tms, 5),
                                  "ms_per_launch_rocprof_all_launches": round(tr[1], 5),
                                  "launches_rocprof": tr[0],
+                                 "launches_rocprof_timed": tr[3],
                                  "frac_rocprof": round(ach_r / HBM_PEAK_GBPS, 4),
                                  "event_vs_rocprof": round(ms / tms, 4),
                                  "rocprof_source": trace_note})
