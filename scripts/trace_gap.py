@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Does rocprofv3 --kernel-trace itself slow the headline call down? (r04)  Runs bench.py's
+timed-call shape (pre-warm calls, a fresh problem, warmup cycles, `steps` cycles in one call)
+and prints the call's ms per V-cycle from stream events.  Run it plain and under
+`rocprofv3 --kernel-trace -- python3 scripts/trace_gap.py` on the same box: if the traced run's
+own event time is slower by the same ~4 % as the trace's kernel durations, the gap between
+bench.py's event-timed and rocprof-timed `k_postpre_lds` is the profiler's.
+
+    python scripts/trace_gap.py [--n 16385] [--steps 20] [--warmup 2] [--prewarm 4] [--reps 3]
+"""
+import argparse
+import json
+import pathlib
+import statistics
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=16385)
+ap.add_argument("--steps", type=int, default=20)
+ap.add_argument("--warmup", type=int, default=2)
+ap.add_argument("--prewarm", type=int, default=4)
+ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--tag", default="plain")
+args = ap.parse_args()
+
+import torch  # noqa: E402
+import _pkgload  # noqa: E402
+
+pg = _pkgload.load()
+ms = []
+with pg.Solver(args.n, dtype="f64") as s:
+    for _ in range(args.prewarm):
+        s.set_problem()
+        s.vcycle(args.steps)
+        s.sync()
+    for _ in range(args.reps):
+        s.set_problem()
+        s.vcycle(max(args.warmup, 0))
+        s.sync()
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        s.vcycle(args.steps)
+        s.sync()
+        b.record()
+        b.synchronize()
+        ms.append(a.elapsed_time(b) / args.steps)
+print(json.dumps({"tag": args.tag, "n": args.n, "ms_per_cycle": [round(x, 4) for x in ms],
+                  "median": round(statistics.median(ms), 4)}), flush=True)
