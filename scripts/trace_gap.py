@@ -7,6 +7,9 @@ own event time is slower by the same ~4 % as the trace's kernel durations, the g
 bench.py's event-timed and rocprof-timed `k_postpre_lds` is the profiler's.
 
     python scripts/trace_gap.py [--n 16385] [--steps 20] [--warmup 2] [--prewarm 4] [--reps 3]
+
+--ab: instead, contexts with and without PGMG_FLAG_TIME_FINE (events between the finest
+passes) interleaved over rounds, a fresh context each time, as bench.py's legs do.
 """
 import argparse
 import json
@@ -24,12 +27,41 @@ ap.add_argument("--warmup", type=int, default=2)
 ap.add_argument("--prewarm", type=int, default=4)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--tag", default="plain")
+ap.add_argument("--ab", type=int, default=0, help="rounds of the TIME_FINE A/B")
 args = ap.parse_args()
 
 import torch  # noqa: E402
 import _pkgload  # noqa: E402
 
 pg = _pkgload.load()
+
+
+def call_ms(s):
+    s.set_problem()
+    s.vcycle(max(args.warmup, 0))
+    s.sync()
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
+    a.record()
+    s.vcycle(args.steps)
+    s.sync()
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) / args.steps
+
+
+if args.ab:
+    res = {"plain": [], "time_fine": []}
+    for rnd in range(args.ab):
+        for name, fl in (("plain", 0), ("time_fine", pg.PGMG_FLAG_TIME_FINE)):
+            with pg.Solver(args.n, dtype="f64", flags=fl) as s:
+                if rnd == 0:
+                    for _ in range(args.prewarm):
+                        call_ms(s)
+                res[name] += [round(call_ms(s), 4) for _ in range(args.reps)]
+    print(json.dumps({"n": args.n, **res, **{k + "_median": round(statistics.median(v), 4)
+                                             for k, v in res.items()}}), flush=True)
+    sys.exit(0)
 ms = []
 with pg.Solver(args.n, dtype="f64") as s:
     for _ in range(args.prewarm):
