@@ -50,6 +50,7 @@ sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 TRACE_PREWARM = 4         # pre-warm calls before the kernel-trace child's timed call
+INST_REPS = 3             # repetitions with per-pass events (the roofline's event-timed median)
 METRIC = "V-cycles/sec + fine-grid stencil HBM GB/s, 2D Poisson N=16384², fp64"
 # rocprofv3 FETCH_SIZE/WRITE_SIZE of the finest-level passes (scripts/pmc_summary.py); the
 # profile names the build it was measured on
@@ -574,12 +575,14 @@ def main():
 
     def run_leg(extra_flags, reps):
         """`reps` clean repetitions on one context (set_problem restarts each from phi0 = 0)
-        + one repetition with per-pass events on a second; returns times, parity, passes"""
+        + INST_REPS repetitions with per-pass events on a second (per pass, the median over
+        them); returns times, parity, passes"""
         out = {"times": [], "parity": [], "passes": [], "inst_dt": None}
+        inst_dt, inst_passes = [], []
         for inst in (False, True):
             s = new_solver(extra_flags | (pg.PGMG_FLAG_TIME_FINE if inst else 0))
             run = {"V": s.vcycle, "W": s.wcycle, "F": s.fcycle}[args.cycle]
-            for _ in range(1 if inst else reps):
+            for _ in range(INST_REPS if inst else reps):
                 s.set_problem()
                 run(max(args.warmup, 0))
                 s.sync()
@@ -595,8 +598,8 @@ def main():
                 t1 = time.perf_counter()
                 dt = max_over_ranks(t1 - t0)
                 if inst:
-                    out["inst_dt"] = dt
-                    out["passes"] = [(w,) + tuple(s.fine_pass_time(w)) for w in (0, 1, 2, 3)]
+                    inst_dt.append(dt)
+                    inst_passes.append([tuple(s.fine_pass_time(w)) for w in (0, 1, 2, 3)])
                     out["bytes"] = {w: s.fine_pass_bytes(w) for w in (0, 1, 2, 3)}
                 else:
                     out["times"].append(dt)
@@ -612,6 +615,10 @@ def main():
             out["gen"] = s.fused and s.fine_pass_bytes(3) < s.fine_pass_bytes(0)
             out["r2"] = world > 1 and not s.dist_info()[0]
             s.close()
+        out["inst_dt"] = statistics.median(inst_dt)
+        out["passes"] = [(w, inst_passes[0][w][0],
+                          statistics.median(r[w][1] for r in inst_passes)) for w in (0, 1, 2, 3)]
+        out["passes_reps"] = {w: [r[w][1] for r in inst_passes] for w in (0, 1, 2, 3)}
         return out
 
     main_leg = run_leg(0, max(1, args.reps))
@@ -830,7 +837,8 @@ def main():
                          "traffic_source": source if traffic else None,
                          "traffic_ratio": round(traffic / nbytes, 4) if traffic else None,
                          "bytes_per_launch": nbytes, "launches_timed": cnt,
-                         "ms_per_launch": round(ms, 5)})
+                         "ms_per_launch": round(ms, 5),
+                         "ms_per_launch_reps": [round(x, 5) for x in leg["passes_reps"][w]]})
             tr = trace.get(key) if trace is not None and not leg.get("fast") and not leg.get(
                 "stored") else None
             if tr is not None:
