@@ -10,6 +10,8 @@ bench.py's event-timed and rocprof-timed `k_postpre_lds` is the profiler's.
 
 --ab: instead, contexts with and without PGMG_FLAG_TIME_FINE (events between the finest
 passes) interleaved over rounds, a fresh context each time, as bench.py's legs do.
+--ctx K: K fresh plain contexts one after another, `reps` calls each: the spread between
+contexts against the spread within one (does the allocation a context gets set its speed?).
 """
 import argparse
 import json
@@ -28,6 +30,7 @@ ap.add_argument("--prewarm", type=int, default=4)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--tag", default="plain")
 ap.add_argument("--ab", type=int, default=0, help="rounds of the TIME_FINE A/B")
+ap.add_argument("--ctx", type=int, default=0, help="fresh contexts for the per-context spread")
 args = ap.parse_args()
 
 import torch  # noqa: E402
@@ -50,6 +53,20 @@ def call_ms(s):
     return a.elapsed_time(b) / args.steps
 
 
+if args.ctx:
+    per = []
+    with pg.Solver(args.n, dtype="f64") as s:
+        for _ in range(args.prewarm):
+            call_ms(s)
+    for k in range(args.ctx):
+        with pg.Solver(args.n, dtype="f64") as s:
+            per.append([round(call_ms(s), 4) for _ in range(args.reps)])
+        print(json.dumps({"ctx": k, "ms_per_cycle": per[-1]}), flush=True)
+    med = [statistics.median(v) for v in per]
+    print(json.dumps({"n": args.n, "ctx_medians": med, "between_pct": round(
+        100 * (max(med) - min(med)) / statistics.median(med), 2), "within_pct_max": round(
+        max(100 * (max(v) - min(v)) / statistics.median(v) for v in per), 2)}), flush=True)
+    sys.exit(0)
 if args.ab:
     res = {"plain": [], "time_fine": []}
     for rnd in range(args.ab):
