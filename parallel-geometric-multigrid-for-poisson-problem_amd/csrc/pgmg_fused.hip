@@ -1328,10 +1328,14 @@ int fused_blocks(int N, int jc0, int jc1)
 }
 
 // k_post_r2's workgroups (its 116-column tiles): the partial sums its check writes
+// k_post_r2's grid target (0: fused_geometry's default, 3072 at N = 16385 = 4 rounds of the 768
+// resident at 3 waves/SIMD); one function for the launch and the log sizing
+static int r2_target() { return tuning_int("PGMG_R2_BLOCKS", 0); }
+
 int post_r2_blocks(int N, int jc0, int jc1)
 {
     int t, gx, gy, r;
-    fused_geometry(N, jc0, jc1, &t, &gx, &gy, &r, kR2Stride);
+    fused_geometry(N, jc0, jc1, &t, &gx, &gy, &r, kR2Stride, r2_target());
     return gx * gy;
 }
 
@@ -1524,7 +1528,7 @@ template <class T>
 int launch_post_r2(const PostArgsT<T> &a0, hipStream_t s)
 {
     int t, gx, gy, r;
-    fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, kR2Stride);
+    fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, kR2Stride, r2_target());
     if (a0.r2out == nullptr || a0.pre_fired != nullptr || a0.Po != 0 || a0.Nr2 < 3 ||
         4 * (a0.Nr2 - 1) != a0.N - 1)
         return PGMG_ERR_ARG;
