@@ -49,20 +49,6 @@ def test_fspec_golden_16385(pgmg, oracle_mod, golden_cycles):
         assert s.dist_info()[1] == 0
 
 
-def test_fspec_bench_shape_16385(pgmg, oracle_mod, golden_cycles):
-    """bench.py --cycle F's shape (2 + 20 F-cycles in two calls, k_post_r2 between consecutive
-    F-cycles) against the reference's 22 F-cycles (tests/golden/big_logs/F16385.txt)."""
-    case = next(c for c in golden_cycles if c["kind"] == "F" and c["N"] == 16385)
-    assert len(case["cycles"]) >= 22
-    with pgmg.Solver(16385) as s:
-        s.set_problem()
-        s.fcycle(2)
-        s.fcycle(20)
-        assert oracle_mod.fnv_hash(s.solution()) == case["cycles"][21]["hash"]
-        assert s.stats()[0] == case["cycles"][21]["sweeps"]
-        assert s.dist_info()[1] == 0
-
-
 @pytest.mark.parametrize("eps", [1e5, 1e3, 3.0, 1e-2])
 @pytest.mark.parametrize("N", [129, 1025])
 def test_fspec_rollback(pgmg, oracle_mod, N, eps):

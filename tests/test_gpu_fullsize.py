@@ -12,9 +12,9 @@ What runs here is the code path the bench times, not a simplified one: at N = 16
 multi-cycle pgmg_vcycle call is the cross-cycle fused finest level (k_postpre_lds at its
 3072-workgroup band geometry), speculative early-exit decisions validated after the call,
 the analytic f regenerated in-kernel; the coarse levels' checks fire from cycle 12 on, so
-the long calls also cover the in-stream prediction and the rare paths.  BASELINE configs 4
-and 5 (8 GPUs, N = 32769) run as 8 loopback ranks on the one GPU of the test box (the
-production strip code; RCCL itself cannot host two ranks on one device).
+the long calls also cover the in-stream prediction and the rare paths.  The call shapes
+bench.py times for each BASELINE config are tests/test_gpu_baseline_configs.py; this file keeps
+the other full-size cases (F and FMG + W at 16385, FMG + W on 8 loopback strips at 32769).
 """
 import threading
 
@@ -40,9 +40,10 @@ def _check(oracle_mod, phi, stats, rows, k, what):
     assert stats[1] <= want["exits"], (what, stats, want["exits"])
 
 
-@pytest.mark.parametrize("calls", [[3], [2, 20], [5, 20]])
+@pytest.mark.parametrize("calls", [[3], [2, 20]])
 def test_vcycle_16385_bench_path(pgmg, oracle_mod, golden_cycles, calls):
-    """[2, 20] is bench.py's default run (warmup 2, steps 20, with its timing events)."""
+    """[2, 20]: warmup 2 + steps 20 with the timing events (the driver's 5 + 20 shape is
+    tests/test_gpu_baseline_configs.py::test_config2_16385)."""
     rows = _case(golden_cycles, "V", 16385)
     flags = pgmg.PGMG_FLAG_TIME_FINE if calls == [2, 20] else 0
     with pgmg.Solver(16385, flags=flags) as s:
@@ -54,16 +55,6 @@ def test_vcycle_16385_bench_path(pgmg, oracle_mod, golden_cycles, calls):
         spec, rollbacks = s.dist_info()
         assert spec, "speculative decisions off"
         _check(oracle_mod, s.solution(), s.stats(), rows, sum(calls), f"V16385 calls={calls}")
-
-
-def test_vcycle_16385_stored_rhs(pgmg, oracle_mod, golden_cycles):
-    """The general-RHS path (f streamed from HBM, 24 B/pt) at the bench's size."""
-    rows = _case(golden_cycles, "V", 16385)
-    with pgmg.Solver(16385, flags=pgmg.PGMG_FLAG_STORED_RHS) as s:
-        s.set_problem()
-        assert s.fine_pass_bytes(3) > s.fine_pass_bytes(0), "f regenerated despite the flag"
-        s.vcycle(3)
-        _check(oracle_mod, s.solution(), s.stats(), rows, 3, "V16385 stored f")
 
 
 def test_fcycle_16385(pgmg, oracle_mod, golden_cycles):
@@ -114,25 +105,6 @@ def _ranks(pgmg, world, N, work, **cfg):
     return out
 
 
-def test_vcycle_32769_bench_shape(pgmg, oracle_mod, golden_cycles):
-    """BASELINE config 4's grid on one GPU in bench.py's shape (1 + 5 cycles, two calls):
-    phi after 6 cycles bitwise oracle/mg_cpu_exec_port's (tests/golden/big_logs/V32769.txt)."""
-    rows = _case(golden_cycles, "V", 32769)
-    with pgmg.Solver(32769) as s:
-        s.set_problem()
-        s.vcycle(1)
-        s.vcycle(5)
-        _check(oracle_mod, s.solution(), s.stats(), rows, 6, "V32769 1 + 5")
-
-
-def test_strips8_vcycle_32769(pgmg, oracle_mod, golden_cycles):
-    """BASELINE config 4: N = 32769 on 8 row strips, one pgmg_vcycle(2) call per rank
-    (cross-fused finest level per strip, speculative decisions, RCCL-shaped halos)."""
-    rows = _case(golden_cycles, "V", 32769)
-    out = _ranks(pgmg, 8, 32769, lambda s: s.vcycle(2))
-    _check(oracle_mod, out[0][0], out[0][1], rows, 2, "V32769 on 8 strips")
-
-
 def test_strips8_fmg_w_32769(pgmg, oracle_mod, golden_cycles):
     """BASELINE config 5: FMG start + one W-cycle at N = 32769 on 8 row strips."""
     rows = _case(golden_cycles, "G", 32769)
@@ -143,47 +115,3 @@ def test_strips8_fmg_w_32769(pgmg, oracle_mod, golden_cycles):
 
     out = _ranks(pgmg, 8, 32769, work)
     _check(oracle_mod, out[0][0], out[0][1], rows, 2, "FMG+W 32769 on 8 strips")
-
-
-def test_fmg_w_32769_one_gpu(pgmg, oracle_mod, golden_cycles):
-    rows = _case(golden_cycles, "G", 32769)
-    with pgmg.Solver(32769) as s:
-        s.set_problem()
-        s.fcycle(1)
-        s.wcycle(1)
-        _check(oracle_mod, s.solution(), s.stats(), rows, 2, "FMG+W 32769")
-
-
-def test_strips8_fmg_w_32769_fp32(pgmg, oracle_mod, golden_cycles):
-    """BASELINE config 5's fp32 half: FMG start + one W-cycle at N = 32769 in fp32 on 8 row
-    strips is bitwise the fp32 run on one GPU (same kernels, pointwise arithmetic), and its
-    distance from the fp64 result -- which is bitwise the reference's hash -- is the one the
-    sweep measured (profiles/r02_fp32/fp32_sweep.json, kind G cycle 2: 0.02353 relative;
-    fp32's residual round-off, (N-1)^2 ulp(x), dominates at this size).
-    Tolerance: relative L2 difference <= 0.03 (the measured 0.0235 plus margin)."""
-    import numpy as np
-    N = 32769
-
-    def work(s):
-        s.fcycle(1)
-        s.wcycle(1)
-
-    out = _ranks(pgmg, 8, N, work, dtype="f32")
-    phi8 = out[0][0]
-    with pgmg.Solver(N, dtype="f32") as s:
-        s.set_problem()
-        work(s)
-        phi1 = s.solution()
-        st1 = s.stats()
-    assert np.array_equal(phi8.view(np.uint64), phi1.view(np.uint64)), "fp32: 8 strips != 1 GPU"
-    assert out[0][1][0] == st1[0]
-    del phi8
-    rows = _case(golden_cycles, "G", N)
-    with pgmg.Solver(N) as s:
-        s.set_problem()
-        work(s)
-        phi64 = s.solution()
-        _check(oracle_mod, phi64, s.stats(), rows, 2, "FMG+W 32769 fp64")
-    rel = float(np.linalg.norm(phi1 - phi64) / np.linalg.norm(phi64))
-    print(f"fp32 vs fp64 after FMG + W at 32769: {rel:.6e} relative (sweep: 2.3532e-02)")
-    assert rel <= 0.03, rel
