@@ -1102,6 +1102,12 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         if (nbk > maxblocks) maxblocks = nbk;
         nbk = std::max(tile_np(c, l, false), tile_np(c, l, true));
         if (nbk > maxblocks) maxblocks = nbk;
+        // k_post_r2 (the finest k_post of consecutive F-cycles, 116-column stride): its
+        // partials may land in c->partials when the check log is full
+        if (l == 0) {
+            nbk = post_r2_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2);
+            if (nbk > maxblocks) maxblocks = nbk;
+        }
     }
     if (rc == PGMG_OK && c->cross) rc = alloc_grid(c->S, c->lv[0]);
     // partial sums of k_postpre's second and third checks (cross-cycle fusion, and the
@@ -1428,13 +1434,23 @@ static void ext_frames(pgmg_ctx *c)
 // the null stream (an async copy into phi, a kernel writing f).  Work on the caller's own
 // non-blocking streams is the caller's to synchronise (include/pgmg.h).  The wait is skipped
 // when the null stream is already idle (the usual case: the previous call synchronised).
+// The null stream is the CALLING thread's current device's, so the record runs with the
+// context's device made current (and the caller's restored): one thread may drive contexts on
+// several devices.
 static int order_after_caller(pgmg_ctx *c)
 {
-    HIPC(hipEventRecord(c->ev_caller, nullptr));
-    const hipError_t q = hipEventQuery(c->ev_caller);
-    if (q == hipSuccess) return PGMG_OK;
-    if (q != hipErrorNotReady) return set_err(PGMG_ERR_HIP, hipGetErrorString(q));
-    HIPC(hipStreamWaitEvent(c->s, c->ev_caller, 0));
+    int prev = -1;
+    HIPC(hipGetDevice(&prev));
+    const bool swap = prev != c->cfg.device;
+    if (swap) HIPC(hipSetDevice(c->cfg.device));
+    hipError_t e = hipEventRecord(c->ev_caller, nullptr);
+    hipError_t q = e == hipSuccess ? hipEventQuery(c->ev_caller) : e;
+    if (q == hipErrorNotReady) q = hipStreamWaitEvent(c->s, c->ev_caller, 0);
+    if (swap) {
+        const hipError_t r = hipSetDevice(prev);
+        if (q == hipSuccess) q = r;
+    }
+    if (q != hipSuccess) return set_err(PGMG_ERR_HIP, hipGetErrorString(q));
     return PGMG_OK;
 }
 

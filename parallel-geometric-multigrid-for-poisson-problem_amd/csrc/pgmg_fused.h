@@ -69,8 +69,9 @@ struct PostArgsT {
     long long Po;
     // k_post_r2 (the finest level's last pass of an F-cycle followed by another, speculative
     // calls): also the two-step full weighting of x2 into level 2 (r2out, pitch Pr2, N = Nr2),
-    // the next F-cycle's first restriction step; launch_r2_fixup adds the columns the pass's
-    // wave tiles cannot form (pgmg_fused.hip "k_post_r2")
+    // the next F-cycle's first restriction step.  With the 116-column tile stride and the
+    // 6-column margin the pass forms every level-2 centre column itself: lanes 3..60 own the
+    // centres and lane 63 loads its own east coarse column (pgmg_fused.hip "k_post_r2")
     T *r2out;
     long long Pr2;
     int Nr2;
@@ -122,9 +123,9 @@ int post_r2_blocks(int N, int jc0, int jc1);   // k_post_r2's workgroups (check 
 // would read or write lies outside its array's allocation (check_span)
 template <class T> int launch_pre(const PreArgsT<T> &a, bool x0_zero, bool fine, hipStream_t s);
 template <class T> int launch_post(const PostArgsT<T> &a, bool fine, hipStream_t s);
-// the finest level's k_post with the two-step restriction of its result into a.r2out, then
-// the wave-tile boundary columns (launch_r2_fixup): one GPU, the analytic f regenerated or
-// streamed, phi read (not RECOMP)
+// the finest level's k_post with the two-step restriction of its result into a.r2out (every
+// level-2 centre column formed by the pass's own wave tiles): one GPU, the analytic f
+// regenerated or streamed, phi read (not RECOMP)
 template <class T> int launch_post_r2(const PostArgsT<T> &a, hipStream_t s);
 // coarse levels (x0 = 0, RECOMP) whose checks are predicted to fire: the one-sweep passes
 // with the checks' partials (k_pre1 / k_post1)

@@ -14,7 +14,7 @@ pg = _pkgload.load()
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 2049
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 200
 if len(sys.argv) > 3 and sys.argv[3] == "W":   # W-cycles: calls of K cycles, the plan per call
-    # PGMG_TRACE_FLAGS: pgmg_config.flags (e.g. 8192 = PGMG_FLAG_NO_SPEC_FIRE: no W plans)
+    # PGMG_TRACE_FLAGS: pgmg_config.flags (e.g. 32768 = PGMG_FLAG_NO_SPEC_FIRE: no W plans)
     flags = int(os.environ.get("PGMG_TRACE_FLAGS", "0"))
     with pg.Solver(N, flags=flags) as s:
         s.set_problem()

@@ -30,7 +30,8 @@ def _run(pgmg, N, calls, flags=0, phi0=None, f=None, **cfg):
                                      (2049, [("F", 4)]), (16385, [("F", 3)])])
 def test_fspec_equals_in_stream(pgmg, N, calls):
     """Consecutive F-cycles of one call also exercise k_post_r2 (the finest k_post forming the
-    next F-cycle's level-2 restriction, N >= 257) and its fix-up columns (i2 = 30, 60, ...)."""
+    next F-cycle's level-2 restriction, N >= 257), whose 116-column wave tiles form every
+    level-2 centre column themselves (lanes 3..60 own the centres)."""
     got, st, info = _run(pgmg, N, calls)
     want, st_x, _ = _run(pgmg, N, calls, flags=pgmg.PGMG_FLAG_EXACT_DIST)
     assert_bitwise(got, want, f"N={N} calls={calls}")
