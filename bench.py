@@ -206,23 +206,24 @@ def op_cases(pg, n):
     r = torch.zeros_like(x)
     c = torch.zeros((nc, nc), dtype=torch.float64, device=dev)
     e = torch.ones((nc, nc), dtype=torch.float64, device=dev)
-    def sweep(check, pair=None):   # trace keys: k_op_sweep[_ov]<U,CHECK,SEED,NT>, k_op_sweep2<U,SEED,NT>
+    def sweep(check, pair=None):
+        # trace keys: k_op_sweep<U,CHECK,SEED,NT> (the checked smoother's ping-pong sweeps),
+        # k_op_sweep_ip<U,NT> / k_op_sweep2_ip<U,NT> (the in-place single / paired sweeps)
         def m(k):
-            if k.startswith("k_op_sweep2<"):
-                return not check and pair is not False
-            return (k.startswith("k_op_sweep") and pair is not True and
-                    k.split("<")[1].split(",")[1] == ("true" if check else "false"))
+            if not check:
+                return (k.startswith("k_op_sweep2_ip") if pair is True else
+                        k.startswith("k_op_sweep_ip") if pair is False else
+                        k.startswith("k_op_sweep_ip") or k.startswith("k_op_sweep2_ip"))
+            return k.startswith("k_op_sweep<")   # v = 1 checked: two ping-pong sweeps
         return m
 
-    def named(prefix):
-        return lambda k: k.startswith(prefix)
-
     cases = [
-        ("jacobi v=0 (one sweep: the single-sweep kernel k_op_sweep, + the interior copy back)",
+        ("jacobi v=0 (one sweep in place on x: k_op_sweep_ip + the scatter of its deferred "
+         "tile edges)",
          lambda: pg.ops.jacobi(x, f, h, 0, eps=-1.0, tmp=tmp), 24 * fine, sweep(False, False), 1),
         ("jacobi v=1 (2 sweeps, no early exit: Parallel::ComputeJacobi's call in the V-cycle; "
-         "one paired pass k_op_sweep2 + the interior copy back)",
-         lambda: pg.ops.jacobi(x, f, h, 1, eps=-1.0, tmp=tmp), 2 * 24 * fine, sweep(False), 2),
+         "one paired pass in place, k_op_sweep2_ip + the scatter)",
+         lambda: pg.ops.jacobi(x, f, h, 1, eps=-1.0, tmp=tmp), 2 * 24 * fine, sweep(False, True), 2),
         ("jacobi v=100 (101 sweeps, no early exit: the per-op study's ComputeJacobi call)",
          lambda: pg.ops.jacobi(x, f, h, 100, eps=-1.0, tmp=tmp), 101 * 24 * fine, sweep(False),
          101),

@@ -23,6 +23,8 @@
 // -ffp-contract=off, so every value is bit-identical to the CPU reference (the KATs in
 // tests/test_gpu_parity.py).  Per-block partial sums use a fixed grid, so early-exit
 // decisions are deterministic run to run.
+#include <algorithm>
+
 #include "pgmg_internal.h"
 
 namespace pgmg {
@@ -392,6 +394,7 @@ void launch_g_sweep2(const double *xin, const double *f, double *xout, unsigned 
 }
 
 bool g_fuse2() { return tuning_int("PGMG_OP_FUSE2", 1) != 0; }
+bool g_inplace() { return tuning_int("PGMG_OP_INPLACE", 1) != 0; }
 
 constexpr int kOpTarget = 4096;   // workgroups per op launch (16 per CU)
 
@@ -545,6 +548,305 @@ void launch_g_copy_interior(const double *src, double *dst, int H, int W, hipStr
     }
     const OpGeom g = op_geom((W - 1) / 2, H - 2, 8, tuning_int("PGMG_OPC_BLOCKS", 2048));
     k_op_copy_interior<8><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(src, dst, H, W, g.rpb);
+}
+
+// ---------------------------------------------------------------------------
+// In-place sweeps (r05): Parallel::ComputeJacobi updates the caller's one array d_x
+// (Parallel_Method.cu:144-160, jacobi_kernel :6-24, which races -- SURVEY Q3); these passes
+// write x in place and still compute exactly the out-of-place sweep J(x), with no ping-pong
+// buffer and no interior copy-back.
+//
+// A workgroup owns a tile: a band of rows [jb, je) by its column range.  Inside the tile it
+// marches the rows as the out-of-place kernels do (each row's old values are read before the
+// row is written, and are kept in registers for the next row); an output that ANOTHER
+// workgroup reads as an input is never written in place, it is deferred to a side buffer:
+//   * the band's edge rows (the band above reads row jb, the one below row je-1; two rows per
+//     side for the paired sweeps, which read two rows of halo) -> SR, one row per slot;
+//   * the columns at the boundary between column blocks e and e+1 (the single sweep: 2, the
+//     paired sweeps: 8 columns, contiguous) -> SC[(e*H + row)*K + k].
+// The waves of one workgroup read each other's edge columns; a barrier between an
+// iteration's loads (waited for) and its stores orders them: iteration i stores rows that no
+// wave loads in iteration i+1 or later.  launch_g_defer_scatter then writes the deferred
+// values into x (after the pass, in stream order): ~1 % of the points at N = 16385.
+// No wave leaves early (lanes past the grid shadow or load zeros), so every barrier is met.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void wait_loads_then_barrier()
+{
+    __builtin_amdgcn_s_waitcnt(0);   // this wave's loads have returned
+    __syncthreads();
+}
+
+template <int U, bool NT>
+__global__ __launch_bounds__(kBlock) void k_op_sweep_ip(double *X, const double *__restrict__ F,
+                                                        double *__restrict__ SR,
+                                                        double *__restrict__ SC, unsigned *reset,
+                                                        unsigned long long *stats, double hh,
+                                                        int H, int W, int rpb)
+{
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+        if (reset != nullptr) *reset = 0u;
+        if (stats != nullptr) atomicAdd(&stats[0], 1ull);
+    }
+    const int lane = threadIdx.x & 63;
+    const int npairs = (W - 1) >> 1;
+    const int t_raw = blockIdx.x * kBlock + threadIdx.x;
+    const bool act = t_raw < npairs;
+    const int t = act ? t_raw : npairs - 1;  // idle lanes shadow the last pair (no stores)
+    const int c = 1 + 2 * t;
+    const bool second = c + 1 <= W - 2;
+    const bool lastp = t == npairs - 1;
+    const bool ld_l = lane == 0;
+    const bool ld_r = (lane == 63 || lastp) && second;
+    const int jb = 1 + blockIdx.y * rpb;
+    const int je = min(jb + rpb, H - 1);
+    const bool def_top = jb > 1, def_bot = je < H - 1;
+    // column-block boundaries: block e's last lane (.y) and block e+1's first lane (.x)
+    const bool def_l = threadIdx.x == 0 && blockIdx.x > 0;
+    const bool def_r = threadIdx.x == kBlock - 1 && blockIdx.x + 1 < gridDim.x;
+    const long long Wl = W;
+    double2 w0 = ldvu<double>(X + (long long)(jb - 1) * Wl + c);
+    double2 w1 = ldvu<double>(X + (long long)jb * Wl + c);
+    for (int j = jb; j < je; j += U) {
+        double2 xn[U], fv[U];
+        double el[U], er[U];
+        #pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long long r = min(j + u, je - 1);
+            fv[u] = ldvu<double>(F + r * Wl + c);
+            xn[u] = ldvu<double>(X + (r + 1) * Wl + c);
+            el[u] = ld_l ? X[r * Wl + c - 1] : 0.0;
+            er[u] = ld_r ? X[r * Wl + c + 2] : 0.0;
+        }
+        wait_loads_then_barrier();
+        #pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = j + u;
+            const double2 up = (u == 0) ? w0 : (u == 1 ? w1 : xn[u - 2]);
+            const double2 ce = (u == 0) ? w1 : xn[u - 1];
+            const double2 dn = xn[u];
+            double left = dpp_shr(ce.y);
+            double right = dpp_shl(ce.x);
+            if (ld_l) left = el[u];
+            if (ld_r) right = er[u];
+            double2 o;
+            o.x = 0.25 * ((hh * fv[u].x) + left + ce.y + up.x + dn.x);
+            o.y = second ? 0.25 * ((hh * fv[u].y) + ce.x + right + up.y + dn.y) : ce.y;
+            if (act && r < je) {
+                const bool dt = def_top && r == jb, db = def_bot && r == je - 1;
+                if (dt) stvu<double>(SR + (long long)(2 * blockIdx.y) * Wl + c, o);
+                if (db) stvu<double>(SR + (long long)(2 * blockIdx.y + 1) * Wl + c, o);
+                if (def_l) SC[((long long)(blockIdx.x - 1) * H + r) * 2 + 1] = o.x;
+                if (def_r) SC[((long long)blockIdx.x * H + r) * 2] = o.y;
+                if (!dt && !db) {
+                    double *q = X + (long long)r * Wl + c;
+                    if (def_l) q[1] = o.y;
+                    else if (def_r) q[0] = o.x;
+                    else st2<NT>(q, o);
+                }
+            }
+        }
+        w0 = xn[U - 2];
+        w1 = xn[U - 1];
+    }
+}
+
+// Two sweeps in one pass, in place: k_op_sweep2's wave tiles (128 columns loaded, the 120 of
+// lanes 2..61 owned); the workgroup boundary columns are block e's last wave's lanes 60, 61
+// and block e+1's first wave's lanes 2, 3 (8 contiguous columns), the deferred rows two per
+// band side.
+template <int U, bool NT>
+__global__ __launch_bounds__(kBlock) void k_op_sweep2_ip(double *X, const double *__restrict__ F,
+                                                         double *__restrict__ SR,
+                                                         double *__restrict__ SC,
+                                                         unsigned long long *stats, double hh,
+                                                         int H, int W, int rpb)
+{
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && stats != nullptr)
+        atomicAdd(&stats[0], 2ull);
+    constexpr int kWaves = kBlock / 64;
+    const int lane = threadIdx.x & 63;
+    const int wib = threadIdx.x >> 6;
+    const int wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int c = kOv2Stride * wave - 3 + 2 * lane;
+    const bool inx = c >= 1 && c <= W - 2, iny = c + 1 >= 1 && c + 1 <= W - 2;
+    const bool mid = lane >= 2 && lane <= 61;
+    const bool ox = mid && inx, oy = mid && iny;
+    // this lane's slot in the boundary buffer (-1: not a boundary column)
+    int kc = -1;
+    long long eb = 0;
+    if (wib == kWaves - 1 && (lane == 60 || lane == 61) && blockIdx.x + 1 < gridDim.x) {
+        kc = (lane - 60) * 2;
+        eb = blockIdx.x;
+    } else if (wib == 0 && (lane == 2 || lane == 3) && blockIdx.x > 0) {
+        kc = 4 + (lane - 2) * 2;
+        eb = blockIdx.x - 1;
+    }
+    const int jb = 1 + blockIdx.y * rpb;
+    const int je = min(jb + rpb, H - 1);   // x2 rows [jb, je)
+    const bool def_top = jb > 1, def_bot = je < H - 1;
+    const long long Wl = W;
+    auto ldrow = [&](const double *A, int r) {
+        return (r >= 0 && r <= H - 1) ? ld_pair(A + (long long)r * Wl, c, W) : make_double2(0.0, 0.0);
+    };
+    auto jrow = [&](double2 up, double2 ce, double2 dn, double2 f) {
+        const double l = dpp_shr(ce.y);
+        const double r = dpp_shl(ce.x);
+        double2 o;
+        o.x = inx ? 0.25 * ((hh * f.x) + l + ce.y + up.x + dn.x) : ce.x;
+        o.y = iny ? 0.25 * ((hh * f.y) + ce.x + r + up.y + dn.y) : ce.y;
+        return o;
+    };
+    double2 xa = ldrow(X, jb - 2), xb = ldrow(X, jb - 1);
+    double2 fa = make_double2(0.0, 0.0), fb = ldrow(F, jb - 1);
+    double2 ya = make_double2(0.0, 0.0), yb = make_double2(0.0, 0.0);
+    const int iend = je + 2;   // new rows i = jb .. je+1
+    for (int i = jb; i < iend; i += U) {
+        double2 xn[U], fn[U];
+        #pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = min(i + u, iend - 1);
+            xn[u] = ldrow(X, r);
+            fn[u] = ldrow(F, r);
+        }
+        wait_loads_then_barrier();
+        #pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int ii = i + u;
+            if (ii < iend) {
+                const int r1 = ii - 1;
+                double2 y1 = jrow(xa, xb, xn[u], fb);
+                if (r1 < 1 || r1 > H - 2) y1 = xb;
+                const int r2 = ii - 2;
+                if (r2 >= jb) {
+                    const double2 z = jrow(ya, yb, y1, fa);
+                    const bool dt = def_top && r2 < jb + 2, db = def_bot && r2 >= je - 2;
+                    if (dt) st_owned<false>(SR + (long long)(4 * blockIdx.y + (r2 - jb)) * Wl + c, z, ox, oy);
+                    if (db) st_owned<false>(SR + (long long)(4 * blockIdx.y + 2 + r2 - (je - 2)) * Wl + c, z, ox, oy);
+                    if (kc >= 0) stvu<double>(SC + (eb * H + r2) * 8 + kc, z);
+                    else if (!dt && !db) st_owned<NT>(X + (long long)r2 * Wl + c, z, ox, oy);
+                }
+                xa = xb;
+                xb = xn[u];
+                fa = fb;
+                fb = fn[u];
+                ya = yb;
+                yb = y1;
+            }
+        }
+    }
+}
+
+// The deferred outputs into x: blockIdx.y == 0 the band rows (nslot = 2R slots per band: the
+// first R rows of the band when a band lies above, the last R when one lies below), 1 the
+// column-block boundaries (K columns from col0(e) = ca*e + cb, rows 1 .. H-2).
+__global__ __launch_bounds__(kBlock) void k_op_defer_scatter(double *X, const double *SR,
+                                                             const double *SC, int H, int W,
+                                                             int rpb, int gy, int R, int nbound,
+                                                             int K, int ca, int cb)
+{
+    const long long Wl = W;
+    const long long tid = (long long)blockIdx.x * kBlock + threadIdx.x;
+    const long long nthr = (long long)gridDim.x * kBlock;
+    if (blockIdx.y == 0) {
+        const long long n = (long long)gy * 2 * R * (W - 2);
+        for (long long k = tid; k < n; k += nthr) {
+            const int col = 1 + (int)(k % (W - 2));
+            const long long slot = k / (W - 2);
+            const int by = (int)(slot / (2 * R)), s = (int)(slot % (2 * R));
+            const int jb = 1 + by * rpb, je = min(jb + rpb, H - 1);
+            int row;
+            bool ok;
+            if (s < R) {
+                row = jb + s;
+                ok = jb > 1 && row < je;
+            } else {
+                row = je - R + (s - R);
+                ok = je < H - 1 && row >= jb;
+            }
+            if (ok) X[row * Wl + col] = SR[slot * Wl + col];
+        }
+    } else {
+        const long long n = (long long)nbound * (H - 2);
+        for (long long k = tid; k < n; k += nthr) {
+            const int e = (int)(k / (H - 2));
+            const int row = 1 + (int)(k % (H - 2));
+            const int c0 = ca * e + cb;
+            const double *src = SC + ((long long)e * H + row) * K;
+            double *dst = X + row * Wl + c0;
+            for (int q = 0; q < K; ++q)
+                if (c0 + q >= 1 && c0 + q <= W - 2) dst[q] = src[q];
+        }
+    }
+}
+
+static OpGeom sweep_ip_geom(int H, int W, int U)
+{
+    return op_geom((W - 1) / 2, H - 2, U, tuning_int("PGMG_OPIP_BLOCKS", 1024));
+}
+static OpGeom sweep2_ip_geom(int H, int W, int U)
+{
+    return sweep2_geom(H, W, U, tuning_int("PGMG_OP2IP_BLOCKS", 1024));
+}
+
+// side buffer elements for either in-place pass at any of its row-step choices
+size_t g_defer_elems(int H, int W)
+{
+    size_t m = 0;
+    for (int U : {8, 16}) {
+        const OpGeom a = sweep_ip_geom(H, W, U);
+        m = std::max(m, (size_t)a.gy * 2 * W + (size_t)(a.gx > 1 ? a.gx - 1 : 0) * H * 2);
+    }
+    for (int U : {4, 8}) {
+        const OpGeom b = sweep2_ip_geom(H, W, U);
+        m = std::max(m, (size_t)b.gy * 4 * W + (size_t)(b.gx > 1 ? b.gx - 1 : 0) * H * 8);
+    }
+    return m + 64;
+}
+
+static void defer_scatter(double *x, const double *SR, const double *SC, const OpGeom &g, int R,
+                          int K, int ca, int cb, int H, int W, hipStream_t s)
+{
+    const long long n = std::max((long long)g.gy * 2 * R * (W - 2),
+                                 (long long)(g.gx - 1) * (H - 2));
+    long long nb = (n + kBlock - 1) / kBlock;
+    if (nb > 1024) nb = 1024;
+    if (nb < 1) nb = 1;
+    k_op_defer_scatter<<<dim3((unsigned)nb, 2), kBlock, 0, s>>>(x, SR, SC, H, W, g.rpb, g.gy, R,
+                                                                g.gx - 1, K, ca, cb);
+}
+
+void launch_g_sweep_ip(double *x, const double *f, double *side, unsigned *reset,
+                       unsigned long long *stats, double hh, int H, int W, hipStream_t s)
+{
+    const int U = tuning_int("PGMG_OPIP_U", 16) == 8 ? 8 : 16;
+    const OpGeom g = sweep_ip_geom(H, W, U);
+    const bool nt = tuning_int("PGMG_OP_NT", 1) != 0;
+    double *SR = side, *SC = side + (size_t)g.gy * 2 * W;
+    const dim3 grid(g.gx, g.gy);
+#define PGMG_KI(UU, NTV) k_op_sweep_ip<UU, NTV><<<grid, kBlock, 0, s>>>(x, f, SR, SC, reset, stats, hh, H, W, g.rpb)
+    if (U == 8) { if (nt) PGMG_KI(8, true); else PGMG_KI(8, false); }
+    else { if (nt) PGMG_KI(16, true); else PGMG_KI(16, false); }
+#undef PGMG_KI
+    // boundary e: columns 2 kBlock (e+1) and the next
+    defer_scatter(x, SR, SC, g, 1, 2, 2 * kBlock, 2 * kBlock, H, W, s);
+}
+
+void launch_g_sweep2_ip(double *x, const double *f, double *side, unsigned long long *stats,
+                        double hh, int H, int W, hipStream_t s)
+{
+    const int U = tuning_int("PGMG_OP2IP_U", 8) == 4 ? 4 : 8;
+    const OpGeom g = sweep2_ip_geom(H, W, U);
+    const bool nt = tuning_int("PGMG_OP_NT", 1) != 0;
+    double *SR = side, *SC = side + (size_t)g.gy * 4 * W;
+    const dim3 grid(g.gx, g.gy);
+#define PGMG_KI(UU, NTV) k_op_sweep2_ip<UU, NTV><<<grid, kBlock, 0, s>>>(x, f, SR, SC, stats, hh, H, W, g.rpb)
+    if (U == 4) { if (nt) PGMG_KI(4, true); else PGMG_KI(4, false); }
+    else { if (nt) PGMG_KI(8, true); else PGMG_KI(8, false); }
+#undef PGMG_KI
+    // boundary e: block e's last wave w = kWaves (e+1) - 1, lanes 60, 61 -> columns
+    // kOv2Stride w + 117 ...; 8 columns
+    constexpr int kWaves = kBlock / 64;
+    defer_scatter(x, SR, SC, g, 2, 8, kOv2Stride * kWaves, kOv2Stride * (kWaves - 1) + 117, H, W, s);
 }
 
 // ---------------------------------------------------------------------------

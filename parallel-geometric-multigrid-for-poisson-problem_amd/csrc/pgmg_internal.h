@@ -230,6 +230,14 @@ void launch_g_copy_interior(const double *src, double *dst, int H, int W, hipStr
 void launch_g_sweep2(const double *xin, const double *f, double *xout, unsigned long long *stats,
                      double hh, int H, int W, bool seed, hipStream_t s);
 bool g_fuse2();   // pgmg_jacobi without checks runs its sweeps in pairs (default)
+// in-place sweeps on the caller's x (r05): one sweep / two sweeps per pass, each followed by
+// the scatter of its deferred tile-edge outputs; `side` holds g_defer_elems(H, W) doubles
+size_t g_defer_elems(int H, int W);
+void launch_g_sweep_ip(double *x, const double *f, double *side, unsigned *reset,
+                       unsigned long long *stats, double hh, int H, int W, hipStream_t s);
+void launch_g_sweep2_ip(double *x, const double *f, double *side, unsigned long long *stats,
+                        double hh, int H, int W, hipStream_t s);
+bool g_inplace();   // pgmg_jacobi sweeps in place (default; PGMG_OP_INPLACE=0: ping-pong)
 void launch_g_fixup(const double *partials, int np, double eps, const unsigned *done_prev,
                     unsigned *done_next, const double *src, double *dst,
                     unsigned long long *stats, int H, int W, hipStream_t s);

@@ -3,10 +3,11 @@
 // ComputeProlungator (3_part_parallel/Parallel_Method.cu:144-199), plus device
 // memory helpers so host code can drive the library without HIP headers.
 //
-// Unlike the reference kernels, the Jacobi op is out-of-place (ping-pong; the
-// reference's in-place jacobi_kernel races) and applies the CPU
-// smoother's residual-norm early exit when eps >= 0, so its result equals
-// JacobiSmoother::smooth bit for bit.
+// Like the reference's, the Jacobi op updates the caller's x in place -- but race-free: its
+// passes defer every tile-edge output another workgroup reads (pgmg_gops.hip "In-place
+// sweeps"; the reference's jacobi_kernel races), so each sweep is exactly the
+// out-of-place Jacobi sweep; with eps >= 0 it applies the CPU smoother's residual-norm early
+// exit, so its result equals JacobiSmoother::smooth bit for bit.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -31,6 +32,8 @@ struct OpScratch {
     double *scalar = nullptr;
     double *tmp = nullptr;
     size_t tmp_elems = 0;
+    double *side = nullptr;   // the in-place passes' deferred tile-edge outputs
+    size_t side_elems = 0;
 };
 
 // One scratch set per stream: ops enqueued on different streams never share partial sums,
@@ -63,6 +66,21 @@ int ensure_scratch(hipStream_t s, size_t tmp_elems, OpScratch **out)
     return PGMG_OK;
 }
 
+int ensure_side(hipStream_t s, OpScratch &o, size_t elems)
+{
+    std::lock_guard<std::mutex> lk(g_op_mu);
+    if (elems <= o.side_elems) return PGMG_OK;
+    if (o.side) {
+        HIPC(hipStreamSynchronize(s));
+        HIPC(hipFree(o.side));
+    }
+    o.side = nullptr;
+    o.side_elems = 0;
+    HIPC(hipMalloc((void **)&o.side, elems * sizeof(double)));
+    o.side_elems = elems;
+    return PGMG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -74,12 +92,16 @@ int pgmg_jacobi(double *d_x, double *d_tmp, const double *d_f, int H, int W, dou
     hipStream_t s = (hipStream_t)stream;
     const size_t L = (size_t)H * W;
     const int S = v + 1;
+    const bool check = eps >= 0.0;
+    const bool inplace = g_inplace();
+    // in place, only a checked call with v >= 1 needs a ping-pong buffer
+    const bool need_tmp = !inplace || (check && S >= 2);
     OpScratch *op = nullptr;
-    int e = ensure_scratch(s, d_tmp ? 0 : L, &op);
+    int e = ensure_scratch(s, (d_tmp || !need_tmp) ? 0 : L, &op);
     if (e) return e;
     OpScratch &g_op = *op;
+    if (inplace && (e = ensure_side(s, g_op, g_defer_elems(H, W)))) return e;
     double *tmp = d_tmp ? d_tmp : g_op.tmp;
-    const bool check = eps >= 0.0;
     // flag slots: a fresh block of S+1 words per call would need a ring; the op is
     // synchronous w.r.t. its own flags because every launch is stream-ordered.
     unsigned *D = g_op.flags;
@@ -89,13 +111,55 @@ int pgmg_jacobi(double *d_x, double *d_tmp, const double *d_f, int H, int W, dou
     if (nb > kOpPartialsCap) return set_err(PGMG_ERR_STATE, "pgmg_jacobi: too many blocks");
     if (check && S >= (kMaxSweeps + 2) * 128)
         return set_err(PGMG_ERR_ARG, "pgmg_jacobi: v too large for the early-exit flags");
-    // Sweeps alternate x -> tmp -> x ...  No seed copy of tmp (Smoother.hpp:47 copies the whole
-    // grid into its output buffer): the first sweep writes x's boundary into tmp besides the
-    // interior, which is all a later sweep reads of it.  An odd sweep count ends in tmp and
-    // copies its interior back (x's boundary is never written).
+    auto finish = [&]() -> int {
+        HIPC(hipGetLastError());
+        if (sweeps_done) {
+            unsigned long long st[4];
+            HIPC(hipMemcpyAsync(st, g_op.stats, sizeof(st), hipMemcpyDeviceToHost, s));
+            HIPC(hipStreamSynchronize(s));
+            *sweeps_done = (int)st[0];
+        }
+        return PGMG_OK;
+    };
+    if (inplace && !check) {
+        // the reference GPU op (ComputeJacobi decides nothing between its v+1 sweeps,
+        // Parallel_Method.cu:144-160): every sweep on d_x itself, in pairs (k_op_sweep2_ip)
+        // with an odd count's single sweep first (k_op_sweep_ip); no tmp, no copy-back
+        int left = S;
+        if (left & 1) {
+            launch_g_sweep_ip(d_x, d_f, g_op.side, &D[1], g_op.stats, hh, H, W, s);
+            left -= 1;
+        }
+        for (; left > 0; left -= 2)
+            if (g_fuse2()) launch_g_sweep2_ip(d_x, d_f, g_op.side, g_op.stats, hh, H, W, s);
+            else {
+                launch_g_sweep_ip(d_x, d_f, g_op.side, nullptr, g_op.stats, hh, H, W, s);
+                launch_g_sweep_ip(d_x, d_f, g_op.side, nullptr, g_op.stats, hh, H, W, s);
+            }
+        return finish();
+    }
+    if (inplace && (S & 1)) {
+        // JacobiSmoother::smooth's checks (Smoother.hpp:59-88) with an odd sweep count: sweep
+        // 1 has no check and runs in place; sweeps k = 2 .. S alternate x -> tmp -> x, each
+        // deciding the previous sweep's check (k_g_fixup undoes the sweep after a firing
+        // check) and ending in x; the first of them also writes x's boundary into tmp (no
+        // seed copy).  An even count is the ping-pong below, which ends in x by itself.
+        launch_g_sweep_ip(d_x, d_f, g_op.side, &D[1], g_op.stats, hh, H, W, s);
+        for (int k = 2; k <= S; ++k) {
+            const double *in = (k & 1) ? tmp : d_x;
+            double *out = (k & 1) ? d_x : tmp;
+            launch_g_sweep(in, d_f, out, g_op.partials, &D[k - 1], nullptr, g_op.stats, hh, ih,
+                           H, W, k == 2, s);
+            launch_g_fixup(g_op.partials, nb, eps, &D[k - 1], &D[k], in, out, g_op.stats, H, W, s);
+        }
+        return finish();
+    }
+    // ping-pong (an even checked count; everything with PGMG_OP_INPLACE=0 in the measurement
+    // build, the r04 form): sweeps alternate x -> tmp -> x ...  No seed copy of tmp (Smoother.hpp:47 copies the whole grid into its
+    // output buffer): the first sweep writes x's boundary into tmp besides the interior, which
+    // is all a later sweep reads of it.  An odd sweep count ends in tmp and copies its interior
+    // back (x's boundary is never written).
     if (!check && g_fuse2()) {
-        // no checks (the reference GPU op's ComputeJacobi): sweeps in pairs, one pass each
-        // (k_op_sweep2), an odd count's single sweep first; passes alternate x -> tmp -> x
         const double *cur = d_x;
         double *other = tmp;
         int left = S;
@@ -115,14 +179,7 @@ int pgmg_jacobi(double *d_x, double *d_tmp, const double *d_f, int H, int W, dou
             other = nc;
         }
         if (cur == tmp) launch_g_copy_interior(tmp, d_x, H, W, s);
-        HIPC(hipGetLastError());
-        if (sweeps_done) {
-            unsigned long long st[4];
-            HIPC(hipMemcpyAsync(st, g_op.stats, sizeof(st), hipMemcpyDeviceToHost, s));
-            HIPC(hipStreamSynchronize(s));
-            *sweeps_done = (int)st[0];
-        }
-        return PGMG_OK;
+        return finish();
     }
     for (int k = 1; k <= S; ++k) {
         const double *in = (k & 1) ? d_x : tmp;
@@ -135,14 +192,7 @@ int pgmg_jacobi(double *d_x, double *d_tmp, const double *d_f, int H, int W, dou
             launch_g_fixup(g_op.partials, nb, eps, &D[k - 1], &D[k], in, out, g_op.stats, H, W, s);
     }
     if (S & 1) launch_g_copy_interior(tmp, d_x, H, W, s);
-    HIPC(hipGetLastError());
-    if (sweeps_done) {
-        unsigned long long st[4];
-        HIPC(hipMemcpyAsync(st, g_op.stats, sizeof(st), hipMemcpyDeviceToHost, s));
-        HIPC(hipStreamSynchronize(s));
-        *sweeps_done = (int)st[0];
-    }
-    return PGMG_OK;
+    return finish();
 }
 
 int pgmg_residual(double *d_r, const double *d_x, const double *d_f, int H, int W, double h,
@@ -231,7 +281,7 @@ int pgmg_ops_release(void *stream)
     }
     HIPC(hipStreamSynchronize(s));   // ops still queued on s may use the set
     for (void *p : {(void *)o.partials, (void *)o.flags, (void *)o.stats, (void *)o.scalar,
-                    (void *)o.tmp})
+                    (void *)o.tmp, (void *)o.side})
         if (p) HIPC(hipFree(p));
     return PGMG_OK;
 }

@@ -3,13 +3,16 @@ reference's Parallel::ComputeJacobi / ComputeResidual / ComputeRestriction /
 ComputeProlungator (3_part_parallel/Parallel_Method.cu:144-199) -- on ragged and edge-case
 shapes, bitwise against the oracle (oracle/pgmg_oracle.c, pinned to the compiled reference).
 
-The r04 kernels march row bands with column pairs per lane on the caller's layout (pitch W,
-any alignment), seed only the ping-pong buffer's boundary, and copy an odd sweep count's
-interior back; these cases cover what that can get wrong: even and odd W (the last lane pair
-is whole or half boundary), W not a multiple of the 512-column block, H != W, the smallest
-grids, every sweep-count parity, checks that fire at the first or a later sweep, a caller
-ping-pong buffer full of NaN (nothing may read what the op did not write), and the caller's
-non-zero boundary."""
+The kernels march row bands with column pairs per lane on the caller's layout (pitch W, any
+alignment).  Since r05 the sweeps without checks run IN PLACE on x (k_op_sweep_ip /
+k_op_sweep2_ip: the tile-edge outputs other workgroups read are deferred to a side buffer and
+scattered after the pass); a checked call with an odd sweep count runs its first sweep in place
+and the rest ping-pong, seeding only the ping-pong buffer's boundary.  These cases cover what
+that can get wrong: even and odd W (the last lane pair is whole or half boundary), W not a
+multiple of the 512-column block, many column blocks and row bands (deferred rows and columns
+meeting at tile corners), H != W, the smallest grids, every sweep-count parity, checks that fire
+at the first or a later sweep, a caller ping-pong buffer full of NaN (nothing may read what the
+op did not write), and the caller's non-zero boundary."""
 import ctypes as C
 
 import numpy as np
@@ -54,6 +57,47 @@ def test_jacobi_ragged_shapes(pgmg, oracle_mod, H, W):
             n = pgmg.ops.jacobi(xt, _t(f), h, v, eps=eps, tmp=tmp)
             assert n == n_ref, (H, W, v, eps)
             assert_bitwise(xt.cpu().numpy(), x, f"jacobi {H}x{W} v={v} eps={eps}")
+
+
+@pytest.mark.parametrize("H,W", [(1031, 1537), (700, 2053), (2049, 2049), (4097, 1030),
+                                 (517, 4100)])
+def test_jacobi_in_place_tiles(pgmg, oracle_mod, H, W):
+    """Grids of several column blocks (512 columns for the single sweep, 480 for the paired
+    pass) and many row bands: every deferred tile edge, bitwise the oracle, for 1 .. 4 sweeps
+    without checks (single, paired, single + paired, two paired passes) and 3 sweeps with
+    checks (the first in place, then ping-pong)."""
+    import torch
+    rng = np.random.default_rng(H * 13 + W)
+    x0 = rng.uniform(-1, 1, (H, W))
+    f = rng.uniform(-1, 1, (H, W))
+    h = 1.0 / (max(H, W) - 1)
+    ft = _t(f)
+    for v, eps in ((0, -1.0), (1, -1.0), (2, -1.0), (3, -1.0), (2, 1e-30), (2, 1e9)):
+        x = x0.copy()
+        n_ref = _orc_smooth(oracle_mod, x, f, h, v, eps)
+        xt = _t(x0)
+        tmp = torch.full_like(xt, float("nan"))
+        n = pgmg.ops.jacobi(xt, ft, h, v, eps=eps, tmp=tmp)
+        assert n == n_ref, (H, W, v, eps)
+        assert_bitwise(xt.cpu().numpy(), x, f"in-place jacobi {H}x{W} v={v} eps={eps}")
+
+
+def test_jacobi_in_place_repeated_calls(pgmg, oracle_mod):
+    """Back-to-back in-place calls on one stream share the side buffer: 7 calls of 1 .. 3
+    sweeps equal the oracle's 7 smoother calls."""
+    import torch
+    H, W = 1500, 1800
+    rng = np.random.default_rng(5)
+    x = rng.uniform(-1, 1, (H, W))
+    f = rng.uniform(-1, 1, (H, W))
+    h = 1.0 / (W - 1)
+    xt, ft = _t(x), _t(f)
+    for k in range(7):
+        v = k % 3
+        _orc_smooth(oracle_mod, x, f, h, v, -1.0)
+        pgmg.ops.jacobi(xt, ft, h, v, eps=-1.0)
+    torch.cuda.synchronize()
+    assert_bitwise(xt.cpu().numpy(), x, "7 in-place calls")
 
 
 @pytest.mark.parametrize("N", [65, 257, 1025])
