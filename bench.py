@@ -220,15 +220,15 @@ def op_cases(pg, n):
     cases = [
         ("jacobi v=0 (one sweep in place on x: k_op_sweep_ip + the scatter of its deferred "
          "tile edges)",
-         lambda: pg.ops.jacobi(x, f, h, 0, eps=-1.0, tmp=tmp), 24 * fine, sweep(False, False), 1),
+         lambda: pg.ops.jacobi(x, f, h, 0, eps=-1.0, tmp=tmp, count=False), 24 * fine, sweep(False, False), 1),
         ("jacobi v=1 (2 sweeps, no early exit: Parallel::ComputeJacobi's call in the V-cycle; "
          "one paired pass in place, k_op_sweep2_ip + the scatter)",
-         lambda: pg.ops.jacobi(x, f, h, 1, eps=-1.0, tmp=tmp), 2 * 24 * fine, sweep(False, True), 2),
+         lambda: pg.ops.jacobi(x, f, h, 1, eps=-1.0, tmp=tmp, count=False), 2 * 24 * fine, sweep(False, True), 2),
         ("jacobi v=100 (101 sweeps, no early exit: the per-op study's ComputeJacobi call)",
-         lambda: pg.ops.jacobi(x, f, h, 100, eps=-1.0, tmp=tmp), 101 * 24 * fine, sweep(False),
+         lambda: pg.ops.jacobi(x, f, h, 100, eps=-1.0, tmp=tmp, count=False), 101 * 24 * fine, sweep(False),
          101),
         ("jacobi v=1 with the smoother's early-exit checks (JacobiSmoother::smooth)",
-         lambda: pg.ops.jacobi(x, f, h, 1, eps=1e-7, tmp=tmp), 2 * 24 * fine,
+         lambda: pg.ops.jacobi(x, f, h, 1, eps=1e-7, tmp=tmp, count=False), 2 * 24 * fine,
          sweep(True), 2),
         ("residual (ComputeResidual)", lambda: pg.ops.residual(r, x, f, h), 24 * fine,
          named("k_op_residual"), 0),

@@ -404,12 +404,15 @@ class _Ops:
             return C.c_void_p(t)
         return C.c_void_p(t.data_ptr())
 
-    def jacobi(self, x, f, h, v, eps=1e-7, tmp=None, stream=None):
+    def jacobi(self, x, f, h, v, eps=1e-7, tmp=None, stream=None, count=True):
+        """count=False: the reference's void ComputeJacobi shape -- no sweep count returned,
+        so no device-to-host readback (the call stays asynchronous on `stream`)."""
         H, W = x.shape
         done = C.c_int()
         check(load().pgmg_jacobi(self._ptr(x), self._ptr(tmp), self._ptr(f), H, W, float(h),
-                                 int(v), float(eps), C.byref(done), stream), "pgmg_jacobi")
-        return done.value
+                                 int(v), float(eps), C.byref(done) if count else None, stream),
+              "pgmg_jacobi")
+        return done.value if count else None
 
     def residual(self, r, x, f, h, stream=None):
         H, W = x.shape

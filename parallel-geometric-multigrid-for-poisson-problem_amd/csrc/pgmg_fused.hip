@@ -873,6 +873,42 @@ __device__ __forceinline__ V2<T> rsn(V2<T> up, V2<T> ce, V2<T> dn, Nbr<T> n, V2<
 constexpr int kPPWaves = 4;   // waves per k_postpre block (8-wave blocks measured equal, r02)
 constexpr int kPPLdsRow = kPPWaves * kPPStride + 2 * kPPMargin + 4;          // doubles per row
 constexpr int kPPLdsCoarse = kPPWaves * (kPPStride / 2) + kPPMargin + 8;     // per coarse row
+// fp32 (r05): the rows are staged from 16-byte loads of FOUR columns per lane (8-byte lane
+// loads stream at 0.54-0.70x the 16-byte rate, MI355X_MICROARCH.md), starting two columns
+// left of the window (column L0 - 2 is 16-byte aligned: column 1 of every row sits on a
+// 128-byte boundary), so an fp32 LDS row carries a 2-element shift and 4 more elements; the
+// coarse rows likewise from 16-byte loads at cc0 (aligned), rows padded to whole 16 bytes.
+// Compile-time A/B knobs of the fp32 form (scripts/build_variant.sh): quad row loads, quad
+// coarse loads, quad x4 stores, register sets of loads in flight.  Measured (r05,
+// scripts/pp_ab.py --dtype f32, profiles/r05_fp32/pp_f32.jsonl, 3 interleaved rounds at 16385):
+// k_postpre_lds<float> 0.636-0.651 ms as built before, 0.644-0.648 with every knob off,
+// 0.675-0.687 with quad loads (2 waves of 4 do all the loading, ds_write_b128), 0.647-0.649
+// with quad stores only -- the knobs stay off; the pass's cost for fp32 is its per-lane work
+// on 2 columns, not the load width.
+#ifndef PGMG_F32_QLOAD
+#define PGMG_F32_QLOAD 0
+#endif
+#ifndef PGMG_F32_QCOARSE
+#define PGMG_F32_QCOARSE 0
+#endif
+#ifndef PGMG_F32_QSTORE
+#define PGMG_F32_QSTORE 0
+#endif
+#ifndef PGMG_F32_DEPTH
+#define PGMG_F32_DEPTH 3
+#endif
+template <class T> constexpr bool pp_ql() { return sizeof(T) == 4 && PGMG_F32_QLOAD; }
+template <class T> constexpr bool pp_qc() { return sizeof(T) == 4 && PGMG_F32_QCOARSE; }
+template <class T> constexpr bool pp_qs() { return sizeof(T) == 4 && PGMG_F32_QSTORE; }
+template <class T> constexpr int pp_sh() { return pp_ql<T>() ? 2 : 0; }
+template <class T> constexpr int pp_lds_row() { return kPPLdsRow + (pp_ql<T>() ? 4 : 0); }
+template <class T> constexpr int pp_lds_coarse()
+{
+    return pp_qc<T>() ? (kPPLdsCoarse + 3) / 4 * 4 : kPPLdsCoarse;
+}
+// the register type of one row's staging load: a column pair (fp64), a column quad (fp32)
+template <class T> using PPV = typename std::conditional<pp_ql<T>(), float4, V2<T>>::type;
+template <class T> using PPC = typename std::conditional<pp_qc<T>(), float4, V2<T>>::type;
 
 // R2 (row strips): also sum r(x2)^2 into partials3.  When the post check fires the
 // pre-smooth restarts from x1 and its first check is ||r(J(x1))|| = ||r(x2)||; having it
@@ -898,7 +934,7 @@ constexpr int kPPR = 2;   // rows per LDS slot (a row pair)
 template <class T, bool R2, bool GENF, int OPT>
 constexpr int pp_depth()
 {
-    return (sizeof(T) == 4 || (GENF && !R2 && !(OPT & (64 | 32)))) ? 3 : 2;
+    return sizeof(T) == 4 ? PGMG_F32_DEPTH : ((GENF && !R2 && !(OPT & (64 | 32))) ? 3 : 2);
 }
 // Lane t's 16-byte (fp32: 8-byte) column pair of a row segment starting at `base`; lanes
 // t >= n read 0 (descriptor range check).  The descriptor is built from wave-uniform values.
@@ -938,6 +974,20 @@ __device__ __forceinline__ void buf_store_one(T *base, int bytes, int off, T v)
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
     }
 }
+// fp32: lane t's 16-byte column quad of a row segment of n quads starting at `base`
+__device__ __forceinline__ float4 buf_quad(const float *base, int n, int t)
+{
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(base), (short)0, n * 16, 0x00020000);
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, t * 16, 0, 0));
+}
+template <int NT>
+__device__ __forceinline__ void buf_store_quad(float *base, int bytes, int off, float4 v)
+{
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, bytes, 0x00020000);
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, off, 0, NT ? 2 : 0);
+}
 template <class T>
 __device__ __forceinline__ T buf_one(const T *base, int n, int t)
 {
@@ -953,10 +1003,13 @@ __device__ __forceinline__ T buf_one(const T *base, int n, int t)
 // no column of this wave is a boundary, so the Jacobi stages carry no passthrough selects.
 template <class T, bool R2, bool GENF, bool EDGE, int OPT>
 __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const Cols &k,
-                                                double *red, T (&sx)[2][kPPR][kPPLdsRow],
-                                                T (&sf)[2][kPPR][GENF ? 1 : kPPLdsRow],
-                                                T (&se)[3][kPPLdsCoarse], const Blk bk)
+                                                double *red, T (&sx)[2][kPPR][pp_lds_row<T>()],
+                                                T (&sf)[2][kPPR][GENF ? 1 : pp_lds_row<T>()],
+                                                T (&se)[3][pp_lds_coarse<T>()], const Blk bk)
 {
+    constexpr bool Q = pp_ql<T>();   // fp32: 16-byte column quads (above)
+    constexpr bool QC = pp_qc<T>(), QS = pp_qs<T>();
+    constexpr int SH = pp_sh<T>();
     constexpr int R = kPPR;
     const int N = a.N, Nc = a.Nc;
     const long long P = a.P, Pc = a.Pc;
@@ -1005,6 +1058,18 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int xo = kPPStride * w + 2 * lane;
     const int co = (kPPStride / 2) * w + lane;
+    // fp32 quads: the window's 2 * npairs columns from L0 - 2 (nq4 quads; nvq of them inside
+    // the loaded range, the rest read 0); coarse: ncc columns from cc0 (ncq quads, nveq valid).
+    // A quad past the old pair/element range loads columns past the grid's last one or the
+    // window: they reach only lanes that own nothing (the margins), as before.
+    const int nq4 = (2 * npairs + 2 + 3) / 4, nvq = (2 * nvx + 2 + 3) / 4;
+    const int ncq = (ncc + 3) / 4, nveq = (nve + 3) / 4;
+    // fp32 x4 stores: odd lane l (16-byte aligned column) stores its pair and lane l+1's as
+    // one quad when both own theirs; an owning odd lane without an owning partner (the grid's
+    // right edge) stores its pair alone
+    const bool own_next = lane + 1 < kPPMargin / 2 + kPPStride / 2 && k.c + 2 <= N - 2;
+    const int xoff16 = (QS && (lane & 1) && k.own && own_next) ? xoff : kOOB;
+    const int xoff8 = QS ? (((lane & 1) && k.own && !own_next) ? xoff : kOOB) : xoff;
 
     V2<T> e0 = z, e1 = z, b0 = z, b1 = z, c0 = z, c1 = z, g0 = z, g1 = z, h0 = z, h1 = z,
             d0 = z, d1 = z;
@@ -1017,7 +1082,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     auto ring = [](int m) { return (m + 3 * 4096) % 3; };  // m >= -3
 
     if (t < 2 * R * 4) {   // the 4 pad doubles past the window (read by spare lanes only)
-        const int sl = t >> 3, q = (t >> 2) & 1, j = kPPLdsRow - 4 + (t & 3);
+        const int sl = t >> 3, q = (t >> 2) & 1, j = pp_lds_row<T>() - 4 + (t & 3);
         sx[sl][q][j] = T(0);
         if constexpr (!GENF) sf[sl][q][j] = T(0);
     }
@@ -1025,30 +1090,54 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     // A, B; D = 3: A, B, C)
     constexpr int D = pp_depth<T, R2, GENF, OPT>();
     static_assert(D == 2 || D == 3, "two or three register sets");
-    V2<T> pxA[R], pfA[R], pxB[R], pfB[R], pxC[R], pfC[R];   // C unused (dead) when D = 2
-    V2<T> peA = z, peB = z, peC = z;   // the pair's second coarse row (in .x)
-    auto load_pair = [&](int p, V2<T> (&px)[R], V2<T> (&pf)[R], V2<T> &pe) {
+    using PV = PPV<T>;
+    const PV pz{};
+    PV pxA[R], pfA[R], pxB[R], pfB[R], pxC[R], pfC[R];   // C unused (dead) when D = 2
+    using PC = PPC<T>;
+    const PC cz{};
+    PC peA = cz, peB = cz, peC = cz;   // the pair's second coarse row (pairs: in .x)
+    auto load_coarse = [&](int m) {
+        if constexpr (QC) return buf_quad(reinterpret_cast<const float *>(a.ec) + (long long)m * Pc + cc0, nveq, t);
+        else {
+            PC v = cz;
+            v.x = buf_one<T>(a.ec + (long long)m * Pc + cc0, nve, t);
+            return v;
+        }
+    };
+    auto store_coarse = [&](int m, PC v) {
+        if constexpr (QC) {
+            if (t < ncq) *reinterpret_cast<float4 *>(&se[ring(m)][4 * t]) = v;
+        } else {
+            if (t < ncc) se[ring(m)][t] = v.x;
+        }
+    };
+    auto load_pair = [&](int p, PV (&px)[R], PV (&pf)[R], PC &pe) {
         #pragma unroll
         for (int q = 0; q < R; ++q) {
             const long long row = (long long)(i_begin + p * R + q) * P + L0;
-            px[q] = buf_row<T, 0>(a.phi + row, nvx, t);
-            if constexpr (!GENF) pf[q] = buf_row<T, 0>(a.f + row, nvx, t);
-        }
-        pe.x = buf_one<T>(a.ec + (long long)(m0 + p + 1) * Pc + cc0, nve, t);   // 2nd coarse row
-    };
-    auto store_pair = [&](int p, const V2<T> (&px)[R], const V2<T> (&pf)[R], V2<T> pe) {
-        if (t < npairs) {
-            #pragma unroll
-            for (int q = 0; q < R; ++q) {
-                *reinterpret_cast<V2<T> *>(&sx[p & 1][q][2 * t]) = px[q];
-                if constexpr (!GENF) *reinterpret_cast<V2<T> *>(&sf[p & 1][q][2 * t]) = pf[q];
+            if constexpr (Q) {
+                px[q] = buf_quad(reinterpret_cast<const float *>(a.phi) + row - SH, nvq, t);
+                if constexpr (!GENF) pf[q] = buf_quad(reinterpret_cast<const float *>(a.f) + row - SH, nvq, t);
+            } else {
+                px[q] = buf_row<T, 0>(a.phi + row, nvx, t);
+                if constexpr (!GENF) pf[q] = buf_row<T, 0>(a.f + row, nvx, t);
             }
         }
-        if (t < ncc) se[ring(m0 + p + 1)][t] = pe.x;
+        pe = load_coarse(m0 + p + 1);   // 2nd coarse row
+    };
+    auto store_pair = [&](int p, const PV (&px)[R], const PV (&pf)[R], PC pe) {
+        if (t < (Q ? nq4 : npairs)) {
+            #pragma unroll
+            for (int q = 0; q < R; ++q) {
+                *reinterpret_cast<PV *>(&sx[p & 1][q][(Q ? 4 : 2) * t]) = px[q];
+                if constexpr (!GENF) *reinterpret_cast<PV *>(&sf[p & 1][q][(Q ? 4 : 2) * t]) = pf[q];
+            }
+        }
+        store_coarse(m0 + p + 1, pe);
     };
     // prologue: pair 0 (+ its first coarse row) into slot 0; pairs 1 .. D in flight
     load_pair(0, pxA, pfA, peA);
-    if (t < ncc) se[ring(m0)][t] = buf_one<T>(a.ec + (long long)m0 * Pc + cc0, nve, t);
+    store_coarse(m0, load_coarse(m0));
     store_pair(0, pxA, pfA, peA);
     if (ng > 1) load_pair(1, pxB, pfB, peB);
     if constexpr (D == 3) {
@@ -1062,7 +1151,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     // pair gi: compute from slot gi & 1; pair gi+1 (set (gi+1) & 1) -> the other slot;
     // issue pair gi+3 into the set just freed; one barrier
     T wprev = T(0);   // dpp_shl(d2.x) of the previous restriction row (d0 starts as zero)
-    auto step = [&](int gi, V2<T> (&px)[R], V2<T> (&pf)[R], V2<T> &pe) {
+    auto step = [&](int gi, PV (&px)[R], PV (&pf)[R], PC &pe) {
         // keep the scheduler inside one pair: interleaving the unrolled pairs only raises
         // the register pressure (the loads of a pair are issued two pairs ahead anyway)
         __builtin_amdgcn_sched_barrier(0);
@@ -1079,12 +1168,12 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
         #pragma unroll
         for (int s = 0; s < R; ++s) {
             const int ii = i + s;
-            const V2<T> xr = ldv(&sx[slot][s][xo]);
+            const V2<T> xr = ldv(&sx[slot][s][xo + SH]);
             // f[ii]: from LDS, or (GENF) generated once here and carried in the f window
             // (regenerating it at every use instead: fewer VGPRs, 8 more multiplies per
             // row, measured slower in r01)
             V2<T> f0 = z;
-            if constexpr (!GENF) f0 = ldv(&sf[slot][s][xo]);
+            if constexpr (!GENF) f0 = ldv(&sf[slot][s][xo + SH]);
             if constexpr (GENF) {
                 const double sy = gsy_s(a.gsy, ii);
                 f0 = mk2<T>((T)(fxa * sy), (T)(fxb * sy));
@@ -1138,8 +1227,18 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
             // branch-free: rows outside the band get a zero-record descriptor, lanes that do
             // not own their pair an out-of-range offset (every step issues the same memory
             // instructions, so the compiler can count its waits)
-            buf_store_row<T, (OPT & 2) ? 1 : 0>(a.x4 + (long long)(ii - 4) * P + L0,
-                                               (ii - 4 >= olo && ii - 4 < ohi) ? xbytes : 0, xoff, h2);
+            {
+                const int xb = (ii - 4 >= olo && ii - 4 < ohi) ? xbytes : 0;
+                T *xrow = a.x4 + (long long)(ii - 4) * P + L0;
+                if constexpr (QS) {   // lane l+1's pair by DPP; odd lanes store the quad
+                    const float4 v4 = make_float4(h2.x, h2.y, dpp_shl(h2.x), dpp_shl(h2.y));
+                    buf_store_quad<(OPT & 2) ? 1 : 0>(reinterpret_cast<float *>(xrow), xb, xoff16, v4);
+                    if constexpr (EDGE)
+                        buf_store_row<T, (OPT & 2) ? 1 : 0>(xrow, xb, xoff8, h2);
+                } else {
+                    buf_store_row<T, (OPT & 2) ? 1 : 0>(xrow, xb, xoff8, h2);
+                }
+            }
             // r(x4) on row ii-5
             const V2<T> d2 = FAST ? rsum<T>(nsum<T>(h0, h1, h2, nbr<T>(h1)), h1, fq5, ih)
                                   : rsn<T>(h0, h1, h2, nbr<T>(h1), fq5, ih);
@@ -1206,9 +1305,9 @@ __global__ __launch_bounds__(64 * kPPWaves) __attribute__((amdgpu_waves_per_eu(2
 void k_postpre_lds(PostPreArgsT<T> a)
 {
     __shared__ double red[kPPWaves];
-    __shared__ __attribute__((aligned(16))) T sx[2][kPPR][kPPLdsRow];
-    __shared__ __attribute__((aligned(16))) T sf[2][kPPR][GENF ? 1 : kPPLdsRow];
-    __shared__ __attribute__((aligned(16))) T se[3][kPPLdsCoarse];
+    __shared__ __attribute__((aligned(16))) T sx[2][kPPR][pp_lds_row<T>()];
+    __shared__ __attribute__((aligned(16))) T sf[2][kPPR][GENF ? 1 : pp_lds_row<T>()];
+    __shared__ __attribute__((aligned(16))) T se[3][pp_lds_coarse<T>()];
     const Blk bk{(int)blockIdx.x, (int)blockIdx.y};
     const Cols k = lane_cols_t<kPPStride, kPPMargin>(a.N, bk.x);
     // the band's rows 2jcb-6 .. 2jce+5 (see postpre_lds_run): does it reach row 0 or N-1?

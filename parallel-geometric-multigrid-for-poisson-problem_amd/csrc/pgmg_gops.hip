@@ -564,10 +564,12 @@ void launch_g_copy_interior(const double *src, double *dst, int H, int W, hipStr
 //     side for the paired sweeps, which read two rows of halo) -> SR, one row per slot;
 //   * the columns at the boundary between column blocks e and e+1 (the single sweep: 2, the
 //     paired sweeps: 8 columns, contiguous) -> SC[(e*H + row)*K + k].
-// The waves of one workgroup read each other's edge columns; a barrier between an
-// iteration's loads (waited for) and its stores orders them: iteration i stores rows that no
-// wave loads in iteration i+1 or later.  launch_g_defer_scatter then writes the deferred
-// values into x (after the pass, in stream order): ~1 % of the points at N = 16385.
+// The waves of one workgroup read each other's edge columns.  BAR: a barrier between an
+// iteration's loads (waited for) and its stores orders them (iteration i stores rows that no
+// wave loads in iteration i+1 or later), and only the workgroup boundaries are deferred;
+// !BAR: no barrier, every WAVE boundary is deferred instead (2 of 128 columns for the single
+// sweep, 8 of 120 for the paired pass).  launch_g_defer_scatter then writes the deferred
+// values into x (after the pass, in stream order).
 // No wave leaves early (lanes past the grid shadow or load zeros), so every barrier is met.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void wait_loads_then_barrier()
@@ -576,7 +578,7 @@ __device__ __forceinline__ void wait_loads_then_barrier()
     __syncthreads();
 }
 
-template <int U, bool NT>
+template <int U, bool NT, bool BAR>
 __global__ __launch_bounds__(kBlock) void k_op_sweep_ip(double *X, const double *__restrict__ F,
                                                         double *__restrict__ SR,
                                                         double *__restrict__ SC, unsigned *reset,
@@ -600,9 +602,13 @@ __global__ __launch_bounds__(kBlock) void k_op_sweep_ip(double *X, const double 
     const int jb = 1 + blockIdx.y * rpb;
     const int je = min(jb + rpb, H - 1);
     const bool def_top = jb > 1, def_bot = je < H - 1;
-    // column-block boundaries: block e's last lane (.y) and block e+1's first lane (.x)
-    const bool def_l = threadIdx.x == 0 && blockIdx.x > 0;
-    const bool def_r = threadIdx.x == kBlock - 1 && blockIdx.x + 1 < gridDim.x;
+    // boundaries (BAR: of column blocks, else of waves) e: unit e's last lane (.y) and unit
+    // e+1's first lane (.x); a next unit exists iff its first pair is in the row
+    const int gw = t_raw >> 6;   // the wave's index along the row
+    const bool def_l = BAR ? (threadIdx.x == 0 && blockIdx.x > 0) : (lane == 0 && gw > 0);
+    const bool def_r = BAR ? (threadIdx.x == kBlock - 1 && blockIdx.x + 1 < gridDim.x)
+                           : (lane == 63 && 64 * (gw + 1) < npairs);
+    const long long ue = BAR ? (long long)blockIdx.x : (long long)gw;   // this lane's unit
     const long long Wl = W;
     double2 w0 = ldvu<double>(X + (long long)(jb - 1) * Wl + c);
     double2 w1 = ldvu<double>(X + (long long)jb * Wl + c);
@@ -617,7 +623,7 @@ __global__ __launch_bounds__(kBlock) void k_op_sweep_ip(double *X, const double 
             el[u] = ld_l ? X[r * Wl + c - 1] : 0.0;
             er[u] = ld_r ? X[r * Wl + c + 2] : 0.0;
         }
-        wait_loads_then_barrier();
+        if (BAR) wait_loads_then_barrier();
         #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int r = j + u;
@@ -635,8 +641,8 @@ __global__ __launch_bounds__(kBlock) void k_op_sweep_ip(double *X, const double 
                 const bool dt = def_top && r == jb, db = def_bot && r == je - 1;
                 if (dt) stvu<double>(SR + (long long)(2 * blockIdx.y) * Wl + c, o);
                 if (db) stvu<double>(SR + (long long)(2 * blockIdx.y + 1) * Wl + c, o);
-                if (def_l) SC[((long long)(blockIdx.x - 1) * H + r) * 2 + 1] = o.x;
-                if (def_r) SC[((long long)blockIdx.x * H + r) * 2] = o.y;
+                if (def_l) SC[((ue - 1) * H + r) * 2 + 1] = o.x;
+                if (def_r) SC[(ue * H + r) * 2] = o.y;
                 if (!dt && !db) {
                     double *q = X + (long long)r * Wl + c;
                     if (def_l) q[1] = o.y;
@@ -654,7 +660,7 @@ __global__ __launch_bounds__(kBlock) void k_op_sweep_ip(double *X, const double 
 // lanes 2..61 owned); the workgroup boundary columns are block e's last wave's lanes 60, 61
 // and block e+1's first wave's lanes 2, 3 (8 contiguous columns), the deferred rows two per
 // band side.
-template <int U, bool NT>
+template <int U, bool NT, bool BAR>
 __global__ __launch_bounds__(kBlock) void k_op_sweep2_ip(double *X, const double *__restrict__ F,
                                                          double *__restrict__ SR,
                                                          double *__restrict__ SC,
@@ -674,12 +680,23 @@ __global__ __launch_bounds__(kBlock) void k_op_sweep2_ip(double *X, const double
     // this lane's slot in the boundary buffer (-1: not a boundary column)
     int kc = -1;
     long long eb = 0;
-    if (wib == kWaves - 1 && (lane == 60 || lane == 61) && blockIdx.x + 1 < gridDim.x) {
-        kc = (lane - 60) * 2;
-        eb = blockIdx.x;
-    } else if (wib == 0 && (lane == 2 || lane == 3) && blockIdx.x > 0) {
-        kc = 4 + (lane - 2) * 2;
-        eb = blockIdx.x - 1;
+    if (BAR) {   // column-block boundaries
+        if (wib == kWaves - 1 && (lane == 60 || lane == 61) && blockIdx.x + 1 < gridDim.x) {
+            kc = (lane - 60) * 2;
+            eb = blockIdx.x;
+        } else if (wib == 0 && (lane == 2 || lane == 3) && blockIdx.x > 0) {
+            kc = 4 + (lane - 2) * 2;
+            eb = blockIdx.x - 1;
+        }
+    } else {     // wave boundaries (a next wave exists iff its first owned column is in the row)
+        const int nwaves = (W - 2 + kOv2Stride - 1) / kOv2Stride;
+        if ((lane == 60 || lane == 61) && wave + 1 < nwaves) {
+            kc = (lane - 60) * 2;
+            eb = wave;
+        } else if ((lane == 2 || lane == 3) && wave > 0 && wave < nwaves) {
+            kc = 4 + (lane - 2) * 2;
+            eb = wave - 1;
+        }
     }
     const int jb = 1 + blockIdx.y * rpb;
     const int je = min(jb + rpb, H - 1);   // x2 rows [jb, je)
@@ -708,7 +725,7 @@ __global__ __launch_bounds__(kBlock) void k_op_sweep2_ip(double *X, const double
             xn[u] = ldrow(X, r);
             fn[u] = ldrow(F, r);
         }
-        wait_loads_then_barrier();
+        if (BAR) wait_loads_then_barrier();
         #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int ii = i + u;
@@ -789,30 +806,41 @@ static OpGeom sweep2_ip_geom(int H, int W, int U)
 }
 
 // side buffer elements for either in-place pass at any of its row-step choices
+// boundaries between deferral units along a row: column blocks (BAR) or waves
+static int ip_bounds(const OpGeom &g, int W, bool pair, bool bar)
+{
+    if (bar) return g.gx > 1 ? g.gx - 1 : 0;
+    const int nw = pair ? (W - 2 + kOv2Stride - 1) / kOv2Stride : ((W - 1) / 2 + 63) / 64;
+    return nw > 1 ? nw - 1 : 0;
+}
+static bool ip_bar() { return tuning_int("PGMG_OPIP_BAR", 1) != 0; }
+static bool ip2_bar() { return tuning_int("PGMG_OP2IP_BAR", 1) != 0; }
+
 size_t g_defer_elems(int H, int W)
 {
     size_t m = 0;
     for (int U : {8, 16}) {
         const OpGeom a = sweep_ip_geom(H, W, U);
-        m = std::max(m, (size_t)a.gy * 2 * W + (size_t)(a.gx > 1 ? a.gx - 1 : 0) * H * 2);
+        for (bool bar : {false, true})
+            m = std::max(m, (size_t)a.gy * 2 * W + (size_t)ip_bounds(a, W, false, bar) * H * 2);
     }
     for (int U : {4, 8}) {
         const OpGeom b = sweep2_ip_geom(H, W, U);
-        m = std::max(m, (size_t)b.gy * 4 * W + (size_t)(b.gx > 1 ? b.gx - 1 : 0) * H * 8);
+        for (bool bar : {false, true})
+            m = std::max(m, (size_t)b.gy * 4 * W + (size_t)ip_bounds(b, W, true, bar) * H * 8);
     }
     return m + 64;
 }
 
 static void defer_scatter(double *x, const double *SR, const double *SC, const OpGeom &g, int R,
-                          int K, int ca, int cb, int H, int W, hipStream_t s)
+                          int nbound, int K, int ca, int cb, int H, int W, hipStream_t s)
 {
-    const long long n = std::max((long long)g.gy * 2 * R * (W - 2),
-                                 (long long)(g.gx - 1) * (H - 2));
+    const long long n = std::max((long long)g.gy * 2 * R * (W - 2), (long long)nbound * (H - 2));
     long long nb = (n + kBlock - 1) / kBlock;
-    if (nb > 1024) nb = 1024;
+    if (nb > 2048) nb = 2048;
     if (nb < 1) nb = 1;
     k_op_defer_scatter<<<dim3((unsigned)nb, 2), kBlock, 0, s>>>(x, SR, SC, H, W, g.rpb, g.gy, R,
-                                                                g.gx - 1, K, ca, cb);
+                                                                nbound, K, ca, cb);
 }
 
 void launch_g_sweep_ip(double *x, const double *f, double *side, unsigned *reset,
@@ -821,14 +849,21 @@ void launch_g_sweep_ip(double *x, const double *f, double *side, unsigned *reset
     const int U = tuning_int("PGMG_OPIP_U", 16) == 8 ? 8 : 16;
     const OpGeom g = sweep_ip_geom(H, W, U);
     const bool nt = tuning_int("PGMG_OP_NT", 1) != 0;
+    const bool bar = ip_bar();
     double *SR = side, *SC = side + (size_t)g.gy * 2 * W;
     const dim3 grid(g.gx, g.gy);
-#define PGMG_KI(UU, NTV) k_op_sweep_ip<UU, NTV><<<grid, kBlock, 0, s>>>(x, f, SR, SC, reset, stats, hh, H, W, g.rpb)
-    if (U == 8) { if (nt) PGMG_KI(8, true); else PGMG_KI(8, false); }
-    else { if (nt) PGMG_KI(16, true); else PGMG_KI(16, false); }
+#define PGMG_KI(UU, NTV, BR) k_op_sweep_ip<UU, NTV, BR><<<grid, kBlock, 0, s>>>(x, f, SR, SC, reset, stats, hh, H, W, g.rpb)
+    if (bar) {
+        if (U == 8) { if (nt) PGMG_KI(8, true, true); else PGMG_KI(8, false, true); }
+        else { if (nt) PGMG_KI(16, true, true); else PGMG_KI(16, false, true); }
+    } else {
+        if (U == 8) { if (nt) PGMG_KI(8, true, false); else PGMG_KI(8, false, false); }
+        else { if (nt) PGMG_KI(16, true, false); else PGMG_KI(16, false, false); }
+    }
 #undef PGMG_KI
-    // boundary e: columns 2 kBlock (e+1) and the next
-    defer_scatter(x, SR, SC, g, 1, 2, 2 * kBlock, 2 * kBlock, H, W, s);
+    // boundary e: columns 2 kBlock (e+1) and the next (waves: 128 (e+1) and the next)
+    const int cs = bar ? 2 * kBlock : 128;
+    defer_scatter(x, SR, SC, g, 1, ip_bounds(g, W, false, bar), 2, cs, cs, H, W, s);
 }
 
 void launch_g_sweep2_ip(double *x, const double *f, double *side, unsigned long long *stats,
@@ -837,16 +872,26 @@ void launch_g_sweep2_ip(double *x, const double *f, double *side, unsigned long 
     const int U = tuning_int("PGMG_OP2IP_U", 8) == 4 ? 4 : 8;
     const OpGeom g = sweep2_ip_geom(H, W, U);
     const bool nt = tuning_int("PGMG_OP_NT", 1) != 0;
+    const bool bar = ip2_bar();
     double *SR = side, *SC = side + (size_t)g.gy * 4 * W;
     const dim3 grid(g.gx, g.gy);
-#define PGMG_KI(UU, NTV) k_op_sweep2_ip<UU, NTV><<<grid, kBlock, 0, s>>>(x, f, SR, SC, stats, hh, H, W, g.rpb)
-    if (U == 4) { if (nt) PGMG_KI(4, true); else PGMG_KI(4, false); }
-    else { if (nt) PGMG_KI(8, true); else PGMG_KI(8, false); }
+#define PGMG_KI(UU, NTV, BR) k_op_sweep2_ip<UU, NTV, BR><<<grid, kBlock, 0, s>>>(x, f, SR, SC, stats, hh, H, W, g.rpb)
+    if (bar) {
+        if (U == 4) { if (nt) PGMG_KI(4, true, true); else PGMG_KI(4, false, true); }
+        else { if (nt) PGMG_KI(8, true, true); else PGMG_KI(8, false, true); }
+    } else {
+        if (U == 4) { if (nt) PGMG_KI(4, true, false); else PGMG_KI(4, false, false); }
+        else { if (nt) PGMG_KI(8, true, false); else PGMG_KI(8, false, false); }
+    }
 #undef PGMG_KI
-    // boundary e: block e's last wave w = kWaves (e+1) - 1, lanes 60, 61 -> columns
-    // kOv2Stride w + 117 ...; 8 columns
+    // boundary e: block e's last wave w = kWaves (e+1) - 1 (waves: w = e), lanes 60, 61 ->
+    // columns kOv2Stride w + 117 ...; 8 columns
     constexpr int kWaves = kBlock / 64;
-    defer_scatter(x, SR, SC, g, 2, 8, kOv2Stride * kWaves, kOv2Stride * (kWaves - 1) + 117, H, W, s);
+    if (bar)
+        defer_scatter(x, SR, SC, g, 2, ip_bounds(g, W, true, true), 8, kOv2Stride * kWaves,
+                      kOv2Stride * (kWaves - 1) + 117, H, W, s);
+    else
+        defer_scatter(x, SR, SC, g, 2, ip_bounds(g, W, true, false), 8, kOv2Stride, 117, H, W, s);
 }
 
 // ---------------------------------------------------------------------------

@@ -105,7 +105,8 @@ int pgmg_jacobi(double *d_x, double *d_tmp, const double *d_f, int H, int W, dou
     // flag slots: a fresh block of S+1 words per call would need a ring; the op is
     // synchronous w.r.t. its own flags because every launch is stream-ordered.
     unsigned *D = g_op.flags;
-    HIPC(hipMemsetAsync(g_op.stats, 0, 4 * sizeof(unsigned long long), s));
+    // the sweep counter is read back only for a caller that asks for it
+    if (sweeps_done) HIPC(hipMemsetAsync(g_op.stats, 0, 4 * sizeof(unsigned long long), s));
     const double hh = h * h, ih = 1.0 / (h * h);
     const int nb = g_blocks(H, W);
     if (nb > kOpPartialsCap) return set_err(PGMG_ERR_STATE, "pgmg_jacobi: too many blocks");

@@ -10,7 +10,7 @@ B=$PKG/build_v_$NAME
 mkdir -p $B
 HIPFLAGS="-O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fPIC -Wall -Wno-unused-result -I$PKG/../include -DPGMG_TUNING $FLAGS"
 pids=()
-for s in pgmg_fused pgmg_kernels pgmg_tail pgmg_gops pgmg_ctx pgmg_ops pgmg_comm; do
+for s in pgmg_fused pgmg_coarse pgmg_kernels pgmg_tail pgmg_gops pgmg_ctx pgmg_ops pgmg_comm; do
   /opt/rocm/bin/hipcc $HIPFLAGS -c $PKG/csrc/$s.hip -o $B/$s.o &
   pids+=($!)
 done

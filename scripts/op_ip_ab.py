@@ -37,22 +37,25 @@ pg.ops.rhs(f, h)
 tmp = torch.empty_like(x)
 byt = 24.0 * (n - 2) ** 2
 
-KNOBS = ("PGMG_OP_INPLACE", "PGMG_OPIP_U", "PGMG_OPIP_BLOCKS", "PGMG_OP2IP_U", "PGMG_OP2IP_BLOCKS")
-variants = [{"PGMG_OP_INPLACE": 0}, {"PGMG_OP_INPLACE": 1}]
+KNOBS = ("PGMG_OP_INPLACE", "PGMG_OPIP_U", "PGMG_OPIP_BLOCKS", "PGMG_OP2IP_U", "PGMG_OP2IP_BLOCKS",
+         "PGMG_OPIP_BAR", "PGMG_OP2IP_BAR")
+variants = [{"PGMG_OP_INPLACE": 0}, {"PGMG_OP_INPLACE": 1},
+            {"PGMG_OP_INPLACE": 1, "PGMG_OPIP_BAR": 0, "PGMG_OP2IP_BAR": 0}]
 if not args.quick:
-    for u, b in ((16, 512), (16, 2048), (8, 1024), (8, 2048)):
-        variants.append({"PGMG_OP_INPLACE": 1, "PGMG_OPIP_U": u, "PGMG_OPIP_BLOCKS": b})
-    for u, b in ((4, 1024), (4, 2048), (8, 512), (8, 2048), (8, 4096)):
-        variants.append({"PGMG_OP_INPLACE": 1, "PGMG_OP2IP_U": u, "PGMG_OP2IP_BLOCKS": b})
-
+    for u, b in ((16, 2048), (8, 1024), (8, 2048)):
+        variants.append({"PGMG_OP_INPLACE": 1, "PGMG_OPIP_BAR": 0, "PGMG_OPIP_U": u,
+                         "PGMG_OPIP_BLOCKS": b})
+    for u, b in ((4, 2048), (8, 2048)):
+        variants.append({"PGMG_OP_INPLACE": 1, "PGMG_OP2IP_BAR": 0, "PGMG_OP2IP_U": u,
+                         "PGMG_OP2IP_BLOCKS": b})
 
 def timed(v):
-    pg.ops.jacobi(x, f, h, v, eps=-1.0, tmp=tmp)
+    pg.ops.jacobi(x, f, h, v, eps=-1.0, tmp=tmp, count=os.environ.get("AB_COUNT") == "1")
     ts = []
     for _ in range(5):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
-        pg.ops.jacobi(x, f, h, v, eps=-1.0, tmp=tmp)
+        pg.ops.jacobi(x, f, h, v, eps=-1.0, tmp=tmp, count=os.environ.get("AB_COUNT") == "1")
         b.record()
         b.synchronize()
         ts.append(a.elapsed_time(b))
