@@ -138,7 +138,9 @@ template <class T> void launch_post_fixup(const FixArgsF &a, const PostArgsT<T> 
 template <class T>
 int launch_pre_rare(const FixArgsF &f, const PreArgsT<T> &a, bool x0_zero, hipStream_t s);
 template <class T> int launch_post_rare(const FixArgsF &f, const PostArgsT<T> &a, hipStream_t s);
-int postpre_blocks(int N, int jc0, int jc1);
+// k_postpre's workgroups (check partials); q4: the fp32 form k_postpre_q4 (launch_postpre of
+// an fp32 context; the F-cycle's smooth(3) keeps the 2-column kernel, q4 = false)
+int postpre_blocks(int N, int jc0, int jc1, bool q4 = false);
 template <class T> int launch_postpre(const PostPreArgsT<T> &a, hipStream_t s);
 // fused smooth(3): x4 of a.phi into a.x4 with the three checks' partial sums
 // (partials1 r(x1), partials3 r(x2), partials2 r(x3)); then the decision + rare path
