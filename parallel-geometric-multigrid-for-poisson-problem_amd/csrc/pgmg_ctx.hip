@@ -720,7 +720,7 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
     const T *in = c->x_in != nullptr ? static_cast<const T *>(c->x_in) : A;
     T *const xout = static_cast<T *>(c->x_out);
     const int np = fused_blocks(L.N, sr.jc0, sr.jc1);
-    const int npp = postpre_blocks(L.N, sr.jc0, sr.jc1, c->fp32);
+    const int npp = postpre_blocks(L.N, sr.jc0, sr.jc1, c->fp32 && pp_q4());
     FixArgsF fa{};
     fa.partials = c->partials;
     fa.np = np;
@@ -1099,7 +1099,7 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         nbk = fused_blocks(L.N, pr.jc0, pr.jc1);
         if (nbk > maxblocks) maxblocks = nbk;
         nbk = std::max(postpre_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2),
-                       postpre_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2, c->fp32));
+                       postpre_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2, c->fp32 && pp_q4()));
         if (nbk > maxblocks) maxblocks = nbk;
         nbk = std::max(tile_np(c, l, false), tile_np(c, l, true));
         if (nbk > maxblocks) maxblocks = nbk;
@@ -1885,7 +1885,7 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
 {
     Level &L0 = c->lv[0];
     const int np0 = fused_blocks(L0.N, L0.lo / 2, (L0.hi < L0.N ? L0.hi : L0.N - 1) / 2);
-    const int npp = c->cross ? postpre_blocks(L0.N, L0.lo / 2, (L0.hi < L0.N ? L0.hi : L0.N - 1) / 2, c->fp32) : 0;
+    const int npp = c->cross ? postpre_blocks(L0.N, L0.lo / 2, (L0.hi < L0.N ? L0.hi : L0.N - 1) / 2, c->fp32 && pp_q4()) : 0;
     long long d1, k1;
     spec_need_level(c, 1, gamma, &d1, &k1);
     // (level 0 visits level 1 gamma times per cycle)

@@ -139,8 +139,9 @@ template <class T>
 int launch_pre_rare(const FixArgsF &f, const PreArgsT<T> &a, bool x0_zero, hipStream_t s);
 template <class T> int launch_post_rare(const FixArgsF &f, const PostArgsT<T> &a, hipStream_t s);
 // k_postpre's workgroups (check partials); q4: the fp32 form k_postpre_q4 (launch_postpre of
-// an fp32 context; the F-cycle's smooth(3) keeps the 2-column kernel, q4 = false)
+// an fp32 context with pp_q4(); the F-cycle's smooth(3) keeps the 2-column kernel)
 int postpre_blocks(int N, int jc0, int jc1, bool q4 = false);
+bool pp_q4();   // fp32 launch_postpre runs k_postpre_q4 (PGMG_PPQ=1, measurement build only)
 template <class T> int launch_postpre(const PostPreArgsT<T> &a, hipStream_t s);
 // fused smooth(3): x4 of a.phi into a.x4 with the three checks' partial sums
 // (partials1 r(x1), partials3 r(x2), partials2 r(x3)); then the decision + rare path

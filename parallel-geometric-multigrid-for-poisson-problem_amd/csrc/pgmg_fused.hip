@@ -2014,6 +2014,14 @@ static int pp_target(int jc0, int jc1)
     return tuning_int("PGMG_PP_BLOCKS", (2048 / kPPWaves) * rounds);   // 512 resident at 4 waves
 }
 
+// fp32 contexts run k_postpre_q4 only with PGMG_PPQ=1 (measurement build).  Measured (r05,
+// scripts/pp_ab.py --dtype f32, profiles/r05_fp32/pp_f32_q4.jsonl, 3 interleaved rounds at
+// N = 16385, bitwise equal): 0.723-0.732 ms per launch (1536 workgroups; 2048 / 3072:
+// 0.706-0.716) against 0.650-0.653 for the 2-column k_postpre_lds<float>.  The quad lanes
+// need 221 VGPRs (2 waves per SIMD) where the 2-column fp32 pass fits 110 (4 waves per SIMD):
+// the occupancy it loses costs more than the halved per-lane row work saves.
+bool pp_q4() { return tuning_int("PGMG_PPQ", 0) != 0; }
+
 // k_postpre_q4's grid target (fp32): the same band height as the 2-column form's at
 // PGMG_PPQ_BLOCKS unset (half its workgroups: each covers twice the columns)
 static int ppq_target(int jc0, int jc1) { return tuning_int("PGMG_PPQ_BLOCKS", pp_target(jc0, jc1) / 2); }
@@ -2070,7 +2078,8 @@ static int postpre_q4_spans(const PostPreArgsT<float> &a, int t, int gx, int r)
 template <class T>
 int launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
 {
-    if constexpr (sizeof(T) == 4) {   // fp32: four columns per lane (k_postpre_q4)
+    if constexpr (sizeof(T) == 4) {
+      if (pp_q4()) {   // fp32: four columns per lane (k_postpre_q4, opt-in)
         int t, gx, gy, r;
         fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, kQStride, ppq_target(a0.jc0, a0.jc1),
                        kPPWaves);
@@ -2087,6 +2096,7 @@ int launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
             else k_postpre_q4<false, false><<<g, b, 0, s>>>(a);
         }
         return PGMG_OK;
+      }
     }
     int t, gx, gy, r;
     fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, kPPStride, pp_target(a0.jc0, a0.jc1),

@@ -40,13 +40,18 @@ def _f32_oracle(oracle_mod, kind, N, cycles, phi0=None, f=None, **kw):
                                            (129, 9, "fused"), (513, 65, "fused"),
                                            (129, 33, "unfused"), (257, 17, "cross"),
                                            (513, 65, "cross"), (129, 17, "norecompute"),
-                                           (2049, 65, "fused")])
+                                           (2049, 65, "fused"), (1025, 65, "cross"),
+                                           (2049, 33, "cross_stored"), (4097, 65, "cross")])
 def test_fp32_vcycle_bitwise_vs_fp32_oracle(pgmg, oracle_mod, plan, N, tail_n, mode):
     cfg = dict(dtype="f32", tail_n=tail_n)
     if mode == "unfused":
         cfg["flags"] = pgmg.PGMG_FLAG_UNFUSED
-    if mode == "cross":
+    if mode in ("cross", "cross_stored"):
+        # the cross-cycle finest pass (fp32: k_postpre_q4, four columns per lane; several
+        # column blocks from N = 1025 on, the analytic f regenerated or, stored, streamed)
         plan(cross_min_n=9)
+    if mode == "cross_stored":
+        cfg["flags"] = pgmg.PGMG_FLAG_STORED_RHS
     if mode == "norecompute":
         cfg["flags"] = pgmg.PGMG_FLAG_NO_RECOMPUTE
     cycles = 3
@@ -54,7 +59,7 @@ def test_fp32_vcycle_bitwise_vs_fp32_oracle(pgmg, oracle_mod, plan, N, tail_n, m
     with pgmg.Solver(N, **cfg) as s:
         assert s.elem_bytes == 4
         s.set_problem()
-        if mode == "cross":
+        if mode in ("cross", "cross_stored"):
             assert s.stats_detail()[2] >= 0, "cross-cycle fusion not active"
             s.vcycle(cycles)
         else:
@@ -119,10 +124,15 @@ def test_fp32_within_stated_tolerance_of_fp64(pgmg, N):
     assert d <= FP32_TOL[N], (N, d)
 
 
-def test_fp32_strips_bitwise_equal_single_gpu(pgmg):
+@pytest.mark.parametrize("exact", [False, True])
+def test_fp32_strips_bitwise_equal_single_gpu(pgmg, plan, exact):
     """Row strips (loopback transport, 4 ranks) in fp32: same words as one GPU in fp32
-    (halo rows and gathered levels move 4-byte elements)."""
+    (halo rows and gathered levels move 4-byte elements).  exact: every check decided
+    in-stream (PGMG_FLAG_EXACT_DIST) with the cross-cycle finest pass on, so the strips run
+    k_postpre_q4's third sum (R2)."""
     N, world = 1025, 4
+    if exact:
+        plan(cross_min_n=9, flags=pgmg.PGMG_FLAG_EXACT_DIST)
     with pgmg.Solver(N, dtype="f32") as s:
         s.set_problem()
         s.vcycle(3)
