@@ -562,8 +562,11 @@ void launch_g_copy_interior(const double *src, double *dst, int H, int W, hipStr
 // workgroup reads as an input is never written in place, it is deferred to a side buffer:
 //   * the band's edge rows (the band above reads row jb, the one below row je-1; two rows per
 //     side for the paired sweeps, which read two rows of halo) -> SR, one row per slot;
-//   * the columns at the boundary between column blocks e and e+1 (the single sweep: 2, the
-//     paired sweeps: 8 columns, contiguous) -> SC[(e*H + row)*K + k].
+//   * the columns at the boundary between column blocks e and e+1 -> SC[(e*H + row)*K + k]:
+//     the single sweep's 2 (block e's last column, block e+1's first), the paired pass's 4
+//     (two per side: an owned output two columns from the boundary reads x two columns
+//     across it; the next two columns the neighbour's edge lanes load reach only lanes that
+//     own nothing, so their values may be old or new).
 // The waves of one workgroup read each other's edge columns.  BAR: a barrier between an
 // iteration's loads (waited for) and its stores orders them (iteration i stores rows that no
 // wave loads in iteration i+1 or later), and only the workgroup boundaries are deferred;
@@ -657,9 +660,8 @@ __global__ __launch_bounds__(kBlock) void k_op_sweep_ip(double *X, const double 
 }
 
 // Two sweeps in one pass, in place: k_op_sweep2's wave tiles (128 columns loaded, the 120 of
-// lanes 2..61 owned); the workgroup boundary columns are block e's last wave's lanes 60, 61
-// and block e+1's first wave's lanes 2, 3 (8 contiguous columns), the deferred rows two per
-// band side.
+// lanes 2..61 owned); the boundary columns are block e's last wave's lane 61 and block e+1's
+// first wave's lane 2 (4 contiguous columns), the deferred rows two per band side.
 template <int U, bool NT, bool BAR>
 __global__ __launch_bounds__(kBlock) void k_op_sweep2_ip(double *X, const double *__restrict__ F,
                                                          double *__restrict__ SR,
@@ -681,20 +683,20 @@ __global__ __launch_bounds__(kBlock) void k_op_sweep2_ip(double *X, const double
     int kc = -1;
     long long eb = 0;
     if (BAR) {   // column-block boundaries
-        if (wib == kWaves - 1 && (lane == 60 || lane == 61) && blockIdx.x + 1 < gridDim.x) {
-            kc = (lane - 60) * 2;
+        if (wib == kWaves - 1 && lane == 61 && blockIdx.x + 1 < gridDim.x) {
+            kc = 0;
             eb = blockIdx.x;
-        } else if (wib == 0 && (lane == 2 || lane == 3) && blockIdx.x > 0) {
-            kc = 4 + (lane - 2) * 2;
+        } else if (wib == 0 && lane == 2 && blockIdx.x > 0) {
+            kc = 2;
             eb = blockIdx.x - 1;
         }
     } else {     // wave boundaries (a next wave exists iff its first owned column is in the row)
         const int nwaves = (W - 2 + kOv2Stride - 1) / kOv2Stride;
-        if ((lane == 60 || lane == 61) && wave + 1 < nwaves) {
-            kc = (lane - 60) * 2;
+        if (lane == 61 && wave + 1 < nwaves) {
+            kc = 0;
             eb = wave;
-        } else if ((lane == 2 || lane == 3) && wave > 0 && wave < nwaves) {
-            kc = 4 + (lane - 2) * 2;
+        } else if (lane == 2 && wave > 0 && wave < nwaves) {
+            kc = 2;
             eb = wave - 1;
         }
     }
@@ -739,7 +741,7 @@ __global__ __launch_bounds__(kBlock) void k_op_sweep2_ip(double *X, const double
                     const bool dt = def_top && r2 < jb + 2, db = def_bot && r2 >= je - 2;
                     if (dt) st_owned<false>(SR + (long long)(4 * blockIdx.y + (r2 - jb)) * Wl + c, z, ox, oy);
                     if (db) st_owned<false>(SR + (long long)(4 * blockIdx.y + 2 + r2 - (je - 2)) * Wl + c, z, ox, oy);
-                    if (kc >= 0) stvu<double>(SC + (eb * H + r2) * 8 + kc, z);
+                    if (kc >= 0) stvu<double>(SC + (eb * H + r2) * 4 + kc, z);
                     else if (!dt && !db) st_owned<NT>(X + (long long)r2 * Wl + c, z, ox, oy);
                 }
                 xa = xb;
@@ -753,45 +755,50 @@ __global__ __launch_bounds__(kBlock) void k_op_sweep2_ip(double *X, const double
     }
 }
 
-// The deferred outputs into x: blockIdx.y == 0 the band rows (nslot = 2R slots per band: the
-// first R rows of the band when a band lies above, the last R when one lies below), 1 the
-// column-block boundaries (K columns from col0(e) = ca*e + cb, rows 1 .. H-2).
+// The deferred outputs into x.  blockIdx.y < nslot (= gy * 2R): one band-row slot (the first R
+// rows of band by when a band lies above it, the last R when one lies below), the x blocks
+// striding over its columns; blockIdx.y >= nslot: one column-block boundary e (K columns from
+// col0(e) = ca*e + cb), the x blocks striding over rows 1 .. H-2.  No division in the loops.
 __global__ __launch_bounds__(kBlock) void k_op_defer_scatter(double *X, const double *SR,
                                                              const double *SC, int H, int W,
-                                                             int rpb, int gy, int R, int nbound,
-                                                             int K, int ca, int cb)
+                                                             int rpb, int gy, int R, int K,
+                                                             int ca, int cb)
 {
     const long long Wl = W;
-    const long long tid = (long long)blockIdx.x * kBlock + threadIdx.x;
-    const long long nthr = (long long)gridDim.x * kBlock;
-    if (blockIdx.y == 0) {
-        const long long n = (long long)gy * 2 * R * (W - 2);
-        for (long long k = tid; k < n; k += nthr) {
-            const int col = 1 + (int)(k % (W - 2));
-            const long long slot = k / (W - 2);
-            const int by = (int)(slot / (2 * R)), s = (int)(slot % (2 * R));
-            const int jb = 1 + by * rpb, je = min(jb + rpb, H - 1);
-            int row;
-            bool ok;
-            if (s < R) {
-                row = jb + s;
-                ok = jb > 1 && row < je;
-            } else {
-                row = je - R + (s - R);
-                ok = je < H - 1 && row >= jb;
-            }
-            if (ok) X[row * Wl + col] = SR[slot * Wl + col];
+    const int nslot = gy * 2 * R;
+    const int tid = blockIdx.x * kBlock + threadIdx.x, nthr = gridDim.x * kBlock;
+    if ((int)blockIdx.y < nslot) {
+        const int slot = blockIdx.y;
+        const int by = slot / (2 * R), sl = slot - by * 2 * R;
+        const int jb = 1 + by * rpb, je = min(jb + rpb, H - 1);
+        int row;
+        bool ok;
+        if (sl < R) {
+            row = jb + sl;
+            ok = jb > 1 && row < je;
+        } else {
+            row = je - R + (sl - R);
+            ok = je < H - 1 && row >= jb;
         }
+        if (!ok) return;
+        const double *src = SR + (long long)slot * Wl;
+        double *dst = X + row * Wl;
+        for (int col = 1 + tid; col <= W - 2; col += nthr) dst[col] = src[col];
     } else {
-        const long long n = (long long)nbound * (H - 2);
-        for (long long k = tid; k < n; k += nthr) {
-            const int e = (int)(k / (H - 2));
-            const int row = 1 + (int)(k % (H - 2));
-            const int c0 = ca * e + cb;
+        const int e = blockIdx.y - nslot;
+        const int c0 = ca * e + cb;
+        for (int row = 1 + tid; row <= H - 2; row += nthr) {
             const double *src = SC + ((long long)e * H + row) * K;
             double *dst = X + row * Wl + c0;
-            for (int q = 0; q < K; ++q)
-                if (c0 + q >= 1 && c0 + q <= W - 2) dst[q] = src[q];
+            for (int q = 0; q < K; q += 2) {
+                const double2 v = ldvu<double>(src + q);
+                if (c0 + q >= 1 && c0 + q + 1 <= W - 2) {
+                    stvu<double>(dst + q, v);
+                } else {
+                    if (c0 + q >= 1 && c0 + q <= W - 2) dst[q] = v.x;
+                    if (c0 + q + 1 >= 1 && c0 + q + 1 <= W - 2) dst[q + 1] = v.y;
+                }
+            }
         }
     }
 }
@@ -827,7 +834,7 @@ size_t g_defer_elems(int H, int W)
     for (int U : {4, 8}) {
         const OpGeom b = sweep2_ip_geom(H, W, U);
         for (bool bar : {false, true})
-            m = std::max(m, (size_t)b.gy * 4 * W + (size_t)ip_bounds(b, W, true, bar) * H * 8);
+            m = std::max(m, (size_t)b.gy * 4 * W + (size_t)ip_bounds(b, W, true, bar) * H * 4);
     }
     return m + 64;
 }
@@ -835,12 +842,12 @@ size_t g_defer_elems(int H, int W)
 static void defer_scatter(double *x, const double *SR, const double *SC, const OpGeom &g, int R,
                           int nbound, int K, int ca, int cb, int H, int W, hipStream_t s)
 {
-    const long long n = std::max((long long)g.gy * 2 * R * (W - 2), (long long)nbound * (H - 2));
-    long long nb = (n + kBlock - 1) / kBlock;
-    if (nb > 2048) nb = 2048;
-    if (nb < 1) nb = 1;
-    k_op_defer_scatter<<<dim3((unsigned)nb, 2), kBlock, 0, s>>>(x, SR, SC, H, W, g.rpb, g.gy, R,
-                                                                nbound, K, ca, cb);
+    const int nslot = g.gy * 2 * R;
+    // x blocks per slot / boundary: ~4 elements (rows) per thread
+    int bx = (std::max(W, H) + 4 * kBlock - 1) / (4 * kBlock);
+    if (bx < 1) bx = 1;
+    k_op_defer_scatter<<<dim3(bx, nslot + nbound), kBlock, 0, s>>>(x, SR, SC, H, W, g.rpb, g.gy, R,
+                                                                   K, ca, cb);
 }
 
 void launch_g_sweep_ip(double *x, const double *f, double *side, unsigned *reset,
@@ -884,14 +891,14 @@ void launch_g_sweep2_ip(double *x, const double *f, double *side, unsigned long 
         else { if (nt) PGMG_KI(8, true, false); else PGMG_KI(8, false, false); }
     }
 #undef PGMG_KI
-    // boundary e: block e's last wave w = kWaves (e+1) - 1 (waves: w = e), lanes 60, 61 ->
-    // columns kOv2Stride w + 117 ...; 8 columns
+    // boundary e: block e's last wave w = kWaves (e+1) - 1 (waves: w = e), lane 61 ->
+    // columns kOv2Stride w + 119 ...; 4 columns
     constexpr int kWaves = kBlock / 64;
     if (bar)
-        defer_scatter(x, SR, SC, g, 2, ip_bounds(g, W, true, true), 8, kOv2Stride * kWaves,
-                      kOv2Stride * (kWaves - 1) + 117, H, W, s);
+        defer_scatter(x, SR, SC, g, 2, ip_bounds(g, W, true, true), 4, kOv2Stride * kWaves,
+                      kOv2Stride * (kWaves - 1) + 119, H, W, s);
     else
-        defer_scatter(x, SR, SC, g, 2, ip_bounds(g, W, true, false), 8, kOv2Stride, 117, H, W, s);
+        defer_scatter(x, SR, SC, g, 2, ip_bounds(g, W, true, false), 4, kOv2Stride, 119, H, W, s);
 }
 
 // ---------------------------------------------------------------------------
