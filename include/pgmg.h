@@ -333,9 +333,12 @@ int pgmg_fused(pgmg_ctx *ctx, int *fused);
 int pgmg_bench_sweep(pgmg_ctx *ctx, int reps, double *ms_per_sweep);
 
 /* ---- op level (device pointers, reference layout, pitch = W) ------------- */
-/* v+1 sweeps; eps < 0 disables the early exit.  d_tmp: W*H scratch or NULL
- * (allocated internally).  *sweeps_done (may be NULL) receives the sweep count
- * (synchronous when non-NULL). */
+/* v+1 sweeps on d_x IN PLACE (Parallel::ComputeJacobi, Parallel_Method.cu:144-160; each
+ * sweep is exactly the out-of-place Jacobi sweep: tile-edge outputs another workgroup reads
+ * are deferred and scattered after each pass).  eps < 0 disables the early exit.  d_tmp: W*H
+ * scratch or NULL (allocated internally), used only by checked calls (eps >= 0) with v >= 1.
+ * *sweeps_done (may be NULL) receives the sweep count (synchronous when non-NULL; NULL keeps
+ * the call asynchronous on `stream`). */
 int pgmg_jacobi(double *d_x, double *d_tmp, const double *d_f, int H, int W, double h, int v,
                 double eps, int *sweeps_done, void *stream);
 int pgmg_residual(double *d_r, const double *d_x, const double *d_f, int H, int W, double h,

@@ -30,10 +30,11 @@ def child(args):
         kw.update(rank=args.rank, world=args.world, flags=kw.get("flags", 0) | pg.PGMG_FLAG_SOLO)
     with pg.Solver(args.n, **kw) as s:
         s.set_problem()
-        run = {"W": s.wcycle, "F": s.fcycle}.get(args.kind, s.vcycle)
-        run(3 if args.kind == "V" else 1)
+        run = {"W": s.wcycle, "F": s.fcycle, "G": s.wcycle}.get(args.kind, s.vcycle)
+        # G: BASELINE configs[4]'s shape -- one F-cycle (the FMG start), then the timed W call
+        (s.fcycle if args.kind == "G" else run)(3 if args.kind == "V" else 1)
         s.sync()
-        if args.kind == "F":   # a marker kernel before the timed call (F calls start variously)
+        if args.kind in ("F", "G"):   # a marker kernel before the timed call
             torch.full((64,), 1.0, device=f"cuda:{torch.cuda.current_device()}")
             torch.cuda.synchronize()
         run(args.cycles)
@@ -50,8 +51,8 @@ def parse(args):
         ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name, gx, gy))
     ks.sort()
     marks = [i for i, k in enumerate(ks) if "FillFunctor" in k[2]]
-    if args.kind == "F" and marks:
-        # F: the timed call is everything after the child's marker kernel
+    if args.kind in ("F", "G") and marks:
+        # F, G: the timed call is everything after the child's marker kernel
         seg = ks[marks[-1] + 1:]
     else:
         # the timed call starts at the first finest-level k_pre after the warmup call
@@ -90,7 +91,7 @@ if __name__ == "__main__":
     ap.add_argument("--n", type=int, default=16385)
     ap.add_argument("--cycles", type=int, default=10)
     ap.add_argument("--flags", type=int, default=0)
-    ap.add_argument("--kind", default="V", choices=["V", "W", "F"])
+    ap.add_argument("--kind", default="V", choices=["V", "W", "F", "G"])
     ap.add_argument("--world", type=int, default=1)
     ap.add_argument("--rank", type=int, default=0)
     a = ap.parse_args()
