@@ -334,10 +334,11 @@ static int enqueue_smooth(pgmg_ctx *c, int l, int which, int v, bool x0_zero)
 }
 
 template <class T>
-static int enqueue_tail_t(pgmg_ctx *c, int gamma, bool x0_from_global)
+static int enqueue_tail_t(pgmg_ctx *c, int gamma, bool x0_from_global, int visits = 1)
 {
     Level &Lt = c->lv[c->nb];
     TailArgsT<T> t{};
+    t.visits = visits;
     t.f_top = G<T>(Lt.F);
     t.e_top = G<T>(Lt.A);
     t.P_top = Lt.P;
@@ -383,6 +384,11 @@ static int enqueue_children(pgmg_ctx *c, int l, int gamma)
 {
     if (c->comm && l + 1 == c->comm->gathered_level())
         return c->comm->run_gathered(c, l + 1, gamma, gamma);
+    // the tail level: the gamma visits (same right-hand side, each from the previous one's
+    // result; the first from zero) in one launch -- at N = 32769 a W-cycle launches the tail
+    // 3^9 times, one launch per visit cost ~8 % of its time in launch overhead
+    if (l + 1 == c->nb && gamma > 1 && tuning_int("PGMG_TAIL_VISITS", 1) != 0)
+        return enqueue_tail_t<T>(c, gamma, false, gamma);
     for (int i = 0; i < gamma; ++i) {
         int e = enqueue_cycle_t<T>(c, l + 1, gamma, i == 0);
         if (e) return e;

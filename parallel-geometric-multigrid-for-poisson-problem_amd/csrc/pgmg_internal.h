@@ -155,6 +155,10 @@ struct TailArgsT {
     int N_top;
     double h_top;
     int x0_from_global;     // 1: start from e_top's contents; 0: from zero
+    // consecutive cycles on the top level with the same right-hand side (the W recursion's
+    // alpha visits from its parent, MultiGrid.hpp:126-128), each from the previous one's
+    // result, in ONE launch (0 or 1: one cycle)
+    int visits;
     int v1, v2, coarse_iter, n_coarse;
     double eps;
     unsigned long long *stats;

@@ -1282,7 +1282,8 @@ __global__ __launch_bounds__(kTailThreads) void k_tail(TailArgsDev<Real> d)
     int par = 0;
     const int last = d.nl - 1;
     if (!a.fmg) {
-        cnt += tail_gcycle<BlockTeam>(d, 0, 1, E, F, T, red, par);
+        for (int v = 0; v < max(1, a.visits); ++v)
+            cnt += tail_gcycle<BlockTeam>(d, 0, 1, E, F, T, red, par);
     } else {
         // compute_coarsest_grid: restrict phi down to the coarsest level
         for (int t = 0; t < last; ++t)

@@ -34,7 +34,7 @@ def child(args):
         # G: BASELINE configs[4]'s shape -- one F-cycle (the FMG start), then the timed W call
         (s.fcycle if args.kind == "G" else run)(3 if args.kind == "V" else 1)
         s.sync()
-        if args.kind in ("F", "G"):   # a marker kernel before the timed call
+        if args.kind in ("F", "G") or args.whole:   # a marker kernel before the timed call
             torch.full((64,), 1.0, device=f"cuda:{torch.cuda.current_device()}")
             torch.cuda.synchronize()
         run(args.cycles)
@@ -51,8 +51,9 @@ def parse(args):
         ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name, gx, gy))
     ks.sort()
     marks = [i for i, k in enumerate(ks) if "FillFunctor" in k[2]]
-    if args.kind in ("F", "G") and marks:
-        # F, G: the timed call is everything after the child's marker kernel
+    if (args.kind in ("F", "G") or args.whole) and marks:
+        # F, G, --whole: the timed call is everything after the child's marker kernel (a
+        # speculative V call may be split into segments, each starting with a level-0 k_pre)
         seg = ks[marks[-1] + 1:]
     else:
         # the timed call starts at the first finest-level k_pre after the warmup call
@@ -93,6 +94,8 @@ if __name__ == "__main__":
     ap.add_argument("--flags", type=int, default=0)
     ap.add_argument("--kind", default="V", choices=["V", "W", "F", "G"])
     ap.add_argument("--world", type=int, default=1)
+    ap.add_argument("--whole", action="store_true",
+                    help="V: the whole timed call (marker kernel before it), not the last segment")
     ap.add_argument("--rank", type=int, default=0)
     a = ap.parse_args()
     if a.child:
