@@ -4,8 +4,8 @@
     python scripts/pp_ab.py [--n 16385] [--rounds 3] NAME=LIB[:VAR=v[,VAR=v...]] ...
 
 LIB is a libpgmg build (e.g. parallel-.../libpgmg_ab.so, built with `make ab`); VAR=v are
-environment knobs the measurement build reads (pgmg_internal.h: tuning_int), or AB_FLAGS=n:
-PGMG_FLAG_* bits OR-ed into the solver's flags.  Every
+environment knobs the measurement build reads (pgmg_internal.h: tuning_int), AB_FLAGS=n:
+PGMG_FLAG_* bits OR-ed into the solver's flags, or AB_TAIL_N=n: the solver's tail_n.  Every
 variant runs in its own process (set_problem, 2 warmup V-cycles, 20 timed in one call
 with per-pass hipEvents); the rounds interleave the variants so box drift hits all alike.
 Prints one JSON line per run: k_postpre / k_pre / k_post ms per launch, ms per V-cycle,
@@ -28,7 +28,8 @@ import _pkgload
 pg = _pkgload.load()
 N = %(n)d
 K = %(steps)d
-with pg.Solver(N, flags=pg.PGMG_FLAG_TIME_FINE | int(os.environ.get("AB_FLAGS", "0")), dtype=%(dtype)r) as s:
+kw = {"tail_n": int(os.environ["AB_TAIL_N"])} if os.environ.get("AB_TAIL_N") else {}
+with pg.Solver(N, flags=pg.PGMG_FLAG_TIME_FINE | int(os.environ.get("AB_FLAGS", "0")), dtype=%(dtype)r, **kw) as s:
     s.set_problem()
     run = {"V": s.vcycle, "W": s.wcycle, "F": s.fcycle}[%(kind)r]
     run(2); s.sync()
