@@ -190,12 +190,12 @@ def pmc_child(args):
 # algorithmic bytes per interior point of each op (fine grid n = (N-2)^2,
 # coarse nc = (Nc-2)^2): Jacobi sweep 24 (read x, f; write x_new), residual 24, restriction
 # 8 per fine + 8 per coarse point, prolongation 16 per fine (RMW) + 8 per coarse point
-def op_cases(pg, n):
+def op_cases(pg, n, device="cuda:0"):
     """The per-op study (ParallelTestRunner.cu:231-468 times ComputeJacobi(v = 100),
     ComputeResidual, ComputeRestriction, ComputeProlungator) on reference-layout device arrays
     at grid n: [(name, call, bytes per call, kernel keys, sweeps)], and the arrays."""
     import torch
-    dev = torch.device("cuda:0")
+    dev = torch.device(device)
     h = 1.0 / (n - 1)
     nc = (n - 1) // 2 + 1
     fine, coarse = float((n - 2) ** 2), float((nc - 2) ** 2)
@@ -216,6 +216,9 @@ def op_cases(pg, n):
                         k.startswith("k_op_sweep_ip") or k.startswith("k_op_sweep2_ip"))
             return k.startswith("k_op_sweep<")   # v = 1 checked: two ping-pong sweeps
         return m
+
+    def named(prefix):
+        return lambda k: k.startswith(prefix)
 
     cases = [
         ("jacobi v=0 (one sweep in place on x: k_op_sweep_ip + the scatter of its deferred "

@@ -61,3 +61,36 @@ def test_bench_options_listed():
     for opt in ("--gpus", "--steps", "--warmup", "--big-grid", "--other-configs", "--cycle",
                 "--save-profiles", "--trace", "--pmc", "--cpu-baseline", "--ops"):
         assert opt in r.stdout, opt
+
+
+def test_op_cases_build_and_match_kernel_names():
+    """bench.py's per-op study table builds (every case callable) and each case's trace-key
+    matcher picks the kernels that call launches (bench.kernel_key form: no spaces) -- a stub library on the CPU,
+    no GPU."""
+    import importlib
+    sys.path.insert(0, str(ROOT))
+    bench = importlib.import_module("bench")
+
+    class Ops:
+        def __getattr__(self, name):
+            return lambda *a, **k: None
+
+    class PG:
+        ops = Ops()
+        PGMG_PROLONG_SYMMETRIC, PGMG_PROLONG_REFERENCE = 1, 0
+
+    cases, keep = bench.op_cases(PG(), 33, device="cpu")
+    assert len(cases) == 8 and len(keep) == 6
+    for _, call, nbytes, keys, sweeps in cases:
+        call()
+        assert nbytes > 0 and callable(keys)
+    names = {
+        0: "k_op_sweep_ip<16,true,true>", 1: "k_op_sweep2_ip<8,true,true>",
+        2: "k_op_sweep2_ip<8,true,true>", 3: "k_op_sweep<16,true,false,true>",
+        4: "k_op_residual<16>", 5: "k_op_restrict<8>", 6: "k_op_prolong<1>", 7: "k_op_prolong<0>",
+    }
+    for i, k in names.items():
+        assert cases[i][3](k), (i, k)
+    assert not cases[0][3]("k_op_sweep2_ip<8,true,true>")
+    assert not cases[1][3]("k_op_sweep_ip<16,true,true>")
+    assert cases[2][3]("k_op_sweep_ip<16,true,true>")
