@@ -23,6 +23,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=16385)
 ap.add_argument("--rounds", type=int, default=2)
 ap.add_argument("--quick", action="store_true", help="defaults and the ping-pong form only")
+ap.add_argument("--only-inplace", action="store_true", help="the in-place default only")
 args = ap.parse_args()
 
 import torch  # noqa: E402
@@ -41,7 +42,9 @@ KNOBS = ("PGMG_OP_INPLACE", "PGMG_OPIP_U", "PGMG_OPIP_BLOCKS", "PGMG_OP2IP_U", "
          "PGMG_OPIP_BAR", "PGMG_OP2IP_BAR")
 variants = [{"PGMG_OP_INPLACE": 0}, {"PGMG_OP_INPLACE": 1},
             {"PGMG_OP_INPLACE": 1, "PGMG_OPIP_BAR": 0, "PGMG_OP2IP_BAR": 0}]
-if not args.quick:
+if args.only_inplace:
+    variants = [{"PGMG_OP_INPLACE": 1}]
+elif not args.quick:
     for u, b in ((16, 2048), (8, 1024), (8, 2048)):
         variants.append({"PGMG_OP_INPLACE": 1, "PGMG_OPIP_BAR": 0, "PGMG_OPIP_U": u,
                          "PGMG_OPIP_BLOCKS": b})
