@@ -759,7 +759,6 @@ __global__ __launch_bounds__(kBlock) void k_op_sweep2_ip(double *X, const double
 // rows of band by when a band lies above it, the last R when one lies below), the x blocks
 // striding over its columns; blockIdx.y >= nslot: one column-block boundary e (K columns from
 // col0(e) = ca*e + cb), the x blocks striding over rows 1 .. H-2.  No division in the loops.
-template <bool FULL>
 __global__ __launch_bounds__(kBlock) void k_op_defer_scatter(double *X, const double *SR,
                                                              const double *SC, int H, int W,
                                                              int rpb, int gy, int R, int K,
@@ -791,27 +790,6 @@ __global__ __launch_bounds__(kBlock) void k_op_defer_scatter(double *X, const do
         for (int row = 1 + tid; row <= H - 2; row += nthr) {
             const double *src = SC + ((long long)e * H + row) * K;
             double *dst = X + row * Wl + c0;
-            if (FULL) {
-                // whole 64-byte segments: the K deferred values merged into the segments'
-                // current contents (the pass's in-place values), so the memory sees full-segment
-                // writes instead of 8/16-byte partial ones (a read-modify-write each).  A
-                // deferred ROW's segments are the row slots' (skipped here: no race on them).
-                const int band = (row - 1) / rpb, jb = 1 + band * rpb, je = min(jb + rpb, H - 1);
-                if ((jb > 1 && row < jb + R) || (je < H - 1 && row >= je - R)) continue;
-                const uintptr_t a0 = (uintptr_t)dst & ~(uintptr_t)63;
-                const uintptr_t a1 = ((uintptr_t)(dst + K) + 63) & ~(uintptr_t)63;
-                // segments reaching past this row's columns 1 .. W-2 (another row may be a
-                // deferred row its slot rewrites concurrently): the partial writes below
-                const bool inrow = a0 >= (uintptr_t)(dst - c0 + 1) && a1 <= (uintptr_t)(dst - c0 + W - 1);
-                for (uintptr_t a = a0; inrow && a < a1; a += 16) {
-                    double2 v = *reinterpret_cast<const double2 *>(a);
-                    const long long q0 = (long long)((double *)a - dst);
-                    if (q0 >= 0 && q0 < K && c0 + q0 >= 1 && c0 + q0 <= W - 2) v.x = src[q0];
-                    if (q0 + 1 >= 0 && q0 + 1 < K && c0 + q0 + 1 >= 1 && c0 + q0 + 1 <= W - 2) v.y = src[q0 + 1];
-                    *reinterpret_cast<double2 *>(a) = v;
-                }
-                if (inrow) continue;
-            }
             for (int q = 0; q < K; q += 2) {
                 const double2 v = ldvu<double>(src + q);
                 if (c0 + q >= 1 && c0 + q + 1 <= W - 2) {
@@ -865,20 +843,20 @@ static void defer_scatter(double *x, const double *SR, const double *SC, const O
                           int nbound, int K, int ca, int cb, int H, int W, hipStream_t s)
 {
     const int nslot = g.gy * 2 * R;
-    // x blocks per slot / boundary: ~4 elements (rows) per thread
-    int bx = (std::max(W, H) + tuning_int("PGMG_SCAT_PER", 4) * kBlock - 1) /
-             (tuning_int("PGMG_SCAT_PER", 4) * kBlock);
+    // x blocks per slot / boundary: ~16 elements (rows) per thread.  Measured (r05,
+    // profiles/r05_ops/scatter_ab.txt, kernel trace at 16385): 16 per thread 26.6 / 36.2 us for
+    // the single / paired pass's scatter against 28.2 / 60.0 with 4 and 42 / 74 with 64 -- the
+    // boundary columns' scattered 16-byte writes (one row each) go faster with fewer writers in
+    // flight; writing whole 64-byte segments (merged with the pass's in-place values) instead:
+    // 63-153 / 99-208 us, not kept
+    const int per = tuning_int("PGMG_SCAT_PER", 16);
+    int bx = (std::max(W, H) + per * kBlock - 1) / (per * kBlock);
     if (bx < 1) bx = 1;
     // measurement build only: PGMG_SCAT_PART = 1 rows only, 2 columns only (wrong results)
     const int part = tuning_int("PGMG_SCAT_PART", 0);
     if (part == 1) nbound = 0;
-    const dim3 grid(bx, part == 2 ? nbound : nslot + nbound);
-    if (tuning_int("PGMG_SCAT_FULL", 0))
-        k_op_defer_scatter<true><<<grid, kBlock, 0, s>>>(x, SR, SC, H, W, g.rpb, part == 2 ? 0 : g.gy,
-                                                         R, K, ca, cb);
-    else
-        k_op_defer_scatter<false><<<grid, kBlock, 0, s>>>(x, SR, SC, H, W, g.rpb, part == 2 ? 0 : g.gy,
-                                                          R, K, ca, cb);
+    k_op_defer_scatter<<<dim3(bx, part == 2 ? nbound : nslot + nbound), kBlock, 0, s>>>(
+        x, SR, SC, H, W, g.rpb, part == 2 ? 0 : g.gy, R, K, ca, cb);
 }
 
 void launch_g_sweep_ip(double *x, const double *f, double *side, unsigned *reset,
