@@ -885,6 +885,9 @@ constexpr int kPPLdsCoarse = kPPWaves * (kPPStride / 2) + kPPMargin + 8;     // 
 // 0.675-0.687 with quad loads (2 waves of 4 do all the loading, ds_write_b128), 0.647-0.649
 // with quad stores only -- the knobs stay off; the pass's cost for fp32 is its per-lane work
 // on 2 columns, not the load width.
+#ifndef PGMG_PP_CHEAPCHK
+#define PGMG_PP_CHEAPCHK 0
+#endif
 #ifndef PGMG_F32_QLOAD
 #define PGMG_F32_QLOAD 0
 #endif
@@ -1190,7 +1193,11 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
             // and a check
             const V2<T> sb = FAST ? nsum<T>(b0, b1, b2, nb1) : z;
             {   // post check: r(x1) on row ii-2
+#if PGMG_PP_CHEAPCHK   // measurement only: what the checks' residuals cost (the sums are wrong)
+                const V2<T> r1 = b1;
+#else
                 const V2<T> r1 = FAST ? rsum<T>(sb, b1, fq2, ih) : rsn<T>(b0, b1, b2, nb1, fq2, ih);
+#endif
                 const int row = ii - 2;
                 if (row >= olo && row < ohi && k.own) {
                     acc1 = sqacc(acc1, r1.x);
@@ -1213,7 +1220,11 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                                   : jsh<T, EDGE>(c0, c1, c2, nc1, hq3, k, boundary_row(ii - 3, N));
             const V2<T> sgg = FAST ? nsum<T>(g0, g1, g2, ng1) : z;
             {   // pre check: r(x3) on row ii-4
+#if PGMG_PP_CHEAPCHK
+                const V2<T> r3 = g1;
+#else
                 const V2<T> r3 = FAST ? rsum<T>(sgg, g1, fq4, ih) : rsn<T>(g0, g1, g2, ng1, fq4, ih);
+#endif
                 const int row = ii - 4;
                 if (row >= olo && row < ohi && k.own) {
                     acc2 = sqacc(acc2, r3.x);
