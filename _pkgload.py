@@ -17,3 +17,22 @@ def load():
     sys.modules[NAME] = mod
     spec.loader.exec_module(mod)
     return mod
+
+
+def source_hash():
+    """The hash the Makefile stamps into libpgmg.so (pgmg_source_hash), computed over this
+    tree: sha256 of csrc/<SRCS> and csrc/*.h and include/pgmg.h concatenated in path order
+    (the Makefile's $(sort ...) of the same path strings), first 16 hex digits."""
+    import hashlib
+    import re
+    here = str(PKG_DIR) + "/"
+    mk = (PKG_DIR / "Makefile").read_text()
+    srcs = re.search(r"^SRCS = (.*)$", mk, re.M).group(1).split()
+    paths = [here + "csrc/" + x for x in srcs]
+    paths += [str(p) for p in sorted((PKG_DIR / "csrc").glob("*.h"))]
+    paths.append(here + "../include/pgmg.h")
+    h = hashlib.sha256()
+    for p in sorted(set(paths)):
+        h.update(pathlib.Path(p).read_bytes())
+    return h.hexdigest()[:16]
+

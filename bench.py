@@ -152,6 +152,20 @@ def cpu_baseline(n, cycles=1, kind="V", skip=0):
                       f"{t:.4f} s per {kind}-cycle; host {_cpu_model()}, {os.cpu_count()} CPUs"}
 
 
+def build_sources():
+    """Which sources the loaded libpgmg.so was built from (its pgmg_source_hash stamp) against
+    the sources of this tree (_pkgload.source_hash): a prebuilt library that travelled with the
+    tree is shown to match it, or not."""
+    try:
+        import _pkgload
+        pg = _pkgload.load()
+        lib = pg.load().pgmg_source_hash().decode()
+        tree = _pkgload.source_hash()
+        return {"library": lib, "tree": tree, "match": lib == tree}
+    except Exception as e:  # reported, never fatal
+        return {"error": str(e)[:200]}
+
+
 def lib_build_id():
     """sha256 prefix of the libpgmg.so this run loads (names the build a profile measured)."""
     import hashlib
@@ -931,6 +945,7 @@ def main():
             "pmc": pmc_note,
             "trace": trace_note,
             "build": lib_build_id(),
+            "build_sources": build_sources(),
         }
         if others is not None:
             line["other_configs"] = others

@@ -26,8 +26,9 @@
  *   op level (caller-owned device arrays in the reference's row-major layout,
  *   element (y, x) at p[y*W + x]; the optional `stream` is a hipStream_t)
  *     pgmg_jacobi    Parallel::ComputeJacobi       3_part_parallel/Parallel_Method.cu:144-160
- *                    (numerics of JacobiSmoother::smooth, Smoother.hpp:38-116: v+1
- *                    out-of-place sweeps with the residual-norm early exit)
+ *                    (in place on d_x like the reference's, each sweep exactly the
+ *                    out-of-place sweep; numerics of JacobiSmoother::smooth,
+ *                    Smoother.hpp:38-116: v+1 sweeps with the residual-norm early exit)
  *     pgmg_residual  Parallel::ComputeResidual     Parallel_Method.cu:162-173
  *                    (DynamicGridUtils::compute_residual, DynamicGridUtils.hpp:59-69)
  *     pgmg_restrict  Parallel::ComputeRestriction  Parallel_Method.cu:175-186
@@ -394,6 +395,9 @@ int pgmg_plan_strips(int N, int world, int rank, int tail_n, int gather_n, int *
 
 const char *pgmg_last_error(void);
 const char *pgmg_version(void);
+/* First 16 hex digits of the sha256 of the sources this library was built from (the csrc .hip
+ * and .h files, include/pgmg.h, concatenated in path order; Makefile "srchash"). */
+const char *pgmg_source_hash(void);
 
 #ifdef __cplusplus
 }

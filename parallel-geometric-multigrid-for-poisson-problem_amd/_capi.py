@@ -150,6 +150,7 @@ SIGNATURES = [
                                    C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("pgmg_last_error", C.c_char_p, []),
     ("pgmg_version", C.c_char_p, []),
+    ("pgmg_source_hash", C.c_char_p, []),
 ]
 
 _lib = None

@@ -101,3 +101,11 @@ def test_retired_flag_bits_rejected(pgmg, bit):
     h = C.c_void_p()
     assert lib.pgmg_create(C.byref(h), C.byref(cfg)) == -1   # PGMG_ERR_ARG
     assert not h.value
+
+
+def test_library_built_from_this_tree(pgmg):
+    """libpgmg.so carries the hash of the sources it was built from (Makefile "srchash"); it
+    must equal this tree's, so the library the GPU box loads is the one these sources make."""
+    import _pkgload
+    assert pgmg.load().pgmg_source_hash().decode() == _pkgload.source_hash()
+
