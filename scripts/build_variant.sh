@@ -15,6 +15,8 @@ for s in pgmg_fused pgmg_coarse pgmg_kernels pgmg_tail pgmg_gops pgmg_ctx pgmg_o
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait $p; done
+printf 'extern "C" const char *pgmg_source_hash(void) { return "variant-%s"; }\n' $NAME > $B/srchash.cpp
+g++ -O2 -fPIC -c $B/srchash.cpp -o $B/srchash.o
 /opt/rocm/bin/hipcc $HIPFLAGS $B/*.o -shared -L/opt/rocm/lib -lamdhip64 -lrccl -Wl,-rpath,/opt/rocm/lib -o $PKG/libpgmg_$NAME.so
 rm -rf $B
 echo "built $PKG/libpgmg_$NAME.so"
