@@ -581,8 +581,8 @@ __device__ __forceinline__ void wait_loads_then_barrier()
     __syncthreads();
 }
 
-template <int U, bool NT, bool BAR>
-__global__ __launch_bounds__(kBlock) void k_op_sweep_ip(double *X, const double *__restrict__ F,
+template <int U, bool NT, bool BAR, int NTH = kBlock>
+__global__ __launch_bounds__(NTH) void k_op_sweep_ip(double *X, const double *__restrict__ F,
                                                         double *__restrict__ SR,
                                                         double *__restrict__ SC, unsigned *reset,
                                                         unsigned long long *stats, double hh,
@@ -594,7 +594,7 @@ __global__ __launch_bounds__(kBlock) void k_op_sweep_ip(double *X, const double 
     }
     const int lane = threadIdx.x & 63;
     const int npairs = (W - 1) >> 1;
-    const int t_raw = blockIdx.x * kBlock + threadIdx.x;
+    const int t_raw = blockIdx.x * NTH + threadIdx.x;
     const bool act = t_raw < npairs;
     const int t = act ? t_raw : npairs - 1;  // idle lanes shadow the last pair (no stores)
     const int c = 1 + 2 * t;
@@ -609,7 +609,7 @@ __global__ __launch_bounds__(kBlock) void k_op_sweep_ip(double *X, const double 
     // e+1's first lane (.x); a next unit exists iff its first pair is in the row
     const int gw = t_raw >> 6;   // the wave's index along the row
     const bool def_l = BAR ? (threadIdx.x == 0 && blockIdx.x > 0) : (lane == 0 && gw > 0);
-    const bool def_r = BAR ? (threadIdx.x == kBlock - 1 && blockIdx.x + 1 < gridDim.x)
+    const bool def_r = BAR ? (threadIdx.x == NTH - 1 && blockIdx.x + 1 < gridDim.x)
                            : (lane == 63 && 64 * (gw + 1) < npairs);
     const long long ue = BAR ? (long long)blockIdx.x : (long long)gw;   // this lane's unit
     const long long Wl = W;
@@ -662,8 +662,8 @@ __global__ __launch_bounds__(kBlock) void k_op_sweep_ip(double *X, const double 
 // Two sweeps in one pass, in place: k_op_sweep2's wave tiles (128 columns loaded, the 120 of
 // lanes 2..61 owned); the boundary columns are block e's last wave's lane 61 and block e+1's
 // first wave's lane 2 (4 contiguous columns), the deferred rows two per band side.
-template <int U, bool NT, bool BAR>
-__global__ __launch_bounds__(kBlock) void k_op_sweep2_ip(double *X, const double *__restrict__ F,
+template <int U, bool NT, bool BAR, int NTH = kBlock>
+__global__ __launch_bounds__(NTH) void k_op_sweep2_ip(double *X, const double *__restrict__ F,
                                                          double *__restrict__ SR,
                                                          double *__restrict__ SC,
                                                          unsigned long long *stats, double hh,
@@ -671,10 +671,10 @@ __global__ __launch_bounds__(kBlock) void k_op_sweep2_ip(double *X, const double
 {
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && stats != nullptr)
         atomicAdd(&stats[0], 2ull);
-    constexpr int kWaves = kBlock / 64;
+    constexpr int kWaves = NTH / 64;
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;
-    const int wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int wave = (blockIdx.x * NTH + threadIdx.x) >> 6;
     const int c = kOv2Stride * wave - 3 + 2 * lane;
     const bool inx = c >= 1 && c <= W - 2, iny = c + 1 >= 1 && c + 1 <= W - 2;
     const bool mid = lane >= 2 && lane <= 61;
@@ -803,13 +803,34 @@ __global__ __launch_bounds__(kBlock) void k_op_defer_scatter(double *X, const do
     }
 }
 
-static OpGeom sweep_ip_geom(int H, int W, int U)
+// The single in-place sweep: 512-thread workgroups (8 waves; half the column-block boundaries
+// to defer of 256) and 512 of them (one per CU at 217 VGPRs).  Measured at 16385 (r05,
+// scripts/op_ip_ab.py --nth, profiles/r05_ops/op_ip_nth.jsonl, 3 interleaved rounds): one-sweep
+// call 1.320-1.329 ms against 1.382-1.398 with 256 threads x 1024 (1.333-1.336 at 512 x 1024,
+// 1.359-1.364 with 8 rows in flight); PGMG_OPIP_NTH=256 in the measurement build for the form
+// before.
+static int ip_nth() { return tuning_int("PGMG_OPIP_NTH", 512) == 256 ? 256 : 512; }
+static OpGeom sweep_ip_geom(int H, int W, int U, int nth = 512)
 {
-    return op_geom((W - 1) / 2, H - 2, U, tuning_int("PGMG_OPIP_BLOCKS", 1024));
+    // op_geom counts columns in workgroups of kBlock lanes: scale the pair count
+    OpGeom g = op_geom(((W - 1) / 2 + nth / kBlock - 1) / (nth / kBlock), H - 2, U,
+                       tuning_int("PGMG_OPIP_BLOCKS", nth == 512 ? 512 : 1024));
+    g.gx = ((W - 1) / 2 + nth - 1) / nth;
+    return g;
 }
-static OpGeom sweep2_ip_geom(int H, int W, int U)
+// the paired pass keeps 256-thread workgroups: 512 measured slower (r05, op_ip_nth.jsonl: two
+// sweeps 1.44-1.48 ms at 512 / 1024 workgroups, 1.41-1.42 at 2048, against 1.377-1.389)
+static int ip2_nth() { return tuning_int("PGMG_OP2IP_NTH", 256) == 512 ? 512 : 256; }
+static OpGeom sweep2_ip_geom(int H, int W, int U, int nth = 256)
 {
-    return sweep2_geom(H, W, U, tuning_int("PGMG_OP2IP_BLOCKS", 1024));
+    OpGeom g = sweep2_geom(H, W, U, tuning_int("PGMG_OP2IP_BLOCKS", 1024));
+    if (nth != kBlock) {   // the same bands' worth of workgroups, each nth / 64 waves wide
+        const int waves = (W - 2 + kOv2Stride - 1) / kOv2Stride;
+        g = op_geom(((waves * 64) + nth / kBlock - 1) / (nth / kBlock), H - 2, U,
+                    tuning_int("PGMG_OP2IP_BLOCKS", 1024));
+        g.gx = (waves * 64 + nth - 1) / nth;
+    }
+    return g;
 }
 
 // side buffer elements for either in-place pass at any of its row-step choices
@@ -826,16 +847,18 @@ static bool ip2_bar() { return tuning_int("PGMG_OP2IP_BAR", 1) != 0; }
 size_t g_defer_elems(int H, int W)
 {
     size_t m = 0;
-    for (int U : {8, 16}) {
-        const OpGeom a = sweep_ip_geom(H, W, U);
-        for (bool bar : {false, true})
-            m = std::max(m, (size_t)a.gy * 2 * W + (size_t)ip_bounds(a, W, false, bar) * H * 2);
-    }
-    for (int U : {4, 8}) {
-        const OpGeom b = sweep2_ip_geom(H, W, U);
-        for (bool bar : {false, true})
-            m = std::max(m, (size_t)b.gy * 4 * W + (size_t)ip_bounds(b, W, true, bar) * H * 4);
-    }
+    for (int U : {8, 16})
+        for (int nth : {256, 512}) {
+            const OpGeom a = sweep_ip_geom(H, W, U, nth);
+            for (bool bar : {false, true})
+                m = std::max(m, (size_t)a.gy * 2 * W + (size_t)ip_bounds(a, W, false, bar) * H * 2);
+        }
+    for (int U : {4, 8})
+        for (int nth : {256, 512}) {
+            const OpGeom b = sweep2_ip_geom(H, W, U, nth);
+            for (bool bar : {false, true})
+                m = std::max(m, (size_t)b.gy * 4 * W + (size_t)ip_bounds(b, W, true, bar) * H * 4);
+        }
     return m + 64;
 }
 
@@ -863,11 +886,19 @@ void launch_g_sweep_ip(double *x, const double *f, double *side, unsigned *reset
                        unsigned long long *stats, double hh, int H, int W, hipStream_t s)
 {
     const int U = tuning_int("PGMG_OPIP_U", 16) == 8 ? 8 : 16;
-    const OpGeom g = sweep_ip_geom(H, W, U);
     const bool nt = tuning_int("PGMG_OP_NT", 1) != 0;
     const bool bar = ip_bar();
+    const int nth = (bar && nt) ? ip_nth() : 256;   // the other forms: 256-thread workgroups
+    const OpGeom g = sweep_ip_geom(H, W, U, nth);
     double *SR = side, *SC = side + (size_t)g.gy * 2 * W;
     const dim3 grid(g.gx, g.gy);
+    if (nth == 512 && bar && nt) {   // the default
+        if (U == 8) k_op_sweep_ip<8, true, true, 512><<<grid, 512, 0, s>>>(x, f, SR, SC, reset, stats, hh, H, W, g.rpb);
+        else k_op_sweep_ip<16, true, true, 512><<<grid, 512, 0, s>>>(x, f, SR, SC, reset, stats, hh, H, W, g.rpb);
+        defer_scatter(x, SR, SC, g, 1, ip_bounds(g, W, false, true), 2, 1024, 1024, H, W, s);
+        return;
+    }
+    // (measurement build: 256-thread workgroups, default-policy stores or wave-boundary deferral)
 #define PGMG_KI(UU, NTV, BR) k_op_sweep_ip<UU, NTV, BR><<<grid, kBlock, 0, s>>>(x, f, SR, SC, reset, stats, hh, H, W, g.rpb)
     if (bar) {
         if (U == 8) { if (nt) PGMG_KI(8, true, true); else PGMG_KI(8, false, true); }
@@ -886,11 +917,18 @@ void launch_g_sweep2_ip(double *x, const double *f, double *side, unsigned long 
                         double hh, int H, int W, hipStream_t s)
 {
     const int U = tuning_int("PGMG_OP2IP_U", 8) == 4 ? 4 : 8;
-    const OpGeom g = sweep2_ip_geom(H, W, U);
     const bool nt = tuning_int("PGMG_OP_NT", 1) != 0;
     const bool bar = ip2_bar();
+    const int nth = (bar && nt && U == 8) ? ip2_nth() : 256;
+    const OpGeom g = sweep2_ip_geom(H, W, U, nth);
     double *SR = side, *SC = side + (size_t)g.gy * 4 * W;
     const dim3 grid(g.gx, g.gy);
+    if (nth == 512) {   // measurement build (PGMG_OP2IP_NTH=512)
+        k_op_sweep2_ip<8, true, true, 512><<<grid, 512, 0, s>>>(x, f, SR, SC, stats, hh, H, W, g.rpb);
+        defer_scatter(x, SR, SC, g, 2, ip_bounds(g, W, true, true), 4, kOv2Stride * 8,
+                      kOv2Stride * 7 + 119, H, W, s);
+        return;
+    }
 #define PGMG_KI(UU, NTV, BR) k_op_sweep2_ip<UU, NTV, BR><<<grid, kBlock, 0, s>>>(x, f, SR, SC, stats, hh, H, W, g.rpb)
     if (bar) {
         if (U == 4) { if (nt) PGMG_KI(4, true, true); else PGMG_KI(4, false, true); }

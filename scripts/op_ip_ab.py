@@ -24,6 +24,7 @@ ap.add_argument("--n", type=int, default=16385)
 ap.add_argument("--rounds", type=int, default=2)
 ap.add_argument("--quick", action="store_true", help="defaults and the ping-pong form only")
 ap.add_argument("--only-inplace", action="store_true", help="the in-place default only")
+ap.add_argument("--nth", action="store_true", help="the single in-place sweep's workgroup size")
 args = ap.parse_args()
 
 import torch  # noqa: E402
@@ -39,11 +40,15 @@ tmp = torch.empty_like(x)
 byt = 24.0 * (n - 2) ** 2
 
 KNOBS = ("PGMG_OP_INPLACE", "PGMG_OPIP_U", "PGMG_OPIP_BLOCKS", "PGMG_OP2IP_U", "PGMG_OP2IP_BLOCKS",
-         "PGMG_OPIP_BAR", "PGMG_OP2IP_BAR")
+         "PGMG_OPIP_BAR", "PGMG_OP2IP_BAR", "PGMG_OPIP_NTH", "PGMG_OP2IP_NTH")
 variants = [{"PGMG_OP_INPLACE": 0}, {"PGMG_OP_INPLACE": 1},
             {"PGMG_OP_INPLACE": 1, "PGMG_OPIP_BAR": 0, "PGMG_OP2IP_BAR": 0}]
 if args.only_inplace:
     variants = [{"PGMG_OP_INPLACE": 1}]
+elif args.nth:
+    variants = [{"PGMG_OP_INPLACE": 1}, {"PGMG_OPIP_NTH": 256},
+                {"PGMG_OP2IP_NTH": 512}, {"PGMG_OP2IP_NTH": 512, "PGMG_OP2IP_BLOCKS": 512},
+                {"PGMG_OP2IP_NTH": 512, "PGMG_OP2IP_BLOCKS": 2048}]
 elif not args.quick:
     for u, b in ((16, 2048), (8, 1024), (8, 2048)):
         variants.append({"PGMG_OP_INPLACE": 1, "PGMG_OPIP_BAR": 0, "PGMG_OPIP_U": u,
