@@ -1014,6 +1014,8 @@ void launch_g_residual(double *r, const double *x, const double *f, double inv_h
     // 16 rows in flight, as the sweep (r04, scripts/op_ru_ab.py, profiles/r04_ops/op_ru.jsonl:
     // 1.344-1.351 ms against 1.360-1.362 for 8 rows, 3 interleaved rounds; 2048 workgroups
     // 1.362-1.382); PGMG_OPR_U = 8 in the measurement build for the old form
+    // (r05: 512-thread workgroups x 512 / 1024 measured the same or slower, 1.357-1.378 ms
+    // against 1.358-1.363; profiles/r05_ops/op_misc_ab.jsonl)
     if (tuning_int("PGMG_OPR_U", 16) == 16) {
         const OpGeom g = op_geom((W - 1) / 2, H - 2, 16, tuning_int("PGMG_OPR_BLOCKS", 1024));
         k_op_residual<16><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(r, x, f, inv_hh, H, W, g.rpb);
