@@ -43,6 +43,11 @@ struct Cols {
     bool edge;      // wave-uniform: some lane of this wave has a boundary/outside column
 };
 
+// fp32 stencil stages as packed 2-vector arithmetic (pgmg_real.h pf2); 0 = the scalar
+// expressions (measurement builds: scripts/build_variant.sh NAME -DPGMG_F32_PK=0)
+#ifndef PGMG_F32_PK
+#define PGMG_F32_PK 1
+#endif
 // One Jacobi stage on a row: J(ce) with boundary passthrough.  EDGE = false: the caller
 // guarantees that neither the row nor any column of the wave is a boundary (no selects).
 template <class T, bool EDGE = true>
@@ -52,8 +57,13 @@ __device__ __forceinline__ V2<T> jstage(V2<T> up, V2<T> ce, V2<T> dn, V2<T> f, T
     const T l = dpp_shr(ce.y);
     const T r = dpp_shl(ce.x);
     V2<T> o;
-    o.x = T(0.25) * ((hh * f.x) + l + ce.y + up.x + dn.x);
-    o.y = T(0.25) * ((hh * f.y) + ce.x + r + up.y + dn.y);
+    if constexpr (sizeof(T) == 4 && PGMG_F32_PK) {   // packed: L = (l, c), R = (c+1, r)
+        const pf2 L = {l, ce.x}, R = {ce.y, r};
+        o = unpk(0.25f * (((((hh * pk(f)) + L) + R) + pk(up)) + pk(dn)));
+    } else {
+        o.x = T(0.25) * ((hh * f.x) + l + ce.y + up.x + dn.x);
+        o.y = T(0.25) * ((hh * f.y) + ce.x + r + up.y + dn.y);
+    }
     if constexpr (EDGE) {
         if (brow || k.bx) o.x = ce.x;
         if (brow || k.by) o.y = ce.y;
@@ -84,8 +94,13 @@ __device__ __forceinline__ V2<T> rstage(V2<T> up, V2<T> ce, V2<T> dn, V2<T> f, T
     const T l = dpp_shr(ce.y);
     const T r = dpp_shl(ce.x);
     V2<T> o;
-    o.x = f.x - ih * (T(4) * ce.x - l - ce.y - up.x - dn.x);
-    o.y = f.y - ih * (T(4) * ce.y - ce.x - r - up.y - dn.y);
+    if constexpr (sizeof(T) == 4 && PGMG_F32_PK) {
+        const pf2 L = {l, ce.x}, R = {ce.y, r};
+        o = unpk(pk(f) - ih * ((((4.0f * pk(ce) - L) - R) - pk(up)) - pk(dn)));
+    } else {
+        o.x = f.x - ih * (T(4) * ce.x - l - ce.y - up.x - dn.x);
+        o.y = f.y - ih * (T(4) * ce.y - ce.x - r - up.y - dn.y);
+    }
     return o;
 }
 
@@ -797,8 +812,13 @@ __device__ __forceinline__ V2<T> jsn(V2<T> up, V2<T> ce, V2<T> dn, Nbr<T> n, V2<
                                        const Cols &k, bool brow)
 {
     V2<T> o;
-    o.x = T(0.25) * ((hh * f.x) + n.l + ce.y + up.x + dn.x);
-    o.y = T(0.25) * ((hh * f.y) + ce.x + n.r + up.y + dn.y);
+    if constexpr (sizeof(T) == 4 && PGMG_F32_PK) {   // packed (as jstage)
+        const pf2 L = {n.l, ce.x}, R = {ce.y, n.r};
+        o = unpk(0.25f * (((((hh * pk(f)) + L) + R) + pk(up)) + pk(dn)));
+    } else {
+        o.x = T(0.25) * ((hh * f.x) + n.l + ce.y + up.x + dn.x);
+        o.y = T(0.25) * ((hh * f.y) + ce.x + n.r + up.y + dn.y);
+    }
     if constexpr (EDGE) {
         if (brow || k.bx) o.x = ce.x;
         if (brow || k.by) o.y = ce.y;
@@ -812,8 +832,13 @@ __device__ __forceinline__ V2<T> jsh(V2<T> up, V2<T> ce, V2<T> dn, Nbr<T> n, V2<
                                        const Cols &k, bool brow)
 {
     V2<T> o;
-    o.x = T(0.25) * (hf.x + n.l + ce.y + up.x + dn.x);
-    o.y = T(0.25) * (hf.y + ce.x + n.r + up.y + dn.y);
+    if constexpr (sizeof(T) == 4 && PGMG_F32_PK) {   // packed: L = (l, c), R = (c+1, r), same order per element
+        const pf2 L = {n.l, ce.x}, R = {ce.y, n.r};
+        o = unpk(0.25f * ((((pk(hf) + L) + R) + pk(up)) + pk(dn)));
+    } else {
+        o.x = T(0.25) * (hf.x + n.l + ce.y + up.x + dn.x);
+        o.y = T(0.25) * (hf.y + ce.x + n.r + up.y + dn.y);
+    }
     if constexpr (EDGE) {
         if (brow || k.bx) o.x = ce.x;
         if (brow || k.by) o.y = ce.y;
@@ -854,8 +879,13 @@ template <class T>
 __device__ __forceinline__ V2<T> rsn(V2<T> up, V2<T> ce, V2<T> dn, Nbr<T> n, V2<T> f, T ih)
 {
     V2<T> o;
-    o.x = f.x - ih * (T(4) * ce.x - n.l - ce.y - up.x - dn.x);
-    o.y = f.y - ih * (T(4) * ce.y - ce.x - n.r - up.y - dn.y);
+    if constexpr (sizeof(T) == 4 && PGMG_F32_PK) {   // packed (as jsh)
+        const pf2 L = {n.l, ce.x}, R = {ce.y, n.r};
+        o = unpk(pk(f) - ih * ((((4.0f * pk(ce) - L) - R) - pk(up)) - pk(dn)));
+    } else {
+        o.x = f.x - ih * (T(4) * ce.x - n.l - ce.y - up.x - dn.x);
+        o.y = f.y - ih * (T(4) * ce.y - ce.x - n.r - up.y - dn.y);
+    }
     return o;
 }
 
@@ -1000,6 +1030,30 @@ __device__ __forceinline__ T buf_one(const T *base, int n, int t)
         return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, t * 8, 0, 0));
     else
         return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, t * 4, 0, 0));
+}
+
+// Check sums of k_postpre_lds: acc + r.x^2 (+ r.y^2 unless column c+1 is a boundary) on an
+// owned pair of a band row.  PGMG_CHK_SEL (r05): as selects instead of a branch around the
+// residual (0: neither type, 1: fp32 only, 2: both, 3: fp64 only) -- a skipped term adds
+// (+0)^2, which leaves the sum (>= +0) bitwise unchanged, and the residual's dependent chain,
+// no longer in a branch of its own, can interleave with the sweeps around it.  Measured at
+// 16385 (scripts/pp_ab.py, profiles/r05_fp32/chk_sel_*.jsonl, 3-4 interleaved rounds on two
+// boxes): fp64 0.4-0.6 % faster (1.0687 -> 1.0646 ms); fp32 6 % slower although its packed
+// chains lose their s_nops (92 -> 12 per 6 rows): 118 -> 161 VGPRs, 4 -> 3 waves per SIMD
+// (and at 2 register sets of loads, 109 VGPRs, still 4.6 % slower) -- so fp64 only.
+#ifndef PGMG_CHK_SEL
+#define PGMG_CHK_SEL 3
+#endif
+template <class T> constexpr bool chk_sel()
+{
+    return PGMG_CHK_SEL == 2 || (PGMG_CHK_SEL == 1 && sizeof(T) == 4) || (PGMG_CHK_SEL == 3 && sizeof(T) == 8);
+}
+template <class T>
+__device__ __forceinline__ double chk_acc(double acc, V2<T> r, bool in, bool by)
+{
+    const T rx = in ? r.x : T(0);
+    const T ry = (in && !by) ? r.y : T(0);
+    return sqacc(sqacc(acc, rx), ry);
 }
 
 // The body of k_postpre_lds for one block.  EDGE = false: no row of the block's band and
@@ -1199,7 +1253,9 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                 const V2<T> r1 = FAST ? rsum<T>(sb, b1, fq2, ih) : rsn<T>(b0, b1, b2, nb1, fq2, ih);
 #endif
                 const int row = ii - 2;
-                if (row >= olo && row < ohi && k.own) {
+                if constexpr (chk_sel<T>()) {
+                    acc1 = chk_acc<T>(acc1, r1, row >= olo && row < ohi && k.own, k.by);
+                } else if (row >= olo && row < ohi && k.own) {
                     acc1 = sqacc(acc1, r1.x);
                     if (!k.by) acc1 = sqacc(acc1, r1.y);
                 }
@@ -1210,7 +1266,9 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
             if (R2) {   // r(x2) on row ii-3
                 const V2<T> r2 = rsn<T>(c0, c1, c2, nc1, fq3, ih);
                 const int row = ii - 3;
-                if (row >= olo && row < ohi && k.own) {
+                if constexpr (chk_sel<T>()) {
+                    acc3 = chk_acc<T>(acc3, r2, row >= olo && row < ohi && k.own, k.by);
+                } else if (row >= olo && row < ohi && k.own) {
                     acc3 = sqacc(acc3, r2.x);
                     if (!k.by) acc3 = sqacc(acc3, r2.y);
                 }
@@ -1226,7 +1284,9 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                 const V2<T> r3 = FAST ? rsum<T>(sgg, g1, fq4, ih) : rsn<T>(g0, g1, g2, ng1, fq4, ih);
 #endif
                 const int row = ii - 4;
-                if (row >= olo && row < ohi && k.own) {
+                if constexpr (chk_sel<T>()) {
+                    acc2 = chk_acc<T>(acc2, r3, row >= olo && row < ohi && k.own, k.by);
+                } else if (row >= olo && row < ohi && k.own) {
                     acc2 = sqacc(acc2, r3.x);
                     if (!k.by) acc2 = sqacc(acc2, r3.y);
                 }
@@ -1310,8 +1370,15 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
 
 
 // two waves per SIMD (3 spills and measured slower, r02)
+// fp32: the minimum waves per SIMD the register allocation must allow (PGMG_F32_WAVES, r05);
+// 2 lets it take up to 256 VGPRs (it uses 118 with the branch-form checks: 4 waves anyway;
+// 4 with the select-form checks spills 140 bytes)
+#ifndef PGMG_F32_WAVES
+#define PGMG_F32_WAVES 2
+#endif
+template <class T> constexpr int pp_waves() { return sizeof(T) == 4 ? PGMG_F32_WAVES : 2; }
 template <class T, bool R2, bool GENF, int OPT>
-__global__ __launch_bounds__(64 * kPPWaves) __attribute__((amdgpu_waves_per_eu(2)))
+__global__ __launch_bounds__(64 * kPPWaves) __attribute__((amdgpu_waves_per_eu(pp_waves<T>())))
 void k_postpre_lds(PostPreArgsT<T> a)
 {
     __shared__ double red[kPPWaves];

@@ -50,6 +50,15 @@ __device__ __forceinline__ V2<T> mk2(T a, T b)
 }
 template <class T> __device__ __forceinline__ V2<T> zero2() { return mk2<T>(T(0), T(0)); }
 
+// An fp32 column pair as a native 2-vector: arithmetic on it selects the packed VOP3P
+// instructions (v_pk_add_f32 / v_pk_mul_f32, a subtraction as an add with neg modifiers),
+// each element the same IEEE operation as the scalar expression it restates.  The fp32 pass
+// is VALU-bound (half the bytes of fp64 for the same per-row work), so two columns per
+// instruction is where its time goes.
+typedef float pf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pf2 pk(float2 v) { return pf2{v.x, v.y}; }
+__device__ __forceinline__ float2 unpk(pf2 v) { return mk2<float>(v.x, v.y); }
+
 // r*r accumulated in double (identical to r*r for T = double)
 template <class T> __device__ __forceinline__ double sq(T r) { return (double)r * (double)r; }
 // acc + r*r with one fused multiply-add: the early-exit partial sums are order-dependent
