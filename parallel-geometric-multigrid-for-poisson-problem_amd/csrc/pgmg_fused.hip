@@ -104,6 +104,38 @@ __device__ __forceinline__ V2<T> rstage(V2<T> up, V2<T> ce, V2<T> dn, V2<T> f, T
     return o;
 }
 
+// Check sums of k_postpre_lds: acc + r.x^2 (+ r.y^2 unless column c+1 is a boundary) on an
+// owned pair of a band row.  PGMG_CHK_SEL (r05): as selects instead of a branch around the
+// residual (0: neither type, 1: fp32 only, 2: both, 3: fp64 only) -- a skipped term adds
+// (+0)^2, which leaves the sum (>= +0) bitwise unchanged, and the residual's dependent chain,
+// no longer in a branch of its own, can interleave with the sweeps around it.  Measured at
+// 16385 (scripts/pp_ab.py, profiles/r05_fp32/chk_sel_*.jsonl, 3-4 interleaved rounds on two
+// boxes): fp64 0.4-0.6 % faster (1.0687 -> 1.0646 ms); fp32 6 % slower although its packed
+// chains lose their s_nops (92 -> 12 per 6 rows): 118 -> 161 VGPRs, 4 -> 3 waves per SIMD
+// (and at 2 register sets of loads, 109 VGPRs, still 4.6 % slower) -- so fp64 only.
+#ifndef PGMG_CHK_SEL
+#define PGMG_CHK_SEL 3
+#endif
+template <int M, class T> constexpr bool chk_sel_m() { return M == 2 || (M == 1 && sizeof(T) == 4) || (M == 3 && sizeof(T) == 8); }
+template <class T> constexpr bool chk_sel() { return chk_sel_m<PGMG_CHK_SEL, T>(); }
+// the same choice for the check sums of k_post_r2 (the F-cycle's finest post pass; same
+// values).  Measured (scripts/pp_ab.py, profiles/r05_fp32/chk_sel_post_*.jsonl, 3 interleaved
+// rounds): selects in every k_post -- F at 16385 4.449 -> 4.408 ms per cycle (-0.9 %, all of
+// it k_post_r2), V at 16385 1.7875 -> 1.7917 (+0.2 %, level 1's k_post), V at 4097 equal; so
+// k_post_r2 only.  In k_pre the select form raises most instantiations' VGPRs by 14-100,
+// several from 3 to 2 waves per SIMD: not used there.
+#ifndef PGMG_CHK_SEL_LV
+#define PGMG_CHK_SEL_LV 3
+#endif
+template <class T> constexpr bool chk_sel_lv() { return chk_sel_m<PGMG_CHK_SEL_LV, T>(); }
+template <class T>
+__device__ __forceinline__ double chk_acc(double acc, V2<T> r, bool in, bool by)
+{
+    const T rx = in ? r.x : T(0);
+    const T ry = (in && !by) ? r.y : T(0);
+    return sqacc(sqacc(acc, rx), ry);
+}
+
 // Row factor of the regenerated RHS through the constant address space: a scalar load
 // (the table is read-only), not a per-row vector load the row loop would wait on
 __device__ __forceinline__ double gsy_s(const double *gsy, int row)
@@ -676,7 +708,9 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
                     if constexpr (S1P) {   // the check's terms: r(x1) on row ii-2 (k_post1)
                         const int row = ii - 2;
                         const V2<T> r1 = rstage(b0, b1, b2, f1, ih);
-                        if (row >= slo && row < shi && k.own) {
+                        if constexpr (R2 && chk_sel_lv<T>()) {
+                            acc = chk_acc<T>(acc, r1, row >= slo && row < shi && k.own, k.by);
+                        } else if (row >= slo && row < shi && k.own) {
                             acc = sqacc(acc, r1.x);
                             if (!k.by) acc = sqacc(acc, r1.y);
                         }
@@ -692,7 +726,9 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
                 {
                     const int row = ii - 2;
                     const V2<T> r1 = rstage(b0, b1, b2, f1, ih);
-                    if ((FULL || (row >= slo && row < shi)) && k.own) {
+                    if constexpr (R2 && chk_sel_lv<T>()) {
+                        acc = chk_acc<T>(acc, r1, (FULL || (row >= slo && row < shi)) && k.own, !FULL && k.by);
+                    } else if ((FULL || (row >= slo && row < shi)) && k.own) {
                         acc = sqacc(acc, r1.x);
                         if (FULL || !k.by) acc = sqacc(acc, r1.y);
                     }
@@ -1030,30 +1066,6 @@ __device__ __forceinline__ T buf_one(const T *base, int n, int t)
         return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, t * 8, 0, 0));
     else
         return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, t * 4, 0, 0));
-}
-
-// Check sums of k_postpre_lds: acc + r.x^2 (+ r.y^2 unless column c+1 is a boundary) on an
-// owned pair of a band row.  PGMG_CHK_SEL (r05): as selects instead of a branch around the
-// residual (0: neither type, 1: fp32 only, 2: both, 3: fp64 only) -- a skipped term adds
-// (+0)^2, which leaves the sum (>= +0) bitwise unchanged, and the residual's dependent chain,
-// no longer in a branch of its own, can interleave with the sweeps around it.  Measured at
-// 16385 (scripts/pp_ab.py, profiles/r05_fp32/chk_sel_*.jsonl, 3-4 interleaved rounds on two
-// boxes): fp64 0.4-0.6 % faster (1.0687 -> 1.0646 ms); fp32 6 % slower although its packed
-// chains lose their s_nops (92 -> 12 per 6 rows): 118 -> 161 VGPRs, 4 -> 3 waves per SIMD
-// (and at 2 register sets of loads, 109 VGPRs, still 4.6 % slower) -- so fp64 only.
-#ifndef PGMG_CHK_SEL
-#define PGMG_CHK_SEL 3
-#endif
-template <class T> constexpr bool chk_sel()
-{
-    return PGMG_CHK_SEL == 2 || (PGMG_CHK_SEL == 1 && sizeof(T) == 4) || (PGMG_CHK_SEL == 3 && sizeof(T) == 8);
-}
-template <class T>
-__device__ __forceinline__ double chk_acc(double acc, V2<T> r, bool in, bool by)
-{
-    const T rx = in ? r.x : T(0);
-    const T ry = (in && !by) ? r.y : T(0);
-    return sqacc(sqacc(acc, rx), ry);
 }
 
 // The body of k_postpre_lds for one block.  EDGE = false: no row of the block's band and
