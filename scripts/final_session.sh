@@ -25,7 +25,7 @@ step smoke 120 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --warmup 5 --steps 20 --save-profiles ${OUT}/prof
 step bench_F 300 python bench.py --cycle F --warmup 2 --steps 20 --cpu-baseline off --pmc off --trace off
 step bench_W 300 python bench.py --cycle W --n 4097 --warmup 2 --steps 10 --cpu-baseline off --pmc off --trace off
-step bench_f32 300 python bench.py --dtype f32 --warmup 5 --steps 20 --cpu-baseline off
+step bench_f32 400 python bench.py --dtype f32 --warmup 5 --steps 20 --cpu-baseline off --save-profiles ${OUT}/prof_f32
 [ "${SKIP_COARSE:-0}" = 1 ] || step coarse 900 bash scripts/coarse_session.sh ${OUT}/coarse
 tail -3 ${OUT}/tests.out >&2
 cat ${OUT}/bench.out
