@@ -1852,6 +1852,25 @@ static void spec_record_norms(pgmg_ctx *c, int n)
         }
         fprintf(stderr, "W plan: %d visits per cycle, %d predicted to fire, %d not (1 cycle)\n",
                 vc, f, q);
+        // per level: visits, both checks < eps/4, max < eps, and the first visits (in cycle
+        // order) whose max norm is >= eps/4 (measurement trace)
+        std::vector<int> vlev(vc, -1);
+        for (int i = 0; i < n; ++i)
+            if (c->chk_visit[i] >= v0) vlev[c->chk_visit[i] - v0] = c->chks[i].level;
+        for (int l = 1; l < 32; ++l) {
+            int tot = 0, f4 = 0, f1 = 0;
+            std::string nf;
+            for (int i = 0; i < vc; ++i) {
+                if (vlev[i] != l) continue;
+                const bool a = c->wmax[i] >= 0.0 && c->wmax[i] < 0.25 * c->cfg.eps;
+                f4 += a;
+                f1 += c->wmax[i] >= 0.0 && c->wmax[i] < c->cfg.eps;
+                if (!a && nf.size() < 400) nf += " " + std::to_string(tot) + ":" + std::to_string(c->wmax[i] / c->cfg.eps);
+                ++tot;
+            }
+            if (tot) fprintf(stderr, "  level %d: %d visits, %d < eps/4, %d < eps; others (index:max/eps):%s\n",
+                             l, tot, f4, f1, nf.c_str());
+        }
     }
 }
 
