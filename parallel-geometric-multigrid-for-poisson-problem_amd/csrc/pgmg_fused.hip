@@ -122,8 +122,9 @@ template <class T> constexpr bool chk_sel() { return chk_sel_m<PGMG_CHK_SEL, T>(
 // values).  Measured (scripts/pp_ab.py, profiles/r05_fp32/chk_sel_post_*.jsonl, 3 interleaved
 // rounds): selects in every k_post -- F at 16385 4.449 -> 4.408 ms per cycle (-0.9 %), V at
 // 16385 1.7875 -> 1.7917 (+0.2 %, level 1's k_post), V at 4097 equal; in k_post_r2 alone
-// (chk_sel_r2only_*.jsonl) F 4.470 -> 4.421 (-1.1 %), V unchanged -- so k_post_r2 only.  In k_pre the select form raises most instantiations' VGPRs by 14-100,
-// several from 3 to 2 waves per SIMD: not used there.
+// (chk_sel_r2only_*.jsonl) F 4.470 -> 4.421 (-1.1 %), V unchanged -- so k_post_r2 only.
+// In k_pre the select form raises most instantiations' VGPRs by 14-100, several from 3 to 2
+// waves per SIMD: not used there.
 #ifndef PGMG_CHK_SEL_LV
 #define PGMG_CHK_SEL_LV 3
 #endif
