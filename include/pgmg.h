@@ -125,6 +125,9 @@ extern "C" {
 #define PGMG_FLAG_NO_CTILE 65536u /* the small coarse levels (N <= 513, entered with x0 = 0)
                                      run the row-marching fused passes instead of the 2D LDS
                                      tile passes (r04).  Results are identical either way */
+#define PGMG_FLAG_NO_CARRY 131072u /* do not carry the next call's pre-smooth across
+                                      pgmg_vcycle calls (the carry: below pgmg_vcycle).  Results
+                                      and statistics are identical either way */
 #define PGMG_FLAG_HOST_TRANSPORT 2048u /* world > 1 without RCCL: nccl_unique_id points to
                                        a pgmg_host_transport; every message and reduction
                                        is staged through host memory and handed to the
@@ -235,6 +238,17 @@ int pgmg_pointer_is_device(const void *p, int *is_device);
  * F-cycle call is speculative too (its bulk checks recorded "does not fire" and validated once
  * after the call; a rollback reruns the call in-stream from the saved restricted grid and the
  * problem's later F calls decide in-stream); PGMG_FLAG_EXACT_DIST turns that off. */
+/* The carry (r06; one GPU, cross-fused contexts, problems set with pgmg_set_problem): a
+ * speculative V call ends with a finest-level pass that also runs the NEXT cycle's pre-smooth,
+ * residual and restriction (MultiGrid.hpp:57-94's first half) into context-owned buffers and
+ * checks it; the next pgmg_vcycle on the same problem starts from them instead of running its
+ * own first pass.  Entries that only read the problem (pgmg_get_solution, pgmg_solution_hash,
+ * pgmg_residual_norm, pgmg_stats*, pgmg_sync ...) keep the carry; every entry that changes phi,
+ * f, eps, the flags or the cycle kind (pgmg_set_problem*, pgmg_set_eps, pgmg_wcycle,
+ * pgmg_fcycle, pgmg_bench_sweep, pgmg_phi_device -- its pointer allows writes -- ) drops it.
+ * A carried pre-smooth whose early-exit check could fire is dropped, not rolled back.  Results
+ * and statistics (its two sweeps count in the call that uses them) equal the uncarried ones,
+ * bit for bit.  PGMG_FLAG_NO_CARRY turns it off; pgmg_carry_info counts it. */
 int pgmg_vcycle(pgmg_ctx *ctx, int ncycles);
 int pgmg_wcycle(pgmg_ctx *ctx, int ncycles);
 int pgmg_fcycle(pgmg_ctx *ctx, int ncycles);
@@ -315,14 +329,28 @@ int pgmg_spec_fire_levels(pgmg_ctx *ctx, unsigned long long *fire);
  * V call. */
 int pgmg_spec_visit_modes(pgmg_ctx *ctx, long long counts[3]);
 
+/* The carry (above pgmg_vcycle): out[0] calls that started from a carried pre-smooth, out[1]
+ * carries made, out[2] carries dropped because their check could fire. */
+int pgmg_carry_info(pgmg_ctx *ctx, long long out[3]);
+
+/* A new early-exit threshold (JacobiSmoother's eps, Smoother.hpp:38) for the following calls:
+ * drops the carry and the speculation history (the statistics continue). */
+int pgmg_set_eps(pgmg_ctx *ctx, double eps);
+
 /* The context's PGMG_PRECISION_* and its grid element size in bytes (8 or 4). */
 int pgmg_precision(pgmg_ctx *ctx, int *precision, int *elem_bytes);
 
 /* Count and mean device duration (ms) of the finest-level kernels launched since
  * the last call (needs PGMG_FLAG_TIME_FINE; synchronous).  pass 0: plain Jacobi
  * sweep (unfused path), 1: fused pre-smooth+residual+restriction (k_pre),
- * 2: fused prolongation+post-smooth (k_post), 3: cross-cycle k_postpre. */
+ * 2: fused prolongation+post-smooth (k_post), 3: cross-cycle k_postpre, 4: the carry pass
+ * (k_postpre that also stores the call's result). */
 int pgmg_fine_pass_time(pgmg_ctx *ctx, int pass, int *count, double *mean_ms);
+/* What the launches the last pgmg_fine_pass_time(pass) averaged were: the kernel symbol of the
+ * last of them (demangled, e.g. "pgmg::k_postpre_lds<double, false, true, 2>"; "" when none was
+ * timed) and the mean of their algorithmic bytes (the pgmg_fine_pass_bytes model applied to
+ * what each launch actually read and wrote: an F-cycle's k_pre reads no x0, ...). */
+int pgmg_fine_pass_info(pgmg_ctx *ctx, int pass, char *symbol, int len, double *bytes_per_launch);
 int pgmg_fine_sweep_time(pgmg_ctx *ctx, int *count, double *mean_ms);  /* pass 0 */
 
 /* 1 when the context runs the fused two-pass-per-level cycle (v1 = v2 = 1). */

@@ -22,7 +22,7 @@ from ._capi import (PGMG_FLAG_LOOPBACK, PGMG_FLAG_NO_CROSS, PGMG_FLAG_NO_GRAPH,
                     PGMG_FLAG_TIME_FINE, PGMG_PRECISION_FP32, PGMG_PRECISION_FP64,
                     PGMG_FLAG_UNFUSED, PGMG_FLAG_NO_RECOMPUTE, PGMG_FLAG_NO_PIN,
                     PGMG_FLAG_NO_R2, PGMG_FLAG_HOST_TRANSPORT, PGMG_FLAG_FAST,
-                    PGMG_FLAG_NO_SPEC_FIRE, PGMG_FLAG_NO_CTILE,
+                    PGMG_FLAG_NO_SPEC_FIRE, PGMG_FLAG_NO_CTILE, PGMG_FLAG_NO_CARRY,
                     PGMG_PROLONG_REFERENCE,
                     PGMG_PROLONG_SYMMETRIC, PGMG_OK, PGMG_ERR_STATE, PgmgConfig, PgmgError,
                     check, load)
@@ -35,7 +35,7 @@ __all__ = [
     "PGMG_PROLONG_REFERENCE", "plan_strips", "LoopbackHub", "unique_id",
     "PGMG_PROLONG_SYMMETRIC", "PGMG_PRECISION_FP64", "PGMG_PRECISION_FP32",
     "PGMG_FLAG_STORED_RHS", "PGMG_FLAG_EXACT_DIST", "PGMG_FLAG_SOLO",
-    "PGMG_FLAG_NO_RECOMPUTE", "PGMG_FLAG_NO_PIN", "PGMG_FLAG_NO_R2", "PGMG_FLAG_FAST", "PGMG_FLAG_NO_SPEC_FIRE", "PGMG_FLAG_NO_CTILE",
+    "PGMG_FLAG_NO_RECOMPUTE", "PGMG_FLAG_NO_PIN", "PGMG_FLAG_NO_R2", "PGMG_FLAG_FAST", "PGMG_FLAG_NO_SPEC_FIRE", "PGMG_FLAG_NO_CTILE", "PGMG_FLAG_NO_CARRY",
     "PGMG_FLAG_HOST_TRANSPORT", "HostTransport", "DeviceGrid",
 ]
 
@@ -279,7 +279,8 @@ class Solver:
         return n.value, m.value
 
     def fine_pass_time(self, which):
-        """(count, mean ms) of finest-level kernels: 0 plain sweep, 1 k_pre, 2 k_post."""
+        """(count, mean ms) of finest-level kernels: 0 plain sweep, 1 k_pre, 2 k_post,
+        3 k_postpre, 4 the carry pass."""
         n, m = C.c_int(), C.c_double()
         check(self.lib.pgmg_fine_pass_time(self.h, int(which), C.byref(n), C.byref(m)),
               "pgmg_fine_pass_time")
@@ -290,6 +291,25 @@ class Solver:
         v = C.c_int()
         check(self.lib.pgmg_fused(self.h, C.byref(v)), "pgmg_fused")
         return bool(v.value)
+
+    def fine_pass_info(self, which):
+        """(kernel symbol, algorithmic bytes per launch) of the launches the last
+        fine_pass_time(which) averaged ("" / 0 when none was timed)."""
+        buf = C.create_string_buffer(512)
+        b = C.c_double()
+        check(self.lib.pgmg_fine_pass_info(self.h, int(which), buf, 512, C.byref(b)),
+              "pgmg_fine_pass_info")
+        return buf.value.decode(errors="replace"), b.value
+
+    def carry_info(self):
+        """(calls that started from a carried pre-smooth, carries made, carries dropped)."""
+        a = (C.c_longlong * 3)()
+        check(self.lib.pgmg_carry_info(self.h, a), "pgmg_carry_info")
+        return tuple(a)
+
+    def set_eps(self, eps):
+        """A new early-exit threshold for the following calls (drops the carry)."""
+        check(self.lib.pgmg_set_eps(self.h, float(eps)), "pgmg_set_eps")
 
     def fine_pass_bytes(self, which):
         """Algorithmic HBM bytes of one launch of finest-level pass `which` on this rank."""

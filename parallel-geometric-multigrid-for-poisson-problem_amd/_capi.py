@@ -38,6 +38,7 @@ PGMG_FLAG_FAST = 4096
 PGMG_FLAG_NO_SPEC_FIRE = 32768
 PGMG_FLAGS_RETIRED = 8192 | 16384
 PGMG_FLAG_NO_CTILE = 65536
+PGMG_FLAG_NO_CARRY = 131072
 
 PGMG_PRECISION_FP64 = 0
 PGMG_PRECISION_FP32 = 1
@@ -116,6 +117,7 @@ SIGNATURES = [
                                   C.POINTER(C.c_int)]),
     ("pgmg_fine_sweep_time", C.c_int, [_P, C.POINTER(C.c_int), _DP]),
     ("pgmg_fine_pass_time", C.c_int, [_P, C.c_int, C.POINTER(C.c_int), _DP]),
+    ("pgmg_fine_pass_info", C.c_int, [_P, C.c_int, C.c_char_p, C.c_int, _DP]),
     ("pgmg_fused", C.c_int, [_P, C.POINTER(C.c_int)]),
     ("pgmg_precision", C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("pgmg_fine_pass_bytes", C.c_int, [_P, C.c_int, _DP]),
@@ -123,6 +125,8 @@ SIGNATURES = [
     ("pgmg_spec_levels", C.c_int, [_P, C.POINTER(C.c_ulonglong)]),
     ("pgmg_spec_fire_levels", C.c_int, [_P, C.POINTER(C.c_ulonglong)]),
     ("pgmg_spec_visit_modes", C.c_int, [_P, C.POINTER(C.c_longlong)]),
+    ("pgmg_carry_info", C.c_int, [_P, C.POINTER(C.c_longlong)]),
+    ("pgmg_set_eps", C.c_int, [_P, C.c_double]),
     ("pgmg_bench_sweep", C.c_int, [_P, C.c_int, _DP]),
     ("pgmg_jacobi", C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_double, C.c_int, C.c_double,
                               C.POINTER(C.c_int), _P]),

@@ -81,7 +81,13 @@ struct pgmg_ctx {
         int used = 0;
     };
     // finest-level kernel timing (PGMG_FLAG_TIME_FINE): 0 plain sweep, 1 k_pre, 2 k_post
-    EventPool tpool[4];           // 3: k_postpre
+    EventPool tpool[5];           // 3: k_postpre, 4: the carry pass
+    // per timed pass: the kernels and algorithmic bytes of the launches timed since the last
+    // pgmg_fine_pass_time (LaunchNote), and what that call averaged (pgmg_fine_pass_info)
+    double tbytes[5] = {0, 0, 0, 0, 0};
+    const void *tkern[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    double info_bytes[5] = {0, 0, 0, 0, 0};
+    const void *info_kern[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     bool fused = false;           // v1 = v2 = 1: two fused passes per level
     bool cross = false;           // finest level fuses post(k) with pre(k+1) across cycles
     bool recompute = true;        // levels entered with x0 = 0 recompute x2 in k_post
@@ -174,6 +180,18 @@ struct pgmg_ctx {
     long long ext_P = 0;
     bool defer_post = false;
     void *pend_pr = nullptr;
+    // the carry (pgmg_ctx.hip "carry"): a speculative V call on the context's own grids ends
+    // with the carry pass, which also runs the next cycle's pre-smooth into Y and its
+    // restriction into lv[1].F; the next V call starts from them when no entry touched the
+    // problem in between
+    pgmg::Grid Y;                 // fourth level-0 grid (one GPU, cross-fused contexts)
+    bool carry = false;           // Y / lv[1].F hold the validated pre-smooth of lv[0].A
+    bool carry_use = false;       // the segment being enqueued starts from the carry
+    bool carry_make = false;      // the segment being enqueued ends with the carry pass
+    bool carry_made = false;      // ... and it did
+    bool carry_took = false;      // the last segment enqueued started from the carry
+    int carry_chk = -1;           // index in chks of the carried pre-smooth's check
+    long long carry_n[3] = {0, 0, 0};   // calls that took a carry, carries made, dropped
 };
 
 namespace pgmg {

@@ -18,6 +18,8 @@
 // global row numbers and the fine/coarse row parity (j = 2 jc) is preserved.
 #include <hip/hip_runtime.h>
 
+#include <cxxabi.h>
+
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -375,6 +377,8 @@ static int timed_end(pgmg_ctx *c, int slot, int idx)
     auto &pool = c->tpool[slot];
     HIPC(hipEventRecord(pool.ev[idx + 1], c->s));
     pool.used = idx + 2;
+    c->tbytes[slot] += g_last_launch.bytes;   // the launch just timed (LaunchNote)
+    c->tkern[slot] = g_last_launch.kernel;
     return PGMG_OK;
 }
 
@@ -705,66 +709,97 @@ static PostArgsT<T> make_post(pgmg_ctx *c, const T *phi, T *x2)
     return po;
 }
 
+// ---------------------------------------------------------------------------
+// The carry (r06).  A call's cycles are cross-fused (k_pre, k_postpre ..., k_post), but a
+// caller that runs one cycle per call, or checks the residual between calls (the reference
+// harness, ParallelTestRunner.cu:172-173), pays the opening k_pre and the closing k_post of
+// every call: two passes over the finest grid where a multi-cycle call runs one k_postpre.
+// So a speculative V call on the context's own grids (one GPU) ends with the CARRY PASS: the
+// last cycle's k_postpre, which also stores x2 -- the call's result -- besides the next
+// cycle's pre-smoothed iterate x4 (into the fourth level-0 grid Y) and its restricted
+// residual (into lv[1].F).  The pre-smooth's early-exit check is logged beside the call's own
+// checks and validated with them; it never rolls the call back: a carry whose check could fire
+// is dropped (carry_n[2]) and the next call runs its own k_pre.  The next pgmg_vcycle on the
+// same problem starts from the carry: no k_pre, straight into the coarse levels
+// (MultiGrid.hpp:57-94 from line 69 on), and its first finest pass counts the carried
+// pre-smooth's two sweeps (sw_adj).  Every entry that changes phi, f, eps, the flags or the
+// cycle kind drops the carry (run_cycles takes it or drops it at every call); caller-owned
+// arrays (pgmg_set_problem_device) never carry: the caller may change them between calls.
+// A rollback of the call that took a carry reruns from lv[0].A, which the carry pass left
+// untouched, with its own k_pre.  Cost: the x2 store, 8 B per fine point (~0.45 ms at 16385)
+// against the k_pre it saves (16 B per fine point + the restriction, ~0.98 ms).
+// ---------------------------------------------------------------------------
 template <class T>
 static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
 {
     Level &L = c->lv[0], &C = c->lv[1];
     const bool dist = is_dist(c, 0);
     const StripRows sr = strip_rows(L, C);
-    Grid gA = L.A, gB = L.B, gS = c->S;
+    Grid gA = L.A, gB = L.B, gS = c->S, gY = c->Y;
     T *A = G<T>(gA), *B = G<T>(gB);
-    T *S = G<T>(gS);
+    T *S = G<T>(gS), *Y = G<T>(gY);   // Y: nullptr without a fourth grid
     // speculative call: no rare path can run, so the scratch S is free and the level-0
-    // buffers rotate through B and S; A (the call's input) is never written and a
+    // buffers rotate through B and S (and Y); A (the call's input) is never written and a
     // rollback restarts from it
     const bool lean = c->lean;
-    auto grid_of = [&](const T *p) -> const Grid * { return p == A ? &gA : p == B ? &gB : &gS; };
+    auto grid_of = [&](const T *p) -> const Grid * {
+        return p == A ? &gA : p == B ? &gB : p == S ? &gS : &gY;
+    };
     // (an external input is followed by B: the first k_pre writes B, then B <-> S (lean) or
-    // B <-> A, both free of the input)
+    // B <-> A, both free of the input; a carried input Y is followed by B as well)
     auto next_of = [&](const T *p) -> T * { return lean ? (p == B ? S : B) : (p == B ? A : B); };
     // the caller's array (pgmg_set_problem_device) as the call's input / output
     const T *in = c->x_in != nullptr ? static_cast<const T *>(c->x_in) : A;
     T *const xout = static_cast<T *>(c->x_out);
     const int np = fused_blocks(L.N, sr.jc0, sr.jc1);
-    const int npp = postpre_blocks(L.N, sr.jc0, sr.jc1, c->fp32 && pp_q4());
+    const int npp = postpre_blocks(L.N, sr.jc0, sr.jc1);
+    // the carry: taken (this call starts from Y and lv[1].F) / made (it ends with the carry
+    // pass); both only on speculative calls on the context's own grids, one GPU
+    const bool take = c->carry_use && lean && !dist && Y != nullptr && c->x_in == nullptr;
+    const bool make = c->carry_make && lean && !dist && Y != nullptr && xout == nullptr &&
+                      !c->defer_post;
+    c->carry_use = false;
+    c->carry_made = false;
+    c->carry_took = take;
+    int sw_adj = take ? 2 : 0;   // the carried pre-smooth's two sweeps: counted by the next pass
     FixArgsF fa{};
     fa.partials = c->partials;
     fa.np = np;
     fa.eps = c->cfg.eps;
     fa.stats = c->stats;
-    int e;
-    // cycle 1: pre-smooth (+ residual, restriction) A -> B
-    if (dist && (e = c->comm->halo(gA, L, 4, c->s))) return e;
-    PreArgsT<T> pa = make_pre<T>(c, in, B);
-    if (c->x_in != nullptr) pa.Px = c->ext_P;
-    double *lp = chk_partials(c, np, 0);
-    if (lp) pa.partials = lp;
-    int ev = timed_begin(c, 1);
-    if ((e = launch_pre(pa, false, true, c->s))) return e;
-    if ((e = timed_end(c, 1, ev))) return e;
-    if (!lp) {
-        if (dist && (e = global_sum(c, np, &fa.global_sum))) return e;
-        launch_pre_fixup(fa, pa, false, c->s);
-        fa.global_sum = nullptr;
+    int e, ev;
+    T *pr;   // pre-smoothed solution of the current cycle
+    if (take) {
+        pr = Y;
+    } else {
+        // cycle 1: pre-smooth (+ residual, restriction) A -> B
+        if (dist && (e = c->comm->halo(gA, L, 4, c->s))) return e;
+        PreArgsT<T> pa = make_pre<T>(c, in, B);
+        if (c->x_in != nullptr) pa.Px = c->ext_P;
+        double *lp = chk_partials(c, np, 0);
+        if (lp) pa.partials = lp;
+        ev = timed_begin(c, 1);
+        if ((e = launch_pre(pa, false, true, c->s))) return e;
+        if ((e = timed_end(c, 1, ev))) return e;
+        if (!lp) {
+            if (dist && (e = global_sum(c, np, &fa.global_sum))) return e;
+            launch_pre_fixup(fa, pa, false, c->s);
+            fa.global_sum = nullptr;
+        }
+        pr = B;
     }
-    T *pr = B;  // pre-smoothed solution of the current cycle
     // its halo rows (6 for k_postpre, 2 for the last k_post) are final now and read only
     // after the whole coarse hierarchy: the exchange runs on the comm's side stream
     // meanwhile (the coarse correction's halo rows are computed locally, kPostExt)
     if (dist && (e = c->comm->halo_begin(*grid_of(pr), L, 6, c->s))) return e;
     if ((e = enqueue_children<T>(c, 0, gamma))) return e;
-    for (int k = 1; k < n; ++k) {
-        T *nx = next_of(pr);
-        if (dist && (e = c->comm->halo_end(c->s))) return e;
+    auto postpre_args = [&](T *phi, T *x4) {
         PostPreArgsT<T> q{};
-        q.phi = pr;
+        q.phi = phi;
         q.ec = G<T>(C.A);
         q.f = G<T>(L.F);
-        q.x4 = nx;
+        q.x4 = x4;
         q.rc = G<T>(C.F);
-        q.partials1 = lean ? chk_partials(c, npp, 0) : c->partials;
-        q.partials2 = lean ? chk_partials(c, npp, 0) : c->partials2;
-        q.partials3 = (dist && !lean) ? c->partials3 : nullptr;   // lean: no rare path runs
         q.gfx = c->rgfx;
         q.gsy = c->rgsy;
         q.stats = c->stats;
@@ -781,6 +816,17 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         q.rc_lo = sr.rc_lo;
         q.rc_hi = sr.rc_hi;
         q.fast = (c->cfg.flags & PGMG_FLAG_FAST) != 0 && !dist;
+        q.sw_adj = sw_adj;
+        sw_adj = 0;
+        return q;
+    };
+    for (int k = 1; k < n; ++k) {
+        T *nx = next_of(pr);
+        if (dist && (e = c->comm->halo_end(c->s))) return e;
+        PostPreArgsT<T> q = postpre_args(pr, nx);
+        q.partials1 = lean ? chk_partials(c, npp, 0) : c->partials;
+        q.partials2 = lean ? chk_partials(c, npp, 0) : c->partials2;
+        q.partials3 = (dist && !lean) ? c->partials3 : nullptr;   // lean: no rare path runs
         ev = timed_begin(c, 3);
         if ((e = launch_postpre(q, c->s))) return e;
         if ((e = timed_end(c, 3, ev))) return e;
@@ -849,11 +895,50 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         c->pend_pr = pr;
         return PGMG_OK;
     }
+    // the solution's buffer becomes L.A, the carried iterate's Y (every level-0 grid mirrors
+    // the boundary, so any may play any role); an external output holds the solution instead
+    // (the level-0 grids keep their roles)
+    auto set_roles = [&](const T *sol, const T *carried) {
+        const Grid *all[4] = {&gA, &gB, &gS, &gY};
+        std::vector<Grid> rest;
+        for (const Grid *g : all)
+            if (g->base && g != grid_of(sol) && (carried == nullptr || g != grid_of(carried)))
+                rest.push_back(*g);
+        L.A = *grid_of(sol);
+        if (carried != nullptr) c->Y = *grid_of(carried);
+        size_t i = 0;
+        L.B = rest[i++];
+        c->S = rest[i++];
+        if (carried == nullptr && gY.base) c->Y = rest[i++];
+    };
+    if (make) {
+        // the carry pass: x2 (the result) into a grid that is neither the input A nor pr, x4 of
+        // the next cycle into another; its post check is this call's, its pre check the carry's
+        T *free2[2] = {nullptr, nullptr};
+        int m = 0;
+        for (T *g : {B, S, Y})
+            if (g != pr && m < 2) free2[m++] = g;
+        T *const out = free2[0], *const nx = free2[1];
+        PostPreArgsT<T> q = postpre_args(pr, nx);
+        q.x2 = out;
+        q.sw_adj -= 2;   // the pre-smooth's sweeps count in the call that uses them
+        q.partials1 = chk_partials(c, npp, 0);
+        q.partials2 = chk_log(c, npp, 0, 0);
+        c->carry_chk = (int)c->chks.size() - 1;
+        if (q.partials1 == nullptr || q.partials2 == nullptr) return set_err(PGMG_ERR_STATE, "carry pass: check log");
+        ev = timed_begin(c, 4);
+        if ((e = launch_postpre(q, c->s))) return e;
+        if ((e = timed_end(c, 4, ev))) return e;
+        set_roles(out, nx);
+        c->carry_made = true;
+        return PGMG_OK;
+    }
     T *out = xout != nullptr ? xout : next_of(pr);
     if (dist && (e = c->comm->halo_end(c->s))) return e;
     PostArgsT<T> po = make_post<T>(c, pr, out);
     if (xout != nullptr) po.Po = c->ext_P;
-    lp = chk_partials(c, np, 0);
+    po.sw_adj = sw_adj;
+    double *lp = chk_partials(c, np, 0);
     if (lp) po.partials = lp;
     ev = timed_begin(c, 2);
     if ((e = launch_post(po, true, c->s))) return e;
@@ -862,14 +947,9 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         if (dist && (e = global_sum(c, np, &fa.global_sum))) return e;
         launch_post_fixup(fa, po, c->s);
     }
-    // the solution's buffer becomes L.A (all three mirror the boundary); an external output
-    // holds it instead (the level-0 grids keep their roles)
     if (xout != nullptr) {
     } else if (lean) {
-        const Grid go = *grid_of(out), gp = *grid_of(pr);
-        L.A = go;
-        L.B = gA;
-        c->S = gp;
+        set_roles(out, nullptr);
     } else if (out != A) {
         std::swap(L.A, L.B);
     }
@@ -993,6 +1073,7 @@ int pgmg_destroy(pgmg_ctx *c)
     free_grid(c->ftop);
     if (c->ppflags) (void)hipFree(c->ppflags);
     free_grid(c->S);
+    free_grid(c->Y);
     free_grid(c->Ffmg);
     for (auto &g : c->Ffmg_l) free_grid(g);
     if (c->fmg_tab) (void)hipFree(c->fmg_tab);
@@ -1104,8 +1185,7 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         const PostRows pr = post_rows(c, l);
         nbk = fused_blocks(L.N, pr.jc0, pr.jc1);
         if (nbk > maxblocks) maxblocks = nbk;
-        nbk = std::max(postpre_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2),
-                       postpre_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2, c->fp32 && pp_q4()));
+        nbk = postpre_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2);
         if (nbk > maxblocks) maxblocks = nbk;
         nbk = std::max(tile_np(c, l, false), tile_np(c, l, true));
         if (nbk > maxblocks) maxblocks = nbk;
@@ -1117,6 +1197,9 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         }
     }
     if (rc == PGMG_OK && c->cross) rc = alloc_grid(c->S, c->lv[0]);
+    // the carry's fourth level-0 grid (one GPU; see "carry"): ~2.15 GB at N = 16385 fp64
+    if (rc == PGMG_OK && c->cross && c->comm == nullptr && !(cfg->flags & PGMG_FLAG_NO_CARRY))
+        rc = alloc_grid(c->Y, c->lv[0]);
     // partial sums of k_postpre's second and third checks (cross-cycle fusion, and the
     // F-cycle's fused smooth(3)), its decision flags
     if (rc == PGMG_OK && (hipMalloc((void **)&c->partials2, sizeof(double) * maxblocks) != hipSuccess ||
@@ -1220,6 +1303,7 @@ static int problem_reset(pgmg_ctx *c)
     HIPC(hipMemset(c->stats, 0, 4 * sizeof(unsigned long long)));
     HIPC(hipDeviceSynchronize());
     c->have_problem = true;
+    c->carry = false;
     c->spec_off = false;   // a new problem: speculate again, every level
     c->fspec_off = false;
     c->lvl_exact.assign(c->nb + 1, 0);
@@ -1313,6 +1397,9 @@ int pgmg_set_problem(pgmg_ctx *c, const double *phi0, const double *f)
     // write boundary rows/columns, the k_pre that reads it passes them through)
     if (c->S.base)
         HIPC(hipMemcpy2D(row_ptr(c->S, r0, L.P, L.es), pitch, row_ptr(L.A, r0, L.P, L.es), pitch,
+                         width, rows, hipMemcpyDeviceToDevice));
+    if (c->Y.base)   // the carry's grid likewise
+        HIPC(hipMemcpy2D(row_ptr(c->Y, r0, L.P, L.es), pitch, row_ptr(L.A, r0, L.P, L.es), pitch,
                          width, rows, hipMemcpyDeviceToDevice));
     if ((e = setup_rhs(c, f, r0, r1))) return e;
     return problem_reset(c);
@@ -1878,7 +1965,8 @@ static void spec_record_norms(pgmg_ctx *c, int n)
 // re-reduced and compared with its recorded decision (k_verify_checks; row strips: the ranks
 // agree by allreduce(min)).  *h = 1 when some check could not be confirmed -- the call must
 // be rolled back -- or the log overflowed; per-check norms and verdicts land in hnorm / hflag.
-static int spec_validate(pgmg_ctx *c, unsigned *h_out, bool *overflow_out)
+// Only the first n_any checks decide the rollback (the carry pass logs one more).
+static int spec_validate(pgmg_ctx *c, unsigned *h_out, bool *overflow_out, int n_any)
 {
     const int n = (int)c->chks.size();
     bool overflow = false;
@@ -1893,7 +1981,8 @@ static int spec_validate(pgmg_ctx *c, unsigned *h_out, bool *overflow_out)
         launch_verify_checks(c->chk_dev, n, c->cfg.eps, c->uflags, c->chk_norm, c->s);
         int e;
         if (c->comm && (e = c->comm->allreduce_min_u32(c->uflags, n, c->s))) return e;
-        launch_any_flag(c->uflags, n, any, c->s);
+        // (the checks past n_any -- the carried pre-smooth's -- never roll the call back)
+        launch_any_flag(c->uflags, n_any, any, c->s);
         HIPC(hipMemcpyAsync(&h, any, sizeof(unsigned), hipMemcpyDeviceToHost, c->s));
         HIPC(hipMemcpyAsync(c->hnorm.data(), c->chk_norm, n * sizeof(double),
                             hipMemcpyDeviceToHost, c->s));
@@ -1910,13 +1999,13 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
 {
     Level &L0 = c->lv[0];
     const int np0 = fused_blocks(L0.N, L0.lo / 2, (L0.hi < L0.N ? L0.hi : L0.N - 1) / 2);
-    const int npp = c->cross ? postpre_blocks(L0.N, L0.lo / 2, (L0.hi < L0.N ? L0.hi : L0.N - 1) / 2, c->fp32 && pp_q4()) : 0;
+    const int npp = c->cross ? postpre_blocks(L0.N, L0.lo / 2, (L0.hi < L0.N ? L0.hi : L0.N - 1) / 2) : 0;
     long long d1, k1;
     spec_need_level(c, 1, gamma, &d1, &k1);
     // (level 0 visits level 1 gamma times per cycle)
     const long long per_dbl = 2LL * std::max(np0, npp) + gamma * d1, per_chk = 2 + gamma * k1;
     // segments of at most 2^27 logged doubles (1 GiB) / 2^22 checks
-    long long seg_max = std::min(((1LL << 27) - 2LL * np0) / per_dbl, ((1LL << 22) - 2) / per_chk);
+    long long seg_max = std::min(((1LL << 27) - 2LL * std::max(np0, npp)) / per_dbl, ((1LL << 22) - 2) / per_chk);
     if (c->cfg.spec_segment > 0) seg_max = std::min<long long>(seg_max, c->cfg.spec_segment);
     if (seg_max < 1) return run_cycles_plain(c, ncycles, gamma);
     // the cross-fused cycles keep A intact (rotation through S); otherwise copy it
@@ -1933,13 +2022,13 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
         const int seg = spec_plan_segment(c, (int)std::min<long long>(ncycles, seg_max));
         c->x_in = first ? ext_in : nullptr;
         c->x_out = ext_out;
-        int e = spec_reserve(c, seg * per_dbl + 2LL * np0 + 64, seg * per_chk + 4);
+        int e = spec_reserve(c, seg * per_dbl + 2LL * std::max(np0, npp) + 64, seg * per_chk + 4);
         if (e) return e;
         if ((e = spec_mark_levels(c, seg))) return e;
         if (c->spec_off) return run_cycles_plain(c, ncycles, gamma, first);
         const bool last = seg == ncycles;
         const bool seg_first = first;
-        const Grid A0 = L0.A, B0 = L0.B, S0 = c->S;
+        const Grid A0 = L0.A, B0 = L0.B, S0 = c->S, Y0 = c->Y;
         if (!rotate) {
             if (!c->bk.base && (e = alloc_grid(c->bk, L0))) return e;
             HIPC(hipMemcpyAsync(c->bk.base, L0.A.base, L0.A.bytes, hipMemcpyDeviceToDevice, c->s));
@@ -1957,16 +2046,27 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
         std::fill(c->lvl_vis.begin(), c->lvl_vis.end(), 0);
         if (!last) c->x_out = nullptr;   // intermediate segments end in the level-0 grids
         c->defer_post = ext_out != nullptr && last;
+        // the carry: the last segment of a V call on the context's own grids ends with the
+        // carry pass (enqueue_cross_cycles, "carry"); c->carry_use was set by run_cycles for
+        // the first segment
+        c->carry_make = last && gamma == 1 && ext_out == nullptr &&
+                        !(c->cfg.flags & PGMG_FLAG_NO_CARRY);
+        c->carry_chk = -1;
         e = run_cycles_plain(c, seg, gamma, first);
         c->defer_post = false;
+        c->carry_make = false;
+        c->carry_use = false;
         c->x_out = ext_out;
         c->lean = false;
         first = false;
         if (e) return e;
-        const int n = (int)c->chks.size();
+        int n = (int)c->chks.size();
+        const bool made = c->carry_made && c->carry_chk == n - 1;
+        if (c->carry_made && !made) return set_err(PGMG_ERR_STATE, "carry check out of place");
+        c->carry_made = false;
         unsigned h = 0;
         bool overflow = false;
-        if ((e = spec_validate(c, &h, &overflow))) return e;
+        if ((e = spec_validate(c, &h, &overflow, made ? n - 1 : n))) return e;
         if (h) {
             // some check could fire: roll back this segment, rerun the rest of the call with
             // in-stream decisions; the levels whose checks could fire stay in-stream
@@ -1993,6 +2093,8 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
             L0.A = A0;
             L0.B = B0;
             c->S = S0;
+            c->Y = Y0;
+            c->carry = false;
             if (!rotate)
                 HIPC(hipMemcpyAsync(L0.A.base, c->bk.base, L0.A.bytes, hipMemcpyDeviceToDevice, c->s));
             HIPC(hipMemcpyAsync(c->stats, c->stats_bk, 4 * sizeof(unsigned long long),
@@ -2000,6 +2102,20 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
             c->x_in = seg_first ? ext_in : nullptr;
             c->pend_pr = nullptr;
             return run_cycles_plain(c, ncycles, gamma, false);
+        }
+        if (seg_first && c->carry_took) ++c->carry_n[0];
+        c->carry_took = false;
+        if (made) {
+            // the carried pre-smooth: usable unless its check could fire (then dropped: the
+            // next call runs its own k_pre); not one of this call's checks
+            const bool ok = !overflow && c->hflag[n - 1] == 0u;
+            c->carry = ok;
+            ++c->carry_n[ok ? 1 : 2];
+            --n;
+            c->chks.pop_back();
+            c->chk_visit.pop_back();
+            c->hnorm.pop_back();
+            c->hflag.pop_back();
         }
         spec_record_norms(c, n);
         if (ext_out != nullptr && last) {
@@ -2050,8 +2166,52 @@ static int run_cycles(pgmg_ctx *c, int ncycles, int gamma)
     if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
     if (!c->have_problem) return set_err(PGMG_ERR_STATE, "pgmg_set_problem first");
     if (ncycles <= 0) return PGMG_OK;
-    if (c->ext_phi) return run_cycles_ext(c, ncycles, gamma);
-    return run_cycles_core(c, ncycles, gamma);
+    // the carry is this call's to take (a V call on the context's own problem: the first
+    // speculative segment starts from it) or gone; a call that runs in-stream drops it
+    c->carry_use = c->carry && gamma == 1 && c->ext_phi == nullptr;
+    c->carry = false;
+    c->carry_took = false;
+    const int e = c->ext_phi ? run_cycles_ext(c, ncycles, gamma) : run_cycles_core(c, ncycles, gamma);
+    c->carry_use = false;
+    return e;
+}
+
+int pgmg_carry_info(pgmg_ctx *c, long long out[3])
+{
+    if (!c || !out) return set_err(PGMG_ERR_ARG, "null argument");
+    for (int i = 0; i < 3; ++i) out[i] = c->carry_n[i];
+    return PGMG_OK;
+}
+
+// JacobiSmoother(eps) (Smoother.hpp:38): a new threshold for the following calls.  The carried
+// pre-smooth was checked against the old one, and the speculation history's predictions are
+// relative to eps: both go (the statistics continue)
+int pgmg_set_eps(pgmg_ctx *c, double eps)
+{
+    if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
+    if (!(eps >= 0.0) || !std::isfinite(eps)) return set_err(PGMG_ERR_ARG, "eps must be finite and >= 0");
+    PGMG_TRY(stream_wait(c));
+    c->cfg.eps = eps;
+    c->carry = false;
+    if (c->gexec) {   // a captured cycle holds the old eps in its kernel arguments
+        HIPC(hipGraphExecDestroy(c->gexec));
+        c->gexec = nullptr;
+    }
+    c->spec_off = false;
+    c->fspec_off = false;
+    c->lvl_exact.assign(c->nb + 1, 0);
+    c->lvl_fire.assign(c->nb + 1, 0);
+    c->lvl_fire_block.assign(c->nb + 1, 0);
+    c->lvl_fire_try.assign(c->nb + 1, 0.0);
+    c->lvl_kx.assign(c->nb + 1, 0);
+    c->lvl_vis.assign(c->nb + 1, 0);
+    c->wmax.clear();
+    c->wmin.clear();
+    c->wrho.clear();
+    c->wplan_gamma = 0;
+    c->wplan_off = false;
+    c->lvl_hist.assign(c->nb + 1, std::vector<double>());
+    return PGMG_OK;
 }
 
 int pgmg_dist_info(pgmg_ctx *c, int *speculative, long long *rollbacks)
@@ -2316,6 +2476,7 @@ static int enqueue_fcycle(pgmg_ctx *c, int opt = 0)
         launch_zero_frame(G<T>(L.A), L.P, L.N, c->s, r0, r1);
         launch_zero_frame(G<T>(L.B), L.P, L.N, c->s, r0, r1);
         if (l == 0 && c->S.base) launch_zero_frame(G<T>(c->S), L.P, L.N, c->s, r0, r1);   // S mirrors too
+        if (l == 0 && c->Y.base) launch_zero_frame(G<T>(c->Y), L.P, L.N, c->s, r0, r1);   // and Y
         const bool use_pin = !(c->cfg.flags & PGMG_FLAG_NO_PIN);
         if (c->fused && use_pin) {
             // the V-cycle's k_pre computes the prolongation on the fly (PIN): no separate
@@ -2426,7 +2587,7 @@ static int run_fcycles_spec(pgmg_ctx *c, int ncycles)
     if (e) return e;
     unsigned h = 0;
     bool overflow = false;
-    if ((e = spec_validate(c, &h, &overflow))) return e;
+    if ((e = spec_validate(c, &h, &overflow, (int)c->chks.size()))) return e;
     if (!h) return PGMG_OK;
     ++c->rollbacks;
     c->fspec_off = true;
@@ -2448,6 +2609,7 @@ int pgmg_fcycle(pgmg_ctx *c, int ncycles)
     if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
     if (!c->have_problem) return set_err(PGMG_ERR_STATE, "pgmg_set_problem first");
     if (ncycles <= 0) return PGMG_OK;
+    c->carry = false;   // an F-cycle starts from phi itself
     int e = fmg_tables(c);
     if (e) return e;
     Level &L0 = c->lv[0];
@@ -2702,7 +2864,7 @@ int pgmg_vcycle_bytes(pgmg_ctx *c, double *bytes)
 
 int pgmg_fine_pass_bytes(pgmg_ctx *c, int pass, double *bytes)
 {
-    if (!c || !bytes || pass < 0 || pass > 3) return set_err(PGMG_ERR_ARG, "bad argument");
+    if (!c || !bytes || pass < 0 || pass > 4) return set_err(PGMG_ERR_ARG, "bad argument");
     if (c->nb == 0) return set_err(PGMG_ERR_STATE, "no bulk level");
     const Level &L = c->lv[0], &C = c->lv[1];
     const double n = (double)(L.u1 - L.u0) * (L.N - 2);
@@ -2716,6 +2878,7 @@ int pgmg_fine_pass_bytes(pgmg_ctx *c, int pass, double *bytes)
     case 1: b = (16.0 + fb) * n + 8.0 * nc; break;             // x0, (f) in; x2, rc out
     case 2: b = (16.0 + fb) * n + 8.0 * nc; break;             // phi, (f,) ec in; x2 out
     case 3: b = (16.0 + fb) * n + 16.0 * nc; break;            // phi, (f,) ec; x4, rc
+    case 4: b = (24.0 + fb) * n + 16.0 * nc; break;            // the same + x2 (carry pass)
     }
     *bytes = b * (L.es / 8.0);
     return PGMG_OK;
@@ -2741,6 +2904,7 @@ int pgmg_phi_device(pgmg_ctx *c, double **ptr, int *pitch, int *row0, int *rows)
 {
     if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
     Level &L = c->lv[0];
+    c->carry = false;   // the pointer allows writes to phi
     if (ptr) *ptr = static_cast<double *>(L.A.o);
     if (pitch) *pitch = L.P;
     if (row0) *row0 = L.lo;
@@ -2775,6 +2939,7 @@ int pgmg_bench_sweep(pgmg_ctx *c, int reps, double *ms)
 {
     if (!c || !ms || reps <= 0) return set_err(PGMG_ERR_ARG, "bad argument");
     if (c->nb == 0) return set_err(PGMG_ERR_STATE, "no bulk level");
+    c->carry = false;   // the sweeps overwrite phi
     auto run = [&](int n) { c->fp32 ? bench_sweeps<float>(c, n) : bench_sweeps<double>(c, n); };
     run(2);  // warm
     HIPC(hipEventRecord(c->ev0, c->s));
@@ -2789,7 +2954,7 @@ int pgmg_bench_sweep(pgmg_ctx *c, int reps, double *ms)
 
 int pgmg_fine_pass_time(pgmg_ctx *c, int pass, int *count, double *mean_ms)
 {
-    if (!c || pass < 0 || pass > 3) return set_err(PGMG_ERR_ARG, "bad argument");
+    if (!c || pass < 0 || pass > 4) return set_err(PGMG_ERR_ARG, "bad argument");
     PGMG_TRY(stream_wait(c));
     auto &pool = c->tpool[pass];
     double tot = 0.0;
@@ -2802,6 +2967,30 @@ int pgmg_fine_pass_time(pgmg_ctx *c, int pass, int *count, double *mean_ms)
     if (count) *count = n;
     if (mean_ms) *mean_ms = n ? tot / n : 0.0;
     pool.used = 0;
+    c->info_bytes[pass] = n ? c->tbytes[pass] / n : 0.0;
+    c->info_kern[pass] = n ? c->tkern[pass] : nullptr;
+    c->tbytes[pass] = 0.0;
+    c->tkern[pass] = nullptr;
+    return PGMG_OK;
+}
+
+int pgmg_fine_pass_info(pgmg_ctx *c, int pass, char *symbol, int len, double *bytes)
+{
+    if (!c || pass < 0 || pass > 4 || (symbol && len < 1)) return set_err(PGMG_ERR_ARG, "bad argument");
+    if (bytes) *bytes = c->info_bytes[pass];
+    if (symbol) {
+        std::string name;
+        if (c->info_kern[pass]) {
+            const char *m = hipKernelNameRefByPtr(c->info_kern[pass], c->s);
+            if (m) {
+                int st = 0;
+                char *d = abi::__cxa_demangle(m, nullptr, nullptr, &st);
+                name = (st == 0 && d) ? d : m;
+                std::free(d);
+            }
+        }
+        std::snprintf(symbol, (size_t)len, "%s", name.c_str());
+    }
     return PGMG_OK;
 }
 

@@ -75,6 +75,10 @@ struct PostArgsT {
     T *r2out;
     long long Pr2;
     int Nr2;
+    // added to the sweeps the pass counts (stats[0] += 2 + sw_adj): +2 on the first finest pass
+    // of a call that took over a carried pre-smooth (pgmg_ctx.hip "carry"), whose two sweeps
+    // were run by the previous call's last pass
+    int sw_adj;
 };
 
 // post-smooth of cycle k + pre-smooth/residual/restriction of cycle k+1 in one pass
@@ -100,6 +104,10 @@ struct PostPreArgsT {
     int rc_lo, rc_hi;
     int rows_per_block;
     int fast;                   // PGMG_FLAG_FAST (one GPU, f regenerated or stored)
+    // non-null: the carry pass, the LAST finest pass of a call that also runs the next call's
+    // pre-smooth (pgmg_ctx.hip "carry"): x2, the call's result, is stored here besides x4
+    T *x2;
+    int sw_adj;                 // stats[0] += 4 + sw_adj (the carry pass: -2; see PostArgsT)
 };
 
 struct FixArgsF {
@@ -138,10 +146,8 @@ template <class T> void launch_post_fixup(const FixArgsF &a, const PostArgsT<T> 
 template <class T>
 int launch_pre_rare(const FixArgsF &f, const PreArgsT<T> &a, bool x0_zero, hipStream_t s);
 template <class T> int launch_post_rare(const FixArgsF &f, const PostArgsT<T> &a, hipStream_t s);
-// k_postpre's workgroups (check partials); q4: the fp32 form k_postpre_q4 (launch_postpre of
-// an fp32 context with pp_q4(); the F-cycle's smooth(3) keeps the 2-column kernel)
-int postpre_blocks(int N, int jc0, int jc1, bool q4 = false);
-bool pp_q4();   // fp32 launch_postpre runs k_postpre_q4 (PGMG_PPQ=1, measurement build only)
+// k_postpre's workgroups (check partials)
+int postpre_blocks(int N, int jc0, int jc1);
 template <class T> int launch_postpre(const PostPreArgsT<T> &a, hipStream_t s);
 // fused smooth(3): x4 of a.phi into a.x4 with the three checks' partial sums
 // (partials1 r(x1), partials3 r(x2), partials2 r(x3)); then the decision + rare path

@@ -583,7 +583,7 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
     const int slo = a.sum_hi > a.sum_lo ? max(olo, a.sum_lo) : olo;
     const int shi = a.sum_hi > a.sum_lo ? min(ohi, a.sum_hi) : ohi;
     if (!S1 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
-        atomicAdd(&a.stats[0], 2ull);
+        atomicAdd(&a.stats[0], (unsigned long long)(2 + a.sw_adj));
     ProlongCols pc;
     pc.ic = (k.c - 1) >> 1;
     pc.vx = k.c >= 3 && k.c <= N - 2;
@@ -989,7 +989,8 @@ template <class T> using PPC = typename std::conditional<pp_qc<T>(), float4, V2<
 // same IEEE operations as k_rhs, so the values are identical to the stored f.  One
 // multiply per point replaces 8 bytes per point of the pass (28 -> 20 B/pt).
 // OPT (compile-time, result-identical): 2 non-temporal x4 stores, 4 non-temporal rc
-// stores, 64 the F-cycle's smooth(3) (no correction, no restriction).
+// stores, 64 the F-cycle's smooth(3) (no correction, no restriction), 128 the carry pass
+// (x2 stored too: the last pass of a call that hands the next call its pre-smooth).
 // Logical block of the 2D grid (x: column block, y: band).
 struct Blk {
     int x, y;
@@ -1088,7 +1089,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     const int olo = max(2 * jcb, a.row_lo), ohi = min(2 * jce, a.row_hi);
     const int clo = max(jcb, max(1, a.rc_lo)), chi = min(jce, min(N / 2, a.rc_hi));
     if (bk.x == 0 && bk.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
-        atomicAdd(&a.stats[0], 4ull);
+        atomicAdd(&a.stats[0], (unsigned long long)(4 + a.sw_adj));
     ProlongCols pc;
     pc.ic = (k.c - 1) >> 1;
     pc.vx = k.c >= 3 && k.c <= N - 2;
@@ -1276,6 +1277,10 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
             // post-smooth sweep 2: x2 row ii-2 (= phi of cycle k+1)
             const V2<T> c2 = FAST ? jsum<T, EDGE>(sb, b1, hq2, k, boundary_row(ii - 2, N))
                                   : jsh<T, EDGE>(b0, b1, b2, nb1, hq2, k, boundary_row(ii - 2, N));
+            if constexpr ((OPT & 128) != 0) {   // the carry pass: x2 is the call's result
+                const int xb2 = (ii - 2 >= olo && ii - 2 < ohi) ? xbytes : 0;
+                buf_store_row<T, (OPT & 2) ? 1 : 0>(a.x2 + (long long)(ii - 2) * P + L0, xb2, xoff, c2);
+            }
             if (R2) {   // r(x2) on row ii-3
                 const V2<T> r2 = rsn<T>(c0, c1, c2, nc1, fq3, ih);
                 const int row = ii - 3;
@@ -1410,364 +1415,6 @@ void k_postpre_lds(PostPreArgsT<T> a)
         postpre_lds_run<T, R2, GENF, false, OPT>(a, k, red, sx, sf, se, bk);
 }
 
-// ---------------------------------------------------------------------------
-// k_postpre_q4 (fp32, r05): the cross-cycle finest-level pass with FOUR columns per lane.
-// The 2-column form of k_postpre_lds streams fp32 rows as 8-byte lane accesses and spends its
-// per-lane row work (LDS reads, DPP, address and loop bookkeeping) on 8 bytes per row and
-// array; here lane t owns the quad (c, c+1, c+2, c+3), c = 1 mod 4 (one 16-byte load, LDS
-// read and store per row and array).  A wave tile loads 256 columns and owns the 240 of lanes
-// 2..61 (six stencil levels shrink the validity six columns per side; the 8-column margin
-// keeps every quad 16-byte aligned); a block's 4 waves stage a 976-column window (244 quads)
-// per row.  Horizontal neighbours: inside the quad, or the adjacent lane's .w / .x by DPP.
-// The prolongation of a quad reads coarse columns ic, ic+1, ic+2 (ic = (c-1)/2), staged per
-// coarse row in LDS from 16-byte loads starting at cc0 - 3 (aligned); the restriction forms
-// the coarse columns of the quad's two even fine columns c+1 and c+3 (right neighbour of c+3:
-// the next lane's .x).  Same row pipeline, checks, stores and expressions as k_postpre_lds,
-// element by element, so the results are bitwise those of the 2-column form (and of the fp32
-// restatement of the oracle).
-// ---------------------------------------------------------------------------
-constexpr int kQStride = 240, kQMargin = 8;
-constexpr int kQLdsRow = kPPWaves * kQStride + 2 * kQMargin + 4;     // 980 floats
-constexpr int kQCoarseShift = 3;                                     // coarse col cc0 - 3 at 0
-constexpr int kQLdsCoarse = 124 * 4;                                 // 123 quads + pad
-
-struct ColsQ {
-    int c;            // first column of the quad (c = 1 mod 4 relative to column 1)
-    bool b[4];        // column c+k is a boundary or outside column: passthrough
-    bool own[4];      // the lane owns the quad and column c+k <= N-2
-    bool lown;        // lane 2..61 of the tile and c <= N-2
-    bool edge;        // wave-uniform: some loaded column is a boundary/outside column
-};
-
-__device__ __forceinline__ ColsQ lane_cols_q(int N, int bx)
-{
-    const int wave = (bx * blockDim.x + threadIdx.x) >> 6;
-    const int lane = threadIdx.x & 63;
-    ColsQ k;
-    k.c = kQStride * wave + 1 - kQMargin + 4 * lane;
-    k.lown = lane >= kQMargin / 4 && lane < kQMargin / 4 + kQStride / 4 && k.c <= N - 2;
-    #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        k.b[q] = k.c + q <= 0 || k.c + q >= N - 1;
-        k.own[q] = k.lown && k.c + q <= N - 2;
-    }
-    const int c0 = __builtin_amdgcn_readfirstlane(kQStride * wave + 1 - kQMargin);
-    k.edge = c0 <= 0 || c0 + 255 >= N - 1;
-    return k;
-}
-
-struct NbrQ {
-    float l, r;   // column c-1 (previous lane's .w), column c+4 (next lane's .x)
-};
-__device__ __forceinline__ NbrQ nbrq(float4 ce) { return NbrQ{dpp_shr(ce.w), dpp_shl(ce.x)}; }
-
-// Jacobi stage of a quad row with hh*f precomputed (jsh, element by element)
-template <bool EDGE>
-__device__ __forceinline__ float4 jq(float4 up, float4 ce, float4 dn, NbrQ n, float4 hf,
-                                     const ColsQ &k, bool brow)
-{
-    float4 o;
-    o.x = 0.25f * (hf.x + n.l + ce.y + up.x + dn.x);
-    o.y = 0.25f * (hf.y + ce.x + ce.z + up.y + dn.y);
-    o.z = 0.25f * (hf.z + ce.y + ce.w + up.z + dn.z);
-    o.w = 0.25f * (hf.w + ce.z + n.r + up.w + dn.w);
-    if constexpr (EDGE) {
-        if (brow || k.b[0]) o.x = ce.x;
-        if (brow || k.b[1]) o.y = ce.y;
-        if (brow || k.b[2]) o.z = ce.z;
-        if (brow || k.b[3]) o.w = ce.w;
-    }
-    return o;
-}
-// residual of a quad row (rsn, element by element)
-__device__ __forceinline__ float4 rq(float4 up, float4 ce, float4 dn, NbrQ n, float4 f, float ih)
-{
-    float4 o;
-    o.x = f.x - ih * (4.0f * ce.x - n.l - ce.y - up.x - dn.x);
-    o.y = f.y - ih * (4.0f * ce.y - ce.x - ce.z - up.y - dn.y);
-    o.z = f.z - ih * (4.0f * ce.z - ce.y - ce.w - up.z - dn.z);
-    o.w = f.w - ih * (4.0f * ce.w - ce.z - n.r - up.w - dn.w);
-    return o;
-}
-// prolongation into a quad row (add_prolong, MultiGrid.hpp:219-223): coarse row m = row/2
-// columns ic, ic+1, ic+2 (ca, cb, cc) and row m+1 (da, db, dc); odd fine columns (c, c+2)
-// are corrected on [3, N-2], even ones (c+1, c+3) on [2, N-3]
-template <bool EDGE>
-__device__ __forceinline__ float4 prolq(float4 p, int row, float ca, float cb, float cc, float da,
-                                        float db, float dc, const bool (&v)[4], int Nc)
-{
-    const int m = row >> 1;
-    if (EDGE && (m < 1 || m > Nc - 2)) return p;
-    if ((row & 1) == 0) {
-        if (!EDGE || v[0]) p.x = p.x + 0.5f * (ca + cb);
-        if (!EDGE || v[1]) p.y = p.y + cb;
-        if (!EDGE || v[2]) p.z = p.z + 0.5f * (cb + cc);
-        if (!EDGE || v[3]) p.w = p.w + cc;
-    } else {
-        if (!EDGE || v[0]) p.x = p.x + 0.25f * (ca + cb + da + db);
-        if (!EDGE || v[1]) p.y = p.y + 0.5f * (cb + db);
-        if (!EDGE || v[2]) p.z = p.z + 0.25f * (cb + cc + db + dc);
-        if (!EDGE || v[3]) p.w = p.w + 0.5f * (cc + dc);
-    }
-    return p;
-}
-__device__ __forceinline__ double sq4(double acc, float4 r, const ColsQ &k)
-{
-    if (k.own[0]) acc = sqacc(acc, r.x);
-    if (k.own[1]) acc = sqacc(acc, r.y);
-    if (k.own[2]) acc = sqacc(acc, r.z);
-    if (k.own[3]) acc = sqacc(acc, r.w);
-    return acc;
-}
-__device__ __forceinline__ void buf_store_f2(float *base, int bytes, int off, float a, float b)
-{
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, bytes, 0x00020000);
-    typedef unsigned u2 __attribute__((ext_vector_type(2)));
-    u2 v;
-    v.x = __builtin_bit_cast(unsigned, a);
-    v.y = __builtin_bit_cast(unsigned, b);
-    __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, 0);
-}
-
-template <bool R2, bool GENF, bool EDGE>
-__device__ __forceinline__ void postpre_q4_run(const PostPreArgsT<float> &a, const ColsQ &k,
-                                               double *red, float (&sx)[2][kPPR][kQLdsRow],
-                                               float (&sf)[2][kPPR][GENF ? 4 : kQLdsRow],
-                                               float (&se)[3][kQLdsCoarse], const Blk bk)
-{
-    constexpr int R = kPPR;
-    const int N = a.N, Nc = a.Nc;
-    const long long P = a.P, Pc = a.Pc;
-    const int jcb = a.jc0 + bk.y * a.rows_per_block;
-    const int jce = min(jcb + a.rows_per_block, a.jc1);
-    const int olo = max(2 * jcb, a.row_lo), ohi = min(2 * jce, a.row_hi);
-    const int clo = max(jcb, max(1, a.rc_lo)), chi = min(jce, min(N / 2, a.rc_hi));
-    if (bk.x == 0 && bk.y == 0 && threadIdx.x == 0 && a.stats != nullptr)
-        atomicAdd(&a.stats[0], 4ull);
-    bool pv[4];   // prolongation corrects column c+q
-    #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int col = k.c + q;
-        pv[q] = (q & 1) == 0 ? (col >= 3 && col <= N - 2) : (col >= 2 && col <= N - 3);
-    }
-    const float hh = a.hh, ih = a.ih;
-    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-
-    const int t = threadIdx.x;
-    const int wpb = blockDim.x >> 6;
-    const int L0 = kQStride * wpb * bk.x + 1 - kQMargin;     // = 1 mod 4: 16-byte aligned
-    const int nq = (kQStride * wpb + 2 * kQMargin) / 4;      // quads per window row (244)
-    const int cc0 = (L0 - 1) >> 1;                           // coarse column of the first quad
-    const int cb0 = cc0 - kQCoarseShift;                     // first staged coarse column
-    const int ncq = kQLdsCoarse / 4 - 1;                     // coarse quads per row (123)
-    // quads inside the row (columns <= N-1; the rest read 0) and coarse quads (<= Nc-1)
-    const int nvq = max(0, min(nq, (N - 1 - L0) / 4 + 1));
-    const int nvc = max(0, min(ncq, (Nc - 1 - cb0) / 4 + 1));
-    constexpr int kOOB = 1 << 30;
-    // stores: the quad of an owning lane (a partly owned quad at the grid's right edge: its
-    // owned columns one by one); rc: the coarse columns of fine columns c+1 and c+3
-    const int xbytes = (4 * nq + 8) * 4;
-    const int xoff = (k.c - L0) * 4;
-    const bool xfull = k.own[0] && k.own[3];
-    const int ica = (k.c + 1) >> 1;                          // coarse column of fine c+1
-    const bool oa = k.own[1] && ica >= 1 && ica <= Nc - 2, ob = k.own[3] && ica + 1 <= Nc - 2;
-    const int cbytes = (2 * nq + 16) * 4;
-    const int coff2 = (oa && ob) ? (ica - cc0) * 4 : kOOB;
-    const int coffa = (EDGE && oa && !ob) ? (ica - cc0) * 4 : kOOB;
-    const int coffb = (EDGE && ob && !oa) ? (ica + 1 - cc0) * 4 : kOOB;
-    double fx[4] = {0.0, 0.0, 0.0, 0.0};
-    if constexpr (GENF) {
-        #pragma unroll
-        for (int q = 0; q < 4; ++q) fx[q] = a.gfx[k.c + q];
-    }
-    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): fx landed before the row loop
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int xo = kQStride * w + 4 * lane;                  // this lane's quad in the LDS row
-    const int co = (kQStride / 2) * w + 2 * lane + kQCoarseShift;   // coarse column ic
-
-    float4 e0 = z, e1 = z, b0 = z, b1 = z, c0 = z, c1 = z, g0 = z, g1 = z, h0 = z, h1 = z,
-           d0 = z, d1 = z;
-    float4 f1 = z, f2 = z, f3 = z, f4 = z, f5 = z;
-    float4 q1 = z, q2 = z, q3 = z, q4 = z;
-    double acc1 = 0.0, acc2 = 0.0, acc3 = 0.0;
-    const int i_begin = 2 * jcb - 6;
-    const int ng = (2 * (jce - jcb) + 11 + R - 1) / R;
-    const int m0 = i_begin >> 1;
-    auto ring = [](int m) { return (m + 3 * 4096) % 3; };
-
-    if (t < 2 * R * 4) {   // the pad past the window (never owned data)
-        const int sl = t >> 3, q = (t >> 2) & 1, j = kQLdsRow - 4 + (t & 3);
-        sx[sl][q][j] = 0.f;
-        if constexpr (!GENF) sf[sl][q][j] = 0.f;
-    }
-    constexpr int D = 3;
-    float4 pxA[R], pfA[R], pxB[R], pfB[R], pxC[R], pfC[R];
-    float4 peA = z, peB = z, peC = z;
-    auto load_pair = [&](int p, float4 (&px)[R], float4 (&pf)[R], float4 &pe) {
-        #pragma unroll
-        for (int q = 0; q < R; ++q) {
-            const long long row = (long long)(i_begin + p * R + q) * P + L0;
-            px[q] = buf_quad(a.phi + row, nvq, t);
-            if constexpr (!GENF) pf[q] = buf_quad(a.f + row, nvq, t);
-        }
-        pe = buf_quad(a.ec + (long long)(m0 + p + 1) * Pc + cb0, nvc, t);   // 2nd coarse row
-    };
-    auto store_pair = [&](int p, const float4 (&px)[R], const float4 (&pf)[R], float4 pe) {
-        if (t < nq) {
-            #pragma unroll
-            for (int q = 0; q < R; ++q) {
-                *reinterpret_cast<float4 *>(&sx[p & 1][q][4 * t]) = px[q];
-                if constexpr (!GENF) *reinterpret_cast<float4 *>(&sf[p & 1][q][4 * t]) = pf[q];
-            }
-        }
-        if (t < ncq) *reinterpret_cast<float4 *>(&se[ring(m0 + p + 1)][4 * t]) = pe;
-    };
-    load_pair(0, pxA, pfA, peA);
-    {
-        const float4 v = buf_quad(a.ec + (long long)m0 * Pc + cb0, nvc, t);
-        if (t < ncq) *reinterpret_cast<float4 *>(&se[ring(m0)][4 * t]) = v;
-    }
-    store_pair(0, pxA, pfA, peA);
-    if (ng > 1) load_pair(1, pxB, pfB, peB);
-    if (ng > 2) load_pair(2, pxC, pfC, peC);
-    if (ng > 3) load_pair(3, pxA, pfA, peA);
-    __syncthreads();
-
-    float wprev = 0.f;   // dpp_shl(d2.x) of the previous restriction row
-    auto step = [&](int gi, float4 (&px)[R], float4 (&pf)[R], float4 &pe) {
-        __builtin_amdgcn_sched_barrier(0);
-        const int slot = gi & 1;
-        if (gi + 1 < ng) store_pair(gi + 1, px, pf, pe);
-        if (gi + 1 + D < ng) load_pair(gi + 1 + D, px, pf, pe);
-        const int i = i_begin + gi * R;
-        const int m = m0 + gi;
-        const float *E0 = se[ring(m)], *E1 = se[ring(m + 1)];
-        const float ca = E0[co], cb = E0[co + 1], cc = E0[co + 2];
-        const float da = E1[co], db = E1[co + 1], dc = E1[co + 2];
-        #pragma unroll
-        for (int s = 0; s < R; ++s) {
-            const int ii = i + s;
-            const float4 xr = *reinterpret_cast<const float4 *>(&sx[slot][s][xo]);
-            float4 f0 = z;
-            if constexpr (!GENF) f0 = *reinterpret_cast<const float4 *>(&sf[slot][s][xo]);
-            if constexpr (GENF) {
-                const double sy = gsy_s(a.gsy, ii);
-                f0 = make_float4((float)(fx[0] * sy), (float)(fx[1] * sy), (float)(fx[2] * sy),
-                                 (float)(fx[3] * sy));
-            }
-            const float4 qq0 = make_float4(hh * f0.x, hh * f0.y, hh * f0.z, hh * f0.w);
-            const float4 e2 = prolq<EDGE>(xr, ii, ca, cb, cc, da, db, dc, pv, Nc);
-            // post-smooth sweep 1: x1 row ii-1
-            const float4 b2 = jq<EDGE>(e0, e1, e2, nbrq(e1), q1, k, boundary_row(ii - 1, N));
-            const NbrQ nb1 = nbrq(b1), nc1 = nbrq(c1), ng1 = nbrq(g1);
-            {   // post check: r(x1) on row ii-2
-                const float4 r1 = rq(b0, b1, b2, nb1, f2, ih);
-                const int row = ii - 2;
-                if (row >= olo && row < ohi) acc1 = sq4(acc1, r1, k);
-            }
-            // post-smooth sweep 2: x2 row ii-2
-            const float4 c2 = jq<EDGE>(b0, b1, b2, nb1, q2, k, boundary_row(ii - 2, N));
-            if (R2) {   // r(x2) on row ii-3
-                const float4 r2 = rq(c0, c1, c2, nc1, f3, ih);
-                const int row = ii - 3;
-                if (row >= olo && row < ohi) acc3 = sq4(acc3, r2, k);
-            }
-            // pre-smooth sweep 1: x3 row ii-3
-            const float4 g2 = jq<EDGE>(c0, c1, c2, nc1, q3, k, boundary_row(ii - 3, N));
-            {   // pre check: r(x3) on row ii-4
-                const float4 r3 = rq(g0, g1, g2, ng1, f4, ih);
-                const int row = ii - 4;
-                if (row >= olo && row < ohi) acc2 = sq4(acc2, r3, k);
-            }
-            // pre-smooth sweep 2: x4 row ii-4 (stored)
-            const float4 h2 = jq<EDGE>(g0, g1, g2, ng1, q4, k, boundary_row(ii - 4, N));
-            {
-                const int xb = (ii - 4 >= olo && ii - 4 < ohi) ? xbytes : 0;
-                float *xrow = a.x4 + (long long)(ii - 4) * P + L0;
-                buf_store_quad<1>(xrow, xb, xfull ? xoff : kOOB, h2);
-                if constexpr (EDGE) {   // a partly owned quad: its owned columns
-                    const bool part = k.own[0] && !xfull;
-                    buf_store_one<float>(xrow, xb, part ? xoff : kOOB, h2.x);
-                    buf_store_one<float>(xrow, xb, (part && k.own[1]) ? xoff + 4 : kOOB, h2.y);
-                    buf_store_one<float>(xrow, xb, (part && k.own[2]) ? xoff + 8 : kOOB, h2.z);
-                }
-            }
-            // r(x4) on row ii-5
-            const float4 d2 = rq(h0, h1, h2, nbrq(h1), f5, ih);
-            // restriction: rows ii-7, ii-6, ii-5 = 2jc-1, 2jc, 2jc+1 when ii is even
-            if ((s & 1) == 0) {
-                const int jc = (ii - 6) >> 1;
-                const float r1n = dpp_shl(d1.x);   // column c+4 of rows 2jc, 2jc+1, 2jc-1
-                const float r2n = dpp_shl(d2.x);
-                const float r0n = wprev;
-                wprev = r2n;
-                // centre c+1: MultiGrid.hpp:195-202 order
-                const float va = 0.25f * d1.y + 0.125f * (d1.z + d1.x + d2.y + d0.y) +
-                                 0.0625f * (d0.x + d0.z + d2.x + d2.z);
-                // centre c+3
-                const float vb = 0.25f * d1.w + 0.125f * (r1n + d1.z + d2.w + d0.w) +
-                                 0.0625f * (d0.z + r0n + d2.z + r2n);
-                const bool in = jc >= clo && jc < chi;
-                float *crow = a.rc + (long long)jc * Pc + cc0;
-                buf_store_f2(crow, in ? cbytes : 0, coff2, va, vb);
-                if constexpr (EDGE) {
-                    buf_store_one<float>(crow, in ? cbytes : 0, coffa, va);
-                    buf_store_one<float>(crow, in ? cbytes : 0, coffb, vb);
-                }
-            }
-            e0 = e1; e1 = e2;
-            b0 = b1; b1 = b2;
-            c0 = c1; c1 = c2;
-            g0 = g1; g1 = g2;
-            h0 = h1; h1 = h2;
-            d0 = d1; d1 = d2;
-            f5 = f4; f4 = f3; f3 = f2; f2 = f1; f1 = f0;
-            q4 = q3; q3 = q2; q2 = q1; q1 = qq0;
-        }
-        __syncthreads();
-    };
-    int gi = 0;
-    for (; gi + 3 <= ng; gi += 3) {
-        step(gi, pxB, pfB, peB);
-        step(gi + 1, pxC, pfC, peC);
-        step(gi + 2, pxA, pfA, peA);
-    }
-    if (gi < ng) step(gi, pxB, pfB, peB);
-    if (gi + 1 < ng) step(gi + 1, pxC, pfC, peC);
-    const int slot = bk.y * gridDim.x + bk.x;
-    const double s1 = fused_block_sum(acc1, red);
-    __syncthreads();
-    const double s2 = fused_block_sum(acc2, red);
-    if (R2) {
-        __syncthreads();
-        const double s3 = fused_block_sum(acc3, red);
-        if (threadIdx.x == 0) a.partials3[slot] = s3;
-    }
-    if (threadIdx.x == 0) {
-        a.partials1[slot] = s1;
-        a.partials2[slot] = s2;
-    }
-}
-
-template <bool R2, bool GENF>
-__global__ __launch_bounds__(64 * kPPWaves) __attribute__((amdgpu_waves_per_eu(2)))
-void k_postpre_q4(PostPreArgsT<float> a)
-{
-    __shared__ double red[kPPWaves];
-    __shared__ __attribute__((aligned(16))) float sx[2][kPPR][kQLdsRow];
-    __shared__ __attribute__((aligned(16))) float sf[2][kPPR][GENF ? 4 : kQLdsRow];
-    __shared__ __attribute__((aligned(16))) float se[3][kQLdsCoarse];
-    const Blk bk{(int)blockIdx.x, (int)blockIdx.y};
-    const ColsQ k = lane_cols_q(a.N, bk.x);
-    const int jcb = a.jc0 + bk.y * a.rows_per_block;
-    const int jce = min(jcb + a.rows_per_block, a.jc1);
-    const bool edge_rows = 2 * jcb - 6 <= 0 || 2 * jce + 6 >= a.N - 1;
-    if (k.edge || edge_rows)
-        postpre_q4_run<R2, GENF, true>(a, k, red, sx, sf, se, bk);
-    else
-        postpre_q4_run<R2, GENF, false>(a, k, red, sx, sf, se, bk);
-}
-
 // one block: both decisions, stats, flags for the conditional rare-path kernels
 // global != nullptr (row strips): the all-rank sums {post, pre} instead of the partials
 __global__ __launch_bounds__(256) void k_postpre_decide(const double *p1, const double *p2, int np,
@@ -1817,6 +1464,8 @@ __global__ __launch_bounds__(256) void k_postpre_decide(const double *p1, const 
 // Launch geometry.  Blocks march down long row bands: the grid is sized to about
 // the number of workgroups resident at once, so the 8 halo rows per band are a small
 // fraction and there is no tail wave of blocks.
+thread_local LaunchNote g_last_launch;
+
 #ifdef PGMG_TUNING
 int tuning_int(const char *name, int dflt)
 {
@@ -2007,6 +1656,7 @@ static int postpre_spans(const PostPreArgsT<T> &a, int t, int gx, int r, bool co
         PGMG_SPAN(a.ec, a.Pc, a.jc0 - 3, fdiv2(sp.r1 + 1), e0, e1, "k_postpre coarse correction");
     const int olo = std::max(2 * a.jc0, a.row_lo), ohi = std::min(2 * a.jc1, a.row_hi);
     PGMG_SPAN(a.x4, a.P, olo, ohi - 1, 1, a.N - 1, "k_postpre x4");
+    if (a.x2 != nullptr) PGMG_SPAN(a.x2, a.P, olo, ohi - 1, 1, a.N - 1, "k_postpre x2 (carry pass)");
     if (coarse && a.rc != nullptr) {
         const int clo = std::max(a.jc0, std::max(1, a.rc_lo));
         const int chi = std::min(a.jc1, std::min(a.N / 2, a.rc_hi));
@@ -2033,22 +1683,39 @@ int launch_pre(const PreArgsT<T> &a0, bool x0_zero, bool fine, hipStream_t s)
     // two row pairs per iteration (r01 sweeps: on x0 = 0 levels 2 as fast as 3 at 8193 and
     // faster below, 4 slower; one pair slower everywhere)
     if (a.pin_ec != nullptr) {   // F-cycle: x0 = prolongation of the coarse grid
-        if (fine && a.gfx != nullptr) k_pre<T, false, true, 2, true, true><<<g, b, 0, s>>>(a);
-        else if (fine) k_pre<T, false, true, 2, false, true><<<g, b, 0, s>>>(a);
-        else if (a.gfx != nullptr) k_pre<T, false, false, 2, true, true><<<g, b, 0, s>>>(a);
-        else k_pre<T, false, false, 2, false, true><<<g, b, 0, s>>>(a);
+        if (fine && a.gfx != nullptr) launchk(k_pre<T, false, true, 2, true, true>, g, b, s, a);
+        else if (fine) launchk(k_pre<T, false, true, 2, false, true>, g, b, s, a);
+        else if (a.gfx != nullptr) launchk(k_pre<T, false, false, 2, true, true>, g, b, s, a);
+        else launchk(k_pre<T, false, false, 2, false, true>, g, b, s, a);
     } else if (x0_zero) {
-        k_pre<T, true, false, 2><<<g, b, 0, s>>>(a);
+        launchk(k_pre<T, true, false, 2>, g, b, s, a);
     } else if (fine && a.gfx != nullptr) {
-        k_pre<T, false, true, 2, true><<<g, b, 0, s>>>(a);
+        launchk(k_pre<T, false, true, 2, true>, g, b, s, a);
     } else if (fine) {
-        k_pre<T, false, true, 2><<<g, b, 0, s>>>(a);
+        launchk(k_pre<T, false, true, 2>, g, b, s, a);
     } else if (a.gfx != nullptr) {
-        k_pre<T, false, false, 2, true><<<g, b, 0, s>>>(a);
+        launchk(k_pre<T, false, false, 2, true>, g, b, s, a);
     } else {
-        k_pre<T, false, false, 2><<<g, b, 0, s>>>(a);
+        launchk(k_pre<T, false, false, 2>, g, b, s, a);
     }
+    // x0 (unless zero or the F-cycle's prolongation, which reads the coarse grid instead), f
+    // (unless regenerated) in; x2 (unless recomputed later), rc out
+    const double n = row_pts(std::max(2 * a.jc0, a.row_lo), std::min(2 * a.jc1, a.row_hi), a.N);
+    const double nc = row_pts(a.rc_lo, a.rc_hi, a.Nc);
+    const bool rx0 = !x0_zero && a.pin_ec == nullptr;
+    g_last_launch.bytes = (8.0 * n * ((rx0 ? 1 : 0) + (a.gfx == nullptr ? 1 : 0) + (a.x2 != nullptr ? 1 : 0)) +
+                           8.0 * nc * (a.pin_ec != nullptr ? 2 : 1)) * sizeof(T) / 8.0;
     return PGMG_OK;
+}
+
+// phi (unless recomputed from f), f (unless regenerated), ec in; x2 out
+template <class T>
+static double post_bytes(const PostArgsT<T> &a)
+{
+    const double n = row_pts(std::max(2 * a.jc0, a.row_lo), std::min(2 * a.jc1, a.row_hi), a.N);
+    const double nc = row_pts(std::max(a.jc0, 1), std::min(a.jc1 + 1, a.Nc - 1), a.Nc);
+    return (8.0 * n * ((a.pre_fired == nullptr ? 1 : 0) + (a.gfx == nullptr ? 1 : 0) + 1) + 8.0 * nc) *
+           sizeof(T) / 8.0;
 }
 
 template <class T>
@@ -2063,11 +1730,12 @@ int launch_post(const PostArgsT<T> &a0, bool fine, hipStream_t s)
     a.nt = fine ? 4 : 0;
     const dim3 g(gx, gy), b(t);
     const bool rec = a.pre_fired != nullptr;
-    if (fine && a.gfx != nullptr) k_post<T, true, 2, false, true><<<g, b, 0, s>>>(a);
-    else if (fine) k_post<T, true, 2, false><<<g, b, 0, s>>>(a);
-    else if (rec) k_post<T, false, 2, true><<<g, b, 0, s>>>(a);
-    else if (a.gfx != nullptr) k_post<T, false, 2, false, true><<<g, b, 0, s>>>(a);
-    else k_post<T, false, 2, false><<<g, b, 0, s>>>(a);
+    if (fine && a.gfx != nullptr) launchk(k_post<T, true, 2, false, true>, g, b, s, a);
+    else if (fine) launchk(k_post<T, true, 2, false>, g, b, s, a);
+    else if (rec) launchk(k_post<T, false, 2, true>, g, b, s, a);
+    else if (a.gfx != nullptr) launchk(k_post<T, false, 2, false, true>, g, b, s, a);
+    else launchk(k_post<T, false, 2, false>, g, b, s, a);
+    g_last_launch.bytes = post_bytes(a);
     return PGMG_OK;
 }
 
@@ -2085,8 +1753,10 @@ int launch_post_r2(const PostArgsT<T> &a0, hipStream_t s)
     a.rows_per_block = r;
     a.nt = 4 | (tuning_int("PGMG_R2_EALL", 0) ? 8 : 0);
     const dim3 g(gx, gy), b(t);
-    if (a.gfx != nullptr) k_post_r2<T, true><<<g, b, 0, s>>>(a);
-    else k_post_r2<T, false><<<g, b, 0, s>>>(a);
+    if (a.gfx != nullptr) launchk(k_post_r2<T, true>, g, b, s, a);
+    else launchk(k_post_r2<T, false>, g, b, s, a);
+    // k_post's, plus the level-2 restriction written
+    g_last_launch.bytes = post_bytes(a) + 8.0 * row_pts(1, a.Nr2 - 1, a.Nr2) * sizeof(T) / 8.0;
     return PGMG_OK;
 }
 
@@ -2105,62 +1775,11 @@ static int pp_target(int jc0, int jc1)
     return tuning_int("PGMG_PP_BLOCKS", (2048 / kPPWaves) * rounds);   // 512 resident at 4 waves
 }
 
-// fp32 contexts run k_postpre_q4 only with PGMG_PPQ=1 (measurement build).  Measured (r05,
-// scripts/pp_ab.py --dtype f32, profiles/r05_fp32/pp_f32_q4.jsonl, 3 interleaved rounds at
-// N = 16385, bitwise equal): 0.723-0.732 ms per launch (1536 workgroups; 2048 / 3072:
-// 0.706-0.716) against 0.650-0.653 for the 2-column k_postpre_lds<float>.  The quad lanes
-// need 221 VGPRs (2 waves per SIMD) where the 2-column fp32 pass fits 110 (4 waves per SIMD):
-// the occupancy it loses costs more than the halved per-lane row work saves.
-bool pp_q4() { return tuning_int("PGMG_PPQ", 0) != 0; }
-
-// k_postpre_q4's grid target (fp32): the same band height as the 2-column form's at
-// PGMG_PPQ_BLOCKS unset (half its workgroups: each covers twice the columns)
-static int ppq_target(int jc0, int jc1) { return tuning_int("PGMG_PPQ_BLOCKS", pp_target(jc0, jc1) / 2); }
-
-int postpre_blocks(int N, int jc0, int jc1, bool q4)
+int postpre_blocks(int N, int jc0, int jc1)
 {
     int t, gx, gy, r;
-    if (q4) fused_geometry(N, jc0, jc1, &t, &gx, &gy, &r, kQStride, ppq_target(jc0, jc1), kPPWaves);
-    else fused_geometry(N, jc0, jc1, &t, &gx, &gy, &r, kPPStride, pp_target(jc0, jc1), kPPWaves);
+    fused_geometry(N, jc0, jc1, &t, &gx, &gy, &r, kPPStride, pp_target(jc0, jc1), kPPWaves);
     return gx * gy;
-}
-
-// k_postpre_q4: each block loads quads of its 976-column window from column L0 (nvq of them
-// inside the row) and coarse quads from cc0 - 3 (nvc inside the coarse row)
-static int postpre_q4_spans(const PostPreArgsT<float> &a, int t, int gx, int r)
-{
-    using T = float;
-    const Span sp = band_rows(a.jc0, a.jc1, r, 6, 11, kPPR);
-    if (!sp.any) return PGMG_OK;
-    const int wpb = t / 64;
-    const int nq = (kQStride * wpb + 2 * kQMargin) / 4, ncq = kQLdsCoarse / 4 - 1;
-    long long c1 = -1, e0 = 0, e1 = -1;
-    bool first = true;
-    for (int bx = 0; bx < gx; ++bx) {
-        const int L0 = kQStride * wpb * bx + 1 - kQMargin;
-        const int nvq = std::max(0, std::min(nq, (a.N - 1 - L0) / 4 + 1));
-        if (nvq > 0) c1 = std::max(c1, (long long)L0 + 4 * nvq - 1);
-        const int cb0 = ((L0 - 1) >> 1) - kQCoarseShift;
-        const int nvc = std::max(0, std::min(ncq, (a.Nc - 1 - cb0) / 4 + 1));
-        if (nvc > 0) {
-            e0 = first ? cb0 : std::min(e0, (long long)cb0);
-            e1 = std::max(e1, (long long)cb0 + 4 * nvc - 1);
-            first = false;
-        }
-    }
-    const long long c0 = 1 - kQMargin;
-    if (c1 < c0) return PGMG_OK;
-    PGMG_SPAN(a.phi, a.P, sp.r0, sp.r1, c0, c1, "k_postpre_q4 phi");
-    if (a.gfx == nullptr) PGMG_SPAN(a.f, a.P, sp.r0, sp.r1, c0, c1, "k_postpre_q4 f");
-    if (e1 >= e0) PGMG_SPAN(a.ec, a.Pc, a.jc0 - 3, fdiv2(sp.r1 + 1), e0, e1, "k_postpre_q4 coarse correction");
-    const int olo = std::max(2 * a.jc0, a.row_lo), ohi = std::min(2 * a.jc1, a.row_hi);
-    PGMG_SPAN(a.x4, a.P, olo, ohi - 1, 1, a.N - 1, "k_postpre_q4 x4");
-    if (a.rc != nullptr) {
-        const int clo = std::max(a.jc0, std::max(1, a.rc_lo));
-        const int chi = std::min(a.jc1, std::min(a.N / 2, a.rc_hi));
-        PGMG_SPAN(a.rc, a.Pc, clo, chi - 1, 1, a.Nc - 2, "k_postpre_q4 rc");
-    }
-    return PGMG_OK;
 }
 
 // The cross-cycle finest-level pass.  OPT 2: non-temporal x4 stores (x4 is read again
@@ -2169,26 +1788,6 @@ static int postpre_q4_spans(const PostPreArgsT<float> &a, int t, int gx, int r)
 template <class T>
 int launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
 {
-    if constexpr (sizeof(T) == 4) {
-      if (pp_q4()) {   // fp32: four columns per lane (k_postpre_q4, opt-in)
-        int t, gx, gy, r;
-        fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, kQStride, ppq_target(a0.jc0, a0.jc1),
-                       kPPWaves);
-        if (const int e = postpre_q4_spans(a0, t, gx, r)) return e;
-        PostPreArgsT<T> a = a0;
-        a.rows_per_block = r;
-        const dim3 g(gx, gy), b(t);
-        const bool genf = a.gfx != nullptr;
-        if (a.partials3 != nullptr) {
-            if (genf) k_postpre_q4<true, true><<<g, b, 0, s>>>(a);
-            else k_postpre_q4<true, false><<<g, b, 0, s>>>(a);
-        } else {
-            if (genf) k_postpre_q4<false, true><<<g, b, 0, s>>>(a);
-            else k_postpre_q4<false, false><<<g, b, 0, s>>>(a);
-        }
-        return PGMG_OK;
-      }
-    }
     int t, gx, gy, r;
     fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, kPPStride, pp_target(a0.jc0, a0.jc1),
                    kPPWaves);
@@ -2197,16 +1796,28 @@ int launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
     a.rows_per_block = r;
     const dim3 g(gx, gy), b(t);
     const bool genf = a.gfx != nullptr;
-    if (a.partials3 != nullptr) {
-        if (genf) k_postpre_lds<T, true, true, 2><<<g, b, 0, s>>>(a);
-        else k_postpre_lds<T, true, false, 2><<<g, b, 0, s>>>(a);
+    if (a.x2 != nullptr) {   // the carry pass (one GPU: no third sum)
+        if (a.partials3 != nullptr) return PGMG_ERR_ARG;
+        if (a.fast && sizeof(T) == 8) {
+            if (genf) launchk(k_postpre_lds<T, false, true, 2 | 16 | 128>, g, b, s, a);
+            else launchk(k_postpre_lds<T, false, false, 2 | 16 | 128>, g, b, s, a);
+        } else if (genf) launchk(k_postpre_lds<T, false, true, 2 | 128>, g, b, s, a);
+        else launchk(k_postpre_lds<T, false, false, 2 | 128>, g, b, s, a);
+    } else if (a.partials3 != nullptr) {
+        if (genf) launchk(k_postpre_lds<T, true, true, 2>, g, b, s, a);
+        else launchk(k_postpre_lds<T, true, false, 2>, g, b, s, a);
     } else {
         if (a.fast && sizeof(T) == 8) {   // FAST mode (one GPU, fp64)
-            if (genf) k_postpre_lds<T, false, true, 2 | 16><<<g, b, 0, s>>>(a);
-            else k_postpre_lds<T, false, false, 2 | 16><<<g, b, 0, s>>>(a);
-        } else if (genf) k_postpre_lds<T, false, true, 2><<<g, b, 0, s>>>(a);
-        else k_postpre_lds<T, false, false, 2><<<g, b, 0, s>>>(a);
+            if (genf) launchk(k_postpre_lds<T, false, true, 2 | 16>, g, b, s, a);
+            else launchk(k_postpre_lds<T, false, false, 2 | 16>, g, b, s, a);
+        } else if (genf) launchk(k_postpre_lds<T, false, true, 2>, g, b, s, a);
+        else launchk(k_postpre_lds<T, false, false, 2>, g, b, s, a);
     }
+    // phi, f (unless regenerated), ec in; x4, rc (and the carry pass's x2) out
+    const double n = row_pts(std::max(2 * a.jc0, a.row_lo), std::min(2 * a.jc1, a.row_hi), a.N);
+    const double nc = row_pts(a.rc_lo, a.rc_hi, a.Nc);
+    g_last_launch.bytes = (8.0 * n * (2 + (genf ? 0 : 1) + (a.x2 != nullptr ? 1 : 0)) + 16.0 * nc) *
+                          sizeof(T) / 8.0;
     return PGMG_OK;
 }
 

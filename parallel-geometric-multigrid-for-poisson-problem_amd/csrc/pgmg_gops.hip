@@ -174,13 +174,7 @@ __global__ __launch_bounds__(kBlock) void k_op_sweep(const double *__restrict__ 
     }
 }
 
-// The same sweep with overlapping wave tiles: a wave loads 128 columns (lane t: the pair
-// (124 w - 1 + 2t, +1)) and owns the 124 of lanes 1..62, so every neighbour column comes from
-// an adjacent lane by DPP and no lane issues a halo load of its own (the edge-lane halo loads
-// above double the wave's load instructions; the 4 overlapping columns per wave are L2 hits).
-// Lanes whose pair leaves the row (the grid's first and last columns) load element-wise.
-constexpr int kOvStride = 124;
-
+// Lane t's column pair (c, c+1) of a row; a pair that leaves the row loads element-wise.
 __device__ __forceinline__ double2 ld_pair(const double *row, int c, int W)
 {
     if (c >= 0 && c + 1 <= W - 1) return ldvu<double>(row + c);
@@ -198,176 +192,11 @@ __device__ __forceinline__ void st_owned(double *q, double2 o, bool ox, bool oy)
     else if (oy) q[1] = o.y;
 }
 
-template <int U, bool CHECK, bool SEED, bool NT>
-__global__ __launch_bounds__(kBlock) void k_op_sweep_ov(const double *__restrict__ X,
-                                                        const double *__restrict__ F,
-                                                        double *__restrict__ O, double *partials,
-                                                        const unsigned *skip, unsigned *reset,
-                                                        unsigned long long *stats, double hh,
-                                                        double ih, int H, int W, int rpb)
-{
-    __shared__ double red[kBlock / 64];
-    if (skip != nullptr && *skip != 0u) return;
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
-        if (reset != nullptr) *reset = 0u;
-        if (stats != nullptr) atomicAdd(&stats[0], 1ull);
-    }
-    const int lane = threadIdx.x & 63;
-    const int wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const int c = kOvStride * wave - 1 + 2 * lane;
-    const bool mid = lane >= 1 && lane <= 62;
-    const bool ox = mid && c >= 1 && c <= W - 2;
-    const bool oy = mid && c + 1 >= 1 && c + 1 <= W - 2;
-    // SEED: the lanes holding a boundary column copy it (rows jb .. je-1)
-    const bool bx = c == 0 || c == W - 1, by = c + 1 == 0 || c + 1 == W - 1;
-    const int jb = 1 + blockIdx.y * rpb;
-    const int je = min(jb + rpb, H - 1);
-    const long long Wl = W;
-    double acc = 0.0;
-    double2 w0 = ld_pair(X + (long long)(jb - 1) * Wl, c, W);
-    double2 w1 = ld_pair(X + (long long)jb * Wl, c, W);
-    if (SEED && jb == 1) st_owned<false>(O + c, w0, ox, oy);
-    for (int j = jb; j < je; j += U) {
-        double2 xn[U], fv[U];
-        #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const long long r = min(j + u, je - 1);
-            fv[u] = ld_pair(F + r * Wl, c, W);
-            xn[u] = ld_pair(X + (r + 1) * Wl, c, W);
-        }
-        #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int r = j + u;
-            const double2 up = (u == 0) ? w0 : (u == 1 ? w1 : xn[u - 2]);
-            const double2 ce = (u == 0) ? w1 : xn[u - 1];
-            const double2 dn = xn[u];
-            const double left = dpp_shr(ce.y);
-            const double right = dpp_shl(ce.x);
-            double2 o;
-            o.x = 0.25 * ((hh * fv[u].x) + left + ce.y + up.x + dn.x);
-            o.y = 0.25 * ((hh * fv[u].y) + ce.x + right + up.y + dn.y);
-            const bool live = r < je;
-            if (CHECK && live) {
-                const double r0 = fv[u].x - ih * (4 * ce.x - left - ce.y - up.x - dn.x);
-                const double r1 = fv[u].y - ih * (4 * ce.y - ce.x - right - up.y - dn.y);
-                if (ox) acc += r0 * r0;
-                if (oy) acc += r1 * r1;
-            }
-            if (live) {
-                double *q = O + (long long)r * Wl + c;
-                st_owned<NT>(q, o, ox, oy);
-                if (SEED) {
-                    if (bx) q[0] = ce.x;
-                    if (by) q[1] = ce.y;
-                }
-            }
-        }
-        w0 = xn[U - 2];
-        w1 = xn[U - 1];
-    }
-    if (SEED && je == H - 1) st_owned<false>(O + (long long)(H - 1) * Wl + c, w1, ox, oy);
-    if (CHECK) {
-        const double s = gblock_sum<kBlock>(acc, red);
-        if (threadIdx.x == 0) partials[blockIdx.y * gridDim.x + blockIdx.x] = s;
-    }
-}
-
-static OpGeom op_geom_ov(int W, int rows, int U, int target)
-{
-    // columns 1 .. W-2 over waves of 124, kBlock / 64 waves per workgroup
-    const int waves = (W - 2 + kOvStride - 1) / kOvStride;
-    return op_geom(waves * 64, rows, U, target);
-}
-
 // ---------------------------------------------------------------------------
-// Two Jacobi sweeps in one pass, for a smoother call without early-exit checks (the
-// reference GPU op ComputeJacobi decides nothing between its v+1 sweeps,
-// Parallel_Method.cu:144-160): x and f are read once for two sweeps -- 24 B per point per
-// pass instead of 48 (temporal blocking; SURVEY §8(d) counts 24 B per sweep).  Rows march
-// down the band with the first sweep one row behind the loads and the second two rows
-// behind, in registers; wave tiles load 128 columns and own the 120 of lanes 2..61 (two
-// stencil levels shrink the valid columns by one per side each).  Every value is the
-// single sweep's: J(x) on interior points, x's boundary passed through (the reference never
-// writes it).
+// Geometry of the paired sweep (k_op_sweep2_ip below): wave tiles load 128 columns and own
+// the 120 of lanes 2..61 (two stencil levels shrink the valid columns by one per side each).
 // ---------------------------------------------------------------------------
 constexpr int kOv2Stride = 120;
-
-template <int U, bool SEED, bool NT>
-__global__ __launch_bounds__(kBlock) void k_op_sweep2(const double *__restrict__ X,
-                                                      const double *__restrict__ F,
-                                                      double *__restrict__ O,
-                                                      unsigned long long *stats, double hh, int H,
-                                                      int W, int rpb)
-{
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && stats != nullptr)
-        atomicAdd(&stats[0], 2ull);
-    const int lane = threadIdx.x & 63;
-    const int wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const int c = kOv2Stride * wave - 3 + 2 * lane;
-    const bool inx = c >= 1 && c <= W - 2, iny = c + 1 >= 1 && c + 1 <= W - 2;
-    const bool mid = lane >= 2 && lane <= 61;
-    const bool ox = mid && inx, oy = mid && iny;
-    // SEED: lanes holding a boundary column write it (the passthrough value)
-    const bool bx = SEED && (c == 0 || c == W - 1), by = SEED && (c + 1 == 0 || c + 1 == W - 1);
-    const int jb = 1 + blockIdx.y * rpb;
-    const int je = min(jb + rpb, H - 1);   // x2 rows [jb, je)
-    const long long Wl = W;
-    auto ldrow = [&](const double *A, int r) {
-        return (r >= 0 && r <= H - 1) ? ld_pair(A + (long long)r * Wl, c, W) : make_double2(0.0, 0.0);
-    };
-    // one sweep of a row with x's boundary columns passed through
-    auto jrow = [&](double2 up, double2 ce, double2 dn, double2 f) {
-        const double l = dpp_shr(ce.y);
-        const double r = dpp_shl(ce.x);
-        double2 o;
-        o.x = inx ? 0.25 * ((hh * f.x) + l + ce.y + up.x + dn.x) : ce.x;
-        o.y = iny ? 0.25 * ((hh * f.y) + ce.x + r + up.y + dn.y) : ce.y;
-        return o;
-    };
-    // windows at "new row i": x rows i-2, i-1; f rows i-2, i-1; x1 rows i-3, i-2
-    double2 xa = ldrow(X, jb - 2), xb = ldrow(X, jb - 1);
-    double2 fa = make_double2(0.0, 0.0), fb = ldrow(F, jb - 1);
-    double2 ya = make_double2(0.0, 0.0), yb = make_double2(0.0, 0.0);
-    if (SEED && jb == 1) st_owned<false>(O + c, xb, ox || bx, oy || by);   // row 0
-    const int iend = je + 2;   // new rows i = jb .. je+1
-    for (int i = jb; i < iend; i += U) {
-        double2 xn[U], fn[U];
-        #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int r = min(i + u, iend - 1);
-            xn[u] = ldrow(X, r);
-            fn[u] = ldrow(F, r);
-        }
-        #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int ii = i + u;
-            if (ii >= iend) break;
-            // x1 on row ii-1 (a boundary row passes x through)
-            const int r1 = ii - 1;
-            double2 y1 = jrow(xa, xb, xn[u], fb);
-            if (r1 < 1 || r1 > H - 2) y1 = xb;
-            // x2 on row ii-2
-            const int r2 = ii - 2;
-            if (r2 >= jb) {
-                const double2 z = jrow(ya, yb, y1, fa);
-                double *q = O + (long long)r2 * Wl + c;
-                st_owned<NT>(q, z, ox, oy);
-                if (SEED) {
-                    if (bx) q[0] = z.x;
-                    if (by) q[1] = z.y;
-                }
-            }
-            xa = xb;
-            xb = xn[u];
-            fa = fb;
-            fb = fn[u];
-            ya = yb;
-            yb = y1;
-        }
-    }
-    // row H-1: after the last step xa holds x row je
-    if (SEED && je == H - 1) st_owned<false>(O + (long long)(H - 1) * Wl + c, xa, ox || bx, oy || by);
-}
 
 static OpGeom sweep2_geom(int H, int W, int U, int target)
 {
@@ -375,49 +204,16 @@ static OpGeom sweep2_geom(int H, int W, int U, int target)
     return op_geom(waves * 64, H - 2, U, target);
 }
 
-void launch_g_sweep2(const double *xin, const double *f, double *xout, unsigned long long *stats,
-                     double hh, int H, int W, bool seed, hipStream_t s)
-{
-    const int U = tuning_int("PGMG_OP2_U", 4) == 8 ? 8 : 4;
-    const OpGeom g = sweep2_geom(H, W, U, tuning_int("PGMG_OP2_BLOCKS", 2048));
-    const bool nt = tuning_int("PGMG_OP_NT", 1) != 0;
-    const dim3 grid(g.gx, g.gy);
-#define PGMG_K2(UU, SD, NTV) k_op_sweep2<UU, SD, NTV><<<grid, kBlock, 0, s>>>(xin, f, xout, stats, hh, H, W, g.rpb)
-    if (U == 8) {
-        if (seed) { if (nt) PGMG_K2(8, true, true); else PGMG_K2(8, true, false); }
-        else { if (nt) PGMG_K2(8, false, true); else PGMG_K2(8, false, false); }
-    } else {
-        if (seed) { if (nt) PGMG_K2(4, true, true); else PGMG_K2(4, true, false); }
-        else { if (nt) PGMG_K2(4, false, true); else PGMG_K2(4, false, false); }
-    }
-#undef PGMG_K2
-}
-
-bool g_fuse2() { return tuning_int("PGMG_OP_FUSE2", 1) != 0; }
-bool g_inplace() { return tuning_int("PGMG_OP_INPLACE", 1) != 0; }
-
 constexpr int kOpTarget = 4096;   // workgroups per op launch (16 per CU)
 
 // Measured at N = 16385 (scripts/op_ab.py, profiles/r04_ops/): one round of resident
-// workgroups (k_op_sweep<8>: 120 VGPRs, 4 waves per SIMD = 1024 workgroups of 4 waves on 256
-// CUs), 8 rows of loads in flight and non-temporal stores: 1.339 ms per sweep (0.60 of 8 TB/s)
-// against 1.35-1.47 for 2048-8192 workgroups, 4 rows, default stores or the overlapping
-// tiles (k_op_sweep_ov, kept as PGMG_OP_OV=1 of the measurement build).  r04 (op_ab.py --rows,
-// profiles/r04_ops/op_rows.jsonl): 16 rows in flight (214 VGPRs: 2 waves per SIMD, the 1024
-// workgroups in two rounds) 1.390-1.393 ms against 1.403-1.405 for 8 rows on the same box,
-// 16 rows at one round of 512 workgroups 1.45, 4 rows at 1792 1.46 -- 16 is the default
-static bool op_ov() { return tuning_int("PGMG_OP_OV", 0) != 0; }
-static int op_u()
-{
-    const int u = tuning_int("PGMG_OP_U", 16);
-    return u == 4 ? 4 : (u == 8 ? 8 : 16);
-}
-static int op_target() { return tuning_int("PGMG_OP_BLOCKS", 1024); }
-
+// workgroups (1024 of 4 waves on 256 CUs) and non-temporal stores beat 2048-8192 workgroups,
+// 4 rows, default stores or overlapping wave tiles (r04, kept in git history); r04 (op_ab.py
+// --rows, profiles/r04_ops/op_rows.jsonl): 16 rows in flight (214 VGPRs: 2 waves per SIMD, the
+// 1024 workgroups in two rounds) 1.390-1.393 ms against 1.403-1.405 for 8 rows on the same box
 static OpGeom sweep_geom(int H, int W)
 {
-    return op_ov() ? op_geom_ov(W, H - 2, op_u(), op_target())
-                   : op_geom((W - 1) / 2, H - 2, op_u(), op_target());
+    return op_geom((W - 1) / 2, H - 2, 16, tuning_int("PGMG_OP_BLOCKS", 1024));
 }
 
 int g_blocks(int H, int W)
@@ -426,42 +222,19 @@ int g_blocks(int H, int W)
     return g.gx * g.gy;
 }
 
-template <int U, bool CHECK, bool SEED>
-static void sweep_u(const OpGeom &g, bool ov, bool nt, const double *xin, const double *f,
-                    double *xout, double *partials, const unsigned *skip, unsigned *reset,
-                    unsigned long long *stats, double hh, double ih, int H, int W, hipStream_t s)
-{
-    const dim3 grid(g.gx, g.gy);
-#define PGMG_K(KN, NTV) KN<U, CHECK, SEED, NTV><<<grid, kBlock, 0, s>>>(xin, f, xout, partials, skip, reset, stats, hh, ih, H, W, g.rpb)
-    if (ov) {
-        if (nt) PGMG_K(k_op_sweep_ov, true);
-        else PGMG_K(k_op_sweep_ov, false);
-    } else {
-        if (nt) PGMG_K(k_op_sweep, true);
-        else PGMG_K(k_op_sweep, false);
-    }
-#undef PGMG_K
-}
-
 void launch_g_sweep(const double *xin, const double *f, double *xout, double *partials,
                     const unsigned *skip, unsigned *reset, unsigned long long *stats, double hh,
                     double inv_hh, int H, int W, bool seed, hipStream_t s)
 {
     const OpGeom g = sweep_geom(H, W);
-    const bool ov = op_ov();
-    const bool nt = tuning_int("PGMG_OP_NT", 1) != 0;
+    const dim3 grid(g.gx, g.gy);
     const bool chk = partials != nullptr;
-#define PGMG_SW(UU)                                                                                \
-    do {                                                                                           \
-        if (chk && seed) sweep_u<UU, true, true>(g, ov, nt, xin, f, xout, partials, skip, reset, stats, hh, inv_hh, H, W, s); \
-        else if (chk) sweep_u<UU, true, false>(g, ov, nt, xin, f, xout, partials, skip, reset, stats, hh, inv_hh, H, W, s); \
-        else if (seed) sweep_u<UU, false, true>(g, ov, nt, xin, f, xout, partials, skip, reset, stats, hh, inv_hh, H, W, s); \
-        else sweep_u<UU, false, false>(g, ov, nt, xin, f, xout, partials, skip, reset, stats, hh, inv_hh, H, W, s); \
-    } while (0)
-    if (op_u() == 8) PGMG_SW(8);
-    else if (op_u() == 16) PGMG_SW(16);
-    else PGMG_SW(4);
-#undef PGMG_SW
+#define PGMG_K(CH, SD) k_op_sweep<16, CH, SD, true><<<grid, kBlock, 0, s>>>(xin, f, xout, partials, skip, reset, stats, hh, inv_hh, H, W, g.rpb)
+    if (chk && seed) PGMG_K(true, true);
+    else if (chk) PGMG_K(true, false);
+    else if (seed) PGMG_K(false, true);
+    else PGMG_K(false, false);
+#undef PGMG_K
 }
 
 // ---------------------------------------------------------------------------
@@ -506,48 +279,6 @@ void launch_g_fixup(const double *partials, int np, double eps, const unsigned *
 {
     k_g_fixup<<<dim3(256), dim3(kBlock), 0, s>>>(partials, np, eps, done_prev, done_next, src,
                                                   dst, stats, H, W);
-}
-
-// interior copy dst := src (rows 1 .. H-2, columns 1 .. W-2): the result of an odd number of
-// sweeps from the ping-pong buffer back into the caller's x (its boundary is already x's)
-template <int U>
-__global__ __launch_bounds__(kBlock) void k_op_copy_interior(const double *__restrict__ src,
-                                                             double *__restrict__ dst, int H,
-                                                             int W, int rpb)
-{
-    const int npairs = (W - 1) >> 1;
-    const int t = blockIdx.x * kBlock + threadIdx.x;
-    if (t >= npairs) return;
-    const int c = 1 + 2 * t;
-    const bool second = c + 1 <= W - 2;
-    const int jb = 1 + blockIdx.y * rpb;
-    const int je = min(jb + rpb, H - 1);
-    const long long Wl = W;
-    for (int j = jb; j < je; j += U) {
-        double2 v[U];
-        #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = ldvu<double>(src + (long long)min(j + u, je - 1) * Wl + c);
-        #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (j + u >= je) break;
-            double *q = dst + (long long)(j + u) * Wl + c;
-            if (second) st2<true>(q, v[u]);
-            else st_nt1(q, v[u].x);
-        }
-    }
-}
-
-void launch_g_copy_interior(const double *src, double *dst, int H, int W, hipStream_t s)
-{
-    // rows of loads in flight: 8 (PGMG_OPC_U = 16 in the measurement build: the same within
-    // noise, profiles/r04_ops/op_ru.jsonl)
-    if (tuning_int("PGMG_OPC_U", 8) == 16) {
-        const OpGeom g = op_geom((W - 1) / 2, H - 2, 16, tuning_int("PGMG_OPC_BLOCKS", 2048));
-        k_op_copy_interior<16><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(src, dst, H, W, g.rpb);
-        return;
-    }
-    const OpGeom g = op_geom((W - 1) / 2, H - 2, 8, tuning_int("PGMG_OPC_BLOCKS", 2048));
-    k_op_copy_interior<8><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(src, dst, H, W, g.rpb);
 }
 
 // ---------------------------------------------------------------------------
@@ -804,62 +535,39 @@ __global__ __launch_bounds__(kBlock) void k_op_defer_scatter(double *X, const do
 }
 
 // The single in-place sweep: 512-thread workgroups (8 waves; half the column-block boundaries
-// to defer of 256) and 512 of them (one per CU at 217 VGPRs).  Measured at 16385 (r05,
-// scripts/op_ip_ab.py --nth, profiles/r05_ops/op_ip_nth.jsonl, 3 interleaved rounds): one-sweep
-// call 1.320-1.329 ms against 1.382-1.398 with 256 threads x 1024 (1.333-1.336 at 512 x 1024,
-// 1.359-1.364 with 8 rows in flight); PGMG_OPIP_NTH=256 in the measurement build for the form
-// before.
-static int ip_nth() { return tuning_int("PGMG_OPIP_NTH", 512) == 256 ? 256 : 512; }
-static OpGeom sweep_ip_geom(int H, int W, int U, int nth = 512)
+// to defer of 256) and 512 of them (one per CU at 217 VGPRs), 16 rows in flight, non-temporal
+// stores, tile edges deferred per column block.  Measured at 16385 (r05, scripts/op_ip_ab.py
+// --nth, profiles/r05_ops/op_ip_nth.jsonl, 3 interleaved rounds): one-sweep call 1.320-1.329 ms
+// against 1.382-1.398 with 256 threads x 1024 (1.333-1.336 at 512 x 1024, 1.359-1.364 with 8
+// rows in flight); the forms measured against it are in git history (r05).
+constexpr int kIpNth = 512, kIpRows = 16;
+static OpGeom sweep_ip_geom(int H, int W)
 {
     // op_geom counts columns in workgroups of kBlock lanes: scale the pair count
-    OpGeom g = op_geom(((W - 1) / 2 + nth / kBlock - 1) / (nth / kBlock), H - 2, U,
-                       tuning_int("PGMG_OPIP_BLOCKS", nth == 512 ? 512 : 1024));
-    g.gx = ((W - 1) / 2 + nth - 1) / nth;
+    OpGeom g = op_geom(((W - 1) / 2 + kIpNth / kBlock - 1) / (kIpNth / kBlock), H - 2, kIpRows,
+                       tuning_int("PGMG_OPIP_BLOCKS", 512));
+    g.gx = ((W - 1) / 2 + kIpNth - 1) / kIpNth;
     return g;
 }
-// the paired pass keeps 256-thread workgroups: 512 measured slower (r05, op_ip_nth.jsonl: two
-// sweeps 1.44-1.48 ms at 512 / 1024 workgroups, 1.41-1.42 at 2048, against 1.377-1.389)
-static int ip2_nth() { return tuning_int("PGMG_OP2IP_NTH", 256) == 512 ? 512 : 256; }
-static OpGeom sweep2_ip_geom(int H, int W, int U, int nth = 256)
+// the paired pass: 256-thread workgroups, 8 rows in flight (512 threads measured slower, r05,
+// op_ip_nth.jsonl: two sweeps 1.44-1.48 ms at 512 / 1024 workgroups, 1.41-1.42 at 2048,
+// against 1.377-1.389)
+constexpr int kIp2Rows = 8;
+static OpGeom sweep2_ip_geom(int H, int W)
 {
-    OpGeom g = sweep2_geom(H, W, U, tuning_int("PGMG_OP2IP_BLOCKS", 1024));
-    if (nth != kBlock) {   // the same bands' worth of workgroups, each nth / 64 waves wide
-        const int waves = (W - 2 + kOv2Stride - 1) / kOv2Stride;
-        g = op_geom(((waves * 64) + nth / kBlock - 1) / (nth / kBlock), H - 2, U,
-                    tuning_int("PGMG_OP2IP_BLOCKS", 1024));
-        g.gx = (waves * 64 + nth - 1) / nth;
-    }
-    return g;
+    return sweep2_geom(H, W, kIp2Rows, tuning_int("PGMG_OP2IP_BLOCKS", 1024));
 }
 
-// side buffer elements for either in-place pass at any of its row-step choices
-// boundaries between deferral units along a row: column blocks (BAR) or waves
-static int ip_bounds(const OpGeom &g, int W, bool pair, bool bar)
-{
-    if (bar) return g.gx > 1 ? g.gx - 1 : 0;
-    const int nw = pair ? (W - 2 + kOv2Stride - 1) / kOv2Stride : ((W - 1) / 2 + 63) / 64;
-    return nw > 1 ? nw - 1 : 0;
-}
-static bool ip_bar() { return tuning_int("PGMG_OPIP_BAR", 1) != 0; }
-static bool ip2_bar() { return tuning_int("PGMG_OP2IP_BAR", 1) != 0; }
+// boundaries between deferral units along a row: the column blocks
+static int ip_bounds(const OpGeom &g) { return g.gx > 1 ? g.gx - 1 : 0; }
 
+// side buffer elements of either in-place pass
 size_t g_defer_elems(int H, int W)
 {
-    size_t m = 0;
-    for (int U : {8, 16})
-        for (int nth : {256, 512}) {
-            const OpGeom a = sweep_ip_geom(H, W, U, nth);
-            for (bool bar : {false, true})
-                m = std::max(m, (size_t)a.gy * 2 * W + (size_t)ip_bounds(a, W, false, bar) * H * 2);
-        }
-    for (int U : {4, 8})
-        for (int nth : {256, 512}) {
-            const OpGeom b = sweep2_ip_geom(H, W, U, nth);
-            for (bool bar : {false, true})
-                m = std::max(m, (size_t)b.gy * 4 * W + (size_t)ip_bounds(b, W, true, bar) * H * 4);
-        }
-    return m + 64;
+    const OpGeom a = sweep_ip_geom(H, W), b = sweep2_ip_geom(H, W);
+    const size_t m1 = (size_t)a.gy * 2 * W + (size_t)ip_bounds(a) * H * 2;
+    const size_t m2 = (size_t)b.gy * 4 * W + (size_t)ip_bounds(b) * H * 4;
+    return std::max(m1, m2) + 64;
 }
 
 static void defer_scatter(double *x, const double *SR, const double *SC, const OpGeom &g, int R,
@@ -872,80 +580,36 @@ static void defer_scatter(double *x, const double *SR, const double *SC, const O
     // boundary columns' scattered 16-byte writes (one row each) go faster with fewer writers in
     // flight; writing whole 64-byte segments (merged with the pass's in-place values) instead:
     // 63-153 / 99-208 us, not kept
-    const int per = tuning_int("PGMG_SCAT_PER", 16);
+    constexpr int per = 16;
     int bx = (std::max(W, H) + per * kBlock - 1) / (per * kBlock);
     if (bx < 1) bx = 1;
-    // measurement build only: PGMG_SCAT_PART = 1 rows only, 2 columns only (wrong results)
-    const int part = tuning_int("PGMG_SCAT_PART", 0);
-    if (part == 1) nbound = 0;
-    k_op_defer_scatter<<<dim3(bx, part == 2 ? nbound : nslot + nbound), kBlock, 0, s>>>(
-        x, SR, SC, H, W, g.rpb, part == 2 ? 0 : g.gy, R, K, ca, cb);
+    k_op_defer_scatter<<<dim3(bx, nslot + nbound), kBlock, 0, s>>>(x, SR, SC, H, W, g.rpb, g.gy, R,
+                                                                   K, ca, cb);
 }
 
 void launch_g_sweep_ip(double *x, const double *f, double *side, unsigned *reset,
                        unsigned long long *stats, double hh, int H, int W, hipStream_t s)
 {
-    const int U = tuning_int("PGMG_OPIP_U", 16) == 8 ? 8 : 16;
-    const bool nt = tuning_int("PGMG_OP_NT", 1) != 0;
-    const bool bar = ip_bar();
-    const int nth = (bar && nt) ? ip_nth() : 256;   // the other forms: 256-thread workgroups
-    const OpGeom g = sweep_ip_geom(H, W, U, nth);
+    const OpGeom g = sweep_ip_geom(H, W);
     double *SR = side, *SC = side + (size_t)g.gy * 2 * W;
-    const dim3 grid(g.gx, g.gy);
-    if (nth == 512 && bar && nt) {   // the default
-        if (U == 8) k_op_sweep_ip<8, true, true, 512><<<grid, 512, 0, s>>>(x, f, SR, SC, reset, stats, hh, H, W, g.rpb);
-        else k_op_sweep_ip<16, true, true, 512><<<grid, 512, 0, s>>>(x, f, SR, SC, reset, stats, hh, H, W, g.rpb);
-        defer_scatter(x, SR, SC, g, 1, ip_bounds(g, W, false, true), 2, 1024, 1024, H, W, s);
-        return;
-    }
-    // (measurement build: 256-thread workgroups, default-policy stores or wave-boundary deferral)
-#define PGMG_KI(UU, NTV, BR) k_op_sweep_ip<UU, NTV, BR><<<grid, kBlock, 0, s>>>(x, f, SR, SC, reset, stats, hh, H, W, g.rpb)
-    if (bar) {
-        if (U == 8) { if (nt) PGMG_KI(8, true, true); else PGMG_KI(8, false, true); }
-        else { if (nt) PGMG_KI(16, true, true); else PGMG_KI(16, false, true); }
-    } else {
-        if (U == 8) { if (nt) PGMG_KI(8, true, false); else PGMG_KI(8, false, false); }
-        else { if (nt) PGMG_KI(16, true, false); else PGMG_KI(16, false, false); }
-    }
-#undef PGMG_KI
-    // boundary e: columns 2 kBlock (e+1) and the next (waves: 128 (e+1) and the next)
-    const int cs = bar ? 2 * kBlock : 128;
-    defer_scatter(x, SR, SC, g, 1, ip_bounds(g, W, false, bar), 2, cs, cs, H, W, s);
+    k_op_sweep_ip<kIpRows, true, true, kIpNth><<<dim3(g.gx, g.gy), kIpNth, 0, s>>>(
+        x, f, SR, SC, reset, stats, hh, H, W, g.rpb);
+    // boundary e: columns 2 kIpNth (e+1) and the next
+    defer_scatter(x, SR, SC, g, 1, ip_bounds(g), 2, 2 * kIpNth, 2 * kIpNth, H, W, s);
 }
 
 void launch_g_sweep2_ip(double *x, const double *f, double *side, unsigned long long *stats,
                         double hh, int H, int W, hipStream_t s)
 {
-    const int U = tuning_int("PGMG_OP2IP_U", 8) == 4 ? 4 : 8;
-    const bool nt = tuning_int("PGMG_OP_NT", 1) != 0;
-    const bool bar = ip2_bar();
-    const int nth = (bar && nt && U == 8) ? ip2_nth() : 256;
-    const OpGeom g = sweep2_ip_geom(H, W, U, nth);
+    const OpGeom g = sweep2_ip_geom(H, W);
     double *SR = side, *SC = side + (size_t)g.gy * 4 * W;
-    const dim3 grid(g.gx, g.gy);
-    if (nth == 512) {   // measurement build (PGMG_OP2IP_NTH=512)
-        k_op_sweep2_ip<8, true, true, 512><<<grid, 512, 0, s>>>(x, f, SR, SC, stats, hh, H, W, g.rpb);
-        defer_scatter(x, SR, SC, g, 2, ip_bounds(g, W, true, true), 4, kOv2Stride * 8,
-                      kOv2Stride * 7 + 119, H, W, s);
-        return;
-    }
-#define PGMG_KI(UU, NTV, BR) k_op_sweep2_ip<UU, NTV, BR><<<grid, kBlock, 0, s>>>(x, f, SR, SC, stats, hh, H, W, g.rpb)
-    if (bar) {
-        if (U == 4) { if (nt) PGMG_KI(4, true, true); else PGMG_KI(4, false, true); }
-        else { if (nt) PGMG_KI(8, true, true); else PGMG_KI(8, false, true); }
-    } else {
-        if (U == 4) { if (nt) PGMG_KI(4, true, false); else PGMG_KI(4, false, false); }
-        else { if (nt) PGMG_KI(8, true, false); else PGMG_KI(8, false, false); }
-    }
-#undef PGMG_KI
-    // boundary e: block e's last wave w = kWaves (e+1) - 1 (waves: w = e), lane 61 ->
-    // columns kOv2Stride w + 119 ...; 4 columns
+    k_op_sweep2_ip<kIp2Rows, true, true><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(x, f, SR, SC, stats, hh,
+                                                                             H, W, g.rpb);
+    // boundary e: block e's last wave w = kWaves (e+1) - 1, lane 61 -> columns kOv2Stride w +
+    // 119 ...; 4 columns
     constexpr int kWaves = kBlock / 64;
-    if (bar)
-        defer_scatter(x, SR, SC, g, 2, ip_bounds(g, W, true, true), 4, kOv2Stride * kWaves,
-                      kOv2Stride * (kWaves - 1) + 119, H, W, s);
-    else
-        defer_scatter(x, SR, SC, g, 2, ip_bounds(g, W, true, false), 4, kOv2Stride, 119, H, W, s);
+    defer_scatter(x, SR, SC, g, 2, ip_bounds(g), 4, kOv2Stride * kWaves,
+                  kOv2Stride * (kWaves - 1) + 119, H, W, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -1013,16 +677,11 @@ void launch_g_residual(double *r, const double *x, const double *f, double inv_h
     // the sweep's pattern (2 reads, 1 write): its geometry (1024 workgroups)
     // 16 rows in flight, as the sweep (r04, scripts/op_ru_ab.py, profiles/r04_ops/op_ru.jsonl:
     // 1.344-1.351 ms against 1.360-1.362 for 8 rows, 3 interleaved rounds; 2048 workgroups
-    // 1.362-1.382); PGMG_OPR_U = 8 in the measurement build for the old form
+    // 1.362-1.382)
     // (r05: 512-thread workgroups x 512 / 1024 measured the same or slower, 1.357-1.378 ms
     // against 1.358-1.363; profiles/r05_ops/op_misc_ab.jsonl)
-    if (tuning_int("PGMG_OPR_U", 16) == 16) {
-        const OpGeom g = op_geom((W - 1) / 2, H - 2, 16, tuning_int("PGMG_OPR_BLOCKS", 1024));
-        k_op_residual<16><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(r, x, f, inv_hh, H, W, g.rpb);
-        return;
-    }
-    const OpGeom g = op_geom((W - 1) / 2, H - 2, 8, tuning_int("PGMG_OPR_BLOCKS", 1024));
-    k_op_residual<8><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(r, x, f, inv_hh, H, W, g.rpb);
+    const OpGeom g = op_geom((W - 1) / 2, H - 2, 16, tuning_int("PGMG_OPR_BLOCKS", 1024));
+    k_op_residual<16><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(r, x, f, inv_hh, H, W, g.rpb);
 }
 
 // ---------------------------------------------------------------------------
@@ -1089,12 +748,7 @@ void launch_g_restrict(const double *fine, double *coarse, int Nf, int Nc, hipSt
 {
     // 8 coarse rows of loads in flight (r04, scripts/op_ru_ab.py --restrict-prolong,
     // profiles/r04_ops/op_rp.jsonl: 0.561-0.566 ms against 0.573-0.577 for 4, 3 interleaved
-    // rounds; PGMG_OPRS_U = 4 in the measurement build for the old form)
-    if (tuning_int("PGMG_OPRS_U", 8) == 4) {
-        const OpGeom g4 = op_geom(Nc - 2, Nc - 2, 4, tuning_int("PGMG_OPRS_BLOCKS", kOpTarget));
-        k_op_restrict<4><<<dim3(g4.gx, g4.gy), kBlock, 0, s>>>(fine, coarse, Nf, Nc, g4.rpb);
-        return;
-    }
+    // rounds)
     const OpGeom g = op_geom(Nc - 2, Nc - 2, 8, tuning_int("PGMG_OPRS_BLOCKS", kOpTarget));
     k_op_restrict<8><<<dim3(g.gx, g.gy), kBlock, 0, s>>>(fine, coarse, Nf, Nc, g.rpb);
 }

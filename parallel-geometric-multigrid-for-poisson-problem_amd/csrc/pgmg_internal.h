@@ -30,6 +30,25 @@ int tuning_int(const char *name, int dflt);
 inline int tuning_int(const char *, int dflt) { return dflt; }
 #endif
 
+// The last launch of a finest-pass launcher (launch_pre / post / post_r2 / postpre / sweep) on
+// this thread: its kernel's host stub and its algorithmic bytes (the pgmg_fine_pass_bytes
+// model applied to what that launch reads and writes).  The timed passes record it per launch
+// (timed_end), so bench.py names and charges the kernel that actually ran
+// (pgmg_fine_pass_info) instead of deriving both from its own flags.
+struct LaunchNote {
+    const void *kernel = nullptr;
+    double bytes = 0.0;
+};
+extern thread_local LaunchNote g_last_launch;
+template <class... P, class... A>
+inline void launchk(void (*k)(P...), dim3 g, dim3 b, hipStream_t s, A &&...args)
+{
+    k<<<g, b, 0, s>>>(static_cast<P>(args)...);
+    g_last_launch.kernel = reinterpret_cast<const void *>(k);
+}
+// fine points of rows [r0, r1) of an N-point level, times an element size (algorithmic bytes)
+inline double row_pts(int r0, int r1, int N) { return r1 > r0 ? (double)(r1 - r0) * (N - 2) : 0.0; }
+
 // The smoother's early exit is sqrt(s) < eps for s = sum of r^2 (Smoother.hpp:77-80).
 // sqrt is correctly rounded and monotonic, so for s >= 0 (and NaN) the test equals s < T
 // with T = the smallest double whose square root is >= eps: the latency-bound kernels test
@@ -229,11 +248,6 @@ void launch_g_sweep(const double *xin, const double *f, double *xout, double *pa
                     double inv_hh, int H, int W, bool seed, hipStream_t s);
 int g_blocks(int H, int W);
 constexpr int kOpPartialsCap = 65536;   // partial sums per op scratch set (>= g_blocks)
-void launch_g_copy_interior(const double *src, double *dst, int H, int W, hipStream_t s);
-// two sweeps without a check in one pass (stats[0] += 2); seed as launch_g_sweep
-void launch_g_sweep2(const double *xin, const double *f, double *xout, unsigned long long *stats,
-                     double hh, int H, int W, bool seed, hipStream_t s);
-bool g_fuse2();   // pgmg_jacobi without checks runs its sweeps in pairs (default)
 // in-place sweeps on the caller's x (r05): one sweep / two sweeps per pass, each followed by
 // the scatter of its deferred tile-edge outputs; `side` holds g_defer_elems(H, W) doubles
 size_t g_defer_elems(int H, int W);
@@ -241,7 +255,6 @@ void launch_g_sweep_ip(double *x, const double *f, double *side, unsigned *reset
                        unsigned long long *stats, double hh, int H, int W, hipStream_t s);
 void launch_g_sweep2_ip(double *x, const double *f, double *side, unsigned long long *stats,
                         double hh, int H, int W, hipStream_t s);
-bool g_inplace();   // pgmg_jacobi sweeps in place (default; PGMG_OP_INPLACE=0: ping-pong)
 void launch_g_fixup(const double *partials, int np, double eps, const unsigned *done_prev,
                     unsigned *done_next, const double *src, double *dst,
                     unsigned long long *stats, int H, int W, hipStream_t s);

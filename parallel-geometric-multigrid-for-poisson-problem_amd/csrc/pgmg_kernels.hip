@@ -150,14 +150,16 @@ void launch_sweep(const SweepArgsT<T> &a, bool x0_zero, bool fine, hipStream_t s
     const dim3 grid(gx, gy), blk(kBlock);
     const bool norm = a.partials != nullptr;
     if (fine) {
-        if (x0_zero) k_sweep<T, true, false, true><<<grid, blk, 0, s>>>(b);
-        else if (norm) k_sweep<T, false, true, true><<<grid, blk, 0, s>>>(b);
-        else k_sweep<T, false, false, true><<<grid, blk, 0, s>>>(b);
+        if (x0_zero) launchk(k_sweep<T, true, false, true>, grid, blk, s, b);
+        else if (norm) launchk(k_sweep<T, false, true, true>, grid, blk, s, b);
+        else launchk(k_sweep<T, false, false, true>, grid, blk, s, b);
     } else {
-        if (x0_zero) k_sweep<T, true, false, false><<<grid, blk, 0, s>>>(b);
-        else if (norm) k_sweep<T, false, true, false><<<grid, blk, 0, s>>>(b);
-        else k_sweep<T, false, false, false><<<grid, blk, 0, s>>>(b);
+        if (x0_zero) launchk(k_sweep<T, true, false, false>, grid, blk, s, b);
+        else if (norm) launchk(k_sweep<T, false, true, false>, grid, blk, s, b);
+        else launchk(k_sweep<T, false, false, false>, grid, blk, s, b);
     }
+    // x (unless x0 = 0), f in; x out
+    g_last_launch.bytes = (x0_zero ? 16.0 : 24.0) * row_pts(a.row0, a.row1, a.W) * sizeof(T) / 8.0;
 }
 
 // ---------------------------------------------------------------------------

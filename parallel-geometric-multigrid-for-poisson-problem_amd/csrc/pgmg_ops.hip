@@ -93,14 +93,16 @@ int pgmg_jacobi(double *d_x, double *d_tmp, const double *d_f, int H, int W, dou
     const size_t L = (size_t)H * W;
     const int S = v + 1;
     const bool check = eps >= 0.0;
-    const bool inplace = g_inplace();
-    // in place, only a checked call with v >= 1 needs a ping-pong buffer
-    const bool need_tmp = !inplace || (check && S >= 2);
+    // every sweep runs in place; only a checked call with v >= 1 needs a ping-pong buffer
+    const bool need_tmp = check && S >= 2;
     OpScratch *op = nullptr;
     int e = ensure_scratch(s, (d_tmp || !need_tmp) ? 0 : L, &op);
     if (e) return e;
     OpScratch &g_op = *op;
-    if (inplace && (e = ensure_side(s, g_op, g_defer_elems(H, W)))) return e;
+    // the deferred-edge side buffer: only the passes that sweep in place use it (an unchecked
+    // call, or the first sweep of a checked call with an odd count; an even checked count is
+    // the ping-pong below)
+    if ((!check || (S & 1)) && (e = ensure_side(s, g_op, g_defer_elems(H, W)))) return e;
     double *tmp = d_tmp ? d_tmp : g_op.tmp;
     // flag slots: a fresh block of S+1 words per call would need a ring; the op is
     // synchronous w.r.t. its own flags because every launch is stream-ordered.
@@ -122,7 +124,7 @@ int pgmg_jacobi(double *d_x, double *d_tmp, const double *d_f, int H, int W, dou
         }
         return PGMG_OK;
     };
-    if (inplace && !check) {
+    if (!check) {
         // the reference GPU op (ComputeJacobi decides nothing between its v+1 sweeps,
         // Parallel_Method.cu:144-160): every sweep on d_x itself, in pairs (k_op_sweep2_ip)
         // with an odd count's single sweep first (k_op_sweep_ip); no tmp, no copy-back
@@ -131,15 +133,10 @@ int pgmg_jacobi(double *d_x, double *d_tmp, const double *d_f, int H, int W, dou
             launch_g_sweep_ip(d_x, d_f, g_op.side, &D[1], g_op.stats, hh, H, W, s);
             left -= 1;
         }
-        for (; left > 0; left -= 2)
-            if (g_fuse2()) launch_g_sweep2_ip(d_x, d_f, g_op.side, g_op.stats, hh, H, W, s);
-            else {
-                launch_g_sweep_ip(d_x, d_f, g_op.side, nullptr, g_op.stats, hh, H, W, s);
-                launch_g_sweep_ip(d_x, d_f, g_op.side, nullptr, g_op.stats, hh, H, W, s);
-            }
+        for (; left > 0; left -= 2) launch_g_sweep2_ip(d_x, d_f, g_op.side, g_op.stats, hh, H, W, s);
         return finish();
     }
-    if (inplace && (S & 1)) {
+    if (S & 1) {
         // JacobiSmoother::smooth's checks (Smoother.hpp:59-88) with an odd sweep count: sweep
         // 1 has no check and runs in place; sweeps k = 2 .. S alternate x -> tmp -> x, each
         // deciding the previous sweep's check (k_g_fixup undoes the sweep after a firing
@@ -155,33 +152,9 @@ int pgmg_jacobi(double *d_x, double *d_tmp, const double *d_f, int H, int W, dou
         }
         return finish();
     }
-    // ping-pong (an even checked count; everything with PGMG_OP_INPLACE=0 in the measurement
-    // build, the r04 form): sweeps alternate x -> tmp -> x ...  No seed copy of tmp (Smoother.hpp:47 copies the whole grid into its
-    // output buffer): the first sweep writes x's boundary into tmp besides the interior, which
-    // is all a later sweep reads of it.  An odd sweep count ends in tmp and copies its interior
-    // back (x's boundary is never written).
-    if (!check && g_fuse2()) {
-        const double *cur = d_x;
-        double *other = tmp;
-        int left = S;
-        bool first = true;
-        while (left > 0) {
-            if (left & 1) {
-                launch_g_sweep(cur, d_f, other, nullptr, nullptr, first ? &D[1] : nullptr,
-                               g_op.stats, hh, ih, H, W, first, s);
-                left -= 1;
-            } else {
-                launch_g_sweep2(cur, d_f, other, g_op.stats, hh, H, W, first, s);
-                left -= 2;
-            }
-            first = false;
-            double *nc = const_cast<double *>(cur);
-            cur = other;
-            other = nc;
-        }
-        if (cur == tmp) launch_g_copy_interior(tmp, d_x, H, W, s);
-        return finish();
-    }
+    // ping-pong (an even checked count): sweeps alternate x -> tmp -> x and end in x.  No
+    // seed copy of tmp (Smoother.hpp:47 copies the whole grid into its output buffer): the first
+    // sweep writes x's boundary into tmp besides the interior, which is all a later sweep reads
     for (int k = 1; k <= S; ++k) {
         const double *in = (k & 1) ? d_x : tmp;
         double *out = (k & 1) ? tmp : d_x;
@@ -192,7 +165,6 @@ int pgmg_jacobi(double *d_x, double *d_tmp, const double *d_f, int H, int W, dou
         if (with_check)
             launch_g_fixup(g_op.partials, nb, eps, &D[k - 1], &D[k], in, out, g_op.stats, H, W, s);
     }
-    if (S & 1) launch_g_copy_interior(tmp, d_x, H, W, s);
     return finish();
 }
 

@@ -1,0 +1,34 @@
+#!/bin/bash
+# r06 GPU session: the carry's tests first (verbose), smoke(), the whole GPU suite, then the
+# driver-shaped bench line.  bash scripts/r06_session.sh OUT [STEPS...]
+# STEPS (default: carry smoke tests bench): any of carry smoke tests bench bench_nocarry
+# Each GPU step runs under its own time limit; a time limit (124/137), an abort (134) or a
+# fault (139) ends the session.
+set -u
+export TMPDIR=/tmp
+OUT=${1:-gpurun_out/r06}
+shift || true
+STEPS=${*:-carry smoke tests bench}
+mkdir -p ${OUT}
+step() {   # step NAME LIMIT CMD... (stdout -> OUT/NAME.out, stderr -> OUT/NAME.err)
+  local name=$1 lim=$2
+  shift 2
+  echo "[$(date +%T)] ${name}" >&2
+  timeout -k 10 ${lim} "$@" > ${OUT}/${name}.out 2> ${OUT}/${name}.err
+  local rc=$?
+  echo "[$(date +%T)] ${name} rc=${rc}" >&2
+  tail -2 ${OUT}/${name}.out >&2
+  case ${rc} in
+    124|134|137|139) echo "stopping after ${name} (rc ${rc})" >&2; exit ${rc} ;;
+  esac
+  return 0
+}
+for s in ${STEPS}; do
+  case ${s} in
+    carry) step carry 600 python -u -m pytest tests/test_gpu_carry.py -x -v --timeout 300 --timeout-method thread ;;
+    smoke) step smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) step tests 900 python -u -m pytest tests/ -m gpu -q --timeout 300 --timeout-method thread ;;
+    bench) step bench 600 python bench.py --gpus 1 --warmup 5 --steps 20 --save-profiles ${OUT}/prof ;;
+    *) echo "unknown step ${s}" >&2 ;;
+  esac
+done

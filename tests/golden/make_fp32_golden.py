@@ -22,7 +22,7 @@ HERE = pathlib.Path(__file__).resolve().parent
 sys.path.insert(0, str(HERE.parent.parent / "oracle"))
 import oracle  # noqa: E402
 
-CASES = [("V", 16385, 3)]
+CASES = [("V", 16385, 25)]
 
 
 def hash_f32(a):

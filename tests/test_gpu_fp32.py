@@ -47,7 +47,7 @@ def test_fp32_vcycle_bitwise_vs_fp32_oracle(pgmg, oracle_mod, plan, N, tail_n, m
     if mode == "unfused":
         cfg["flags"] = pgmg.PGMG_FLAG_UNFUSED
     if mode in ("cross", "cross_stored"):
-        # the cross-cycle finest pass (fp32: k_postpre_q4, four columns per lane; several
+        # the cross-cycle finest pass (fp32: k_postpre_lds<float>, two columns per lane; several
         # column blocks from N = 1025 on, the analytic f regenerated or, stored, streamed)
         plan(cross_min_n=9)
     if mode == "cross_stored":
@@ -129,7 +129,7 @@ def test_fp32_strips_bitwise_equal_single_gpu(pgmg, plan, exact):
     """Row strips (loopback transport, 4 ranks) in fp32: same words as one GPU in fp32
     (halo rows and gathered levels move 4-byte elements).  exact: every check decided
     in-stream (PGMG_FLAG_EXACT_DIST) with the cross-cycle finest pass on, so the strips run
-    k_postpre_q4's third sum (R2)."""
+    k_postpre_lds<float>'s third sum (R2)."""
     N, world = 1025, 4
     if exact:
         plan(cross_min_n=9, flags=pgmg.PGMG_FLAG_EXACT_DIST)
