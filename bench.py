@@ -28,8 +28,8 @@ Kernel durations for `roofline` come from one more repetition with hipEvents aro
 finest-level pass (PGMG_FLAG_TIME_FINE; the events cost ~2-4 % of the cycle, so the clean
 repetitions give `value`).  `roofline.traffic` is the HBM traffic of the same kernel from
 two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over a short child run of this very
-build, made before this process touches the GPU (--pmc off: the committed
-profiles/pmc_fine.json, labelled with the build it measured).  With N GPUs the same grid is split into row strips (strong
+build, made before this process touches the GPU (--pmc off: null).  Kernel symbols and
+algorithmic bytes per launch of the timed passes come from the library (pgmg_fine_pass_info).  With N GPUs the same grid is split into row strips (strong
 scaling, RCCL halo exchange); value = V-cycles of the whole job per second.
 
 Prints ONE JSON line on rank 0.  See DESIGN.md "Measurement" for every field.
@@ -51,10 +51,8 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 TRACE_PREWARM = 4         # pre-warm calls before the kernel-trace child's timed call
 INST_REPS = 3             # repetitions with per-pass events (the roofline's event-timed median)
+PASSES = (0, 1, 2, 3, 4)  # finest-level passes: sweep, k_pre, k_post, k_postpre, carry pass
 METRIC = "V-cycles/sec + fine-grid stencil HBM GB/s, 2D Poisson N=16384², fp64"
-# rocprofv3 FETCH_SIZE/WRITE_SIZE of the finest-level passes (scripts/pmc_summary.py); the
-# profile names the build it was measured on
-PMC_PROFILE = ROOT / "profiles" / "pmc_fine.json"
 
 
 def parse():
@@ -185,7 +183,8 @@ def kernel_key(name):
 
 def pmc_child(args):
     """The program the live PMC passes profile: the timed call's kernels (a 3-cycle call:
-    first k_pre, two cross-cycle k_postpre, last k_post) of both legs, then exit."""
+    first k_pre, two cross-cycle k_postpre, the carry pass) of every leg and the per-op
+    study's calls, then exit."""
     import torch  # noqa: F401
     import _pkgload
     pg = _pkgload.load()
@@ -199,6 +198,14 @@ def pmc_child(args):
             s.set_problem()
             {"V": s.vcycle, "W": s.wcycle, "F": s.fcycle}[args.cycle](3 if args.cycle != "W" else 1)
             s.sync()
+    if args.ops == "auto" and args.cycle == "V" and args.dtype == "f64":
+        import torch
+        cases, keep = op_cases(pg, args.n)
+        for case in cases:
+            for _ in range(2):
+                case[1]()
+        torch.cuda.synchronize()
+        del keep
 
 
 # algorithmic bytes per interior point of each op (fine grid n = (N-2)^2,
@@ -222,54 +229,102 @@ def op_cases(pg, n, device="cuda:0"):
     e = torch.ones((nc, nc), dtype=torch.float64, device=dev)
     def sweep(check, pair=None):
         # trace keys: k_op_sweep<U,CHECK,SEED,NT> (the checked smoother's ping-pong sweeps),
-        # k_op_sweep_ip<U,NT> / k_op_sweep2_ip<U,NT> (the in-place single / paired sweeps)
+        # k_op_sweep_ip<U,NT> / k_op_sweep2_ip<U,NT> (the in-place single / paired sweeps), and
+        # k_op_defer_scatter (every in-place pass's deferred tile edges: part of the op's cost,
+        # counted as 0 sweeps)
         def m(k):
             if not check:
                 return (k.startswith("k_op_sweep2_ip") if pair is True else
                         k.startswith("k_op_sweep_ip") if pair is False else
-                        k.startswith("k_op_sweep_ip") or k.startswith("k_op_sweep2_ip"))
+                        k.startswith("k_op_sweep_ip") or k.startswith("k_op_sweep2_ip")) or \
+                    k.startswith("k_op_defer_scatter")
             return k.startswith("k_op_sweep<")   # v = 1 checked: two ping-pong sweeps
         return m
 
     def named(prefix):
         return lambda k: k.startswith(prefix)
 
+    # (name, call, bytes per call counted per sweep, trace-key matcher, sweeps,
+    # passes over the grid per call: a paired in-place pass reads x and f and writes x ONCE for
+    # two sweeps, so its one-pass bytes are 24 B per point, not 48)
     cases = [
         ("jacobi v=0 (one sweep in place on x: k_op_sweep_ip + the scatter of its deferred "
          "tile edges)",
-         lambda: pg.ops.jacobi(x, f, h, 0, eps=-1.0, tmp=tmp, count=False), 24 * fine, sweep(False, False), 1),
+         lambda: pg.ops.jacobi(x, f, h, 0, eps=-1.0, tmp=tmp, count=False), 24 * fine, sweep(False, False), 1, 1),
         ("jacobi v=1 (2 sweeps, no early exit: Parallel::ComputeJacobi's call in the V-cycle; "
          "one paired pass in place, k_op_sweep2_ip + the scatter)",
-         lambda: pg.ops.jacobi(x, f, h, 1, eps=-1.0, tmp=tmp, count=False), 2 * 24 * fine, sweep(False, True), 2),
-        ("jacobi v=100 (101 sweeps, no early exit: the per-op study's ComputeJacobi call)",
+         lambda: pg.ops.jacobi(x, f, h, 1, eps=-1.0, tmp=tmp, count=False), 2 * 24 * fine, sweep(False, True), 2, 1),
+        ("jacobi v=100 (101 sweeps, no early exit: the per-op study's ComputeJacobi call; one "
+         "single and 50 paired passes)",
          lambda: pg.ops.jacobi(x, f, h, 100, eps=-1.0, tmp=tmp, count=False), 101 * 24 * fine, sweep(False),
-         101),
+         101, 51),
         ("jacobi v=1 with the smoother's early-exit checks (JacobiSmoother::smooth)",
          lambda: pg.ops.jacobi(x, f, h, 1, eps=1e-7, tmp=tmp, count=False), 2 * 24 * fine,
-         sweep(True), 2),
+         sweep(True), 2, 2),
         ("residual (ComputeResidual)", lambda: pg.ops.residual(r, x, f, h), 24 * fine,
-         named("k_op_residual"), 0),
+         named("k_op_residual"), 0, 1),
         ("restriction (ComputeRestriction)", lambda: pg.ops.restrict(r, c), 8 * fine + 8 * coarse,
-         named("k_op_restrict"), 0),
+         named("k_op_restrict"), 0, 1),
         ("prolongation, symmetric over the reference's launch grid (ComputeProlungator, "
          "num_thread 32)",
          lambda: pg.ops.prolong(e, r, mode=pg.PGMG_PROLONG_SYMMETRIC, num_thread=32),
-         16 * fine + 8 * coarse, named("k_op_prolong<1>"), 0),
+         16 * fine + 8 * coarse, named("k_op_prolong<1>"), 0, 1),
         ("prolongation, the CPU path's (MultiGrid.hpp:208-226)",
          lambda: pg.ops.prolong(e, r, mode=pg.PGMG_PROLONG_REFERENCE), 16 * fine + 8 * coarse,
-         named("k_op_prolong<0>"), 0),
+         named("k_op_prolong<0>"), 0, 1),
     ]
     return cases, (x, f, tmp, r, c, e)
 
 
-def op_study(pg, n, trace, reps=5):
+def op_row(name, nbytes, keys, sweeps, passes, ms, trace, pmc, pmc_source):
+    """One row of the per-op table.  `frac` is the one-pass roofline fraction: the call's
+    passes x the bytes one pass moves (24 B per point for a sweep, single or paired) over its
+    time -- physically bounded by the copy ceiling.  A multi-sweep call also gets
+    `sweep_equiv_frac` (SURVEY §8(d)'s 24 B per SWEEP over the same time; above 1 when two
+    sweeps share one pass).  rocprof: the kernels' average from the trace pass (the scatter of
+    the in-place passes' deferred edges included, as 0 sweeps); PMC: `traffic_ratio` of the
+    call's main kernel, HBM bytes per launch (live rocprofv3 passes of this build) over its
+    one-pass algorithmic bytes."""
+    per_pass = nbytes / sweeps if sweeps else nbytes
+    one = passes * per_pass
+    row = {"op": name, "ms_per_call": round(ms, 5), "bytes_per_call": nbytes,
+           "passes_per_call": passes, "one_pass_bytes": per_pass,
+           "achieved_gbps": round(one / (ms * 1e-3) / 1e9, 1),
+           "frac": round(one / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
+    if sweeps:
+        row["ms_per_sweep"] = round(ms / sweeps, 5)
+        if sweeps > passes:
+            row["sweep_equiv_gbps"] = round(nbytes / (ms * 1e-3) / 1e9, 1)
+            row["sweep_equiv_frac"] = round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+    # rocprof: the case's main kernels (the trace pass ran every case 3 times, so a key shared
+    # by several cases -- the in-place single sweep, the scatter -- averages over them)
+    tk = [(k, v) for k, v in (trace or {}).items() if keys(k) and not k.startswith("k_op_defer_scatter")]
+    if tk:
+        n = sum(v[0] for _, v in tk)
+        avg = sum(v[0] * v[1] for _, v in tk) / n
+        row["kernel_rocprof"] = {k: {"launches": v[0], "ms_per_launch": round(v[1], 5)} for k, v in tk}
+        row["ms_per_launch_rocprof"] = round(avg, 5)
+        row["frac_rocprof"] = round(per_pass / (avg * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+        sc = [v for k, v in (trace or {}).items() if keys(k) and k.startswith("k_op_defer_scatter")]
+        if sc:
+            row["scatter_ms_per_launch_rocprof"] = round(sc[0][1], 5)
+    if pmc:
+        mk = [k for k in pmc if keys(k) and not k.startswith("k_op_defer_scatter")]
+        if mk:
+            k = max(mk, key=lambda q: pmc[q])
+            row.update({"pmc_kernel": k, "traffic": pmc[k],
+                        "traffic_ratio": round(pmc[k] / per_pass, 4), "traffic_source": pmc_source})
+    return row
+
+
+def op_study(pg, n, trace, pmc=None, pmc_source=None, reps=5):
     """Each op of op_cases called `reps` times after one warmup call on the null stream,
     timed with events around each call (median); beside it the op's kernels' rocprof average
-    from the trace pass (same box, same build)."""
+    from the trace pass and their HBM traffic from the PMC passes (same box, same build)."""
     import torch
     cases, keep = op_cases(pg, n)
     out = []
-    for name, call, nbytes, keys, sweeps in cases:
+    for name, call, nbytes, keys, sweeps, passes in cases:
         call()
         torch.cuda.synchronize()
         ts = []
@@ -280,30 +335,8 @@ def op_study(pg, n, trace, reps=5):
             b.record()
             b.synchronize()
             ts.append(a.elapsed_time(b))
-        ms = statistics.median(ts)
-        row = {"op": name, "ms_per_call": round(ms, 5), "bytes_per_call": nbytes,
-               "achieved_gbps": round(nbytes / (ms * 1e-3) / 1e9, 1),
-               "frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
-        if sweeps:
-            per = nbytes / sweeps
-            row["ms_per_sweep"] = round(ms / sweeps, 5)
-            if trace is not None:
-                # the trace pass ran each case 3 times; a k_op_sweep2 launch is two sweeps
-                tk = [(k, v) for k, v in trace.items() if keys(k)]
-                if tk:
-                    tot = sum(v[0] * v[1] for _, v in tk)
-                    nsw = sum(v[0] * (2 if k.startswith("k_op_sweep2") else 1) for k, v in tk)
-                    avg = tot / nsw
-                    row.update({"kernel_rocprof": {k: {"launches": v[0], "ms_per_launch": round(v[1], 5)}
-                                                   for k, v in tk},
-                                "ms_per_sweep_rocprof": round(avg, 5),
-                                "frac_sweep_rocprof": round(per / (avg * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)})
-        elif trace is not None and [k for k in trace if keys(k)]:
-            kk = [k for k in trace if keys(k)][0]
-            avg = trace[kk][1]
-            row.update({"kernel_rocprof": kk, "ms_per_launch_rocprof": round(avg, 5),
-                        "frac_rocprof": round(nbytes / (avg * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)})
-        out.append(row)
+        out.append(op_row(name, nbytes, keys, sweeps, passes, statistics.median(ts), trace, pmc,
+                          pmc_source))
     del keep
     torch.cuda.empty_cache()
     return out
@@ -332,9 +365,9 @@ def trace_child(args):
     if args.ops == "auto" and args.cycle == "V" and args.dtype == "f64":
         import torch
         cases, keep = op_cases(pg, args.n)
-        for _, call, _, _, _ in cases:
+        for case in cases:
             for _ in range(3):
-                call()
+                case[1]()
         torch.cuda.synchronize()
         del keep
 
@@ -377,8 +410,11 @@ def live_trace(args):
         if traces and args.cycle == "V":
             per = {}
             for row in csv.DictReader(open(traces[0])):
+                dur = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
                 per.setdefault(kernel_key(row["Kernel_Name"]), []).append(
-                    (int(row["Start_Timestamp"]), int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
+                    (int(row["Start_Timestamp"]), dur))
+                # per launch grid too: the levels table (levels_table) tells the levels apart
+                GRID["trace"].setdefault((kernel_key(row["Kernel_Name"]), grid_total(row)), []).append(dur)
             last = args.steps - 1
             for k, v in per.items():
                 if k.startswith("k_postpre_lds") and last > 0 and len(v) > last:
@@ -393,6 +429,73 @@ def live_trace(args):
         return None, f"rocprofv3 --kernel-trace failed: {e}"
     finally:
         shutil.rmtree(d, ignore_errors=True)
+
+
+# per (kernel key, launch grid): trace durations (ns) and PMC counters, for the levels table
+GRID = {"trace": {}, "pmc": {}}
+
+
+def grid_total(row):
+    """Work-items of a launch from a rocprofv3 CSV row."""
+    if "Grid_Size" in row:
+        return int(row["Grid_Size"])
+    return int(row.get("Grid_Size_X", 1)) * int(row.get("Grid_Size_Y", 1)) * int(row.get("Grid_Size_Z", 1))
+
+
+def fused_grid(N):
+    """Work-items of a coarse level's k_pre / k_post launch on one GPU (fused_geometry of
+    pgmg_fused.hip restated: the levels table tells the levels apart by it)."""
+    rows = (N - 1) // 2
+    pts = 2 * rows * N
+    target = min(3072, max(512, pts // 21845)) if pts > (1 << 23) else max(256, pts // 8192)
+    waves = (N - 2 + 119) // 120
+    wpb = min(waves, 4)
+    gx = (waves + wpb - 1) // wpb
+    gymax = max(1, target // gx)
+    r = max(2, (rows + gymax - 1) // gymax)
+    r = max(1, min(r, rows))
+    gy = (rows + r - 1) // r
+    return gx * 64 * wpb * gy
+
+
+def levels_table(n, grid, fine_bytes):
+    """Per bulk level and pass of a V-cycle at grid n: mean duration (us, all launches of the
+    trace child), algorithmic GB/s and the HBM traffic ratio (2 x FETCH_SIZE + WRITE_SIZE of
+    the PMC child over the algorithmic bytes).  Levels below the finest enter with x0 = 0:
+    k_pre reads f, writes rc (8 B per point + 8 per coarse point), k_post reads f and the
+    correction and writes x2 (16 + 8); the finest passes' bytes come from the library
+    (fine_bytes: {kernel key: bytes per launch}).  The small levels' 2D tile passes (N <= 513)
+    are launch-bound and listed by kernel only."""
+    lv = {}
+    N = n // 2 + 1
+    while N >= 129:
+        lv[fused_grid(N)] = N
+        N = N // 2 + 1
+    rows = []
+    for (key, g), ds in sorted(grid["trace"].items(), key=lambda kv: (-sum(kv[1]) / len(kv[1]))):
+        if key in fine_bytes:
+            Nl, alg, what = n, fine_bytes[key], key.split("<")[0]
+        elif (key.startswith("k_pre<") or key.startswith("k_post<")) and g in lv:
+            Nl = lv[g]
+            Nc = Nl // 2 + 1
+            fp, cp = float((Nl - 2) ** 2), float((Nc - 2) ** 2)
+            alg = 8 * fp + 8 * cp if key.startswith("k_pre<") else 16 * fp + 8 * cp
+            what = key.split("<")[0]
+        elif key.startswith("k_pre_tile") or key.startswith("k_post_tile"):
+            Nl, alg, what = None, None, key.split("<")[0]
+        else:
+            continue
+        us = sum(ds) / len(ds) / 1e3
+        c = grid["pmc"].get((key, g), {})
+        hbm = None
+        if c.get("FETCH_SIZE") and c.get("WRITE_SIZE"):
+            hbm = (2 * sum(c["FETCH_SIZE"]) / len(c["FETCH_SIZE"]) +
+                   sum(c["WRITE_SIZE"]) / len(c["WRITE_SIZE"])) * 1024.0
+        rows.append({"N": Nl, "pass": what, "kernel": key, "launches": len(ds), "us": round(us, 2),
+                     "alg_gbps": round(alg / us * 1e-3, 1) if alg else None,
+                     "traffic_ratio": round(hbm / alg, 3) if (hbm and alg) else None})
+    rows.sort(key=lambda r: (-(r["N"] or 0), r["pass"]))
+    return rows
 
 
 def launch_ranks(args):
@@ -442,7 +545,7 @@ def live_pmc(args):
         cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", ctr, "--output-format", "csv",
                "-d", d, "-o", "run", "--", sys.executable, str(ROOT / "bench.py"), "--pmc-child",
                "--n", str(args.n), "--dtype", args.dtype, "--cycle", args.cycle,
-               "--general-rhs", args.general_rhs, "--fast-mode", args.fast_mode]
+               "--general-rhs", args.general_rhs, "--fast-mode", args.fast_mode, "--ops", args.ops]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=180)
             files = list(pathlib.Path(d).rglob("*counter_collection.csv"))
@@ -453,6 +556,8 @@ def live_pmc(args):
                 if row.get("Counter_Name") == ctr:
                     vals.setdefault(kernel_key(row["Kernel_Name"]), {}).setdefault(ctr, []).append(
                         float(row["Counter_Value"]))
+                    GRID["pmc"].setdefault((kernel_key(row["Kernel_Name"]), grid_total(row)), {}).setdefault(
+                        ctr, []).append(float(row["Counter_Value"]))
         except (subprocess.SubprocessError, OSError, KeyError, ValueError) as e:
             return None, f"rocprofv3 --pmc {ctr} failed: {e}"
         finally:
@@ -466,24 +571,6 @@ def live_pmc(args):
     return out, "live rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this build (bench.py --pmc)"
 
 
-def pmc_traffic(n, key):
-    """Fallback: HBM bytes per launch of kernel `key` at grid n from the committed rocprofv3
-    PMC summary, and the build it was measured on."""
-    if not PMC_PROFILE.exists():
-        return None, None
-    try:
-        d = json.loads(PMC_PROFILE.read_text())
-        for k in d.get("kernels", []):
-            if int(k.get("N", 0)) == n and k.get("kernel", "") == key:
-                build = d.get("build")
-                label = ("this build" if build and build == lib_build_id()
-                         else f"another build: {build or 'unrecorded'}")
-                return k.get("hbm_bytes_per_launch"), f"{PMC_PROFILE.relative_to(ROOT)} ({label})"
-    except (ValueError, OSError):
-        pass
-    return None, None
-
-
 def golden_hash(kind, n, cycles):
     """The reference's FNV-64 of phi after `cycles` cycles from phi0 = 0 (fixture data:
     tests/golden/cycles.json, generated by tests/golden/make_golden.py), or None."""
@@ -494,6 +581,103 @@ def golden_hash(kind, n, cycles):
         if c["kind"] == kind and c["N"] == n and c["eps"] == 1e-7 and len(c["cycles"]) >= cycles:
             return c["cycles"][cycles - 1]["hash"]
     return None
+
+
+def rank_split_summary(allr, inst_dt, steps):
+    """Per-rank (device ms per cycle, ms inside collective groups per cycle, groups per cycle),
+    rank order -> the line's rank_split: compute vs RCCL time, median and max over ranks."""
+    comp = [r[0] - r[1] for r in allr]
+    comm = [r[1] for r in allr]
+    return {
+        "what": "per rank, per cycle of the instrumented repetitions (hipEvents around every "
+                "collective group on the rank's stream, PGMG_FLAG_TIME_COMM): compute = the "
+                "call's device time minus the time inside collectives (RCCL transfer + waiting "
+                "for a peer)",
+        "compute_ms": {"median": round(statistics.median(comp), 4), "max": round(max(comp), 4),
+                       "per_rank": [round(x, 4) for x in comp]},
+        "rccl_ms": {"median": round(statistics.median(comm), 4), "max": round(max(comm), 4),
+                    "per_rank": [round(x, 4) for x in comm]},
+        "groups_per_cycle": round(allr[0][2], 2),
+        "instrumented_ms_per_step": round(inst_dt * 1e3 / steps, 4)}
+
+
+PASS_NAMES = {
+    0: "k_sweep (finest-level Jacobi sweep, unfused path)",
+    1: "k_pre (finest level: 2 Jacobi sweeps + residual + restriction, fused)",
+    2: "k_post (finest level: prolongation + 2 Jacobi sweeps, fused)",
+    3: "k_postpre (finest level, between cycles: prolongation + 2+2 Jacobi sweeps + residual + "
+       "restriction, fused)",
+    4: "carry pass (the call's last finest pass: k_postpre that also stores the call's result, "
+       "the next call's pre-smooth carried)",
+}
+
+
+def roofline_rows(leg, pmc, pmc_source, trace, trace_note):
+    """One roofline row per finest-level pass timed in the instrumented repetitions, the
+    dominant (largest total time) first.  Kernel symbol and algorithmic bytes per launch come
+    from the library (pgmg_fine_pass_info: the variant that ran and what it read and wrote);
+    `traffic` is the same symbol's HBM bytes per launch from the live PMC passes of this build
+    (null without them: never another build's); rocprof columns from the trace pass."""
+    roof = []
+    for w, cnt, ms in leg["passes"]:
+        if not cnt or ms <= 0:
+            continue
+        sym, nb = leg.get("info", {}).get(w, ("", 0.0))
+        key = kernel_key(sym) if sym else None
+        nbytes = nb if nb > 0 else leg["bytes"][w]
+        ach = nbytes / (ms * 1e-3) / 1e9
+        traffic = pmc.get(key) if (pmc is not None and key) else None
+        name = PASS_NAMES[w] + ("; f regenerated in-kernel" if leg.get("gen") else "; f streamed")
+        if leg.get("fast"):
+            name += " — FAST mode"
+        roof.append({"bound": "hbm", "kernel": name, "symbol": key,
+                     "symbol_source": "pgmg_fine_pass_info (the launched kernel)" if key else
+                                      "unavailable (hipKernelNameRefByPtr returned nothing)",
+                     "achieved": round(ach, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(ach / HBM_PEAK_GBPS, 4),
+                     "traffic": traffic,
+                     "traffic_source": pmc_source if traffic else None,
+                     "traffic_ratio": round(traffic / nbytes, 4) if traffic else None,
+                     "bytes_per_launch": nbytes, "launches_timed": cnt,
+                     "ms_per_launch": round(ms, 5),
+                     "ms_per_launch_reps": [round(x, 5) for x in leg["passes_reps"][w]]})
+        tr = trace.get(key) if (trace is not None and key) else None
+        if tr is not None:
+            tms = tr[2] if tr[2] is not None else tr[1]
+            ach_r = nbytes / (tms * 1e-3) / 1e9
+            roof[-1].update({"ms_per_launch_rocprof": round(tms, 5),
+                             "ms_per_launch_rocprof_all_launches": round(tr[1], 5),
+                             "launches_rocprof": tr[0],
+                             "launches_rocprof_timed": tr[3],
+                             "frac_rocprof": round(ach_r / HBM_PEAK_GBPS, 4),
+                             "event_vs_rocprof": round(ms / tms, 4),
+                             "rocprof_source": trace_note})
+    roof.sort(key=lambda r: -r["ms_per_launch"] * r["launches_timed"])
+    return roof
+
+
+# the measured copy ceiling (MI355X_MICROARCH.md: 6.29 TB/s float4 copy = 0.79 of 8 TB/s); an
+# algorithmic fraction above it means a mis-charged kernel, not a fast one
+FRAC_CEILING = 0.79
+
+
+def implausible_fracs(obj, path="line"):
+    """Every roofline-fraction field above the copy ceiling (keys named frac*, except the
+    op table's sweep_equiv_frac, which counts two sweeps of one pass) and every traffic source
+    that does not name this build: [(path, what)]."""
+    bad = []
+    if isinstance(obj, dict):
+        for k, v in obj.items():
+            p = f"{path}.{k}"
+            if isinstance(v, (int, float)) and k.startswith("frac") and v > FRAC_CEILING:
+                bad.append((p, f"{v} > {FRAC_CEILING}"))
+            if k == "traffic_source" and v is not None and "sha256:" not in str(v):
+                bad.append((p, f"does not name this build: {v}"))
+            bad += implausible_fracs(v, p)
+    elif isinstance(obj, list):
+        for i, v in enumerate(obj):
+            bad += implausible_fracs(v, f"{path}[{i}]")
+    return bad
 
 
 def main():
@@ -542,6 +726,7 @@ def main():
     pmc, pmc_note = None, "off"
     if world == 1 and rank == 0 and args.pmc == "auto":
         pmc, pmc_note = live_pmc(args)
+    pmc_source = f"{pmc_note}; {lib_build_id()}" if pmc is not None else None
     trace, trace_note = None, "off"
     if world == 1 and rank == 0 and args.trace == "auto":
         trace, trace_note = live_trace(args)
@@ -579,6 +764,19 @@ def main():
         return float(tt.item())
 
     want = golden_hash(args.cycle, args.n, args.warmup + args.steps) if args.dtype == "f64" else None
+    # the latency floor of the strips' collectives on this device (world-1 RCCL communicator,
+    # rank 0 only): what DESIGN §5 prices a dependent exchange group at
+    rccl_floor = None
+    if rank == 0 and not (solo or host_tp):
+        try:
+            rccl_floor = dict(pg.rccl_latency(device, 200), what=(
+                "world-1 RCCL communicator on this GPU, hipEvents over 200 calls: a grouped "
+                "send+recv of the finest halo at 16385 (2 rows, 262 KB) to itself, allreduce(sum, "
+                "3 doubles), allreduce(min, 9 u32); a lower bound of one exchange group between "
+                "ranks (no xGMI hop, no peer to wait for)"))
+            rccl_floor = {k: (round(v, 2) if isinstance(v, float) else v) for k, v in rccl_floor.items()}
+        except Exception as e:  # reported, not fatal
+            rccl_floor = {"error": str(e)[:200]}
 
     def new_solver(flags, n=None):
         kw = dict(device=device, dtype=args.dtype)
@@ -591,25 +789,48 @@ def main():
         return pg.Solver(args.n if n is None else n,
                          flags=flags | (pg.PGMG_FLAG_SOLO if solo else 0), **kw)
 
-    def run_leg(extra_flags, reps):
+    def parity_of(leg):
+        p = leg["parity"]
+        if not p or any(x is None for x in p):
+            return None
+        return all(p)
+
+    def gather(x):
+        """x from every rank (rank order); [x] on one rank"""
+        if dist is None:
+            return [x]
+        out = [None] * world
+        dist.all_gather_object(out, x)
+        return out
+
+    def run_leg(extra_flags, reps, n=None, warm=None, steps=None, want_hash=None,
+                inst_reps=INST_REPS):
         """`reps` clean repetitions on one context (set_problem restarts each from phi0 = 0)
-        + INST_REPS repetitions with per-pass events on a second (per pass, the median over
-        them); returns times, parity, passes"""
-        out = {"times": [], "parity": [], "passes": [], "inst_dt": None}
+        + inst_reps repetitions with per-pass events on a second (per pass, the median over
+        them; on row strips also events around every collective group: per-rank compute vs
+        RCCL time); returns times, parity, passes"""
+        warm = max(args.warmup, 0) if warm is None else warm
+        steps = args.steps if steps is None else steps
+        want_hash = want if want_hash is None else want_hash
+        out = {"times": [], "parity": [], "passes": [], "inst_dt": None, "split": []}
         inst_dt, inst_passes = [], []
         for inst in (False, True):
-            s = new_solver(extra_flags | (pg.PGMG_FLAG_TIME_FINE if inst else 0))
+            fl = extra_flags
+            if inst:
+                fl |= pg.PGMG_FLAG_TIME_FINE | (pg.PGMG_FLAG_TIME_COMM if world > 1 else 0)
+            s = new_solver(fl, n=n)
             run = {"V": s.vcycle, "W": s.wcycle, "F": s.fcycle}[args.cycle]
-            for _ in range(INST_REPS if inst else reps):
+            for _ in range(inst_reps if inst else reps):
                 s.set_problem()
-                run(max(args.warmup, 0))
+                run(warm)
                 s.sync()
-                for w in (0, 1, 2, 3):  # drop warmup events
+                for w in PASSES:  # drop warmup events
                     s.fine_pass_time(w)
+                s.comm_stats()
                 barrier()
                 s.sync()
                 t0 = time.perf_counter()
-                run(args.steps)
+                run(steps)
                 t_enq = time.perf_counter()
                 s.sync()
                 barrier()
@@ -617,26 +838,41 @@ def main():
                 dt = max_over_ranks(t1 - t0)
                 if inst:
                     inst_dt.append(dt)
-                    inst_passes.append([tuple(s.fine_pass_time(w)) for w in (0, 1, 2, 3)])
-                    out["bytes"] = {w: s.fine_pass_bytes(w) for w in (0, 1, 2, 3)}
+                    inst_passes.append([tuple(s.fine_pass_time(w)) for w in PASSES])
+                    # what those launches were: kernel symbol and algorithmic bytes per launch,
+                    # from the library (the variant that ran, not one named from flags here)
+                    out["info"] = {w: s.fine_pass_info(w) for w in PASSES}
+                    out["bytes"] = {w: s.fine_pass_bytes(w) for w in PASSES}
+                    if world > 1:   # this rank's device time of the call, its collectives' time
+                        groups, cms = s.comm_stats()
+                        out["split"].append((s.last_elapsed_ms(), cms, groups))
                 else:
                     out["times"].append(dt)
                     out["enq"] = t_enq - t0
                     out["dev_ms"] = s.last_elapsed_ms()
                     if not solo:
                         h = s.solution_hash(0)
-                        out["parity"].append(None if want is None or h is None else h == want)
+                        out["parity"].append(None if want_hash is None or h is None else h == want_hash)
                     out["spec"] = (s.dist_info(), s.spec_levels())
+                    out["carry"] = s.carry_info()
             out["vbytes"] = s.vcycle_bytes()
             out["fused"] = s.fused
             out["levels"] = s.levels()
             out["gen"] = s.fused and s.fine_pass_bytes(3) < s.fine_pass_bytes(0)
             out["r2"] = world > 1 and not s.dist_info()[0]
+            out["comm_ranks"] = s.comm_ranks()
             s.close()
         out["inst_dt"] = statistics.median(inst_dt)
-        out["passes"] = [(w, inst_passes[0][w][0],
-                          statistics.median(r[w][1] for r in inst_passes)) for w in (0, 1, 2, 3)]
-        out["passes_reps"] = {w: [r[w][1] for r in inst_passes] for w in (0, 1, 2, 3)}
+        out["passes"] = [(w, inst_passes[0][i][0], statistics.median(r[i][1] for r in inst_passes))
+                         for i, w in enumerate(PASSES)]
+        out["passes_reps"] = {w: [r[i][1] for r in inst_passes] for i, w in enumerate(PASSES)}
+        if world > 1:
+            # per rank (median over the instrumented repetitions): device ms of the timed call
+            # per cycle, of which inside collective groups (transfer + waiting for a peer)
+            mine = (statistics.median(x[0] for x in out["split"]) / steps,
+                    statistics.median(x[1] for x in out["split"]) / steps,
+                    statistics.median(x[2] for x in out["split"]) / steps)
+            out["rank_split"] = rank_split_summary(gather(mine), out["inst_dt"], steps)
         return out
 
     main_leg = run_leg(0, max(1, args.reps))
@@ -647,27 +883,18 @@ def main():
     # (the host-staged transport runs it too: the harness test of this leg on a one-GPU box)
     if (world > 1 and not solo and args.cycle == "V" and args.dtype == "f64"
             and args.n == 16385 and args.big_grid == "auto"):
-        s = new_solver(0, n=32769)
-        ts = []
-        for _ in range(3):
-            s.set_problem()
-            s.vcycle(1)
-            s.sync()
-            barrier()
-            t0 = time.perf_counter()
-            s.vcycle(5)
-            s.sync()
-            barrier()
-            ts.append(max_over_ranks(time.perf_counter() - t0))
-        w6, h6 = golden_hash("V", 32769, 6), s.solution_hash(0)
-        s.close()
-        dt = statistics.median(ts)
+        bl = run_leg(0, 3, n=32769, warm=1, steps=5, want_hash=golden_hash("V", 32769, 6),
+                     inst_reps=1)
+        dt = statistics.median(bl["times"])
+        broof = roofline_rows(bl, None, None, None, None)
         big_leg = {"config": "BASELINE configs[3]: V-cycle N=32768^2 on the same row strips "
                              f"x{world} ({'host-staged transport, every rank on GPU 0: harness test, not a measurement' if host_tp else 'RCCL halos'}); "
                              "its one-GPU number: other_configs of the N = 1 line",
                    "value": round(5 / dt, 3), "unit": "V-cycles/s", "n_gpus": world,
                    "ms_per_step": round(dt * 1e3 / 5, 4), "timed": "1 + 5 cycles, median of 3",
-                   "parity": None if w6 is None or h6 is None else h6 == w6}
+                   "parity": parity_of(bl),
+                   "roofline": broof[0] if broof else None,
+                   "rank_split": bl.get("rank_split")}
     gen_leg = None
     if (world == 1 and args.cycle == "V" and args.general_rhs == "auto" and main_leg["fused"]
             and main_leg["gen"]):
@@ -738,21 +965,26 @@ def main():
     # API with one-cycle calls (pgmg_vcycle(ctx, 1), no cross-cycle fusion between calls)
     dropin = None
     if world == 1 and args.cycle == "V" and args.dtype == "f64" and args.dropin == "auto":
-        ts = []
-        s = new_solver(0)
-        for _ in range(3):
-            s.set_problem()
-            for _ in range(max(args.warmup, 0)):
-                s.vcycle(1)
-            s.sync()
-            t0 = time.perf_counter()
-            for _ in range(args.steps):
-                s.vcycle(1)
-            s.sync()
-            ts.append(time.perf_counter() - t0)
-        h_ctx = s.solution_hash(0)
-        s.close()
-        ctx_dt = statistics.median(ts)
+        def single_calls(flags):
+            """3 repetitions of W + K one-cycle calls on a fresh problem; K timed (median)"""
+            ts = []
+            s = new_solver(flags)
+            for _ in range(3):
+                s.set_problem()
+                for _ in range(max(args.warmup, 0)):
+                    s.vcycle(1)
+                s.sync()
+                t0 = time.perf_counter()
+                for _ in range(args.steps):
+                    s.vcycle(1)
+                s.sync()
+                ts.append(time.perf_counter() - t0)
+            h = s.solution_hash(0)
+            carry = s.carry_info()
+            s.close()
+            return statistics.median(ts), h, carry
+        ctx_dt, h_ctx, ctx_carry = single_calls(0)
+        nc_dt, h_nc, _ = single_calls(pg.PGMG_FLAG_NO_CARRY)
         exe = pathlib.Path(_pkgload.PKG_DIR) / "host" / "gpu_exec"
         runs = []
         for _ in range(3):
@@ -780,10 +1012,18 @@ def main():
                 "phi_arrays": ok[0][3],
                 "parity": None if want is None else all(x[2] == want for x in ok),
                 "context_single_calls": {
-                    "what": "pgmg_vcycle(ctx, 1) called once per cycle on the context's own grids",
+                    "what": "pgmg_vcycle(ctx, 1) called once per cycle on the context's own grids "
+                            "(each call after the first starts from the carry: the previous "
+                            "call's last pass ran its pre-smooth)",
                     "value": round(args.steps / ctx_dt, 4), "unit": "V-cycles/s",
                     "ms_per_step": round(ctx_dt * 1e3 / args.steps, 4),
-                    "parity": None if want is None or h_ctx is None else h_ctx == want},
+                    "parity": None if want is None or h_ctx is None else h_ctx == want,
+                    "carry_took_made_dropped": list(ctx_carry),
+                    "no_carry": {"what": "the same calls with PGMG_FLAG_NO_CARRY (k_pre + k_post "
+                                         "at level 0 in every call)",
+                                 "value": round(args.steps / nc_dt, 4), "unit": "V-cycles/s",
+                                 "ms_per_step": round(nc_dt * 1e3 / args.steps, 4),
+                                 "parity": None if want is None or h_nc is None else h_nc == want}},
                 "dropin_over_context_time": round(d_dt / ctx_dt, 4),
             }
         else:
@@ -815,69 +1055,14 @@ def main():
     # the per-op study (Parallel::Compute* on reference-layout arrays), VERDICT r03 #3
     op_rows = None
     if world == 1 and args.cycle == "V" and args.dtype == "f64" and args.ops == "auto":
-        op_rows = op_study(pg, args.n, trace)
+        op_rows = op_study(pg, args.n, trace, pmc, pmc_source)
         if args.save_profiles:
             pathlib.Path(args.save_profiles).mkdir(parents=True, exist_ok=True)
             (pathlib.Path(args.save_profiles) / "ops_table.json").write_text(
                 json.dumps({"N": args.n, "build": lib_build_id(), "ops": op_rows}, indent=1))
 
-    T = "double" if args.dtype == "f64" else "float"
-
     def roofline(leg):
-        names = {
-            3: ("k_postpre (finest level, between cycles: prolongation + 2+2 Jacobi sweeps + "
-                "residual + restriction, fused" + ("; f regenerated in-kernel" if leg["gen"] else
-                                                   "; f streamed") + ")",
-                f"k_postpre_lds<{T},{'true' if leg['r2'] else 'false'},"
-                f"{'true' if leg['gen'] else 'false'},2>"),
-            1: ("k_pre (finest level: 2 Jacobi sweeps + residual + restriction, fused)",
-                f"k_pre<{T},false,true,2,{'true' if leg['gen'] else 'false'},false>"),
-            2: ("k_post (finest level: prolongation + 2 Jacobi sweeps, fused)",
-                f"k_post<{T},true,2,false,true>" if leg["gen"] else f"k_post<{T},true,2,false>"),
-            0: ("k_sweep (finest-level Jacobi sweep, unfused path)", f"k_sweep<{T},false,false,true>"),
-        }
-        if leg.get("fast"):
-            names[3] = (names[3][0] + " — FAST mode", names[3][1].replace(",2>", ",18>"))
-        roof = []
-        for w, cnt, ms in leg["passes"]:
-            if not cnt or ms <= 0:
-                continue
-            nbytes = leg["bytes"][w]
-            ach = nbytes / (ms * 1e-3) / 1e9
-            name, key = names[w]
-            if pmc is not None:
-                traffic, source = pmc.get(key), pmc_note
-            else:
-                traffic, source = pmc_traffic(args.n, key) if world == 1 else (None, None)
-            roof.append({"bound": "hbm", "kernel": name, "symbol": key, "achieved": round(ach, 2),
-                         "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic,
-                         "traffic_source": source if traffic else None,
-                         "traffic_ratio": round(traffic / nbytes, 4) if traffic else None,
-                         "bytes_per_launch": nbytes, "launches_timed": cnt,
-                         "ms_per_launch": round(ms, 5),
-                         "ms_per_launch_reps": [round(x, 5) for x in leg["passes_reps"][w]]})
-            tr = trace.get(key) if trace is not None and not leg.get("fast") and not leg.get(
-                "stored") else None
-            if tr is not None:
-                tms = tr[2] if tr[2] is not None else tr[1]
-                ach_r = nbytes / (tms * 1e-3) / 1e9
-                roof[-1].update({"ms_per_launch_rocprof": round(tms, 5),
-                                 "ms_per_launch_rocprof_all_launches": round(tr[1], 5),
-                                 "launches_rocprof": tr[0],
-                                 "launches_rocprof_timed": tr[3],
-                                 "frac_rocprof": round(ach_r / HBM_PEAK_GBPS, 4),
-                                 "event_vs_rocprof": round(ms / tms, 4),
-                                 "rocprof_source": trace_note})
-        # the dominant kernel: largest total time over the timed region
-        roof.sort(key=lambda r: -r["ms_per_launch"] * r["launches_timed"])
-        return roof
-
-    def parity_of(leg):
-        p = leg["parity"]
-        if not p or any(x is None for x in p):
-            return None
-        return all(p)
+        return roofline_rows(leg, pmc, pmc_source, trace, trace_note)
 
     if rank == 0:
         med = statistics.median(main_leg["times"])
@@ -935,6 +1120,14 @@ def main():
             # early-exit checks recorded and validated after each call (DESIGN.md §3 point 8)
             "speculative_checks": {"enabled": spec_info[0], "rollbacks": spec_info[1],
                                    "in_stream_level_mask": spec_mask},
+            # the carry (pgmg_ctx.hip "carry"): the timed call starts from the warmup call's
+            # carried pre-smooth and ends with the carry pass (19 k_postpre + 1 carry pass)
+            "carry": {"took_made_dropped": list(main_leg.get("carry", ())),
+                      "what": "calls that started from the previous call's carried pre-smooth, "
+                              "carries made, carries dropped (check could fire), on the clean "
+                              "repetitions' context"},
+            "rccl_ranks": main_leg.get("comm_ranks"),
+            "rccl_floor": rccl_floor,
             "cpu_baseline": cpu,
             "cpu_baseline_config1": cpu1,
             "cpu_baseline_4097": cpu4,
@@ -987,10 +1180,28 @@ def main():
                 "parity": parity_of(gen_leg),
                 "roofline": groof[0] if groof else None,
             }
+        if "rank_split" in main_leg:
+            line["rank_split"] = main_leg["rank_split"]
+        # every fraction physically possible (below the measured copy ceiling) and every
+        # traffic figure from this build: an empty list
+        if GRID["trace"] and world == 1 and args.cycle == "V":
+            fine_bytes = {kernel_key(sym): b for sym, b in main_leg.get("info", {}).values() if sym}
+            line["levels"] = {
+                "what": "per bulk level and pass (rocprofv3 trace + PMC children of this build, "
+                        "all their launches): mean us, algorithmic GB/s, HBM traffic ratio "
+                        "(2 x FETCH_SIZE + WRITE_SIZE over the algorithmic bytes)",
+                "table": levels_table(args.n, GRID, fine_bytes)}
+        line["implausible"] = implausible_fracs(line)
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    if rank == 0 and not line["build_sources"].get("match", False):
+        # a library that does not carry this tree's source hash measured something else
+        print("bench.py: libpgmg.so was not built from this tree's sources "
+              f"({line['build_sources']}): rebuild (make -C "
+              "parallel-geometric-multigrid-for-poisson-problem_amd)", file=sys.stderr)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

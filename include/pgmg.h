@@ -128,6 +128,9 @@ extern "C" {
 #define PGMG_FLAG_NO_CARRY 131072u /* do not carry the next call's pre-smooth across
                                       pgmg_vcycle calls (the carry: below pgmg_vcycle).  Results
                                       and statistics are identical either way */
+#define PGMG_FLAG_TIME_COMM 262144u /* world > 1: hipEvents around every collective group
+                                       (grouped halo exchange, all-to-all, allreduce) on the
+                                       context's stream, read by pgmg_comm_stats */
 #define PGMG_FLAG_HOST_TRANSPORT 2048u /* world > 1 without RCCL: nccl_unique_id points to
                                        a pgmg_host_transport; every message and reduction
                                        is staged through host memory and handed to the
@@ -329,6 +332,15 @@ int pgmg_spec_fire_levels(pgmg_ctx *ctx, unsigned long long *fire);
  * V call. */
 int pgmg_spec_visit_modes(pgmg_ctx *ctx, long long counts[3]);
 
+/* Row strips (world > 1): the collective groups enqueued since the last call and, with
+ * PGMG_FLAG_TIME_COMM, the stream time spent inside them in ms (-1 without the flag; the
+ * transfer plus any wait for a peer, i.e. the part of a rank's cycle not spent computing);
+ * synchronous, resets both.  One GPU: 0 and 0. */
+int pgmg_comm_stats(pgmg_ctx *ctx, long long *groups, double *ms);
+/* The communicator's rank count (RCCL: ncclCommCount; the world for the loopback / host /
+ * null transports; 1 without strips). */
+int pgmg_comm_ranks(pgmg_ctx *ctx, int *ranks);
+
 /* The carry (above pgmg_vcycle): out[0] calls that started from a carried pre-smooth, out[1]
  * carries made, out[2] carries dropped because their check could fire. */
 int pgmg_carry_info(pgmg_ctx *ctx, long long out[3]);
@@ -401,6 +413,13 @@ int pgmg_comm_unique_id(void *out128);
 /* Self-test of the RCCL transport on one GPU (a world-1 communicator): the strip path's
  * grouped send/recv, allreduce(sum, double) and allreduce(min, u32) on a stream; 0 = ok. */
 int pgmg_rccl_selftest(const void *uid128, int device);
+/* Latency floor of the strips' collectives on THIS device: a world-1 RCCL communicator
+ * (unique id uid128) times, over `reps` repetitions after 3 warm ones with hipEvents on one
+ * stream, us[0] one grouped send + recv of 2 rows of 16385 doubles to itself (the finest
+ * level's halo at N = 16385), us[1] an allreduce(sum) of 3 doubles (k_postpre's decision),
+ * us[2] an allreduce(min) of 9 u32 (the speculation marks); mean microseconds per call.  A
+ * lower bound of the per-group cost between ranks (no xGMI hop, no peer to wait for). */
+int pgmg_rccl_latency(const void *uid128, int device, int reps, double *us3);
 
 /* Measurement (libpgmg_ab.so, built with -DPGMG_TUNING; the product library always
  * returns -1): with PGMG_TAIL_PROF=1 in the environment, the LDS tail accumulates shader-

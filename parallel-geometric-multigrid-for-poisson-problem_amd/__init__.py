@@ -22,7 +22,7 @@ from ._capi import (PGMG_FLAG_LOOPBACK, PGMG_FLAG_NO_CROSS, PGMG_FLAG_NO_GRAPH,
                     PGMG_FLAG_TIME_FINE, PGMG_PRECISION_FP32, PGMG_PRECISION_FP64,
                     PGMG_FLAG_UNFUSED, PGMG_FLAG_NO_RECOMPUTE, PGMG_FLAG_NO_PIN,
                     PGMG_FLAG_NO_R2, PGMG_FLAG_HOST_TRANSPORT, PGMG_FLAG_FAST,
-                    PGMG_FLAG_NO_SPEC_FIRE, PGMG_FLAG_NO_CTILE, PGMG_FLAG_NO_CARRY,
+                    PGMG_FLAG_NO_SPEC_FIRE, PGMG_FLAG_NO_CTILE, PGMG_FLAG_NO_CARRY, PGMG_FLAG_TIME_COMM,
                     PGMG_PROLONG_REFERENCE,
                     PGMG_PROLONG_SYMMETRIC, PGMG_OK, PGMG_ERR_STATE, PgmgConfig, PgmgError,
                     check, load)
@@ -32,10 +32,10 @@ PKG_DIR = pathlib.Path(__file__).resolve().parent
 __all__ = [
     "build", "load", "Solver", "PgmgConfig", "PgmgError", "ops", "config_overrides",
     "PGMG_FLAG_NO_GRAPH", "PGMG_FLAG_TIME_FINE", "PGMG_FLAG_UNFUSED", "PGMG_FLAG_LOOPBACK", "PGMG_FLAG_NO_CROSS",
-    "PGMG_PROLONG_REFERENCE", "plan_strips", "LoopbackHub", "unique_id",
+    "PGMG_PROLONG_REFERENCE", "plan_strips", "LoopbackHub", "unique_id", "rccl_latency",
     "PGMG_PROLONG_SYMMETRIC", "PGMG_PRECISION_FP64", "PGMG_PRECISION_FP32",
     "PGMG_FLAG_STORED_RHS", "PGMG_FLAG_EXACT_DIST", "PGMG_FLAG_SOLO",
-    "PGMG_FLAG_NO_RECOMPUTE", "PGMG_FLAG_NO_PIN", "PGMG_FLAG_NO_R2", "PGMG_FLAG_FAST", "PGMG_FLAG_NO_SPEC_FIRE", "PGMG_FLAG_NO_CTILE", "PGMG_FLAG_NO_CARRY",
+    "PGMG_FLAG_NO_RECOMPUTE", "PGMG_FLAG_NO_PIN", "PGMG_FLAG_NO_R2", "PGMG_FLAG_FAST", "PGMG_FLAG_NO_SPEC_FIRE", "PGMG_FLAG_NO_CTILE", "PGMG_FLAG_NO_CARRY", "PGMG_FLAG_TIME_COMM",
     "PGMG_FLAG_HOST_TRANSPORT", "HostTransport", "DeviceGrid",
 ]
 
@@ -101,6 +101,15 @@ def unique_id():
     buf = (C.c_ubyte * 128)()
     check(load().pgmg_comm_unique_id(buf), "pgmg_comm_unique_id")
     return bytes(buf)
+
+
+def rccl_latency(device=0, reps=200):
+    """Latency floor of the strips' collectives on this device (world-1 RCCL communicator):
+    {"halo_group_us", "allreduce_sum_us", "allreduce_min_us"} (pgmg_rccl_latency)."""
+    us = (C.c_double * 3)()
+    uid = (C.c_ubyte * 128).from_buffer_copy(unique_id())
+    check(load().pgmg_rccl_latency(uid, int(device), int(reps), us), "pgmg_rccl_latency")
+    return {"halo_group_us": us[0], "allreduce_sum_us": us[1], "allreduce_min_us": us[2]}
 
 
 from .hostcomm import HostTransport  # noqa: E402
@@ -306,6 +315,19 @@ class Solver:
         a = (C.c_longlong * 3)()
         check(self.lib.pgmg_carry_info(self.h, a), "pgmg_carry_info")
         return tuple(a)
+
+    def comm_stats(self):
+        """(collective groups since the last call, ms inside them with PGMG_FLAG_TIME_COMM else
+        -1); synchronous, resets."""
+        g, m = C.c_longlong(), C.c_double()
+        check(self.lib.pgmg_comm_stats(self.h, C.byref(g), C.byref(m)), "pgmg_comm_stats")
+        return g.value, m.value
+
+    def comm_ranks(self):
+        """Ranks of the communicator (RCCL: ncclCommCount); 1 without strips."""
+        n = C.c_int()
+        check(self.lib.pgmg_comm_ranks(self.h, C.byref(n)), "pgmg_comm_ranks")
+        return n.value
 
     def set_eps(self, eps):
         """A new early-exit threshold for the following calls (drops the carry)."""

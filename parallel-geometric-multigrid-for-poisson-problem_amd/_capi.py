@@ -39,6 +39,7 @@ PGMG_FLAG_NO_SPEC_FIRE = 32768
 PGMG_FLAGS_RETIRED = 8192 | 16384
 PGMG_FLAG_NO_CTILE = 65536
 PGMG_FLAG_NO_CARRY = 131072
+PGMG_FLAG_TIME_COMM = 262144
 
 PGMG_PRECISION_FP64 = 0
 PGMG_PRECISION_FP32 = 1
@@ -126,6 +127,8 @@ SIGNATURES = [
     ("pgmg_spec_fire_levels", C.c_int, [_P, C.POINTER(C.c_ulonglong)]),
     ("pgmg_spec_visit_modes", C.c_int, [_P, C.POINTER(C.c_longlong)]),
     ("pgmg_carry_info", C.c_int, [_P, C.POINTER(C.c_longlong)]),
+    ("pgmg_comm_stats", C.c_int, [_P, C.POINTER(C.c_longlong), _DP]),
+    ("pgmg_comm_ranks", C.c_int, [_P, C.POINTER(C.c_int)]),
     ("pgmg_set_eps", C.c_int, [_P, C.c_double]),
     ("pgmg_bench_sweep", C.c_int, [_P, C.c_int, _DP]),
     ("pgmg_jacobi", C.c_int, [_P, _P, _P, C.c_int, C.c_int, C.c_double, C.c_int, C.c_double,
@@ -146,6 +149,7 @@ SIGNATURES = [
     ("pgmg_device_count", C.c_int, [C.POINTER(C.c_int)]),
     ("pgmg_comm_unique_id", C.c_int, [_P]),
     ("pgmg_rccl_selftest", C.c_int, [_P, C.c_int]),
+    ("pgmg_rccl_latency", C.c_int, [_P, C.c_int, C.c_int, _DP]),
     ("pgmg_tail_prof", C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
     ("pgmg_loopback_create", C.c_int, [C.c_int, C.POINTER(_P)]),
     ("pgmg_loopback_destroy", C.c_int, [_P]),

@@ -55,7 +55,11 @@ constexpr int kMinRows = 16;  // thinnest strip a distributed level may have
 // ---------------------------------------------------------------------------
 class Transport {
   public:
+    // what the next group / allreduce is (StripComm sets it): named by a stall message
+    std::string label;
+    long long ngroups = 0;       // groups and allreduces enqueued (the stall message's index)
     virtual ~Transport() {}
+    virtual int ranks(int *n) { return *n = -1, PGMG_OK; }
     virtual int group_start() = 0;
     virtual int send(const void *buf, size_t bytes, int peer, hipStream_t s) = 0;
     virtual int recv(void *buf, size_t bytes, int peer, hipStream_t s) = 0;
@@ -78,6 +82,7 @@ class RcclTransport : public Transport {
     // the time behind a long queue of healthy work
     static constexpr int kRing = 64;
     hipEvent_t ring[kRing] = {};
+    std::string ring_label[kRing];
     long long rec = 0, done = 0;
     ~RcclTransport() override
     {
@@ -96,6 +101,7 @@ class RcclTransport : public Transport {
         if (!ring[0])
             for (hipEvent_t &e : ring) PGMG_HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         PGMG_HIPC(hipEventRecord(ring[rec % kRing], s));
+        ring_label[rec % kRing] = "group #" + std::to_string(ngroups) + ": " + label;
         ++rec;
         if (rec - done > kRing) done = rec - kRing;   // older marks were overwritten
         return PGMG_OK;
@@ -126,8 +132,10 @@ class RcclTransport : public Transport {
             if (progressed) t0 = std::chrono::steady_clock::now();
             const double dt =
                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-            if (dt > timeout_s)
-                return abort_with("RCCL wait: no progress for pgmg_config.comm_timeout_s");
+            if (dt > timeout_s)   // name the first group that has not completed
+                return abort_with("RCCL wait: no progress for pgmg_config.comm_timeout_s (" +
+                                  std::to_string(timeout_s) + " s); stalled at " +
+                                  (done < rec ? ring_label[done % kRing] : std::string("the stream's tail")));
             if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
         }
     }
@@ -142,6 +150,12 @@ class RcclTransport : public Transport {
     {
         if (!comm) return set_err(PGMG_ERR_COMM, "communicator aborted by an earlier error");
         NCCLC(ncclGroupStart());
+        return PGMG_OK;
+    }
+    int ranks(int *n) override
+    {
+        if (!comm) return set_err(PGMG_ERR_COMM, "communicator aborted by an earlier error");
+        NCCLC(ncclCommCount(comm, n));
         return PGMG_OK;
     }
     int send(const void *buf, size_t bytes, int peer, hipStream_t s) override
@@ -457,7 +471,67 @@ class StripComm : public Comm {
     Level pend_L;
     int pend_depth = 0;
 
-    ~StripComm() override { delete t; }
+    // PGMG_FLAG_TIME_COMM: events around every collective group on the stream (comm_stats)
+    bool timing = false;
+    std::vector<hipEvent_t> tev;   // start / end pairs
+    int tused = 0;
+    long long groups = 0;
+
+    ~StripComm() override
+    {
+        for (hipEvent_t e : tev)
+            if (e) (void)hipEventDestroy(e);
+        delete t;
+    }
+    // every collective of the strips goes through here: labelled (a stall message names it),
+    // counted and, when timing, bracketed by events
+    template <class F>
+    int collective(hipStream_t s, const std::string &what, F &&f)
+    {
+        t->label = what;
+        int i0 = -1;
+        if (timing) {
+            if (tev.empty()) {
+                tev.assign(2 * 4096, nullptr);
+                for (hipEvent_t &e : tev) PGMG_HIPC(hipEventCreate(&e));
+            }
+            if (tused + 2 <= (int)tev.size()) {
+                i0 = tused;
+                PGMG_HIPC(hipEventRecord(tev[i0], s));
+            }
+        }
+        const int e = f();
+        if (i0 >= 0) {
+            PGMG_HIPC(hipEventRecord(tev[i0 + 1], s));
+            tused = i0 + 2;
+        }
+        ++groups;
+        ++t->ngroups;
+        return e;
+    }
+    int comm_stats(hipStream_t s, long long *ng, double *ms) override
+    {
+        const int e = t->wait(s);
+        if (e) return e;
+        double tot = 0.0;
+        for (int i = 0; i + 1 < tused; i += 2) {
+            float f = 0.f;
+            PGMG_HIPC(hipEventElapsedTime(&f, tev[i], tev[i + 1]));
+            tot += f;
+        }
+        if (ng) *ng = groups;
+        if (ms) *ms = timing ? tot : -1.0;
+        groups = 0;
+        tused = 0;
+        return PGMG_OK;
+    }
+    int comm_ranks(int *n) override
+    {
+        int r = -1;
+        const int e = t->ranks(&r);
+        *n = r > 0 ? r : world;
+        return e;
+    }
     int gathered_level() const override { return Ld; }
     int rank() const override { return me; }
 
@@ -567,17 +641,24 @@ class StripComm : public Comm {
 
     int halos_on(Transport *tp, const HaloReq *reqs, int n, hipStream_t s)
     {
-        int e = tp->group_start();
-        if (e) return e;
-        for (int k = 0; k < n && !e; ++k) e = post_halo(tp, reqs[k], s);
-        const int e2 = tp->group_end(s);   // the group is closed even after a failed call
-        return e ? e : e2;
+        std::string what = "halo exchange";
+        for (int k = 0; k < n; ++k)
+            what += (k ? ", " : " of ") + std::string("level N=") + std::to_string(reqs[k].L->N) +
+                    " (" + std::to_string(reqs[k].depth) + " rows)";
+        return collective(s, what, [&]() {
+            int e = tp->group_start();
+            if (e) return e;
+            for (int k = 0; k < n && !e; ++k) e = post_halo(tp, reqs[k], s);
+            const int e2 = tp->group_end(s);   // the group is closed even after a failed call
+            return e ? e : e2;
+        });
     }
 
     int allreduce_sum(double *d, int n, hipStream_t s) override
     {
         const int e = flush(s);
-        return e ? e : t->allreduce_sum(d, n, s);
+        return e ? e : collective(s, "allreduce(sum) of " + std::to_string(n) + " doubles",
+                                  [&]() { return t->allreduce_sum(d, n, s); });
     }
     int wait(hipStream_t s) override
     {
@@ -587,10 +668,17 @@ class StripComm : public Comm {
     int allreduce_min_u32(unsigned *d, int n, hipStream_t s) override
     {
         const int e = flush(s);
-        return e ? e : t->allreduce_min_u32(d, n, s);
+        return e ? e : collective(s, "allreduce(min) of " + std::to_string(n) + " u32",
+                                  [&]() { return t->allreduce_min_u32(d, n, s); });
     }
 
     int allgather_rows(pgmg_ctx *c, int l, const Grid &g) override
+    {
+        return collective(c->s, "all-to-all rows of gathered level N=" + std::to_string(c->lv[l].N) +
+                                    (pending ? " (+ the finest level's halo)" : ""),
+                          [&]() { return allgather_rows_group(c, l, g); });
+    }
+    int allgather_rows_group(pgmg_ctx *c, int l, const Grid &g)
     {
         Level &L = c->lv[l];
         const size_t row = (size_t)L.P * L.es;
@@ -671,6 +759,7 @@ Comm *Comm::create(pgmg_ctx *c, int *rc)
         auto *sc = new StripComm();
         sc->me = cfg.rank;
         sc->world = cfg.world;
+        sc->timing = (cfg.flags & PGMG_FLAG_TIME_COMM) != 0;
         sc->t = new NullTransport();
         return sc;
     }
@@ -686,6 +775,7 @@ Comm *Comm::create(pgmg_ctx *c, int *rc)
     auto *sc = new StripComm();
     sc->me = cfg.rank;
     sc->world = cfg.world;
+    sc->timing = (cfg.flags & PGMG_FLAG_TIME_COMM) != 0;
     if (cfg.flags & PGMG_FLAG_HOST_TRANSPORT) {
         auto *ht = (const pgmg_host_transport *)cfg.nccl_unique_id;
         if (!ht->exchange || !ht->allreduce_sum_f64 || !ht->allreduce_min_u32) {
@@ -793,6 +883,56 @@ int pgmg_rccl_selftest(const void *uid128, int device)
     (void)hipFree(b);
     (void)hipFree(u);
     if (c2) (void)hipFree(c2);
+    (void)hipStreamDestroy(s);
+    return rc;
+}
+
+// Latency floor of the strips' collectives (world-1 communicator on this device): the three
+// kinds of group a V-cycle on row strips enqueues, each timed over `reps` calls with events
+int pgmg_rccl_latency(const void *uid128, int device, int reps, double *us3)
+{
+    if (!uid128 || !us3 || reps < 1) return pgmg::set_err(PGMG_ERR_ARG, "bad argument");
+    if (hipSetDevice(device) != hipSuccess) return pgmg::set_err(PGMG_ERR_HIP, "hipSetDevice");
+    pgmg::RcclTransport t;
+    int rc = t.init(uid128, 1, 0);
+    if (rc) return rc;
+    hipStream_t s = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)
+        return pgmg::set_err(PGMG_ERR_HIP, "latency: stream / events");
+    const size_t halo = 2 * 16385 * sizeof(double);
+    char *a = nullptr, *b = nullptr;
+    if (hipMalloc(&a, halo) != hipSuccess || hipMalloc(&b, halo) != hipSuccess)
+        rc = pgmg::set_err(PGMG_ERR_NOMEM, "latency buffers");
+    if (!rc && (hipMemset(a, 0, halo) != hipSuccess || hipMemset(b, 0, halo) != hipSuccess))
+        rc = pgmg::set_err(PGMG_ERR_HIP, "latency: memset");
+    for (int kind = 0; kind < 3 && !rc; ++kind) {
+        auto one = [&]() -> int {
+            if (kind == 0) {
+                int e = t.group_start();
+                if (!e) e = t.send(a, halo, 0, s);
+                if (!e) e = t.recv(b, halo, 0, s);
+                const int e2 = t.group_end(s);
+                return e ? e : e2;
+            }
+            if (kind == 1) return t.allreduce_sum(reinterpret_cast<double *>(a), 3, s);
+            return t.allreduce_min_u32(reinterpret_cast<unsigned *>(b), 9, s);
+        };
+        for (int i = 0; i < 3 && !rc; ++i) rc = one();
+        if (!rc) rc = t.wait(s);
+        if (!rc && hipEventRecord(e0, s) != hipSuccess) rc = pgmg::set_err(PGMG_ERR_HIP, "event");
+        for (int i = 0; i < reps && !rc; ++i) rc = one();
+        if (!rc && hipEventRecord(e1, s) != hipSuccess) rc = pgmg::set_err(PGMG_ERR_HIP, "event");
+        if (!rc) rc = t.wait(s);
+        float ms = 0.f;
+        if (!rc && hipEventElapsedTime(&ms, e0, e1) != hipSuccess) rc = pgmg::set_err(PGMG_ERR_HIP, "elapsed");
+        if (!rc) us3[kind] = 1e3 * ms / reps;
+    }
+    if (a) (void)hipFree(a);
+    if (b) (void)hipFree(b);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
     (void)hipStreamDestroy(s);
     return rc;
 }

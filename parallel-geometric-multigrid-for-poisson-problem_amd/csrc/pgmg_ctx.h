@@ -250,6 +250,12 @@ class Comm {
     // error state is polled while waiting, and after cfg.comm_timeout_s the communicator is
     // aborted; PGMG_ERR_COMM then
     virtual int wait(hipStream_t s) = 0;
+    // collective groups (grouped exchanges and allreduces) enqueued since the last call and,
+    // with PGMG_FLAG_TIME_COMM, the stream time spent inside them (events around each group:
+    // the transfer plus any wait for a peer), else ms = -1; synchronous, resets both
+    virtual int comm_stats(hipStream_t s, long long *groups, double *ms) = 0;
+    // ranks of the communicator (RCCL: ncclCommCount), the world for the other transports
+    virtual int comm_ranks(int *n) = 0;
     static Comm *create(pgmg_ctx *c, int *rc);
 };
 

@@ -2176,6 +2176,25 @@ static int run_cycles(pgmg_ctx *c, int ncycles, int gamma)
     return e;
 }
 
+int pgmg_comm_stats(pgmg_ctx *c, long long *groups, double *ms)
+{
+    if (!c) return set_err(PGMG_ERR_ARG, "null ctx");
+    if (!c->comm) {
+        PGMG_TRY(stream_wait(c));
+        if (groups) *groups = 0;
+        if (ms) *ms = 0.0;
+        return PGMG_OK;
+    }
+    return c->comm->comm_stats(c->s, groups, ms);
+}
+
+int pgmg_comm_ranks(pgmg_ctx *c, int *ranks)
+{
+    if (!c || !ranks) return set_err(PGMG_ERR_ARG, "null argument");
+    if (!c->comm) return *ranks = 1, PGMG_OK;
+    return c->comm->comm_ranks(ranks);
+}
+
 int pgmg_carry_info(pgmg_ctx *c, long long out[3])
 {
     if (!c || !out) return set_err(PGMG_ERR_ARG, "null argument");

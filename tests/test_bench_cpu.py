@@ -81,9 +81,9 @@ def test_op_cases_build_and_match_kernel_names():
 
     cases, keep = bench.op_cases(PG(), 33, device="cpu")
     assert len(cases) == 8 and len(keep) == 6
-    for _, call, nbytes, keys, sweeps in cases:
+    for _, call, nbytes, keys, sweeps, passes in cases:
         call()
-        assert nbytes > 0 and callable(keys)
+        assert nbytes > 0 and callable(keys) and 1 <= passes <= max(1, sweeps)
     names = {
         0: "k_op_sweep_ip<16,true,true>", 1: "k_op_sweep2_ip<8,true,true>",
         2: "k_op_sweep2_ip<8,true,true>", 3: "k_op_sweep<16,true,false,true>",
@@ -94,3 +94,79 @@ def test_op_cases_build_and_match_kernel_names():
     assert not cases[0][3]("k_op_sweep2_ip<8,true,true>")
     assert not cases[1][3]("k_op_sweep_ip<16,true,true>")
     assert cases[2][3]("k_op_sweep_ip<16,true,true>")
+    # the in-place passes' deferred-edge scatter is part of their cost (ADVICE r05)
+    for i in (0, 1, 2):
+        assert cases[i][3]("k_op_defer_scatter")
+    assert not cases[3][3]("k_op_defer_scatter")
+
+
+def _bench():
+    import importlib
+    sys.path.insert(0, str(ROOT))
+    return importlib.import_module("bench")
+
+
+def test_fractions_physical_on_a_stub_line():
+    """The roofline rows and the per-op rows bench.py prints, built from stub measurements
+    shaped like a real N = 16385 run (the library's pass info, a trace and live PMC of this
+    build): every frac* field at or below the copy ceiling (0.79), the paired sweep's rate
+    only as sweep_equiv_frac, every traffic_source naming this build; and the checker flags a
+    mis-charged kernel and a traffic figure from another build (VERDICT r05 next #2)."""
+    bench = _bench()
+    n = 16383.0 ** 2
+    build = "live rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this build; libpgmg.so sha256:0123456789abcdef"
+    key = "k_postpre_lds<double,false,true,2>"
+    leg = {"passes": [(1, 0, 0.0), (3, 19, 1.02), (4, 1, 1.45)],
+           "passes_reps": {1: [], 3: [1.03, 1.02, 1.02], 4: [1.45, 1.45, 1.45]},
+           "info": {3: ("pgmg::k_postpre_lds<double, false, true, 2>", 16 * n + 16 * n / 4),
+                    4: ("pgmg::k_postpre_lds<double, false, true, 130>", 24 * n + 16 * n / 4)},
+           "bytes": {1: 16 * n, 3: 16 * n, 4: 24 * n}, "gen": True}
+    pmc = {key: 1.078 * (16 * n + 16 * n / 4)}
+    trace = {key: (95, 1.06, 1.036, 19)}
+    rows = bench.roofline_rows(leg, pmc, build, trace, "trace")
+    assert [r["symbol"] for r in rows] == [key, "k_postpre_lds<double,false,true,130>"]
+    assert rows[0]["traffic_ratio"] == 1.078 and rows[1]["traffic"] is None
+    ops = []
+    for name, nbytes, sweeps, passes, ms in (("v=1", 48 * n, 2, 1, 1.38), ("v=100", 2424 * n, 101, 51, 70.6),
+                                             ("residual", 24 * n, 0, 1, 1.35)):
+        ops.append(bench.op_row(name, nbytes, lambda k: k.startswith("k_op"), sweeps, passes, ms,
+                                {"k_op_sweep2_ip<8,true,true,256>": (153, 1.32, None, None)},
+                                {"k_op_sweep2_ip<8,true,true,256>": 1.05 * 24 * n}, build))
+    assert ops[0]["sweep_equiv_frac"] > 1.0 and ops[0]["frac"] < 0.79
+    line = {"roofline": rows[0], "roofline_other": rows[1:], "ops": {"table": ops}}
+    assert bench.implausible_fracs(line) == []
+    bad = {"roofline": dict(rows[0], frac=0.9158),
+           "x": {"traffic_source": "profiles/pmc_fine.json (another build: unrecorded)"}}
+    found = bench.implausible_fracs(bad)
+    assert len(found) == 2, found
+
+
+def test_rank_split_summary():
+    """--gpus N's per-rank compute / RCCL split (VERDICT r05 next #3): compute = device time
+    minus the time inside collective groups, median and max over ranks."""
+    bench = _bench()
+    allr = [(0.40, 0.05, 11.0), (0.42, 0.09, 11.0), (0.41, 0.02, 11.0), (0.45, 0.10, 11.0)]
+    d = bench.rank_split_summary(allr, 0.0085, 20)
+    assert d["compute_ms"]["per_rank"] == [0.35, 0.33, 0.39, 0.35]
+    assert d["compute_ms"]["max"] == 0.39 and d["rccl_ms"]["max"] == 0.1
+    assert d["rccl_ms"]["median"] == 0.07 and d["groups_per_cycle"] == 11.0
+    assert d["instrumented_ms_per_step"] == 0.425
+
+
+def test_levels_table_maps_launch_grids():
+    """The levels table tells the coarse levels apart by their launch grid (fused_grid, the
+    restated fused_geometry) and charges each pass its algorithmic bytes."""
+    bench = _bench()
+    g8193, g4097 = bench.fused_grid(8193), bench.fused_grid(4097)
+    assert g8193 != g4097
+    grid = {"trace": {("k_pre<double,true,false,2>", g8193): [145000, 147000],
+                      ("k_post<double,false,2,true>", g8193): [251000],
+                      ("k_postpre_lds<double,false,true,2>", 123): [1020000] * 19,
+                      ("k_op_residual<16>", 5): [1300000]},
+            "pmc": {("k_pre<double,true,false,2>", g8193): {"FETCH_SIZE": [330000.0], "WRITE_SIZE": [33000.0]}}}
+    rows = bench.levels_table(16385, grid, {"k_postpre_lds<double,false,true,2>": 5.37e9})
+    assert [(r["N"], r["pass"]) for r in rows] == [(16385, "k_postpre_lds"), (8193, "k_post"), (8193, "k_pre")]
+    pre = rows[2]
+    alg = 8 * 8191.0 ** 2 + 8 * 4095.0 ** 2
+    assert pre["us"] == 146.0 and pre["alg_gbps"] == round(alg / 146.0 * 1e-3, 1)
+    assert pre["traffic_ratio"] == round((2 * 330000 + 33000) * 1024 / alg, 3)

@@ -32,7 +32,8 @@ SEQ = [("v", 1), ("res", None), ("v", 1), ("sol", None), ("v", 1), ("res", None)
        ("set", None), ("v", 1), ("v", 1), ("res", None), ("v", 1), ("eps", 1e-6), ("v", 1),
        ("sol", None), ("v", 1), ("f", 1), ("v", 1), ("res", None), ("v", 1), ("eps", EPS),
        ("v", 2), ("w", 1), ("v", 1), ("v", 1), ("sol", None), ("set", None), ("v", 1),
-       ("res", None), ("v", 1), ("v", 1), ("f", 1), ("v", 1), ("v", 1), ("hash", None), ("v", 1)]
+       ("res", None), ("v", 1), ("v", 1), ("f", 1), ("v", 1), ("v", 1), ("hash", None), ("v", 1),
+       ("res", None), ("v", 1), ("sol", None), ("v", 2), ("v", 1)]
 
 
 def _golden(golden_cycles, N):
