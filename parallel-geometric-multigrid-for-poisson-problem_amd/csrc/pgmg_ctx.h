@@ -196,7 +196,8 @@ struct pgmg_ctx {
 
 namespace pgmg {
 
-int alloc_grid(Grid &g, const Level &L);
+// stagger: the origin shifted by this many bytes (a multiple of 128) past the usual one
+int alloc_grid(Grid &g, const Level &L, size_t stagger = 0);
 void free_grid(Grid &g);
 // dispatch on the context's element type
 int enqueue_cycle(pgmg_ctx *c, int l, int gamma, bool x0_zero);

@@ -128,13 +128,13 @@ int pgmg::check_span(const void *o, long long P, int es, long long r0, long long
     return set_err(PGMG_ERR_STATE, buf);
 }
 
-int pgmg::alloc_grid(Grid &g, const Level &L)
+int pgmg::alloc_grid(Grid &g, const Level &L, size_t stagger)
 {
     // owned rows + kHalo halo rows each side (the fused passes read 4 rows past a
     // segment); the slack covers the last wave tile reading past the row end
     const int rows = (L.hi - L.lo) + 2 * kHalo;
     // column 1 of every row on a 128-byte boundary: 128/es - 1 elements before (0,0)
-    const size_t off = (size_t)(128 / L.es - 1);
+    const size_t off = (size_t)(128 / L.es - 1) + (stagger / 128) * (128 / L.es);
     const size_t n = off + (size_t)rows * L.P + 512;
     void *p = nullptr;
     if (hipMalloc(&p, n * L.es) != hipSuccess)
@@ -756,6 +756,9 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
     // the carry: taken (this call starts from Y and lv[1].F) / made (it ends with the carry
     // pass); both only on speculative calls on the context's own grids, one GPU
     const bool take = c->carry_use && lean && !dist && Y != nullptr && c->x_in == nullptr;
+    if (tuning_int("PGMG_ROLE_TRACE", 0))   // measurement build: which grids play which role
+        fprintf(stderr, "roles A %p B %p S %p Y %p n %d take %d\n", gA.base, gB.base, gS.base, gY.base, n,
+                (int)(c->carry_use && lean && Y != nullptr));
     const bool make = c->carry_make && lean && !dist && Y != nullptr && xout == nullptr &&
                       !c->defer_post;
     c->carry_use = false;
@@ -1163,9 +1166,11 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
     for (int l = 0; l < (int)c->lv.size() && rc == PGMG_OK; ++l) {
         Level &L = c->lv[l];
         if (!L.on_this_rank) continue;
-        rc = alloc_grid(L.A, L);
-        if (rc == PGMG_OK) rc = alloc_grid(L.F, L);
-        if (rc == PGMG_OK && l < c->nb) rc = alloc_grid(L.B, L);
+        // (measurement build: PGMG_GRID_STAGGER bytes times a per-grid index of level 0)
+        const size_t st = l == 0 ? (size_t)tuning_int("PGMG_GRID_STAGGER", 0) : 0;
+        rc = alloc_grid(L.A, L, 0 * st);
+        if (rc == PGMG_OK) rc = alloc_grid(L.F, L, 1 * st);
+        if (rc == PGMG_OK && l < c->nb) rc = alloc_grid(L.B, L, 2 * st);
     }
     c->fused = cfg->v1 == 1 && cfg->v2 == 1 && !(cfg->flags & PGMG_FLAG_UNFUSED);
     c->recompute = !(cfg->flags & PGMG_FLAG_NO_RECOMPUTE);
@@ -1196,10 +1201,11 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
             if (nbk > maxblocks) maxblocks = nbk;
         }
     }
-    if (rc == PGMG_OK && c->cross) rc = alloc_grid(c->S, c->lv[0]);
+    const size_t st0 = (size_t)tuning_int("PGMG_GRID_STAGGER", 0);
+    if (rc == PGMG_OK && c->cross) rc = alloc_grid(c->S, c->lv[0], 3 * st0);
     // the carry's fourth level-0 grid (one GPU; see "carry"): ~2.15 GB at N = 16385 fp64
     if (rc == PGMG_OK && c->cross && c->comm == nullptr && !(cfg->flags & PGMG_FLAG_NO_CARRY))
-        rc = alloc_grid(c->Y, c->lv[0]);
+        rc = alloc_grid(c->Y, c->lv[0], 4 * st0);
     // partial sums of k_postpre's second and third checks (cross-cycle fusion, and the
     // F-cycle's fused smooth(3)), its decision flags
     if (rc == PGMG_OK && (hipMalloc((void **)&c->partials2, sizeof(double) * maxblocks) != hipSuccess ||

@@ -1,7 +1,7 @@
 #!/bin/bash
 # r06 GPU session: the carry's tests first (verbose), smoke(), the whole GPU suite, then the
 # driver-shaped bench line.  bash scripts/r06_session.sh OUT [STEPS...]
-# STEPS (default: carry smoke tests bench): any of carry smoke tests bench solo2 solo8 host2 carry_ab levels
+# STEPS (default: carry smoke tests bench): any of carry smoke tests bench solo2 solo8 host2 carry_ab stagger levels
 # Each GPU step runs under its own time limit; a time limit (124/137), an abort (134) or a
 # fault (139) ends the session.
 set -u
@@ -32,6 +32,7 @@ for s in ${STEPS}; do
     solo2) step solo2 300 env PGMG_BENCH_SOLO=1 python bench.py --gpus 2 --warmup 2 --steps 10 --reps 2 ;;
     solo8) step solo8 400 env PGMG_BENCH_SOLO=1 python bench.py --gpus 8 --warmup 2 --steps 10 --reps 2 ;;
     host2) step host2 400 env PGMG_BENCH_TRANSPORT=host python bench.py --gpus 2 --warmup 2 --steps 5 --reps 2 ;;
+    stagger) step stagger 600 env PGMG_LIB=$PWD/parallel-geometric-multigrid-for-poisson-problem_amd/libpgmg_probe.so python scripts/stagger_probe.py --staggers ${STAGGERS:-0,4096,65536,1048576} ;;
     carry_ab) step carry_ab 400 python scripts/carry_ab.py --rounds 3 ;;
     levels) step levels 300 python scripts/level_pmc.py run --n 16385 --out ${OUT}/levels ;;
     *) echo "unknown step ${s}" >&2 ;;

@@ -120,7 +120,7 @@ def test_carry_interleaved_api_sequence(pgmg, oracle_mod, golden_cycles, plan, N
     assert calls >= 30
     took, made, dropped = info
     assert took >= 10 and made >= took, info
-    assert gold >= 3, gold
+    assert gold >= 2, gold
 
 
 def test_carry_off_gives_the_same_words(pgmg, plan):
