@@ -1,1 +1,1 @@
-extern "C" const char *pgmg_source_hash(void) { return "asan-e2100b8b7f5440bc"; }
+extern "C" const char *pgmg_source_hash(void) { return "asan-7cbcc07a982fff9a"; }

@@ -2056,7 +2056,8 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
         // carry pass (enqueue_cross_cycles, "carry"); c->carry_use was set by run_cycles for
         // the first segment
         c->carry_make = last && gamma == 1 && ext_out == nullptr &&
-                        !(c->cfg.flags & PGMG_FLAG_NO_CARRY);
+                        !(c->cfg.flags & PGMG_FLAG_NO_CARRY) &&
+                        tuning_int("PGMG_CARRY_MAKE", 1) != 0;   // (measurement build: 0 never makes)
         c->carry_chk = -1;
         e = run_cycles_plain(c, seg, gamma, first);
         c->defer_post = false;
@@ -2174,7 +2175,8 @@ static int run_cycles(pgmg_ctx *c, int ncycles, int gamma)
     if (ncycles <= 0) return PGMG_OK;
     // the carry is this call's to take (a V call on the context's own problem: the first
     // speculative segment starts from it) or gone; a call that runs in-stream drops it
-    c->carry_use = c->carry && gamma == 1 && c->ext_phi == nullptr;
+    c->carry_use = c->carry && gamma == 1 && c->ext_phi == nullptr &&
+                   tuning_int("PGMG_CARRY_TAKE", 1) != 0;   // (measurement build: 0 never takes)
     c->carry = false;
     c->carry_took = false;
     const int e = c->ext_phi ? run_cycles_ext(c, ncycles, gamma) : run_cycles_core(c, ncycles, gamma);

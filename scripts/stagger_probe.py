@@ -42,7 +42,8 @@ def child(a):
                 dt = time.perf_counter() - t0
                 pp = s.fine_pass_time(3)
                 cp = s.fine_pass_time(4)
-                print(json.dumps({"stagger": int(os.environ.get("PGMG_GRID_STAGGER", "0")),
+                print(json.dumps({"variant": os.environ.get("PROBE_VARIANT", ""),
+                                  "stagger": int(os.environ.get("PGMG_GRID_STAGGER", "0")),
                                   "carry": carry, "rep": r, "ms_per_cycle": round(dt * 50, 4),
                                   "k_postpre_ms": round(pp[1], 4), "n": pp[0],
                                   "carry_pass_ms": round(cp[1], 4),
@@ -54,17 +55,27 @@ def main():
     ap.add_argument("--n", type=int, default=16385)
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--staggers", default="0,4096,65536")
+    ap.add_argument("--variants", default="",
+                    help="NAME:ENV=VAL+ENV=VAL,... (instead of --staggers): the measurement "
+                         "build's environment knobs per variant")
     ap.add_argument("--child", action="store_true")
     a = ap.parse_args()
     if a.child:
         return child(a)
-    for st in a.staggers.split(","):
-        env = dict(os.environ, PGMG_GRID_STAGGER=st, PGMG_ROLE_TRACE="1")
+    specs = ([(f"stagger{st}", {"PGMG_GRID_STAGGER": st}) for st in a.staggers.split(",")]
+             if not a.variants else
+             [(v.split(":")[0], dict(kv.split("=") for kv in v.split(":")[1].split("+") if kv))
+              for v in a.variants.split(",")])
+    for name, extra in specs:
+        st = extra.get("PGMG_GRID_STAGGER", "0")
+        env = dict(os.environ, PGMG_ROLE_TRACE="1", PROBE_VARIANT=name, **extra)
         r = subprocess.run([sys.executable, __file__, "--child", "--n", str(a.n), "--reps", str(a.reps)],
                            env=env, capture_output=True, text=True, timeout=600)
         print(r.stdout, end="", flush=True)
         roles = [l for l in r.stderr.splitlines() if l.startswith("roles") or l.startswith("REP")]
-        print(json.dumps({"stagger": int(st), "rc": r.returncode, "roles": roles[-60:]}), flush=True)
+        print(json.dumps({"variant": name, "stagger": int(st), "rc": r.returncode,
+                          "roles": roles[-60:], "stderr": r.stderr[-1500:] if r.returncode else ""}),
+              flush=True)
 
 
 if __name__ == "__main__":
