@@ -1163,6 +1163,18 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         }
     }
 
+    // (measurement build: PGMG_Y_ORDER 1 allocates the carry grid before every level grid,
+    // PGMG_DUMMY_MB a dummy buffer of that size there: placement probes)
+    const bool want_y = cfg->world <= 1 && !(cfg->flags & PGMG_FLAG_NO_CARRY);
+    const int y_order = tuning_int("PGMG_Y_ORDER", 0);
+    Grid dummy;
+    if (tuning_int("PGMG_DUMMY_MB", 0) > 0) {
+        Level Ld = c->lv[0];
+        Ld.hi = Ld.lo + (int)(((size_t)tuning_int("PGMG_DUMMY_MB", 0) << 20) / ((size_t)Ld.P * Ld.es));
+        rc = alloc_grid(dummy, Ld);
+    }
+    if (rc == PGMG_OK && want_y && y_order == 1 && c->nb >= 1 && c->lv[0].N >= 2049)
+        rc = alloc_grid(c->Y, c->lv[0]);
     for (int l = 0; l < (int)c->lv.size() && rc == PGMG_OK; ++l) {
         Level &L = c->lv[l];
         if (!L.on_this_rank) continue;
@@ -1204,8 +1216,11 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
     const size_t st0 = (size_t)tuning_int("PGMG_GRID_STAGGER", 0);
     if (rc == PGMG_OK && c->cross) rc = alloc_grid(c->S, c->lv[0], 3 * st0);
     // the carry's fourth level-0 grid (one GPU; see "carry"): ~2.15 GB at N = 16385 fp64
-    if (rc == PGMG_OK && c->cross && c->comm == nullptr && !(cfg->flags & PGMG_FLAG_NO_CARRY))
+    if (rc == PGMG_OK && c->cross && c->comm == nullptr && !(cfg->flags & PGMG_FLAG_NO_CARRY) &&
+        !c->Y.base && y_order == 0)
         rc = alloc_grid(c->Y, c->lv[0], 4 * st0);
+    if (!(c->cross && c->comm == nullptr) && c->Y.base) free_grid(c->Y);
+    (void)dummy;   // (the probe's dummy buffer stays allocated: the context leaks it)
     // partial sums of k_postpre's second and third checks (cross-cycle fusion, and the
     // F-cycle's fused smooth(3)), its decision flags
     if (rc == PGMG_OK && (hipMalloc((void **)&c->partials2, sizeof(double) * maxblocks) != hipSuccess ||
