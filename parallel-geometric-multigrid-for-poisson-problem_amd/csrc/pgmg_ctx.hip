@@ -137,7 +137,11 @@ int pgmg::alloc_grid(Grid &g, const Level &L, size_t stagger)
     const size_t off = (size_t)(128 / L.es - 1) + (stagger / 128) * (128 / L.es);
     const size_t n = off + (size_t)rows * L.P + 512;
     void *p = nullptr;
-    if (hipMalloc(&p, n * L.es) != hipSuccess)
+    // (measurement build: PGMG_CONTIG=1 asks for physically contiguous memory for grids of
+    // 64 MB and more: a placement probe)
+    const bool contig = tuning_int("PGMG_CONTIG", 0) != 0 && n * L.es >= (64u << 20);
+    if ((contig ? hipExtMallocWithFlags(&p, n * L.es, hipDeviceMallocContiguous) : hipMalloc(&p, n * L.es)) !=
+        hipSuccess)
         return set_err(PGMG_ERR_NOMEM, "hipMalloc failed for a level of N=" + std::to_string(L.N));
     HIPC(hipMemset(p, 0, n * L.es));
     g.base = p;
