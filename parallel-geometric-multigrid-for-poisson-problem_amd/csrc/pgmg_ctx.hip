@@ -26,6 +26,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <numeric>
 #include <string>
 #include <utility>
 #include <vector>
@@ -128,6 +129,101 @@ int pgmg::check_span(const void *o, long long P, int es, long long r0, long long
     return set_err(PGMG_ERR_STATE, buf);
 }
 
+// ---------------------------------------------------------------------------
+// Shuffled physical placement (large grids).  The finest pass streams two 2 GB grids at once
+// (reads one, writes the other a few rows behind); how fast depends on where their PHYSICAL
+// pages lie relative to each other (profiles/r06/probes/: the same kernel on the same data runs
+// 1.02 or 1.09 ms depending on the context's allocation, 1.14-1.29 ms with physically
+// contiguous grids).  A grid of this kind is instead built from physical chunks mapped into one
+// virtual range in a fixed pseudo-random order (HIP virtual memory API): whatever the
+// allocator hands out, consecutive chunks of a grid do not sit at a fixed physical distance from
+// the chunks of the other grids the pass streams at the same time.
+// ---------------------------------------------------------------------------
+namespace {
+struct VmmAlloc {
+    size_t bytes = 0, chunk = 0;
+    std::vector<hipMemGenericAllocationHandle_t> h;
+};
+std::mutex g_vmm_mu;
+std::map<uintptr_t, VmmAlloc> g_vmm;   // reserved base -> its chunks
+}  // namespace
+
+static hipError_t vmm_free(void *base)
+{
+    VmmAlloc a;
+    {
+        std::lock_guard<std::mutex> lk(g_vmm_mu);
+        auto it = g_vmm.find((uintptr_t)base);
+        if (it == g_vmm.end()) return hipErrorInvalidValue;
+        a = std::move(it->second);
+        g_vmm.erase(it);
+    }
+    hipError_t e = hipSuccess;
+    for (size_t i = 0; i < a.h.size(); ++i) {
+        if (a.h[i] == 0) continue;
+        const hipError_t u = hipMemUnmap(static_cast<char *>(base) + i * a.chunk, a.chunk);
+        const hipError_t r = hipMemRelease(a.h[i]);
+        if (e == hipSuccess) e = u != hipSuccess ? u : r;
+    }
+    const hipError_t f = hipMemAddressFree(base, a.bytes);
+    return e != hipSuccess ? e : f;
+}
+
+// `bytes` of device memory on the current device from chunks of `chunk_mb` MB (rounded to the
+// allocation granularity) mapped in a fixed shuffled order; *out = nullptr on failure
+static hipError_t vmm_alloc(void **out, size_t bytes, size_t chunk_mb)
+{
+    *out = nullptr;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    hipMemAllocationProp prop{};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = dev;
+    size_t gran = 0;
+    if ((e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum)) != hipSuccess)
+        return e;
+    size_t chunk = std::max(gran, (chunk_mb << 20) / gran * gran);
+    const size_t n = (bytes + chunk - 1) / chunk, total = n * chunk;
+    void *base = nullptr;
+    if ((e = hipMemAddressReserve(&base, total, 0, nullptr, 0)) != hipSuccess) return e;
+    VmmAlloc a;
+    a.bytes = total;
+    a.chunk = chunk;
+    a.h.assign(n, 0);
+    {
+        std::lock_guard<std::mutex> lk(g_vmm_mu);
+        g_vmm[(uintptr_t)base] = a;
+    }
+    // the k-th physical chunk created goes to virtual slot perm[k]: a fixed multiplicative
+    // permutation (odd stride coprime to n) scattering consecutive chunks
+    size_t stride = (size_t)(0.6180339887 * (double)n) | 1;
+    while (std::gcd(stride, n) != 1) stride += 2;
+    for (size_t k = 0; k < n && e == hipSuccess; ++k) {
+        const size_t slot = (k * stride) % n;
+        hipMemGenericAllocationHandle_t h = 0;
+        if ((e = hipMemCreate(&h, chunk, &prop, 0)) != hipSuccess) break;
+        {
+            std::lock_guard<std::mutex> lk(g_vmm_mu);
+            g_vmm[(uintptr_t)base].h[slot] = h;
+        }
+        e = hipMemMap(static_cast<char *>(base) + slot * chunk, chunk, 0, h, 0);
+    }
+    if (e == hipSuccess) {
+        hipMemAccessDesc acc{};
+        acc.location = prop.location;
+        acc.flags = hipMemAccessFlagsProtReadWrite;
+        e = hipMemSetAccess(base, total, &acc, 1);
+    }
+    if (e != hipSuccess) {
+        (void)vmm_free(base);
+        return e;
+    }
+    *out = base;
+    return hipSuccess;
+}
+
 int pgmg::alloc_grid(Grid &g, const Level &L, size_t stagger)
 {
     // owned rows + kHalo halo rows each side (the fused passes read 4 rows past a
@@ -140,9 +236,16 @@ int pgmg::alloc_grid(Grid &g, const Level &L, size_t stagger)
     // (measurement build: PGMG_CONTIG=1 asks for physically contiguous memory for grids of
     // 64 MB and more: a placement probe)
     const bool contig = tuning_int("PGMG_CONTIG", 0) != 0 && n * L.es >= (64u << 20);
-    if ((contig ? hipExtMallocWithFlags(&p, n * L.es, hipDeviceMallocContiguous) : hipMalloc(&p, n * L.es)) !=
-        hipSuccess)
-        return set_err(PGMG_ERR_NOMEM, "hipMalloc failed for a level of N=" + std::to_string(L.N));
+    // (measurement build: PGMG_SHUFFLE_MB > 0: grids of 256 MB and more from shuffled chunks)
+    const int shuffle_mb = tuning_int("PGMG_SHUFFLE_MB", 0);
+    const bool shuffled = shuffle_mb > 0 && n * L.es >= (256u << 20);
+    hipError_t ae;
+    if (shuffled) ae = vmm_alloc(&p, n * L.es, (size_t)shuffle_mb);
+    else if (contig) ae = hipExtMallocWithFlags(&p, n * L.es, hipDeviceMallocContiguous);
+    else ae = hipMalloc(&p, n * L.es);
+    if (ae != hipSuccess)
+        return set_err(PGMG_ERR_NOMEM, "hipMalloc failed for a level of N=" + std::to_string(L.N) + ": " +
+                                           hipGetErrorString(ae));
     HIPC(hipMemset(p, 0, n * L.es));
     g.base = p;
     g.bytes = n * L.es;
@@ -155,7 +258,7 @@ void pgmg::free_grid(Grid &g)
 {
     if (g.base) {
         unregister_alloc(g.base);
-        (void)hipFree(g.base);
+        if (vmm_free(g.base) != hipSuccess) (void)hipFree(g.base);   // (not a shuffled grid)
     }
     g.base = g.o = nullptr;
     g.bytes = 0;
