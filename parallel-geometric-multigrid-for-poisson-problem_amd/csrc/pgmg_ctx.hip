@@ -148,6 +148,17 @@ std::mutex g_vmm_mu;
 std::map<uintptr_t, VmmAlloc> g_vmm;   // reserved base -> its chunks
 }  // namespace
 
+// does p lie in a shuffled (virtual-memory-mapped) grid?  The runtime's 2D copies and memsets
+// refuse those ranges, so every grid transfer checks and takes a kernel or a 1D copy instead
+static bool is_vmm(const void *p)
+{
+    std::lock_guard<std::mutex> lk(g_vmm_mu);
+    auto it = g_vmm.upper_bound((uintptr_t)p);
+    if (it == g_vmm.begin()) return false;
+    --it;
+    return (uintptr_t)p < it->first + it->second.bytes;
+}
+
 static hipError_t vmm_free(void *base)
 {
     VmmAlloc a;
@@ -1391,16 +1402,17 @@ static int upload_rows(pgmg_ctx *c, const Level &L, const Grid &g, const double 
 {
     const int N = L.N;
     const size_t rows = (size_t)(r1 - r0);
-    if (!c->fp32) {
+    if (!c->fp32 && !is_vmm(g.base)) {
         HIPC(hipMemcpy2D(row_ptr(g, r0, L.P, 8), L.P * sizeof(double), host + (size_t)r0 * N,
                          N * sizeof(double), N * sizeof(double), rows, hipMemcpyHostToDevice));
         return PGMG_OK;
     }
-    // fp32: stage the doubles on the device, narrow there
+    // fp32 (or a shuffled grid): stage the doubles on the device, narrow / place them there
     double *d = nullptr;
     HIPC(hipMalloc((void **)&d, rows * N * sizeof(double)));
     HIPC(hipMemcpy(d, host + (size_t)r0 * N, rows * N * sizeof(double), hipMemcpyHostToDevice));
-    launch_from_double(d - (size_t)r0 * N, N, G<float>(g), L.P, r0, r1, c->s);
+    if (c->fp32) launch_from_double(d - (size_t)r0 * N, N, G<float>(g), L.P, r0, r1, c->s);
+    else launch_from_double(d - (size_t)r0 * N, N, G<double>(g), L.P, r0, r1, c->s);
     HIPC(hipGetLastError());
     PGMG_TRY(stream_wait(c));
     HIPC(hipFree(d));
@@ -1409,6 +1421,16 @@ static int upload_rows(pgmg_ctx *c, const Level &L, const Grid &g, const double 
 
 int pgmg::download_grid(pgmg_ctx *c, const void *o, int P, int N, double *host)
 {
+    if (!c->fp32 && is_vmm(o)) {   // a shuffled grid: widen/copy on the device, then 1D
+        double *d = nullptr;
+        HIPC(hipMalloc((void **)&d, (size_t)N * N * sizeof(double)));
+        launch_to_double(static_cast<const double *>(o), P, d, N, 0, N, c->s);
+        HIPC(hipGetLastError());
+        HIPC(hipMemcpyAsync(host, d, (size_t)N * N * sizeof(double), hipMemcpyDeviceToHost, c->s));
+        PGMG_TRY(stream_wait(c));
+        HIPC(hipFree(d));
+        return PGMG_OK;
+    }
     if (!c->fp32) {
         HIPC(hipMemcpy2DAsync(host, N * sizeof(double), o, P * sizeof(double), N * sizeof(double),
                               N, hipMemcpyDeviceToHost, c->s));
@@ -1513,22 +1535,24 @@ int pgmg_set_problem(pgmg_ctx *c, const double *phi0, const double *f)
     c->ext_phi = nullptr;   // host arrays: the problem lives in the context again
     c->ext_f = nullptr;
     // phi (and its boundary copy in the ping-pong buffer B)
+    // (the rows r0 .. r1 of a level-0 grid are one contiguous range, padding included: zeroed
+    // and copied whole with 1D operations, which shuffled grids accept)
+    (void)width;
     if (phi0) {
         if ((e = upload_rows(c, L, L.A, phi0, r0, r1))) return e;
     } else {
-        HIPC(hipMemset2D(row_ptr(L.A, r0, L.P, L.es), pitch, 0, width, rows));
+        HIPC(hipMemset(row_ptr(L.A, r0, L.P, L.es), 0, pitch * rows));
     }
-    if (c->nb > 0)
-        HIPC(hipMemcpy2D(row_ptr(L.B, r0, L.P, L.es), pitch, row_ptr(L.A, r0, L.P, L.es), pitch,
-                         width, rows, hipMemcpyDeviceToDevice));
+    auto mirror = [&](const Grid &g) -> int {
+        HIPC(hipMemcpy(row_ptr(g, r0, L.P, L.es), row_ptr(L.A, r0, L.P, L.es), pitch * rows,
+                       hipMemcpyDeviceToDevice));
+        return PGMG_OK;
+    };
+    if (c->nb > 0) PGMG_TRY(mirror(L.B));
     // the cross-cycle rare-path scratch S mirrors phi's boundary too (its passes never
     // write boundary rows/columns, the k_pre that reads it passes them through)
-    if (c->S.base)
-        HIPC(hipMemcpy2D(row_ptr(c->S, r0, L.P, L.es), pitch, row_ptr(L.A, r0, L.P, L.es), pitch,
-                         width, rows, hipMemcpyDeviceToDevice));
-    if (c->Y.base)   // the carry's grid likewise
-        HIPC(hipMemcpy2D(row_ptr(c->Y, r0, L.P, L.es), pitch, row_ptr(L.A, r0, L.P, L.es), pitch,
-                         width, rows, hipMemcpyDeviceToDevice));
+    if (c->S.base) PGMG_TRY(mirror(c->S));
+    if (c->Y.base) PGMG_TRY(mirror(c->Y));   // the carry's grid likewise
     if ((e = setup_rhs(c, f, r0, r1))) return e;
     return problem_reset(c);
 }
@@ -1685,11 +1709,13 @@ static int ext_stage_in(pgmg_ctx *c, bool inplace)
     const int N = L.N;
     if (c->ext_f) {
         if (c->fp32) launch_from_double(c->ext_f, N, G<float>(L.F), L.P, 0, N, c->s);
+        else if (is_vmm(L.F.base)) launch_from_double(c->ext_f, N, G<double>(L.F), L.P, 0, N, c->s);
         else HIPC(hipMemcpy2DAsync(L.F.o, L.P * sizeof(double), c->ext_f, N * sizeof(double),
                                    N * sizeof(double), N, hipMemcpyDeviceToDevice, c->s));
     }
     if (!inplace) {
         if (c->fp32) launch_from_double(c->ext_phi, N, G<float>(L.A), L.P, 0, N, c->s);
+        else if (is_vmm(L.A.base)) launch_from_double(c->ext_phi, N, G<double>(L.A), L.P, 0, N, c->s);
         else HIPC(hipMemcpy2DAsync(L.A.o, L.P * sizeof(double), c->ext_phi, N * sizeof(double),
                                    N * sizeof(double), N, hipMemcpyDeviceToDevice, c->s));
     }
@@ -1704,6 +1730,7 @@ static int ext_stage_out(pgmg_ctx *c)
     Level &L = c->lv[0];
     const int N = L.N;
     if (c->fp32) launch_to_double(G<float>(L.A), L.P, c->ext_phi, N, 0, N, c->s);
+    else if (is_vmm(L.A.base)) launch_to_double(G<double>(L.A), L.P, c->ext_phi, N, 0, N, c->s);
     else HIPC(hipMemcpy2DAsync(c->ext_phi, N * sizeof(double), L.A.o, L.P * sizeof(double),
                                N * sizeof(double), N, hipMemcpyDeviceToDevice, c->s));
     HIPC(hipGetLastError());
