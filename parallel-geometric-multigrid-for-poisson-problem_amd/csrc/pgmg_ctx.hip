@@ -20,6 +20,7 @@
 
 #include <cxxabi.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -207,12 +208,18 @@ static hipError_t vmm_alloc(void **out, size_t bytes, size_t chunk_mb)
         std::lock_guard<std::mutex> lk(g_vmm_mu);
         g_vmm[(uintptr_t)base] = a;
     }
-    // the k-th physical chunk created goes to virtual slot perm[k]: a fixed multiplicative
-    // permutation (odd stride coprime to n) scattering consecutive chunks
-    size_t stride = (size_t)(0.6180339887 * (double)n) | 1;
+    // the k-th physical chunk created goes to virtual slot (k * stride + shift) % n: a
+    // multiplicative permutation (stride coprime to n) scattering consecutive chunks, different
+    // for every grid (the relative placement of two grids' chunks at the same virtual offset --
+    // what two streams of one pass touch together -- then varies from chunk to chunk)
+    static std::atomic<unsigned> serial{0};
+    const unsigned g = serial.fetch_add(1);
+    const double phi = 0.6180339887 + 0.0731 * (double)(g % 7);
+    size_t stride = ((size_t)(phi * (double)n) % n) | 1;
     while (std::gcd(stride, n) != 1) stride += 2;
+    const size_t shift = ((size_t)g * 40503u) % n;
     for (size_t k = 0; k < n && e == hipSuccess; ++k) {
-        const size_t slot = (k * stride) % n;
+        const size_t slot = (k * stride + shift) % n;
         hipMemGenericAllocationHandle_t h = 0;
         if ((e = hipMemCreate(&h, chunk, &prop, 0)) != hipSuccess) break;
         {

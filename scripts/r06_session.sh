@@ -39,6 +39,7 @@ for s in ${STEPS}; do
     order2) step warm 300 python3 scripts/order_probe.py --order n --reps 30 && step keep 300 python3 scripts/order_probe.py --order nnn --keep ;;
     contig) step contig1 300 env PGMG_LIB=$PWD/parallel-geometric-multigrid-for-poisson-problem_amd/libpgmg_probe.so PGMG_CONTIG=1 python3 scripts/order_probe.py --order ncnc && step contig2 300 env PGMG_LIB=$PWD/parallel-geometric-multigrid-for-poisson-problem_amd/libpgmg_probe.so PGMG_CONTIG=1 python3 scripts/order_probe.py --order nnn --keep && step contig0 300 env PGMG_LIB=$PWD/parallel-geometric-multigrid-for-poisson-problem_amd/libpgmg_probe.so python3 scripts/order_probe.py --order ncnc ;;
     shuffle) for mb in ${SHUFFLE_MB:-2 64}; do step shuffle${mb} 300 env PGMG_LIB=$PWD/parallel-geometric-multigrid-for-poisson-problem_amd/libpgmg_probe.so PGMG_SHUFFLE_MB=${mb} python3 scripts/order_probe.py --order ncnc; done ;;
+    shuffle_rep) for i in 1 2 3; do step shuffle_rep${i} 300 env PGMG_LIB=$PWD/parallel-geometric-multigrid-for-poisson-problem_amd/libpgmg_probe.so PGMG_SHUFFLE_MB=${SHUFFLE_MB:-2} python3 scripts/order_probe.py --order ncnc; done ;;
     carry_ab) step carry_ab 400 python scripts/carry_ab.py --rounds 3 ;;
     levels) step levels 300 python scripts/level_pmc.py run --n 16385 --out ${OUT}/levels ;;
     *) echo "unknown step ${s}" >&2 ;;
