@@ -131,6 +131,10 @@ extern "C" {
 #define PGMG_FLAG_TIME_COMM 262144u /* world > 1: hipEvents around every collective group
                                        (grouped halo exchange, all-to-all, allreduce) on the
                                        context's stream, read by pgmg_comm_stats */
+#define PGMG_FLAG_NO_SHUFFLE 524288u /* one GPU: allocate the grids of 256 MB and more with
+                                        plain hipMalloc instead of from 2 MB physical chunks
+                                        mapped in a shuffled order (the finest
+                                        pass runs ~3-4 % faster in a process's first context) */
 #define PGMG_FLAG_HOST_TRANSPORT 2048u /* world > 1 without RCCL: nccl_unique_id points to
                                        a pgmg_host_transport; every message and reduction
                                        is staged through host memory and handed to the

@@ -61,6 +61,7 @@ struct HaloReq {
 struct pgmg_ctx {
     pgmg_config cfg{};
     bool fp32 = false;            // PGMG_PRECISION_FP32: every level grid stores float
+    bool shuffle = false;         // large grids from shuffled physical chunks (one GPU)
     hipStream_t s = nullptr;
     std::vector<pgmg::Level> lv;  // 0 .. nb-1 bulk levels, nb = the tail's top level
     int nb = 0;
@@ -196,8 +197,9 @@ struct pgmg_ctx {
 
 namespace pgmg {
 
-// stagger: the origin shifted by this many bytes (a multiple of 128) past the usual one
-int alloc_grid(Grid &g, const Level &L, size_t stagger = 0);
+// stagger: the origin shifted by this many bytes (a multiple of 128) past the usual one;
+// shuffle: a grid of 256 MB or more is built from shuffled physical chunks (pgmg_ctx.hip)
+int alloc_grid(Grid &g, const Level &L, size_t stagger = 0, bool shuffle = false);
 void free_grid(Grid &g);
 // dispatch on the context's element type
 int enqueue_cycle(pgmg_ctx *c, int l, int gamma, bool x0_zero);

@@ -242,7 +242,7 @@ static hipError_t vmm_alloc(void **out, size_t bytes, size_t chunk_mb)
     return hipSuccess;
 }
 
-int pgmg::alloc_grid(Grid &g, const Level &L, size_t stagger)
+int pgmg::alloc_grid(Grid &g, const Level &L, size_t stagger, bool shuffle)
 {
     // owned rows + kHalo halo rows each side (the fused passes read 4 rows past a
     // segment); the slack covers the last wave tile reading past the row end
@@ -253,13 +253,16 @@ int pgmg::alloc_grid(Grid &g, const Level &L, size_t stagger)
     void *p = nullptr;
     // (measurement build: PGMG_CONTIG=1 asks for physically contiguous memory for grids of
     // 64 MB and more: a placement probe)
+    // (measurement build: PGMG_CONTIG=1 physically contiguous grids, PGMG_SHUFFLE_MB the chunk
+    // size of the shuffled ones, 0 = no shuffling)
     const bool contig = tuning_int("PGMG_CONTIG", 0) != 0 && n * L.es >= (64u << 20);
-    // (measurement build: PGMG_SHUFFLE_MB > 0: grids of 256 MB and more from shuffled chunks)
-    const int shuffle_mb = tuning_int("PGMG_SHUFFLE_MB", 0);
-    const bool shuffled = shuffle_mb > 0 && n * L.es >= (256u << 20);
-    hipError_t ae;
+    const int shuffle_mb = tuning_int("PGMG_SHUFFLE_MB", 2);
+    const bool shuffled = shuffle && shuffle_mb > 0 && n * L.es >= (256u << 20);
+    hipError_t ae = hipErrorUnknown;
     if (shuffled) ae = vmm_alloc(&p, n * L.es, (size_t)shuffle_mb);
-    else if (contig) ae = hipExtMallocWithFlags(&p, n * L.es, hipDeviceMallocContiguous);
+    if (shuffled && ae != hipSuccess) (void)hipGetLastError();   // no VMM here: plain memory
+    if (ae == hipSuccess) {
+    } else if (contig) ae = hipExtMallocWithFlags(&p, n * L.es, hipDeviceMallocContiguous);
     else ae = hipMalloc(&p, n * L.es);
     if (ae != hipSuccess)
         return set_err(PGMG_ERR_NOMEM, "hipMalloc failed for a level of N=" + std::to_string(L.N) + ": " +
@@ -1245,6 +1248,9 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
     pgmg_ctx *c = new pgmg_ctx();
     c->cfg = *cfg;
     c->fp32 = cfg->precision == PGMG_PRECISION_FP32;
+    // one GPU: the big grids from shuffled physical chunks (vmm_alloc); row strips keep plain
+    // device memory (what RCCL's transfers were validated on)
+    c->shuffle = cfg->world <= 1 && !(cfg->flags & PGMG_FLAG_NO_SHUFFLE);
     int tail_n = cfg->tail_n;
     if (tail_n > kTailMaxN) tail_n = kTailMaxN;
     if (tail_n < cfg->n_coarse) tail_n = cfg->n_coarse;
@@ -1299,15 +1305,15 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         rc = alloc_grid(dummy, Ld);
     }
     if (rc == PGMG_OK && want_y && y_order == 1 && c->nb >= 1 && c->lv[0].N >= 2049)
-        rc = alloc_grid(c->Y, c->lv[0]);
+        rc = alloc_grid(c->Y, c->lv[0], 0, c->shuffle);
     for (int l = 0; l < (int)c->lv.size() && rc == PGMG_OK; ++l) {
         Level &L = c->lv[l];
         if (!L.on_this_rank) continue;
         // (measurement build: PGMG_GRID_STAGGER bytes times a per-grid index of level 0)
         const size_t st = l == 0 ? (size_t)tuning_int("PGMG_GRID_STAGGER", 0) : 0;
-        rc = alloc_grid(L.A, L, 0 * st);
-        if (rc == PGMG_OK) rc = alloc_grid(L.F, L, 1 * st);
-        if (rc == PGMG_OK && l < c->nb) rc = alloc_grid(L.B, L, 2 * st);
+        rc = alloc_grid(L.A, L, 0 * st, c->shuffle);
+        if (rc == PGMG_OK) rc = alloc_grid(L.F, L, 1 * st, c->shuffle);
+        if (rc == PGMG_OK && l < c->nb) rc = alloc_grid(L.B, L, 2 * st, c->shuffle);
     }
     c->fused = cfg->v1 == 1 && cfg->v2 == 1 && !(cfg->flags & PGMG_FLAG_UNFUSED);
     c->recompute = !(cfg->flags & PGMG_FLAG_NO_RECOMPUTE);
@@ -1339,11 +1345,11 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         }
     }
     const size_t st0 = (size_t)tuning_int("PGMG_GRID_STAGGER", 0);
-    if (rc == PGMG_OK && c->cross) rc = alloc_grid(c->S, c->lv[0], 3 * st0);
+    if (rc == PGMG_OK && c->cross) rc = alloc_grid(c->S, c->lv[0], 3 * st0, c->shuffle);
     // the carry's fourth level-0 grid (one GPU; see "carry"): ~2.15 GB at N = 16385 fp64
     if (rc == PGMG_OK && c->cross && c->comm == nullptr && !(cfg->flags & PGMG_FLAG_NO_CARRY) &&
         !c->Y.base && y_order == 0)
-        rc = alloc_grid(c->Y, c->lv[0], 4 * st0);
+        rc = alloc_grid(c->Y, c->lv[0], 4 * st0, c->shuffle);
     if (!(c->cross && c->comm == nullptr) && c->Y.base) free_grid(c->Y);
     (void)dummy;   // (the probe's dummy buffer stays allocated: the context leaks it)
     // partial sums of k_postpre's second and third checks (cross-cycle fusion, and the
