@@ -1,1 +1,1 @@
-extern "C" const char *pgmg_source_hash(void) { return "asan-7cbcc07a982fff9a"; }
+extern "C" const char *pgmg_source_hash(void) { return "asan-456c43c436f0f475"; }
