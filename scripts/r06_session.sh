@@ -29,6 +29,9 @@ for s in ${STEPS}; do
     smoke) step smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step tests 900 python -u -m pytest tests/ -m gpu -q --timeout 300 --timeout-method thread ;;
     bench) step bench 600 python bench.py --gpus 1 --warmup 5 --steps 20 --save-profiles ${OUT}/prof ;;
+    bench_F) step bench_F 300 python bench.py --cycle F --warmup 2 --steps 20 --cpu-baseline off --pmc off --trace off ;;
+    bench_W) step bench_W 300 python bench.py --cycle W --n 4097 --warmup 2 --steps 10 --cpu-baseline off --pmc off --trace off ;;
+    bench_f32) step bench_f32 400 python bench.py --dtype f32 --warmup 5 --steps 20 --cpu-baseline off --save-profiles ${OUT}/prof_f32 ;;
     solo2) step solo2 300 env PGMG_BENCH_SOLO=1 python bench.py --gpus 2 --warmup 2 --steps 10 --reps 2 ;;
     solo8) step solo8 400 env PGMG_BENCH_SOLO=1 python bench.py --gpus 8 --warmup 2 --steps 10 --reps 2 ;;
     host2) step host2 400 env PGMG_BENCH_TRANSPORT=host python bench.py --gpus 2 --warmup 2 --steps 5 --reps 2 ;;
