@@ -138,6 +138,8 @@ struct pgmg_ctx {
     std::vector<pgmg::CheckRef> chks;
     pgmg::CheckRef *chk_dev = nullptr;
     unsigned *uflags = nullptr;   // per-check verdicts (+ one spare word: any)
+    char *pin = nullptr;          // pinned host staging of the validation: chk_cap CheckRefs,
+                                  // norms, verdicts + any (one stream wait per call, no pageable copies)
     long long chk_cap = 0;
     pgmg::Grid bk;                // level-0 solution at the start of the call (rollback)
     // speculative F-cycles (pgmg_ctx.hip "speculative F-cycles"): every bulk check of the

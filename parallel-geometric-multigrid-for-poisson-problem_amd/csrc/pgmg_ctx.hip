@@ -1195,6 +1195,7 @@ int pgmg_destroy(pgmg_ctx *c)
     if (c->rhs_tab) (void)hipFree(c->rhs_tab);
     if (c->fmg_gtab) (void)hipFree(c->fmg_gtab);
     if (c->uflags) (void)hipFree(c->uflags);
+    if (c->pin) (void)hipHostFree(c->pin);
     if (c->plog) (void)hipFree(c->plog);
     if (c->chk_dev) (void)hipFree(c->chk_dev);
     if (c->chk_norm) (void)hipFree(c->chk_norm);
@@ -1859,6 +1860,11 @@ static void spec_need_level(pgmg_ctx *c, int l, int gamma, long long *dbl, long 
     *nchk = 2 + gamma * k;
 }
 
+// the pinned validation staging (pgmg_ctx::pin) for cap checks: CheckRefs, norms, verdicts + any
+static size_t pin_norm_off(long long cap) { return ((size_t)cap * sizeof(CheckRef) + 15) / 16 * 16; }
+static size_t pin_flag_off(long long cap) { return pin_norm_off(cap) + (size_t)cap * sizeof(double); }
+static size_t pin_bytes(long long cap) { return pin_flag_off(cap) + ((size_t)cap + 1) * sizeof(unsigned); }
+
 static int spec_reserve(pgmg_ctx *c, long long dbl, long long nchk)
 {
     if (dbl > c->plog_cap || nchk > c->chk_cap) {
@@ -1879,6 +1885,9 @@ static int spec_reserve(pgmg_ctx *c, long long dbl, long long nchk)
             HIPC(hipMalloc((void **)&c->chk_dev, nchk * sizeof(CheckRef)));
             HIPC(hipMalloc((void **)&c->uflags, (nchk + 1) * sizeof(unsigned)));
             HIPC(hipMalloc((void **)&c->chk_norm, nchk * sizeof(double)));
+            if (c->pin) HIPC(hipHostFree(c->pin));
+            c->pin = nullptr;
+            HIPC(hipHostMalloc((void **)&c->pin, pin_bytes(nchk), hipHostMallocDefault));
             c->chk_cap = nchk;
         }
     }
@@ -2143,21 +2152,29 @@ static int spec_validate(pgmg_ctx *c, unsigned *h_out, bool *overflow_out, int n
     c->hnorm.assign(n, 0.0);
     c->hflag.assign(n, 1u);
     if (n > 0 && !overflow) {
+        // through the pinned staging area: the copies stay asynchronous and the call waits
+        // for the stream once (pageable ones each waited for the stream)
+        CheckRef *hc = reinterpret_cast<CheckRef *>(c->pin);
+        double *hn = reinterpret_cast<double *>(c->pin + pin_norm_off(c->chk_cap));
+        unsigned *hf = reinterpret_cast<unsigned *>(c->pin + pin_flag_off(c->chk_cap));
+        std::memcpy(hc, c->chks.data(), n * sizeof(CheckRef));
         unsigned *any = c->uflags + c->chk_cap;   // the spare word past the verdicts
-        HIPC(hipMemcpyAsync(c->chk_dev, c->chks.data(), n * sizeof(CheckRef),
-                            hipMemcpyHostToDevice, c->s));
+        HIPC(hipMemcpyAsync(c->chk_dev, hc, n * sizeof(CheckRef), hipMemcpyHostToDevice, c->s));
         launch_verify_checks(c->chk_dev, n, c->cfg.eps, c->uflags, c->chk_norm, c->s);
         int e;
         if (c->comm && (e = c->comm->allreduce_min_u32(c->uflags, n, c->s))) return e;
         // (the checks past n_any -- the carried pre-smooth's -- never roll the call back)
         launch_any_flag(c->uflags, n_any, any, c->s);
-        HIPC(hipMemcpyAsync(&h, any, sizeof(unsigned), hipMemcpyDeviceToHost, c->s));
-        HIPC(hipMemcpyAsync(c->hnorm.data(), c->chk_norm, n * sizeof(double),
-                            hipMemcpyDeviceToHost, c->s));
-        HIPC(hipMemcpyAsync(c->hflag.data(), c->uflags, n * sizeof(unsigned),
-                            hipMemcpyDeviceToHost, c->s));
+        HIPC(hipMemcpyAsync(hf + c->chk_cap, any, sizeof(unsigned), hipMemcpyDeviceToHost, c->s));
+        HIPC(hipMemcpyAsync(hn, c->chk_norm, n * sizeof(double), hipMemcpyDeviceToHost, c->s));
+        HIPC(hipMemcpyAsync(hf, c->uflags, n * sizeof(unsigned), hipMemcpyDeviceToHost, c->s));
+        PGMG_TRY(stream_wait(c));
+        h = hf[c->chk_cap];
+        std::memcpy(c->hnorm.data(), hn, n * sizeof(double));
+        std::memcpy(c->hflag.data(), hf, n * sizeof(unsigned));
+    } else {
+        PGMG_TRY(stream_wait(c));
     }
-    PGMG_TRY(stream_wait(c));
     *h_out = h;
     *overflow_out = overflow;
     return PGMG_OK;
