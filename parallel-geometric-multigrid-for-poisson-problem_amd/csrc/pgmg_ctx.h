@@ -136,10 +136,10 @@ struct pgmg_ctx {
     double *plog = nullptr;       // partials of every recorded check of the current call
     long long plog_cap = 0, plog_used = 0;
     std::vector<pgmg::CheckRef> chks;
-    pgmg::CheckRef *chk_dev = nullptr;
     unsigned *uflags = nullptr;   // per-check verdicts (+ one spare word: any)
-    char *pin = nullptr;          // pinned host staging of the validation: chk_cap CheckRefs,
-                                  // norms, verdicts + any (one stream wait per call, no pageable copies)
+    char *pin = nullptr;          // pinned coherent host staging of the validation: chk_cap
+                                  // CheckRefs (read by k_verify_checks), norms, verdicts + any
+                                  // (written by k_spec_reply)
     long long chk_cap = 0;
     pgmg::Grid bk;                // level-0 solution at the start of the call (rollback)
     // speculative F-cycles (pgmg_ctx.hip "speculative F-cycles"): every bulk check of the

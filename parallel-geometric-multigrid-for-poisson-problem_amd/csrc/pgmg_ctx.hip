@@ -1197,7 +1197,6 @@ int pgmg_destroy(pgmg_ctx *c)
     if (c->uflags) (void)hipFree(c->uflags);
     if (c->pin) (void)hipHostFree(c->pin);
     if (c->plog) (void)hipFree(c->plog);
-    if (c->chk_dev) (void)hipFree(c->chk_dev);
     if (c->chk_norm) (void)hipFree(c->chk_norm);
     if (c->mark_dev) (void)hipFree(c->mark_dev);
     if (c->stats_bk) (void)hipFree(c->stats_bk);
@@ -1876,18 +1875,15 @@ static int spec_reserve(pgmg_ctx *c, long long dbl, long long nchk)
             c->plog_cap = dbl;
         }
         if (nchk > c->chk_cap) {
-            if (c->chk_dev) HIPC(hipFree(c->chk_dev));
             if (c->uflags) HIPC(hipFree(c->uflags));
             if (c->chk_norm) HIPC(hipFree(c->chk_norm));
-            c->chk_dev = nullptr;
             c->uflags = nullptr;
             c->chk_norm = nullptr;
-            HIPC(hipMalloc((void **)&c->chk_dev, nchk * sizeof(CheckRef)));
             HIPC(hipMalloc((void **)&c->uflags, (nchk + 1) * sizeof(unsigned)));
             HIPC(hipMalloc((void **)&c->chk_norm, nchk * sizeof(double)));
             if (c->pin) HIPC(hipHostFree(c->pin));
             c->pin = nullptr;
-            HIPC(hipHostMalloc((void **)&c->pin, pin_bytes(nchk), hipHostMallocDefault));
+            HIPC(hipHostMalloc((void **)&c->pin, pin_bytes(nchk), hipHostMallocCoherent));
             c->chk_cap = nchk;
         }
     }
@@ -2152,22 +2148,18 @@ static int spec_validate(pgmg_ctx *c, unsigned *h_out, bool *overflow_out, int n
     c->hnorm.assign(n, 0.0);
     c->hflag.assign(n, 1u);
     if (n > 0 && !overflow) {
-        // through the pinned staging area: the copies stay asynchronous and the call waits
-        // for the stream once (pageable ones each waited for the stream)
+        // through the pinned (coherent) staging area: k_verify_checks reads the CheckRefs from
+        // it and k_spec_reply writes the verdicts, the norms and their OR into it -- two
+        // kernels and one stream wait, no copy operations
         CheckRef *hc = reinterpret_cast<CheckRef *>(c->pin);
         double *hn = reinterpret_cast<double *>(c->pin + pin_norm_off(c->chk_cap));
         unsigned *hf = reinterpret_cast<unsigned *>(c->pin + pin_flag_off(c->chk_cap));
         std::memcpy(hc, c->chks.data(), n * sizeof(CheckRef));
-        unsigned *any = c->uflags + c->chk_cap;   // the spare word past the verdicts
-        HIPC(hipMemcpyAsync(c->chk_dev, hc, n * sizeof(CheckRef), hipMemcpyHostToDevice, c->s));
-        launch_verify_checks(c->chk_dev, n, c->cfg.eps, c->uflags, c->chk_norm, c->s);
+        launch_verify_checks(hc, n, c->cfg.eps, c->uflags, c->chk_norm, c->s);
         int e;
         if (c->comm && (e = c->comm->allreduce_min_u32(c->uflags, n, c->s))) return e;
         // (the checks past n_any -- the carried pre-smooth's -- never roll the call back)
-        launch_any_flag(c->uflags, n_any, any, c->s);
-        HIPC(hipMemcpyAsync(hf + c->chk_cap, any, sizeof(unsigned), hipMemcpyDeviceToHost, c->s));
-        HIPC(hipMemcpyAsync(hn, c->chk_norm, n * sizeof(double), hipMemcpyDeviceToHost, c->s));
-        HIPC(hipMemcpyAsync(hf, c->uflags, n * sizeof(unsigned), hipMemcpyDeviceToHost, c->s));
+        launch_spec_reply(c->uflags, c->chk_norm, n, n_any, hf + c->chk_cap, hn, hf, c->s);
         PGMG_TRY(stream_wait(c));
         h = hf[c->chk_cap];
         std::memcpy(c->hnorm.data(), hn, n * sizeof(double));
@@ -2218,10 +2210,9 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
             if (!c->bk.base && (e = alloc_grid(c->bk, L0))) return e;
             HIPC(hipMemcpyAsync(c->bk.base, L0.A.base, L0.A.bytes, hipMemcpyDeviceToDevice, c->s));
         }
-        HIPC(hipMemcpyAsync(c->stats_bk, c->stats, 4 * sizeof(unsigned long long),
-                            hipMemcpyDeviceToDevice, c->s));
-        // the coarse levels' "pre-smooth fired" flags (written by the skipped fix-ups) = 0
-        HIPC(hipMemsetAsync(c->flags, 0, sizeof(unsigned) * (c->lv.size() + 1) * 2 * kMaxSweeps, c->s));
+        // stats backup + the coarse levels' "pre-smooth fired" flags (written by the skipped
+        // fix-ups) = 0, one launch
+        launch_spec_open(c->stats, c->stats_bk, c->flags, (int)(c->lv.size() + 1) * 2 * kMaxSweeps, c->s);
         c->lean = true;
         c->plog_used = 0;
         c->chks.clear();
@@ -2768,10 +2759,9 @@ static int run_fcycles_spec(pgmg_ctx *c, int ncycles)
         A0[l] = c->lv[l].A;
         B0[l] = c->lv[l].B;
     }
-    HIPC(hipMemcpyAsync(c->stats_bk, c->stats, 4 * sizeof(unsigned long long),
-                        hipMemcpyDeviceToDevice, c->s));
-    // the coarse levels' "pre-smooth fired" flags (written by the skipped rare paths) = 0
-    HIPC(hipMemsetAsync(c->flags, 0, sizeof(unsigned) * (c->lv.size() + 1) * 2 * kMaxSweeps, c->s));
+    // stats backup + the coarse levels' "pre-smooth fired" flags (written by the skipped rare
+    // paths) = 0
+    launch_spec_open(c->stats, c->stats_bk, c->flags, (int)(c->lv.size() + 1) * 2 * kMaxSweeps, c->s);
     c->lean = true;
     c->fspec = true;
     c->spec_gamma = 1;

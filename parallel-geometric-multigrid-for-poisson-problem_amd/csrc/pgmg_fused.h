@@ -165,6 +165,12 @@ void launch_postpre_decide(const double *partials1, const double *partials2,
 void launch_verify_checks(const CheckRef *checks, int n, double eps, unsigned *out, double *norm,
                           hipStream_t s);
 
-void launch_any_flag(const unsigned *flags, int n, unsigned *out, hipStream_t s);
+// the validation's reply, straight into pinned host memory (no copies): any = OR over the
+// first n_any verdicts, and the n norms and verdicts themselves
+void launch_spec_reply(const unsigned *flags, const double *norm, int n, int n_any, unsigned *h_any,
+                       double *h_norm, unsigned *h_flags, hipStream_t s);
+// a speculative segment's opening: stats_bk = stats (4 words), flags[0, nflags) = 0
+void launch_spec_open(const unsigned long long *stats, unsigned long long *stats_bk, unsigned *flags,
+                      int nflags, hipStream_t s);
 
 }  // namespace pgmg

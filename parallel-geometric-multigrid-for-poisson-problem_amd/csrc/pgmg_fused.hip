@@ -1963,23 +1963,47 @@ void launch_verify_checks(const CheckRef *checks, int n, double eps, unsigned *o
     if (n > 0) k_verify_checks<<<dim3(n), dim3(256), 0, s>>>(checks, eps, out, norm);
 }
 
-// OR over n flags (after the all-rank MIN): out = 1 when any check could fire on every
-// rank
-__global__ __launch_bounds__(256) void k_any_flag(const unsigned *f, int n, unsigned *out)
+// The validation's reply (after the all-rank MIN): any = 1 when one of the first n_any checks
+// could fire on every rank, then every check's norm and verdict, each stored straight into
+// the context's pinned host staging -- the call then waits for the stream once, with no copy
+// operations between the kernels and the wait.
+__global__ __launch_bounds__(256) void k_spec_reply(const unsigned *f, const double *norm, int n,
+                                                    int n_any, unsigned *h_any, double *h_norm,
+                                                    unsigned *h_flags)
 {
     __shared__ unsigned any;
     if (threadIdx.x == 0) any = 0u;
     __syncthreads();
     unsigned v = 0u;
-    for (int k = threadIdx.x; k < n; k += blockDim.x) v |= f[k];
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+        const unsigned fk = f[k];
+        if (k < n_any) v |= fk;
+        h_flags[k] = fk;
+        h_norm[k] = norm[k];
+    }
     if (v) atomicOr(&any, 1u);
     __syncthreads();
-    if (threadIdx.x == 0) *out = any;
+    if (threadIdx.x == 0) *h_any = any;
 }
 
-void launch_any_flag(const unsigned *flags, int n, unsigned *out, hipStream_t s)
+void launch_spec_reply(const unsigned *flags, const double *norm, int n, int n_any, unsigned *h_any,
+                       double *h_norm, unsigned *h_flags, hipStream_t s)
 {
-    k_any_flag<<<dim3(1), dim3(256), 0, s>>>(flags, n, out);
+    k_spec_reply<<<dim3(1), dim3(256), 0, s>>>(flags, norm, n, n_any, h_any, h_norm, h_flags);
+}
+
+__global__ __launch_bounds__(256) void k_spec_open(const unsigned long long *stats,
+                                                   unsigned long long *stats_bk, unsigned *flags,
+                                                   int nflags)
+{
+    if (threadIdx.x < 4) stats_bk[threadIdx.x] = stats[threadIdx.x];
+    for (int k = threadIdx.x; k < nflags; k += blockDim.x) flags[k] = 0u;
+}
+
+void launch_spec_open(const unsigned long long *stats, unsigned long long *stats_bk, unsigned *flags,
+                      int nflags, hipStream_t s)
+{
+    k_spec_open<<<dim3(1), dim3(256), 0, s>>>(stats, stats_bk, flags, nflags);
 }
 
 // ---------------------------------------------------------------------------
