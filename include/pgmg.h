@@ -135,6 +135,9 @@ extern "C" {
                                         plain hipMalloc instead of from 2 MB physical chunks
                                         mapped in a shuffled order (the finest
                                         pass runs ~3-4 % faster in a process's first context) */
+#define PGMG_FLAG_NO_SPIN 1048576u /* one GPU: a speculative call waits for its validation with a
+                                      blocking stream wait instead of polling the reply word in
+                                      pinned memory (pgmg_ctx.hip reply_wait) */
 #define PGMG_FLAG_HOST_TRANSPORT 2048u /* world > 1 without RCCL: nccl_unique_id points to
                                        a pgmg_host_transport; every message and reduction
                                        is staged through host memory and handed to the

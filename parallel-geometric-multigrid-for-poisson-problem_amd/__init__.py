@@ -22,7 +22,7 @@ from ._capi import (PGMG_FLAG_LOOPBACK, PGMG_FLAG_NO_CROSS, PGMG_FLAG_NO_GRAPH,
                     PGMG_FLAG_TIME_FINE, PGMG_PRECISION_FP32, PGMG_PRECISION_FP64,
                     PGMG_FLAG_UNFUSED, PGMG_FLAG_NO_RECOMPUTE, PGMG_FLAG_NO_PIN,
                     PGMG_FLAG_NO_R2, PGMG_FLAG_HOST_TRANSPORT, PGMG_FLAG_FAST,
-                    PGMG_FLAG_NO_SPEC_FIRE, PGMG_FLAG_NO_CTILE, PGMG_FLAG_NO_CARRY, PGMG_FLAG_TIME_COMM, PGMG_FLAG_NO_SHUFFLE,
+                    PGMG_FLAG_NO_SPEC_FIRE, PGMG_FLAG_NO_CTILE, PGMG_FLAG_NO_CARRY, PGMG_FLAG_TIME_COMM, PGMG_FLAG_NO_SHUFFLE, PGMG_FLAG_NO_SPIN,
                     PGMG_PROLONG_REFERENCE,
                     PGMG_PROLONG_SYMMETRIC, PGMG_OK, PGMG_ERR_STATE, PgmgConfig, PgmgError,
                     check, load)
@@ -35,7 +35,7 @@ __all__ = [
     "PGMG_PROLONG_REFERENCE", "plan_strips", "LoopbackHub", "unique_id", "rccl_latency",
     "PGMG_PROLONG_SYMMETRIC", "PGMG_PRECISION_FP64", "PGMG_PRECISION_FP32",
     "PGMG_FLAG_STORED_RHS", "PGMG_FLAG_EXACT_DIST", "PGMG_FLAG_SOLO",
-    "PGMG_FLAG_NO_RECOMPUTE", "PGMG_FLAG_NO_PIN", "PGMG_FLAG_NO_R2", "PGMG_FLAG_FAST", "PGMG_FLAG_NO_SPEC_FIRE", "PGMG_FLAG_NO_CTILE", "PGMG_FLAG_NO_CARRY", "PGMG_FLAG_TIME_COMM", "PGMG_FLAG_NO_SHUFFLE",
+    "PGMG_FLAG_NO_RECOMPUTE", "PGMG_FLAG_NO_PIN", "PGMG_FLAG_NO_R2", "PGMG_FLAG_FAST", "PGMG_FLAG_NO_SPEC_FIRE", "PGMG_FLAG_NO_CTILE", "PGMG_FLAG_NO_CARRY", "PGMG_FLAG_TIME_COMM", "PGMG_FLAG_NO_SHUFFLE", "PGMG_FLAG_NO_SPIN",
     "PGMG_FLAG_HOST_TRANSPORT", "HostTransport", "DeviceGrid",
 ]
 

@@ -41,6 +41,7 @@ PGMG_FLAG_NO_CTILE = 65536
 PGMG_FLAG_NO_CARRY = 131072
 PGMG_FLAG_TIME_COMM = 262144
 PGMG_FLAG_NO_SHUFFLE = 524288
+PGMG_FLAG_NO_SPIN = 1048576
 
 PGMG_PRECISION_FP64 = 0
 PGMG_PRECISION_FP32 = 1

@@ -141,6 +141,7 @@ struct pgmg_ctx {
                                   // CheckRefs (read by k_verify_checks), norms, verdicts + any
                                   // (written by k_spec_reply)
     long long chk_cap = 0;
+    unsigned pin_seq = 0;         // the last validation reply's sequence word
     pgmg::Grid bk;                // level-0 solution at the start of the call (rollback)
     // speculative F-cycles (pgmg_ctx.hip "speculative F-cycles"): every bulk check of the
     // climb recorded "does not fire"; a rollback restarts the call's first climb from the

@@ -24,6 +24,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -1862,7 +1863,32 @@ static void spec_need_level(pgmg_ctx *c, int l, int gamma, long long *dbl, long 
 // the pinned validation staging (pgmg_ctx::pin) for cap checks: CheckRefs, norms, verdicts + any
 static size_t pin_norm_off(long long cap) { return ((size_t)cap * sizeof(CheckRef) + 15) / 16 * 16; }
 static size_t pin_flag_off(long long cap) { return pin_norm_off(cap) + (size_t)cap * sizeof(double); }
-static size_t pin_bytes(long long cap) { return pin_flag_off(cap) + ((size_t)cap + 1) * sizeof(unsigned); }
+static size_t pin_seq_off(long long cap) { return pin_flag_off(cap) + ((size_t)cap + 1) * sizeof(unsigned); }
+static size_t pin_bytes(long long cap) { return pin_seq_off(cap) + 64; }
+
+// The validation's wait: poll the reply's sequence word in pinned memory (the call's
+// critical path: a blocking stream wait wakes the host through an interrupt, tens of us
+// later on a busy host, and the next call's kernels queue behind that), asking the runtime
+// every ~20 us whether the stream failed or drained; then the stream wait proper, which returns
+// at once.  One GPU only (row strips wait through their transport).
+static int reply_wait(pgmg_ctx *c, const unsigned *hseq, unsigned seq)
+{
+    if (c->comm == nullptr && !(c->cfg.flags & PGMG_FLAG_NO_SPIN)) {
+        const auto t0 = std::chrono::steady_clock::now();
+        auto next = t0;
+        while (__atomic_load_n(hseq, __ATOMIC_ACQUIRE) != seq) {
+            const auto now = std::chrono::steady_clock::now();
+            if (now < next) continue;
+            next = now + std::chrono::microseconds(20);
+            const hipError_t q = hipStreamQuery(c->s);
+            if (q == hipSuccess) break;
+            if (q != hipErrorNotReady) PGMG_HIPC(q);
+            // a long wait (a slow segment, a contended GPU) stops burning the core
+            if (now - t0 > std::chrono::milliseconds(50)) break;
+        }
+    }
+    return stream_wait(c);
+}
 
 static int spec_reserve(pgmg_ctx *c, long long dbl, long long nchk)
 {
@@ -2159,8 +2185,10 @@ static int spec_validate(pgmg_ctx *c, unsigned *h_out, bool *overflow_out, int n
         int e;
         if (c->comm && (e = c->comm->allreduce_min_u32(c->uflags, n, c->s))) return e;
         // (the checks past n_any -- the carried pre-smooth's -- never roll the call back)
-        launch_spec_reply(c->uflags, c->chk_norm, n, n_any, hf + c->chk_cap, hn, hf, c->s);
-        PGMG_TRY(stream_wait(c));
+        unsigned *hseq = reinterpret_cast<unsigned *>(c->pin + pin_seq_off(c->chk_cap));
+        const unsigned seq = ++c->pin_seq;
+        launch_spec_reply(c->uflags, c->chk_norm, n, n_any, hf + c->chk_cap, hn, hf, hseq, seq, c->s);
+        PGMG_TRY(reply_wait(c, hseq, seq));
         h = hf[c->chk_cap];
         std::memcpy(c->hnorm.data(), hn, n * sizeof(double));
         std::memcpy(c->hflag.data(), hf, n * sizeof(unsigned));

@@ -166,9 +166,10 @@ void launch_verify_checks(const CheckRef *checks, int n, double eps, unsigned *o
                           hipStream_t s);
 
 // the validation's reply, straight into pinned host memory (no copies): any = OR over the
-// first n_any verdicts, and the n norms and verdicts themselves
+// first n_any verdicts, and the n norms and verdicts themselves; then *h_seq = seq (system
+// scope, after the rest: the host polls it)
 void launch_spec_reply(const unsigned *flags, const double *norm, int n, int n_any, unsigned *h_any,
-                       double *h_norm, unsigned *h_flags, hipStream_t s);
+                       double *h_norm, unsigned *h_flags, unsigned *h_seq, unsigned seq, hipStream_t s);
 // a speculative segment's opening: stats_bk = stats (4 words), flags[0, nflags) = 0
 void launch_spec_open(const unsigned long long *stats, unsigned long long *stats_bk, unsigned *flags,
                       int nflags, hipStream_t s);

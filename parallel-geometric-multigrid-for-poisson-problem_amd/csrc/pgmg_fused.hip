@@ -1969,7 +1969,7 @@ void launch_verify_checks(const CheckRef *checks, int n, double eps, unsigned *o
 // operations between the kernels and the wait.
 __global__ __launch_bounds__(256) void k_spec_reply(const unsigned *f, const double *norm, int n,
                                                     int n_any, unsigned *h_any, double *h_norm,
-                                                    unsigned *h_flags)
+                                                    unsigned *h_flags, unsigned *h_seq, unsigned seq)
 {
     __shared__ unsigned any;
     if (threadIdx.x == 0) any = 0u;
@@ -1984,12 +1984,17 @@ __global__ __launch_bounds__(256) void k_spec_reply(const unsigned *f, const dou
     if (v) atomicOr(&any, 1u);
     __syncthreads();
     if (threadIdx.x == 0) *h_any = any;
+    // every store above reaches the host before the sequence word (the host polls it)
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(h_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 void launch_spec_reply(const unsigned *flags, const double *norm, int n, int n_any, unsigned *h_any,
-                       double *h_norm, unsigned *h_flags, hipStream_t s)
+                       double *h_norm, unsigned *h_flags, unsigned *h_seq, unsigned seq, hipStream_t s)
 {
-    k_spec_reply<<<dim3(1), dim3(256), 0, s>>>(flags, norm, n, n_any, h_any, h_norm, h_flags);
+    k_spec_reply<<<dim3(1), dim3(256), 0, s>>>(flags, norm, n, n_any, h_any, h_norm, h_flags, h_seq,
+                                                seq);
 }
 
 __global__ __launch_bounds__(256) void k_spec_open(const unsigned long long *stats,

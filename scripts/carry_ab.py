@@ -22,11 +22,14 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--variants", default="carry,no_carry",
+                    help="comma list of: carry (default flags), no_carry, no_spin")
     a = ap.parse_args()
     import torch  # noqa: F401
     import _pkgload
     pg = _pkgload.load()
-    variants = {"carry": 0, "no_carry": pg.PGMG_FLAG_NO_CARRY}
+    flags = {"carry": 0, "no_carry": pg.PGMG_FLAG_NO_CARRY, "no_spin": pg.PGMG_FLAG_NO_SPIN}
+    variants = {k: flags[k] for k in a.variants.split(",")}
     solvers = {k: pg.Solver(a.n, flags=v) for k, v in variants.items()}
     for r in range(a.rounds):
         for name, s in solvers.items():

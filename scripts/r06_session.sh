@@ -45,6 +45,7 @@ for s in ${STEPS}; do
     shuffle_rep) for i in 1 2 3; do step shuffle_rep${i} 300 env PGMG_LIB=$PWD/parallel-geometric-multigrid-for-poisson-problem_amd/libpgmg_probe.so PGMG_SHUFFLE_MB=${SHUFFLE_MB:-2} python3 scripts/order_probe.py --order ncnc; done ;;
     strace) step strace 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d ${OUT}/strace -o run -- python3 scripts/single_call_trace.py && step strace_an 60 python3 scripts/single_call_trace.py --analyse ${OUT}/strace ;;
     carry_ab) step carry_ab 400 python scripts/carry_ab.py --rounds 3 ;;
+    spin_ab) step spin_ab 400 python scripts/carry_ab.py --rounds 3 --variants carry,no_spin ;;
     levels) step levels 300 python scripts/level_pmc.py run --n 16385 --out ${OUT}/levels ;;
     *) echo "unknown step ${s}" >&2 ;;
   esac

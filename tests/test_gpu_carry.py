@@ -198,3 +198,22 @@ def test_carry_full_size_single_calls(pgmg, golden_cycles):
         assert s.stats()[0] == gold[24]["sweeps"]
         took, made, dropped = s.carry_info()
         assert took >= 20 and made >= took, (took, made, dropped)
+
+
+def test_spin_wait_gives_the_same_words(pgmg, golden_cycles):
+    """The validation's wait polls the reply word in pinned memory (pgmg_ctx.hip reply_wait);
+    PGMG_FLAG_NO_SPIN waits on the stream instead: the same phi, statistics and carries over
+    one-cycle calls at 4097, and the reference's hash after 12 cycles."""
+    gold = _golden(golden_cycles, 4097)
+    out = []
+    for fl in (0, pgmg.PGMG_FLAG_NO_SPIN):
+        with pgmg.Solver(4097, flags=fl) as s:
+            s.set_problem()
+            for _ in range(12):
+                s.vcycle(1)
+                s.residual_norm()
+            assert s.solution_hash(0) == gold[11]["hash"]
+            out.append((s.solution(), s.stats_detail(), s.carry_info()))
+    assert_bitwise(out[0][0], out[1][0], "spin vs stream wait")
+    assert out[0][1] == out[1][1]
+    assert out[0][2] == out[1][2]
