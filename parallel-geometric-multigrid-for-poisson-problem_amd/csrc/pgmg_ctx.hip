@@ -1867,23 +1867,26 @@ static size_t pin_seq_off(long long cap) { return pin_flag_off(cap) + ((size_t)c
 static size_t pin_bytes(long long cap) { return pin_seq_off(cap) + 64; }
 
 // The validation's wait: poll the reply's sequence word in pinned memory (the call's
-// critical path: a blocking stream wait wakes the host through an interrupt, tens of us
-// later on a busy host, and the next call's kernels queue behind that), asking the runtime
-// every ~20 us whether the stream failed or drained; then the stream wait proper, which returns
-// at once.  One GPU only (row strips wait through their transport).
+// critical path: a blocking stream wait wakes the host late -- tens of us on a busy host --
+// and the next call's kernels queue behind that), asking the runtime every ~20 us whether the
+// stream failed or drained.  Once the word arrives the call returns without a stream wait:
+// everything the host reads next is in the pinned reply, and everything it writes next (the
+// staging's CheckRefs) was read by k_verify_checks, which ran before the reply.  A fault
+// surfaces at the runtime's query; a wait past 50 ms (a slow segment, a shared GPU) stops
+// burning the core and blocks.  One GPU only (row strips wait through their transport).
 static int reply_wait(pgmg_ctx *c, const unsigned *hseq, unsigned seq)
 {
     if (c->comm == nullptr && !(c->cfg.flags & PGMG_FLAG_NO_SPIN)) {
         const auto t0 = std::chrono::steady_clock::now();
-        auto next = t0;
-        while (__atomic_load_n(hseq, __ATOMIC_ACQUIRE) != seq) {
+        auto next = t0 + std::chrono::microseconds(20);
+        for (;;) {
+            if (__atomic_load_n(hseq, __ATOMIC_ACQUIRE) == seq) return PGMG_OK;
             const auto now = std::chrono::steady_clock::now();
             if (now < next) continue;
             next = now + std::chrono::microseconds(20);
             const hipError_t q = hipStreamQuery(c->s);
             if (q == hipSuccess) break;
             if (q != hipErrorNotReady) PGMG_HIPC(q);
-            // a long wait (a slow segment, a contended GPU) stops burning the core
             if (now - t0 > std::chrono::milliseconds(50)) break;
         }
     }
