@@ -51,7 +51,8 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 TRACE_PREWARM = 4         # pre-warm calls before the kernel-trace child's timed call
 INST_REPS = 3             # repetitions with per-pass events (the roofline's event-timed median)
-PASSES = (0, 1, 2, 3, 4)  # finest-level passes: sweep, k_pre, k_post, k_postpre, carry pass
+PASSES = (0, 1, 2, 3, 4, 5)  # finest-level passes: sweep, k_pre, k_post, k_postpre, carry pass,
+                             # recompute form
 METRIC = "V-cycles/sec + fine-grid stencil HBM GB/s, 2D Poisson N=16384², fp64"
 
 
@@ -607,8 +608,10 @@ PASS_NAMES = {
     2: "k_post (finest level: prolongation + 2 Jacobi sweeps, fused)",
     3: "k_postpre (finest level, between cycles: prolongation + 2+2 Jacobi sweeps + residual + "
        "restriction, fused)",
-    4: "carry pass (the call's last finest pass: k_postpre that also stores the call's result, "
-       "the next call's pre-smooth carried)",
+    4: "carry pass (the call's last finest pass: k_postpre that stores the call's result instead "
+       "of the next pre-smooth, whose restriction is carried to the next call)",
+    5: "recompute form (the first finest pass of a call that took the carry: k_postpre that "
+       "recomputes the carried pre-smooth from phi in registers)",
 }
 
 

@@ -250,9 +250,10 @@ int pgmg_pointer_is_device(const void *p, int *is_device);
  * problem's later F calls decide in-stream); PGMG_FLAG_EXACT_DIST turns that off. */
 /* The carry (r06; one GPU, cross-fused contexts, problems set with pgmg_set_problem): a
  * speculative V call ends with a finest-level pass that also runs the NEXT cycle's pre-smooth,
- * residual and restriction (MultiGrid.hpp:57-94's first half) into context-owned buffers and
- * checks it; the next pgmg_vcycle on the same problem starts from them instead of running its
- * own first pass.  Entries that only read the problem (pgmg_get_solution, pgmg_solution_hash,
+ * residual and restriction (MultiGrid.hpp:57-94's first half), keeps the restriction in a
+ * context-owned buffer and checks it; the next pgmg_vcycle on the same problem starts from it
+ * instead of running its own first pass (its first finest pass recomputes the pre-smooth from
+ * phi in registers: no pass and no byte is added).  Entries that only read the problem (pgmg_get_solution, pgmg_solution_hash,
  * pgmg_residual_norm, pgmg_stats*, pgmg_sync ...) keep the carry; every entry that changes phi,
  * f, eps, the flags or the cycle kind (pgmg_set_problem*, pgmg_set_eps, pgmg_wcycle,
  * pgmg_fcycle, pgmg_bench_sweep, pgmg_phi_device -- its pointer allows writes -- ) drops it.
@@ -363,7 +364,8 @@ int pgmg_precision(pgmg_ctx *ctx, int *precision, int *elem_bytes);
  * the last call (needs PGMG_FLAG_TIME_FINE; synchronous).  pass 0: plain Jacobi
  * sweep (unfused path), 1: fused pre-smooth+residual+restriction (k_pre),
  * 2: fused prolongation+post-smooth (k_post), 3: cross-cycle k_postpre, 4: the carry pass
- * (k_postpre that also stores the call's result). */
+ * (k_postpre that stores the call's result instead of the next pre-smooth), 5: the recompute
+ * form (the first k_postpre of a call that took the carry). */
 int pgmg_fine_pass_time(pgmg_ctx *ctx, int pass, int *count, double *mean_ms);
 /* What the launches the last pgmg_fine_pass_time(pass) averaged were: the kernel symbol of the
  * last of them (demangled, e.g. "pgmg::k_postpre_lds<double, false, true, 2>"; "" when none was

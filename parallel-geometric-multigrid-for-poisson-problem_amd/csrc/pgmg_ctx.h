@@ -82,13 +82,13 @@ struct pgmg_ctx {
         int used = 0;
     };
     // finest-level kernel timing (PGMG_FLAG_TIME_FINE): 0 plain sweep, 1 k_pre, 2 k_post
-    EventPool tpool[5];           // 3: k_postpre, 4: the carry pass
+    EventPool tpool[6];           // 3: k_postpre, 4: the carry pass, 5: the recompute form
     // per timed pass: the kernels and algorithmic bytes of the launches timed since the last
     // pgmg_fine_pass_time (LaunchNote), and what that call averaged (pgmg_fine_pass_info)
-    double tbytes[5] = {0, 0, 0, 0, 0};
-    const void *tkern[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-    double info_bytes[5] = {0, 0, 0, 0, 0};
-    const void *info_kern[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    double tbytes[6] = {};
+    const void *tkern[6] = {};
+    double info_bytes[6] = {};
+    const void *info_kern[6] = {};
     bool fused = false;           // v1 = v2 = 1: two fused passes per level
     bool cross = false;           // finest level fuses post(k) with pre(k+1) across cycles
     bool recompute = true;        // levels entered with x0 = 0 recompute x2 in k_post
@@ -185,11 +185,10 @@ struct pgmg_ctx {
     bool defer_post = false;
     void *pend_pr = nullptr;
     // the carry (pgmg_ctx.hip "carry"): a speculative V call on the context's own grids ends
-    // with the carry pass, which also runs the next cycle's pre-smooth into Y and its
-    // restriction into lv[1].F; the next V call starts from them when no entry touched the
-    // problem in between
-    pgmg::Grid Y;                 // fourth level-0 grid (one GPU, cross-fused contexts)
-    bool carry = false;           // Y / lv[1].F hold the validated pre-smooth of lv[0].A
+    // with the carry pass, which stores its result and the next cycle's restriction into
+    // lv[1].F; the next V call starts from them (its first finest pass recomputes the
+    // pre-smooth) when no entry touched the problem in between
+    bool carry = false;           // lv[1].F holds the validated restriction of lv[0].A's pre-smooth
     bool carry_use = false;       // the segment being enqueued starts from the carry
     bool carry_make = false;      // the segment being enqueued ends with the carry pass
     bool carry_made = false;      // ... and it did

@@ -844,19 +844,23 @@ static PostArgsT<T> make_post(pgmg_ctx *c, const T *phi, T *x2)
 // harness, ParallelTestRunner.cu:172-173), pays the opening k_pre and the closing k_post of
 // every call: two passes over the finest grid where a multi-cycle call runs one k_postpre.
 // So a speculative V call on the context's own grids (one GPU) ends with the CARRY PASS: the
-// last cycle's k_postpre, which also stores x2 -- the call's result -- besides the next
-// cycle's pre-smoothed iterate x4 (into the fourth level-0 grid Y) and its restricted
-// residual (into lv[1].F).  The pre-smooth's early-exit check is logged beside the call's own
-// checks and validated with them; it never rolls the call back: a carry whose check could fire
-// is dropped (carry_n[2]) and the next call runs its own k_pre.  The next pgmg_vcycle on the
-// same problem starts from the carry: no k_pre, straight into the coarse levels
-// (MultiGrid.hpp:57-94 from line 69 on), and its first finest pass counts the carried
-// pre-smooth's two sweeps (sw_adj).  Every entry that changes phi, f, eps, the flags or the
-// cycle kind drops the carry (run_cycles takes it or drops it at every call); caller-owned
-// arrays (pgmg_set_problem_device) never carry: the caller may change them between calls.
-// A rollback of the call that took a carry reruns from lv[0].A, which the carry pass left
-// untouched, with its own k_pre.  Cost: the x2 store, 8 B per fine point (~0.45 ms at 16385)
-// against the k_pre it saves (16 B per fine point + the restriction, ~0.98 ms).
+// last cycle's k_postpre, which stores x2 -- the call's result -- where a k_postpre stores the
+// next cycle's pre-smoothed iterate x4, and the next cycle's restricted residual into lv[1].F
+// as usual (so it moves the bytes of a k_postpre).  The pre-smooth's early-exit check is
+// logged beside the call's own checks and validated with them; it never rolls the call back: a
+// carry whose check could fire is dropped (carry_n[2]) and the next call runs its own k_pre.
+// The next pgmg_vcycle on the same problem starts from the carry: no k_pre, straight into the
+// coarse levels (MultiGrid.hpp:57-94 from line 69 on); its first finest pass is the RECOMPUTE
+// FORM of k_postpre, which reads the previous call's x2 (lv[0].A), runs the carried
+// pre-smooth again in registers -- the carry pass's own expressions on the same values, so
+// bitwise the x4 it did not store -- and goes on as a k_postpre; it counts the carried
+// pre-smooth's two sweeps (sw_adj).  A one-cycle call that took the carry and makes the next
+// runs one finest pass, both forms at once.  Every entry that changes phi, f, eps, the flags or
+// the cycle kind drops the carry (run_cycles takes it or drops it at every call); caller-owned
+// arrays (pgmg_set_problem_device) never carry: the caller may change them between calls.  A
+// rollback of the call that took a carry reruns from lv[0].A, which no pass of the call writes,
+// with its own k_pre.  Cost: none in bytes (the carry pass and the recompute form each move a
+// k_postpre's); two more Jacobi stages per point in the recompute form.
 // ---------------------------------------------------------------------------
 template <class T>
 static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
@@ -864,32 +868,32 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
     Level &L = c->lv[0], &C = c->lv[1];
     const bool dist = is_dist(c, 0);
     const StripRows sr = strip_rows(L, C);
-    Grid gA = L.A, gB = L.B, gS = c->S, gY = c->Y;
+    Grid gA = L.A, gB = L.B, gS = c->S;
     T *A = G<T>(gA), *B = G<T>(gB);
-    T *S = G<T>(gS), *Y = G<T>(gY);   // Y: nullptr without a fourth grid
+    T *S = G<T>(gS);
     // speculative call: no rare path can run, so the scratch S is free and the level-0
-    // buffers rotate through B and S (and Y); A (the call's input) is never written and a
-    // rollback restarts from it
+    // buffers rotate through B and S; A (the call's input) is never written and a rollback
+    // restarts from it
     const bool lean = c->lean;
-    auto grid_of = [&](const T *p) -> const Grid * {
-        return p == A ? &gA : p == B ? &gB : p == S ? &gS : &gY;
-    };
+    auto grid_of = [&](const T *p) -> const Grid * { return p == A ? &gA : p == B ? &gB : &gS; };
     // (an external input is followed by B: the first k_pre writes B, then B <-> S (lean) or
-    // B <-> A, both free of the input; a carried input Y is followed by B as well)
+    // B <-> A, both free of the input; a carried input -- A itself -- is followed by B as well)
     auto next_of = [&](const T *p) -> T * { return lean ? (p == B ? S : B) : (p == B ? A : B); };
     // the caller's array (pgmg_set_problem_device) as the call's input / output
     const T *in = c->x_in != nullptr ? static_cast<const T *>(c->x_in) : A;
     T *const xout = static_cast<T *>(c->x_out);
     const int np = fused_blocks(L.N, sr.jc0, sr.jc1);
     const int npp = postpre_blocks(L.N, sr.jc0, sr.jc1);
-    // the carry: taken (this call starts from Y and lv[1].F) / made (it ends with the carry
-    // pass); both only on speculative calls on the context's own grids, one GPU
-    const bool take = c->carry_use && lean && !dist && Y != nullptr && c->x_in == nullptr;
+    const int npp_rc = postpre_blocks(L.N, sr.jc0, sr.jc1, true);   // the recompute form's
+    // the carry: made (the call ends with the carry pass) / taken (it starts from lv[0].A's
+    // pre-smooth and lv[1].F, its first finest pass the recompute form -- a k_postpre, so a
+    // call of one cycle takes it only when it also makes the next); both only on speculative
+    // calls on the context's own grids, one GPU
+    const bool make = c->carry_make && lean && !dist && xout == nullptr && !c->defer_post;
+    const bool take = c->carry_use && lean && !dist && c->x_in == nullptr && (n > 1 || make);
     if (tuning_int("PGMG_ROLE_TRACE", 0))   // measurement build: which grids play which role
-        fprintf(stderr, "roles A %p B %p S %p Y %p n %d take %d\n", gA.base, gB.base, gS.base, gY.base, n,
-                (int)(c->carry_use && lean && Y != nullptr));
-    const bool make = c->carry_make && lean && !dist && Y != nullptr && xout == nullptr &&
-                      !c->defer_post;
+        fprintf(stderr, "roles A %p B %p S %p n %d take %d make %d\n", gA.base, gB.base, gS.base, n,
+                (int)take, (int)make);
     c->carry_use = false;
     c->carry_made = false;
     c->carry_took = take;
@@ -900,9 +904,10 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
     fa.eps = c->cfg.eps;
     fa.stats = c->stats;
     int e, ev;
-    T *pr;   // pre-smoothed solution of the current cycle
+    T *pr;   // pre-smoothed solution of the current cycle (a taken carry: the solution A)
+    bool recompute = take;   // the next finest pass recomputes pr's pre-smooth
     if (take) {
-        pr = Y;
+        pr = A;
     } else {
         // cycle 1: pre-smooth (+ residual, restriction) A -> B
         if (dist && (e = c->comm->halo(gA, L, 4, c->s))) return e;
@@ -950,18 +955,22 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         q.fast = (c->cfg.flags & PGMG_FLAG_FAST) != 0 && !dist;
         q.sw_adj = sw_adj;
         sw_adj = 0;
+        q.recompute = recompute ? 1 : 0;
+        recompute = false;
         return q;
     };
     for (int k = 1; k < n; ++k) {
         T *nx = next_of(pr);
         if (dist && (e = c->comm->halo_end(c->s))) return e;
+        const int nq = recompute ? npp_rc : npp;
         PostPreArgsT<T> q = postpre_args(pr, nx);
-        q.partials1 = lean ? chk_partials(c, npp, 0) : c->partials;
-        q.partials2 = lean ? chk_partials(c, npp, 0) : c->partials2;
+        q.partials1 = lean ? chk_partials(c, nq, 0) : c->partials;
+        q.partials2 = lean ? chk_partials(c, nq, 0) : c->partials2;
         q.partials3 = (dist && !lean) ? c->partials3 : nullptr;   // lean: no rare path runs
-        ev = timed_begin(c, 3);
+        const int slot = q.recompute ? 5 : 3;   // (the recompute form: its own timed slot)
+        ev = timed_begin(c, slot);
         if ((e = launch_postpre(q, c->s))) return e;
-        if ((e = timed_end(c, 3, ev))) return e;
+        if ((e = timed_end(c, slot, ev))) return e;
         const double *g3 = nullptr;   // all-rank {post, pre, pre-from-x1} sums
         if (lean) {
             pr = nx;
@@ -1027,44 +1036,39 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
         c->pend_pr = pr;
         return PGMG_OK;
     }
-    // the solution's buffer becomes L.A, the carried iterate's Y (every level-0 grid mirrors
-    // the boundary, so any may play any role); an external output holds the solution instead
-    // (the level-0 grids keep their roles)
-    auto set_roles = [&](const T *sol, const T *carried) {
-        const Grid *all[4] = {&gA, &gB, &gS, &gY};
+    // the solution's buffer becomes L.A (every level-0 grid mirrors the boundary, so any may
+    // play any role); an external output holds the solution instead (the level-0 grids keep
+    // their roles)
+    auto set_roles = [&](const T *sol) {
+        const Grid *all[3] = {&gA, &gB, &gS};
         std::vector<Grid> rest;
         for (const Grid *g : all)
-            if (g->base && g != grid_of(sol) && (carried == nullptr || g != grid_of(carried)))
-                rest.push_back(*g);
+            if (g != grid_of(sol)) rest.push_back(*g);
         L.A = *grid_of(sol);
-        if (carried != nullptr) c->Y = *grid_of(carried);
-        size_t i = 0;
-        L.B = rest[i++];
-        c->S = rest[i++];
-        if (carried == nullptr && gY.base) c->Y = rest[i++];
+        L.B = rest[0];
+        c->S = rest[1];
     };
     if (make) {
-        // the carry pass: x2 (the result) into a grid that is neither the input A nor pr, x4 of
-        // the next cycle into another; its post check is this call's, its pre check the carry's
-        T *free2[2] = {nullptr, nullptr};
-        int m = 0;
-        for (T *g : {B, S, Y})
-            if (g != pr && m < 2) free2[m++] = g;
-        T *const out = free2[0], *const nx = free2[1];
-        PostPreArgsT<T> q = postpre_args(pr, nx);
+        // the carry pass: x2 (the result) into a grid that is neither the input A nor pr (pr is
+        // A itself when this one pass also takes the carry); its post check is this call's, its
+        // pre check the carry's
+        T *const out = (pr == B) ? S : B;
+        const int nq = recompute ? npp_rc : npp;
+        PostPreArgsT<T> q = postpre_args(pr, nullptr);
         q.x2 = out;
         q.sw_adj -= 2;   // the pre-smooth's sweeps count in the call that uses them
-        q.partials1 = chk_partials(c, npp, 0);
-        q.partials2 = chk_log(c, npp, 0, 0);
+        q.partials1 = chk_partials(c, nq, 0);
+        q.partials2 = chk_log(c, nq, 0, 0);
         c->carry_chk = (int)c->chks.size() - 1;
         if (q.partials1 == nullptr || q.partials2 == nullptr) return set_err(PGMG_ERR_STATE, "carry pass: check log");
         ev = timed_begin(c, 4);
         if ((e = launch_postpre(q, c->s))) return e;
         if ((e = timed_end(c, 4, ev))) return e;
-        set_roles(out, nx);
+        set_roles(out);
         c->carry_made = true;
         return PGMG_OK;
     }
+    if (recompute) return set_err(PGMG_ERR_STATE, "a taken carry without a k_postpre");
     T *out = xout != nullptr ? xout : next_of(pr);
     if (dist && (e = c->comm->halo_end(c->s))) return e;
     PostArgsT<T> po = make_post<T>(c, pr, out);
@@ -1081,7 +1085,7 @@ static int enqueue_cross_cycles(pgmg_ctx *c, int n, int gamma)
     }
     if (xout != nullptr) {
     } else if (lean) {
-        set_roles(out, nullptr);
+        set_roles(out);
     } else if (out != A) {
         std::swap(L.A, L.B);
     }
@@ -1205,7 +1209,6 @@ int pgmg_destroy(pgmg_ctx *c)
     free_grid(c->ftop);
     if (c->ppflags) (void)hipFree(c->ppflags);
     free_grid(c->S);
-    free_grid(c->Y);
     free_grid(c->Ffmg);
     for (auto &g : c->Ffmg_l) free_grid(g);
     if (c->fmg_tab) (void)hipFree(c->fmg_tab);
@@ -1295,18 +1298,14 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         }
     }
 
-    // (measurement build: PGMG_Y_ORDER 1 allocates the carry grid before every level grid,
-    // PGMG_DUMMY_MB a dummy buffer of that size there: placement probes)
-    const bool want_y = cfg->world <= 1 && !(cfg->flags & PGMG_FLAG_NO_CARRY);
-    const int y_order = tuning_int("PGMG_Y_ORDER", 0);
+    // (measurement build: PGMG_DUMMY_MB a dummy buffer of that size before every level grid:
+    // placement probes)
     Grid dummy;
     if (tuning_int("PGMG_DUMMY_MB", 0) > 0) {
         Level Ld = c->lv[0];
         Ld.hi = Ld.lo + (int)(((size_t)tuning_int("PGMG_DUMMY_MB", 0) << 20) / ((size_t)Ld.P * Ld.es));
         rc = alloc_grid(dummy, Ld);
     }
-    if (rc == PGMG_OK && want_y && y_order == 1 && c->nb >= 1 && c->lv[0].N >= 2049)
-        rc = alloc_grid(c->Y, c->lv[0], 0, c->shuffle);
     for (int l = 0; l < (int)c->lv.size() && rc == PGMG_OK; ++l) {
         Level &L = c->lv[l];
         if (!L.on_this_rank) continue;
@@ -1336,6 +1335,8 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
         if (nbk > maxblocks) maxblocks = nbk;
         nbk = postpre_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2);
         if (nbk > maxblocks) maxblocks = nbk;
+        nbk = postpre_blocks(L.N, L.lo / 2, (L.hi < L.N ? L.hi : L.N - 1) / 2, true);
+        if (nbk > maxblocks) maxblocks = nbk;
         nbk = std::max(tile_np(c, l, false), tile_np(c, l, true));
         if (nbk > maxblocks) maxblocks = nbk;
         // k_post_r2 (the finest k_post of consecutive F-cycles, 116-column stride): its
@@ -1347,11 +1348,6 @@ int pgmg_create(pgmg_ctx **out, const pgmg_config *cfg)
     }
     const size_t st0 = (size_t)tuning_int("PGMG_GRID_STAGGER", 0);
     if (rc == PGMG_OK && c->cross) rc = alloc_grid(c->S, c->lv[0], 3 * st0, c->shuffle);
-    // the carry's fourth level-0 grid (one GPU; see "carry"): ~2.15 GB at N = 16385 fp64
-    if (rc == PGMG_OK && c->cross && c->comm == nullptr && !(cfg->flags & PGMG_FLAG_NO_CARRY) &&
-        !c->Y.base && y_order == 0)
-        rc = alloc_grid(c->Y, c->lv[0], 4 * st0, c->shuffle);
-    if (!(c->cross && c->comm == nullptr) && c->Y.base) free_grid(c->Y);
     (void)dummy;   // (the probe's dummy buffer stays allocated: the context leaks it)
     // partial sums of k_postpre's second and third checks (cross-cycle fusion, and the
     // F-cycle's fused smooth(3)), its decision flags
@@ -1566,7 +1562,6 @@ int pgmg_set_problem(pgmg_ctx *c, const double *phi0, const double *f)
     // the cross-cycle rare-path scratch S mirrors phi's boundary too (its passes never
     // write boundary rows/columns, the k_pre that reads it passes them through)
     if (c->S.base) PGMG_TRY(mirror(c->S));
-    if (c->Y.base) PGMG_TRY(mirror(c->Y));   // the carry's grid likewise
     if ((e = setup_rhs(c, f, r0, r1))) return e;
     return problem_reset(c);
 }
@@ -2207,7 +2202,10 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
 {
     Level &L0 = c->lv[0];
     const int np0 = fused_blocks(L0.N, L0.lo / 2, (L0.hi < L0.N ? L0.hi : L0.N - 1) / 2);
-    const int npp = c->cross ? postpre_blocks(L0.N, L0.lo / 2, (L0.hi < L0.N ? L0.hi : L0.N - 1) / 2) : 0;
+    // (k_postpre's partials, in any form: the recompute form's tiles are narrower)
+    const int npp = c->cross ? std::max(postpre_blocks(L0.N, L0.lo / 2, (L0.hi < L0.N ? L0.hi : L0.N - 1) / 2),
+                                        postpre_blocks(L0.N, L0.lo / 2, (L0.hi < L0.N ? L0.hi : L0.N - 1) / 2, true))
+                             : 0;
     long long d1, k1;
     spec_need_level(c, 1, gamma, &d1, &k1);
     // (level 0 visits level 1 gamma times per cycle)
@@ -2236,7 +2234,7 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
         if (c->spec_off) return run_cycles_plain(c, ncycles, gamma, first);
         const bool last = seg == ncycles;
         const bool seg_first = first;
-        const Grid A0 = L0.A, B0 = L0.B, S0 = c->S, Y0 = c->Y;
+        const Grid A0 = L0.A, B0 = L0.B, S0 = c->S;
         if (!rotate) {
             if (!c->bk.base && (e = alloc_grid(c->bk, L0))) return e;
             HIPC(hipMemcpyAsync(c->bk.base, L0.A.base, L0.A.bytes, hipMemcpyDeviceToDevice, c->s));
@@ -2301,7 +2299,6 @@ static int run_cycles_spec(pgmg_ctx *c, int ncycles, int gamma)
             L0.A = A0;
             L0.B = B0;
             c->S = S0;
-            c->Y = Y0;
             c->carry = false;
             if (!rotate)
                 HIPC(hipMemcpyAsync(L0.A.base, c->bk.base, L0.A.bytes, hipMemcpyDeviceToDevice, c->s));
@@ -2704,7 +2701,6 @@ static int enqueue_fcycle(pgmg_ctx *c, int opt = 0)
         launch_zero_frame(G<T>(L.A), L.P, L.N, c->s, r0, r1);
         launch_zero_frame(G<T>(L.B), L.P, L.N, c->s, r0, r1);
         if (l == 0 && c->S.base) launch_zero_frame(G<T>(c->S), L.P, L.N, c->s, r0, r1);   // S mirrors too
-        if (l == 0 && c->Y.base) launch_zero_frame(G<T>(c->Y), L.P, L.N, c->s, r0, r1);   // and Y
         const bool use_pin = !(c->cfg.flags & PGMG_FLAG_NO_PIN);
         if (c->fused && use_pin) {
             // the V-cycle's k_pre computes the prolongation on the fly (PIN): no separate
@@ -3091,7 +3087,7 @@ int pgmg_vcycle_bytes(pgmg_ctx *c, double *bytes)
 
 int pgmg_fine_pass_bytes(pgmg_ctx *c, int pass, double *bytes)
 {
-    if (!c || !bytes || pass < 0 || pass > 4) return set_err(PGMG_ERR_ARG, "bad argument");
+    if (!c || !bytes || pass < 0 || pass > 5) return set_err(PGMG_ERR_ARG, "bad argument");
     if (c->nb == 0) return set_err(PGMG_ERR_STATE, "no bulk level");
     const Level &L = c->lv[0], &C = c->lv[1];
     const double n = (double)(L.u1 - L.u0) * (L.N - 2);
@@ -3105,7 +3101,8 @@ int pgmg_fine_pass_bytes(pgmg_ctx *c, int pass, double *bytes)
     case 1: b = (16.0 + fb) * n + 8.0 * nc; break;             // x0, (f) in; x2, rc out
     case 2: b = (16.0 + fb) * n + 8.0 * nc; break;             // phi, (f,) ec in; x2 out
     case 3: b = (16.0 + fb) * n + 16.0 * nc; break;            // phi, (f,) ec; x4, rc
-    case 4: b = (24.0 + fb) * n + 16.0 * nc; break;            // the same + x2 (carry pass)
+    case 4: b = (16.0 + fb) * n + 16.0 * nc; break;            // carry pass: x2 for x4
+    case 5: b = (16.0 + fb) * n + 16.0 * nc; break;            // recompute form: phi = x2
     }
     *bytes = b * (L.es / 8.0);
     return PGMG_OK;
@@ -3181,7 +3178,7 @@ int pgmg_bench_sweep(pgmg_ctx *c, int reps, double *ms)
 
 int pgmg_fine_pass_time(pgmg_ctx *c, int pass, int *count, double *mean_ms)
 {
-    if (!c || pass < 0 || pass > 4) return set_err(PGMG_ERR_ARG, "bad argument");
+    if (!c || pass < 0 || pass > 5) return set_err(PGMG_ERR_ARG, "bad argument");
     PGMG_TRY(stream_wait(c));
     auto &pool = c->tpool[pass];
     double tot = 0.0;
@@ -3203,7 +3200,7 @@ int pgmg_fine_pass_time(pgmg_ctx *c, int pass, int *count, double *mean_ms)
 
 int pgmg_fine_pass_info(pgmg_ctx *c, int pass, char *symbol, int len, double *bytes)
 {
-    if (!c || pass < 0 || pass > 4 || (symbol && len < 1)) return set_err(PGMG_ERR_ARG, "bad argument");
+    if (!c || pass < 0 || pass > 5 || (symbol && len < 1)) return set_err(PGMG_ERR_ARG, "bad argument");
     if (bytes) *bytes = c->info_bytes[pass];
     if (symbol) {
         std::string name;

@@ -85,10 +85,10 @@ struct PostArgsT {
 // (the finest level between consecutive cycles of one pgmg_vcycle call)
 template <class T>
 struct PostPreArgsT {
-    const T *phi;               // pre-smoothed solution of cycle k
+    const T *phi;               // pre-smoothed solution of cycle k (recompute: its phi)
     const T *ec;                // coarse correction of cycle k
     const T *f;
-    T *x4;                      // pre-smoothed solution of cycle k+1
+    T *x4;                      // pre-smoothed solution of cycle k+1 (not the carry pass's)
     T *rc;                      // coarse right-hand side of cycle k+1
     double *partials1;          // sum r(x1)^2 (post-smooth check)
     double *partials2;          // sum r(x3)^2 (pre-smooth check)
@@ -105,9 +105,14 @@ struct PostPreArgsT {
     int rows_per_block;
     int fast;                   // PGMG_FLAG_FAST (one GPU, f regenerated or stored)
     // non-null: the carry pass, the LAST finest pass of a call that also runs the next call's
-    // pre-smooth (pgmg_ctx.hip "carry"): x2, the call's result, is stored here besides x4
+    // pre-smooth (pgmg_ctx.hip "carry"): x2, the call's result, is stored here instead of x4
+    // (x4 = nullptr); its restricted residual goes to rc as usual
     T *x2;
     int sw_adj;                 // stats[0] += 4 + sw_adj (the carry pass: -2; see PostArgsT)
+    // nonzero: the recompute form, the first finest pass of a call that took the carry: phi
+    // is the previous call's x2 and the pass runs its pre-smooth (the carry pass's, bitwise)
+    // before the correction
+    int recompute;
 };
 
 struct FixArgsF {
@@ -146,8 +151,8 @@ template <class T> void launch_post_fixup(const FixArgsF &a, const PostArgsT<T> 
 template <class T>
 int launch_pre_rare(const FixArgsF &f, const PreArgsT<T> &a, bool x0_zero, hipStream_t s);
 template <class T> int launch_post_rare(const FixArgsF &f, const PostArgsT<T> &a, hipStream_t s);
-// k_postpre's workgroups (check partials)
-int postpre_blocks(int N, int jc0, int jc1);
+// k_postpre's workgroups (check partials); rc: the recompute form's (112-column tiles)
+int postpre_blocks(int N, int jc0, int jc1, bool rc = false);
 template <class T> int launch_postpre(const PostPreArgsT<T> &a, hipStream_t s);
 // fused smooth(3): x4 of a.phi into a.x4 with the three checks' partial sums
 // (partials1 r(x1), partials3 r(x2), partials2 r(x3)); then the decision + rare path

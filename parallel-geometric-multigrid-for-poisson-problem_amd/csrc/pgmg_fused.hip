@@ -938,8 +938,17 @@ __device__ __forceinline__ V2<T> rsn(V2<T> up, V2<T> ce, V2<T> dn, Nbr<T> n, V2<
 // row pair.  Coarse rows live in a ring of 3 (pair g reads coarse rows g and g+1).
 // ---------------------------------------------------------------------------
 constexpr int kPPWaves = 4;   // waves per k_postpre block (8-wave blocks measured equal, r02)
+// The recompute form (OPT 256, the first finest pass of a call that took the carry): two more
+// Jacobi stages in front, so two more columns of margin per side (112-column stride) and two
+// more lead rows
+constexpr int kPPStrideRC = 112, kPPMarginRC = 8;
+template <int OPT> constexpr int pp_stride() { return (OPT & 256) ? kPPStrideRC : kPPStride; }
+template <int OPT> constexpr int pp_margin() { return (OPT & 256) ? kPPMarginRC : kPPMargin; }
 constexpr int kPPLdsRow = kPPWaves * kPPStride + 2 * kPPMargin + 4;          // doubles per row
 constexpr int kPPLdsCoarse = kPPWaves * (kPPStride / 2) + kPPMargin + 8;     // per coarse row
+static_assert(kPPWaves * kPPStrideRC + 2 * kPPMarginRC + 4 <= kPPLdsRow &&
+                  kPPWaves * (kPPStrideRC / 2) + kPPMarginRC + 8 <= kPPLdsCoarse,
+              "the recompute form's windows fit the LDS rows");
 // fp32 (r05): the rows are staged from 16-byte loads of FOUR columns per lane (8-byte lane
 // loads stream at 0.54-0.70x the 16-byte rate, MI355X_MICROARCH.md), starting two columns
 // left of the window (column L0 - 2 is 16-byte aligned: column 1 of every row sits on a
@@ -990,7 +999,11 @@ template <class T> using PPC = typename std::conditional<pp_qc<T>(), float4, V2<
 // multiply per point replaces 8 bytes per point of the pass (28 -> 20 B/pt).
 // OPT (compile-time, result-identical): 2 non-temporal x4 stores, 4 non-temporal rc
 // stores, 64 the F-cycle's smooth(3) (no correction, no restriction), 128 the carry pass
-// (x2 stored too: the last pass of a call that hands the next call its pre-smooth).
+// (the last pass of a call that hands the next call its pre-smooth: x2 -- the call's result --
+// is stored INSTEAD of x4; the next call recomputes x4 from it), 256 the recompute form
+// (the first pass of a call that took the carry: the input is the previous call's x2, whose
+// pre-smooth -- two Jacobi stages, the carry pass's own expressions, bitwise its x4 -- runs in
+// front of the correction; the pipeline's rows lag two more).
 // Logical block of the 2D grid (x: column block, y: band).
 struct Blk {
     int x, y;
@@ -1001,11 +1014,11 @@ constexpr int kPPR = 2;   // rows per LDS slot (a row pair)
 // Row pairs of loads in flight per wave (register sets).  3 also makes the guard-free loop
 // body 6 rows, the period of the row windows (no window copies: 141 -> 129 VALU per row);
 // the fp64 instantiations with more live state (streamed f, the strips' third sum, the
-// F-cycle's four-sweep form) keep 2, which fits 256 VGPRs without spilling.
+// F-cycle's four-sweep form, the recompute form) keep 2, which fits 256 VGPRs without spilling.
 template <class T, bool R2, bool GENF, int OPT>
 constexpr int pp_depth()
 {
-    return sizeof(T) == 4 ? PGMG_F32_DEPTH : ((GENF && !R2 && !(OPT & (64 | 32))) ? 3 : 2);
+    return sizeof(T) == 4 ? PGMG_F32_DEPTH : ((GENF && !R2 && !(OPT & (64 | 32 | 256))) ? 3 : 2);
 }
 // Lane t's 16-byte (fp32: 8-byte) column pair of a row segment starting at `base`; lanes
 // t >= n read 0 (descriptor range check).  The descriptor is built from wave-uniform values.
@@ -1082,6 +1095,10 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     constexpr bool QC = pp_qc<T>(), QS = pp_qs<T>();
     constexpr int SH = pp_sh<T>();
     constexpr int R = kPPR;
+    constexpr bool RC = (OPT & 256) != 0;           // the recompute form
+    constexpr bool CARRY = (OPT & 128) != 0;        // the carry pass
+    constexpr int ST = pp_stride<OPT>(), MG = pp_margin<OPT>();
+    constexpr int LAG = RC ? 2 : 0;                 // rows the correction lags the input
     const int N = a.N, Nc = a.Nc;
     const long long P = a.P, Pc = a.Pc;
     const int jcb = a.jc0 + bk.y * a.rows_per_block;
@@ -1100,10 +1117,10 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     // loader geometry: the block window starts at column L0 (odd: 16-byte aligned pairs)
     const int wpb = blockDim.x >> 6;
     const int t = threadIdx.x;
-    const int L0 = kPPStride * wpb * bk.x + 1 - kPPMargin;
-    const int npairs = (kPPStride * wpb + 2 * kPPMargin) / 2;
+    const int L0 = ST * wpb * bk.x + 1 - MG;
+    const int npairs = (ST * wpb + 2 * MG) / 2;
     const int cc0 = (L0 - 1) >> 1;                               // first coarse column
-    const int ncc = (kPPStride / 2) * wpb + kPPMargin + 2;
+    const int ncc = (ST / 2) * wpb + MG + 2;
     // OPT & 64 (F-cycle smooth(3)): no coarse correction, no restriction
     // Row loads through buffer descriptors (one per row, built from wave-uniform values):
     // VMEM-only loads whose out-of-range lanes (past the window or the grid's last column)
@@ -1127,8 +1144,8 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
     // this wave's window in the LDS rows
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int xo = kPPStride * w + 2 * lane;
-    const int co = (kPPStride / 2) * w + lane;
+    const int xo = ST * w + 2 * lane;
+    const int co = (ST / 2) * w + lane;
     // fp32 quads: the window's 2 * npairs columns from L0 - 2 (nq4 quads; nvq of them inside
     // the loaded range, the rest read 0); coarse: ncc columns from cc0 (ncq quads, nveq valid).
     // A quad past the old pair/element range loads columns past the grid's last one or the
@@ -1138,7 +1155,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
     // fp32 x4 stores: odd lane l (16-byte aligned column) stores its pair and lane l+1's as
     // one quad when both own theirs; an owning odd lane without an owning partner (the grid's
     // right edge) stores its pair alone
-    const bool own_next = lane + 1 < kPPMargin / 2 + kPPStride / 2 && k.c + 2 <= N - 2;
+    const bool own_next = lane + 1 < MG / 2 + ST / 2 && k.c + 2 <= N - 2;
     const int xoff16 = (QS && (lane & 1) && k.own && own_next) ? xoff : kOOB;
     const int xoff8 = QS ? (((lane & 1) && k.own && !own_next) ? xoff : kOOB) : xoff;
 
@@ -1146,10 +1163,14 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
             d0 = z, d1 = z;
     V2<T> f1 = z, f2 = z, f3 = z, f4 = z, f5 = z;  // f[i-1], f[i-2], ..., f[i-5]
     V2<T> q1 = z, q2 = z, q3 = z, q4 = z;          // hh * f[i-1], ..., hh * f[i-4]
+    V2<T> f6 = z, f7 = z, q5 = z, q6 = z;          // RC: the windows two rows longer
+    V2<T> p0 = z, p1 = z, a0 = z, a1 = z;          // RC: input rows i-2, i-1; stage-1 rows i-3, i-2
     double acc1 = 0.0, acc2 = 0.0, acc3 = 0.0;
-    const int i_begin = 2 * jcb - 6;
-    const int ng = (2 * (jce - jcb) + 11 + R - 1) / R;   // row pairs (uniform over the block)
-    const int m0 = i_begin >> 1;                          // coarse row of the first pair
+    const int i_begin = 2 * jcb - 6 - LAG;
+    // row pairs (uniform over the block): the input rows 2jcb-6-LAG .. 2jce+4+LAG
+    const int ng = (2 * (jce - jcb) + 11 + 2 * LAG + R - 1) / R;
+    // coarse row of the first pair (RC: the correction of pair gi's rows lags one pair)
+    const int m0 = (i_begin >> 1) - (RC ? 1 : 0);
     auto ring = [](int m) { return (m + 3 * 4096) % 3; };  // m >= -3
 
     if (t < 2 * R * 4) {   // the 4 pad doubles past the window (read by spare lanes only)
@@ -1249,13 +1270,26 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                 f0 = mk2<T>((T)(fxa * sy), (T)(fxb * sy));
             }
             const V2<T> q0 = mk2<T>(hh * f0.x, hh * f0.y);
-            const V2<T> fq2 = f2, fq3 = f3, fq4 = f4, fq5 = f5;
-            const V2<T> hq1 = q1, hq2 = q2, hq3 = q3, hq4 = q4;
-            const V2<T> e2 = (OPT & 64) ? xr : add_prolong<T, EDGE>(xr, ii, cr0, crn0, cr1, crn1, pc, Nc);
             constexpr bool FAST = (OPT & 16) != 0;
+            // RC: the carry pass's pre-smooth of the input (its g / h stages, the same
+            // expressions on the same values: bitwise its x4), row ii-2; then every stage below
+            // runs on row L = ii - 2 with the f windows two rows further back
+            V2<T> xin = xr;
+            if constexpr (RC) {
+                const V2<T> a2 = FAST ? jsum<T, EDGE>(nsum<T>(p0, p1, xr, nbr<T>(p1)), p1, q1, k, boundary_row(ii - 1, N))
+                                      : jsh<T, EDGE>(p0, p1, xr, nbr<T>(p1), q1, k, boundary_row(ii - 1, N));
+                xin = FAST ? jsum<T, EDGE>(nsum<T>(a0, a1, a2, nbr<T>(a1)), a1, q2, k, boundary_row(ii - 2, N))
+                           : jsh<T, EDGE>(a0, a1, a2, nbr<T>(a1), q2, k, boundary_row(ii - 2, N));
+                p0 = p1; p1 = xr;
+                a0 = a1; a1 = a2;
+            }
+            const int L = ii - LAG;
+            const V2<T> fq2 = RC ? f4 : f2, fq3 = RC ? f5 : f3, fq4 = RC ? f6 : f4, fq5 = RC ? f7 : f5;
+            const V2<T> hq1 = RC ? q3 : q1, hq2 = RC ? q4 : q2, hq3 = RC ? q5 : q3, hq4 = RC ? q6 : q4;
+            const V2<T> e2 = (OPT & 64) ? xin : add_prolong<T, EDGE>(xin, L, cr0, crn0, cr1, crn1, pc, Nc);
             // post-smooth sweep 1: x1 row ii-1
-            const V2<T> b2 = FAST ? jsum<T, EDGE>(nsum<T>(e0, e1, e2, nbr<T>(e1)), e1, hq1, k, boundary_row(ii - 1, N))
-                                  : jsh<T, EDGE>(e0, e1, e2, nbr<T>(e1), hq1, k, boundary_row(ii - 1, N));
+            const V2<T> b2 = FAST ? jsum<T, EDGE>(nsum<T>(e0, e1, e2, nbr<T>(e1)), e1, hq1, k, boundary_row(L - 1, N))
+                                  : jsh<T, EDGE>(e0, e1, e2, nbr<T>(e1), hq1, k, boundary_row(L - 1, N));
             const Nbr<T> nb1 = nbr<T>(b1), nc1 = nbr<T>(c1), ng1 = nbr<T>(g1);
             // FAST: the neighbour sums of x1 row ii-2 and x3 row ii-4, each shared by a sweep
             // and a check
@@ -1266,7 +1300,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
 #else
                 const V2<T> r1 = FAST ? rsum<T>(sb, b1, fq2, ih) : rsn<T>(b0, b1, b2, nb1, fq2, ih);
 #endif
-                const int row = ii - 2;
+                const int row = L - 2;
                 if constexpr (chk_sel<T>()) {
                     acc1 = chk_acc<T>(acc1, r1, row >= olo && row < ohi && k.own, k.by);
                 } else if (row >= olo && row < ohi && k.own) {
@@ -1274,16 +1308,16 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                     if (!k.by) acc1 = sqacc(acc1, r1.y);
                 }
             }
-            // post-smooth sweep 2: x2 row ii-2 (= phi of cycle k+1)
-            const V2<T> c2 = FAST ? jsum<T, EDGE>(sb, b1, hq2, k, boundary_row(ii - 2, N))
-                                  : jsh<T, EDGE>(b0, b1, b2, nb1, hq2, k, boundary_row(ii - 2, N));
-            if constexpr ((OPT & 128) != 0) {   // the carry pass: x2 is the call's result
-                const int xb2 = (ii - 2 >= olo && ii - 2 < ohi) ? xbytes : 0;
-                buf_store_row<T, (OPT & 2) ? 1 : 0>(a.x2 + (long long)(ii - 2) * P + L0, xb2, xoff, c2);
+            // post-smooth sweep 2: x2 row L-2 (= phi of cycle k+1)
+            const V2<T> c2 = FAST ? jsum<T, EDGE>(sb, b1, hq2, k, boundary_row(L - 2, N))
+                                  : jsh<T, EDGE>(b0, b1, b2, nb1, hq2, k, boundary_row(L - 2, N));
+            if constexpr (CARRY) {   // the carry pass: x2 is the call's result (x4 is not stored)
+                const int xb2 = (L - 2 >= olo && L - 2 < ohi) ? xbytes : 0;
+                buf_store_row<T, (OPT & 2) ? 1 : 0>(a.x2 + (long long)(L - 2) * P + L0, xb2, xoff, c2);
             }
             if (R2) {   // r(x2) on row ii-3
                 const V2<T> r2 = rsn<T>(c0, c1, c2, nc1, fq3, ih);
-                const int row = ii - 3;
+                const int row = L - 3;
                 if constexpr (chk_sel<T>()) {
                     acc3 = chk_acc<T>(acc3, r2, row >= olo && row < ohi && k.own, k.by);
                 } else if (row >= olo && row < ohi && k.own) {
@@ -1292,8 +1326,8 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                 }
             }
             // pre-smooth sweep 1: x3 row ii-3
-            const V2<T> g2 = FAST ? jsum<T, EDGE>(nsum<T>(c0, c1, c2, nc1), c1, hq3, k, boundary_row(ii - 3, N))
-                                  : jsh<T, EDGE>(c0, c1, c2, nc1, hq3, k, boundary_row(ii - 3, N));
+            const V2<T> g2 = FAST ? jsum<T, EDGE>(nsum<T>(c0, c1, c2, nc1), c1, hq3, k, boundary_row(L - 3, N))
+                                  : jsh<T, EDGE>(c0, c1, c2, nc1, hq3, k, boundary_row(L - 3, N));
             const V2<T> sgg = FAST ? nsum<T>(g0, g1, g2, ng1) : z;
             {   // pre check: r(x3) on row ii-4
 #if PGMG_PP_CHEAPCHK
@@ -1301,7 +1335,7 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
 #else
                 const V2<T> r3 = FAST ? rsum<T>(sgg, g1, fq4, ih) : rsn<T>(g0, g1, g2, ng1, fq4, ih);
 #endif
-                const int row = ii - 4;
+                const int row = L - 4;
                 if constexpr (chk_sel<T>()) {
                     acc2 = chk_acc<T>(acc2, r3, row >= olo && row < ohi && k.own, k.by);
                 } else if (row >= olo && row < ohi && k.own) {
@@ -1310,14 +1344,14 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
                 }
             }
             // pre-smooth sweep 2: x4 row ii-4 (stored)
-            const V2<T> h2 = FAST ? jsum<T, EDGE>(sgg, g1, hq4, k, boundary_row(ii - 4, N))
-                                  : jsh<T, EDGE>(g0, g1, g2, ng1, hq4, k, boundary_row(ii - 4, N));
+            const V2<T> h2 = FAST ? jsum<T, EDGE>(sgg, g1, hq4, k, boundary_row(L - 4, N))
+                                  : jsh<T, EDGE>(g0, g1, g2, ng1, hq4, k, boundary_row(L - 4, N));
             // branch-free: rows outside the band get a zero-record descriptor, lanes that do
             // not own their pair an out-of-range offset (every step issues the same memory
             // instructions, so the compiler can count its waits)
-            {
-                const int xb = (ii - 4 >= olo && ii - 4 < ohi) ? xbytes : 0;
-                T *xrow = a.x4 + (long long)(ii - 4) * P + L0;
+            if constexpr (!CARRY) {
+                const int xb = (L - 4 >= olo && L - 4 < ohi) ? xbytes : 0;
+                T *xrow = a.x4 + (long long)(L - 4) * P + L0;
                 if constexpr (QS) {   // lane l+1's pair by DPP; odd lanes store the quad
                     const float4 v4 = make_float4(h2.x, h2.y, dpp_shl(h2.x), dpp_shl(h2.y));
                     buf_store_quad<(OPT & 2) ? 1 : 0>(reinterpret_cast<float *>(xrow), xb, xoff16, v4);
@@ -1330,9 +1364,9 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
             // r(x4) on row ii-5
             const V2<T> d2 = FAST ? rsum<T>(nsum<T>(h0, h1, h2, nbr<T>(h1)), h1, fq5, ih)
                                   : rsn<T>(h0, h1, h2, nbr<T>(h1), fq5, ih);
-            // restriction: rows ii-7, ii-6, ii-5 = 2jc-1, 2jc, 2jc+1 when ii is even
+            // restriction: rows L-7, L-6, L-5 = 2jc-1, 2jc, 2jc+1 when L is even
             if (!(OPT & 64) && (s & 1) == 0) {
-                const int jc = (ii - 6) >> 1;
+                const int jc = (L - 6) >> 1;
                 const T m2 = dpp_shl(d1.x);
                 const T u2 = wprev;               // = dpp_shl(d0.x): row ii-7 was d2 two rows ago
                 const T w2 = dpp_shl(d2.x);
@@ -1348,6 +1382,10 @@ __device__ __forceinline__ void postpre_lds_run(const PostPreArgsT<T> &a, const 
             g0 = g1; g1 = g2;
             h0 = h1; h1 = h2;
             d0 = d1; d1 = d2;
+            if constexpr (RC) {
+                f7 = f6; f6 = f5;
+                q6 = q5; q5 = q4;
+            }
             f5 = f4; f4 = f3; f3 = f2; f2 = f1; f1 = f0;
             q4 = q3; q3 = q2; q2 = q1; q1 = q0;
         }
@@ -1404,11 +1442,13 @@ void k_postpre_lds(PostPreArgsT<T> a)
     __shared__ __attribute__((aligned(16))) T sf[2][kPPR][GENF ? 1 : pp_lds_row<T>()];
     __shared__ __attribute__((aligned(16))) T se[3][pp_lds_coarse<T>()];
     const Blk bk{(int)blockIdx.x, (int)blockIdx.y};
-    const Cols k = lane_cols_t<kPPStride, kPPMargin>(a.N, bk.x);
-    // the band's rows 2jcb-6 .. 2jce+5 (see postpre_lds_run): does it reach row 0 or N-1?
+    const Cols k = lane_cols_t<pp_stride<OPT>(), pp_margin<OPT>()>(a.N, bk.x);
+    // the band's rows 2jcb-6 .. 2jce+5 (RC: from 2jcb-8; see postpre_lds_run): does it reach
+    // row 0 or N-1?
     const int jcb = a.jc0 + bk.y * a.rows_per_block;
     const int jce = min(jcb + a.rows_per_block, a.jc1);
-    const bool edge_rows = 2 * jcb - 6 <= 0 || 2 * jce + 6 >= a.N - 1;
+    constexpr int lag = (OPT & 256) ? 2 : 0;
+    const bool edge_rows = 2 * jcb - 6 - lag <= 0 || 2 * jce + 6 + lag >= a.N - 1;
     if (k.edge || edge_rows)
         postpre_lds_run<T, R2, GENF, true, OPT>(a, k, red, sx, sf, se, bk);
     else
@@ -1629,15 +1669,17 @@ static int post_spans(const PostArgsT<T> &a, int t, int gx, int r, bool f_read, 
 template <class T>
 static int postpre_spans(const PostPreArgsT<T> &a, int t, int gx, int r, bool coarse)
 {
-    const Span sp = band_rows(a.jc0, a.jc1, r, 6, 11, kPPR);
+    const int lag = a.recompute ? 2 : 0;   // the recompute form: 2 more rows each end
+    const int ST = a.recompute ? kPPStrideRC : kPPStride, MG = a.recompute ? kPPMarginRC : kPPMargin;
+    const Span sp = band_rows(a.jc0, a.jc1, r, 6 + lag, 11 + 2 * lag, kPPR);
     if (!sp.any) return PGMG_OK;
     const int wpb = t / 64;
-    const int npairs = (kPPStride * wpb + 2 * kPPMargin) / 2;
-    const int ncc = (kPPStride / 2) * wpb + kPPMargin + 2;
+    const int npairs = (ST * wpb + 2 * MG) / 2;
+    const int ncc = (ST / 2) * wpb + MG + 2;
     long long c1 = -1, e0 = 0, e1 = -1;
     bool first = true;
     for (int bx = 0; bx < gx; ++bx) {
-        const int L0 = kPPStride * wpb * bx + 1 - kPPMargin;
+        const int L0 = ST * wpb * bx + 1 - MG;
         const int nvx = std::max(0, std::min(npairs, (a.N - 1 - L0) / 2 + 1));
         if (nvx > 0) c1 = std::max(c1, (long long)L0 + 2 * nvx - 1);
         const int cc0 = (L0 - 1) >> 1;
@@ -1648,14 +1690,14 @@ static int postpre_spans(const PostPreArgsT<T> &a, int t, int gx, int r, bool co
             first = false;
         }
     }
-    const long long c0 = 1 - kPPMargin;
+    const long long c0 = 1 - MG;
     if (c1 < c0) return PGMG_OK;
     PGMG_SPAN(a.phi, a.P, sp.r0, sp.r1, c0, c1, "k_postpre phi");
     if (a.gfx == nullptr) PGMG_SPAN(a.f, a.P, sp.r0, sp.r1, c0, c1, "k_postpre f");
-    if (coarse && e1 >= e0)   // coarse rows m0 .. m0 + ng of a band (m0 = jcb - 3)
-        PGMG_SPAN(a.ec, a.Pc, a.jc0 - 3, fdiv2(sp.r1 + 1), e0, e1, "k_postpre coarse correction");
+    if (coarse && e1 >= e0)   // coarse rows m0 .. m0 + ng of a band (m0 = jcb - 3; RC jcb - 5)
+        PGMG_SPAN(a.ec, a.Pc, a.jc0 - 3 - lag, fdiv2(sp.r1 + 1), e0, e1, "k_postpre coarse correction");
     const int olo = std::max(2 * a.jc0, a.row_lo), ohi = std::min(2 * a.jc1, a.row_hi);
-    PGMG_SPAN(a.x4, a.P, olo, ohi - 1, 1, a.N - 1, "k_postpre x4");
+    if (a.x4 != nullptr) PGMG_SPAN(a.x4, a.P, olo, ohi - 1, 1, a.N - 1, "k_postpre x4");
     if (a.x2 != nullptr) PGMG_SPAN(a.x2, a.P, olo, ohi - 1, 1, a.N - 1, "k_postpre x2 (carry pass)");
     if (coarse && a.rc != nullptr) {
         const int clo = std::max(a.jc0, std::max(1, a.rc_lo));
@@ -1775,49 +1817,74 @@ static int pp_target(int jc0, int jc1)
     return tuning_int("PGMG_PP_BLOCKS", (2048 / kPPWaves) * rounds);   // 512 resident at 4 waves
 }
 
-int postpre_blocks(int N, int jc0, int jc1)
+int postpre_blocks(int N, int jc0, int jc1, bool rc)
 {
     int t, gx, gy, r;
-    fused_geometry(N, jc0, jc1, &t, &gx, &gy, &r, kPPStride, pp_target(jc0, jc1), kPPWaves);
+    fused_geometry(N, jc0, jc1, &t, &gx, &gy, &r, rc ? kPPStrideRC : kPPStride, pp_target(jc0, jc1),
+                   kPPWaves);
     return gx * gy;
 }
 
 // The cross-cycle finest-level pass.  OPT 2: non-temporal x4 stores (x4 is read again
 // only by the next cycle's pass; r01: 1.18 vs 1.20 ms; non-temporal rc stores no gain).
+// Forms (one GPU unless noted): the plain pass; R2 (row strips: the third sum); the carry pass
+// (x2 stored instead of x4, OPT 128); the recompute form (OPT 256), alone or as a carry pass
+// too (a one-cycle call that took the carry and makes the next); FAST (fp64) of each.
 // Every launch path below launches: there is no configuration that returns without the pass.
+template <class T, bool GENF, int OPT>
+static void launch_pp_form(const PostPreArgsT<T> &a, dim3 g, dim3 b, hipStream_t s)
+{
+    launchk(k_postpre_lds<T, false, GENF, OPT>, g, b, s, a);
+}
+template <class T, int OPT>
+static void launch_pp_form(const PostPreArgsT<T> &a, bool genf, dim3 g, dim3 b, hipStream_t s)
+{
+    if (genf) launch_pp_form<T, true, OPT>(a, g, b, s);
+    else launch_pp_form<T, false, OPT>(a, g, b, s);
+}
+
 template <class T>
 int launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
 {
+    const bool rc = a0.recompute != 0, carry = a0.x2 != nullptr;
     int t, gx, gy, r;
-    fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, kPPStride, pp_target(a0.jc0, a0.jc1),
-                   kPPWaves);
+    fused_geometry(a0.N, a0.jc0, a0.jc1, &t, &gx, &gy, &r, rc ? kPPStrideRC : kPPStride,
+                   pp_target(a0.jc0, a0.jc1), kPPWaves);
+    if ((rc || carry) && a0.partials3 != nullptr) return PGMG_ERR_ARG;   // one GPU only
+    if (carry == (a0.x4 != nullptr)) return PGMG_ERR_ARG;                // x2 replaces x4
     if (const int e = postpre_spans(a0, t, gx, r, true)) return e;
     PostPreArgsT<T> a = a0;
     a.rows_per_block = r;
     const dim3 g(gx, gy), b(t);
     const bool genf = a.gfx != nullptr;
-    if (a.x2 != nullptr) {   // the carry pass (one GPU: no third sum)
-        if (a.partials3 != nullptr) return PGMG_ERR_ARG;
-        if (a.fast && sizeof(T) == 8) {
-            if (genf) launchk(k_postpre_lds<T, false, true, 2 | 16 | 128>, g, b, s, a);
-            else launchk(k_postpre_lds<T, false, false, 2 | 16 | 128>, g, b, s, a);
-        } else if (genf) launchk(k_postpre_lds<T, false, true, 2 | 128>, g, b, s, a);
-        else launchk(k_postpre_lds<T, false, false, 2 | 128>, g, b, s, a);
-    } else if (a.partials3 != nullptr) {
+    const bool fast = a.fast && sizeof(T) == 8;   // FAST mode: fp64
+    if (a.partials3 != nullptr) {
         if (genf) launchk(k_postpre_lds<T, true, true, 2>, g, b, s, a);
         else launchk(k_postpre_lds<T, true, false, 2>, g, b, s, a);
+    } else if constexpr (sizeof(T) == 8) {
+        switch ((fast ? 16 : 0) | (carry ? 128 : 0) | (rc ? 256 : 0)) {
+        case 0: launch_pp_form<T, 2>(a, genf, g, b, s); break;
+        case 16: launch_pp_form<T, 2 | 16>(a, genf, g, b, s); break;
+        case 128: launch_pp_form<T, 2 | 128>(a, genf, g, b, s); break;
+        case 144: launch_pp_form<T, 2 | 16 | 128>(a, genf, g, b, s); break;
+        case 256: launch_pp_form<T, 2 | 256>(a, genf, g, b, s); break;
+        case 272: launch_pp_form<T, 2 | 16 | 256>(a, genf, g, b, s); break;
+        case 384: launch_pp_form<T, 2 | 128 | 256>(a, genf, g, b, s); break;
+        default: launch_pp_form<T, 2 | 16 | 128 | 256>(a, genf, g, b, s); break;
+        }
     } else {
-        if (a.fast && sizeof(T) == 8) {   // FAST mode (one GPU, fp64)
-            if (genf) launchk(k_postpre_lds<T, false, true, 2 | 16>, g, b, s, a);
-            else launchk(k_postpre_lds<T, false, false, 2 | 16>, g, b, s, a);
-        } else if (genf) launchk(k_postpre_lds<T, false, true, 2>, g, b, s, a);
-        else launchk(k_postpre_lds<T, false, false, 2>, g, b, s, a);
+        switch ((carry ? 128 : 0) | (rc ? 256 : 0)) {
+        case 0: launch_pp_form<T, 2>(a, genf, g, b, s); break;
+        case 128: launch_pp_form<T, 2 | 128>(a, genf, g, b, s); break;
+        case 256: launch_pp_form<T, 2 | 256>(a, genf, g, b, s); break;
+        default: launch_pp_form<T, 2 | 128 | 256>(a, genf, g, b, s); break;
+        }
     }
-    // phi, f (unless regenerated), ec in; x4, rc (and the carry pass's x2) out
+    // phi (x2 of the previous call in the recompute form), f (unless regenerated), ec in; x4
+    // (x2 in the carry pass), rc out: the same bytes in every form
     const double n = row_pts(std::max(2 * a.jc0, a.row_lo), std::min(2 * a.jc1, a.row_hi), a.N);
     const double nc = row_pts(a.rc_lo, a.rc_hi, a.Nc);
-    g_last_launch.bytes = (8.0 * n * (2 + (genf ? 0 : 1) + (a.x2 != nullptr ? 1 : 0)) + 16.0 * nc) *
-                          sizeof(T) / 8.0;
+    g_last_launch.bytes = (8.0 * n * (2 + (genf ? 0 : 1)) + 16.0 * nc) * sizeof(T) / 8.0;
     return PGMG_OK;
 }
 

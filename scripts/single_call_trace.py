@@ -6,6 +6,7 @@ and between calls, and the carry pass."""
 import argparse
 import csv
 import pathlib
+import re
 import sys
 import time
 
@@ -37,8 +38,12 @@ def analyse(d):
                 name = r.get("Kernel_Name") or r.get("Direction") or "copy"
                 ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
     ev.sort()
-    # the calls: split at the carry passes (one per call, its last finest pass)
-    carry = [i for i, e in enumerate(ev) if "130>" in e[2]]
+    # the calls: split at the carry passes (one per call, its last finest pass: a k_postpre_lds
+    # whose OPT has bit 128)
+    def is_carry(name):
+        m = re.search(r"k_postpre_lds<[^>]*, (\d+)>", name)
+        return m is not None and int(m.group(1)) & 128
+    carry = [i for i, e in enumerate(ev) if is_carry(e[2])]
     print(len(ev), "events,", len(carry), "carry passes")
     for a, b in zip(carry[-11:-1], carry[-10:]):
         seg = ev[a + 1:b + 1]

@@ -116,15 +116,17 @@ def test_fractions_physical_on_a_stub_line():
     n = 16383.0 ** 2
     build = "live rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this build; libpgmg.so sha256:0123456789abcdef"
     key = "k_postpre_lds<double,false,true,2>"
-    leg = {"passes": [(1, 0, 0.0), (3, 19, 1.02), (4, 1, 1.45)],
-           "passes_reps": {1: [], 3: [1.03, 1.02, 1.02], 4: [1.45, 1.45, 1.45]},
+    leg = {"passes": [(1, 0, 0.0), (3, 18, 1.02), (4, 1, 1.06), (5, 1, 1.1)],
+           "passes_reps": {1: [], 3: [1.03, 1.02, 1.02], 4: [1.06, 1.06, 1.06], 5: [1.1, 1.1, 1.1]},
            "info": {3: ("pgmg::k_postpre_lds<double, false, true, 2>", 16 * n + 16 * n / 4),
-                    4: ("pgmg::k_postpre_lds<double, false, true, 130>", 24 * n + 16 * n / 4)},
-           "bytes": {1: 16 * n, 3: 16 * n, 4: 24 * n}, "gen": True}
+                    4: ("pgmg::k_postpre_lds<double, false, true, 130>", 16 * n + 16 * n / 4),
+                    5: ("pgmg::k_postpre_lds<double, false, true, 258>", 16 * n + 16 * n / 4)},
+           "bytes": {1: 16 * n, 3: 16 * n, 4: 16 * n, 5: 16 * n}, "gen": True}
     pmc = {key: 1.078 * (16 * n + 16 * n / 4)}
     trace = {key: (95, 1.06, 1.036, 19)}
     rows = bench.roofline_rows(leg, pmc, build, trace, "trace")
-    assert [r["symbol"] for r in rows] == [key, "k_postpre_lds<double,false,true,130>"]
+    assert [r["symbol"] for r in rows] == [key, "k_postpre_lds<double,false,true,258>",
+                                           "k_postpre_lds<double,false,true,130>"]
     assert rows[0]["traffic_ratio"] == 1.078 and rows[1]["traffic"] is None
     ops = []
     for name, nbytes, sweeps, passes, ms in (("v=1", 48 * n, 2, 1, 1.38), ("v=100", 2424 * n, 101, 51, 70.6),
