@@ -1530,7 +1530,9 @@ static void fused_geometry(int N, int jc0, int jc1, int *threads, int *gx, int *
         if (pts > (1LL << 23)) {
             // ~22k points per workgroup, at least one round of the 512 resident (8193 on 8
             // strips: 37+28 -> 34+24 us), at most 3072
-            target = tuning_int("PGMG_FUSED_BLOCKS", (int)std::min(3072LL, std::max(512LL, pts / 21845)));
+            // (measurement build: PGMG_FUSED_BLOCKS_BIG for the levels of N >= 8193 alone)
+            const int dflt = (int)std::min(3072LL, std::max(512LL, pts / 21845));
+            target = tuning_int("PGMG_FUSED_BLOCKS", pts >= (1LL << 25) ? tuning_int("PGMG_FUSED_BLOCKS_BIG", dflt) : dflt);
         } else {
             // latency-bound levels (N <= 2049): short bands (~8k points per workgroup);
             // measured at N = 16385: 2049 26+20 -> 23+18 us, 1025 13+11 -> 12+10, 513..129
