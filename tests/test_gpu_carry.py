@@ -217,3 +217,33 @@ def test_spin_wait_gives_the_same_words(pgmg, golden_cycles):
     assert_bitwise(out[0][0], out[1][0], "spin vs stream wait")
     assert out[0][1] == out[1][1]
     assert out[0][2] == out[1][2]
+
+
+@pytest.mark.parametrize("variant", ["stored", "fast", "fast_stored", "f32", "f32_stored"])
+@pytest.mark.parametrize("N", [1025, 4097])
+def test_carry_forms_equal_uncarried(pgmg, plan, variant, N):
+    """Every compiled form of the carry pass and of the recompute form (f streamed or
+    regenerated, FAST, fp32) against the same calls with PGMG_FLAG_NO_CARRY: the same phi and
+    statistics, bit for bit -- the recompute form's two stages reproduce the carry pass's
+    pre-smooth exactly (FAST: the shared-sum expressions too)."""
+    plan(cross_min_n=9)
+    flags = {"stored": pgmg.PGMG_FLAG_STORED_RHS, "fast": pgmg.PGMG_FLAG_FAST,
+             "fast_stored": pgmg.PGMG_FLAG_FAST | pgmg.PGMG_FLAG_STORED_RHS,
+             "f32": 0, "f32_stored": pgmg.PGMG_FLAG_STORED_RHS}[variant]
+    dtype = "f32" if variant.startswith("f32") else "f64"
+    out = []
+    for fl in (flags, flags | pgmg.PGMG_FLAG_NO_CARRY):
+        with pgmg.Solver(N, flags=fl, dtype=dtype) as s:
+            s.set_problem()
+            for k in range(10):
+                s.vcycle(1)
+                if k % 4 == 3:
+                    s.residual_norm()
+            s.vcycle(3)
+            s.vcycle(1)
+            out.append((s.solution(), s.stats_detail(), s.carry_info()))
+    assert_bitwise(out[0][0], out[1][0], f"{variant} carry vs no carry")
+    assert out[0][1] == out[1][1]
+    took, made, dropped = out[0][2]
+    assert took >= 9 and made >= took, out[0][2]
+    assert out[1][2] == (0, 0, 0)
