@@ -225,7 +225,9 @@ def test_carry_forms_equal_uncarried(pgmg, plan, variant, N):
     """Every compiled form of the carry pass and of the recompute form (f streamed or
     regenerated, FAST, fp32) against the same calls with PGMG_FLAG_NO_CARRY: the same phi and
     statistics, bit for bit -- the recompute form's two stages reproduce the carry pass's
-    pre-smooth exactly (FAST: the shared-sum expressions too)."""
+    pre-smooth exactly.  FAST (a tolerance mode: its cross-cycle passes use shared-sum
+    expressions, its k_pre / k_post the reference's, so where a call starts and ends moves the
+    last bits) is held to tests/test_gpu_fast.py's tolerance, 1e-12 relative, and equal sweeps."""
     plan(cross_min_n=9)
     flags = {"stored": pgmg.PGMG_FLAG_STORED_RHS, "fast": pgmg.PGMG_FLAG_FAST,
              "fast_stored": pgmg.PGMG_FLAG_FAST | pgmg.PGMG_FLAG_STORED_RHS,
@@ -242,7 +244,12 @@ def test_carry_forms_equal_uncarried(pgmg, plan, variant, N):
             s.vcycle(3)
             s.vcycle(1)
             out.append((s.solution(), s.stats_detail(), s.carry_info()))
-    assert_bitwise(out[0][0], out[1][0], f"{variant} carry vs no carry")
+    if variant.startswith("fast"):
+        d = out[0][0] - out[1][0]
+        rel = np.linalg.norm(d) / np.linalg.norm(out[1][0])
+        assert rel <= 1e-12 and np.abs(d).max() <= 1e-12, (variant, rel)
+    else:
+        assert_bitwise(out[0][0], out[1][0], f"{variant} carry vs no carry")
     assert out[0][1] == out[1][1]
     took, made, dropped = out[0][2]
     assert took >= 9 and made >= took, out[0][2]
