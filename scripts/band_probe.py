@@ -45,6 +45,9 @@ def main():
     ap.add_argument("--n", type=int, default=16385)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--values", default="0,1536,2048")
+    ap.add_argument("--knob", default="PGMG_FUSED_BLOCKS_BIG",
+                    help="the measurement build's knob to set (PGMG_PP_BLOCKS: k_postpre's "
+                         "workgroup target)")
     ap.add_argument("--child", action="store_true")
     a = ap.parse_args()
     if a.child:
@@ -53,12 +56,12 @@ def main():
         for v in a.values.split(","):
             env = dict(os.environ)
             if v != "0":
-                env["PGMG_FUSED_BLOCKS_BIG"] = v
+                env[a.knob] = v
             p = subprocess.run([sys.executable, __file__, "--child", "--n", str(a.n)], env=env,
                                capture_output=True, text=True, timeout=300)
             line = p.stdout.strip().splitlines()[-1] if p.stdout.strip() else "{}"
             d = json.loads(line)
-            d.update({"round": r, "blocks_big": int(v), "rc": p.returncode})
+            d.update({"round": r, "knob": a.knob, "value": int(v), "rc": p.returncode})
             if p.returncode:
                 d["stderr"] = p.stderr[-800:]
             print(json.dumps(d), flush=True)
