@@ -113,6 +113,9 @@ struct PostPreArgsT {
     // is the previous call's x2 and the pass runs its pre-smooth (the carry pass's, bitwise)
     // before the correction
     int recompute;
+    // nonzero: XCD-aware tile order (measurement knob PGMG_PP_XCD): the workgroups the hardware
+    // places on one XCD (linear id = x mod 8) take a contiguous run of tiles
+    int xcd;
 };
 
 struct FixArgsF {

@@ -1441,7 +1441,14 @@ void k_postpre_lds(PostPreArgsT<T> a)
     __shared__ __attribute__((aligned(16))) T sx[2][kPPR][pp_lds_row<T>()];
     __shared__ __attribute__((aligned(16))) T sf[2][kPPR][GENF ? 1 : pp_lds_row<T>()];
     __shared__ __attribute__((aligned(16))) T se[3][pp_lds_coarse<T>()];
-    const Blk bk{(int)blockIdx.x, (int)blockIdx.y};
+    Blk bk{(int)blockIdx.x, (int)blockIdx.y};
+    if (a.xcd) {   // XCD x (linear ids = x mod 8) gets tiles [x q + min(x, r), ...) in order
+        const int nb = (int)(gridDim.x * gridDim.y), id = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+        const int q = nb >> 3, r = nb & 7, x = id & 7;
+        const int t = x * q + min(x, r) + (id >> 3);
+        bk.x = t % (int)gridDim.x;
+        bk.y = t / (int)gridDim.x;
+    }
     const Cols k = lane_cols_t<pp_stride<OPT>(), pp_margin<OPT>()>(a.N, bk.x);
     // the band's rows 2jcb-6 .. 2jce+5 (RC: from 2jcb-8; see postpre_lds_run): does it reach
     // row 0 or N-1?
@@ -1857,6 +1864,7 @@ int launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
     if (const int e = postpre_spans(a0, t, gx, r, true)) return e;
     PostPreArgsT<T> a = a0;
     a.rows_per_block = r;
+    a.xcd = tuning_int("PGMG_PP_XCD", 0);
     const dim3 g(gx, gy), b(t);
     const bool genf = a.gfx != nullptr;
     const bool fast = a.fast && sizeof(T) == 8;   // FAST mode: fp64
