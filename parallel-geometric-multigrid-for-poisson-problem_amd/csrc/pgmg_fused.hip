@@ -167,11 +167,23 @@ __device__ __forceinline__ Cols lane_cols_t(int N, int bx = -1)
 
 __device__ __forceinline__ Cols lane_cols(int N, int bx = -1) { return lane_cols_t<120, 4>(N, bx); }
 
-// Logical (column block, band) of this workgroup
-__device__ __forceinline__ void fused_block(int &bx, int &by)
+// Logical (column block, band) of this workgroup.  xcd: XCD-aware order -- the hardware
+// deals linear workgroup ids round-robin to the 8 XCDs (id mod 8), so XCD x takes the ids
+// x, x+8, ...; those get one contiguous run of tiles, and tiles that share halo columns run
+// side by side behind the same L2 (k_postpre: 1.1 % per V-cycle)
+__device__ __forceinline__ void xcd_tile(int &bx, int &by)
+{
+    const int nb = (int)(gridDim.x * gridDim.y), id = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+    const int q = nb >> 3, r = nb & 7, x = id & 7;
+    const int t = x * q + min(x, r) + (id >> 3);
+    bx = t % (int)gridDim.x;
+    by = t / (int)gridDim.x;
+}
+__device__ __forceinline__ void fused_block(int &bx, int &by, bool xcd = false)
 {
     bx = blockIdx.x;
     by = blockIdx.y;
+    if (xcd) xcd_tile(bx, by);
 }
 
 // deterministic sum over the block (fixed tree) -> thread 0
@@ -259,7 +271,7 @@ __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red)
     constexpr int R = 2 * PAIRS;  // rows loaded per iteration (and prefetched ahead)
     if (a.cond != nullptr && *a.cond == 0u) return;  // conditional (rare-path) launch
     int lbx, lby;
-    fused_block(lbx, lby);
+    fused_block(lbx, lby, (a.nt & 16) != 0);
     const Cols k = lane_cols(a.N, lbx);
     const int N = a.N;
     const long long P = a.P;
@@ -468,7 +480,7 @@ __device__ __forceinline__ void pre_body(const PreArgsT<T> &a, double *red)
     row_loop<R, PIN ? 0 : 3>(i_begin, i_end, full_at, iter);
     if constexpr (!S1 || S1P) {
         const double sum = fused_block_sum(acc, red);
-        if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = sum;
+        if (threadIdx.x == 0) a.partials[lby * gridDim.x + lbx] = sum;
     }
 }
 
@@ -572,7 +584,7 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
     constexpr int R = 2 * PAIRS;
     if (a.cond != nullptr && *a.cond == 0u) return;  // conditional (rare-path) launch
     int lbx, lby;
-    fused_block(lbx, lby);
+    fused_block(lbx, lby, (a.nt & 16) != 0);
     // R2: 116-column stride, 6-column margin (kR2Stride): see k_post_r2
     const Cols k = R2 ? lane_cols_t<kR2Stride, 6>(a.N, lbx) : lane_cols(a.N, lbx);
     const int N = a.N, Nc = a.Nc;
@@ -773,7 +785,7 @@ __device__ __forceinline__ void post_body(const PostArgsT<T> &a, double *red)
     row_loop<R, 0>(i_begin, i_end, full_at, iter);
     if constexpr (!S1 || S1P) {
         const double sum = fused_block_sum(acc, red);
-        if (threadIdx.x == 0) a.partials[blockIdx.y * gridDim.x + blockIdx.x] = sum;
+        if (threadIdx.x == 0) a.partials[lby * gridDim.x + lbx] = sum;
     }
 }
 
@@ -1442,13 +1454,7 @@ void k_postpre_lds(PostPreArgsT<T> a)
     __shared__ __attribute__((aligned(16))) T sf[2][kPPR][GENF ? 1 : pp_lds_row<T>()];
     __shared__ __attribute__((aligned(16))) T se[3][pp_lds_coarse<T>()];
     Blk bk{(int)blockIdx.x, (int)blockIdx.y};
-    if (a.xcd) {   // XCD x (linear ids = x mod 8) gets tiles [x q + min(x, r), ...) in order
-        const int nb = (int)(gridDim.x * gridDim.y), id = (int)(blockIdx.y * gridDim.x + blockIdx.x);
-        const int q = nb >> 3, r = nb & 7, x = id & 7;
-        const int t = x * q + min(x, r) + (id >> 3);
-        bk.x = t % (int)gridDim.x;
-        bk.y = t / (int)gridDim.x;
-    }
+    if (a.xcd) xcd_tile(bk.x, bk.y);
     const Cols k = lane_cols_t<pp_stride<OPT>(), pp_margin<OPT>()>(a.N, bk.x);
     // the band's rows 2jcb-6 .. 2jce+5 (RC: from 2jcb-8; see postpre_lds_run): does it reach
     // row 0 or N-1?
@@ -1729,7 +1735,7 @@ int launch_pre(const PreArgsT<T> &a0, bool x0_zero, bool fine, hipStream_t s)
     a.rows_per_block = r;
     // non-temporal stores on the finest level only (its x2 is read again a level-pass later;
     // coarse outputs are re-read while still in the caches): fine k_pre 0.99 -> 0.97 ms
-    a.nt = fine ? 1 : 0;
+    a.nt = (fine ? 1 : 0) | (tuning_int("PGMG_FUSED_XCD", 0) ? 16 : 0);
     const dim3 g(gx, gy), b(t);
     // two row pairs per iteration (r01 sweeps: on x0 = 0 levels 2 as fast as 3 at 8193 and
     // faster below, 4 slower; one pair slower everywhere)
@@ -1778,7 +1784,7 @@ int launch_post(const PostArgsT<T> &a0, bool fine, hipStream_t s)
     PostArgsT<T> a = a0;
     a.rows_per_block = r;
     // fine k_post: 1.01 -> 0.93 ms with non-temporal stores
-    a.nt = fine ? 4 : 0;
+    a.nt = (fine ? 4 : 0) | (tuning_int("PGMG_FUSED_XCD", 0) ? 16 : 0);
     const dim3 g(gx, gy), b(t);
     const bool rec = a.pre_fired != nullptr;
     if (fine && a.gfx != nullptr) launchk(k_post<T, true, 2, false, true>, g, b, s, a);
@@ -1864,7 +1870,7 @@ int launch_postpre(const PostPreArgsT<T> &a0, hipStream_t s)
     if (const int e = postpre_spans(a0, t, gx, r, true)) return e;
     PostPreArgsT<T> a = a0;
     a.rows_per_block = r;
-    a.xcd = tuning_int("PGMG_PP_XCD", 0);
+    a.xcd = tuning_int("PGMG_PP_XCD", 1);
     const dim3 g(gx, gy), b(t);
     const bool genf = a.gfx != nullptr;
     const bool fast = a.fast && sizeof(T) == 8;   // FAST mode: fp64
@@ -1914,6 +1920,7 @@ int launch_smooth4(const PostPreArgsT<T> &a0, hipStream_t s)
     if (const int e = postpre_spans(a0, t, gx, r, false)) return e;
     PostPreArgsT<T> a = a0;
     a.rows_per_block = r;
+    a.xcd = 0;
     if (a.gfx != nullptr) k_postpre_lds<T, true, true, 64><<<dim3(gx, gy), dim3(t), 0, s>>>(a);
     else k_postpre_lds<T, true, false, 64><<<dim3(gx, gy), dim3(t), 0, s>>>(a);
     return PGMG_OK;
