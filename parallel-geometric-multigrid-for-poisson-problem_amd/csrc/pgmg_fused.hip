@@ -1735,7 +1735,7 @@ int launch_pre(const PreArgsT<T> &a0, bool x0_zero, bool fine, hipStream_t s)
     a.rows_per_block = r;
     // non-temporal stores on the finest level only (its x2 is read again a level-pass later;
     // coarse outputs are re-read while still in the caches): fine k_pre 0.99 -> 0.97 ms
-    a.nt = (fine ? 1 : 0) | (tuning_int("PGMG_FUSED_XCD", 0) ? 16 : 0);
+    a.nt = (fine ? 1 : 0) | (tuning_int("PGMG_FUSED_XCD", 1) ? 16 : 0);
     const dim3 g(gx, gy), b(t);
     // two row pairs per iteration (r01 sweeps: on x0 = 0 levels 2 as fast as 3 at 8193 and
     // faster below, 4 slower; one pair slower everywhere)
@@ -1784,7 +1784,7 @@ int launch_post(const PostArgsT<T> &a0, bool fine, hipStream_t s)
     PostArgsT<T> a = a0;
     a.rows_per_block = r;
     // fine k_post: 1.01 -> 0.93 ms with non-temporal stores
-    a.nt = (fine ? 4 : 0) | (tuning_int("PGMG_FUSED_XCD", 0) ? 16 : 0);
+    a.nt = (fine ? 4 : 0) | (tuning_int("PGMG_FUSED_XCD", 1) ? 16 : 0);
     const dim3 g(gx, gy), b(t);
     const bool rec = a.pre_fired != nullptr;
     if (fine && a.gfx != nullptr) launchk(k_post<T, true, 2, false, true>, g, b, s, a);
