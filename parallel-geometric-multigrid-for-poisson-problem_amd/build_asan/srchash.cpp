@@ -1,1 +1,1 @@
-extern "C" const char *pgmg_source_hash(void) { return "asan-456c43c436f0f475"; }
+extern "C" const char *pgmg_source_hash(void) { return "asan-f800e860cd4a5ed5"; }
