@@ -1808,7 +1808,7 @@ int launch_post_r2(const PostArgsT<T> &a0, hipStream_t s)
     PGMG_SPAN(a0.r2out, a0.Pr2, 1, a0.Nr2 - 2, 1, a0.Nr2 - 2, "k_post_r2 level-2 restriction");
     PostArgsT<T> a = a0;
     a.rows_per_block = r;
-    a.nt = 4 | (tuning_int("PGMG_R2_EALL", 0) ? 8 : 0);
+    a.nt = 4 | (tuning_int("PGMG_R2_EALL", 0) ? 8 : 0) | (tuning_int("PGMG_F_XCD", 1) ? 16 : 0);
     const dim3 g(gx, gy), b(t);
     if (a.gfx != nullptr) launchk(k_post_r2<T, true>, g, b, s, a);
     else launchk(k_post_r2<T, false>, g, b, s, a);
@@ -1920,7 +1920,7 @@ int launch_smooth4(const PostPreArgsT<T> &a0, hipStream_t s)
     if (const int e = postpre_spans(a0, t, gx, r, false)) return e;
     PostPreArgsT<T> a = a0;
     a.rows_per_block = r;
-    a.xcd = 0;
+    a.xcd = tuning_int("PGMG_F_XCD", 1);
     if (a.gfx != nullptr) k_postpre_lds<T, true, true, 64><<<dim3(gx, gy), dim3(t), 0, s>>>(a);
     else k_postpre_lds<T, true, false, 64><<<dim3(gx, gy), dim3(t), 0, s>>>(a);
     return PGMG_OK;

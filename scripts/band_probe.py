@@ -26,13 +26,15 @@ def child(a):
     import _pkgload
     pg = _pkgload.load()
     ts = []
+    run = {"V": lambda s, k: s.vcycle(k), "F": lambda s, k: s.fcycle(k)}[a.cycle]
+    warm = 5 if a.cycle == "V" else 2
     with pg.Solver(a.n) as s:
         for _ in range(5):
             s.set_problem()
-            s.vcycle(5)
+            run(s, warm)
             s.sync()
             t0 = time.perf_counter()
-            s.vcycle(20)
+            run(s, 20)
             s.sync()
             ts.append((time.perf_counter() - t0) / 20 * 1e3)
         h = s.solution_hash(0)
@@ -48,6 +50,7 @@ def main():
     ap.add_argument("--knob", default="PGMG_FUSED_BLOCKS_BIG",
                     help="the measurement build's knob to set (PGMG_PP_BLOCKS: k_postpre's "
                          "workgroup target)")
+    ap.add_argument("--cycle", default="V", choices=["V", "F"])
     ap.add_argument("--child", action="store_true")
     a = ap.parse_args()
     if a.child:
@@ -55,13 +58,15 @@ def main():
     for r in range(a.rounds):
         for v in a.values.split(","):
             env = dict(os.environ)
-            if v != "0":
+            if v == "off":     # the knob set to 0 (a switch whose default is on)
+                env[a.knob] = "0"
+            elif v != "0":     # 0: the knob unset (the library's default)
                 env[a.knob] = v
-            p = subprocess.run([sys.executable, __file__, "--child", "--n", str(a.n)], env=env,
+            p = subprocess.run([sys.executable, __file__, "--child", "--n", str(a.n), "--cycle", a.cycle], env=env,
                                capture_output=True, text=True, timeout=300)
             line = p.stdout.strip().splitlines()[-1] if p.stdout.strip() else "{}"
             d = json.loads(line)
-            d.update({"round": r, "knob": a.knob, "value": int(v), "rc": p.returncode})
+            d.update({"round": r, "knob": a.knob, "value": v, "rc": p.returncode})
             if p.returncode:
                 d["stderr"] = p.stderr[-800:]
             print(json.dumps(d), flush=True)
