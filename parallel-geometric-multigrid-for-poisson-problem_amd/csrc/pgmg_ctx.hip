@@ -1908,6 +1908,9 @@ static int spec_reserve(pgmg_ctx *c, long long dbl, long long nchk)
             if (c->pin) HIPC(hipHostFree(c->pin));
             c->pin = nullptr;
             HIPC(hipHostMalloc((void **)&c->pin, pin_bytes(nchk), hipHostMallocCoherent));
+            // (a fresh staging area: its sequence word must not already hold the next seq)
+            std::memset(c->pin, 0, pin_bytes(nchk));
+            c->pin_seq = 0;
             c->chk_cap = nchk;
         }
     }
