@@ -1,1 +1,1 @@
-extern "C" const char *pgmg_source_hash(void) { return "asan-f800e860cd4a5ed5"; }
+extern "C" const char *pgmg_source_hash(void) { return "asan-6ce97a80c44b809e"; }
