@@ -51,6 +51,7 @@ for s in ${STEPS}; do
     ppxcd) step ppxcd 600 env PGMG_LIB=$PWD/parallel-geometric-multigrid-for-poisson-problem_amd/libpgmg_probe.so python3 scripts/band_probe.py --knob PGMG_PP_XCD --values 0,1,0,1 --rounds 2 ;;
     fusedxcd) step fusedxcd 600 env PGMG_LIB=$PWD/parallel-geometric-multigrid-for-poisson-problem_amd/libpgmg_probe.so python3 scripts/band_probe.py --knob PGMG_FUSED_XCD --values 0,1,0,1 --rounds 2 ;;
     fxcd) step fxcd 600 env PGMG_LIB=$PWD/parallel-geometric-multigrid-for-poisson-problem_amd/libpgmg_probe.so python3 scripts/band_probe.py --cycle F --knob PGMG_F_XCD --values 0,off,0,off --rounds 2 ;;
+    wtrace) step wtrace 300 rocprofv3 --kernel-trace --output-format csv -d ${OUT}/wtrace -o run -- python3 scripts/w_trace.py && step wtrace_an 60 python3 scripts/w_trace.py --analyse ${OUT}/wtrace ;;
     levels) step levels 300 python scripts/level_pmc.py run --n 16385 --out ${OUT}/levels ;;
     *) echo "unknown step ${s}" >&2 ;;
   esac
