@@ -943,7 +943,9 @@ def main():
                            "ms_per_step": round(dt * 1e3 / 5, 4), "timed": "1 + 5 cycles, median of 3",
                            "parity": None if w6 is None or h6 is None else h6 == w6,
                            "parity_detail": "FNV-64 of phi after the timed repetitions' 1 + 5 cycles "
-                                            "against oracle/mg_cpu_exec_port's (tests/golden/cycles.json)"})
+                                            "against the reference's (tests/golden/cycles.json: generated by "
+                                            "oracle/mg_cpu_exec_port, confirmed by the reference's own "
+                                            "MultigridSolver, profiles/r06/ref32769/)"})
             # configs[4]'s cycle: the FMG start (one F-cycle) then one W-cycle, fp64
             s.set_problem()
             t0 = time.perf_counter()

@@ -20,7 +20,8 @@ f32) against the fp32 restatement's hashes.
 
 Hashes: FNV-64 over phi's IEEE words; the V/F/G 16385 rows come from the compiled
 reference (oracle/_ref/ref_harness), the 32769 rows from oracle/mg_cpu_exec_port (the C
-restatement pinned to the reference up to 16385), fp32 rows from oracle/liboracle_f32.so.
+restatement), confirmed bitwise in r06 by the reference's own MultigridSolver run at 32769 on a
+GPU box's host (profiles/r06/ref32769/), fp32 rows from oracle/liboracle_f32.so.
 Tolerance: EXACT (bitwise phi, equal sweep counts) except the stated fp32-vs-fp64 bound.
 Reference: /root/reference/2_part_MG/MultiGrid.hpp:57-183.
 """

@@ -5,8 +5,9 @@ The expected values are the BIG cases of tests/golden/make_golden.py (FNV-64 has
 IEEE word of phi and the cumulative sweep / early-exit counts after each cycle):
   V 16385 x 30 cycles, F 16385 x 2, FMG start + W ("G") 16385 — the compiled reference
   (oracle/_ref/ref_harness: MultigridSolver of 2_part_MG/MultiGrid.hpp:57-183);
-  V 32769 x 2, G 32769 — oracle/mg_cpu_exec_port (the C restatement, pinned bit for bit to
-  the reference up to 16385; the reference needs more host memory than the build box has).
+  V 32769 x 2, G 32769 — oracle/mg_cpu_exec_port (the C restatement; the reference needs more
+  host memory than the build box has), confirmed bitwise by the reference's own MultigridSolver
+  on a GPU box's host in r06 (profiles/r06/ref32769/: V 6 cycles, G 2 cycles).
 
 What runs here is the code path the bench times, not a simplified one: at N = 16385 one
 multi-cycle pgmg_vcycle call is the cross-cycle fused finest level (k_postpre_lds at its

@@ -298,9 +298,9 @@ def test_symmetric_prolongation_kat(pgmg, oracle_mod, N):
 def test_vcycle_32769_oracle_hash(pgmg, oracle_mod):
     """N = 32769 (BASELINE config 4's grid, one GPU, ~45 GB of HBM): one V-cycle from
     phi0 = 0 is bitwise the oracle's.  The hash comes from oracle/mg_cpu_exec_port (our C
-    restatement, pinned bit for bit to the compiled reference up to N = 16385; 75 s on one
-    core): `mg_cpu_exec_port V 32769 1 1e-7` -> relerr 0.17198606950442494, hash
-    034c7979d0b231c7, 63 sweeps.  Also exercises 32-bit index headroom (N * pitch ~ 1.07e9)."""
+    restatement; 75 s on one core): `mg_cpu_exec_port V 32769 1 1e-7` -> relerr
+    0.17198606950442494, hash 034c7979d0b231c7, 63 sweeps -- the reference's own
+    MultigridSolver gives the same (profiles/r06/ref32769/V.out).  Also exercises 32-bit index headroom (N * pitch ~ 1.07e9)."""
     N = 32769
     with pgmg.Solver(N) as s:
         s.set_problem()
