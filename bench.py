@@ -184,8 +184,9 @@ def kernel_key(name):
 
 def pmc_child(args):
     """The program the live PMC passes profile: the timed call's kernels (a 3-cycle call:
-    first k_pre, two cross-cycle k_postpre, the carry pass) of every leg and the per-op
-    study's calls, then exit."""
+    first k_pre, two cross-cycle k_postpre, the carry pass; then a 2-cycle call that takes the
+    carry: the recompute form and another carry pass) of every leg and the per-op study's
+    calls, then exit."""
     import torch  # noqa: F401
     import _pkgload
     pg = _pkgload.load()
@@ -198,6 +199,8 @@ def pmc_child(args):
         with pg.Solver(args.n, flags=flags, dtype=args.dtype) as s:
             s.set_problem()
             {"V": s.vcycle, "W": s.wcycle, "F": s.fcycle}[args.cycle](3 if args.cycle != "W" else 1)
+            if args.cycle == "V":
+                s.vcycle(2)
             s.sync()
     if args.ops == "auto" and args.cycle == "V" and args.dtype == "f64":
         import torch
